@@ -1,0 +1,57 @@
+// magpie_oracle — CPU restatement of the reference's decode path and nano-codec.
+//
+// *** TEST INFRASTRUCTURE. *** Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load this library, and only as the checker / the timed CPU
+// baseline. The product (libmagpie_hip.so) never links or calls it.
+//
+// Parity status: the reference's arithmetic lives in ggml (unpinned, absent here),
+// its weights and golden tensors are absent. This oracle is
+// pinned only by the weight-independent known answers the reference holds (the FSQ
+// tables of tests/test_codec_fsq.cpp:41-74, the codec shape progression of
+// docs/CODEC_ARCHITECTURE.md:186-196, token-id constants of magpie.h:70-73) —
+// everything else is "parity unpinned" against real ggml. See DESIGN.md §Oracle.
+#ifndef MAGPIE_ORACLE_H
+#define MAGPIE_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_model orc_model;
+typedef struct orc_codec orc_codec;
+
+// acc64=1: every dot/LN/softmax accumulates in double, tensors stored f32 (the
+// parity judge). acc64=0: f32 accumulation in 8 SIMD lanes (ggml-CPU-like speed;
+// used for the CPU baseline timing). gelu_f16=1 applies ggml-CPU's fp16 GELU table
+// semantics (A.7, assumed). n_threads<=0 keeps the OpenMP default.
+void orc_set_mode(int acc64, int gelu_f16, int n_threads);
+
+orc_model *orc_load(const char *gguf_path);
+void orc_free(orc_model *m);
+int orc_dec_layers(const orc_model *m);
+
+// magpie_synthesize_codes_graph_reuse (magpie.cpp:4063-4432) at temperature 0.
+// Returns n_frames (>=0) or <0 on error. codes_out: [max_steps][8] frame-major.
+// margins_out (nullable): [max_steps][8] top1-top2 gap of the masked logits.
+// hidden_out (nullable): [max_steps+1][768] decoder hidden after every step (BOS first).
+// timing_out (nullable): [0]=preamble ms (encoder+XA+prefill), [1]=decode ms (BOS+loop).
+int orc_synthesize(orc_model *m, const int32_t *tokens, int n_tokens, int speaker_id, int max_steps,
+                   int ignore_eos, int32_t *codes_out, float *margins_out, float *hidden_out,
+                   double *timing_out);
+
+// Component entry points used by unit tests.
+int orc_encode(orc_model *m, const int32_t *tokens, int n_tokens, float *enc_out /*[T][768]*/);
+
+orc_codec *orc_codec_load(const char *gguf_path);
+void orc_codec_free(orc_codec *c);
+// magpie_codec_decode (nano-codec.cpp:758-845). codes: [8][n_frames] cb-major.
+// f16_operands=1 rounds conv_1d operands to fp16 as ggml's F16 im2col does (A.7).
+int orc_codec_decode(orc_codec *c, const int32_t *codes, int n_frames, float *audio_out, int f16_operands);
+// fsq_dequantize_cpu (nano-codec.cpp:721-752): latent [32][n_frames] (time fastest).
+void orc_fsq(const int32_t *codes, int n_frames, float *latent);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

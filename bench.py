@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""bench.py — frames/s of the MI355X-native Magpie decode loop.
+
+Metric (BASELINE.json): audio-codec frames/sec + real-time factor, Magpie-357M.
+Workload at N=1 is BASELINE.json configs[1]: Magpie-357M f32, batch=1, one
+MI355X, HIP decoder-step kernels + hipGraph, KV cache resident in HBM.
+
+A "step" is one decode pass of the batch: the BOS step + 255 autoregressive
+iterations = 256 codec frames per utterance (fixed length, EOS masked; SURVEY
+§8d), exactly what magpie_synthesize_codes_graph_reuse times as gen_time
+(magpie.cpp:4265,4409-4427). Inputs are resident in HBM when the timed region
+starts: the per-utterance preamble (encoder, XA K/V, 110-frame prefill) runs
+once before warm-up; re-decoding re-initialises every per-step state on the
+device, so each step is a complete, identical synthesis of the batch.
+
+value = frames produced by all ranks / max-over-ranks wall time of the K timed
+steps. Multi-GPU: one process per GPU (torchrun), independent utterances per
+rank, no collective on the data path; `gloo` only carries the barrier and the
+max-reduction of the timings ("scaling": "weak").
+
+Weights are synthetic (no checkpoints offline) with the exact GGUF layout.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "magpie-tts.cpp_amd"))
+
+import numpy as np  # noqa: E402
+
+import magpie_amd as ma  # noqa: E402  (loads libmagpie_hip.so before torch can load another HIP runtime)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+FRAMES = 256
+TEXT_TOKENS = 64
+
+
+def decoder_bytes_per_frame(B: int, L_mean: float, T: int, dec_layers: int = 12) -> float:
+    """Algorithmic HBM bytes per frame, f32 weights and f32 KV."""
+    W_dec = dec_layers * 7_276_800 + 768
+    W_lt = 5_147_200
+    per_utt = 73_728 * L_mean * dec_layers / 12 + 12_288 * T * dec_layers / 12 + 49_152 + 73_728 * dec_layers / 12
+    return 4.0 * (W_dec + W_lt) / B + per_utt
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU (configs[1]: 1)")
+    ap.add_argument("--frames", type=int, default=FRAMES)
+    ap.add_argument("--tokens", type=int, default=TEXT_TOKENS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=4,
+                    help="oracle threads for cpu_baseline (ggml's default n_threads, magpie.h:298,306)")
+    ap.add_argument("--profile-ops", type=int, default=30, help="event-timed launches per op for the roofline")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: E402  (gloo: barrier + max only)
+        dist.init_process_group("gloo")
+
+    cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
+    os.makedirs(cache, exist_ok=True)
+    model_path = os.path.join(cache, "magpie_357m_f32.gguf")
+    if rank == 0 or world == 1:
+        ma.synth_gguf(model_path)
+    if dist is not None:
+        dist.barrier()
+        ma.synth_gguf(model_path)  # no-op once rank 0 wrote it
+
+    dev = ma.Device(model_path, device=local)
+    B = args.batch
+    toks = [ma.synthetic_tokens(args.tokens, seed=1000 + rank * B + b) for b in range(B)]
+    speakers = [(rank * B + b) % 5 for b in range(B)]
+
+    # preamble (untimed, inputs resident) + warm-up decodes
+    t_pre = time.perf_counter()
+    r = dev.synthesize(toks, speakers=speakers, max_dec_steps=args.frames, ignore_eos=True)
+    e2e_first_s = time.perf_counter() - t_pre
+    preamble_ms = r.preamble_ms
+    for _ in range(max(args.warmup - 1, 0)):
+        dev.decode(B, args.frames)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    decode_ms = []
+    frames = 0
+    for _ in range(args.steps):
+        rr = dev.decode(B, args.frames)  # synchronises its stream before returning
+        decode_ms.append(rr.decode_ms)
+        frames += int(rr.n_frames.sum())
+    elapsed = time.perf_counter() - t0
+    barrier()
+    assert frames == args.steps * B * args.frames, f"expected fixed-length output, got {frames} frames"
+
+    t_max = elapsed
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+    total_frames = frames * world
+    value = total_frames / t_max
+    ms_per_step = 1e3 * t_max / args.steps
+
+    # ---- roofline of the dominant kernel (event-timed live, same stream as the graph)
+    roofline = None
+    op_table = {}
+    if rank == 0:
+        names = dev.ops()
+        groups = {}
+        for i, n in enumerate(names):
+            groups.setdefault(n, []).append(i)
+        for n, idxs in groups.items():
+            if n == "finalize":
+                continue
+            i = idxs[0]
+            us = dev.time_op(i, reps=args.profile_ops)
+            op_table[n] = {"launches_per_frame": len(idxs), "avg_us": round(us, 3),
+                           "bytes": dev.op_bytes(i), "us_per_frame": round(us * len(idxs), 2)}
+        dom = max(op_table.items(), key=lambda kv: kv[1]["us_per_frame"])
+        name, rec = dom
+        achieved = rec["bytes"] / (rec["avg_us"] * 1e-6) / 1e9
+        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "algorithmic_bytes_per_launch": rec["bytes"], "avg_launch_us": rec["avg_us"]}
+
+    # ---- CPU baseline: the oracle (C restatement, f32 accumulation) on the host cores
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, REPO)
+        from oracle import oracle as orc  # cpu_baseline leg only
+        res = orc.time_decode_fps(model_path, toks[0], args.frames, threads=args.cpu_threads, acc64=False)
+        cpu = {"value": round(res["frames"] / res["decode_s"], 2), "unit": "frames/s", "cores": args.cpu_threads,
+               "kind": "port",
+               "sample": f"1 utterance x {res['frames']} frames (T={args.tokens}), decode loop only "
+                         f"(preamble {res['preamble_s']:.2f}s excluded), oracle f32-accumulate mode"}
+
+    if rank == 0:
+        L_mean = 110 + (args.frames + 1) / 2.0  # keys 111..366 over BOS + 255 steps
+        bpf = decoder_bytes_per_frame(B, L_mean, args.tokens)
+        fps_per_gpu = value / world
+        line = {
+            "metric": "audio-codec frames/sec (decode loop), Magpie-357M",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic random weights, exact GGUF layout; synthetic T=64 prompts)",
+            "config": {"workload": f"Magpie-357M f32, batch={B}/GPU, {args.frames} frames/utterance, "
+                                   f"T={args.tokens}, greedy, EOS masked (configs[1])",
+                       "global_batch": B * world, "frames_per_utterance": args.frames, "text_tokens": args.tokens,
+                       "parallelism": f"replicas x{world} (utterance-partitioned, no collectives)"},
+            "rtf_per_stream": round(value / world / B / ma.FRAMES_PER_SECOND, 2),
+            "decode_fps_events": round(B * args.frames * 1e3 / float(np.mean(decode_ms)), 2),
+            "e2e_fps_first_call": round(B * args.frames / e2e_first_s, 2),
+            "preamble_ms": round(preamble_ms, 2),
+            "decode_roofline": {"bytes_per_frame": round(bpf), "achieved_GBs": round(bpf * fps_per_gpu / 1e9, 1),
+                                "frac": round(bpf * fps_per_gpu / 1e9 / HBM_PEAK_GBS, 4)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "ops": op_table,
+        }
+        print(json.dumps(line), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+/*
+ * magpie_hip.h — the C-ABI boundary of the MI355X-native decode path.
+ *
+ * Plain C, plain pointers and sizes, no torch/ggml types. Every entry point
+ * replaces a piece of the reference's ggml-backed path in m1el/magpie-tts.cpp;
+ * the reference symbol each one stands in for is cited next to it (file:line
+ * under /root/reference). The C++ drop-in API (include/magpie.h) is a thin layer
+ * over these functions; Python (ctypes) and other FFIs bind them directly (see
+ * INTEGRATION.md).
+ *
+ * Conventions (mirroring the reference's error behaviour):
+ *   - every int-returning call returns MP_OK (0) or a negative MP_ERR_* code and
+ *     leaves a message for mp_hip_error(); the reference returns nullptr / an
+ *     empty vector / -1 and prints to stderr.
+ *   - all buffers are caller-owned host memory; one mp_dev == one GPU, used by one
+ *     host thread at a time (the reference context is not thread-safe either,
+ *     magpie.cpp:1129, 2364).
+ */
+#ifndef MAGPIE_HIP_H
+#define MAGPIE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MP_OK 0
+#define MP_ERR_ARG (-1)
+#define MP_ERR_HIP (-2)
+#define MP_ERR_IO (-3)
+#define MP_ERR_FORMAT (-4)
+#define MP_ERR_STATE (-5)
+#define MP_ERR_UNSUPPORTED (-6)
+
+typedef struct mp_dev mp_dev;
+typedef struct mp_codec mp_codec;
+
+/* Inference parameters. The reference carries them on magpie_context
+ * (temperature/top_k/speaker_id, magpie.h:298-306) and hparams.max_dec_steps
+ * (magpie.h:76). */
+typedef struct mp_params {
+    float temperature;  /* < 0.01 => greedy argmax (magpie.cpp:1263-1264) */
+    int top_k;          /* top-k of sample_top_k (magpie.cpp:1072-1109) */
+    int max_dec_steps;  /* frame budget per utterance (magpie.h:76); <= 0 => 500 */
+    int ignore_eos;     /* 1: EOS masked at every step (fixed-length bench mode) */
+    uint64_t seed;      /* sampling RNG seed (reference: unseeded static mt19937, magpie.cpp:1129) */
+    int trace_hidden;   /* 1: keep the decoder hidden state of every step (parity tests) */
+} mp_params;
+
+typedef struct mp_timing {
+    double preamble_ms;  /* encoder + XA K/V + 110-frame prefill (magpie.cpp:4081-4238) */
+    double decode_ms;    /* BOS step + autoregressive loop (gen_time, magpie.cpp:4265,4409) */
+    int frames_total;    /* frames produced over all utterances */
+    int iterations;      /* decode iterations (graph replays) executed */
+} mp_timing;
+
+/* --- device + weights ---------------------------------------------------- */
+int mp_hip_device_count(int *n);
+/* replaces init_backend / ggml_backend_cuda_init (magpie.cpp:14-67) */
+int mp_hip_init(int device, mp_dev **out);
+/* replaces gguf_init_from_file + read_hparams + create_tensors + load_tensor_data
+ * (magpie.cpp:73-121, 572-718, 781-880): parses the GGUF (F32/F16/Q8_0 tensors,
+ * same names and layout) and uploads resident weights once. */
+int mp_hip_load_model(mp_dev *dev, const char *gguf_path);
+int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes);
+/* replaces magpie_free (magpie.cpp:882-910) */
+void mp_hip_free(mp_dev *dev);
+const char *mp_hip_error(mp_dev *dev);
+
+/* --- synthesis ------------------------------------------------------------ */
+/* Per-utterance preamble for B independent utterances: text encoder
+ * (magpie_encode_text, magpie.cpp:2284-2374), cross-attention K/V
+ * (magpie.cpp:4098-4136), baked speaker context + 110-frame prefill
+ * (magpie.cpp:4138-4238). tokens: [B][tmax] row-major (padding ignored),
+ * n_tokens: [B], speaker: [B] (0..4). */
+int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_tokens, const int32_t *speaker, int B,
+                       int tmax, const mp_params *params);
+/* The frame loop of magpie_synthesize_codes_graph_reuse (magpie.cpp:4245-4407)
+ * for the whole batch: one hipGraph replay per frame. codes_out:
+ * [B][max_dec_steps][8] frame-major (BOS excluded, as magpie.cpp:4416-4420);
+ * n_frames: [B]. */
+int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames);
+/* decoder hidden state after every step (BOS first): [B][max_dec_steps+1][768];
+ * requires params.trace_hidden. */
+int mp_hip_get_trace(mp_dev *dev, float *hidden);
+int mp_hip_get_timing(mp_dev *dev, mp_timing *t);
+
+/* --- measurement ---------------------------------------------------------- */
+/* Ops of the captured decode iteration (valid after mp_hip_decode). */
+int mp_hip_num_ops(mp_dev *dev);
+const char *mp_hip_op_name(mp_dev *dev, int op);
+/* algorithmic HBM bytes one launch of `op` moves (weights + activations) */
+double mp_hip_op_bytes(mp_dev *dev, int op);
+/* Re-launch one op of the iteration `reps` times on the decode stream, timed with
+ * a hipEvent pair around each launch; returns the mean launch duration in us. */
+int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us);
+
+/* --- nano-codec ----------------------------------------------------------- */
+/* replaces magpie_codec_init / magpie_codec_load (nano-codec.cpp:205-352) */
+int mp_hip_codec_init(int device, const char *gguf_path, mp_codec **out);
+/* replaces magpie_codec_decode (nano-codec.cpp:758-845): codes [8][n_frames]
+ * codebook-major, audio_out [n_frames * 1024] samples in [-1, 1]. */
+int mp_hip_codec_decode(mp_codec *c, const int32_t *codes, int n_frames, float *audio_out);
+void mp_hip_codec_free(mp_codec *c);
+const char *mp_hip_codec_error(mp_codec *c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAGPIE_HIP_H */

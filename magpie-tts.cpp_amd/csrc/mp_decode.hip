@@ -1,0 +1,437 @@
+// Per-frame decode kernels for gfx950 (f32 path, batch NB <= 8 utterances).
+//
+// One decode iteration = 12 decoder layers (magpie_build_decoder_layer_gpu_cached,
+// magpie.cpp:3484-3528) + the 8-codebook local transformer
+// (magpie_local_transformer_sample_all, magpie.cpp:1113-1317) + EOS bookkeeping
+// (magpie.cpp:4340-4358), all device-resident and captured in one hipGraph.
+//
+// At batch <= 8 every projection is a weight-streaming GEMV: HBM-bound, each
+// weight byte is read once per step and reused across the NB utterances from
+// registers. The fused GEMV family below streams W with 16-byte per-lane loads
+// (one 1 KiB wave-instruction per 256 floats of a row), keeps the activation
+// vector in LDS, and fuses whatever tiny op precedes / follows the projection
+// (LayerNorm, frame embedding, attention combine, argmax, GELU, residual, KV
+// append) into its prologue / epilogue so no extra launch is paid for it.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "mp_device.hpp"
+#include "mp_params.hpp"
+
+namespace mp {
+
+// ---------------------------------------------------------------- prologues
+// Each prologue fills act[NB][K] (LDS) with the activation vector of every slot.
+
+template <int NB, int K>
+__device__ __forceinline__ void pro_ln_vec(const float *x, const float *lnw, float eps, float *act, float *red,
+                                           float *store) {
+    // ggml_norm + ggml_mul (magpie.cpp:2255-2258): (x - mean) / sqrt(var + eps) * w
+    constexpr int PER = K / MP_BLOCK;
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) { v[i] = x[threadIdx.x + MP_BLOCK * i]; s += v[i]; }
+    const float mean = block_sum(s, red) * (1.0f / K);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) { v[i] -= mean; q += v[i] * v[i]; }
+    const float var = block_sum(q, red) * (1.0f / K);
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int k = threadIdx.x + MP_BLOCK * i;
+        const float y = (v[i] * rstd) * lnw[k];
+        act[k] = y;
+        if (store) store[k] = y;
+    }
+}
+
+template <int NB, int K, int PRO>
+__device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
+    const int tid = threadIdx.x;
+    if constexpr (PRO == PRO_PLAIN) {
+        for (int b = 0; b < NB; ++b)
+            for (int k = tid * 4; k < K; k += MP_BLOCK * 4)
+                *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
+        __syncthreads();
+    } else if constexpr (PRO == PRO_LN) {
+        for (int b = 0; b < NB; ++b) {
+            float *store = nullptr;
+            if (p.hidden_out && blockIdx.x == 0) store = p.hidden_out + (size_t)b * K;
+            pro_ln_vec<NB, K>(p.src + (size_t)b * p.src_ld, p.lnw, p.eps, act + b * K, red, store);
+            if (p.trace && blockIdx.x == 0) {
+                __syncthreads();
+                const int s = p.step[b];
+                if (s < p.trace_steps)
+                    for (int k = tid; k < K; k += MP_BLOCK)
+                        p.trace[((size_t)b * p.trace_steps + s) * K + k] = act[b * K + k];
+            }
+        }
+        __syncthreads();
+    } else if constexpr (PRO == PRO_EMBED_LN) {
+        static_assert(K == D, "embed prologue is d_model wide");
+        for (int b = 0; b < NB; ++b) {
+            const int *c = p.codes + b * NCB;
+            const int ps = p.pos[b];
+            float x[K / MP_BLOCK];
+#pragma unroll
+            for (int i = 0; i < K / MP_BLOCK; ++i) {
+                const int k = tid + MP_BLOCK * i;
+                float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
+#pragma unroll
+                for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
+                x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
+                if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
+            }
+            // LN over the freshly built x (registers -> LN helper reads memory; inline here)
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < K / MP_BLOCK; ++i) s += x[i];
+            const float mean = block_sum(s, red) * (1.0f / K);
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < K / MP_BLOCK; ++i) { x[i] -= mean; q += x[i] * x[i]; }
+            const float rstd = 1.0f / sqrtf(block_sum(q, red) * (1.0f / K) + p.eps);
+#pragma unroll
+            for (int i = 0; i < K / MP_BLOCK; ++i) {
+                const int k = tid + MP_BLOCK * i;
+                act[b * K + k] = (x[i] * rstd) * p.lnw[k];
+            }
+        }
+        __syncthreads();
+    } else if constexpr (PRO == PRO_SA_COMBINE) {
+        static_assert(K == D, "SA output is d_model wide");
+        for (int b = 0; b < NB; ++b)
+            for (int k = tid; k < K; k += MP_BLOCK) {
+                const int h = k / DH, d = k % DH;
+                const float *P = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
+                float M = -INFINITY;
+                for (int c = 0; c < p.nch; ++c) M = fmaxf(M, P[c * PART_STRIDE]);
+                float num = 0.f, den = 0.f;
+                for (int c = 0; c < p.nch; ++c) {
+                    const float mc = P[c * PART_STRIDE];
+                    if (mc == -INFINITY) continue;
+                    const float e = expf(mc - M);
+                    den += e * P[c * PART_STRIDE + 1];
+                    num += e * P[c * PART_STRIDE + 16 + d];
+                }
+                act[b * K + k] = num / den;
+            }
+        __syncthreads();
+    } else if constexpr (PRO == PRO_XA) {
+        static_assert(K == DXA, "XA output is 128 wide");
+        const int lane = tid & 63, w = tid >> 6, half = lane >> 5, d4 = lane & 31;
+        const float scale = 1.0f / sqrtf((float)DXA);
+        for (int b = 0; b < NB; ++b) {
+            const int Tb = p.T[b];
+            const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+            const float *Vb = p.xav + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+            const float4 q4 = *(const float4 *)(p.qx + (size_t)b * DXA + 4 * d4);
+            for (int j0 = w * 2; j0 < Tb; j0 += 8) {
+                const int j = j0 + half;
+                float v = 0.f;
+                if (j < Tb) v = dotv(q4, *(const float4 *)(Kb + (size_t)j * DXA + 4 * d4));
+                v = group_sum<32>(v);
+                if (d4 == 0 && j < Tb) sc[j] = v * scale;
+            }
+            __syncthreads();
+            float m = -INFINITY;
+            for (int j = tid; j < Tb; j += MP_BLOCK) m = fmaxf(m, sc[j]);
+            m = block_max(m, red);
+            float l = 0.f;
+            for (int j = tid; j < Tb; j += MP_BLOCK) { const float e = expf(sc[j] - m); sc[j] = e; l += e; }
+            l = block_sum(l, red);  // (its barriers also publish sc[])
+            const int dd = tid & (DXA - 1), par = tid >> 7;
+            float a = 0.f;
+            for (int j = par; j < Tb; j += 2) a += sc[j] * Vb[(size_t)j * DXA + dd];
+            red[8 + tid] = a;
+            __syncthreads();
+            if (tid < DXA) act[b * K + tid] = (red[8 + tid] + red[8 + DXA + tid]) / l;
+            __syncthreads();
+        }
+    } else if constexpr (PRO == PRO_LTX_LN) {
+        static_assert(K == LTD, "LT is 256 wide");
+        for (int b = 0; b < NB; ++b) {
+            const int k = tid;
+            const float X = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+            if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X;
+            const float mean = block_sum(X, red) * (1.0f / K);
+            const float dv = X - mean;
+            const float rstd = 1.0f / sqrtf(block_sum(dv * dv, red) * (1.0f / K) + p.eps);
+            act[b * K + k] = (dv * rstd) * p.lnw[k];
+        }
+        __syncthreads();
+    } else if constexpr (PRO == PRO_LT_ATTN) {
+        static_assert(K == LTD, "LT is 256 wide");
+        const int lane = tid & 63, w = tid >> 6;
+        const int nk = p.cb + 1;
+        for (int b = 0; b < NB; ++b) {
+            const float4 q4 = *(const float4 *)(p.ltq + (size_t)b * LTD + 4 * lane);
+            for (int j = w; j < nk; j += MP_NWAVES) {
+                float v = dotv(q4, *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane));
+                v = wave_sum(v);
+                if (lane == 0) sc[j] = v * (1.0f / 16.0f);  // 1/sqrt(256)
+            }
+            __syncthreads();
+            float m = -INFINITY;
+            for (int j = 0; j < nk; ++j) m = fmaxf(m, sc[j]);
+            float l = 0.f, a = 0.f;
+            for (int j = 0; j < nk; ++j) {
+                const float e = expf(sc[j] - m);
+                l += e;
+                a += e * p.ltv[((size_t)b * NCB + j) * LTD + tid];
+            }
+            act[b * K + tid] = a / l;
+            __syncthreads();
+        }
+    } else if constexpr (PRO == PRO_ARGMAX_EMB) {
+        static_assert(K == D, "embedding is d_model wide");
+        for (int b = 0; b < NB; ++b) {
+            const float *lg = p.logits + (size_t)b * VCB;
+            const bool forbid_eos = p.ignore_eos || p.step[b] < 4;  // min_generated_frames
+            float bv = -INFINITY;
+            int bi = 0x7fffffff;
+            for (int i = tid; i < VCB; i += MP_BLOCK) {
+                float v = lg[i];
+                if (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos)) v = -INFINITY;
+                argmax_merge(bv, bi, v, i);
+            }
+            wave_argmax(bv, bi);
+            if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
+            __syncthreads();
+            float v0 = red[0];
+            int i0 = ((int *)red)[4];
+            for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
+            if (i0 < 0 || i0 >= VCB) i0 = 0;  // all -inf / NaN logits: reference argmax stays 0
+            __syncthreads();
+            if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb] = i0;
+            const float *e = p.emb + ((size_t)p.cb * VCB + i0) * D;
+            for (int k = tid; k < K; k += MP_BLOCK) act[b * K + k] = e[k];
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- GEMV core
+// Rows [row0, row0+RW) of W (row-major [N][K]) dotted with act[NB][K].
+// Lane l owns elements 4*(l + 64*i): every weight load is a 1 KiB coalesced
+// wave-instruction; activations come from LDS with conflict-free ds_read_b128.
+template <int NB, int RW, int K, int PRO, int EPI>
+__global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
+    if (p.ndone && *p.ndone >= p.nslots) return;
+    constexpr int VW = K >= 256 ? 4 : K / 64;
+    constexpr int NV = K / (64 * VW);
+    using VT = typename vecf<VW>::T;
+    constexpr int SC = (PRO == PRO_XA) ? TMAX_LIMIT : (PRO == PRO_LT_ATTN ? 16 : 1);
+    __shared__ __attribute__((aligned(16))) float act[NB * K];
+    __shared__ float red[8 + 2 * DXA];
+    __shared__ float sc[SC];
+    prologue<NB, K, PRO>(p, act, red, sc);
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int row0 = (blockIdx.x * MP_NWAVES + w) * RW;
+    VT wv[RW][NV];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        const int n = row0 + r < p.N ? row0 + r : p.N - 1;
+        const VT *wr = (const VT *)(p.W + (size_t)n * K);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) wv[r][i] = wr[lane + 64 * i];
+    }
+    float acc[RW][NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        VT av[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) av[i] = ((const VT *)(act + b * K))[lane + 64 * i];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) s += dotv(wv[r][i], av[i]);
+            acc[r][b] = wave_sum(s);
+        }
+    }
+    if (lane != 0) return;
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        const int n = row0 + r;
+        if (n >= p.N) break;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const float v = acc[r][b];
+            if constexpr (EPI == EPI_STORE) p.out[(size_t)b * p.out_ld + n] = v;
+            else if constexpr (EPI == EPI_BIAS) p.out[(size_t)b * p.out_ld + n] = v + p.bias[n];
+            else if constexpr (EPI == EPI_GELU) p.out[(size_t)b * p.out_ld + n] = gelu_tanh(v);
+            else if constexpr (EPI == EPI_RESID) p.resid[(size_t)b * D + n] = v + p.resid[(size_t)b * D + n];
+            else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
+            else if constexpr (EPI == EPI_QKV) {
+                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + p.pos[b]) * D;
+                if (n < D) p.out[(size_t)b * D + n] = v;
+                else if (n < 2 * D) p.kc[slot + n - D] = v;
+                else p.vc[slot + n - 2 * D] = v;
+            } else if constexpr (EPI == EPI_LTQKV) {
+                if (n < LTD) p.lq[(size_t)b * LTD + n] = v;
+                else if (n < 2 * LTD) p.lk[((size_t)b * NCB + p.cb) * LTD + n - LTD] = v;
+                else p.lv[((size_t)b * NCB + p.cb) * LTD + n - 2 * LTD] = v;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- SA decode attention
+// Split-K over the key axis: workgroup (chunk, head, slot) handles 64 keys and
+// writes (max, sum, o[64]) for the combine in the O-projection prologue.
+// 16 lanes x float4 cover one 64-dim key row (256 B, coalesced); a wave does 4
+// keys per instruction. Keys j > pos are masked (L = pos + 1, magpie.cpp:3412).
+__global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
+    if (p.ndone && *p.ndone >= p.nslots) return;
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int L = p.pos[b] + 1;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float *P = p.part + ((size_t)(b * NH + h) * p.nch + c) * PART_STRIDE;
+    const int j0 = c * SA_CHUNK;
+    if (j0 >= L) {
+        if (tid < PART_STRIDE) P[tid] = tid == 0 ? -INFINITY : 0.f;
+        return;
+    }
+    __shared__ float sc[SA_CHUNK];
+    __shared__ float ow[MP_NWAVES][DH];
+    const int kk = lane >> 4, dc = lane & 15;
+    const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
+    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
+    float s[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int j = j0 + w * 16 + it * 4 + kk;
+        float v = 0.f;
+        if (j < L) v = dotv(q4, *(const float4 *)(p.kc + base + (size_t)j * D));
+        v = group_sum<16>(v);
+        s[it] = j < L ? v * 0.125f : -INFINITY;  // 1/sqrt(64)
+    }
+    if (dc == 0)
+#pragma unroll
+        for (int it = 0; it < 4; ++it) sc[w * 16 + it * 4 + kk] = s[it];
+    __syncthreads();
+    float m = -INFINITY;
+#pragma unroll 8
+    for (int i = 0; i < SA_CHUNK; ++i) m = fmaxf(m, sc[i]);
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int j = j0 + w * 16 + it * 4 + kk;
+        if (j < L) {
+            const float e = expf(s[it] - m);
+            const float4 v4 = *(const float4 *)(p.vc + base + (size_t)j * D);
+            o.x += e * v4.x; o.y += e * v4.y; o.z += e * v4.z; o.w += e * v4.w;
+        }
+    }
+#pragma unroll
+    for (int msk = 16; msk <= 32; msk <<= 1) {
+        o.x += __shfl_xor(o.x, msk, 64); o.y += __shfl_xor(o.y, msk, 64);
+        o.z += __shfl_xor(o.z, msk, 64); o.w += __shfl_xor(o.w, msk, 64);
+    }
+    if (lane < 16) *(float4 *)(&ow[w][4 * lane]) = o;
+    __syncthreads();
+    if (tid < DH) P[16 + tid] = (ow[0][tid] + ow[1][tid]) + (ow[2][tid] + ow[3][tid]);
+    if (tid == 64) {
+        float l = 0.f;
+        for (int i = 0; i < SA_CHUNK; ++i) if (sc[i] != -INFINITY) l += expf(sc[i] - m);
+        P[0] = m;
+        P[1] = l;
+    }
+}
+
+// ---------------------------------------------------------------- frame finalize
+// Codebook 7's masked argmax, then the reference's loop bookkeeping
+// (magpie.cpp:4340-4358): stop on EOS in any codebook (frame not emitted), else
+// append the frame; stop at max_dec_steps; otherwise the frame becomes the next
+// decoder input and the position advances.
+__global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (p.done[b]) return;
+    __shared__ float red[8];
+    const float *lg = p.logits + (size_t)b * VCB;
+    const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < VCB; i += MP_BLOCK) {
+        float v = lg[i];
+        if (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos)) v = -INFINITY;
+        argmax_merge(bv, bi, v, i);
+    }
+    wave_argmax(bv, bi);
+    if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
+    __syncthreads();
+    if (tid != 0) return;
+    float v0 = red[0];
+    int i0 = ((int *)red)[4];
+    for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
+    if (i0 < 0 || i0 >= VCB) i0 = 0;
+    int *cc = p.codes_cur + b * NCB;
+    cc[NCB - 1] = i0;
+    bool eos = false;
+    for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
+    const int s = p.step[b];
+    if (eos) {
+        p.done[b] = 1;
+        p.nframes[b] = s;
+        atomicAdd(p.ndone, 1);
+        return;
+    }
+    for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
+    p.step[b] = s + 1;
+    if (s + 1 >= p.max_steps) {
+        p.done[b] = 1;
+        p.nframes[b] = s + 1;
+        atomicAdd(p.ndone, 1);
+        return;
+    }
+    for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
+    p.pos[b] += 1;
+}
+
+// ---------------------------------------------------------------- host launchers
+template <int NB, int RW, int K, int PRO, int EPI>
+static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
+    const int rows_per_block = MP_NWAVES * RW;
+    const int grid = (p.N + rows_per_block - 1) / rows_per_block;
+    hipLaunchKernelGGL((gemv_kernel<NB, RW, K, PRO, EPI>), dim3(grid), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
+// Named entry points (one per fused op of the decode iteration), instantiated
+// for NB in {1, 2, 4, 8}.
+#define MP_DECODE_OPS(NB)                                                                                        \
+    hipError_t op_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
+    hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
+    hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_SA_COMBINE, EPI_RESID>(p, s); } \
+    hipError_t op_xq_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_STORE>(p, s); }            \
+    hipError_t op_xo_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DXA, PRO_XA, EPI_RESID>(p, s); }          \
+    hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_GELU>(p, s); }            \
+    hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_RESID>(p, s); }      \
+    hipError_t op_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_BIAS>(p, s); }         \
+    hipError_t op_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
+    hipError_t op_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
+    hipError_t op_lt_c_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LN, EPI_GELU>(p, s); }         \
+    hipError_t op_lt_d_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTF, PRO_PLAIN, EPI_ADD_STORE>(p, s); } \
+    hipError_t op_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }      \
+    hipError_t op_lt_f_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_ARGMAX_EMB, EPI_BIAS>(p, s); }
+
+MP_DECODE_OPS(1)
+MP_DECODE_OPS(2)
+MP_DECODE_OPS(4)
+MP_DECODE_OPS(8)
+
+hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
+    hipLaunchKernelGGL(sa_attn_partial_kernel, dim3(p.nch, NH, B), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t op_finalize(const FinP &p, int B, hipStream_t s) {
+    hipLaunchKernelGGL(lt_finalize_kernel, dim3(B), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace mp

@@ -1,0 +1,108 @@
+// Kernel parameter blocks shared by the host runtime (mp_runtime.hip) and the
+// kernels. Plain pointers only: every launch in a decode iteration reads its
+// per-utterance state (positions, codes, done flags) from device memory, so one
+// captured hipGraph replays unchanged for every frame.
+#pragma once
+#include <stdint.h>
+
+namespace mp {
+
+constexpr int D = 768;        // d_model                      (magpie.h:37)
+constexpr int DFF = 3072;     // d_ffn                        (magpie.h:38)
+constexpr int NH = 12;        // decoder SA heads             (magpie.h:48)
+constexpr int DH = 64;        // SA head dim                  (magpie.h:39)
+constexpr int DXA = 128;      // XA 1 head x 128              (magpie.h:49-50)
+constexpr int LTD = 256;      // local transformer dim        (magpie.h:54)
+constexpr int LTF = 1024;     // LT ffn dim                   (magpie.h:55)
+constexpr int NCB = 8;        // codebooks                    (magpie.h:61)
+constexpr int VCB = 2024;     // vocab per codebook           (magpie.h:63)
+constexpr int CTX = 110;      // baked context frames         (magpie.h:67)
+constexpr int SA_CHUNK = 64;  // keys per split-K attention workgroup
+constexpr int PART_STRIDE = 80;  // [m, l, pad.., o[64] at +16]
+constexpr int TMAX_LIMIT = 1024;  // text tokens per utterance (LDS score buffer)
+
+// prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
+enum Pro {
+    PRO_PLAIN = 0,      // act = src
+    PRO_LN = 1,         // act = LN(src) * lnw                          (magpie.cpp:2237-2259)
+    PRO_EMBED_LN = 2,   // x = sum_cb emb[cb][code]/8 + pos; act = LN(x)*lnw (2746-2787, 4376-4379)
+    PRO_SA_COMBINE = 3, // act = split-K softmax combine of SA partials (3457-3476)
+    PRO_XA = 4,         // act = softmax(K q / sqrt(128)) V over the text memory (1713-1767)
+    PRO_LTX_LN = 5,     // X = s_cb + lt_pos[cb]; act = LN(X)*lnw       (1015-1034, 946-958)
+    PRO_LT_ATTN = 6,    // act = causal 1x256 attention over LT positions 0..cb (965-966)
+    PRO_ARGMAX_EMB = 7, // code = masked argmax(logits); act = audio_emb[cb][code] (1243-1291)
+};
+enum Epi {
+    EPI_STORE = 0,      // out = v
+    EPI_BIAS = 1,       // out = v + bias
+    EPI_GELU = 2,       // out = gelu(v)
+    EPI_RESID = 3,      // resid += v
+    EPI_QKV = 4,        // q -> out, k/v -> SA cache at pos       (3415-3442)
+    EPI_LTQKV = 5,      // q -> lq, k/v -> LT position cb
+    EPI_ADD_STORE = 6,  // out = v + addsrc
+};
+
+struct GemvP {
+    const float *W;
+    int N;
+    const float *bias;
+    // prologue inputs
+    const float *src;
+    int src_ld;
+    const float *lnw;
+    float eps;
+    float *hidden_out;   // PRO_LN: block 0 stores the normalised vector (decoder hidden)
+    float *trace;        // optional [B][trace_steps][768] hidden trace
+    int trace_steps;
+    const float *emb;    // audio embeddings [8][2024][768]
+    const int *codes;    // [B][8]
+    const float *pos_emb;
+    const int *pos;      // [B] decoder position
+    float *xres;         // [B][768] residual stream
+    const float *part;   // SA partials
+    int nch;
+    const float *qx;     // XA query [B][128]
+    const float *xak, *xav;  // [B][L][Tmax][128]
+    const int *T;
+    int Tmax, layer, nlayers;
+    const float *lt_s;   // [B][9][256]
+    int cb;
+    const float *lt_pos;
+    float *ltX;
+    const float *ltq, *ltk, *ltv;
+    const float *logits;  // [B][2024]
+    int *codes_cur;       // [B][8]
+    const int *step;      // [B]
+    int ignore_eos, audio_bos, audio_eos;
+    // epilogue outputs
+    float *out;
+    int out_ld;
+    float *resid;
+    const float *addsrc;
+    float *kc, *vc;
+    int max_seq;
+    float *lq, *lk, *lv;
+    // early exit once every slot is done (count >= nslots)
+    const int *ndone;
+    int nslots;
+};
+
+struct FinP {
+    const float *logits;
+    int *codes_cur, *codes_prev, *codes_out;
+    int *step, *pos, *done, *nframes, *ndone;
+    int max_steps, ignore_eos, audio_bos, audio_eos, nslots;
+};
+
+struct AttnP {  // split-K decode self-attention (one query per utterance)
+    const float *q;
+    const float *kc, *vc;
+    int layer, nlayers, max_seq;
+    const int *pos;
+    float *part;
+    int nch;
+    const int *ndone;
+    int nslots;
+};
+
+}  // namespace mp

@@ -1,0 +1,245 @@
+// Per-utterance preamble kernels (run once per batch, outside the frame loop):
+// text encoder (magpie_encode_text, magpie.cpp:2284-2374), cross-attention K/V
+// precompute (magpie.cpp:1663-1711, 4098-4136) and the batched 110-frame context
+// prefill (magpie.cpp:3911-4060, 4167-4238).
+//
+// Rows are (utterance, position) pairs laid out r = b * rows_per_utt + t. The
+// projections are an LDS-tiled f32 GEMM (64x64 tile, 4x4 per thread) with the
+// tiny neighbouring ops fused into its operand loader (causal k=3 conv taps) or
+// its epilogue (residual, GELU, KV-cache scatter, XA K/V split).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "mp_device.hpp"
+#include "mp_params.hpp"
+#include "mp_prefill_api.hpp"
+
+namespace mp {
+
+template <int EPI, int TAPS>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
+    constexpr int BM = 64, BN = 64, BK = 16;
+    __shared__ float As[BK][BM + 4];
+    __shared__ float Ws[BK][BN + 4];
+    const int tid = threadIdx.x;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int tx = tid & 15, ty = tid >> 4;
+    float acc[4][4] = {};
+    const int lr = tid >> 2, lk = (tid & 3) * 4;  // loader: row lr, k lk..lk+3
+    for (int k0 = 0; k0 < p.K; k0 += BK) {
+        {   // A tile
+            const int m = m0 + lr;
+            float a[4] = {0.f, 0.f, 0.f, 0.f};
+            if (m < p.M) {
+                if constexpr (TAPS == 0) {
+                    const float4 v = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + lk);
+                    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+                } else {
+                    const int t = m % p.rows_per_utt;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int kk = k0 + lk + e, i = kk / TAPS, tap = kk % TAPS;
+                        const int st = t - (TAPS - 1) + tap;
+                        a[e] = st >= 0 ? p.A[(size_t)(m - (TAPS - 1) + tap) * p.lda + i] : 0.f;
+                    }
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) As[lk + e][lr] = a[e];
+        }
+        {   // W tile
+            const int n = n0 + lr;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n < p.N) v = *(const float4 *)(p.W + (size_t)n * p.K + k0 + lk);
+            Ws[lk + 0][lr] = v.x; Ws[lk + 1][lr] = v.y; Ws[lk + 2][lr] = v.z; Ws[lk + 3][lr] = v.w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < BK; ++kk) {
+            const float4 a4 = *(const float4 *)&As[kk][ty * 4];
+            const float4 w4 = *(const float4 *)&Ws[kk][tx * 4];
+            const float a[4] = {a4.x, a4.y, a4.z, a4.w}, w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * w[j];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + ty * 4 + i;
+        if (m >= p.M) continue;
+        const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + tx * 4 + j;
+            if (n >= p.N) continue;
+            float v = acc[i][j];
+            if (p.bias) v += p.bias[n];
+            if constexpr (EPI == GE_STORE) p.C[(size_t)m * p.ldc + n] = v;
+            else if constexpr (EPI == GE_RESID) p.C[(size_t)m * p.ldc + n] = v + p.C[(size_t)m * p.ldc + n];
+            else if constexpr (EPI == GE_GELU) p.C[(size_t)m * p.ldc + n] = gelu_tanh(v);
+            else if constexpr (EPI == GE_QKV_CACHE) {
+                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + t) * D;
+                if (n < D) p.C[(size_t)m * p.ldc + n] = v;
+                else if (n < 2 * D) p.kc[slot + n - D] = v;
+                else p.vc[slot + n - 2 * D] = v;
+            } else if constexpr (EPI == GE_XAKV) {
+                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.Tmax + t) * DXA;
+                if (n < DXA) p.xak[slot + n] = v;
+                else p.xav[slot + n - DXA] = v;
+            }
+        }
+    }
+}
+
+// Y[m] = LN(X[m]) * w for rows of width 768 (ggml_norm + ggml_mul).
+__global__ __launch_bounds__(256) void ln_rows_kernel(const float *X, int ldx, const float *w, float *Y, int ldy,
+                                                      float eps) {
+    __shared__ float red[8];
+    const int m = blockIdx.x, tid = threadIdx.x;
+    const float *x = X + (size_t)m * ldx;
+    float v[3], s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { v[i] = x[tid + 256 * i]; s += v[i]; }
+    const float mean = block_sum(s, red) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { v[i] -= mean; q += v[i] * v[i]; }
+    const float rstd = 1.0f / sqrtf(block_sum(q, red) * (1.0f / D) + eps);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Y[(size_t)m * ldy + tid + 256 * i] = (v[i] * rstd) * w[tid + 256 * i];
+}
+
+// Causal multi-head attention for every (row, head): one wave per pair.
+// Keys for row (b, t) are rows j <= t of the same utterance, read through
+// (kbase, vbase) + b * utt_stride + j * row_stride + h * 64.
+
+__global__ __launch_bounds__(256) void row_attn_kernel(RowAttnP p) {
+    __shared__ float pr[4][TMAX_LIMIT];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pair = blockIdx.x * 4 + w;
+    if (pair >= p.M * p.heads) return;
+    const int m = pair / p.heads, h = pair % p.heads;
+    const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
+    const int nk = t + 1;
+    const float *q = p.Q + (size_t)m * p.ldq + h * DH;
+    const float *Kb = p.Kb + b * p.utt_stride + h * DH;
+    const float *Vb = p.Vb + b * p.utt_stride + h * DH;
+    float mx = -INFINITY;
+    for (int j = lane; j < nk; j += 64) {
+        const float *k = Kb + (size_t)j * p.row_stride;
+        float s = 0.f;
+        for (int d = 0; d < DH; d += 4) s += dotv(*(const float4 *)(q + d), *(const float4 *)(k + d));
+        s *= 0.125f;
+        pr[w][j] = s;
+        mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    float l = 0.f;
+    for (int j = lane; j < nk; j += 64) { const float e = expf(pr[w][j] - mx); pr[w][j] = e; l += e; }
+    l = wave_sum(l);
+    __builtin_amdgcn_wave_barrier();
+    float o = 0.f;
+    for (int j = 0; j < nk; ++j) o += pr[w][j] * Vb[(size_t)j * p.row_stride + lane];
+    p.O[(size_t)m * D + h * DH + lane] = o / l;
+}
+
+// Cross-attention for a block of rows: 1 head x 128 over the utterance's T[b]
+// text positions (no mask).
+
+__global__ __launch_bounds__(256) void row_xa_kernel(RowXaP p) {
+    __shared__ float pr[4][TMAX_LIMIT];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int m = blockIdx.x * 4 + w;
+    if (m >= p.M) return;
+    const int b = m / p.rows_per_utt, Tb = p.T[b];
+    const float *q = p.Q + (size_t)m * DXA;
+    const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+    const float *Vb = p.xav + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+    const float scale = 1.0f / sqrtf((float)DXA);
+    float mx = -INFINITY;
+    for (int j = lane; j < Tb; j += 64) {
+        float s = 0.f;
+        for (int d = 0; d < DXA; d += 4) s += dotv(*(const float4 *)(q + d), *(const float4 *)(Kb + (size_t)j * DXA + d));
+        s *= scale;
+        pr[w][j] = s;
+        mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    float l = 0.f;
+    for (int j = lane; j < Tb; j += 64) { const float e = expf(pr[w][j] - mx); pr[w][j] = e; l += e; }
+    l = wave_sum(l);
+    __builtin_amdgcn_wave_barrier();
+    float o0 = 0.f, o1 = 0.f;
+    for (int j = 0; j < Tb; ++j) {
+        o0 += pr[w][j] * Vb[(size_t)j * DXA + lane];
+        o1 += pr[w][j] * Vb[(size_t)j * DXA + 64 + lane];
+    }
+    p.O[(size_t)m * DXA + lane] = o0 / l;
+    p.O[(size_t)m * DXA + 64 + lane] = o1 / l;
+}
+
+// x[b][t] = text_emb[tok] + enc_pos[t] (t < T[b]), zero rows for padding.
+__global__ void embed_text_kernel(const int *tok, const int *T, int Tmax, const float *text_emb,
+                                  const float *enc_pos, float *X) {
+    const int m = blockIdx.x, b = m / Tmax, t = m % Tmax;
+    const bool valid = t < T[b];
+    const int id = valid ? tok[m] : 0;
+    for (int k = threadIdx.x; k < D; k += blockDim.x)
+        X[(size_t)m * D + k] = valid ? text_emb[(size_t)id * D + k] + enc_pos[(size_t)t * D + k] : 0.f;
+}
+
+// x[b][t] = baked_context[spk_b][t] + dec_pos[t] for the 110 context frames (4138-4189).
+__global__ void embed_context_kernel(const int *spk, const float *baked, const float *dec_pos, float *X) {
+    const int m = blockIdx.x, b = m / CTX, t = m % CTX;
+    const float *src = baked + (size_t)spk[b] * CTX * D + (size_t)t * D;
+    for (int k = threadIdx.x; k < D; k += blockDim.x) X[(size_t)m * D + k] = src[k] + dec_pos[(size_t)t * D + k];
+}
+
+// ---------------------------------------------------------------- launchers
+template <int EPI, int TAPS>
+static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
+    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64);
+    hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s) {
+    if (p.conv_taps == 3) {
+        if (epi == GE_GELU) return launch_gemm<GE_GELU, 3>(p, s);
+        if (epi == GE_RESID) return launch_gemm<GE_RESID, 3>(p, s);
+        return hipErrorInvalidValue;
+    }
+    switch (epi) {
+    case GE_STORE: return launch_gemm<GE_STORE, 0>(p, s);
+    case GE_RESID: return launch_gemm<GE_RESID, 0>(p, s);
+    case GE_GELU: return launch_gemm<GE_GELU, 0>(p, s);
+    case GE_QKV_CACHE: return launch_gemm<GE_QKV_CACHE, 0>(p, s);
+    case GE_XAKV: return launch_gemm<GE_XAKV, 0>(p, s);
+    }
+    return hipErrorInvalidValue;
+}
+hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ldy, int M, float eps, hipStream_t s) {
+    hipLaunchKernelGGL(ln_rows_kernel, dim3(M), dim3(256), 0, s, X, ldx, w, Y, ldy, eps);
+    return hipGetLastError();
+}
+hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s) {
+    hipLaunchKernelGGL(row_attn_kernel, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t pre_row_xa(const RowXaP &p, hipStream_t s) {
+    hipLaunchKernelGGL(row_xa_kernel, dim3((p.M + 3) / 4), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t pre_embed_text(const int *tok, const int *T, int B, int Tmax, const float *te, const float *ep, float *X,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(embed_text_kernel, dim3(B * Tmax), dim3(256), 0, s, tok, T, Tmax, te, ep, X);
+    return hipGetLastError();
+}
+hipError_t pre_embed_context(const int *spk, int B, const float *baked, const float *dp, float *X, hipStream_t s) {
+    hipLaunchKernelGGL(embed_context_kernel, dim3(B * CTX), dim3(256), 0, s, spk, baked, dp, X);
+    return hipGetLastError();
+}
+
+}  // namespace mp

@@ -1,0 +1,63 @@
+// Parameter blocks + launchers of the per-utterance preamble kernels
+// (mp_prefill.hip), shared with the host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace mp {
+
+enum GemmEpi {
+    GE_STORE = 0,     // C[m][n] = v (+bias)
+    GE_RESID = 1,     // C[m][n] += v
+    GE_GELU = 2,      // C[m][n] = gelu(v)
+    GE_QKV_CACHE = 3, // n < D: q rows; k/v -> SA cache at position t (prefill, 3942-3955)
+    GE_XAKV = 4,      // n < 128: XA K, else XA V, at [b][layer][t]  (1689-1710)
+};
+
+struct GemmP {
+    const float *A;  // [M][lda]
+    int lda;
+    const float *W;  // [N][K]
+    const float *bias;
+    float *C;
+    int ldc;
+    int M, N, K;
+    int conv_taps;     // 0: plain A; 3: causal conv, A[m][i*3+k] = X[t-2+k][i] (1816-1866)
+    int rows_per_utt;  // for (b, t) decomposition of a row
+    const int *T;      // valid rows per utterance (conv zero padding / masking)
+    float *kc, *vc;
+    int layer, nlayers, max_seq;
+    float *xak, *xav;
+    int Tmax;
+};
+
+// Causal multi-head attention for every (row, head) of a block of rows.
+struct RowAttnP {
+    const float *Q;  // [M][ldq], head h at +h*64
+    int ldq;
+    const float *Kb, *Vb;
+    size_t utt_stride, row_stride;
+    float *O;  // [M][768]
+    int M, rows_per_utt, heads;
+    int key_limit_T;  // 1: also mask keys j >= T[b] (unused when causal suffices)
+    const int *T;
+};
+
+// Cross-attention for a block of rows (1 head x 128, no mask).
+struct RowXaP {
+    const float *Q;  // [M][128]
+    const float *xak, *xav;
+    int layer, nlayers, Tmax, rows_per_utt, M;
+    const int *T;
+    float *O;  // [M][128]
+};
+
+hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s);
+hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ldy, int M, float eps, hipStream_t s);
+hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s);
+hipError_t pre_row_xa(const RowXaP &p, hipStream_t s);
+hipError_t pre_embed_text(const int *tok, const int *T, int B, int Tmax, const float *te, const float *ep, float *X,
+                          hipStream_t s);
+hipError_t pre_embed_context(const int *spk, int B, const float *baked, const float *dp, float *X, hipStream_t s);
+
+}  // namespace mp

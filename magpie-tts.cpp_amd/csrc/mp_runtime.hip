@@ -1,0 +1,766 @@
+// Host runtime of the MI355X decode path: weight residency, per-batch device
+// state, the per-utterance preamble, and the hipGraph-captured frame loop.
+// Exposes the C-ABI declared in include/magpie_hip.h.
+//
+// Design: one mp_dev per GPU. Weights are uploaded once (f32, one
+// arena). A batch of B <= 8 utterances occupies NB = next_pow2(B) slots; every
+// per-utterance quantity (residual stream, KV cache, XA K/V, codes, position,
+// done flag) lives in HBM and is addressed by slot, so one decode iteration
+// (12 decoder layers + 8-codebook local transformer + EOS bookkeeping, 133
+// kernels at NB=1) is captured once as a hipGraph and replayed per frame with
+// no host round trip; the host only polls the done counter every few frames.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/magpie_hip.h"
+#include "mp_gguf.hpp"
+#include "mp_params.hpp"
+
+namespace mp {
+
+// ---- launchers (mp_decode.hip / mp_prefill.hip)
+using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
+#define MP_DECL_OPS(NB)                                                                                     \
+    hipError_t op_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t op_qkv_##NB(const GemvP &, hipStream_t);        \
+    hipError_t op_oproj_##NB(const GemvP &, hipStream_t); hipError_t op_xq_##NB(const GemvP &, hipStream_t);             \
+    hipError_t op_xo_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);               \
+    hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
+    hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
+    hipError_t op_lt_c_##NB(const GemvP &, hipStream_t); hipError_t op_lt_d_##NB(const GemvP &, hipStream_t);            \
+    hipError_t op_lt_e_##NB(const GemvP &, hipStream_t); hipError_t op_lt_f_##NB(const GemvP &, hipStream_t);
+MP_DECL_OPS(1)
+MP_DECL_OPS(2)
+MP_DECL_OPS(4)
+MP_DECL_OPS(8)
+hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
+hipError_t op_finalize(const FinP &, int, hipStream_t);
+
+}  // namespace mp
+
+#include "mp_prefill_api.hpp"
+
+namespace mp {
+
+struct OpTable { GemvFn qkv_embed, qkv, oproj, xq, xo, ff1, ff2, lt_in0, lt_a, lt_b, lt_c, lt_d, lt_e, lt_f; };
+#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_xq_##NB, op_xo_##NB, op_ff1_##NB, op_ff2_##NB, \
+                       op_lt_in0_##NB, op_lt_a_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, op_lt_f_##NB }
+static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
+static const OpTable &table_for(int NB) { return kTables[NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : 3]; }
+
+struct EncLayerW { const float *norm_self, *qkv, *o, *norm_ff, *ff1, *ff2; };
+struct DecLayerW { const float *norm_self, *qkv, *o, *norm_xq, *xq, *xkv, *xo, *norm_xmem, *norm_ff, *ff1, *ff2; };
+
+struct Model {
+    int enc_layers = 6, dec_layers = 12, n_spk = 5, dec_pos_rows = 0, text_vocab = 2380;
+    int audio_bos = 2016, audio_eos = 2017, max_dec_steps = 500;
+    float eps = 1e-5f;
+    const float *text_emb = nullptr, *enc_pos = nullptr, *enc_norm_out = nullptr, *dec_pos = nullptr;
+    const float *dec_norm_out = nullptr, *baked = nullptr, *audio_emb = nullptr;
+    std::vector<EncLayerW> enc;
+    std::vector<DecLayerW> dec;
+    const float *lt_in_w, *lt_in_b, *lt_pos, *lt_norm_self, *lt_qkv, *lt_o, *lt_norm_ff, *lt_ff1, *lt_ff2, *lt_out_w,
+        *lt_out_b;
+    float *arena = nullptr;
+    size_t arena_bytes = 0;
+};
+
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2 };
+struct OpRec {
+    std::string name;
+    int kind;
+    GemvFn fn;
+    GemvP g;
+    AttnP a;
+    FinP f;
+    int B;
+    double bytes;
+};
+
+}  // namespace mp
+
+struct mp_dev {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    mp::Model m;
+    bool loaded = false;
+    // batch configuration
+    int B = 0, NB = 0, Tmax = 0, max_steps = 0, max_seq = 0, nch = 0;
+    mp_params params{};
+    // device state (one allocation per buffer, sized for the configuration)
+    std::vector<void *> allocs;
+    float *x = nullptr, *q = nullptr, *part = nullptr, *qx = nullptr, *h = nullptr, *hidden = nullptr;
+    float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
+    float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
+          *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
+    int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
+        *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr;
+    // preamble scratch
+    float *pX = nullptr, *pH = nullptr, *pQKV = nullptr, *pATT = nullptr, *pF = nullptr, *pXQ = nullptr,
+          *pXAO = nullptr, *enc_out = nullptr;
+    // graph
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    std::vector<mp::OpRec> ops;
+    bool batch_ready = false;
+    mp_timing timing{};
+    int *h_ndone = nullptr;  // pinned
+};
+
+namespace {
+
+#define HIPCHK(expr)                                                                           \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            dev->err = std::string(#expr) + " failed: " + hipGetErrorString(e_);               \
+            return MP_ERR_HIP;                                                                 \
+        }                                                                                      \
+    } while (0)
+
+int fail(mp_dev *dev, int code, const std::string &msg) {
+    dev->err = msg;
+    return code;
+}
+
+template <class T> int dalloc(mp_dev *dev, T **p, size_t count) {
+    void *v = nullptr;
+    HIPCHK(hipMalloc(&v, count * sizeof(T) + 256));
+    HIPCHK(hipMemsetAsync(v, 0, count * sizeof(T) + 256, dev->stream));
+    dev->allocs.push_back(v);
+    *p = (T *)v;
+    return MP_OK;
+}
+
+void free_batch(mp_dev *dev) {
+    if (dev->exec) hipGraphExecDestroy(dev->exec);
+    if (dev->graph) hipGraphDestroy(dev->graph);
+    dev->exec = nullptr;
+    dev->graph = nullptr;
+    for (void *p : dev->allocs) hipFree(p);
+    dev->allocs.clear();
+    dev->ops.clear();
+    dev->batch_ready = false;
+    dev->B = dev->NB = dev->Tmax = dev->max_steps = 0;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// ------------------------------------------------------------------ weights
+// Tensor names and mapping: create_tensors (magpie.cpp:572-672).
+int load_model(mp_dev *dev, const char *path) {
+    mp::Gguf g;
+    std::string err;
+    if (!g.open(path, err)) return fail(dev, MP_ERR_IO, err);
+    mp::Model &m = dev->m;
+    // read_hparams (magpie.cpp:73-121): the reader's keys, struct defaults otherwise
+    if (g.get_u32("magpie.d_model", 768) != 768 || g.get_u32("magpie.d_ffn", 3072) != 3072 ||
+        g.get_u32("magpie.d_head", 64) != 64 || g.get_u32("magpie.dec_sa_heads", 12) != 12 ||
+        g.get_u32("magpie.dec_xa_heads", 1) != 1 || g.get_u32("magpie.dec_xa_d_head", 128) != 128 ||
+        g.get_u32("magpie.lt_dim", 256) != 256 || g.get_u32("magpie.lt_ffn_dim", 1024) != 1024 ||
+        g.get_u32("magpie.num_codebooks", 8) != 8 || g.get_u32("magpie.vocab_per_cb", 2024) != 2024 ||
+        g.get_u32("magpie.context_frames", 110) != 110 || g.get_u32("magpie.enc_heads", 12) != 12 ||
+        g.get_u32("magpie.enc_kernel", 3) != 3 || g.get_u32("magpie.dec_kernel", 1) != 1 ||
+        g.get_u32("magpie.lt_layers", 1) != 1 || g.get_u32("magpie.lt_heads", 1) != 1)
+        return fail(dev, MP_ERR_UNSUPPORTED, "model dimensions differ from Magpie-357M (kernels are specialised)");
+    m.enc_layers = (int)g.get_u32("magpie.enc_layers", 6);
+    m.dec_layers = (int)g.get_u32("magpie.dec_layers", 12);
+    m.n_spk = (int)g.get_u32("magpie.num_speakers", 5);
+    m.text_vocab = (int)g.get_u32("magpie.text_vocab_size", 2380);
+    m.audio_bos = (int)g.get_u32("magpie.audio_bos_id", 2016);
+    m.audio_eos = (int)g.get_u32("magpie.audio_eos_id", 2017);
+    m.max_dec_steps = (int)g.get_u32("magpie.max_dec_steps", 500);
+    m.eps = (float)g.get_f32("magpie.eps", 1e-5);
+    if (m.enc_layers < 1 || m.dec_layers < 1 || m.enc_layers > 64 || m.dec_layers > 64)
+        return fail(dev, MP_ERR_FORMAT, "bad layer counts");
+
+    struct Want { std::string name; int64_t n; const float **dst; };
+    std::vector<Want> want;
+    auto need = [&](const std::string &name, int64_t n, const float **dst) { want.push_back({name, n, dst}); };
+    const int64_t D = 768;
+    need("text_embedding.weight", (int64_t)m.text_vocab * D, &m.text_emb);
+    need("encoder.position_embeddings.weight", -1, &m.enc_pos);
+    m.enc.resize(m.enc_layers);
+    for (int l = 0; l < m.enc_layers; ++l) {
+        const std::string p = "encoder.layers." + std::to_string(l) + ".";
+        mp::EncLayerW &L = m.enc[l];
+        need(p + "norm_self.weight", D, &L.norm_self);
+        need(p + "self_attention.qkv_net.weight", 3 * D * D, &L.qkv);
+        need(p + "self_attention.o_net.weight", D * D, &L.o);
+        need(p + "norm_pos_ff.weight", D, &L.norm_ff);
+        need(p + "pos_ff.proj.conv.weight", 3072 * D * 3, &L.ff1);
+        need(p + "pos_ff.o_net.conv.weight", 3072 * D * 3, &L.ff2);
+    }
+    need("encoder.norm_out.weight", D, &m.enc_norm_out);
+    need("decoder.position_embeddings.weight", -1, &m.dec_pos);
+    m.dec.resize(m.dec_layers);
+    for (int l = 0; l < m.dec_layers; ++l) {
+        const std::string p = "decoder.layers." + std::to_string(l) + ".";
+        mp::DecLayerW &L = m.dec[l];
+        need(p + "norm_self.weight", D, &L.norm_self);
+        need(p + "self_attention.qkv_net.weight", 3 * D * D, &L.qkv);
+        need(p + "self_attention.o_net.weight", D * D, &L.o);
+        need(p + "norm_xattn_query.weight", D, &L.norm_xq);
+        need(p + "cross_attention.q_net.weight", 128 * D, &L.xq);
+        need(p + "cross_attention.kv_net.weight", 256 * D, &L.xkv);
+        need(p + "cross_attention.o_net.weight", D * 128, &L.xo);
+        need(p + "norm_xattn_memory.weight", D, &L.norm_xmem);
+        need(p + "norm_pos_ff.weight", D, &L.norm_ff);
+        need(p + "pos_ff.proj.conv.weight", 3072 * D, &L.ff1);
+        need(p + "pos_ff.o_net.conv.weight", 3072 * D, &L.ff2);
+    }
+    need("decoder.norm_out.weight", D, &m.dec_norm_out);
+    need("baked_context_embedding.weight", -1, &m.baked);
+    need("local_transformer_in_projection.weight", 256 * D, &m.lt_in_w);
+    need("local_transformer_in_projection.bias", 256, &m.lt_in_b);
+    need("local_transformer.position_embeddings.weight", -1, &m.lt_pos);
+    need("local_transformer.layers.0.norm_self.weight", 256, &m.lt_norm_self);
+    need("local_transformer.layers.0.self_attention.qkv_net.weight", 768 * 256, &m.lt_qkv);
+    need("local_transformer.layers.0.self_attention.o_net.weight", 256 * 256, &m.lt_o);
+    need("local_transformer.layers.0.norm_pos_ff.weight", 256, &m.lt_norm_ff);
+    need("local_transformer.layers.0.pos_ff.proj.conv.weight", 1024 * 256, &m.lt_ff1);
+    need("local_transformer.layers.0.pos_ff.o_net.conv.weight", 1024 * 256, &m.lt_ff2);
+    // per-codebook tensors become one contiguous [8][...] array each so a kernel
+    // can index them by a codebook read from device memory
+    std::vector<std::string> grouped[3];
+    for (int c = 0; c < 8; ++c) {
+        grouped[0].push_back("audio_embeddings." + std::to_string(c) + ".weight");
+        grouped[1].push_back("local_transformer_out_projections." + std::to_string(c) + ".weight");
+        grouped[2].push_back("local_transformer_out_projections." + std::to_string(c) + ".bias");
+    }
+    const int64_t gsize[3] = {2024 * D, 2024 * 256, 2024};
+    const float **gdst[3] = {&m.audio_emb, &m.lt_out_w, &m.lt_out_b};
+
+    // size the arena
+    auto align_up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    size_t total = 0;
+    for (auto &w : want) {
+        const mp::GgufTensor *t = g.find(w.name);
+        if (!t) return fail(dev, MP_ERR_FORMAT, "missing tensor " + w.name);
+        if (w.n >= 0 && t->nelements() != w.n) return fail(dev, MP_ERR_FORMAT, "unexpected shape for " + w.name);
+        total += align_up((size_t)t->nelements() * 4);
+    }
+    for (int k = 0; k < 3; ++k)
+        for (auto &nm : grouped[k]) {
+            const mp::GgufTensor *t = g.find(nm);
+            if (!t) return fail(dev, MP_ERR_FORMAT, "missing tensor " + nm);
+            if (t->nelements() != gsize[k]) return fail(dev, MP_ERR_FORMAT, "unexpected shape for " + nm);
+        }
+    for (int k = 0; k < 3; ++k) total += align_up((size_t)gsize[k] * 8 * 4);
+    {
+        const mp::GgufTensor *dp = g.find("decoder.position_embeddings.weight");
+        const mp::GgufTensor *bk = g.find("baked_context_embedding.weight");
+        const mp::GgufTensor *ep = g.find("encoder.position_embeddings.weight");
+        const mp::GgufTensor *lp = g.find("local_transformer.position_embeddings.weight");
+        if (dp->ne[0] != D || bk->ne[0] != 110 * D || ep->ne[0] != D || lp->ne[0] != 256 || lp->ne[1] < 8)
+            return fail(dev, MP_ERR_FORMAT, "unexpected embedding table shapes");
+        m.dec_pos_rows = (int)dp->ne[1];
+        m.n_spk = (int)std::min<int64_t>(m.n_spk, bk->ne[1]);
+    }
+    if (m.arena) { hipFree(m.arena); m.arena = nullptr; }
+    HIPCHK(hipMalloc(&m.arena, total));
+    m.arena_bytes = total;
+    std::vector<float> host;
+    size_t off = 0;
+    auto upload = [&](const mp::GgufTensor *t, float *dst) -> int {
+        host.resize((size_t)t->nelements());
+        if (!g.to_f32(*t, host.data())) return fail(dev, MP_ERR_FORMAT, "unsupported tensor type in " + t->name);
+        HIPCHK(hipMemcpy(dst, host.data(), host.size() * 4, hipMemcpyHostToDevice));
+        return MP_OK;
+    };
+    for (auto &w : want) {
+        const mp::GgufTensor *t = g.find(w.name);
+        float *dst = (float *)((char *)m.arena + off);
+        if (int rc = upload(t, dst)) return rc;
+        *w.dst = dst;
+        off += align_up((size_t)t->nelements() * 4);
+    }
+    for (int k = 0; k < 3; ++k) {
+        float *base = (float *)((char *)m.arena + off);
+        for (int c = 0; c < 8; ++c)
+            if (int rc = upload(g.find(grouped[k][c]), base + (size_t)c * gsize[k])) return rc;
+        *gdst[k] = base;
+        off += align_up((size_t)gsize[k] * 8 * 4);
+    }
+    dev->loaded = true;
+    return MP_OK;
+}
+
+// ------------------------------------------------------------------ batch state
+int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
+    free_batch(dev);
+    const int NB = B <= 1 ? 1 : B <= 2 ? 2 : B <= 4 ? 4 : 8;
+    const int L = dev->m.dec_layers;
+    dev->B = B;
+    dev->NB = NB;
+    dev->Tmax = Tmax;
+    dev->max_steps = max_steps;
+    dev->max_seq = mp::CTX + max_steps + 16;  // magpie.cpp:4077
+    dev->nch = (dev->max_seq + mp::SA_CHUNK - 1) / mp::SA_CHUNK;
+    const size_t D = 768;
+    int rc = MP_OK;
+#define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
+    A(x, NB * D); A(q, NB * D); A(part, (size_t)NB * 12 * dev->nch * mp::PART_STRIDE); A(qx, NB * 128);
+    A(h, NB * 3072); A(hidden, NB * D);
+    A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
+    A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
+    A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
+    A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
+    if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
+    A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);
+    A(codes_cur, NB * 8); A(codes_prev, NB * 8); A(codes_out, (size_t)NB * max_steps * 8); A(tok, (size_t)NB * Tmax);
+    const size_t rows = (size_t)NB * std::max(Tmax, mp::CTX);
+    A(pX, rows * D); A(pH, rows * D); A(pQKV, rows * 3 * D); A(pATT, rows * D); A(pF, rows * 3072);
+    A(pXQ, rows * 128); A(pXAO, rows * 128); A(enc_out, (size_t)NB * Tmax * D);
+#undef A
+    return MP_OK;
+}
+
+mp::GemvP gemv_base(mp_dev *dev) {
+    mp::GemvP g;
+    memset(&g, 0, sizeof g);
+    g.eps = dev->m.eps;
+    g.nlayers = dev->m.dec_layers;
+    g.max_seq = dev->max_seq;
+    g.Tmax = dev->Tmax;
+    g.T = dev->T;
+    g.pos = dev->pos;
+    g.step = dev->step;
+    g.ndone = dev->ndone;
+    g.nslots = dev->NB;
+    g.ignore_eos = dev->params.ignore_eos;
+    g.audio_bos = dev->m.audio_bos;
+    g.audio_eos = dev->m.audio_eos;
+    return g;
+}
+
+// Enqueue one decode iteration: decoder step at pos (embedding codes_prev), LT
+// over 8 codebooks, finalize. When `record` is set, the op list is rebuilt for
+// measurement (mp_hip_time_op).
+int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
+    const mp::Model &m = dev->m;
+    const int NB = dev->NB, L = m.dec_layers;
+    const mp::OpTable &tb = mp::table_for(NB);
+    const double F = 4.0, act = (double)NB;
+    if (record) dev->ops.clear();
+    auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
+        if (record) {
+            mp::OpRec r{};
+            r.name = name; r.kind = mp::K_GEMV; r.fn = fn; r.g = g; r.B = NB; r.bytes = bytes;
+            dev->ops.push_back(r);
+        }
+        HIPCHK(fn(g, s));
+        return MP_OK;
+    };
+    int rc;
+    for (int l = 0; l < L; ++l) {
+        const mp::DecLayerW &W = m.dec[l];
+        mp::GemvP g = gemv_base(dev);
+        g.layer = l;
+        // LN + QKV (+ frame embedding on layer 0) + KV append   (3415-3442)
+        g.W = W.qkv; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
+        g.kc = dev->kc; g.vc = dev->vc;
+        if (l == 0) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
+        if ((rc = run(l == 0 ? "qkv_embed" : "qkv", l == 0 ? tb.qkv_embed : tb.qkv, g,
+                      F * (2304.0 * 768 + act * (768 + 2304)))) != MP_OK) return rc;
+        // split-K self-attention over the cache (3457-3476)
+        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->part, dev->nch, dev->ndone, NB};
+        if (record) {
+            mp::OpRec r{};
+            r.name = "sa_attn"; r.kind = mp::K_ATTN; r.a = a; r.B = NB;
+            r.bytes = -1;  // depends on the live cache length; computed at timing time
+            dev->ops.push_back(r);
+        }
+        HIPCHK(mp::op_sa_attn(a, NB, s));
+        // O-proj + residual, combine fused in the prologue (3479, 3509)
+        g = gemv_base(dev); g.layer = l;
+        g.W = W.o; g.N = 768; g.part = dev->part; g.nch = dev->nch; g.resid = dev->x;
+        if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768 + act * (768 * 2 + 12.0 * dev->nch * 80)))) != MP_OK) return rc;
+        // LN + XA query (1733)
+        g = gemv_base(dev); g.layer = l;
+        g.W = W.xq; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768; g.out = dev->qx; g.out_ld = 128;
+        if ((rc = run("xq", tb.xq, g, F * (128.0 * 768 + act * (768 + 128)))) != MP_OK) return rc;
+        // XA attention (prologue) + XA out-proj + residual (1742-1764, 3519)
+        g = gemv_base(dev); g.layer = l;
+        g.W = W.xo; g.N = 768; g.qx = dev->qx; g.xak = dev->xak; g.xav = dev->xav; g.resid = dev->x;
+        if ((rc = run("xo", tb.xo, g, F * (768.0 * 128 + act * (128 + 2.0 * 128 * dev->Tmax + 2 * 768)))) != MP_OK) return rc;
+        // LN + FFN up + GELU (1796-1799)
+        g = gemv_base(dev); g.layer = l;
+        g.W = W.ff1; g.N = 3072; g.lnw = W.norm_ff; g.src = dev->x; g.src_ld = 768; g.out = dev->h; g.out_ld = 3072;
+        if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768 + act * (768 + 3072)))) != MP_OK) return rc;
+        // FFN down + residual (1805, 3525)
+        g = gemv_base(dev); g.layer = l;
+        g.W = W.ff2; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.resid = dev->x;
+        if ((rc = run("ff2", tb.ff2, g, F * (768.0 * 3072 + act * (3072 + 2 * 768)))) != MP_OK) return rc;
+    }
+    // final LN -> hidden (4394) fused into LT in_proj (1162-1163)
+    {
+        mp::GemvP g = gemv_base(dev);
+        g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.lnw = m.dec_norm_out; g.src = dev->x; g.src_ld = 768;
+        g.hidden_out = dev->hidden; g.out = dev->lt_s; g.out_ld = 9 * 256;
+        if (dev->trace) { g.trace = dev->trace; g.trace_steps = dev->max_steps + 1; }
+        if ((rc = run("lt_in0", tb.lt_in0, g, F * (256.0 * 768 + act * (768 + 768 + 256)))) != MP_OK) return rc;
+    }
+    for (int cb = 0; cb < 8; ++cb) {
+        mp::GemvP g = gemv_base(dev);
+        g.cb = cb;
+        g.W = m.lt_qkv; g.N = 768; g.lt_s = dev->lt_s; g.lt_pos = m.lt_pos; g.ltX = dev->ltX; g.lnw = m.lt_norm_self;
+        g.lq = dev->ltq; g.lk = dev->ltk; g.lv = dev->ltv;
+        if ((rc = run("lt_a", tb.lt_a, g, F * (768.0 * 256 + act * (256 * 3 + 768)))) != MP_OK) return rc;
+        g = gemv_base(dev); g.cb = cb;
+        g.W = m.lt_o; g.N = 256; g.ltq = dev->ltq; g.ltk = dev->ltk; g.ltv = dev->ltv; g.out = dev->ltY; g.out_ld = 256;
+        g.addsrc = dev->ltX;
+        if ((rc = run("lt_b", tb.lt_b, g, F * (256.0 * 256 + act * (256 * (2 * cb + 5))))) != MP_OK) return rc;
+        g = gemv_base(dev); g.cb = cb;
+        g.W = m.lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = dev->ltY; g.src_ld = 256; g.out = dev->ltf; g.out_ld = 1024;
+        if ((rc = run("lt_c", tb.lt_c, g, F * (1024.0 * 256 + act * (256 + 1024)))) != MP_OK) return rc;
+        g = gemv_base(dev); g.cb = cb;
+        g.W = m.lt_ff2; g.N = 256; g.src = dev->ltf; g.src_ld = 1024; g.out = dev->lty2; g.out_ld = 256; g.addsrc = dev->ltY;
+        if ((rc = run("lt_d", tb.lt_d, g, F * (256.0 * 1024 + act * (1024 + 512)))) != MP_OK) return rc;
+        g = gemv_base(dev); g.cb = cb;
+        g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024; g.bias = m.lt_out_b + (size_t)cb * 2024;
+        g.src = dev->lty2; g.src_ld = 256; g.out = dev->logits; g.out_ld = 2024;
+        if ((rc = run("lt_e", tb.lt_e, g, F * (2024.0 * 256 + 2024 + act * (256 + 2024)))) != MP_OK) return rc;
+        if (cb < 7) {
+            g = gemv_base(dev); g.cb = cb;
+            g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.logits = dev->logits; g.codes_cur = dev->codes_cur;
+            g.emb = m.audio_emb; g.out = dev->lt_s + (size_t)(cb + 1) * 256; g.out_ld = 9 * 256;
+            if ((rc = run("lt_f", tb.lt_f, g, F * (256.0 * 768 + act * (2024 + 768 + 256)))) != MP_OK) return rc;
+        }
+    }
+    mp::FinP f{dev->logits, dev->codes_cur, dev->codes_prev, dev->codes_out, dev->step, dev->pos, dev->done,
+               dev->nframes, dev->ndone, dev->max_steps, dev->params.ignore_eos, m.audio_bos, m.audio_eos, NB};
+    if (record) {
+        mp::OpRec r{};
+        r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = F * act * 2024;
+        dev->ops.push_back(r);
+    }
+    HIPCHK(mp::op_finalize(f, NB, s));
+    return MP_OK;
+}
+
+// ------------------------------------------------------------------ preamble
+int run_preamble(mp_dev *dev) {
+    using namespace mp;
+    const Model &m = dev->m;
+    const int NB = dev->NB, Tmax = dev->Tmax, L = m.dec_layers;
+    hipStream_t s = dev->stream;
+    const int Me = NB * Tmax;
+    // --- text encoder (magpie_build_full_encoder, 1960-1995)
+    HIPCHK(pre_embed_text(dev->tok, dev->T, NB, Tmax, m.text_emb, m.enc_pos, dev->pX, s));
+    for (int l = 0; l < m.enc_layers; ++l) {
+        const EncLayerW &W = m.enc[l];
+        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_self, dev->pH, 768, Me, m.eps, s));
+        GemmP gp{};
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Me; gp.N = 2304; gp.K = 768;
+        gp.rows_per_utt = Tmax; gp.T = dev->T;
+        HIPCHK(pre_gemm(gp, GE_STORE, s));
+        RowAttnP ra{};
+        ra.Q = dev->pQKV; ra.ldq = 2304; ra.Kb = dev->pQKV + 768; ra.Vb = dev->pQKV + 1536;
+        ra.utt_stride = (size_t)Tmax * 2304; ra.row_stride = 2304; ra.O = dev->pATT; ra.M = Me; ra.rows_per_utt = Tmax;
+        ra.heads = 12; ra.T = dev->T;
+        HIPCHK(pre_row_attn(ra, s));
+        gp = GemmP{};
+        gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.C = dev->pX; gp.ldc = 768; gp.M = Me; gp.N = 768; gp.K = 768;
+        gp.rows_per_utt = Tmax; gp.T = dev->T;
+        HIPCHK(pre_gemm(gp, GE_RESID, s));
+        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_ff, dev->pH, 768, Me, m.eps, s));
+        gp = GemmP{};  // causal conv k=3 d_model -> d_ffn + GELU (1816-1869)
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.ff1; gp.C = dev->pF; gp.ldc = 3072; gp.M = Me; gp.N = 3072;
+        gp.K = 768 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = dev->T;
+        HIPCHK(pre_gemm(gp, GE_GELU, s));
+        gp = GemmP{};  // causal conv k=3 d_ffn -> d_model + residual (1875-1916)
+        gp.A = dev->pF; gp.lda = 3072; gp.W = W.ff2; gp.C = dev->pX; gp.ldc = 768; gp.M = Me; gp.N = 768;
+        gp.K = 3072 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = dev->T;
+        HIPCHK(pre_gemm(gp, GE_RESID, s));
+    }
+    HIPCHK(pre_ln_rows(dev->pX, 768, m.enc_norm_out, dev->enc_out, 768, Me, m.eps, s));
+    // --- cross-attention K/V per layer (1663-1711)
+    for (int l = 0; l < L; ++l) {
+        HIPCHK(pre_ln_rows(dev->enc_out, 768, m.dec[l].norm_xmem, dev->pH, 768, Me, m.eps, s));
+        GemmP gp{};
+        gp.A = dev->pH; gp.lda = 768; gp.W = m.dec[l].xkv; gp.M = Me; gp.N = 256; gp.K = 768; gp.rows_per_utt = Tmax;
+        gp.T = dev->T; gp.xak = dev->xak; gp.xav = dev->xav; gp.layer = l; gp.nlayers = L; gp.Tmax = Tmax;
+        HIPCHK(pre_gemm(gp, GE_XAKV, s));
+    }
+    // --- baked context + 110-frame causal prefill (3991-4060, 4167-4238)
+    const int Mc = NB * CTX;
+    HIPCHK(pre_embed_context(dev->spk, NB, m.baked, m.dec_pos, dev->pX, s));
+    for (int l = 0; l < L; ++l) {
+        const DecLayerW &W = m.dec[l];
+        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_self, dev->pH, 768, Mc, m.eps, s));
+        GemmP gp{};
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Mc; gp.N = 2304; gp.K = 768;
+        gp.rows_per_utt = CTX; gp.kc = dev->kc; gp.vc = dev->vc; gp.layer = l; gp.nlayers = L; gp.max_seq = dev->max_seq;
+        HIPCHK(pre_gemm(gp, GE_QKV_CACHE, s));
+        RowAttnP ra{};
+        ra.Q = dev->pQKV; ra.ldq = 2304;
+        ra.Kb = dev->kc + (size_t)l * dev->max_seq * 768; ra.Vb = dev->vc + (size_t)l * dev->max_seq * 768;
+        ra.utt_stride = (size_t)L * dev->max_seq * 768; ra.row_stride = 768; ra.O = dev->pATT; ra.M = Mc;
+        ra.rows_per_utt = CTX; ra.heads = 12; ra.T = dev->T;
+        HIPCHK(pre_row_attn(ra, s));
+        gp = GemmP{};
+        gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 768;
+        gp.rows_per_utt = CTX;
+        HIPCHK(pre_gemm(gp, GE_RESID, s));
+        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_xq, dev->pH, 768, Mc, m.eps, s));
+        gp = GemmP{};
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.xq; gp.C = dev->pXQ; gp.ldc = 128; gp.M = Mc; gp.N = 128; gp.K = 768;
+        gp.rows_per_utt = CTX;
+        HIPCHK(pre_gemm(gp, GE_STORE, s));
+        RowXaP rx{dev->pXQ, dev->xak, dev->xav, l, L, Tmax, CTX, Mc, dev->T, dev->pXAO};
+        HIPCHK(pre_row_xa(rx, s));
+        gp = GemmP{};
+        gp.A = dev->pXAO; gp.lda = 128; gp.W = W.xo; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 128;
+        gp.rows_per_utt = CTX;
+        HIPCHK(pre_gemm(gp, GE_RESID, s));
+        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_ff, dev->pH, 768, Mc, m.eps, s));
+        gp = GemmP{};
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.ff1; gp.C = dev->pF; gp.ldc = 3072; gp.M = Mc; gp.N = 3072; gp.K = 768;
+        gp.rows_per_utt = CTX;
+        HIPCHK(pre_gemm(gp, GE_GELU, s));
+        gp = GemmP{};
+        gp.A = dev->pF; gp.lda = 3072; gp.W = W.ff2; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 3072;
+        gp.rows_per_utt = CTX;
+        HIPCHK(pre_gemm(gp, GE_RESID, s));
+    }
+    return MP_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+int mp_hip_device_count(int *n) {
+    if (!n) return MP_ERR_ARG;
+    if (hipGetDeviceCount(n) != hipSuccess) { *n = 0; return MP_ERR_HIP; }
+    return MP_OK;
+}
+
+int mp_hip_init(int device, mp_dev **out) {
+    if (!out) return MP_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return MP_ERR_HIP;
+    mp_dev *dev = new mp_dev();
+    dev->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&dev->h_ndone, 64, 0) != hipSuccess) {
+        delete dev;
+        return MP_ERR_HIP;
+    }
+    *out = dev;
+    return MP_OK;
+}
+
+int mp_hip_load_model(mp_dev *dev, const char *path) {
+    if (!dev || !path) return MP_ERR_ARG;
+    HIPCHK(hipSetDevice(dev->device));
+    free_batch(dev);
+    return load_model(dev, path);
+}
+
+int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes) {
+    if (!dev || !dev->loaded) return MP_ERR_STATE;
+    if (dec_layers) *dec_layers = dev->m.dec_layers;
+    if (enc_layers) *enc_layers = dev->m.enc_layers;
+    if (weight_bytes) *weight_bytes = dev->m.arena_bytes;
+    return MP_OK;
+}
+
+void mp_hip_free(mp_dev *dev) {
+    if (!dev) return;
+    hipSetDevice(dev->device);
+    if (dev->stream) hipStreamSynchronize(dev->stream);
+    free_batch(dev);
+    if (dev->m.arena) hipFree(dev->m.arena);
+    if (dev->h_ndone) hipHostFree(dev->h_ndone);
+    if (dev->stream) hipStreamDestroy(dev->stream);
+    delete dev;
+}
+
+const char *mp_hip_error(mp_dev *dev) { return dev ? dev->err.c_str() : "null mp_dev"; }
+
+int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_tokens, const int32_t *speaker, int B,
+                       int tmax, const mp_params *params) {
+    if (!dev) return MP_ERR_ARG;
+    if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
+    if (!tokens || !n_tokens || !speaker || B < 1 || B > 8 || tmax < 1 || !params)
+        return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..8)");
+    if (params->temperature >= 0.01f)
+        return fail(dev, MP_ERR_UNSUPPORTED, "temperature sampling is not implemented on the device path yet");
+    int Tmax = 0;
+    for (int b = 0; b < B; ++b) {
+        if (n_tokens[b] < 1 || n_tokens[b] > tmax) return fail(dev, MP_ERR_ARG, "n_tokens out of range");
+        if (speaker[b] < 0 || speaker[b] >= dev->m.n_spk) return fail(dev, MP_ERR_ARG, "speaker id out of range");
+        for (int t = 0; t < n_tokens[b]; ++t)
+            if (tokens[(size_t)b * tmax + t] < 0 || tokens[(size_t)b * tmax + t] >= dev->m.text_vocab)
+                return fail(dev, MP_ERR_ARG, "token id out of range");
+        Tmax = std::max(Tmax, (int)n_tokens[b]);
+    }
+    if (Tmax > mp::TMAX_LIMIT || Tmax > 4096) return fail(dev, MP_ERR_ARG, "too many text tokens");
+    const int max_steps = params->max_dec_steps > 0 ? params->max_dec_steps : dev->m.max_dec_steps;
+    if (mp::CTX + max_steps > dev->m.dec_pos_rows)
+        return fail(dev, MP_ERR_ARG, "max_dec_steps exceeds the decoder position table");
+    HIPCHK(hipSetDevice(dev->device));
+    const bool trace = params->trace_hidden != 0;
+    const bool same = dev->NB > 0 && dev->B == B && dev->Tmax == Tmax && dev->max_steps == max_steps &&
+                      (dev->trace != nullptr) == trace && dev->params.ignore_eos == params->ignore_eos;
+    dev->params = *params;
+    if (!same) {
+        if (int rc = alloc_batch(dev, B, Tmax, max_steps, trace)) return rc;
+    }
+    const int NB = dev->NB;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<int> h_tok((size_t)NB * Tmax, 0), h_T(NB, 1), h_spk(NB, 0);
+    for (int b = 0; b < B; ++b) {
+        h_T[b] = n_tokens[b];
+        h_spk[b] = speaker[b];
+        for (int t = 0; t < n_tokens[b]; ++t) h_tok[(size_t)b * Tmax + t] = tokens[(size_t)b * tmax + t];
+    }
+    for (int b = B; b < NB; ++b) { h_T[b] = h_T[0]; h_spk[b] = h_spk[0]; }
+    HIPCHK(hipMemcpyAsync(dev->tok, h_tok.data(), h_tok.size() * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(dev->T, h_T.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(dev->spk, h_spk.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+    if (int rc = run_preamble(dev)) return rc;
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    dev->timing = mp_timing{};
+    dev->timing.preamble_ms = ms_since(t0);
+    dev->batch_ready = true;
+    return MP_OK;
+}
+
+int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
+    if (!dev) return MP_ERR_ARG;
+    if (!dev->batch_ready) return fail(dev, MP_ERR_STATE, "mp_hip_begin_batch must precede mp_hip_decode");
+    HIPCHK(hipSetDevice(dev->device));
+    const int NB = dev->NB, B = dev->B;
+    // iteration state: BOS frame at position 110 (magpie.cpp:4243-4318)
+    std::vector<int> h_pos(NB, mp::CTX), h_zero(NB, 0), h_done(NB, 0), h_prev((size_t)NB * 8, dev->m.audio_bos);
+    for (int b = B; b < NB; ++b) h_done[b] = 1;
+    int h_nd[4] = {NB - B, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(dev->pos, h_pos.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(dev->step, h_zero.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(dev->nframes, h_zero.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(dev->done, h_done.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(dev->ndone, h_nd, 16, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
+    if (!dev->exec) {
+        // capture one iteration; the op list is recorded for measurement
+        HIPCHK(hipStreamBeginCapture(dev->stream, hipStreamCaptureModeThreadLocal));
+        int rc = enqueue_iteration(dev, dev->stream, true);
+        hipGraph_t g = nullptr;
+        hipError_t e = hipStreamEndCapture(dev->stream, &g);
+        if (rc != MP_OK) { if (g) hipGraphDestroy(g); return rc; }
+        if (e != hipSuccess) return fail(dev, MP_ERR_HIP, std::string("graph capture failed: ") + hipGetErrorString(e));
+        dev->graph = g;
+        HIPCHK(hipGraphInstantiate(&dev->exec, dev->graph, nullptr, nullptr, 0));
+    }
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, dev->stream));
+    const int poll = 8;
+    int it = 0;
+    for (; it < dev->max_steps; ++it) {
+        HIPCHK(hipGraphLaunch(dev->exec, dev->stream));
+        if (!dev->params.ignore_eos && (it + 1) % poll == 0 && it + 1 < dev->max_steps) {
+            HIPCHK(hipMemcpyAsync(dev->h_ndone, dev->ndone, 4, hipMemcpyDeviceToHost, dev->stream));
+            HIPCHK(hipStreamSynchronize(dev->stream));
+            if (*dev->h_ndone >= NB) { ++it; break; }
+        }
+    }
+    HIPCHK(hipEventRecord(e1, dev->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    std::vector<int> h_nf(NB);
+    HIPCHK(hipMemcpy(h_nf.data(), dev->nframes, NB * 4, hipMemcpyDeviceToHost));
+    std::vector<int> h_codes((size_t)NB * dev->max_steps * 8);
+    HIPCHK(hipMemcpy(h_codes.data(), dev->codes_out, h_codes.size() * 4, hipMemcpyDeviceToHost));
+    int total = 0;
+    for (int b = 0; b < B; ++b) {
+        if (n_frames) n_frames[b] = h_nf[b];
+        total += h_nf[b];
+    }
+    if (codes_out) memcpy(codes_out, h_codes.data(), (size_t)B * dev->max_steps * 8 * 4);
+    dev->timing.decode_ms = ms;
+    dev->timing.frames_total = total;
+    dev->timing.iterations = it;
+    return MP_OK;
+}
+
+int mp_hip_get_trace(mp_dev *dev, float *hidden) {
+    if (!dev || !hidden) return MP_ERR_ARG;
+    if (!dev->trace) return fail(dev, MP_ERR_STATE, "trace_hidden was not enabled");
+    HIPCHK(hipMemcpy(hidden, dev->trace, (size_t)dev->B * (dev->max_steps + 1) * 768 * 4, hipMemcpyDeviceToHost));
+    return MP_OK;
+}
+
+int mp_hip_get_timing(mp_dev *dev, mp_timing *t) {
+    if (!dev || !t) return MP_ERR_ARG;
+    *t = dev->timing;
+    return MP_OK;
+}
+
+int mp_hip_num_ops(mp_dev *dev) { return dev ? (int)dev->ops.size() : 0; }
+
+const char *mp_hip_op_name(mp_dev *dev, int op) {
+    if (!dev || op < 0 || op >= (int)dev->ops.size()) return "";
+    return dev->ops[op].name.c_str();
+}
+
+double mp_hip_op_bytes(mp_dev *dev, int op) {
+    if (!dev || op < 0 || op >= (int)dev->ops.size()) return -1.0;
+    const mp::OpRec &r = dev->ops[op];
+    if (r.kind == mp::K_ATTN) {
+        // live cache length of slot 0 after the run: keys 0..pos
+        int pos = 0;
+        hipMemcpy(&pos, dev->pos, 4, hipMemcpyDeviceToHost);
+        return 4.0 * dev->NB * ((double)(pos + 1) * 768 * 2 + 768 + 12.0 * dev->nch * 80);
+    }
+    return r.bytes;
+}
+
+int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
+    if (!dev || !avg_us || reps < 1 || op < 0 || op >= (int)dev->ops.size()) return MP_ERR_ARG;
+    HIPCHK(hipSetDevice(dev->device));
+    mp::OpRec r = dev->ops[op];
+    r.g.ndone = nullptr;
+    r.a.ndone = nullptr;
+    r.g.trace = nullptr;
+    std::vector<hipEvent_t> ev(2 * (size_t)reps);
+    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+    for (int i = 0; i < reps; ++i) {
+        HIPCHK(hipEventRecord(ev[2 * i], dev->stream));
+        if (r.kind == mp::K_GEMV) HIPCHK(r.fn(r.g, dev->stream));
+        else if (r.kind == mp::K_ATTN) HIPCHK(mp::op_sa_attn(r.a, r.B, dev->stream));
+        else return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");
+        HIPCHK(hipEventRecord(ev[2 * i + 1], dev->stream));
+    }
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    double tot = 0.0;
+    for (int i = 0; i < reps; ++i) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+        tot += ms;
+    }
+    for (auto &e : ev) hipEventDestroy(e);
+    *avg_us = (float)(tot * 1000.0 / reps);
+    return MP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,240 @@
+"""magpie_amd — Python binding of the MI355X-native Magpie decode path.
+
+The product is the C-ABI shared library ``lib/libmagpie_hip.so`` (hand-written
+gfx950 HIP kernels + runtime, boundary declared in ``include/magpie_hip.h``).
+This module only binds it with ctypes: no torch types, no fallback. If the
+library or a GPU is missing, every entry point raises — there is deliberately
+no CPU path here (the CPU oracle under ``oracle/`` is test infrastructure).
+
+Reference interface mirrored (m1el/magpie-tts.cpp, src/magpie.h):
+  magpie_init / magpie_free              -> Device(model_path) / Device.close()
+  magpie_synthesize_codes_graph_reuse    -> Device.synthesize(tokens, ...)   (magpie.h:592-595)
+  magpie_codec_init / magpie_codec_decode -> Codec(path).decode(codes)       (magpie.h:746-759)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmagpie_hip.so")
+SYNTH_BIN = os.path.join(PKG_DIR, "bin", "mp_synth_gguf")
+
+MP_OK = 0
+_ERRS = {-1: "MP_ERR_ARG", -2: "MP_ERR_HIP", -3: "MP_ERR_IO", -4: "MP_ERR_FORMAT", -5: "MP_ERR_STATE",
+         -6: "MP_ERR_UNSUPPORTED"}
+
+# magpie.h:70-73 token constants
+TEXT_BOS, TEXT_EOS, AUDIO_BOS, AUDIO_EOS = 2378, 2379, 2016, 2017
+NUM_CODEBOOKS, VOCAB_PER_CB, CONTEXT_FRAMES = 8, 2024, 110
+FRAMES_PER_SECOND = 22050.0 / 1024.0  # 21.533 codec frames per audio second
+
+
+class MagpieError(RuntimeError):
+    pass
+
+
+class mp_params(ctypes.Structure):
+    _fields_ = [("temperature", ctypes.c_float), ("top_k", ctypes.c_int), ("max_dec_steps", ctypes.c_int),
+                ("ignore_eos", ctypes.c_int), ("seed", ctypes.c_uint64), ("trace_hidden", ctypes.c_int)]
+
+
+class mp_timing(ctypes.Structure):
+    _fields_ = [("preamble_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("frames_total", ctypes.c_int),
+                ("iterations", ctypes.c_int)]
+
+
+# (name, restype, argtypes) of every symbol include/magpie_hip.h declares
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+SYMBOLS = [
+    ("mp_hip_device_count", _I, [ctypes.POINTER(_I)]),
+    ("mp_hip_init", _I, [_I, ctypes.POINTER(_P)]),
+    ("mp_hip_load_model", _I, [_P, ctypes.c_char_p]),
+    ("mp_hip_model_info", _I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_size_t)]),
+    ("mp_hip_free", None, [_P]),
+    ("mp_hip_error", ctypes.c_char_p, [_P]),
+    ("mp_hip_begin_batch", _I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(mp_params)]),
+    ("mp_hip_decode", _I, [_P, _P, _P]),
+    ("mp_hip_get_trace", _I, [_P, _P]),
+    ("mp_hip_get_timing", _I, [_P, ctypes.POINTER(mp_timing)]),
+    ("mp_hip_num_ops", _I, [_P]),
+    ("mp_hip_op_name", ctypes.c_char_p, [_P, _I]),
+    ("mp_hip_op_bytes", ctypes.c_double, [_P, _I]),
+    ("mp_hip_time_op", _I, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+    ("mp_hip_codec_init", _I, [_I, ctypes.c_char_p, ctypes.POINTER(_P)]),
+    ("mp_hip_codec_decode", _I, [_P, _P, _I, _P]),
+    ("mp_hip_codec_free", None, [_P]),
+    ("mp_hip_codec_error", ctypes.c_char_p, [_P]),
+]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libmagpie_hip.so (RTLD_GLOBAL so its HIP runtime is the process's)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise MagpieError(f"{path} is missing: build it with `make -C {PKG_DIR}` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, res, args in SYMBOLS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    load_library().mp_hip_device_count(ctypes.byref(n))
+    return n.value
+
+
+def build(jobs: int = 8) -> None:
+    subprocess.run(["make", "-C", PKG_DIR, f"-j{jobs}"], check=True)
+
+
+def synth_gguf(path: str, kind: str = "magpie", seed: int = 0x4D414750, dtype: str = "f32",
+               dec_layers: int = 12, enc_layers: int = 6) -> str:
+    """Write (or reuse) a deterministic synthetic GGUF with the reference's layout."""
+    if os.path.exists(path):
+        return path
+    cmd = [SYNTH_BIN, kind, path, "--seed", str(seed)]
+    if kind == "magpie":
+        cmd += ["--dtype", dtype, "--dec-layers", str(dec_layers), "--enc-layers", str(enc_layers)]
+    subprocess.run(cmd, check=True)
+    return path
+
+
+def synthetic_tokens(T: int, seed: int) -> np.ndarray:
+    """BOS + (T-2) ids ~ U[0,96) + EOS, seeded per utterance."""
+    rng = np.random.default_rng(seed)
+    body = rng.integers(0, 96, max(T - 2, 0))
+    return np.concatenate([[TEXT_BOS], body, [TEXT_EOS]]).astype(np.int32)[:T]
+
+
+@dataclass
+class SynthResult:
+    codes: List[np.ndarray]          # per utterance [n_frames][8]
+    n_frames: np.ndarray
+    preamble_ms: float
+    decode_ms: float
+    iterations: int
+    hidden: Optional[np.ndarray] = None  # [B][max_steps+1][768] when traced
+
+
+class Device:
+    """One GPU with resident Magpie weights (magpie_init_with_backend, magpie.cpp:781)."""
+
+    def __init__(self, model_path: str, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.mp_hip_init(device, ctypes.byref(h))
+        if rc != MP_OK or not h.value:
+            raise MagpieError(f"mp_hip_init(device={device}) failed ({_ERRS.get(rc, rc)}): no usable HIP device")
+        self.h = h
+        self._check(self.lib.mp_hip_load_model(self.h, model_path.encode()))
+
+    def _check(self, rc: int) -> None:
+        if rc != MP_OK:
+            msg = self.lib.mp_hip_error(self.h).decode(errors="replace")
+            raise MagpieError(f"{_ERRS.get(rc, rc)}: {msg}")
+
+    def close(self) -> None:
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.mp_hip_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def model_info(self):
+        dl, el, wb = ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
+        self._check(self.lib.mp_hip_model_info(self.h, ctypes.byref(dl), ctypes.byref(el), ctypes.byref(wb)))
+        return {"dec_layers": dl.value, "enc_layers": el.value, "weight_bytes": wb.value}
+
+    def synthesize(self, tokens: Sequence[Sequence[int]], speakers: Optional[Sequence[int]] = None,
+                   max_dec_steps: int = 500, temperature: float = 0.0, top_k: int = 80, ignore_eos: bool = False,
+                   seed: int = 0, trace: bool = False) -> SynthResult:
+        """Batched magpie_synthesize_codes_graph_reuse over independent utterances."""
+        B = len(tokens)
+        tmax = max(len(t) for t in tokens)
+        tok = np.zeros((B, tmax), np.int32)
+        for b, t in enumerate(tokens):
+            tok[b, :len(t)] = np.asarray(t, np.int32)
+        nt = np.array([len(t) for t in tokens], np.int32)
+        spk = np.zeros(B, np.int32) if speakers is None else np.asarray(speakers, np.int32)
+        p = mp_params(temperature, top_k, max_dec_steps, int(ignore_eos), seed, int(trace))
+        self._check(self.lib.mp_hip_begin_batch(self.h, tok.ctypes.data, nt.ctypes.data, spk.ctypes.data, B, tmax,
+                                                ctypes.byref(p)))
+        return self.decode(B, max_dec_steps, trace)
+
+    def decode(self, B: int, max_dec_steps: int, trace: bool = False) -> SynthResult:
+        codes = np.zeros((B, max_dec_steps, 8), np.int32)
+        nf = np.zeros(B, np.int32)
+        self._check(self.lib.mp_hip_decode(self.h, codes.ctypes.data, nf.ctypes.data))
+        tm = mp_timing()
+        self._check(self.lib.mp_hip_get_timing(self.h, ctypes.byref(tm)))
+        hidden = None
+        if trace:
+            hidden = np.zeros((B, max_dec_steps + 1, 768), np.float32)
+            self._check(self.lib.mp_hip_get_trace(self.h, hidden.ctypes.data))
+        return SynthResult([codes[b, :nf[b]].copy() for b in range(B)], nf, tm.preamble_ms, tm.decode_ms,
+                           tm.iterations, hidden)
+
+    # ---- measurement
+    def ops(self) -> List[str]:
+        return [self.lib.mp_hip_op_name(self.h, i).decode() for i in range(self.lib.mp_hip_num_ops(self.h))]
+
+    def op_bytes(self, op: int) -> float:
+        return float(self.lib.mp_hip_op_bytes(self.h, op))
+
+    def time_op(self, op: int, reps: int = 50) -> float:
+        us = ctypes.c_float()
+        self._check(self.lib.mp_hip_time_op(self.h, op, reps, ctypes.byref(us)))
+        return us.value
+
+
+class Codec:
+    """Nano-codec on the GPU (magpie_codec_init / magpie_codec_decode, nano-codec.cpp:339-845)."""
+
+    def __init__(self, path: str, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.mp_hip_codec_init(device, path.encode(), ctypes.byref(h))
+        if rc != MP_OK or not h.value:
+            raise MagpieError(f"mp_hip_codec_init failed ({_ERRS.get(rc, rc)})")
+        self.h = h
+
+    def decode(self, codes_cb_major: np.ndarray) -> np.ndarray:
+        codes = np.ascontiguousarray(codes_cb_major, np.int32)
+        assert codes.ndim == 2 and codes.shape[0] == 8
+        F = codes.shape[1]
+        out = np.zeros(F * 1024, np.float32)
+        rc = self.lib.mp_hip_codec_decode(self.h, codes.ctypes.data, F, out.ctypes.data)
+        if rc != MP_OK:
+            raise MagpieError(f"{_ERRS.get(rc, rc)}: {self.lib.mp_hip_codec_error(self.h).decode(errors='replace')}")
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.mp_hip_codec_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

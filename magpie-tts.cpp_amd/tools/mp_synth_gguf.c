@@ -10,7 +10,7 @@
 // bytes from the seed instead of shipping ~1 GB of weights.
 //
 // usage: mp_synth_gguf magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|f16]
-//                      [--dec-layers N] [--enc-layers N] [--dec-pos P]
+//                      [--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V]
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -21,6 +21,7 @@ enum { T_F32 = 0, T_F16 = 1, T_Q8_0 = 8 };
 enum { KV_U32 = 4, KV_F32 = 6, KV_STR = 8 };
 
 static uint64_t g_seed = 0x4D414750ull;  // "MAGP"
+static float g_eos_bias = 0.f;            // test-only: added to out_proj[3].bias[2017]
 
 static uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -125,12 +126,17 @@ static void fill_f32(const tdesc *t, float *dst) {
     const int64_t n = nel(t);
     const uint64_t key = fnv1a64(t->name) ^ splitmix64(g_seed);
     switch (t->init) {
-    case I_NORMAL: for (int64_t i = 0; i < n; ++i) dst[i] = (float)(t->p0 * gauss(key, (uint64_t)i)); break;
+    case I_NORMAL:
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < n; ++i) dst[i] = (float)(t->p0 * gauss(key, (uint64_t)i)); break;
     case I_LNW:    for (int64_t i = 0; i < n; ++i) dst[i] = (float)(1.0 + t->p0 * gauss(key, (uint64_t)i)); break;
     case I_ALPHA:  for (int64_t i = 0; i < n; ++i) dst[i] = (float)(t->p0 + (t->p1 - t->p0) * unif(key, (uint64_t)i)); break;
     case I_FIXED_BASE: { const float v[4] = {1, 8, 56, 336}; for (int64_t i = 0; i < n; ++i) dst[i] = v[i & 3]; } break;
     case I_FIXED_LEVELS: { const float v[4] = {8, 7, 6, 6}; for (int64_t i = 0; i < n; ++i) dst[i] = v[i & 3]; } break;
     }
+    // EOS-forcing variant for the stop-logic tests: codebook 3 prefers audio EOS
+    // once it is no longer forbidden (step >= 4, magpie.cpp:4325)
+    if (g_eos_bias != 0.f && !strcmp(t->name, "local_transformer_out_projections.3.bias")) dst[2017] += g_eos_bias;
 }
 
 // Q8_0 exactly as scripts/convert_magpie_to_gguf.py:79-104 (numpy): fp16 scale =
@@ -306,6 +312,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--dec-layers")) dec_layers = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--enc-layers")) enc_layers = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--dec-pos")) dec_pos = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--eos-bias")) g_eos_bias = (float)atof(argv[i + 1]);
         else { fprintf(stderr, "unknown option %s\n", argv[i]); return 2; }
     }
     if (!strcmp(kind, "magpie")) plan_magpie(dtype, dec_layers, enc_layers, dec_pos);

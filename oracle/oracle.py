@@ -1,0 +1,123 @@
+"""ctypes binding of the CPU oracle (liboracle.so).
+
+*** TEST INFRASTRUCTURE. *** Importable only from tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg — as the checker or the timed CPU baseline, never
+as the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import time
+
+import numpy as np
+
+ORACLE_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-C", ORACLE_DIR], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P, I = ctypes.c_void_p, ctypes.c_int
+        L.orc_set_mode.argtypes = [I, I, I]
+        L.orc_load.restype = P
+        L.orc_load.argtypes = [ctypes.c_char_p]
+        L.orc_free.argtypes = [P]
+        L.orc_dec_layers.argtypes = [P]
+        L.orc_synthesize.argtypes = [P, P, I, I, I, I, P, P, P, P]
+        L.orc_encode.argtypes = [P, P, I, P]
+        L.orc_codec_load.restype = P
+        L.orc_codec_load.argtypes = [ctypes.c_char_p]
+        L.orc_codec_free.argtypes = [P]
+        L.orc_codec_decode.argtypes = [P, P, I, P, I]
+        L.orc_fsq.argtypes = [P, I, P]
+        _lib = L
+    return _lib
+
+
+def set_mode(acc64: bool = True, gelu_f16: bool = False, threads: int = 0) -> None:
+    lib().orc_set_mode(int(acc64), int(gelu_f16), int(threads))
+
+
+class Model:
+    def __init__(self, path: str):
+        self.h = lib().orc_load(path.encode())
+        if not self.h:
+            raise RuntimeError(f"oracle: cannot load {path}")
+
+    def close(self):
+        if self.h:
+            lib().orc_free(self.h)
+            self.h = None
+
+    def synthesize(self, tokens, speaker=0, max_steps=32, ignore_eos=False, trace=True):
+        tok = np.ascontiguousarray(tokens, np.int32)
+        codes = np.zeros((max_steps, 8), np.int32)
+        marg = np.zeros((max_steps, 8), np.float32)
+        hid = np.zeros((max_steps + 1, 768), np.float32) if trace else None
+        tim = np.zeros(2, np.float64)
+        n = lib().orc_synthesize(self.h, tok.ctypes.data, len(tok), speaker, max_steps, int(ignore_eos),
+                                 codes.ctypes.data, marg.ctypes.data,
+                                 hid.ctypes.data if trace else None, tim.ctypes.data)
+        if n < 0:
+            raise RuntimeError(f"oracle synthesize failed ({n})")
+        return {"n_frames": n, "codes": codes[:n], "margins": marg[:max(n + 1, 0)],
+                "hidden": hid, "preamble_ms": tim[0], "decode_ms": tim[1]}
+
+    def encode(self, tokens):
+        tok = np.ascontiguousarray(tokens, np.int32)
+        out = np.zeros((len(tok), 768), np.float32)
+        if lib().orc_encode(self.h, tok.ctypes.data, len(tok), out.ctypes.data) != 0:
+            raise RuntimeError("oracle encode failed")
+        return out
+
+
+class Codec:
+    def __init__(self, path: str):
+        self.h = lib().orc_codec_load(path.encode())
+        if not self.h:
+            raise RuntimeError(f"oracle: cannot load codec {path}")
+
+    def decode(self, codes_cb_major, f16_operands=True):
+        c = np.ascontiguousarray(codes_cb_major, np.int32)
+        F = c.shape[1]
+        out = np.zeros(F * 1024, np.float32)
+        if lib().orc_codec_decode(self.h, c.ctypes.data, F, out.ctypes.data, int(f16_operands)) < 0:
+            raise RuntimeError("oracle codec decode failed")
+        return out
+
+    def close(self):
+        if self.h:
+            lib().orc_codec_free(self.h)
+            self.h = None
+
+
+def fsq(codes_cb_major):
+    c = np.ascontiguousarray(codes_cb_major, np.int32)
+    F = c.shape[1]
+    out = np.zeros((32, F), np.float32)
+    lib().orc_fsq(c.ctypes.data, F, out.ctypes.data)
+    return out
+
+
+def time_decode_fps(model_path: str, tokens, n_frames: int, threads: int, acc64: bool = False):
+    """CPU baseline: frames/s of the oracle's decode loop (BOS + AR steps), f32 accumulation."""
+    set_mode(acc64=acc64, gelu_f16=False, threads=threads)
+    m = Model(model_path)
+    t0 = time.time()
+    r = m.synthesize(tokens, max_steps=n_frames, ignore_eos=True, trace=False)
+    wall = time.time() - t0
+    m.close()
+    set_mode(acc64=True, gelu_f16=False, threads=threads)
+    return {"frames": r["n_frames"], "decode_s": r["decode_ms"] / 1e3, "preamble_s": r["preamble_ms"] / 1e3,
+            "wall_s": wall}

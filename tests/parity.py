@@ -1,0 +1,26 @@
+"""Helpers for GPU-vs-oracle code parity at temperature 0.
+
+Codes must be bit-identical. The one admissible deviation is a genuine near-tie:
+if the first differing codebook decision is one where the oracle's top-1/top-2
+logit gap is below TIE_EPS, the f32 GPU and the f64-accumulating oracle may
+legitimately pick different argmaxes; the comparison then stops there (the
+trajectories diverge afterwards by construction) and reports it.
+"""
+import numpy as np
+
+TIE_EPS = 2e-4  # logit units; GPU f32 vs oracle f64 logit error is ~1e-6
+
+
+def compare_codes(gpu_codes, orc_codes, orc_margins):
+    g = np.asarray(gpu_codes)
+    o = np.asarray(orc_codes)
+    n = min(len(g), len(o))
+    diff = np.argwhere(g[:n] != o[:n])
+    if len(diff) == 0:
+        assert len(g) == len(o), f"frame counts differ: gpu {len(g)} vs oracle {len(o)}"
+        return {"identical": True, "frames": n}
+    f, cb = diff[0]
+    margin = float(orc_margins[f, cb])
+    assert margin < TIE_EPS, (f"codes differ at frame {f} cb {cb}: gpu {g[f].tolist()} oracle {o[f].tolist()} "
+                              f"with oracle margin {margin:.3g} >= {TIE_EPS}")
+    return {"identical": False, "frames": int(f), "tie_margin": margin}

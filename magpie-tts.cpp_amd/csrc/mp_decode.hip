@@ -29,19 +29,15 @@ __device__ __forceinline__ void pro_ln_vec(const float *x, const float *lnw, flo
     // ggml_norm + ggml_mul (magpie.cpp:2255-2258): (x - mean) / sqrt(var + eps) * w
     constexpr int PER = K / MP_BLOCK;
     float v[PER];
-    float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) { v[i] = x[threadIdx.x + MP_BLOCK * i]; s += v[i]; }
-    const float mean = block_sum(s, red) * (1.0f / K);
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) { v[i] -= mean; q += v[i] * v[i]; }
-    const float var = block_sum(q, red) * (1.0f / K);
+    for (int i = 0; i < PER; ++i) v[i] = x[threadIdx.x + MP_BLOCK * i];
+    float mean, var;
+    block_meanvar<PER>(v, red, mean, var);
     const float rstd = 1.0f / sqrtf(var + eps);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int k = threadIdx.x + MP_BLOCK * i;
-        const float y = (v[i] * rstd) * lnw[k];
+        const float y = ((v[i] - mean) * rstd) * lnw[k];
         act[k] = y;
         if (store) store[k] = y;
     }
@@ -54,21 +50,21 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         for (int b = 0; b < NB; ++b)
             for (int k = tid * 4; k < K; k += MP_BLOCK * 4)
                 *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
-        __syncthreads();
+        lds_sync();
     } else if constexpr (PRO == PRO_LN) {
         for (int b = 0; b < NB; ++b) {
             float *store = nullptr;
             if (p.hidden_out && blockIdx.x == 0) store = p.hidden_out + (size_t)b * K;
             pro_ln_vec<NB, K>(p.src + (size_t)b * p.src_ld, p.lnw, p.eps, act + b * K, red, store);
             if (p.trace && blockIdx.x == 0) {
-                __syncthreads();
+                lds_sync();
                 const int s = p.step[b];
                 if (s < p.trace_steps)
                     for (int k = tid; k < K; k += MP_BLOCK)
                         p.trace[((size_t)b * p.trace_steps + s) * K + k] = act[b * K + k];
             }
         }
-        __syncthreads();
+        lds_sync();
     } else if constexpr (PRO == PRO_EMBED_LN) {
         static_assert(K == D, "embed prologue is d_model wide");
         for (int b = 0; b < NB; ++b) {
@@ -84,41 +80,57 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
                 if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
             }
-            // LN over the freshly built x (registers -> LN helper reads memory; inline here)
-            float s = 0.f;
-#pragma unroll
-            for (int i = 0; i < K / MP_BLOCK; ++i) s += x[i];
-            const float mean = block_sum(s, red) * (1.0f / K);
-            float q = 0.f;
-#pragma unroll
-            for (int i = 0; i < K / MP_BLOCK; ++i) { x[i] -= mean; q += x[i] * x[i]; }
-            const float rstd = 1.0f / sqrtf(block_sum(q, red) * (1.0f / K) + p.eps);
+            // LN over the freshly built x
+            float mean, var;
+            block_meanvar<K / MP_BLOCK>(x, red, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
             for (int i = 0; i < K / MP_BLOCK; ++i) {
                 const int k = tid + MP_BLOCK * i;
-                act[b * K + k] = (x[i] * rstd) * p.lnw[k];
+                act[b * K + k] = ((x[i] - mean) * rstd) * p.lnw[k];
             }
         }
-        __syncthreads();
+        lds_sync();
     } else if constexpr (PRO == PRO_SA_COMBINE) {
         static_assert(K == D, "SA output is d_model wide");
-        for (int b = 0; b < NB; ++b)
-            for (int k = tid; k < K; k += MP_BLOCK) {
-                const int h = k / DH, d = k % DH;
-                const float *P = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
-                float M = -INFINITY;
-                for (int c = 0; c < p.nch; ++c) M = fmaxf(M, P[c * PART_STRIDE]);
-                float num = 0.f, den = 0.f;
-                for (int c = 0; c < p.nch; ++c) {
-                    const float mc = P[c * PART_STRIDE];
-                    if (mc == -INFINITY) continue;
-                    const float e = expf(mc - M);
-                    den += e * P[c * PART_STRIDE + 1];
-                    num += e * P[c * PART_STRIDE + 16 + d];
-                }
-                act[b * K + k] = num / den;
+        // (1) stage every chunk's (max, sum) in LDS with one independent load per thread
+        const int nml = NB * NH * p.nch;
+        for (int i = tid; i < nml; i += MP_BLOCK) {
+            sc[2 * i] = p.part[(size_t)i * PART_STRIDE];
+            sc[2 * i + 1] = p.part[(size_t)i * PART_STRIDE + 1];
+        }
+        lds_sync();
+        // (2) per (slot, head): chunk weights w_c = exp(m_c - M) / sum_c exp(m_c - M) l_c
+        for (int bh = tid; bh < NB * NH; bh += MP_BLOCK) {
+            float M = -INFINITY;
+            for (int c = 0; c < p.nch; ++c) M = fmaxf(M, sc[2 * (bh * p.nch + c)]);
+            float den = 0.f;
+            for (int c = 0; c < p.nch; ++c) {
+                const float mc = sc[2 * (bh * p.nch + c)];
+                den += mc == -INFINITY ? 0.f : expf(mc - M) * sc[2 * (bh * p.nch + c) + 1];
             }
-        __syncthreads();
+            const float inv = 1.0f / den;
+            for (int c = 0; c < p.nch; ++c) {
+                const float mc = sc[2 * (bh * p.nch + c)];
+                sc[2 * (bh * p.nch + c)] = mc == -INFINITY ? 0.f : expf(mc - M) * inv;
+            }
+        }
+        lds_sync();
+        // (3) act = sum_c w_c o_c : all chunk loads of a thread issued together
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int i = 0; i < K / MP_BLOCK; ++i) {
+                const int k = tid + MP_BLOCK * i, h = k / DH, d = k % DH, bh = b * NH + h;
+                const float *P = p.part + (size_t)bh * p.nch * PART_STRIDE + 16 + d;
+                float o[NCH_MAX];
+#pragma unroll
+                for (int c = 0; c < NCH_MAX; ++c) o[c] = c < p.nch ? P[c * PART_STRIDE] : 0.f;
+                float a = 0.f;
+#pragma unroll
+                for (int c = 0; c < NCH_MAX; ++c) if (c < p.nch) a += sc[2 * (bh * p.nch + c)] * o[c];
+                act[b * K + k] = a;
+            }
+        lds_sync();
     } else if constexpr (PRO == PRO_XA) {
         static_assert(K == DXA, "XA output is 128 wide");
         const int lane = tid & 63, w = tid >> 6, half = lane >> 5, d4 = lane & 31;
@@ -128,14 +140,23 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
             const float *Vb = p.xav + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
             const float4 q4 = *(const float4 *)(p.qx + (size_t)b * DXA + 4 * d4);
-            for (int j0 = w * 2; j0 < Tb; j0 += 8) {
-                const int j = j0 + half;
-                float v = 0.f;
-                if (j < Tb) v = dotv(q4, *(const float4 *)(Kb + (size_t)j * DXA + 4 * d4));
-                v = group_sum<32>(v);
-                if (d4 == 0 && j < Tb) sc[j] = v * scale;
+            // half-wave hw (0..7) scores keys hw, hw+8, ...; 4 key rows in flight per lane
+            const int hw = w * 2 + half;
+            for (int jb = hw; jb < Tb; jb += 32) {
+                float4 kv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = jb + 8 * u;
+                    kv[u] = j < Tb ? *(const float4 *)(Kb + (size_t)j * DXA + 4 * d4) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = jb + 8 * u;
+                    const float v = group_sum<32>(dotv(q4, kv[u]));
+                    if (d4 == 0 && j < Tb) sc[j] = v * scale;
+                }
             }
-            __syncthreads();
+            lds_sync();
             float m = -INFINITY;
             for (int j = tid; j < Tb; j += MP_BLOCK) m = fmaxf(m, sc[j]);
             m = block_max(m, red);
@@ -144,11 +165,12 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             l = block_sum(l, red);  // (its barriers also publish sc[])
             const int dd = tid & (DXA - 1), par = tid >> 7;
             float a = 0.f;
+#pragma unroll 8
             for (int j = par; j < Tb; j += 2) a += sc[j] * Vb[(size_t)j * DXA + dd];
             red[8 + tid] = a;
-            __syncthreads();
+            lds_sync();
             if (tid < DXA) act[b * K + tid] = (red[8 + tid] + red[8 + DXA + tid]) / l;
-            __syncthreads();
+            lds_sync();
         }
     } else if constexpr (PRO == PRO_LTX_LN) {
         static_assert(K == LTD, "LT is 256 wide");
@@ -156,12 +178,13 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             const int k = tid;
             const float X = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
             if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X;
-            const float mean = block_sum(X, red) * (1.0f / K);
-            const float dv = X - mean;
-            const float rstd = 1.0f / sqrtf(block_sum(dv * dv, red) * (1.0f / K) + p.eps);
-            act[b * K + k] = (dv * rstd) * p.lnw[k];
+            const float xv[1] = {X};
+            float mean, var;
+            block_meanvar<1>(xv, red, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
         }
-        __syncthreads();
+        lds_sync();
     } else if constexpr (PRO == PRO_LT_ATTN) {
         static_assert(K == LTD, "LT is 256 wide");
         const int lane = tid & 63, w = tid >> 6;
@@ -173,7 +196,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 v = wave_sum(v);
                 if (lane == 0) sc[j] = v * (1.0f / 16.0f);  // 1/sqrt(256)
             }
-            __syncthreads();
+            lds_sync();
             float m = -INFINITY;
             for (int j = 0; j < nk; ++j) m = fmaxf(m, sc[j]);
             float l = 0.f, a = 0.f;
@@ -183,7 +206,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 a += e * p.ltv[((size_t)b * NCB + j) * LTD + tid];
             }
             act[b * K + tid] = a / l;
-            __syncthreads();
+            lds_sync();
         }
     } else if constexpr (PRO == PRO_ARGMAX_EMB) {
         static_assert(K == D, "embedding is d_model wide");
@@ -192,24 +215,32 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             const bool forbid_eos = p.ignore_eos || p.step[b] < 4;  // min_generated_frames
             float bv = -INFINITY;
             int bi = 0x7fffffff;
-            for (int i = tid; i < VCB; i += MP_BLOCK) {
-                float v = lg[i];
-                if (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos)) v = -INFINITY;
+            float lv[(VCB + MP_BLOCK - 1) / MP_BLOCK];
+#pragma unroll
+            for (int r = 0; r < (VCB + MP_BLOCK - 1) / MP_BLOCK; ++r) {
+                const int i = tid + MP_BLOCK * r;
+                lv[r] = i < VCB ? lg[i] : -INFINITY;
+            }
+#pragma unroll
+            for (int r = 0; r < (VCB + MP_BLOCK - 1) / MP_BLOCK; ++r) {
+                const int i = tid + MP_BLOCK * r;
+                float v = lv[r];
+                if (i >= VCB || (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos))) v = -INFINITY;
                 argmax_merge(bv, bi, v, i);
             }
             wave_argmax(bv, bi);
             if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
-            __syncthreads();
+            lds_sync();
             float v0 = red[0];
             int i0 = ((int *)red)[4];
             for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
             if (i0 < 0 || i0 >= VCB) i0 = 0;  // all -inf / NaN logits: reference argmax stays 0
-            __syncthreads();
+            lds_sync();
             if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb] = i0;
             const float *e = p.emb + ((size_t)p.cb * VCB + i0) * D;
             for (int k = tid; k < K; k += MP_BLOCK) act[b * K + k] = e[k];
         }
-        __syncthreads();
+        lds_sync();
     }
 }
 
@@ -219,16 +250,22 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
 // wave-instruction; activations come from LDS with conflict-free ds_read_b128.
 template <int NB, int RW, int K, int PRO, int EPI>
 __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
-    if (p.ndone && *p.ndone >= p.nslots) return;
+    // No early exit on the done counter: a dependent load there would sit in
+    // front of the weight stream of every launch. Once every slot is done the
+    // iteration recomputes identical values (codes_prev / pos are frozen) and
+    // lt_finalize_kernel refuses to touch the outputs.
     constexpr int VW = K >= 256 ? 4 : K / 64;
     constexpr int NV = K / (64 * VW);
     using VT = typename vecf<VW>::T;
-    constexpr int SC = (PRO == PRO_XA) ? TMAX_LIMIT : (PRO == PRO_LT_ATTN ? 16 : 1);
+    constexpr int SC = (PRO == PRO_XA) ? TMAX_LIMIT
+                       : (PRO == PRO_LT_ATTN) ? 16
+                       : (PRO == PRO_SA_COMBINE) ? 2 * NB * NH * NCH_MAX : 1;
     __shared__ __attribute__((aligned(16))) float act[NB * K];
     __shared__ float red[8 + 2 * DXA];
     __shared__ float sc[SC];
-    prologue<NB, K, PRO>(p, act, red, sc);
 
+    // The weight rows do not depend on the prologue: issue the whole stream first
+    // so the HBM latency overlaps the prologue's own dependent loads/reductions.
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int row0 = (blockIdx.x * MP_NWAVES + w) * RW;
     VT wv[RW][NV];
@@ -239,6 +276,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) wv[r][i] = wr[lane + 64 * i];
     }
+    prologue<NB, K, PRO>(p, act, red, sc);
     float acc[RW][NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -286,45 +324,51 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 // 16 lanes x float4 cover one 64-dim key row (256 B, coalesced); a wave does 4
 // keys per instruction. Keys j > pos are masked (L = pos + 1, magpie.cpp:3412).
 __global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
-    if (p.ndone && *p.ndone >= p.nslots) return;
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int L = p.pos[b] + 1;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    float *P = p.part + ((size_t)(b * NH + h) * p.nch + c) * PART_STRIDE;
+    __shared__ float sc[SA_CHUNK];
+    __shared__ float ow[MP_NWAVES][DH];
     const int j0 = c * SA_CHUNK;
+    const int kk = lane >> 4, dc = lane & 15;
+    // Issue q, all 4 K rows and all 4 V rows of this lane first: rows j < max_seq
+    // are always valid memory, so no load waits for the live length L = pos + 1.
+    const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
+    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
+    float4 k4[4], v4[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int j = j0 + w * 16 + it * 4 + kk;
+        k4[it] = *(const float4 *)(p.kc + base + (size_t)j * D);
+        v4[it] = *(const float4 *)(p.vc + base + (size_t)j * D);
+    }
+    const int L = p.pos[b] + 1;
+    float *P = p.part + ((size_t)(b * NH + h) * p.nch + c) * PART_STRIDE;
     if (j0 >= L) {
         if (tid < PART_STRIDE) P[tid] = tid == 0 ? -INFINITY : 0.f;
         return;
     }
-    __shared__ float sc[SA_CHUNK];
-    __shared__ float ow[MP_NWAVES][DH];
-    const int kk = lane >> 4, dc = lane & 15;
-    const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
-    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
     float s[4];
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
         const int j = j0 + w * 16 + it * 4 + kk;
-        float v = 0.f;
-        if (j < L) v = dotv(q4, *(const float4 *)(p.kc + base + (size_t)j * D));
-        v = group_sum<16>(v);
+        const float v = group_sum<16>(dotv(q4, k4[it]));
         s[it] = j < L ? v * 0.125f : -INFINITY;  // 1/sqrt(64)
     }
     if (dc == 0)
 #pragma unroll
         for (int it = 0; it < 4; ++it) sc[w * 16 + it * 4 + kk] = s[it];
-    __syncthreads();
-    float m = -INFINITY;
-#pragma unroll 8
-    for (int i = 0; i < SA_CHUNK; ++i) m = fmaxf(m, sc[i]);
+    lds_sync();
+    // every wave reduces the chunk's 64 scores itself: lane i holds key i
+    const float si = sc[lane];
+    const float m = wave_max(si);
+    const float l = wave_sum(si == -INFINITY ? 0.f : expf(si - m));
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
         const int j = j0 + w * 16 + it * 4 + kk;
         if (j < L) {
             const float e = expf(s[it] - m);
-            const float4 v4 = *(const float4 *)(p.vc + base + (size_t)j * D);
-            o.x += e * v4.x; o.y += e * v4.y; o.z += e * v4.z; o.w += e * v4.w;
+            o.x += e * v4[it].x; o.y += e * v4[it].y; o.z += e * v4[it].z; o.w += e * v4[it].w;
         }
     }
 #pragma unroll
@@ -333,11 +377,9 @@ __global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
         o.z += __shfl_xor(o.z, msk, 64); o.w += __shfl_xor(o.w, msk, 64);
     }
     if (lane < 16) *(float4 *)(&ow[w][4 * lane]) = o;
-    __syncthreads();
+    lds_sync();
     if (tid < DH) P[16 + tid] = (ow[0][tid] + ow[1][tid]) + (ow[2][tid] + ow[3][tid]);
     if (tid == 64) {
-        float l = 0.f;
-        for (int i = 0; i < SA_CHUNK; ++i) if (sc[i] != -INFINITY) l += expf(sc[i] - m);
         P[0] = m;
         P[1] = l;
     }
@@ -363,7 +405,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
     }
     wave_argmax(bv, bi);
     if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
-    __syncthreads();
+    lds_sync();
     if (tid != 0) return;
     float v0 = red[0];
     int i0 = ((int *)red)[4];

@@ -8,23 +8,61 @@
 #define MP_BLOCK 256
 #define MP_NWAVES (MP_BLOCK / MP_WAVE)
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---- wave64 reductions on DPP (data-parallel primitives move lanes inside the
+// VALU; no LDS round trip per step, unlike __shfl_xor's ds_bpermute).
+// ctrl: quad_perm(1,0,3,2)=0xB1, quad_perm(2,3,0,1)=0x4E, row_half_mirror=0x141,
+// row_mirror=0x140, row_bcast15=0x142, row_bcast31=0x143.
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF, false));
+}
+__device__ __forceinline__ float bcast_lane63(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+// every lane gets the sum of its 16-lane row
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
     return v;
+}
+__device__ __forceinline__ float row_max16(float v) {
+    v = fmaxf(v, dpp_mov<0xB1>(v));
+    v = fmaxf(v, dpp_mov<0x4E>(v));
+    v = fmaxf(v, dpp_mov<0x141>(v));
+    v = fmaxf(v, dpp_mov<0x140>(v));
+    return v;
+}
+// full-wave sum / max, returned uniformly (SGPR broadcast of lane 63)
+__device__ __forceinline__ float wave_sum(float v) {
+    v = row_sum16(v);
+    v += dpp_mov<0x142, 0xA>(v);
+    v += dpp_mov<0x143, 0xC>(v);
+    return bcast_lane63(v);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = row_max16(v);
+    v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                                    __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false)));
+    v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                                    __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false)));
+    return bcast_lane63(v);
 }
-// sum over lanes that differ only in the low log2(W) bits (W = 2..64)
+// sum over lanes that differ only in the low log2(W) bits (W = 16 or 32)
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    static_assert(W == 16 || W == 32, "group_sum: 16 or 32 lanes");
+    v = row_sum16(v);
+    if constexpr (W == 32) v += __shfl_xor(v, 16, 64);
     return v;
 }
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt) but NOT for outstanding global loads, so a weight stream issued
+// before a prologue stays in flight across it (__syncthreads() would drain it).
+// The "memory" clobber keeps the compiler from moving memory ops across.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Block-wide reduction for 256 threads; `red` is an LDS scratch of >= 4 floats.
 // Every thread returns the total. Contains two barriers.
@@ -32,19 +70,60 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
     v = wave_sum(v);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
+    lds_sync();
     const float r = (red[0] + red[1]) + (red[2] + red[3]);
-    __syncthreads();
+    lds_sync();
     return r;
 }
 __device__ __forceinline__ float block_max(float v, float *red) {
     v = wave_max(v);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
+    lds_sync();
     const float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    __syncthreads();
+    lds_sync();
     return r;
+}
+
+// LayerNorm statistics of K elements held PER per thread (256 threads):
+// one pass, numerically stable pairwise combination of (mean, M2) — groups
+// combined at every step have equal element counts. Returns biased variance.
+template <int PER>
+__device__ __forceinline__ void block_meanvar(const float (&v)[PER], float *red, float &mean, float &var) {
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) m += v[i];
+    m *= 1.0f / PER;
+    float M2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) { const float d = v[i] - m; M2 += d * d; }
+    float n = (float)PER;  // elements per side at the current step
+    auto comb = [&](float mb, float M2b) {
+        const float d = mb - m;
+        m = m + 0.5f * d;
+        M2 = M2 + M2b + d * d * (0.5f * n);
+        n *= 2.f;
+    };
+    comb(dpp_mov<0xB1>(m), dpp_mov<0xB1>(M2));
+    comb(dpp_mov<0x4E>(m), dpp_mov<0x4E>(M2));
+    comb(dpp_mov<0x141>(m), dpp_mov<0x141>(M2));
+    comb(dpp_mov<0x140>(m), dpp_mov<0x140>(M2));
+    comb(dpp_mov<0x142, 0xA>(m), dpp_mov<0x142, 0xA>(M2));  // valid in rows 1,3
+    comb(dpp_mov<0x143, 0xC>(m), dpp_mov<0x143, 0xC>(M2));  // valid in row 3 (lane 63 = whole wave)
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) { red[2 * w] = m; red[2 * w + 1] = M2; }
+    lds_sync();
+    float m0 = red[0], q0 = red[1], m1 = red[2], q1 = red[3], m2 = red[4], q2 = red[5], m3 = red[6], q3 = red[7];
+    lds_sync();
+    const float nw = 64.f * PER;
+    float d = m1 - m0;
+    const float ma = m0 + 0.5f * d, Qa = q0 + q1 + d * d * (0.5f * nw);
+    d = m3 - m2;
+    const float mb = m2 + 0.5f * d, Qb = q2 + q3 + d * d * (0.5f * nw);
+    d = mb - ma;
+    mean = ma + 0.5f * d;
+    const float Q = Qa + Qb + d * d * nw;
+    var = Q * (1.0f / (4.f * nw));
 }
 
 // (value, index) argmax with the reference's tie rule: the FIRST maximal index

@@ -18,6 +18,7 @@ constexpr int NCB = 8;        // codebooks                    (magpie.h:61)
 constexpr int VCB = 2024;     // vocab per codebook           (magpie.h:63)
 constexpr int CTX = 110;      // baked context frames         (magpie.h:67)
 constexpr int SA_CHUNK = 64;  // keys per split-K attention workgroup
+constexpr int NCH_MAX = 16;   // split-K chunks -> max_seq <= 1024 (reference: 626, magpie.cpp:4077)
 constexpr int PART_STRIDE = 80;  // [m, l, pad.., o[64] at +16]
 constexpr int TMAX_LIMIT = 1024;  // text tokens per utterance (LDS score buffer)
 

@@ -100,16 +100,14 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const float *X, int ldx, c
     __shared__ float red[8];
     const int m = blockIdx.x, tid = threadIdx.x;
     const float *x = X + (size_t)m * ldx;
-    float v[3], s = 0.f;
+    float v[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { v[i] = x[tid + 256 * i]; s += v[i]; }
-    const float mean = block_sum(s, red) * (1.0f / D);
-    float q = 0.f;
+    for (int i = 0; i < 3; ++i) v[i] = x[tid + 256 * i];
+    float mean, var;
+    block_meanvar<3>(v, red, mean, var);
+    const float rstd = 1.0f / sqrtf(var + eps);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { v[i] -= mean; q += v[i] * v[i]; }
-    const float rstd = 1.0f / sqrtf(block_sum(q, red) * (1.0f / D) + eps);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) Y[(size_t)m * ldy + tid + 256 * i] = (v[i] * rstd) * w[tid + 256 * i];
+    for (int i = 0; i < 3; ++i) Y[(size_t)m * ldy + tid + 256 * i] = ((v[i] - mean) * rstd) * w[tid + 256 * i];
 }
 
 // Causal multi-head attention for every (row, head): one wave per pair.

@@ -13,6 +13,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -305,6 +306,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     dev->max_steps = max_steps;
     dev->max_seq = mp::CTX + max_steps + 16;  // magpie.cpp:4077
     dev->nch = (dev->max_seq + mp::SA_CHUNK - 1) / mp::SA_CHUNK;
+    dev->max_seq = dev->nch * mp::SA_CHUNK;  // whole chunks: attention loads never leave the cache slab
     const size_t D = 768;
     int rc = MP_OK;
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
@@ -609,6 +611,8 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     }
     if (Tmax > mp::TMAX_LIMIT || Tmax > 4096) return fail(dev, MP_ERR_ARG, "too many text tokens");
     const int max_steps = params->max_dec_steps > 0 ? params->max_dec_steps : dev->m.max_dec_steps;
+    if (mp::CTX + max_steps + 16 > mp::NCH_MAX * mp::SA_CHUNK)
+        return fail(dev, MP_ERR_ARG, "max_dec_steps too large (cache limited to 1024 positions)");
     if (mp::CTX + max_steps > dev->m.dec_pos_rows)
         return fail(dev, MP_ERR_ARG, "max_dec_steps exceeds the decoder position table");
     HIPCHK(hipSetDevice(dev->device));
@@ -655,7 +659,25 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     HIPCHK(hipMemcpyAsync(dev->ndone, h_nd, 16, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
-    if (!dev->exec) {
+    // MAGPIE_EAGER=1: launch the iteration's kernels directly instead of replaying
+    // the captured graph (identical kernels and arguments; used under rocprofv3,
+    // whose kernel tracer crashes on graph replays on this image).
+    const char *eager_env = getenv("MAGPIE_EAGER");
+    const bool eager = eager_env && atoi(eager_env) != 0;
+    if (eager) {
+        if (dev->ops.empty()) {
+            if (int rc = enqueue_iteration(dev, dev->stream, true)) return rc;  // also records op list
+            HIPCHK(hipStreamSynchronize(dev->stream));
+            // that was a real first iteration: restore the initial state
+            HIPCHK(hipMemcpyAsync(dev->pos, h_pos.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+            HIPCHK(hipMemcpyAsync(dev->step, h_zero.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+            HIPCHK(hipMemcpyAsync(dev->nframes, h_zero.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+            HIPCHK(hipMemcpyAsync(dev->done, h_done.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+            HIPCHK(hipMemcpyAsync(dev->ndone, h_nd, 16, hipMemcpyHostToDevice, dev->stream));
+            HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
+            HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
+        }
+    } else if (!dev->exec) {
         // capture one iteration; the op list is recorded for measurement
         HIPCHK(hipStreamBeginCapture(dev->stream, hipStreamCaptureModeThreadLocal));
         int rc = enqueue_iteration(dev, dev->stream, true);
@@ -674,7 +696,11 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     const int poll = 8;
     int it = 0;
     for (; it < dev->max_steps; ++it) {
-        HIPCHK(hipGraphLaunch(dev->exec, dev->stream));
+        if (eager) {
+            if (int rc = enqueue_iteration(dev, dev->stream, false)) return rc;
+        } else {
+            HIPCHK(hipGraphLaunch(dev->exec, dev->stream));
+        }
         if (!dev->params.ignore_eos && (it + 1) % poll == 0 && it + 1 < dev->max_steps) {
             HIPCHK(hipMemcpyAsync(dev->h_ndone, dev->ndone, 4, hipMemcpyDeviceToHost, dev->stream));
             HIPCHK(hipStreamSynchronize(dev->stream));

@@ -1,0 +1,55 @@
+"""World-size-2 gloo test of the replica coordination used by bench.py
+(utterance sharding, barrier, max/sum over ranks) — the N>1 path, on CPU."""
+import os
+import socket
+
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "magpie-tts.cpp_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from magpie_amd.dist import max_over_ranks, shard_utterances, sum_over_ranks
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = shard_utterances(64, rank, world)
+    t = max_over_ranks(1.0 + rank)
+    n = sum_over_ranks(float(len(mine)))
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, mine, t, n))
+
+
+def test_shard_utterances_partition():
+    from magpie_amd.dist import shard_utterances
+    for n, w in [(64, 8), (64, 3), (7, 4), (1, 1)]:
+        parts = [shard_utterances(n, r, w) for r in range(w)]
+        assert sorted(sum(parts, [])) == list(range(n))
+        assert all(p == sorted(p) for p in parts)
+    assert shard_utterances(64, 1, 8) == list(range(8, 16))  # 8 per GPU at B=64 (configs[3])
+
+
+def test_gloo_world_size_2():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == list(range(32)) and res[1][1] == list(range(32, 64))
+    assert res[0][2] == res[1][2] == 2.0
+    assert res[0][3] == res[1][3] == 64.0

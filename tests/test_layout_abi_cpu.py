@@ -1,0 +1,229 @@
+"""CPU-only checks of the boundary: GGUF layout of the synthetic weights, the
+C-ABI library's exports, error behaviour without a GPU, and the committed golden
+fixtures."""
+import json
+import os
+import re
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(REPO, "include", "magpie_hip.h")
+
+
+def read_gguf_index(path):
+    """Independent minimal GGUF v3 index reader (header + tensor infos)."""
+    with open(path, "rb") as f:
+        assert f.read(4) == b"GGUF"
+        ver, = struct.unpack("<I", f.read(4))
+        nt, nkv = struct.unpack("<QQ", f.read(16))
+
+        def rstr():
+            n, = struct.unpack("<Q", f.read(8))
+            return f.read(n).decode()
+        sizes = {0: 1, 1: 1, 2: 2, 3: 2, 4: 4, 5: 4, 6: 4, 7: 1, 10: 8, 11: 8, 12: 8}
+        kv = {}
+
+        def rval(t):
+            if t == 8:
+                return rstr()
+            if t == 9:
+                et, = struct.unpack("<I", f.read(4))
+                n, = struct.unpack("<Q", f.read(8))
+                return [rval(et) for _ in range(n)]
+            b = f.read(sizes[t])
+            return struct.unpack({4: "<I", 5: "<i", 6: "<f"}.get(t, "<Q" if sizes[t] == 8 else "<B"), b)[0]
+        for _ in range(nkv):
+            k = rstr()
+            t, = struct.unpack("<I", f.read(4))
+            kv[k] = rval(t)
+        tensors = {}
+        for _ in range(nt):
+            name = rstr()
+            nd, = struct.unpack("<I", f.read(4))
+            ne = struct.unpack("<" + "Q" * nd, f.read(8 * nd))
+            typ, off = struct.unpack("<IQ", f.read(12))
+            tensors[name] = (tuple(reversed(ne)), typ, off)
+    return ver, kv, tensors
+
+
+# Tensor names/shapes mapped by create_tensors (magpie.cpp:572-672), shapes per
+# docs/MAGPIE_ARCHITECTURE.md:265-307 (PyTorch order).
+def expected_magpie(dec_layers=12, enc_layers=6):
+    e = {"text_embedding.weight": (2380, 768), "encoder.position_embeddings.weight": (4096, 768),
+         "encoder.norm_out.weight": (768,), "decoder.norm_out.weight": (768,),
+         "baked_context_embedding.weight": (5, 84480), "final_proj.weight": (16192, 768), "final_proj.bias": (16192,),
+         "local_transformer_in_projection.weight": (256, 768), "local_transformer_in_projection.bias": (256,),
+         "local_transformer.position_embeddings.weight": (10, 256),
+         "local_transformer.layers.0.norm_self.weight": (256,),
+         "local_transformer.layers.0.self_attention.qkv_net.weight": (768, 256),
+         "local_transformer.layers.0.self_attention.o_net.weight": (256, 256),
+         "local_transformer.layers.0.norm_pos_ff.weight": (256,),
+         "local_transformer.layers.0.pos_ff.proj.conv.weight": (1024, 256, 1),
+         "local_transformer.layers.0.pos_ff.o_net.conv.weight": (256, 1024, 1)}
+    for l in range(enc_layers):
+        p = f"encoder.layers.{l}."
+        e.update({p + "norm_self.weight": (768,), p + "self_attention.qkv_net.weight": (2304, 768),
+                  p + "self_attention.o_net.weight": (768, 768), p + "norm_pos_ff.weight": (768,),
+                  p + "pos_ff.proj.conv.weight": (3072, 768, 3), p + "pos_ff.o_net.conv.weight": (768, 3072, 3)})
+    for l in range(dec_layers):
+        p = f"decoder.layers.{l}."
+        e.update({p + "norm_self.weight": (768,), p + "self_attention.qkv_net.weight": (2304, 768),
+                  p + "self_attention.o_net.weight": (768, 768), p + "norm_xattn_query.weight": (768,),
+                  p + "cross_attention.q_net.weight": (128, 768), p + "cross_attention.kv_net.weight": (256, 768),
+                  p + "cross_attention.o_net.weight": (768, 128), p + "norm_xattn_memory.weight": (768,),
+                  p + "norm_pos_ff.weight": (768,), p + "pos_ff.proj.conv.weight": (3072, 768, 1),
+                  p + "pos_ff.o_net.conv.weight": (768, 3072, 1)})
+    for c in range(8):
+        e[f"audio_embeddings.{c}.weight"] = (2024, 768)
+        e[f"local_transformer_out_projections.{c}.weight"] = (2024, 256)
+        e[f"local_transformer_out_projections.{c}.bias"] = (2024,)
+    return e
+
+
+def test_magpie_gguf_layout(small_model):
+    ver, kv, t = read_gguf_index(small_model)
+    assert ver == 3
+    exp = expected_magpie(dec_layers=2, enc_layers=1)
+    exp["decoder.position_embeddings.weight"] = t["decoder.position_embeddings.weight"][0]
+    assert t["decoder.position_embeddings.weight"][0][0] >= 610  # max position 110 + 499
+    assert {k: v[0] for k, v in t.items()} == exp
+    assert all(v[1] == 0 for v in t.values())  # F32 file
+    assert all(v[2] % 32 == 0 for v in t.values())  # 32-byte aligned data
+    assert kv["magpie.d_model"] == 768 and kv["magpie.audio_eos_id"] == 2017
+    assert kv["magpie.dec_layers"] == 2 and kv["magpie.enc_layers"] == 1
+
+
+def test_q8_gguf_quantizes_reference_patterns(q8_model):
+    """convert_magpie_to_gguf.py:155-176,311-320: attention/LT projections Q8_0;
+    pos_ff conv weights stay F32 (inner dim 1 or 3 < 32)."""
+    _, _, t = read_gguf_index(q8_model)
+    q8 = {k for k, v in t.items() if v[1] == 8}
+    assert "decoder.layers.0.self_attention.qkv_net.weight" in q8
+    assert "decoder.layers.1.cross_attention.kv_net.weight" in q8
+    assert "local_transformer_out_projections.7.weight" in q8
+    assert "local_transformer_in_projection.weight" in q8
+    assert "decoder.layers.0.pos_ff.proj.conv.weight" not in q8
+    assert "encoder.layers.0.pos_ff.o_net.conv.weight" not in q8
+    assert "audio_embeddings.0.weight" not in q8
+
+
+def test_q8_block_semantics_match_converter(tmp_path):
+    """Q8_0 = fp16 scale amax/127 + round-half-even int8 (convert_magpie_to_gguf.py:79-104),
+    re-derived with numpy from the F32 twin of the same tensor."""
+    import magpie_amd as ma
+    f32 = ma.synth_gguf(str(tmp_path / "a.gguf"), dec_layers=1, enc_layers=1)
+    q8 = ma.synth_gguf(str(tmp_path / "b.gguf"), dtype="q8_0", dec_layers=1, enc_layers=1)
+    name = "decoder.layers.0.cross_attention.q_net.weight"
+    _, _, t32 = read_gguf_index(f32)
+    _, _, t8 = read_gguf_index(q8)
+
+    def data_start(path):
+        """(file bytes, offset of the 32-aligned data section)"""
+        with open(path, "rb") as f:
+            buf = f.read()
+        p = 24
+        def rstr(p):
+            ln, = struct.unpack_from("<Q", buf, p)
+            return p + 8 + ln
+        nt, nkv = struct.unpack_from("<QQ", buf, 8)
+        for _ in range(nkv):
+            p = rstr(p)
+            t, = struct.unpack_from("<I", buf, p); p += 4
+            if t == 8:
+                p = rstr(p)
+            else:
+                p += {4: 4, 5: 4, 6: 4}[t]
+        for _ in range(nt):
+            p = rstr(p)
+            nd, = struct.unpack_from("<I", buf, p); p += 4 + 8 * nd + 12
+        return buf, (p + 31) // 32 * 32
+    b32, s32 = data_start(f32)
+    b8, s8 = data_start(q8)
+    x = np.frombuffer(b32, np.float32, n, s32 + off32).reshape(-1, 32)
+    blk = np.frombuffer(b8, np.dtype([("d", "<f2"), ("q", "i1", 32)]), n // 32, s8 + t8[name][2])
+    amax = np.abs(x).max(axis=1)
+    d = (amax / 127.0).astype(np.float16)
+    np.testing.assert_array_equal(blk["d"], d)
+    q = np.round(x / d.astype(np.float32)[:, None]).astype(np.int8)
+    np.testing.assert_array_equal(blk["q"], q)
+
+
+def test_codec_gguf_layout(codec_model):
+    """nano-codec.cpp:84-199 names (shortened by convert_codec_to_gguf.py:110-132)."""
+    _, kv, t = read_gguf_index(codec_model)
+    assert t["dec.pre.weight"][0] == (864, 32, 7)
+    assert t["dec.post.weight"][0] == (1, 27, 3)
+    assert t["dec.post_act.alpha"][0] == (1, 13, 1)
+    assert t["dec.up.0.c.weight"][0] == (864, 1, 16)
+    assert t["dec.up.4.c.weight"][0] == (54, 1, 4)
+    assert t["dec.rl.2.rb.1.rb.0.in_conv.weight"][0] == (108, 108, 7)
+    assert t["dec.rl.4.rb.2.rb.2.sk_act.alpha"][0] == (1, 13, 1)
+    assert t["dec.act.0.activation.snake_act.alpha"][0] == (1, 432, 1)
+    assert t["vq.fsqs.7.num_levels"][0] == (1, 4, 1)
+    assert len(t) == 2 + 2 + 1 + 5 * (3 + 9 * 6) + 16
+    assert kv["codec.hop_length"] == 1024
+
+
+def test_generator_is_deterministic(tmp_path):
+    import magpie_amd as ma
+    a = ma.synth_gguf(str(tmp_path / "x.gguf"), kind="codec")
+    b = ma.synth_gguf(str(tmp_path / "y.gguf"), kind="codec")
+    assert open(a, "rb").read() == open(b, "rb").read()
+
+
+def _declared_symbols():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"\b(mp_hip_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    import magpie_amd as ma
+    lib = ma.load_library()
+    declared = _declared_symbols()
+    assert len(declared) >= 15
+    for s in declared:
+        assert hasattr(lib, s), s
+    assert {s for s, _, _ in ma.SYMBOLS} == set(declared)
+    # C++ drop-in API (include/magpie.h) is exported from the same library
+    out = subprocess.run(["nm", "-DC", ma.LIB_PATH], capture_output=True, text=True).stdout
+    for fn in ["magpie_init(char const*)", "magpie_free(magpie_context*)",
+               "magpie_synthesize_codes_graph_reuse(magpie_context*, int const*, int)",
+               "magpie_codec_decode(magpie_codec*, int const*, int)", "magpie_codec_init(char const*)"]:
+        assert fn in out, fn
+
+
+def test_no_device_fails_loudly():
+    """No GPU in this container: the product path must refuse, not fall back."""
+    import magpie_amd as ma
+    if ma.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(ma.MagpieError):
+        ma.Device("/nonexistent.gguf")
+    import ctypes
+    h = ctypes.c_void_p()
+    assert ma.load_library().mp_hip_init(0, ctypes.byref(h)) != 0
+
+
+def test_golden_small_model_matches_oracle(oracle, small_model):
+    """The committed oracle fixture still reproduces (oracle regression pin)."""
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "small_model_codes.json")))
+    case = g["cases"][1]
+    m = oracle.Model(small_model)
+    r = m.synthesize(np.array(case["tokens"], np.int32), speaker=case["speaker"], max_steps=case["max_steps"])
+    m.close()
+    assert r["n_frames"] == case["n_frames"]
+    np.testing.assert_array_equal(r["codes"], np.array(case["codes"]))
+    np.testing.assert_allclose(np.abs(r["hidden"][:r["n_frames"] + 1]).sum(axis=1), case["hidden_l1"], rtol=1e-6)
+
+
+def test_bench_bytes_per_frame_matches_survey():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    # ~388.4 MB/frame at B=1, L=238.5, T=64 (f32)
+    assert abs(bench.decoder_bytes_per_frame(1, 238.5, 64) / 1e6 - 388.4) < 0.5

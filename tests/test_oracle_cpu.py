@@ -1,0 +1,119 @@
+"""CPU oracle pinned against the weight-independent known answers the reference
+holds: the FSQ formula/tables of tests/test_codec_fsq.cpp:41-74 and
+nano-codec.cpp:721-752, the codec shape progression of
+docs/CODEC_ARCHITECTURE.md:186-196, and structural properties of the path.
+Everything weight-dependent is "parity unpinned" (no weights/fixtures offline).
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def fsq_ref_numpy(codes):
+    """Independent restatement of fsq_dequantize_cpu (nano-codec.cpp:721-752)."""
+    base = np.array([1, 8, 56, 336])
+    levels = np.array([8, 7, 6, 6])
+    c = np.asarray(codes)[:, :, None]  # [8][F][1]
+    nonneg = (c // base) % levels
+    half = levels // 2
+    v = (nonneg - half).astype(np.float32) / half.astype(np.float32)  # [8][F][4]
+    return v.transpose(0, 2, 1).reshape(32, -1)  # channel = 4*cb + d, time fastest
+
+
+def test_fsq_exhaustive(oracle):
+    codes = np.tile(np.arange(2016, dtype=np.int32), (8, 1))
+    np.testing.assert_array_equal(oracle.fsq(codes), fsq_ref_numpy(codes))
+
+
+def test_fsq_known_answers(oracle):
+    # hand-derived: 0 -> all levels at 0 -> -1 everywhere; 2015 = 7 + 8*(6 + 7*(5 + 6*5))
+    c = np.zeros((8, 2), np.int32)
+    c[:, 1] = 2015
+    lat = oracle.fsq(c)
+    np.testing.assert_array_equal(lat[:4, 0], [-1, -1, -1, -1])
+    np.testing.assert_allclose(lat[:4, 1], [0.75, 1.0, 2 / 3, 2 / 3], rtol=0, atol=1e-7)
+
+
+def test_fsq_reference_fallback_codes(oracle):
+    """tests/test_codec_fsq.cpp:90-103 falls back to srand(42); rand() % 2016 codes —
+    reproduced here with the C library's rand() so the inputs are the reference's."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(42)
+    codes = np.array([libc.rand() % 2016 for _ in range(8 * 5)], np.int32).reshape(8, 5)
+    lat = oracle.fsq(codes)
+    np.testing.assert_array_equal(lat, fsq_ref_numpy(codes))
+    with open(os.path.join(GOLDEN, "fsq_srand42.json")) as f:
+        g = json.load(f)
+    np.testing.assert_array_equal(codes, np.array(g["codes"], np.int32))
+    np.testing.assert_array_equal(lat, np.array(g["latent"], np.float32))
+
+
+@pytest.mark.slow
+def test_codec_shape_progression(oracle, codec_model):
+    """5 input frames -> 5 x 1024 = 5120 samples (docs/CODEC_ARCHITECTURE.md:186-196)."""
+    c = oracle.Codec(codec_model)
+    codes = np.random.default_rng(0).integers(0, 2016, (8, 5)).astype(np.int32)
+    a = c.decode(codes, f16_operands=True)
+    c.close()
+    assert a.shape == (5120,)
+    assert np.all(np.abs(a) <= 1.0) and np.isfinite(a).all()
+
+
+def test_encoder_is_causal(oracle, small_model):
+    """The NeMo encoder uses causal attention and causal k=3 convs (magpie.cpp:1948,
+    1816-1866): the encoding of a prefix equals the prefix of the encoding."""
+    import magpie_amd as ma
+    m = oracle.Model(small_model)
+    tok = ma.synthetic_tokens(20, seed=3)
+    full = m.encode(tok)
+    pre = m.encode(tok[:9])
+    m.close()
+    np.testing.assert_allclose(pre, full[:9], rtol=0, atol=1e-6)
+
+
+def test_oracle_modes_agree(oracle, small_model):
+    """f64-accumulating parity mode vs f32 baseline mode on the same weights."""
+    import magpie_amd as ma
+    tok = ma.synthetic_tokens(12, seed=5)
+    m = oracle.Model(small_model)
+    a = m.synthesize(tok, max_steps=6, ignore_eos=True)
+    oracle.set_mode(acc64=False, gelu_f16=False, threads=4)
+    b = m.synthesize(tok, max_steps=6, ignore_eos=True)
+    oracle.set_mode(acc64=True, gelu_f16=False, threads=4)
+    m.close()
+    assert np.abs(a["hidden"] - b["hidden"]).max() < 1e-3
+    np.testing.assert_array_equal(a["codes"], b["codes"])
+
+
+def test_eos_forbidden_for_first_four_frames(oracle, eos_model):
+    """min_generated_frames = 4 (magpie.cpp:4267, 4325): the EOS-biased model stops
+    at step 4 exactly; the EOS frame is not emitted (4349-4352)."""
+    import magpie_amd as ma
+    m = oracle.Model(eos_model)
+    r = m.synthesize(ma.synthetic_tokens(10, seed=1), max_steps=32)
+    m.close()
+    assert r["n_frames"] == 4
+    assert not np.any(r["codes"] == 2017)
+
+
+def test_forbidden_tokens_never_sampled(oracle, small_model):
+    """2016 and 2018..2023 are masked before the argmax (magpie.cpp:1133-1145)."""
+    import magpie_amd as ma
+    m = oracle.Model(small_model)
+    r = m.synthesize(ma.synthetic_tokens(12, seed=9), max_steps=12, ignore_eos=True)
+    m.close()
+    assert r["codes"].max() <= 2015 and r["codes"].min() >= 0
+
+
+def test_bad_inputs_rejected(oracle, small_model):
+    m = oracle.Model(small_model)
+    with pytest.raises(RuntimeError):
+        m.synthesize(np.array([5000], np.int32), max_steps=2)
+    with pytest.raises(RuntimeError):
+        m.synthesize(np.array([1, 2], np.int32), speaker=9, max_steps=2)
+    m.close()

@@ -141,6 +141,8 @@ def test_q8_block_semantics_match_converter(tmp_path):
             p = rstr(p)
             nd, = struct.unpack_from("<I", buf, p); p += 4 + 8 * nd + 12
         return buf, (p + 31) // 32 * 32
+    shape, _, off32 = t32[name]
+    n = int(np.prod(shape))
     b32, s32 = data_start(f32)
     b8, s8 = data_start(q8)
     x = np.frombuffer(b32, np.float32, n, s32 + off32).reshape(-1, 32)

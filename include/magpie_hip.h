@@ -103,6 +103,12 @@ int mp_hip_codec_init(int device, const char *gguf_path, mp_codec **out);
 /* replaces magpie_codec_decode (nano-codec.cpp:758-845): codes [8][n_frames]
  * codebook-major, audio_out [n_frames * 1024] samples in [-1, 1]. */
 int mp_hip_codec_decode(mp_codec *c, const int32_t *codes, int n_frames, float *audio_out);
+/* n_chunks independent chunks of chunk_frames frames in one launch sequence
+ * (the CLI decodes stateless 32-frame chunks, magpie-tts.cpp:181-206):
+ * codes [n_chunks][8][chunk_frames], audio_out [n_chunks][chunk_frames * 1024]. */
+int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, int chunk_frames, float *audio_out);
+/* device time (hipEvents) of the last decode's kernel sequence, ms */
+int mp_hip_codec_last_ms(mp_codec *c, float *ms);
 void mp_hip_codec_free(mp_codec *c);
 const char *mp_hip_codec_error(mp_codec *c);
 

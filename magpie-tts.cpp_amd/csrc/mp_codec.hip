@@ -1,25 +1,532 @@
-// Nano-codec decoder on gfx950 (placeholder until the conv kernels land).
+// Nano-codec decoder on gfx950 (magpie_codec_decode, nano-codec.cpp:758-845).
+//
+// codes [8][F] -> FSQ latent -> pre-conv 32->864 k7 -> 5 x (HalfSnake -> grouped
+// convT up x{8,8,4,2,2} -> ResLayer = mean of 3 HiFiGAN blocks k{3,7,11} x
+// dilations {1,3,5}) -> HalfSnake -> conv 27->1 k3 -> tanh   
+//
+// MI355X design:
+//  * Every causal conv is an implicit GEMM on MFMA v_mfma_f32_16x16x32_f16:
+//    M = out channels, N = time, K = taps x in channels. f16 operands with f32
+//    accumulation is exactly ggml_conv_1d's semantics (F16 im2col + mul_mat,
+//    A.7), so the MFMA path is the reference's numerics, not an approximation.
+//  * Activations live in HBM as [chunk][time][channel] f32 (channel fastest,
+//    channels zero-padded to a multiple of 32): a 32-channel K-block of one time
+//    step is 64 contiguous bytes, so an input tile is staged once into LDS (with
+//    its causal halo) as f16 and reused by all ks taps -> the B fragment of every
+//    tap is one ds_read_b128.
+//  * The op before each conv is fused into its operand loader: HalfSnake
+//    (nano-codec.cpp:376-426), the FSQ dequant (721-752) for the pre-conv, and the
+//    3-branch ResLayer mean (619-641) for the next stage's input. Bias and the
+//    residual add (568-599) are fused into the epilogue. The 3 HiFiGAN branches
+//    of a ResLayer run in one launch (grid.z).
+//  * Weight-norm is already folded in the GGUF (convert_codec_to_gguf.py:169-221);
+//    weights are re-laid out once at init as f16 [Cout_p][tap][Cin_p].
+//  * The grouped ConvTranspose1d (481-565) is 4 MACs per output: an elementwise
+//    f32 kernel (ggml's conv_transpose_1d with F32 weights is an f32 dot, A.7).
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
+#include <math.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/magpie_hip.h"
+#include "mp_device.hpp"
+#include "mp_gguf.hpp"
 
+namespace mpc {
+
+constexpr int NSTAGE = 5;
+constexpr int CH[6] = {864, 432, 216, 108, 54, 27};   // real channels (stage i input CH[i], output CH[i+1])
+constexpr int CP[5] = {448, 224, 128, 64, 32};         // padded channels of stage i's output
+constexpr int BMS[5] = {64, 32, 64, 64, 32};           // MFMA tile rows per stage
+constexpr int CP_PRE = 896;                            // pre-conv output 864 padded
+constexpr int RATE[5] = {8, 8, 4, 2, 2};
+constexpr int KS[3] = {3, 7, 11};
+constexpr int DIL[3] = {1, 3, 5};
+constexpr int HOP = 1024;
+
+enum InMode { IN_PLAIN = 0, IN_FSQ = 1, IN_AVG3 = 2 };
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct ConvP {
+    // per-branch (grid.z) operands
+    const _Float16 *W[3];   // [Coutp][ks][Cinp] f16
+    const float *bias[3];   // [Coutp] (zero padded)
+    const float *alpha[3];  // HalfSnake alpha (nullptr: no activation)
+    const float *x[3];      // input [chunk][T][Cinp]
+    float *out[3];          // output [chunk][T][Coutp]
+    const float *resid[3];  // optional residual [chunk][T][Coutp]
+    int ks[3];
+    const float *xa, *xb;   // IN_AVG3: second and third branch inputs (x[] = first)
+    const int *codes;       // IN_FSQ: [chunk][8][T]
+    int n_snake, cin_real;
+    int Cinp, Coutp, T, dil;
+    int tiles_per_chunk;
+};
+
+__device__ __forceinline__ float half_snake(float v, int c, int n_snake, int cin_real, const float *alpha) {
+    // nano-codec.cpp:401-417 in ggml op order: mul, sin, sqr, div, add | leaky 0.01
+    if (c < n_snake) {
+        const float a = alpha[c];
+        const float s = sinf(v * a);
+        return v + (s * s) / a;
+    }
+    if (c < cin_real) return v > 0.f ? v : 0.01f * v;
+    return 0.f;
+}
+
+// fsq_dequantize_cpu (nano-codec.cpp:721-752): channel c = 4*cb + d
+__device__ __forceinline__ float fsq(int code, int d) {
+    const int base = d == 0 ? 1 : d == 1 ? 8 : d == 2 ? 56 : 336;
+    const int lev = d == 0 ? 8 : d == 1 ? 7 : 6;
+    const int half = lev / 2;
+    return (float)((code / base) % lev - half) / (float)half;
+}
+
+// Implicit-GEMM causal conv. Block tile BM (out ch) x BN (time), 4 waves.
+template <int BM, int BN, int MODE>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
+    constexpr int RW = BM / 16;          // row blocks of 16
+    constexpr int CWN = 4 / RW;          // column groups
+    constexpr int WCOLS = BN / CWN;      // columns per wave
+    constexpr int NT = WCOLS / 16;       // MFMA column tiles per wave
+    constexpr int ROWB = 80;             // LDS bytes per time row: 32 halves + 16 B pad
+    constexpr int MAXHALO = 50;          // (11 - 1) * 5
+    __shared__ __attribute__((aligned(16))) char xs[(BN + MAXHALO) * ROWB];
+
+    const int br = blockIdx.z;
+    const int ks = p.ks[br];
+    const int pad = (ks - 1) * p.dil;
+    const int m0 = blockIdx.x * BM;
+    const int chunk = blockIdx.y / p.tiles_per_chunk;
+    const int t0 = (blockIdx.y % p.tiles_per_chunk) * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rw = w % RW, cw = w / RW;
+    const int kg = lane >> 4, l16 = lane & 15;
+    const size_t chunk_in = (size_t)chunk * p.T * p.Cinp;
+    const float *xin = p.x[br] + chunk_in;
+    const float *alpha = p.alpha[br];
+    const _Float16 *W = p.W[br];
+    const int Kw = ks * p.Cinp;
+    const int orow = m0 + rw * 16 + l16;
+
+    floatx4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int rows = BN + pad;
+    for (int i0 = 0; i0 < p.Cinp; i0 += 32) {
+        // ---- stage input rows [t0 - pad, t0 + BN) x channels [i0, i0+32) as f16
+        for (int e = tid; e < rows * 8; e += 256) {
+            const int r = e >> 3, c4 = (e & 7) * 4;
+            const int t = t0 - pad + r;
+            float v[4] = {0.f, 0.f, 0.f, 0.f};
+            if (t >= 0 && t < p.T) {
+                if constexpr (MODE == IN_FSQ) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int c = i0 + c4 + u;
+                        v[u] = fsq(p.codes[((size_t)chunk * 8 + (c >> 2)) * p.T + t], c & 3);
+                    }
+                } else {
+                    float4 a = *(const float4 *)(xin + (size_t)t * p.Cinp + i0 + c4);
+                    if constexpr (MODE == IN_AVG3) {
+                        const float4 b = *(const float4 *)(p.xa + chunk_in + (size_t)t * p.Cinp + i0 + c4);
+                        const float4 c = *(const float4 *)(p.xb + chunk_in + (size_t)t * p.Cinp + i0 + c4);
+                        // magpie_codec_build_reslayer: (b0 + b1) + b2, then * (1/3)
+                        a.x = ((a.x + b.x) + c.x) * (1.0f / 3.0f);
+                        a.y = ((a.y + b.y) + c.y) * (1.0f / 3.0f);
+                        a.z = ((a.z + b.z) + c.z) * (1.0f / 3.0f);
+                        a.w = ((a.w + b.w) + c.w) * (1.0f / 3.0f);
+                    }
+                    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+                    if (alpha) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) v[u] = half_snake(v[u], i0 + c4 + u, p.n_snake, p.cin_real, alpha);
+                    }
+                }
+            }
+            _Float16 *dst = (_Float16 *)(xs + r * ROWB) + c4;
+            dst[0] = (_Float16)v[0]; dst[1] = (_Float16)v[1]; dst[2] = (_Float16)v[2]; dst[3] = (_Float16)v[3];
+        }
+        __syncthreads();
+        // ---- ks taps: A from the f16 weight image (L2-resident), B from LDS
+        for (int k = 0; k < ks; ++k) {
+            const half8 a = *(const half8 *)(W + (size_t)orow * Kw + k * p.Cinp + i0 + 8 * kg);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int col = cw * WCOLS + j * 16 + l16;
+                const half8 b = *(const half8 *)(xs + (col + k * p.dil) * ROWB + 16 * kg);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[j], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // ---- epilogue: C[row = 4*kg + r][col = l16] -> 4 consecutive channels of one time step
+    const int o = m0 + rw * 16 + 4 * kg;
+    const float4 bb = *(const float4 *)(p.bias[br] + o);
+    const size_t chunk_out = (size_t)chunk * p.T * p.Coutp;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int t = t0 + cw * WCOLS + j * 16 + l16;
+        if (t >= p.T) continue;
+        float4 v = make_float4(acc[j][0] + bb.x, acc[j][1] + bb.y, acc[j][2] + bb.z, acc[j][3] + bb.w);
+        const size_t off = chunk_out + (size_t)t * p.Coutp + o;
+        if (p.resid[br]) {
+            const float4 r = *(const float4 *)(p.resid[br] + off);
+            v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;  // input + h (568-599)
+        }
+        *(float4 *)(p.out[br] + off) = v;
+    }
+}
+
+// Grouped ConvTranspose1d (nano-codec.cpp:481-565), HalfSnake on its input,
+// optional 3-branch mean before it: out[t][g] = b[g] + sum_{c in {2g,2g+1}}
+// sum_{tau: 0 <= t - tau*s < 2s} x[tau][c] * w[c][t - tau*s]; kept length T*s.
+struct ConvTP {
+    const float *x, *xa, *xb;  // input [chunk][Tin][Cinp] (xa/xb: AVG3)
+    const float *alpha;
+    int n_snake, cin_real, Cinp;
+    const float *w;            // [Cin_real][2s] f32
+    const float *bias;         // [Cout_real]
+    float *out;                // [chunk][Tin*s][Coutp]
+    int cout_real, Coutp, Tin, s, nchunk;
+};
+template <bool AVG>
+__global__ __launch_bounds__(256) void conv_transpose_kernel(ConvTP p) {
+    const size_t total = (size_t)p.nchunk * p.Tin * p.s * p.Coutp;
+    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (size_t)gridDim.x * 256) {
+        const int g = (int)(e % p.Coutp);
+        const size_t tt = e / p.Coutp;
+        const int t = (int)(tt % ((size_t)p.Tin * p.s));
+        const int chunk = (int)(tt / ((size_t)p.Tin * p.s));
+        float acc = 0.f;
+        if (g < p.cout_real) {
+            const int K = 2 * p.s;
+            for (int ci = 0; ci < 2; ++ci) {
+                const int c = 2 * g + ci;
+                for (int tau = t / p.s - 1; tau <= t / p.s; ++tau) {
+                    if (tau < 0 || tau >= p.Tin) continue;
+                    const size_t xo = ((size_t)chunk * p.Tin + tau) * p.Cinp + c;
+                    float v = p.x[xo];
+                    if constexpr (AVG) v = ((v + p.xa[xo]) + p.xb[xo]) * (1.0f / 3.0f);
+                    v = half_snake(v, c, p.n_snake, p.cin_real, p.alpha);
+                    acc += v * p.w[(size_t)c * K + (t - tau * p.s)];
+                }
+            }
+            acc += p.bias[g];
+        }
+        p.out[e] = acc;
+    }
+}
+
+// HalfSnake(post) -> causal conv 27->1 k3 (f16 operands, ggml_conv_1d) -> +b -> tanh
+// (nano-codec.cpp:702-712) on the 3-branch mean of the last ResLayer.
+struct PostP {
+    const float *x, *xa, *xb;  // [chunk][T][32]
+    const float *alpha;        // 13
+    const float *w;            // [27][3] f32
+    const float *bias;
+    float *audio;              // [chunk][T]
+    int T, nchunk;
+};
+__global__ __launch_bounds__(256) void post_conv_kernel(PostP p) {
+    const size_t total = (size_t)p.nchunk * p.T;
+    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (size_t)gridDim.x * 256) {
+        const int t = (int)(e % p.T);
+        const size_t cbase = (e / p.T) * p.T;
+        float acc = 0.f;
+        for (int k = 0; k < 3; ++k) {
+            const int ts = t - 2 + k;
+            if (ts < 0) continue;
+            const float *x = p.x + (cbase + ts) * 32, *xa = p.xa + (cbase + ts) * 32, *xb = p.xb + (cbase + ts) * 32;
+            for (int i = 0; i < 27; ++i) {
+                float v = ((x[i] + xa[i]) + xb[i]) * (1.0f / 3.0f);
+                v = half_snake(v, i, 13, 27, p.alpha);
+                acc += (float)(_Float16)v * (float)(_Float16)p.w[i * 3 + k];
+            }
+        }
+        p.audio[e] = tanhf(acc + p.bias[0]);
+    }
+}
+
+}  // namespace mpc
+
+// ====================================================================== runtime
 struct mp_codec {
     int device = 0;
     std::string err;
+    hipStream_t stream = nullptr;
+    // weights
+    struct Conv { _Float16 *w = nullptr; float *b = nullptr; int ks = 0, cin = 0, cout = 0, cinp = 0, coutp = 0; };
+    Conv pre, rb[5][3][3][2];  // [stage][kernel j][dilation k][in/skip]
+    float *rb_alpha[5][3][3][2] = {};
+    float *up_alpha[5] = {}, *up_w[5] = {}, *up_b[5] = {};
+    float *post_alpha = nullptr, *post_w = nullptr, *post_b = nullptr;
+    std::vector<void *> weight_allocs;
+    // activations (grown on demand)
+    size_t cap_elems = 0;
+    float *x_pre = nullptr, *x0 = nullptr, *brb[3] = {}, *tmp[3] = {}, *audio = nullptr;
+    int *codes = nullptr;
+    size_t codes_cap = 0, audio_cap = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.f;  // device time of the last decode (launch sequence only)
 };
 
+namespace {
+
+#define CHK(expr)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            c->err = std::string(#expr) + " failed: " + hipGetErrorString(e_);                     \
+            return MP_ERR_HIP;                                                                     \
+        }                                                                                          \
+    } while (0)
+
+template <class T> int upload(mp_codec *c, T **dst, const std::vector<T> &h) {
+    void *p = nullptr;
+    CHK(hipMalloc(&p, h.size() * sizeof(T) + 64));
+    CHK(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    c->weight_allocs.push_back(p);
+    *dst = (T *)p;
+    return MP_OK;
+}
+
+int load_f32(mp_codec *c, const mp::Gguf &g, const std::string &name, int64_t n, std::vector<float> &out) {
+    const mp::GgufTensor *t = g.find(name);
+    if (!t) { c->err = "missing codec tensor " + name; return MP_ERR_FORMAT; }
+    if (n >= 0 && t->nelements() != n) { c->err = "unexpected shape for " + name; return MP_ERR_FORMAT; }
+    out.resize((size_t)t->nelements());
+    if (!g.to_f32(*t, out.data())) { c->err = "unsupported tensor type in " + name; return MP_ERR_FORMAT; }
+    return MP_OK;
+}
+
+// conv weight [cout][cin][ks] (PyTorch) -> f16 [coutp][ks][cinp] zero padded
+int load_conv(mp_codec *c, const mp::Gguf &g, const std::string &wname, const std::string &bname, int cout, int cin,
+              int ks, int coutp, int cinp, mp_codec::Conv &cv) {
+    std::vector<float> w, b;
+    if (int rc = load_f32(c, g, wname, (int64_t)cout * cin * ks, w)) return rc;
+    if (int rc = load_f32(c, g, bname, cout, b)) return rc;
+    std::vector<_Float16> wi((size_t)coutp * ks * cinp, (_Float16)0.f);
+    for (int o = 0; o < cout; ++o)
+        for (int i = 0; i < cin; ++i)
+            for (int k = 0; k < ks; ++k) wi[((size_t)o * ks + k) * cinp + i] = (_Float16)w[((size_t)o * cin + i) * ks + k];
+    b.resize(coutp, 0.f);
+    cv.ks = ks; cv.cin = cin; cv.cout = cout; cv.cinp = cinp; cv.coutp = coutp;
+    if (int rc = upload(c, &cv.w, wi)) return rc;
+    return upload(c, &cv.b, b);
+}
+
+int load_codec(mp_codec *c, const char *path) {
+    mp::Gguf g;
+    std::string err;
+    if (!g.open(path, err)) { c->err = err; return MP_ERR_IO; }
+    if (g.get_u32("codec.num_codebooks", 8) != 8 || g.get_u32("codec.hop_length", 1024) != 1024 ||
+        g.get_u32("codec.latent_dim", 32) != 32) {
+        c->err = "codec hyperparameters differ from the nano-codec (kernels are specialised)";
+        return MP_ERR_UNSUPPORTED;
+    }
+    using namespace mpc;
+    if (int rc = load_conv(c, g, "dec.pre.weight", "dec.pre.bias", 864, 32, 7, CP_PRE, 32, c->pre)) return rc;
+    std::vector<float> v;
+    for (int i = 0; i < NSTAGE; ++i) {
+        const int cin = CH[i], C = CH[i + 1];
+        if (int rc = load_f32(c, g, "dec.act." + std::to_string(i) + ".activation.snake_act.alpha", cin / 2, v)) return rc;
+        if (int rc = upload(c, &c->up_alpha[i], v)) return rc;
+        if (int rc = load_f32(c, g, "dec.up." + std::to_string(i) + ".c.weight", (int64_t)cin * 2 * RATE[i], v)) return rc;
+        if (int rc = upload(c, &c->up_w[i], v)) return rc;
+        if (int rc = load_f32(c, g, "dec.up." + std::to_string(i) + ".c.bias", C, v)) return rc;
+        if (int rc = upload(c, &c->up_b[i], v)) return rc;
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) {
+                const std::string p = "dec.rl." + std::to_string(i) + ".rb." + std::to_string(j) + ".rb." + std::to_string(k) + ".";
+                if (int rc = load_f32(c, g, p + "in_act.alpha", C / 2, v)) return rc;
+                if (int rc = upload(c, &c->rb_alpha[i][j][k][0], v)) return rc;
+                if (int rc = load_f32(c, g, p + "sk_act.alpha", C / 2, v)) return rc;
+                if (int rc = upload(c, &c->rb_alpha[i][j][k][1], v)) return rc;
+                if (int rc = load_conv(c, g, p + "in_conv.weight", p + "in_conv.bias", C, C, KS[j], CP[i], CP[i], c->rb[i][j][k][0])) return rc;
+                if (int rc = load_conv(c, g, p + "sk_conv.weight", p + "sk_conv.bias", C, C, KS[j], CP[i], CP[i], c->rb[i][j][k][1])) return rc;
+            }
+    }
+    if (int rc = load_f32(c, g, "dec.post_act.alpha", 13, v)) return rc;
+    if (int rc = upload(c, &c->post_alpha, v)) return rc;
+    if (int rc = load_f32(c, g, "dec.post.weight", 27 * 3, v)) return rc;
+    if (int rc = upload(c, &c->post_w, v)) return rc;
+    if (int rc = load_f32(c, g, "dec.post.bias", 1, v)) return rc;
+    return upload(c, &c->post_b, v);
+}
+
+int ensure_buffers(mp_codec *c, int nchunk, int F) {
+    using namespace mpc;
+    size_t need = 0;
+    for (int i = 0; i < NSTAGE; ++i) {
+        size_t T = (size_t)F;
+        for (int s = 0; s <= i; ++s) T *= RATE[s];
+        need = std::max(need, (size_t)nchunk * T * CP[i]);
+    }
+    need = std::max(need, (size_t)nchunk * F * CP_PRE);
+    if (need > c->cap_elems) {
+        float **bufs[8] = {&c->x_pre, &c->x0, &c->brb[0], &c->brb[1], &c->brb[2], &c->tmp[0], &c->tmp[1], &c->tmp[2]};
+        for (auto b : bufs) if (*b) { hipFree(*b); *b = nullptr; }
+        for (auto b : bufs) CHK(hipMalloc((void **)b, need * 4 + 256));
+        c->cap_elems = need;
+    }
+    const size_t ncodes = (size_t)nchunk * 8 * F, naudio = (size_t)nchunk * F * HOP;
+    if (ncodes > c->codes_cap) {
+        if (c->codes) hipFree(c->codes);
+        CHK(hipMalloc((void **)&c->codes, ncodes * 4));
+        c->codes_cap = ncodes;
+    }
+    if (naudio > c->audio_cap) {
+        if (c->audio) hipFree(c->audio);
+        CHK(hipMalloc((void **)&c->audio, naudio * 4));
+        c->audio_cap = naudio;
+    }
+    return MP_OK;
+}
+
+template <int BM, int BN, int MODE>
+hipError_t launch_conv(const mpc::ConvP &p, int nchunk, int nbranch, hipStream_t s) {
+    dim3 grid(p.Coutp / BM, nchunk * p.tiles_per_chunk, nbranch);
+    hipLaunchKernelGGL((mpc::conv_mfma_kernel<BM, BN, MODE>), grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t run_conv(const mpc::ConvP &p, int BM, int mode, int nchunk, int nbranch, hipStream_t s) {
+    using namespace mpc;
+    if (BM == 64) {
+        if (mode == IN_FSQ) return launch_conv<64, 64, IN_FSQ>(p, nchunk, nbranch, s);
+        return launch_conv<64, 64, IN_PLAIN>(p, nchunk, nbranch, s);
+    }
+    return launch_conv<32, 128, IN_PLAIN>(p, nchunk, nbranch, s);
+}
+
+// Decode nchunk independent chunks of F frames each (codes [chunk][8][F]).
+int codec_run(mp_codec *c, int nchunk, int F) {
+    using namespace mpc;
+    hipStream_t s = c->stream;
+    // pre-conv with the FSQ dequant in its loader
+    {
+        ConvP p{};
+        p.W[0] = c->pre.w; p.bias[0] = c->pre.b; p.alpha[0] = nullptr; p.x[0] = nullptr; p.out[0] = c->x_pre;
+        p.resid[0] = nullptr; p.ks[0] = 7; p.codes = c->codes; p.n_snake = 0; p.cin_real = 32;
+        p.Cinp = 32; p.Coutp = CP_PRE; p.T = F; p.dil = 1; p.tiles_per_chunk = (F + 63) / 64;
+        CHK(run_conv(p, 64, IN_FSQ, nchunk, 1, s));
+    }
+    int T = F;
+    for (int i = 0; i < NSTAGE; ++i) {
+        const int cin = CH[i], C = CH[i + 1], Cin_p = i == 0 ? CP_PRE : CP[i - 1], Cp = CP[i];
+        // HalfSnake -> grouped convT (input: pre-conv, or mean of the previous ResLayer's branches)
+        ConvTP tp{};
+        tp.x = i == 0 ? c->x_pre : c->brb[0];
+        tp.xa = c->brb[1]; tp.xb = c->brb[2];
+        tp.alpha = c->up_alpha[i]; tp.n_snake = cin / 2; tp.cin_real = cin; tp.Cinp = Cin_p;
+        tp.w = c->up_w[i]; tp.bias = c->up_b[i]; tp.out = c->x0; tp.cout_real = C; tp.Coutp = Cp;
+        tp.Tin = T; tp.s = RATE[i]; tp.nchunk = nchunk;
+        const size_t total = (size_t)nchunk * T * RATE[i] * Cp;
+        const int grid = (int)std::min<size_t>((total + 255) / 256, 65536);
+        if (i == 0) hipLaunchKernelGGL(conv_transpose_kernel<false>, dim3(grid), dim3(256), 0, s, tp);
+        else hipLaunchKernelGGL(conv_transpose_kernel<true>, dim3(grid), dim3(256), 0, s, tp);
+        CHK(hipGetLastError());
+        T *= RATE[i];
+        const int BM = BMS[i], BN = BM == 64 ? 64 : 128;
+        for (int k = 0; k < 3; ++k) {
+            // h = conv_{ks_j, d_k}(HS_in(x)) for the 3 branches j
+            ConvP p{};
+            for (int j = 0; j < 3; ++j) {
+                const mp_codec::Conv &cv = c->rb[i][j][k][0];
+                p.W[j] = cv.w; p.bias[j] = cv.b; p.alpha[j] = c->rb_alpha[i][j][k][0];
+                p.x[j] = k == 0 ? c->x0 : c->brb[j]; p.out[j] = c->tmp[j]; p.resid[j] = nullptr; p.ks[j] = KS[j];
+            }
+            p.n_snake = C / 2; p.cin_real = C; p.Cinp = Cp; p.Coutp = Cp; p.T = T; p.dil = DIL[k];
+            p.tiles_per_chunk = (T + BN - 1) / BN;
+            CHK(run_conv(p, BM, IN_PLAIN, nchunk, 3, s));
+            // x' = x + conv_{ks_j, 1}(HS_sk(h))
+            for (int j = 0; j < 3; ++j) {
+                const mp_codec::Conv &cv = c->rb[i][j][k][1];
+                p.W[j] = cv.w; p.bias[j] = cv.b; p.alpha[j] = c->rb_alpha[i][j][k][1];
+                p.x[j] = c->tmp[j]; p.out[j] = c->brb[j]; p.resid[j] = k == 0 ? c->x0 : c->brb[j];
+            }
+            p.dil = 1;
+            CHK(run_conv(p, BM, IN_PLAIN, nchunk, 3, s));
+        }
+    }
+    PostP pp{c->brb[0], c->brb[1], c->brb[2], c->post_alpha, c->post_w, c->post_b, c->audio, T, nchunk};
+    const size_t total = (size_t)nchunk * T;
+    hipLaunchKernelGGL(post_conv_kernel, dim3((int)std::min<size_t>((total + 255) / 256, 65536)), dim3(256), 0, s, pp);
+    CHK(hipGetLastError());
+    return MP_OK;
+}
+
+}  // namespace
+
 extern "C" {
+
 int mp_hip_codec_init(int device, const char *path, mp_codec **out) {
-    (void)device; (void)path;
-    if (out) *out = nullptr;
-    return MP_ERR_UNSUPPORTED;
+    if (!out || !path) return MP_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return MP_ERR_HIP;
+    mp_codec *c = new mp_codec();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return MP_ERR_HIP;
+    }
+    if (int rc = load_codec(c, path)) {
+        fprintf(stderr, "mp_hip_codec_init: %s\n", c->err.c_str());
+        mp_hip_codec_free(c);
+        return rc;
+    }
+    *out = c;
+    return MP_OK;
 }
+
+int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, int chunk_frames, float *audio_out) {
+    if (!c) return MP_ERR_ARG;
+    if (!codes || !audio_out || n_chunks < 1 || chunk_frames < 1) { c->err = "invalid arguments"; return MP_ERR_ARG; }
+    CHK(hipSetDevice(c->device));
+    if (int rc = ensure_buffers(c, n_chunks, chunk_frames)) return rc;
+    CHK(hipMemcpyAsync(c->codes, codes, (size_t)n_chunks * 8 * chunk_frames * 4, hipMemcpyHostToDevice, c->stream));
+    if (!c->ev0) { CHK(hipEventCreate(&c->ev0)); CHK(hipEventCreate(&c->ev1)); }
+    CHK(hipEventRecord(c->ev0, c->stream));
+    if (int rc = codec_run(c, n_chunks, chunk_frames)) return rc;
+    CHK(hipEventRecord(c->ev1, c->stream));
+    CHK(hipMemcpyAsync(audio_out, c->audio, (size_t)n_chunks * chunk_frames * mpc::HOP * 4, hipMemcpyDeviceToHost, c->stream));
+    CHK(hipStreamSynchronize(c->stream));
+    CHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MP_OK;
+}
+
+int mp_hip_codec_last_ms(mp_codec *c, float *ms) {
+    if (!c || !ms) return MP_ERR_ARG;
+    *ms = c->last_ms;
+    return MP_OK;
+}
+
 int mp_hip_codec_decode(mp_codec *c, const int32_t *codes, int n_frames, float *audio_out) {
-    (void)c; (void)codes; (void)n_frames; (void)audio_out;
-    return MP_ERR_UNSUPPORTED;
+    return mp_hip_codec_decode_chunks(c, codes, 1, n_frames, audio_out);
 }
-void mp_hip_codec_free(mp_codec *c) { delete c; }
+
+void mp_hip_codec_free(mp_codec *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (void *p : c->weight_allocs) hipFree(p);
+    float *bufs[8] = {c->x_pre, c->x0, c->brb[0], c->brb[1], c->brb[2], c->tmp[0], c->tmp[1], c->tmp[2]};
+    for (float *b : bufs) if (b) hipFree(b);
+    if (c->codes) hipFree(c->codes);
+    if (c->audio) hipFree(c->audio);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
 const char *mp_hip_codec_error(mp_codec *c) { return c ? c->err.c_str() : "null mp_codec"; }
-}
+
+}  // extern "C"

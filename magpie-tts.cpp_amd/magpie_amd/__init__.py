@@ -70,6 +70,8 @@ SYMBOLS = [
     ("mp_hip_time_op", _I, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mp_hip_codec_init", _I, [_I, ctypes.c_char_p, ctypes.POINTER(_P)]),
     ("mp_hip_codec_decode", _I, [_P, _P, _I, _P]),
+    ("mp_hip_codec_decode_chunks", _I, [_P, _P, _I, _I, _P]),
+    ("mp_hip_codec_last_ms", _I, [_P, ctypes.POINTER(ctypes.c_float)]),
     ("mp_hip_codec_free", None, [_P]),
     ("mp_hip_codec_error", ctypes.c_char_p, [_P]),
 ]
@@ -227,6 +229,22 @@ class Codec:
         if rc != MP_OK:
             raise MagpieError(f"{_ERRS.get(rc, rc)}: {self.lib.mp_hip_codec_error(self.h).decode(errors='replace')}")
         return out
+
+    def decode_chunks(self, codes: np.ndarray) -> np.ndarray:
+        """codes [n_chunks][8][F] -> audio [n_chunks][F*1024], chunks independent."""
+        codes = np.ascontiguousarray(codes, np.int32)
+        n, eight, F = codes.shape
+        assert eight == 8
+        out = np.zeros((n, F * 1024), np.float32)
+        rc = self.lib.mp_hip_codec_decode_chunks(self.h, codes.ctypes.data, n, F, out.ctypes.data)
+        if rc != MP_OK:
+            raise MagpieError(f"{_ERRS.get(rc, rc)}: {self.lib.mp_hip_codec_error(self.h).decode(errors='replace')}")
+        return out
+
+    def last_ms(self) -> float:
+        ms = ctypes.c_float()
+        self.lib.mp_hip_codec_last_ms(self.h, ctypes.byref(ms))
+        return ms.value
 
     def close(self) -> None:
         if getattr(self, "h", None) is not None and self.h.value:

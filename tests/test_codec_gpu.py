@@ -1,0 +1,66 @@
+"""GPU nano-codec (C-ABI -> MFMA conv kernels) vs the CPU oracle.
+
+Reference: magpie_codec_decode (nano-codec.cpp:758-845). The oracle's
+f16_operands mode applies ggml_conv_1d's F16 im2col rounding (A.7) — the same
+operand precision as the f16 MFMA path — with f64 accumulation.
+Tolerance: 2e-3 abs on the waveform (the reference's own full-decoder test uses
+0.05, observed 0.0045: tests/test_codec_decode.cpp:562, docs/STATUS.md:149-173).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+WAVE_TOL = 2e-3
+
+
+@pytest.fixture(scope="module")
+def gpu_codec(codec_model):
+    import magpie_amd as ma
+    if ma.device_count() < 1:
+        pytest.fail("no HIP device visible")
+    c = ma.Codec(codec_model)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def cpu_codec(oracle, codec_model):
+    c = oracle.Codec(codec_model)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("F", [1, 5, 8])
+def test_codec_matches_oracle(gpu_codec, cpu_codec, F):
+    codes = np.random.default_rng(100 + F).integers(0, 2016, (8, F)).astype(np.int32)
+    g = gpu_codec.decode(codes)
+    o = cpu_codec.decode(codes, f16_operands=True)
+    assert g.shape == (F * 1024,)  # docs/CODEC_ARCHITECTURE.md:186-196
+    err = np.abs(g - o).max()
+    rel = np.linalg.norm(g - o) / np.linalg.norm(o)
+    assert err < WAVE_TOL and rel < 2e-3, f"max abs err {err}, rel L2 {rel}"
+    # and against plain f32 operands (the precision gap ggml's F16 im2col introduces)
+    o32 = cpu_codec.decode(codes, f16_operands=False)
+    assert np.abs(g - o32).max() < 1e-2
+
+
+def test_codec_32_frame_chunk(gpu_codec, cpu_codec):
+    """The CLI decodes stateless 32-frame chunks (magpie-tts.cpp:181-206)."""
+    codes = np.random.default_rng(7).integers(0, 2016, (8, 32)).astype(np.int32)
+    g = gpu_codec.decode(codes)
+    o = cpu_codec.decode(codes, f16_operands=True)
+    assert np.abs(g - o).max() < WAVE_TOL
+
+
+def test_chunked_equals_independent(gpu_codec):
+    rng = np.random.default_rng(3)
+    chunks = rng.integers(0, 2016, (3, 8, 16)).astype(np.int32)
+    batched = gpu_codec.decode_chunks(chunks)
+    for i in range(3):
+        np.testing.assert_array_equal(batched[i], gpu_codec.decode(chunks[i]))
+
+
+def test_codec_deterministic(gpu_codec):
+    codes = np.random.default_rng(11).integers(0, 2016, (8, 12)).astype(np.int32)
+    np.testing.assert_array_equal(gpu_codec.decode(codes), gpu_codec.decode(codes))

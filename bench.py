@@ -36,6 +36,9 @@ import numpy as np  # noqa: E402
 import magpie_amd as ma  # noqa: E402  (loads libmagpie_hip.so before torch can load another HIP runtime)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
+CODEC_FLOP_PER_FRAME = 2.447e9  # 1.2234 G MAC per codec frame
+CODEC_CHUNK = 32  # the CLI decodes stateless 32-frame chunks (magpie-tts.cpp:181-206)
 FRAMES = 256
 TEXT_TOKENS = 64
 
@@ -60,6 +63,7 @@ def main() -> None:
     ap.add_argument("--cpu-threads", type=int, default=4,
                     help="oracle threads for cpu_baseline (ggml's default n_threads, magpie.h:298,306)")
     ap.add_argument("--profile-ops", type=int, default=30, help="event-timed launches per op for the roofline")
+    ap.add_argument("--no-codec", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -117,6 +121,36 @@ def main() -> None:
     total_frames = frames * world
     value = total_frames / t_max
     ms_per_step = 1e3 * t_max / args.steps
+
+    # ---- nano-codec on the device: every utterance's 256 frames as 32-frame chunks
+    codec = None
+    if not args.no_codec:
+        codec_path = os.path.join(cache, "nano_codec.gguf")
+        if rank == 0 or world == 1:
+            ma.synth_gguf(codec_path, kind="codec")
+        if dist is not None:
+            dist.barrier()
+        cdc = ma.Codec(codec_path, device=local)
+        chunks = []
+        for b in range(B):
+            c = rr.codes[b]
+            for s0 in range(0, len(c), CODEC_CHUNK):
+                ch = c[s0:s0 + CODEC_CHUNK]
+                if len(ch) == CODEC_CHUNK:
+                    chunks.append(ch.T)  # frame-major -> codebook-major (magpie-tts.cpp:186-191)
+        chunks = np.stack(chunks).astype(np.int32)
+        cdc.decode_chunks(chunks)  # warm-up
+        cms = []
+        for _ in range(3):
+            audio = cdc.decode_chunks(chunks)
+            cms.append(cdc.last_ms())
+        cdc.close()
+        codec_ms = float(np.median(cms))
+        cframes = chunks.shape[0] * CODEC_CHUNK
+        tfs = CODEC_FLOP_PER_FRAME * cframes / (codec_ms * 1e-3) / 1e12
+        codec = {"frames": cframes, "ms": round(codec_ms, 3), "fps": round(cframes / (codec_ms * 1e-3), 1),
+                 "tflops": round(tfs, 1), "mfma_f16_peak_tflops": MFMA_F16_PEAK_TFS,
+                 "frac": round(tfs / MFMA_F16_PEAK_TFS, 4), "audio_peak": round(float(np.abs(audio).max()), 4)}
 
     # ---- roofline of the dominant kernel (event-timed live, same stream as the graph)
     roofline = None
@@ -176,6 +210,11 @@ def main() -> None:
             "decode_fps_events": round(B * args.frames * 1e3 / float(np.mean(decode_ms)), 2),
             "e2e_fps_first_call": round(B * args.frames / e2e_first_s, 2),
             "preamble_ms": round(preamble_ms, 2),
+            "codec": codec,
+            "e2e_fps_per_gpu": (round(B * args.frames / ((ms_per_step + preamble_ms + (codec["ms"] if codec else 0))
+                                                        * 1e-3), 1)),
+            "rtf_e2e_per_stream": (round(args.frames / ma.FRAMES_PER_SECOND /
+                                         ((ms_per_step + preamble_ms + (codec["ms"] if codec else 0)) * 1e-3), 1)),
             "decode_roofline": {"bytes_per_frame": round(bpf), "achieved_GBs": round(bpf * fps_per_gpu / 1e9, 1),
                                 "frac": round(bpf * fps_per_gpu / 1e9 / HBM_PEAK_GBS, 4)},
             "roofline": roofline,

@@ -93,8 +93,9 @@ int mp_hip_num_ops(mp_dev *dev);
 const char *mp_hip_op_name(mp_dev *dev, int op);
 /* algorithmic HBM bytes one launch of `op` moves (weights + activations) */
 double mp_hip_op_bytes(mp_dev *dev, int op);
-/* Re-launch one op of the iteration `reps` times on the decode stream, timed with
- * a hipEvent pair around each launch; returns the mean launch duration in us. */
+/* Re-launch one op of the iteration `reps` times back to back on the decode
+ * stream (same arguments as in the captured graph), one hipEvent pair around
+ * the whole run; returns the mean per-launch time in us (kernel + dispatch gap). */
 int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us);
 
 /* --- nano-codec ----------------------------------------------------------- */

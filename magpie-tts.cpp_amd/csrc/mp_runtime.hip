@@ -768,24 +768,25 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     r.g.ndone = nullptr;
     r.a.ndone = nullptr;
     r.g.trace = nullptr;
-    std::vector<hipEvent_t> ev(2 * (size_t)reps);
-    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
-    for (int i = 0; i < reps; ++i) {
-        HIPCHK(hipEventRecord(ev[2 * i], dev->stream));
-        if (r.kind == mp::K_GEMV) HIPCHK(r.fn(r.g, dev->stream));
-        else if (r.kind == mp::K_ATTN) HIPCHK(mp::op_sa_attn(r.a, r.B, dev->stream));
-        else return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");
-        HIPCHK(hipEventRecord(ev[2 * i + 1], dev->stream));
-    }
-    HIPCHK(hipStreamSynchronize(dev->stream));
-    double tot = 0.0;
-    for (int i = 0; i < reps; ++i) {
-        float ms = 0.f;
-        HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
-        tot += ms;
-    }
-    for (auto &e : ev) hipEventDestroy(e);
-    *avg_us = (float)(tot * 1000.0 / reps);
+    auto launch = [&]() -> hipError_t {
+        if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
+        if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
+        return hipErrorInvalidValue;
+    };
+    if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");
+    HIPCHK(launch());  // warm
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, dev->stream));
+    for (int i = 0; i < reps; ++i) HIPCHK(launch());
+    HIPCHK(hipEventRecord(e1, dev->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    *avg_us = ms * 1000.f / reps;
     return MP_OK;
 }
 

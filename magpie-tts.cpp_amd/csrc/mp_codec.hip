@@ -233,24 +233,35 @@ struct PostP {
     float *audio;              // [chunk][T]
     int T, nchunk;
 };
+// One workgroup = 256 consecutive output samples of one chunk. HalfSnake of the
+// 3-branch mean is computed once per (time, channel) into LDS (with the 2-sample
+// causal halo), rounded to f16 like ggml's im2col, then each thread dots its 3
+// taps x 27 channels against the f16-rounded weights.
 __global__ __launch_bounds__(256) void post_conv_kernel(PostP p) {
-    const size_t total = (size_t)p.nchunk * p.T;
-    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (size_t)gridDim.x * 256) {
-        const int t = (int)(e % p.T);
-        const size_t cbase = (e / p.T) * p.T;
-        float acc = 0.f;
-        for (int k = 0; k < 3; ++k) {
-            const int ts = t - 2 + k;
-            if (ts < 0) continue;
-            const float *x = p.x + (cbase + ts) * 32, *xa = p.xa + (cbase + ts) * 32, *xb = p.xb + (cbase + ts) * 32;
-            for (int i = 0; i < 27; ++i) {
-                float v = ((x[i] + xa[i]) + xb[i]) * (1.0f / 3.0f);
-                v = half_snake(v, i, 13, 27, p.alpha);
-                acc += (float)(_Float16)v * (float)(_Float16)p.w[i * 3 + k];
-            }
+    __shared__ float hs[258][28];
+    __shared__ float wh[27 * 3];
+    const int tiles = (p.T + 255) / 256;
+    const int chunk = blockIdx.x / tiles, t0 = (blockIdx.x % tiles) * 256;
+    const size_t cbase = (size_t)chunk * p.T;
+    if (threadIdx.x < 81) wh[threadIdx.x] = (float)(_Float16)p.w[threadIdx.x];
+    for (int e = threadIdx.x; e < 258 * 27; e += 256) {
+        const int r = e / 27, i = e % 27, t = t0 - 2 + r;
+        float v = 0.f;
+        if (t >= 0 && t < p.T) {
+            const size_t o = (cbase + t) * 32 + i;
+            v = ((p.x[o] + p.xa[o]) + p.xb[o]) * (1.0f / 3.0f);
+            v = (float)(_Float16)half_snake(v, i, 13, 27, p.alpha);
         }
-        p.audio[e] = tanhf(acc + p.bias[0]);
+        hs[r][i] = v;
     }
+    __syncthreads();
+    const int t = t0 + threadIdx.x;
+    if (t >= p.T) return;
+    float acc = 0.f;
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int i = 0; i < 27; ++i) acc += hs[threadIdx.x + k][i] * wh[i * 3 + k];
+    p.audio[cbase + t] = tanhf(acc + p.bias[0]);
 }
 
 }  // namespace mpc
@@ -456,8 +467,7 @@ int codec_run(mp_codec *c, int nchunk, int F) {
         }
     }
     PostP pp{c->brb[0], c->brb[1], c->brb[2], c->post_alpha, c->post_w, c->post_b, c->audio, T, nchunk};
-    const size_t total = (size_t)nchunk * T;
-    hipLaunchKernelGGL(post_conv_kernel, dim3((int)std::min<size_t>((total + 255) / 256, 65536)), dim3(256), 0, s, pp);
+    hipLaunchKernelGGL(post_conv_kernel, dim3(nchunk * ((T + 255) / 256)), dim3(256), 0, s, pp);
     CHK(hipGetLastError());
     return MP_OK;
 }

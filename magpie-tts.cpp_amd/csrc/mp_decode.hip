@@ -43,6 +43,40 @@ __device__ __forceinline__ void pro_ln_vec(const float *x, const float *lnw, flo
     }
 }
 
+// Masked first-max argmax of slot b's logits (magpie.cpp:1133-1145, 1243-1259):
+// 2016 and 2018..2023 always forbidden, 2017 (EOS) too while step < 4 or in
+// fixed-length mode. Every thread returns the winner.
+__device__ __forceinline__ int block_masked_argmax(const GemvP &p, int b, float *red) {
+    const int tid = threadIdx.x;
+    const float *lg = p.logits + (size_t)b * VCB;
+    const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
+    constexpr int R = (VCB + MP_BLOCK - 1) / MP_BLOCK;
+    float lv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = tid + MP_BLOCK * r;
+        lv[r] = i < VCB ? lg[i] : -INFINITY;
+    }
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = tid + MP_BLOCK * r;
+        float v = lv[r];
+        if (i >= VCB || (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos))) v = -INFINITY;
+        argmax_merge(bv, bi, v, i);
+    }
+    wave_argmax(bv, bi);
+    if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
+    lds_sync();
+    float v0 = red[0];
+    int i0 = ((int *)red)[4];
+    for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
+    lds_sync();
+    if (i0 < 0 || i0 >= VCB) i0 = 0;  // all -inf / NaN: the reference's argmax stays 0
+    return i0;
+}
+
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
     const int tid = threadIdx.x;
@@ -93,42 +127,33 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         lds_sync();
     } else if constexpr (PRO == PRO_SA_COMBINE) {
         static_assert(K == D, "SA output is d_model wide");
-        // (1) stage every chunk's (max, sum) in LDS with one independent load per thread
-        const int nml = NB * NH * p.nch;
-        for (int i = tid; i < nml; i += MP_BLOCK) {
-            sc[2 * i] = p.part[(size_t)i * PART_STRIDE];
-            sc[2 * i + 1] = p.part[(size_t)i * PART_STRIDE + 1];
-        }
-        lds_sync();
-        // (2) per (slot, head): chunk weights w_c = exp(m_c - M) / sum_c exp(m_c - M) l_c
-        for (int bh = tid; bh < NB * NH; bh += MP_BLOCK) {
-            float M = -INFINITY;
-            for (int c = 0; c < p.nch; ++c) M = fmaxf(M, sc[2 * (bh * p.nch + c)]);
-            float den = 0.f;
-            for (int c = 0; c < p.nch; ++c) {
-                const float mc = sc[2 * (bh * p.nch + c)];
-                den += mc == -INFINITY ? 0.f : expf(mc - M) * sc[2 * (bh * p.nch + c) + 1];
-            }
-            const float inv = 1.0f / den;
-            for (int c = 0; c < p.nch; ++c) {
-                const float mc = sc[2 * (bh * p.nch + c)];
-                sc[2 * (bh * p.nch + c)] = mc == -INFINITY ? 0.f : expf(mc - M) * inv;
-            }
-        }
-        lds_sync();
-        // (3) act = sum_c w_c o_c : all chunk loads of a thread issued together
+        // One round trip: every thread loads (max, sum, o[d]) of all chunks of its
+        // heads at once, then combines them in registers:
+        // a[d] = sum_c e^(m_c - M) o_c[d] / sum_c e^(m_c - M) l_c
         for (int b = 0; b < NB; ++b)
 #pragma unroll
             for (int i = 0; i < K / MP_BLOCK; ++i) {
-                const int k = tid + MP_BLOCK * i, h = k / DH, d = k % DH, bh = b * NH + h;
-                const float *P = p.part + (size_t)bh * p.nch * PART_STRIDE + 16 + d;
-                float o[NCH_MAX];
+                const int k = tid + MP_BLOCK * i, h = k / DH, d = k % DH;
+                const float *P = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
+                float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
 #pragma unroll
-                for (int c = 0; c < NCH_MAX; ++c) o[c] = c < p.nch ? P[c * PART_STRIDE] : 0.f;
-                float a = 0.f;
+                for (int c = 0; c < NCH_MAX; ++c) {
+                    const bool ok = c < p.nch;
+                    mv[c] = ok ? P[c * PART_STRIDE] : -INFINITY;
+                    lv[c] = ok ? P[c * PART_STRIDE + 1] : 0.f;
+                    ov[c] = ok ? P[c * PART_STRIDE + 16 + d] : 0.f;
+                }
+                float M = -INFINITY;
 #pragma unroll
-                for (int c = 0; c < NCH_MAX; ++c) if (c < p.nch) a += sc[2 * (bh * p.nch + c)] * o[c];
-                act[b * K + k] = a;
+                for (int c = 0; c < NCH_MAX; ++c) M = fmaxf(M, mv[c]);
+                float num = 0.f, den = 0.f;
+#pragma unroll
+                for (int c = 0; c < NCH_MAX; ++c) {
+                    const float e = mv[c] == -INFINITY ? 0.f : expf(mv[c] - M);
+                    den += e * lv[c];
+                    num += e * ov[c];
+                }
+                act[b * K + k] = num / den;
             }
         lds_sync();
     } else if constexpr (PRO == PRO_XA) {
@@ -211,34 +236,25 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
     } else if constexpr (PRO == PRO_ARGMAX_EMB) {
         static_assert(K == D, "embedding is d_model wide");
         for (int b = 0; b < NB; ++b) {
-            const float *lg = p.logits + (size_t)b * VCB;
-            const bool forbid_eos = p.ignore_eos || p.step[b] < 4;  // min_generated_frames
-            float bv = -INFINITY;
-            int bi = 0x7fffffff;
-            float lv[(VCB + MP_BLOCK - 1) / MP_BLOCK];
-#pragma unroll
-            for (int r = 0; r < (VCB + MP_BLOCK - 1) / MP_BLOCK; ++r) {
-                const int i = tid + MP_BLOCK * r;
-                lv[r] = i < VCB ? lg[i] : -INFINITY;
-            }
-#pragma unroll
-            for (int r = 0; r < (VCB + MP_BLOCK - 1) / MP_BLOCK; ++r) {
-                const int i = tid + MP_BLOCK * r;
-                float v = lv[r];
-                if (i >= VCB || (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos))) v = -INFINITY;
-                argmax_merge(bv, bi, v, i);
-            }
-            wave_argmax(bv, bi);
-            if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
-            lds_sync();
-            float v0 = red[0];
-            int i0 = ((int *)red)[4];
-            for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
-            if (i0 < 0 || i0 >= VCB) i0 = 0;  // all -inf / NaN logits: reference argmax stays 0
-            lds_sync();
+            const int i0 = block_masked_argmax(p, b, red);
             if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb] = i0;
             const float *e = p.emb + ((size_t)p.cb * VCB + i0) * D;
             for (int k = tid; k < K; k += MP_BLOCK) act[b * K + k] = e[k];
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LTARG_LN) {
+        static_assert(K == LTD, "LT is 256 wide");
+        for (int b = 0; b < NB; ++b) {
+            const int code = block_masked_argmax(p, b, red);  // codebook cb-1's code
+            if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb - 1] = code;
+            const int k = tid;
+            const float X = p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+            if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X;
+            const float xv[1] = {X};
+            float mean, var;
+            block_meanvar<1>(xv, red, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
         }
         lds_sync();
     }
@@ -259,7 +275,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     using VT = typename vecf<VW>::T;
     constexpr int SC = (PRO == PRO_XA) ? TMAX_LIMIT
                        : (PRO == PRO_LT_ATTN) ? 16
-                       : (PRO == PRO_SA_COMBINE) ? 2 * NB * NH * NCH_MAX : 1;
+                       : 1;
     __shared__ __attribute__((aligned(16))) float act[NB * K];
     __shared__ float red[8 + 2 * DXA];
     __shared__ float sc[SC];
@@ -455,11 +471,12 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
     hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_RESID>(p, s); }      \
     hipError_t op_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_BIAS>(p, s); }         \
     hipError_t op_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
+    hipError_t op_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \
     hipError_t op_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
     hipError_t op_lt_c_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LN, EPI_GELU>(p, s); }         \
     hipError_t op_lt_d_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTF, PRO_PLAIN, EPI_ADD_STORE>(p, s); } \
     hipError_t op_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }      \
-    hipError_t op_lt_f_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_ARGMAX_EMB, EPI_BIAS>(p, s); }
+
 
 MP_DECODE_OPS(1)
 MP_DECODE_OPS(2)

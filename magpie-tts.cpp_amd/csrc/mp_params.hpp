@@ -32,6 +32,9 @@ enum Pro {
     PRO_LTX_LN = 5,     // X = s_cb + lt_pos[cb]; act = LN(X)*lnw       (1015-1034, 946-958)
     PRO_LT_ATTN = 6,    // act = causal 1x256 attention over LT positions 0..cb (965-966)
     PRO_ARGMAX_EMB = 7, // code = masked argmax(logits); act = audio_emb[cb][code] (1243-1291)
+    PRO_LTARG_LN = 8,   // code_{cb-1} = masked argmax(logits); X = P[cb-1][code] + lt_pos[cb];
+                        // act = LN(X)*lnw, with P[c][v] = in_proj(audio_emb[c][v]) + b
+                        // precomputed at load (1274-1313 depend only on (c, v))
 };
 enum Epi {
     EPI_STORE = 0,      // out = v
@@ -67,6 +70,7 @@ struct GemvP {
     const int *T;
     int Tmax, layer, nlayers;
     const float *lt_s;   // [B][9][256]
+    const float *ptab;   // [8][2024][256] in_proj(audio_emb) + b
     int cb;
     const float *lt_pos;
     float *ltX;

@@ -35,12 +35,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
                     const float4 v = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + lk);
                     a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
                 } else {
+                    // weights are tap-major [N][tap][Cin] (re-laid out at load), so a
+                    // 16-wide K step lies inside one tap: one float4 of input row t-2+tap
                     const int t = m % p.rows_per_utt;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int kk = k0 + lk + e, i = kk / TAPS, tap = kk % TAPS;
-                        const int st = t - (TAPS - 1) + tap;
-                        a[e] = st >= 0 ? p.A[(size_t)(m - (TAPS - 1) + tap) * p.lda + i] : 0.f;
+                    const int tap = k0 / p.lda, i = k0 % p.lda + lk;
+                    const int st = t - (TAPS - 1) + tap;
+                    if (st >= 0) {
+                        const float4 v = *(const float4 *)(p.A + (size_t)(m - (TAPS - 1) + tap) * p.lda + i);
+                        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
                     }
                 }
             }

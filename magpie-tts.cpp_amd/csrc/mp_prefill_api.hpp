@@ -22,7 +22,8 @@ struct GemmP {
     float *C;
     int ldc;
     int M, N, K;
-    int conv_taps;     // 0: plain A; 3: causal conv, A[m][i*3+k] = X[t-2+k][i] (1816-1866)
+    int conv_taps;     // 0: plain A; 3: causal conv, A[m][k*Cin+i] = X[t-2+k][i] (1816-1866),
+                       //    W re-laid out tap-major [N][k][Cin] at load
     int rows_per_utt;  // for (b, t) decomposition of a row
     const int *T;      // valid rows per utterance (conv zero padding / masking)
     float *kc, *vc;

@@ -33,8 +33,9 @@ using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
     hipError_t op_xo_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);               \
     hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
     hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
+    hipError_t op_lt_ag_##NB(const GemvP &, hipStream_t);                                                              \
     hipError_t op_lt_c_##NB(const GemvP &, hipStream_t); hipError_t op_lt_d_##NB(const GemvP &, hipStream_t);            \
-    hipError_t op_lt_e_##NB(const GemvP &, hipStream_t); hipError_t op_lt_f_##NB(const GemvP &, hipStream_t);
+    hipError_t op_lt_e_##NB(const GemvP &, hipStream_t);
 MP_DECL_OPS(1)
 MP_DECL_OPS(2)
 MP_DECL_OPS(4)
@@ -48,9 +49,9 @@ hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 namespace mp {
 
-struct OpTable { GemvFn qkv_embed, qkv, oproj, xq, xo, ff1, ff2, lt_in0, lt_a, lt_b, lt_c, lt_d, lt_e, lt_f; };
+struct OpTable { GemvFn qkv_embed, qkv, oproj, xq, xo, ff1, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
 #define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_xq_##NB, op_xo_##NB, op_ff1_##NB, op_ff2_##NB, \
-                       op_lt_in0_##NB, op_lt_a_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, op_lt_f_##NB }
+                       op_lt_in0_##NB, op_lt_a_##NB, op_lt_ag_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
 static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
 static const OpTable &table_for(int NB) { return kTables[NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : 3]; }
 
@@ -67,6 +68,7 @@ struct Model {
     std::vector<DecLayerW> dec;
     const float *lt_in_w, *lt_in_b, *lt_pos, *lt_norm_self, *lt_qkv, *lt_o, *lt_norm_ff, *lt_ff1, *lt_ff2, *lt_out_w,
         *lt_out_b;
+    float *lt_ptab = nullptr;  // [8][2024][256] = in_proj(audio_emb[c][v]) + b, built at load
     float *arena = nullptr;
     size_t arena_bytes = 0;
 };
@@ -271,9 +273,19 @@ int load_model(mp_dev *dev, const char *path) {
     m.arena_bytes = total;
     std::vector<float> host;
     size_t off = 0;
+    std::vector<float> tmp;
     auto upload = [&](const mp::GgufTensor *t, float *dst) -> int {
         host.resize((size_t)t->nelements());
         if (!g.to_f32(*t, host.data())) return fail(dev, MP_ERR_FORMAT, "unsupported tensor type in " + t->name);
+        if (t->n_dims == 3 && t->ne[0] == 3 && t->name.rfind("encoder.layers.", 0) == 0) {
+            // causal k=3 conv weight [out][in][k] -> tap-major [out][k][in] (mp_prefill.hip loader)
+            const int64_t K = 3, Cin = t->ne[1], Co = t->ne[2];
+            tmp.resize(host.size());
+            for (int64_t o = 0; o < Co; ++o)
+                for (int64_t i = 0; i < Cin; ++i)
+                    for (int64_t k = 0; k < K; ++k) tmp[(o * K + k) * Cin + i] = host[(o * Cin + i) * K + k];
+            host.swap(tmp);
+        }
         HIPCHK(hipMemcpy(dst, host.data(), host.size() * 4, hipMemcpyHostToDevice));
         return MP_OK;
     };
@@ -290,6 +302,17 @@ int load_model(mp_dev *dev, const char *path) {
             if (int rc = upload(g.find(grouped[k][c]), base + (size_t)c * gsize[k])) return rc;
         *gdst[k] = base;
         off += align_up((size_t)gsize[k] * 8 * 4);
+    }
+    // P[c][v] = in_proj(audio_emb[c][v]) + b: the LT's per-codebook re-embedding
+    // (magpie.cpp:1274-1313) depends only on (c, v) -> one GEMM at load time.
+    if (m.lt_ptab) { hipFree(m.lt_ptab); m.lt_ptab = nullptr; }
+    HIPCHK(hipMalloc(&m.lt_ptab, (size_t)8 * 2024 * 256 * 4));
+    {
+        mp::GemmP gp{};
+        gp.A = m.audio_emb; gp.lda = 768; gp.W = m.lt_in_w; gp.bias = m.lt_in_b; gp.C = m.lt_ptab; gp.ldc = 256;
+        gp.M = 8 * 2024; gp.N = 256; gp.K = 768; gp.rows_per_utt = 8 * 2024;
+        HIPCHK(mp::pre_gemm(gp, mp::GE_STORE, dev->stream));
+        HIPCHK(hipStreamSynchronize(dev->stream));
     }
     dev->loaded = true;
     return MP_OK;
@@ -412,11 +435,14 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         if ((rc = run("lt_in0", tb.lt_in0, g, F * (256.0 * 768 + act * (768 + 768 + 256)))) != MP_OK) return rc;
     }
     for (int cb = 0; cb < 8; ++cb) {
+        // cb > 0: codebook cb-1's masked argmax + table gather fused into this prologue
         mp::GemvP g = gemv_base(dev);
         g.cb = cb;
         g.W = m.lt_qkv; g.N = 768; g.lt_s = dev->lt_s; g.lt_pos = m.lt_pos; g.ltX = dev->ltX; g.lnw = m.lt_norm_self;
         g.lq = dev->ltq; g.lk = dev->ltk; g.lv = dev->ltv;
-        if ((rc = run("lt_a", tb.lt_a, g, F * (768.0 * 256 + act * (256 * 3 + 768)))) != MP_OK) return rc;
+        if (cb > 0) { g.logits = dev->logits; g.codes_cur = dev->codes_cur; g.ptab = m.lt_ptab; }
+        if ((rc = run(cb == 0 ? "lt_a" : "lt_ag", cb == 0 ? tb.lt_a : tb.lt_ag, g,
+                      F * (768.0 * 256 + act * (256 * 3 + 768 + (cb > 0 ? 2024 + 256 : 256))))) != MP_OK) return rc;
         g = gemv_base(dev); g.cb = cb;
         g.W = m.lt_o; g.N = 256; g.ltq = dev->ltq; g.ltk = dev->ltk; g.ltv = dev->ltv; g.out = dev->ltY; g.out_ld = 256;
         g.addsrc = dev->ltX;
@@ -431,12 +457,6 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024; g.bias = m.lt_out_b + (size_t)cb * 2024;
         g.src = dev->lty2; g.src_ld = 256; g.out = dev->logits; g.out_ld = 2024;
         if ((rc = run("lt_e", tb.lt_e, g, F * (2024.0 * 256 + 2024 + act * (256 + 2024)))) != MP_OK) return rc;
-        if (cb < 7) {
-            g = gemv_base(dev); g.cb = cb;
-            g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.logits = dev->logits; g.codes_cur = dev->codes_cur;
-            g.emb = m.audio_emb; g.out = dev->lt_s + (size_t)(cb + 1) * 256; g.out_ld = 9 * 256;
-            if ((rc = run("lt_f", tb.lt_f, g, F * (256.0 * 768 + act * (2024 + 768 + 256)))) != MP_OK) return rc;
-        }
     }
     mp::FinP f{dev->logits, dev->codes_cur, dev->codes_prev, dev->codes_out, dev->step, dev->pos, dev->done,
                dev->nframes, dev->ndone, dev->max_steps, dev->params.ignore_eos, m.audio_bos, m.audio_eos, NB};
@@ -585,6 +605,7 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->stream) hipStreamSynchronize(dev->stream);
     free_batch(dev);
     if (dev->m.arena) hipFree(dev->m.arena);
+    if (dev->m.lt_ptab) hipFree(dev->m.lt_ptab);
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
     if (dev->stream) hipStreamDestroy(dev->stream);
     delete dev;

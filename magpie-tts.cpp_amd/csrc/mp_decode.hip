@@ -401,6 +401,77 @@ __global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
     }
 }
 
+// ---------------------------------------------------------------- fused XA
+// grid (768/64, B): every workgroup recomputes LN(x) and all T scores (K' rows
+// are L2-resident after the first workgroup), then owns 64 output dims.
+__global__ __launch_bounds__(MP_BLOCK) void xa_fused_kernel(XaP p) {
+    __shared__ __attribute__((aligned(16))) float act[D];
+    __shared__ float red[8];
+    __shared__ float sc[TMAX_LIMIT];
+    __shared__ float part[MP_NWAVES][64];
+    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int d0 = blockIdx.x * 64;
+    const int Tb = p.T[b];
+    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
+    const float *Kp = p.kp + base, *Vp = p.vp + base;
+    // LN(x) (magpie.cpp:3513)
+    {
+        float v[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = p.x[(size_t)b * D + tid + MP_BLOCK * i];
+        float mean, var;
+        block_meanvar<3>(v, red, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) act[tid + MP_BLOCK * i] = ((v[i] - mean) * rstd) * p.lnw[tid + MP_BLOCK * i];
+    }
+    lds_sync();
+    const float4 a0 = *(const float4 *)(act + 4 * lane), a1 = *(const float4 *)(act + 256 + 4 * lane),
+                 a2 = *(const float4 *)(act + 512 + 4 * lane);
+    const float scale = 1.0f / sqrtf((float)DXA);
+    // scores: wave w takes rows w, w+4, ...; 4 rows (12 float4 per lane) in flight
+    for (int tb = w; tb < Tb; tb += 16) {
+        float4 k[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = tb + 4 * u;
+            const float *kr = Kp + (size_t)(t < Tb ? t : 0) * D;
+            k[u][0] = *(const float4 *)(kr + 4 * lane);
+            k[u][1] = *(const float4 *)(kr + 256 + 4 * lane);
+            k[u][2] = *(const float4 *)(kr + 512 + 4 * lane);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = tb + 4 * u;
+            const float sv = wave_sum(dotv(k[u][0], a0) + dotv(k[u][1], a1) + dotv(k[u][2], a2));
+            if (lane == 0 && t < Tb) sc[t] = sv * scale;
+        }
+    }
+    lds_sync();
+    float m = -INFINITY;
+    for (int t = tid; t < Tb; t += MP_BLOCK) m = fmaxf(m, sc[t]);
+    m = block_max(m, red);
+    float l = 0.f;
+    for (int t = tid; t < Tb; t += MP_BLOCK) { const float e = expf(sc[t] - m); sc[t] = e; l += e; }
+    l = block_sum(l, red);
+    // out[d] = sum_t e_t V'_t[d] / l for the workgroup's 64 dims; 4 time groups
+    float acc = 0.f;
+#pragma unroll 8
+    for (int t = w; t < Tb; t += MP_NWAVES) acc += sc[t] * Vp[(size_t)t * D + d0 + lane];
+    part[w][lane] = acc;
+    lds_sync();
+    if (tid < 64) {
+        const float o = ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid])) / l;
+        p.x_out[(size_t)b * D + d0 + tid] = o + p.x[(size_t)b * D + d0 + tid];
+    }
+}
+
+hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
+    if (!p.x || !p.x_out || !p.lnw || !p.kp || !p.vp || !p.T || p.Tmax < 1 || p.Tmax > TMAX_LIMIT) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xa_fused_kernel, dim3(D / 64, B), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- frame finalize
 // Codebook 7's masked argmax, then the reference's loop bookkeeping
 // (magpie.cpp:4340-4358): stop on EOS in any codebook (frame not emitted), else
@@ -451,8 +522,34 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
 }
 
 // ---------------------------------------------------------------- host launchers
+// Host-side check that every pointer the (PRO, EPI) pair dereferences is set:
+// a mismatch between an op's compile-time epilogue and its arguments must fail
+// at launch, not fault on the device.
+template <int PRO, int EPI>
+static bool gemv_args_ok(const GemvP &p) {
+    if (!p.W || p.N <= 0) return false;
+    bool ok = true;
+    if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
+    if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
+    if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
+    if constexpr (PRO == PRO_SA_COMBINE) ok &= p.part && p.nch > 0 && p.nch <= NCH_MAX;
+    if constexpr (PRO == PRO_XA) ok &= p.qx && p.xak && p.xav && p.T;
+    if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
+    if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
+    if constexpr (PRO == PRO_ARGMAX_EMB) ok &= p.logits && p.codes_cur && p.emb && p.step;
+    if constexpr (PRO == PRO_LTARG_LN) ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step;
+    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
+    if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
+    if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
+    if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
+    if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
+    return ok;
+}
+
 template <int NB, int RW, int K, int PRO, int EPI>
 static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
+    if (!gemv_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
     const int rows_per_block = MP_NWAVES * RW;
     const int grid = (p.N + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL((gemv_kernel<NB, RW, K, PRO, EPI>), dim3(grid), dim3(MP_BLOCK), 0, s, p);
@@ -468,7 +565,7 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
     hipError_t op_xq_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_STORE>(p, s); }            \
     hipError_t op_xo_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DXA, PRO_XA, EPI_RESID>(p, s); }          \
     hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_GELU>(p, s); }            \
-    hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_RESID>(p, s); }      \
+    hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \
     hipError_t op_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_BIAS>(p, s); }         \
     hipError_t op_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
     hipError_t op_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \
@@ -484,6 +581,7 @@ MP_DECODE_OPS(4)
 MP_DECODE_OPS(8)
 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
+    if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || p.nch < 1 || p.nch * SA_CHUNK > p.max_seq) return hipErrorInvalidValue;
     hipLaunchKernelGGL(sa_attn_partial_kernel, dim3(p.nch, NH, B), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }

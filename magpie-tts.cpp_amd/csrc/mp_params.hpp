@@ -99,6 +99,20 @@ struct FinP {
     int max_steps, ignore_eos, audio_bos, audio_eos, nslots;
 };
 
+// Fused cross-attention for one decode step (replaces the xq GEMV + XA attention
+// + xo GEMV). With K'_t = W_q^T K_t and V'_t = W_o V_t precomputed per utterance
+// and layer:  x += sum_t softmax_t(K'_t . LN(x) / sqrt(128)) V'_t
+// (= o_net(attn(q_net(LN(x)), K, V)), magpie.cpp:1713-1767, by associativity).
+struct XaP {
+    const float *x;        // [B][768] residual in
+    float *x_out;          // [B][768] = x + XA(x) (separate buffer: every workgroup reads all of x)
+    const float *lnw;      // norm_xattn_query
+    float eps;
+    const float *kp, *vp;  // K', V': [B][L][Tmax][768]
+    const int *T;
+    int Tmax, layer, nlayers;
+};
+
 struct AttnP {  // split-K decode self-attention (one query per utterance)
     const float *q;
     const float *kc, *vc;

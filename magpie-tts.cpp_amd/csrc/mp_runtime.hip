@@ -41,6 +41,7 @@ MP_DECL_OPS(2)
 MP_DECL_OPS(4)
 MP_DECL_OPS(8)
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
+hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 }  // namespace mp
@@ -69,11 +70,12 @@ struct Model {
     const float *lt_in_w, *lt_in_b, *lt_pos, *lt_norm_self, *lt_qkv, *lt_o, *lt_norm_ff, *lt_ff1, *lt_ff2, *lt_out_w,
         *lt_out_b;
     float *lt_ptab = nullptr;  // [8][2024][256] = in_proj(audio_emb[c][v]) + b, built at load
+    std::vector<float *> xq_t;  // per layer W_q^T [768][128] (for K' = K W_q)
     float *arena = nullptr;
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3 };
 struct OpRec {
     std::string name;
     int kind;
@@ -81,6 +83,7 @@ struct OpRec {
     GemvP g;
     AttnP a;
     FinP f;
+    XaP x;
     int B;
     double bytes;
 };
@@ -98,7 +101,7 @@ struct mp_dev {
     mp_params params{};
     // device state (one allocation per buffer, sized for the configuration)
     std::vector<void *> allocs;
-    float *x = nullptr, *q = nullptr, *part = nullptr, *qx = nullptr, *h = nullptr, *hidden = nullptr;
+    float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *part = nullptr, *qx = nullptr, *h = nullptr, *hidden = nullptr;
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
@@ -303,6 +306,19 @@ int load_model(mp_dev *dev, const char *path) {
         *gdst[k] = base;
         off += align_up((size_t)gsize[k] * 8 * 4);
     }
+    // W_q^T per decoder layer (for the per-utterance K' = K W_q of the fused XA)
+    for (float *p : m.xq_t) hipFree(p);
+    m.xq_t.assign(m.dec_layers, nullptr);
+    {
+        std::vector<float> wq((size_t)128 * 768), wt((size_t)768 * 128);
+        for (int l = 0; l < m.dec_layers; ++l) {
+            HIPCHK(hipMemcpy(wq.data(), m.dec[l].xq, wq.size() * 4, hipMemcpyDeviceToHost));
+            for (int j = 0; j < 128; ++j)
+                for (int n = 0; n < 768; ++n) wt[(size_t)n * 128 + j] = wq[(size_t)j * 768 + n];
+            HIPCHK(hipMalloc(&m.xq_t[l], wt.size() * 4));
+            HIPCHK(hipMemcpy(m.xq_t[l], wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
+        }
+    }
     // P[c][v] = in_proj(audio_emb[c][v]) + b: the LT's per-codebook re-embedding
     // (magpie.cpp:1274-1313) depends only on (c, v) -> one GEMM at load time.
     if (m.lt_ptab) { hipFree(m.lt_ptab); m.lt_ptab = nullptr; }
@@ -333,7 +349,8 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     const size_t D = 768;
     int rc = MP_OK;
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
-    A(x, NB * D); A(q, NB * D); A(part, (size_t)NB * 12 * dev->nch * mp::PART_STRIDE); A(qx, NB * 128);
+    A(x, NB * D); A(x2, NB * D); A(q, NB * D);
+    A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(part, (size_t)NB * 12 * dev->nch * mp::PART_STRIDE); A(qx, NB * 128);
     A(h, NB * 3072); A(hidden, NB * D);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -409,21 +426,22 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.N = 768; g.part = dev->part; g.nch = dev->nch; g.resid = dev->x;
         if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768 + act * (768 * 2 + 12.0 * dev->nch * 80)))) != MP_OK) return rc;
-        // LN + XA query (1733)
-        g = gemv_base(dev); g.layer = l;
-        g.W = W.xq; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768; g.out = dev->qx; g.out_ld = 128;
-        if ((rc = run("xq", tb.xq, g, F * (128.0 * 768 + act * (768 + 128)))) != MP_OK) return rc;
-        // XA attention (prologue) + XA out-proj + residual (1742-1764, 3519)
-        g = gemv_base(dev); g.layer = l;
-        g.W = W.xo; g.N = 768; g.qx = dev->qx; g.xak = dev->xak; g.xav = dev->xav; g.resid = dev->x;
-        if ((rc = run("xo", tb.xo, g, F * (768.0 * 128 + act * (128 + 2.0 * 128 * dev->Tmax + 2 * 768)))) != MP_OK) return rc;
+        // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
+        mp::XaP xp{dev->x, dev->x2, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
+        if (record) {
+            mp::OpRec r{};
+            r.name = "xa"; r.kind = mp::K_XA; r.x = xp; r.B = NB;
+            r.bytes = F * act * (768.0 * 2 + 2.0 * 768 * dev->Tmax);
+            dev->ops.push_back(r);
+        }
+        HIPCHK(mp::op_xa(xp, NB, s));
         // LN + FFN up + GELU (1796-1799)
         g = gemv_base(dev); g.layer = l;
-        g.W = W.ff1; g.N = 3072; g.lnw = W.norm_ff; g.src = dev->x; g.src_ld = 768; g.out = dev->h; g.out_ld = 3072;
+        g.W = W.ff1; g.N = 3072; g.lnw = W.norm_ff; g.src = dev->x2; g.src_ld = 768; g.out = dev->h; g.out_ld = 3072;
         if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768 + act * (768 + 3072)))) != MP_OK) return rc;
-        // FFN down + residual (1805, 3525)
+        // FFN down + residual (1805, 3525): x = x2 + W2 h
         g = gemv_base(dev); g.layer = l;
-        g.W = W.ff2; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.resid = dev->x;
+        g.W = W.ff2; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.out = dev->x; g.out_ld = 768; g.addsrc = dev->x2;
         if ((rc = run("ff2", tb.ff2, g, F * (768.0 * 3072 + act * (3072 + 2 * 768)))) != MP_OK) return rc;
     }
     // final LN -> hidden (4394) fused into LT in_proj (1162-1163)
@@ -513,6 +531,17 @@ int run_preamble(mp_dev *dev) {
         gp.T = dev->T; gp.xak = dev->xak; gp.xav = dev->xav; gp.layer = l; gp.nlayers = L; gp.Tmax = Tmax;
         HIPCHK(pre_gemm(gp, GE_XAKV, s));
     }
+    // --- K'_t = W_q^T K_t, V'_t = W_o V_t per utterance and layer (decode-time fused XA)
+    for (int b = 0; b < NB; ++b)
+        for (int l = 0; l < L; ++l) {
+            const size_t xo = ((size_t)(b * L + l) * Tmax) * 128, po = ((size_t)(b * L + l) * Tmax) * 768;
+            GemmP gp{};
+            gp.A = dev->xak + xo; gp.lda = 128; gp.W = m.xq_t[l]; gp.C = dev->kp + po; gp.ldc = 768;
+            gp.M = Tmax; gp.N = 768; gp.K = 128; gp.rows_per_utt = Tmax;
+            HIPCHK(pre_gemm(gp, GE_STORE, s));
+            gp.A = dev->xav + xo; gp.W = m.dec[l].xo; gp.C = dev->vp + po;
+            HIPCHK(pre_gemm(gp, GE_STORE, s));
+        }
     // --- baked context + 110-frame causal prefill (3991-4060, 4167-4238)
     const int Mc = NB * CTX;
     HIPCHK(pre_embed_context(dev->spk, NB, m.baked, m.dec_pos, dev->pX, s));
@@ -606,6 +635,7 @@ void mp_hip_free(mp_dev *dev) {
     free_batch(dev);
     if (dev->m.arena) hipFree(dev->m.arena);
     if (dev->m.lt_ptab) hipFree(dev->m.lt_ptab);
+    for (float *p : dev->m.xq_t) hipFree(p);
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
     if (dev->stream) hipStreamDestroy(dev->stream);
     delete dev;
@@ -792,6 +822,11 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     auto launch = [&]() -> hipError_t {
         if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
         if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
+        if (r.kind == mp::K_XA) {
+            mp::XaP xp = r.x;
+            xp.x_out = dev->q;  // scratch: timing must not disturb the residual stream
+            return mp::op_xa(xp, r.B, dev->stream);
+        }
         return hipErrorInvalidValue;
     };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");

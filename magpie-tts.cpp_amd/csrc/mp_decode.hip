@@ -77,6 +77,32 @@ __device__ __forceinline__ int block_masked_argmax(const GemvP &p, int b, float 
     return i0;
 }
 
+// Wave-level variant of the masked argmax (one wave owns one slot).
+__device__ __forceinline__ int wave_masked_argmax(const GemvP &p, int b) {
+    const int lane = threadIdx.x & 63;
+    const float *lg = p.logits + (size_t)b * VCB;
+    const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
+    constexpr int R = (VCB + 63) / 64;
+    float lv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        lv[r] = i < VCB ? lg[i] : -INFINITY;
+    }
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        float v = lv[r];
+        if (i >= VCB || (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos))) v = -INFINITY;
+        argmax_merge(bv, bi, v, i);
+    }
+    wave_argmax(bv, bi);
+    if (bi < 0 || bi >= VCB) bi = 0;
+    return bi;
+}
+
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
     const int tid = threadIdx.x;
@@ -84,6 +110,29 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         for (int b = 0; b < NB; ++b)
             for (int k = tid * 4; k < K; k += MP_BLOCK * 4)
                 *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
+        lds_sync();
+    } else if constexpr (PRO == PRO_LN && NB >= 2) {
+        // batched: wave w owns slots w, w+4 (DPP-only statistics, one barrier)
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            constexpr int PER = K / 64;
+            float v[PER];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) v[i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
+            float mean, var;
+            wave_meanvar<PER>(v, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            const bool st = p.hidden_out && blockIdx.x == 0;
+            const int s = (p.trace && blockIdx.x == 0) ? p.step[b] : 0;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int k = lane + 64 * i;
+                const float y = ((v[i] - mean) * rstd) * p.lnw[k];
+                act[b * K + k] = y;
+                if (st) p.hidden_out[(size_t)b * K + k] = y;
+                if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[((size_t)b * p.trace_steps + s) * K + k] = y;
+            }
+        }
         lds_sync();
     } else if constexpr (PRO == PRO_LN) {
         for (int b = 0; b < NB; ++b) {
@@ -96,6 +145,32 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 if (s < p.trace_steps)
                     for (int k = tid; k < K; k += MP_BLOCK)
                         p.trace[((size_t)b * p.trace_steps + s) * K + k] = act[b * K + k];
+            }
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_EMBED_LN && NB >= 2) {
+        static_assert(K == D, "embed prologue is d_model wide");
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            const int *c = p.codes + b * NCB;
+            const int ps = p.pos[b];
+            float x[K / 64];
+#pragma unroll
+            for (int i = 0; i < K / 64; ++i) {
+                const int k = lane + 64 * i;
+                float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
+#pragma unroll
+                for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
+                x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
+                if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
+            }
+            float mean, var;
+            wave_meanvar<K / 64>(x, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+            for (int i = 0; i < K / 64; ++i) {
+                const int k = lane + 64 * i;
+                act[b * K + k] = ((x[i] - mean) * rstd) * p.lnw[k];
             }
         }
         lds_sync();
@@ -197,6 +272,70 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             if (tid < DXA) act[b * K + tid] = (red[8 + tid] + red[8 + DXA + tid]) / l;
             lds_sync();
         }
+    } else if constexpr (PRO == PRO_LTX_LN && NB >= 2) {
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            float X[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = lane + 64 * i;
+                X[i] = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+                if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X[i];
+            }
+            float mean, var;
+            wave_meanvar<4>(X, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LTARG_LN && NB >= 2) {
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            const int code = wave_masked_argmax(p, b);
+            if (blockIdx.x == 0 && lane == 0) p.codes_cur[b * NCB + p.cb - 1] = code;
+            float X[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = lane + 64 * i;
+                X[i] = p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+                if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X[i];
+            }
+            float mean, var;
+            wave_meanvar<4>(X, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LT_ATTN && NB >= 2) {
+        const int lane = tid & 63, w = tid >> 6;
+        const int nk = p.cb + 1;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            const float4 q4 = *(const float4 *)(p.ltq + (size_t)b * LTD + 4 * lane);
+            float sj[NCB];
+#pragma unroll
+            for (int j = 0; j < NCB; ++j)
+                sj[j] = j < nk ? wave_sum(dotv(q4, *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane))) *
+                                     (1.0f / 16.0f)
+                               : -INFINITY;
+            float m = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < NCB; ++j) m = fmaxf(m, sj[j]);
+            float l = 0.f;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < NCB; ++j) {
+                if (j >= nk) break;
+                const float e = expf(sj[j] - m);
+                l += e;
+                const float4 v4 = *(const float4 *)(p.ltv + ((size_t)b * NCB + j) * LTD + 4 * lane);
+                a.x += e * v4.x; a.y += e * v4.y; a.z += e * v4.z; a.w += e * v4.w;
+            }
+            const float il = 1.0f / l;
+            *(float4 *)(act + b * K + 4 * lane) = make_float4(a.x * il, a.y * il, a.z * il, a.w * il);
+        }
+        lds_sync();
     } else if constexpr (PRO == PRO_LTX_LN) {
         static_assert(K == LTD, "LT is 256 wide");
         for (int b = 0; b < NB; ++b) {
@@ -401,6 +540,39 @@ __global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
     }
 }
 
+// ---------------------------------------------------------------- SA combine (NB > 1)
+// One wave per (head, slot): a[d] = sum_c e^(m_c - M) o_c[d] / sum_c e^(m_c - M) l_c.
+// At batch > 1 this runs once instead of redundantly in every O-proj workgroup.
+__global__ __launch_bounds__(64) void sa_combine_kernel(const float *part, int nch, float *out) {
+    const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+    const float *P = part + (size_t)(b * NH + h) * nch * PART_STRIDE;
+    float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
+#pragma unroll
+    for (int c = 0; c < NCH_MAX; ++c) {
+        const bool ok = c < nch;
+        mv[c] = ok ? P[c * PART_STRIDE] : -INFINITY;
+        lv[c] = ok ? P[c * PART_STRIDE + 1] : 0.f;
+        ov[c] = ok ? P[c * PART_STRIDE + 16 + d] : 0.f;
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < NCH_MAX; ++c) M = fmaxf(M, mv[c]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH_MAX; ++c) {
+        const float e = mv[c] == -INFINITY ? 0.f : expf(mv[c] - M);
+        den += e * lv[c];
+        num += e * ov[c];
+    }
+    out[(size_t)b * D + h * DH + d] = num / den;
+}
+
+hipError_t op_sa_combine(const float *part, int nch, float *out, int B, hipStream_t s) {
+    if (!part || !out || nch < 1 || nch > NCH_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sa_combine_kernel, dim3(NH, B), dim3(64), 0, s, part, nch, out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- fused XA
 // grid (768/64, B): every workgroup recomputes LN(x) and all T scores (K' rows
 // are L2-resident after the first workgroup), then owns 64 output dims.
@@ -562,6 +734,7 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
     hipError_t op_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_SA_COMBINE, EPI_RESID>(p, s); } \
+    hipError_t op_oprojp_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_PLAIN, EPI_RESID>(p, s); }   \
     hipError_t op_xq_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_STORE>(p, s); }            \
     hipError_t op_xo_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DXA, PRO_XA, EPI_RESID>(p, s); }          \
     hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_GELU>(p, s); }            \

@@ -126,6 +126,34 @@ __device__ __forceinline__ void block_meanvar(const float (&v)[PER], float *red,
     var = Q * (1.0f / (4.f * nw));
 }
 
+// Wave-level LayerNorm statistics of 64*PER elements (PER per lane), same
+// pairwise (mean, M2) combination as block_meanvar; uniform result, no barrier.
+template <int PER>
+__device__ __forceinline__ void wave_meanvar(const float (&v)[PER], float &mean, float &var) {
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) m += v[i];
+    m *= 1.0f / PER;
+    float M2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) { const float d = v[i] - m; M2 += d * d; }
+    float n = (float)PER;
+    auto comb = [&](float mb, float M2b) {
+        const float d = mb - m;
+        m = m + 0.5f * d;
+        M2 = M2 + M2b + d * d * (0.5f * n);
+        n *= 2.f;
+    };
+    comb(dpp_mov<0xB1>(m), dpp_mov<0xB1>(M2));
+    comb(dpp_mov<0x4E>(m), dpp_mov<0x4E>(M2));
+    comb(dpp_mov<0x141>(m), dpp_mov<0x141>(M2));
+    comb(dpp_mov<0x140>(m), dpp_mov<0x140>(M2));
+    comb(dpp_mov<0x142, 0xA>(m), dpp_mov<0x142, 0xA>(M2));
+    comb(dpp_mov<0x143, 0xC>(m), dpp_mov<0x143, 0xC>(M2));
+    mean = bcast_lane63(m);
+    var = bcast_lane63(M2) * (1.0f / (64.f * PER));
+}
+
 // (value, index) argmax with the reference's tie rule: the FIRST maximal index
 // wins (strict '>' scan from index 0, magpie.cpp:1250-1258).
 __device__ __forceinline__ void argmax_merge(float &v, int &i, float v2, int i2) {

@@ -33,7 +33,7 @@ using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
     hipError_t op_xo_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);               \
     hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
     hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
-    hipError_t op_lt_ag_##NB(const GemvP &, hipStream_t);                                                              \
+    hipError_t op_lt_ag_##NB(const GemvP &, hipStream_t); hipError_t op_oprojp_##NB(const GemvP &, hipStream_t);        \
     hipError_t op_lt_c_##NB(const GemvP &, hipStream_t); hipError_t op_lt_d_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_lt_e_##NB(const GemvP &, hipStream_t);
 MP_DECL_OPS(1)
@@ -42,6 +42,7 @@ MP_DECL_OPS(4)
 MP_DECL_OPS(8)
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
+hipError_t op_sa_combine(const float *, int, float *, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 }  // namespace mp
@@ -50,8 +51,8 @@ hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 namespace mp {
 
-struct OpTable { GemvFn qkv_embed, qkv, oproj, xq, xo, ff1, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
-#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_xq_##NB, op_xo_##NB, op_ff1_##NB, op_ff2_##NB, \
+struct OpTable { GemvFn qkv_embed, qkv, oproj, oprojp, ff1, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
+#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_oprojp_##NB, op_ff1_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_ag_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
 static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
 static const OpTable &table_for(int NB) { return kTables[NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : 3]; }
@@ -75,7 +76,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_COMB = 4 };
 struct OpRec {
     std::string name;
     int kind;
@@ -422,10 +423,23 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             dev->ops.push_back(r);
         }
         HIPCHK(mp::op_sa_attn(a, NB, s));
-        // O-proj + residual, combine fused in the prologue (3479, 3509)
+        // O-proj + residual (3479, 3509). Batch 1: chunk combine fused in the
+        // prologue; batch > 1: one combine pass, then a plain GEMV.
         g = gemv_base(dev); g.layer = l;
-        g.W = W.o; g.N = 768; g.part = dev->part; g.nch = dev->nch; g.resid = dev->x;
-        if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768 + act * (768 * 2 + 12.0 * dev->nch * 80)))) != MP_OK) return rc;
+        g.W = W.o; g.N = 768; g.resid = dev->x;
+        if (NB == 1) {
+            g.part = dev->part; g.nch = dev->nch;
+            if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768 + act * (768 * 2 + 12.0 * dev->nch * 80)))) != MP_OK) return rc;
+        } else {
+            if (record) {
+                mp::OpRec r{};
+                r.name = "sa_combine"; r.kind = mp::K_COMB; r.B = NB; r.bytes = F * act * (12.0 * dev->nch * 80 + 768);
+                dev->ops.push_back(r);
+            }
+            HIPCHK(mp::op_sa_combine(dev->part, dev->nch, dev->q, NB, s));  // q is free once attention ran
+            g.src = dev->q; g.src_ld = 768;
+            if ((rc = run("oproj", tb.oprojp, g, F * (768.0 * 768 + act * 768 * 3))) != MP_OK) return rc;
+        }
         // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
         mp::XaP xp{dev->x, dev->x2, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
         if (record) {
@@ -822,6 +836,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     auto launch = [&]() -> hipError_t {
         if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
         if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
+        if (r.kind == mp::K_COMB) return mp::op_sa_combine(dev->part, dev->nch, dev->h, r.B, dev->stream);
         if (r.kind == mp::K_XA) {
             mp::XaP xp = r.x;
             xp.x_out = dev->q;  // scratch: timing must not disturb the residual stream

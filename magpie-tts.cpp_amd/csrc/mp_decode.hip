@@ -103,6 +103,123 @@ __device__ __forceinline__ int wave_masked_argmax(const GemvP &p, int b) {
     return bi;
 }
 
+// One wave picks slot b's code for codebook `cb` of this frame: masked first-max
+// argmax (always, for EOS detection, magpie.cpp:1250-1259), and at temperature
+// >= 0.01 a top-k draw with the reference's sample_top_k arithmetic
+// (magpie.cpp:1072-1109): the k largest masked logits in descending order (ties by
+// ascending index), p_i = exp((l_i - l_max) / T) summed sequentially, normalised,
+// and the first i with u < cumsum_i (fallback: the k-th). Radix-select finds the
+// k-th key, a ballot compaction gathers the k candidates into LDS, a counting rank
+// orders them, lane 0 runs the two sequential float loops. scratch: 2*VCB floats.
+__device__ int wave_pick(const float *lg, bool forbid_eos, int audio_bos, int audio_eos, const Sampling &smp,
+                         int stream, int step, int cb, float *scratch, int &amax) {
+    const int lane = threadIdx.x & 63;
+    constexpr int R = (VCB + 63) / 64;
+    float lv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        lv[r] = i < VCB ? lg[i] : -INFINITY;
+    }
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        if (i >= VCB || (i >= audio_bos && i <= audio_bos + 7 && (i != audio_eos || forbid_eos))) lv[r] = -INFINITY;
+        argmax_merge(bv, bi, lv[r], i);
+    }
+    wave_argmax(bv, bi);
+    if (bi < 0 || bi >= VCB) bi = 0;
+    amax = bi;
+    if (!smp.on) return bi;
+    const float temp = smp.cfg->temperature;
+    const float M = bv;
+    const int k = min(max(smp.cfg->top_k, 1), VCB);
+    // order-preserving keys; padding lanes get 0 (below every real key)
+    unsigned key[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const unsigned u = __float_as_uint(lv[r]);
+        key[r] = (lane + 64 * r) < VCB ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0u;
+    }
+    unsigned t = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = t | (1u << bit);
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) c += key[r] >= cand;
+        if ((int)wave_sum((float)c) >= k) t = cand;
+    }
+    int cgt = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) cgt += key[r] > t;
+    const int need = k - (int)wave_sum((float)cgt);
+    float *sv = scratch;
+    int *si = (int *)(scratch + VCB);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int ties = 0, base = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const bool tie = key[r] == t;
+        const unsigned long long bt = __ballot(tie);
+        const bool sel = key[r] > t || (tie && ties + __popcll(bt & below) < need);
+        ties += __popcll(bt);
+        const unsigned long long bs = __ballot(sel);
+        if (sel) {
+            const int q = base + __popcll(bs & below);
+            sv[q] = lv[r];
+            si[q] = lane + 64 * r;
+        }
+        base += __popcll(bs);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // counting rank (descending value, ascending index), then scatter in place
+    constexpr int RK = (VCB + 63) / 64;
+    float ev[RK];
+    int ei[RK], rk[RK];
+    for (int j = 0; j < RK; ++j) {
+        const int e = lane + 64 * j;
+        if (j * 64 >= k) break;
+        if (e < k) {
+            const float v = sv[e];
+            const int i = si[e];
+            int rank = 0;
+            for (int e2 = 0; e2 < k; ++e2) {
+                const float v2 = sv[e2];
+                rank += (v2 > v) || (v2 == v && si[e2] < i);
+            }
+            rk[j] = rank;
+            ev[j] = expf((v - M) / temp);
+            ei[j] = i;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    for (int j = 0; j < RK; ++j) {
+        if (j * 64 >= k) break;
+        if (lane + 64 * j < k) { sv[rk[j]] = ev[j]; si[rk[j]] = ei[j]; }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    int code = 0;
+    if (lane == 0) {
+        float sum = 0.f;
+        for (int i = 0; i < k; ++i) sum += sv[i];
+        const float u = mp_uniform(smp.cfg->seed, stream, step, cb);
+        float cum = 0.f;
+        code = si[k - 1];
+        for (int i = 0; i < k; ++i) {
+            cum += sv[i] / sum;
+            if (u < cum) { code = si[i]; break; }
+        }
+    }
+    code = __shfl(code, 0, 64);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    return code;
+}
+
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
     const int tid = threadIdx.x;
@@ -292,8 +409,13 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
     } else if constexpr (PRO == PRO_LTARG_LN && NB >= 2) {
         const int lane = tid & 63, w = tid >> 6;
         for (int b = w; b < NB; b += MP_NWAVES) {
-            const int code = wave_masked_argmax(p, b);
-            if (blockIdx.x == 0 && lane == 0) p.codes_cur[b * NCB + p.cb - 1] = code;
+            int amax;
+            const int code = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos,
+                                       p.smp, b, p.step[b], p.cb - 1, sc + w * 2 * VCB, amax);
+            if (blockIdx.x == 0 && lane == 0) {
+                p.codes_cur[b * NCB + p.cb - 1] = code;
+                if (amax == p.audio_eos) p.smp.argeos[b] = 1;
+            }
             float X[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -383,8 +505,25 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         lds_sync();
     } else if constexpr (PRO == PRO_LTARG_LN) {
         static_assert(K == LTD, "LT is 256 wide");
+        const int lane = tid & 63, w = tid >> 6;
         for (int b = 0; b < NB; ++b) {
-            const int code = block_masked_argmax(p, b, red);  // codebook cb-1's code
+            int code;
+            if (p.smp.on) {
+                if (w == 0) {
+                    int amax;
+                    code = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos,
+                                     p.audio_eos, p.smp, b, p.step[b], p.cb - 1, sc, amax);
+                    if (lane == 0) {
+                        red[0] = __int_as_float(code);
+                        if (blockIdx.x == 0 && amax == p.audio_eos) p.smp.argeos[b] = 1;
+                    }
+                }
+                lds_sync();
+                code = __float_as_int(red[0]);
+                lds_sync();
+            } else {
+                code = block_masked_argmax(p, b, red);  // codebook cb-1's code
+            }
             if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb - 1] = code;
             const int k = tid;
             const float X = p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
@@ -414,6 +553,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     using VT = typename vecf<VW>::T;
     constexpr int SC = (PRO == PRO_XA) ? TMAX_LIMIT
                        : (PRO == PRO_LT_ATTN) ? 16
+                       : (PRO == PRO_LTARG_LN) ? (NB >= 2 ? MP_NWAVES : 1) * 2 * VCB
                        : 1;
     __shared__ __attribute__((aligned(16))) float act[NB * K];
     __shared__ float red[8 + 2 * DXA];
@@ -653,26 +793,39 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
     const int b = blockIdx.x, tid = threadIdx.x;
     if (p.done[b]) return;
     __shared__ float red[8];
-    const float *lg = p.logits + (size_t)b * VCB;
-    const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = tid; i < VCB; i += MP_BLOCK) {
-        float v = lg[i];
-        if (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos)) v = -INFINITY;
-        argmax_merge(bv, bi, v, i);
+    int i0, amax;
+    if (p.smp.on) {  // one wave draws
+        __shared__ float scratch[2 * VCB];
+        if (tid >= 64) return;
+        i0 = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos, p.smp, b,
+                       p.step[b], NCB - 1, scratch, amax);
+        if (tid != 0) return;
+    } else {
+        const float *lg = p.logits + (size_t)b * VCB;
+        const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < VCB; i += MP_BLOCK) {
+            float v = lg[i];
+            if (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos)) v = -INFINITY;
+            argmax_merge(bv, bi, v, i);
+        }
+        wave_argmax(bv, bi);
+        if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
+        lds_sync();
+        if (tid != 0) return;
+        float v0 = red[0];
+        i0 = ((int *)red)[4];
+        for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
+        if (i0 < 0 || i0 >= VCB) i0 = 0;
+        amax = i0;
     }
-    wave_argmax(bv, bi);
-    if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
-    lds_sync();
-    if (tid != 0) return;
-    float v0 = red[0];
-    int i0 = ((int *)red)[4];
-    for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
-    if (i0 < 0 || i0 >= VCB) i0 = 0;
     int *cc = p.codes_cur + b * NCB;
     cc[NCB - 1] = i0;
-    bool eos = false;
+    // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
+    bool eos = amax == p.audio_eos;
+    eos |= p.smp.argeos[b] != 0;
+    p.smp.argeos[b] = 0;
     for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
     const int s = p.step[b];
     if (eos) {
@@ -709,7 +862,7 @@ static bool gemv_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
     if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
     if constexpr (PRO == PRO_ARGMAX_EMB) ok &= p.logits && p.codes_cur && p.emb && p.step;
-    if constexpr (PRO == PRO_LTARG_LN) ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step;
+    if constexpr (PRO == PRO_LTARG_LN) ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step && p.smp.cfg && p.smp.argeos;
     if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
     if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
@@ -760,6 +913,7 @@ hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
 }
 
 hipError_t op_finalize(const FinP &p, int B, hipStream_t s) {
+    if (!p.smp.cfg || !p.smp.argeos) return hipErrorInvalidValue;
     hipLaunchKernelGGL(lt_finalize_kernel, dim3(B), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }

@@ -46,6 +46,35 @@ enum Epi {
     EPI_ADD_STORE = 6,  // out = v + addsrc
 };
 
+// Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
+// temperature < 0.01 (greedy, 1263-1264). Every draw is keyed by
+// (seed, slot, step, codebook) through mp_uniform(), so a decode is reproducible
+// and graph replays need no RNG state.
+struct SmpCfg {                // device-resident, so a captured graph serves any setting
+    float temperature;
+    int top_k;                 // 1..VCB
+    unsigned long long seed;
+};
+struct Sampling {
+    int on;                    // temperature >= 0.01 (baked into the captured graph)
+    const SmpCfg *cfg;
+    int *argeos;               // [B] 1 once a codebook's argmax was EOS this frame (4343-4346)
+};
+
+// splitmix64 finaliser
+__host__ __device__ inline unsigned long long mp_mix64(unsigned long long x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+// u in [0, 1) with 24 random bits, like uniform_real_distribution<float>(0, 1)
+__host__ __device__ inline float mp_uniform(unsigned long long seed, int stream, int step, int cb) {
+    unsigned long long h = mp_mix64(seed ^ ((unsigned long long)(unsigned)stream * 0xD1B54A32D192ED03ull));
+    h = mp_mix64(h ^ (((unsigned long long)(unsigned)step << 8) | (unsigned)cb));
+    return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+
 struct GemvP {
     const float *W;
     int N;
@@ -79,6 +108,7 @@ struct GemvP {
     int *codes_cur;       // [B][8]
     const int *step;      // [B]
     int ignore_eos, audio_bos, audio_eos;
+    Sampling smp;
     // epilogue outputs
     float *out;
     int out_ld;
@@ -97,6 +127,7 @@ struct FinP {
     int *codes_cur, *codes_prev, *codes_out;
     int *step, *pos, *done, *nframes, *ndone;
     int max_steps, ignore_eos, audio_bos, audio_eos, nslots;
+    Sampling smp;
 };
 
 // Fused cross-attention for one decode step (replaces the xq GEMV + XA attention

@@ -107,7 +107,9 @@ struct mp_dev {
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
-        *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr;
+        *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
+        *argeos = nullptr;
+    mp::SmpCfg *smpcfg = nullptr;
     // preamble scratch
     float *pX = nullptr, *pH = nullptr, *pQKV = nullptr, *pATT = nullptr, *pF = nullptr, *pXQ = nullptr,
           *pXAO = nullptr, *enc_out = nullptr;
@@ -359,6 +361,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);
+    A(argeos, NB); A(smpcfg, 1);
     A(codes_cur, NB * 8); A(codes_prev, NB * 8); A(codes_out, (size_t)NB * max_steps * 8); A(tok, (size_t)NB * Tmax);
     const size_t rows = (size_t)NB * std::max(Tmax, mp::CTX);
     A(pX, rows * D); A(pH, rows * D); A(pQKV, rows * 3 * D); A(pATT, rows * D); A(pF, rows * 3072);
@@ -378,6 +381,7 @@ mp::GemvP gemv_base(mp_dev *dev) {
     g.pos = dev->pos;
     g.step = dev->step;
     g.ndone = dev->ndone;
+    g.smp = mp::Sampling{dev->params.temperature >= 0.01f, dev->smpcfg, dev->argeos};
     g.nslots = dev->NB;
     g.ignore_eos = dev->params.ignore_eos;
     g.audio_bos = dev->m.audio_bos;
@@ -491,7 +495,8 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         if ((rc = run("lt_e", tb.lt_e, g, F * (2024.0 * 256 + 2024 + act * (256 + 2024)))) != MP_OK) return rc;
     }
     mp::FinP f{dev->logits, dev->codes_cur, dev->codes_prev, dev->codes_out, dev->step, dev->pos, dev->done,
-               dev->nframes, dev->ndone, dev->max_steps, dev->params.ignore_eos, m.audio_bos, m.audio_eos, NB};
+               dev->nframes, dev->ndone, dev->max_steps, dev->params.ignore_eos, m.audio_bos, m.audio_eos, NB,
+               mp::Sampling{dev->params.temperature >= 0.01f, dev->smpcfg, dev->argeos}};
     if (record) {
         mp::OpRec r{};
         r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = F * act * 2024;
@@ -663,8 +668,8 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
     if (!tokens || !n_tokens || !speaker || B < 1 || B > 8 || tmax < 1 || !params)
         return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..8)");
-    if (params->temperature >= 0.01f)
-        return fail(dev, MP_ERR_UNSUPPORTED, "temperature sampling is not implemented on the device path yet");
+    if (params->temperature >= 0.01f && (params->top_k < 1 || params->top_k > mp::VCB))
+        return fail(dev, MP_ERR_ARG, "top_k must be in 1..2024 when sampling");
     int Tmax = 0;
     for (int b = 0; b < B; ++b) {
         if (n_tokens[b] < 1 || n_tokens[b] > tmax) return fail(dev, MP_ERR_ARG, "n_tokens out of range");
@@ -683,7 +688,8 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     HIPCHK(hipSetDevice(dev->device));
     const bool trace = params->trace_hidden != 0;
     const bool same = dev->NB > 0 && dev->B == B && dev->Tmax == Tmax && dev->max_steps == max_steps &&
-                      (dev->trace != nullptr) == trace && dev->params.ignore_eos == params->ignore_eos;
+                      (dev->trace != nullptr) == trace && dev->params.ignore_eos == params->ignore_eos &&
+                      (dev->params.temperature >= 0.01f) == (params->temperature >= 0.01f);
     dev->params = *params;
     if (!same) {
         if (int rc = alloc_batch(dev, B, Tmax, max_steps, trace)) return rc;
@@ -700,6 +706,11 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     HIPCHK(hipMemcpyAsync(dev->tok, h_tok.data(), h_tok.size() * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemcpyAsync(dev->T, h_T.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemcpyAsync(dev->spk, h_spk.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
+    {   // sampling settings live on the device: the captured graph serves any of them
+        mp::SmpCfg cfg{params->temperature, params->top_k, (unsigned long long)params->seed};
+        HIPCHK(hipMemcpyAsync(dev->smpcfg, &cfg, sizeof cfg, hipMemcpyHostToDevice, dev->stream));
+        HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
+    }
     if (int rc = run_preamble(dev)) return rc;
     HIPCHK(hipStreamSynchronize(dev->stream));
     dev->timing = mp_timing{};
@@ -724,6 +735,7 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     HIPCHK(hipMemcpyAsync(dev->ndone, h_nd, 16, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
     // MAGPIE_EAGER=1: launch the iteration's kernels directly instead of replaying
     // the captured graph (identical kernels and arguments; used under rocprofv3,
     // whose kernel tracer crashes on graph replays on this image).
@@ -741,6 +753,8 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
             HIPCHK(hipMemcpyAsync(dev->ndone, h_nd, 16, hipMemcpyHostToDevice, dev->stream));
             HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
             HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
+            HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
         }
     } else if (!dev->exec) {
         // capture one iteration; the op list is recorded for measurement

@@ -413,10 +413,60 @@ static void frame_embed(const orc_model *m, const int32_t *codes, int pos, float
     }
 }
 
-// magpie_local_transformer_sample_all (magpie.cpp:1113-1317) at temperature 0,
-// computed incrementally over positions (causal => identical to the reference's
-// per-codebook recompute).
-static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, int32_t *codes, float *margins) {
+// Sampling stream (this repo's convention; the reference draws from an unseeded
+// process-global mt19937, magpie.cpp:1129, so its draws are not reproducible):
+// u(seed, stream, step, cb) = 24 high bits of splitmix64(splitmix64(seed ^ stream*C) ^ (step<<8 | cb)) / 2^24.
+static uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+float orc_draw_u(uint64_t seed, int stream, int step, int cb) {
+    uint64_t h = mix64(seed ^ ((uint64_t)(uint32_t)stream * 0xD1B54A32D192ED03ull));
+    h = mix64(h ^ (((uint64_t)(uint32_t)step << 8) | (uint32_t)cb));
+    return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+
+typedef struct { float v; int i; } scored_t;
+static int scored_desc(const void *a, const void *b) {
+    const scored_t *x = a, *y = b;
+    if (x->v != y->v) return x->v > y->v ? -1 : 1;
+    return x->i - y->i;  // ties: ascending index (std::partial_sort leaves them unspecified)
+}
+
+// sample_top_k (magpie.cpp:1072-1109): top-k by value, p_i = exp((l_i - l_0)/T)
+// normalised by a sequential float sum, first i with u < cumsum_i, else the k-th.
+// *margin = distance of u to the nearest boundary of the chosen interval.
+int orc_sample_top_k(const float *logits, int n, float temperature, int top_k, float u, float *margin) {
+    scored_t *sc = malloc(sizeof(scored_t) * (size_t)n);
+    for (int i = 0; i < n; ++i) { sc[i].v = logits[i]; sc[i].i = i; }
+    qsort(sc, (size_t)n, sizeof(scored_t), scored_desc);
+    const int k = top_k < n ? top_k : n;
+    float *pr = malloc(sizeof(float) * (size_t)k);
+    const float mx = sc[0].v;
+    float sum = 0.0f;
+    for (int i = 0; i < k; ++i) { pr[i] = expf((sc[i].v - mx) / temperature); sum += pr[i]; }
+    for (int i = 0; i < k; ++i) pr[i] /= sum;
+    float cum = 0.0f, lo = 0.0f;
+    int pick = sc[k - 1].i;
+    float mg = INFINITY;
+    for (int i = 0; i < k; ++i) {
+        lo = cum;
+        cum += pr[i];
+        if (u < cum) { pick = sc[i].i; mg = fminf(u - lo, cum - u); break; }
+    }
+    if (margin) *margin = mg;
+    free(pr); free(sc);
+    return pick;
+}
+
+// magpie_local_transformer_sample_all (magpie.cpp:1113-1317), computed
+// incrementally over positions (causal => identical to the reference's
+// per-codebook recompute). temperature < 0.01 => argmax (1263-1264).
+// *argeos is set when any codebook's argmax is EOS (the loop's EOS test, 4340-4346).
+static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, float temperature, int top_k,
+                      uint64_t seed, int stream, int step, int32_t *codes, float *margins, int *argeos) {
     const int D = m->lt_dim, F = m->lt_ffn, V = m->vocab_cb, d = m->d;
     float s[9][256], X[256], h[256], qkv[768], kk[8][256], vv[8][256], a[256], Y[256], f[1024], y2[256];
     float *logits = malloc(sizeof(float) * (size_t)V);
@@ -445,10 +495,18 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, i
         for (int i = 1; i < V; ++i) if (logits[i] > mx) { mx = logits[i]; am = i; }
         float second = -INFINITY;
         for (int i = 0; i < V; ++i) if (i != am && logits[i] > second) second = logits[i];
-        codes[cb] = am;
-        if (margins) margins[cb] = mx - second;
+        int code = am;
+        float mg = mx - second;
+        if (am == m->audio_eos && argeos) *argeos = 1;
+        if (temperature >= 0.01f) {
+            float sm;
+            code = orc_sample_top_k(logits, V, temperature, top_k, orc_draw_u(seed, stream, step, cb), &sm);
+            mg = fminf(mg, sm);
+        }
+        codes[cb] = code;
+        if (margins) margins[cb] = mg;
         if (cb < 7) {
-            const float *e = m->audio_emb[cb] + (size_t)am * d;  // no 1/8 here (1284-1291)
+            const float *e = m->audio_emb[cb] + (size_t)code * d;  // no 1/8 here (1284-1291)
             matmul(m->lt_in_w, m->lt_in_b, e, s[cb + 1], 1, D, d);
         }
     }
@@ -457,6 +515,14 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, i
 
 int orc_synthesize(orc_model *m, const int32_t *tokens, int T, int speaker, int max_steps, int ignore_eos,
                    int32_t *codes_out, float *margins_out, float *hidden_out, double *timing_out) {
+    return orc_synthesize_ex(m, tokens, T, speaker, max_steps, ignore_eos, 0.0f, 80, 0, 0, codes_out, margins_out,
+                             hidden_out, timing_out);
+}
+
+int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, int max_steps, int ignore_eos,
+                      float temperature, int top_k, uint64_t seed, int stream, int32_t *codes_out,
+                      float *margins_out, float *hidden_out, double *timing_out) {
+    if (temperature >= 0.01f && top_k < 1) return -1;
     if (!m || !tokens || T <= 0 || speaker < 0 || speaker >= m->n_spk) return -1;
     if (max_steps <= 0) max_steps = m->max_dec_steps;
     const int d = m->d, L = m->dec_layers, dxa = m->xa_heads * m->xa_dh;
@@ -505,8 +571,9 @@ int orc_synthesize(orc_model *m, const int32_t *tokens, int T, int speaker, int 
     for (int step = 0; step < max_steps; ++step) {
         int32_t codes[8];
         const int forbid = ignore_eos || step < 4;  // min_generated_frames (4267,4325)
-        lt_sample(m, hid, forbid, codes, margins_out ? margins_out + (size_t)step * 8 : NULL);
         int eos = 0;
+        lt_sample(m, hid, forbid, temperature, top_k, seed, stream, step, codes,
+                  margins_out ? margins_out + (size_t)step * 8 : NULL, &eos);
         for (int c = 0; c < 8; ++c) if (codes[c] == m->audio_eos) eos = 1;
         if (eos) break;
         memcpy(codes_out + (size_t)step * 8, codes, sizeof codes);

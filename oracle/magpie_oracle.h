@@ -40,7 +40,17 @@ int orc_synthesize(orc_model *m, const int32_t *tokens, int n_tokens, int speake
                    int ignore_eos, int32_t *codes_out, float *margins_out, float *hidden_out,
                    double *timing_out);
 
+// Same with the reference's temperature/top-k sampling (sample_top_k,
+// magpie.cpp:1072-1109). Draws use this repo's counter-based stream
+// u(seed, stream, step, codebook) (see magpie_oracle.c); stream = batch slot.
+// margins_out then holds min(argmax gap, distance of u to the chosen interval).
+int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int n_tokens, int speaker_id, int max_steps,
+                      int ignore_eos, float temperature, int top_k, uint64_t seed, int stream,
+                      int32_t *codes_out, float *margins_out, float *hidden_out, double *timing_out);
+
 // Component entry points used by unit tests.
+float orc_draw_u(uint64_t seed, int stream, int step, int cb);
+int orc_sample_top_k(const float *logits, int n, float temperature, int top_k, float u, float *margin);
 int orc_encode(orc_model *m, const int32_t *tokens, int n_tokens, float *enc_out /*[T][768]*/);
 
 orc_codec *orc_codec_load(const char *gguf_path);

@@ -35,7 +35,11 @@ def lib() -> ctypes.CDLL:
         L.orc_free.argtypes = [P]
         L.orc_dec_layers.argtypes = [P]
         L.orc_synthesize.argtypes = [P, P, I, I, I, I, P, P, P, P]
+        L.orc_synthesize_ex.argtypes = [P, P, I, I, I, I, ctypes.c_float, I, ctypes.c_uint64, I, P, P, P, P]
         L.orc_encode.argtypes = [P, P, I, P]
+        L.orc_draw_u.restype = ctypes.c_float
+        L.orc_draw_u.argtypes = [ctypes.c_uint64, I, I, I]
+        L.orc_sample_top_k.argtypes = [P, I, ctypes.c_float, I, ctypes.c_float, P]
         L.orc_codec_load.restype = P
         L.orc_codec_load.argtypes = [ctypes.c_char_p]
         L.orc_codec_free.argtypes = [P]
@@ -49,6 +53,18 @@ def set_mode(acc64: bool = True, gelu_f16: bool = False, threads: int = 0) -> No
     lib().orc_set_mode(int(acc64), int(gelu_f16), int(threads))
 
 
+def draw_u(seed: int, stream: int, step: int, cb: int) -> float:
+    return float(lib().orc_draw_u(int(seed) & (2**64 - 1), stream, step, cb))
+
+
+def sample_top_k(logits, temperature: float, top_k: int, u: float):
+    """(index, margin) of sample_top_k (magpie.cpp:1072-1109) for one logits row."""
+    lg = np.ascontiguousarray(logits, np.float32)
+    mg = ctypes.c_float()
+    i = lib().orc_sample_top_k(lg.ctypes.data, len(lg), float(temperature), int(top_k), float(u), ctypes.byref(mg))
+    return i, mg.value
+
+
 class Model:
     def __init__(self, path: str):
         self.h = lib().orc_load(path.encode())
@@ -60,15 +76,20 @@ class Model:
             lib().orc_free(self.h)
             self.h = None
 
-    def synthesize(self, tokens, speaker=0, max_steps=32, ignore_eos=False, trace=True):
+    def synthesize(self, tokens, speaker=0, max_steps=32, ignore_eos=False, trace=True,
+                   temperature=0.0, top_k=80, seed=0, stream=0):
+        """magpie_synthesize_codes_graph_reuse restated (magpie.cpp:4063-4432).
+        temperature >= 0.01 samples with sample_top_k's arithmetic (1072-1109) from
+        the counter-based stream u(seed, stream, step, cb); stream = batch slot."""
         tok = np.ascontiguousarray(tokens, np.int32)
         codes = np.zeros((max_steps, 8), np.int32)
         marg = np.zeros((max_steps, 8), np.float32)
         hid = np.zeros((max_steps + 1, 768), np.float32) if trace else None
         tim = np.zeros(2, np.float64)
-        n = lib().orc_synthesize(self.h, tok.ctypes.data, len(tok), speaker, max_steps, int(ignore_eos),
-                                 codes.ctypes.data, marg.ctypes.data,
-                                 hid.ctypes.data if trace else None, tim.ctypes.data)
+        n = lib().orc_synthesize_ex(self.h, tok.ctypes.data, len(tok), speaker, max_steps, int(ignore_eos),
+                                    float(temperature), int(top_k), int(seed) & (2**64 - 1), int(stream),
+                                    codes.ctypes.data, marg.ctypes.data,
+                                    hid.ctypes.data if trace else None, tim.ctypes.data)
         if n < 0:
             raise RuntimeError(f"oracle synthesize failed ({n})")
         return {"n_frames": n, "codes": codes[:n], "margins": marg[:max(n + 1, 0)],

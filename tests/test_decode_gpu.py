@@ -110,3 +110,61 @@ def test_invalid_arguments_fail_loudly(ma, small_model):
     with pytest.raises(ma.MagpieError):
         dev.synthesize([[1, 2, 3]], speakers=[7], max_dec_steps=4)
     dev.close()
+
+
+# ---------------------------------------------------------------- sampling
+# sample_top_k (magpie.cpp:1072-1109) on the device. The reference draws from an
+# unseeded mt19937 (1129), so its sampled codes are not reproducible run to run;
+# parity here is GPU == oracle on the same counter-based stream u(seed, slot,
+# step, cb), bit-identical up to a reported near-boundary draw (margin < TIE_EPS).
+
+def _sample_both(ma, oracle, model_path, toks, steps, temperature, top_k, seed, ignore_eos=False):
+    dev = ma.Device(model_path)
+    r = dev.synthesize(toks, speakers=[b % 5 for b in range(len(toks))], max_dec_steps=steps,
+                       temperature=temperature, top_k=top_k, seed=seed, ignore_eos=ignore_eos)
+    dev.close()
+    om = oracle.Model(model_path)
+    outs = [om.synthesize(t, speaker=b % 5, max_steps=steps, ignore_eos=ignore_eos, trace=False,
+                          temperature=temperature, top_k=top_k, seed=seed, stream=b) for b, t in enumerate(toks)]
+    om.close()
+    return r, outs
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_topk_sampling_matches_oracle(ma, oracle, small_model, B):
+    toks = [ma.synthetic_tokens(12 + 3 * b, seed=500 + b) for b in range(B)]
+    r, outs = _sample_both(ma, oracle, small_model, toks, steps=32, temperature=0.7, top_k=80, seed=1234)
+    for b in range(B):
+        compare_codes(r.codes[b], outs[b]["codes"], outs[b]["margins"])
+    # sampling actually departs from greedy
+    g = ma.Device(small_model)
+    rg = g.synthesize(toks[:1], speakers=[0], max_dec_steps=32)
+    g.close()
+    assert not np.array_equal(rg.codes[0], r.codes[0])
+
+
+def test_topk_full_vocab_sampling(ma, oracle, small_model):
+    """top_k = 2024: plain temperature sampling over every unmasked token."""
+    toks = [ma.synthetic_tokens(10, seed=77)]
+    r, outs = _sample_both(ma, oracle, small_model, toks, steps=6, temperature=1.0, top_k=2024, seed=9)
+    compare_codes(r.codes[0], outs[0]["codes"], outs[0]["margins"])
+
+
+def test_top1_sampling_is_greedy(ma, small_model):
+    toks = [ma.synthetic_tokens(16, seed=3)]
+    d = ma.Device(small_model)
+    s = d.synthesize(toks, max_dec_steps=20, temperature=0.9, top_k=1, seed=5)
+    g = d.synthesize(toks, max_dec_steps=20)
+    d.close()
+    assert np.array_equal(s.codes[0], g.codes[0])
+
+
+def test_sampling_eos_from_argmax(ma, oracle, eos_model):
+    """EOS stops the utterance when any codebook's sampled code OR argmax is EOS
+    (magpie.cpp:4340-4348); EOS is forbidden for the first 4 frames."""
+    toks = [ma.synthetic_tokens(16, seed=7), ma.synthetic_tokens(9, seed=8)]
+    r, outs = _sample_both(ma, oracle, eos_model, toks, steps=64, temperature=0.7, top_k=80, seed=99)
+    for b in range(2):
+        assert outs[b]["n_frames"] == 4
+        assert r.n_frames[b] == 4
+        compare_codes(r.codes[b], outs[b]["codes"], outs[b]["margins"])

@@ -117,3 +117,60 @@ def test_bad_inputs_rejected(oracle, small_model):
     with pytest.raises(RuntimeError):
         m.synthesize(np.array([1, 2], np.int32), speaker=9, max_steps=2)
     m.close()
+
+
+# ---------------------------------------------------------------- sampling
+def _py_sample_top_k(logits, temperature, top_k, u):
+    """Pure-Python sample_top_k (magpie.cpp:1072-1109), float32 at every step;
+    ties ordered by ascending index."""
+    f = np.float32
+    order = sorted(range(len(logits)), key=lambda i: (-float(logits[i]), i))
+    k = min(top_k, len(logits))
+    top = [order[i] for i in range(k)]
+    mx = f(logits[top[0]])
+    probs = [f(np.exp(f(f(logits[i]) - mx) / f(temperature))) for i in top]
+    s = f(0)
+    for p in probs:
+        s = f(s + p)
+    cum = f(0)
+    for i, p in zip(top, probs):
+        cum = f(cum + f(p / s))
+        if f(u) < cum:
+            return i
+    return top[-1]
+
+
+def test_sample_top_k_known_answers(oracle):
+    rng = np.random.default_rng(0)
+    for trial in range(60):
+        n = int(rng.integers(5, 300))
+        lg = rng.normal(0, 2, n).astype(np.float32)
+        if trial % 5 == 0:
+            lg[rng.integers(0, n, 4)] = lg[0]  # exact ties
+        if trial % 7 == 0:
+            lg[rng.integers(0, n, 3)] = -np.inf  # masked tokens
+        T = float(rng.choice([0.05, 0.3, 0.7, 1.0, 2.5]))
+        k = int(rng.choice([1, 2, 5, 80, n]))
+        u = float(rng.random())
+        got, _ = oracle.sample_top_k(lg, T, k, u)
+        assert got == _py_sample_top_k(lg, T, k, u), (trial, n, T, k, u)
+
+
+def test_sampling_stream_is_reproducible(oracle, small_model):
+    import magpie_amd as ma
+    us = [oracle.draw_u(7, s, st, cb) for s in range(2) for st in range(3) for cb in range(8)]
+    assert all(0.0 <= u < 1.0 for u in us) and len(set(us)) == len(us)
+    m = oracle.Model(small_model)
+    tok = ma.synthetic_tokens(12, seed=4)
+    kw = dict(max_steps=10, ignore_eos=True, trace=False, temperature=0.7, top_k=80)
+    a = m.synthesize(tok, seed=11, **kw)["codes"]
+    b = m.synthesize(tok, seed=11, **kw)["codes"]
+    c = m.synthesize(tok, seed=12, **kw)["codes"]
+    d = m.synthesize(tok, seed=11, stream=1, **kw)["codes"]
+    g = m.synthesize(tok, max_steps=10, ignore_eos=True, trace=False)["codes"]
+    t1 = m.synthesize(tok, seed=11, max_steps=10, ignore_eos=True, trace=False, temperature=0.7, top_k=1)["codes"]
+    m.close()
+    assert np.array_equal(a, b)
+    assert not np.array_equal(a, c) and not np.array_equal(a, d)
+    assert np.array_equal(t1, g)  # top-1 sampling is greedy
+    assert a.max() <= 2015 and a.min() >= 0

@@ -317,78 +317,6 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             }
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_SA_COMBINE) {
-        static_assert(K == D, "SA output is d_model wide");
-        // One round trip: every thread loads (max, sum, o[d]) of all chunks of its
-        // heads at once, then combines them in registers:
-        // a[d] = sum_c e^(m_c - M) o_c[d] / sum_c e^(m_c - M) l_c
-        for (int b = 0; b < NB; ++b)
-#pragma unroll
-            for (int i = 0; i < K / MP_BLOCK; ++i) {
-                const int k = tid + MP_BLOCK * i, h = k / DH, d = k % DH;
-                const float *P = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
-                float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
-#pragma unroll
-                for (int c = 0; c < NCH_MAX; ++c) {
-                    const bool ok = c < p.nch;
-                    mv[c] = ok ? P[c * PART_STRIDE] : -INFINITY;
-                    lv[c] = ok ? P[c * PART_STRIDE + 1] : 0.f;
-                    ov[c] = ok ? P[c * PART_STRIDE + 16 + d] : 0.f;
-                }
-                float M = -INFINITY;
-#pragma unroll
-                for (int c = 0; c < NCH_MAX; ++c) M = fmaxf(M, mv[c]);
-                float num = 0.f, den = 0.f;
-#pragma unroll
-                for (int c = 0; c < NCH_MAX; ++c) {
-                    const float e = mv[c] == -INFINITY ? 0.f : expf(mv[c] - M);
-                    den += e * lv[c];
-                    num += e * ov[c];
-                }
-                act[b * K + k] = num / den;
-            }
-        lds_sync();
-    } else if constexpr (PRO == PRO_XA) {
-        static_assert(K == DXA, "XA output is 128 wide");
-        const int lane = tid & 63, w = tid >> 6, half = lane >> 5, d4 = lane & 31;
-        const float scale = 1.0f / sqrtf((float)DXA);
-        for (int b = 0; b < NB; ++b) {
-            const int Tb = p.T[b];
-            const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-            const float *Vb = p.xav + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-            const float4 q4 = *(const float4 *)(p.qx + (size_t)b * DXA + 4 * d4);
-            // half-wave hw (0..7) scores keys hw, hw+8, ...; 4 key rows in flight per lane
-            const int hw = w * 2 + half;
-            for (int jb = hw; jb < Tb; jb += 32) {
-                float4 kv[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int j = jb + 8 * u;
-                    kv[u] = j < Tb ? *(const float4 *)(Kb + (size_t)j * DXA + 4 * d4) : make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int j = jb + 8 * u;
-                    const float v = group_sum<32>(dotv(q4, kv[u]));
-                    if (d4 == 0 && j < Tb) sc[j] = v * scale;
-                }
-            }
-            lds_sync();
-            float m = -INFINITY;
-            for (int j = tid; j < Tb; j += MP_BLOCK) m = fmaxf(m, sc[j]);
-            m = block_max(m, red);
-            float l = 0.f;
-            for (int j = tid; j < Tb; j += MP_BLOCK) { const float e = expf(sc[j] - m); sc[j] = e; l += e; }
-            l = block_sum(l, red);  // (its barriers also publish sc[])
-            const int dd = tid & (DXA - 1), par = tid >> 7;
-            float a = 0.f;
-#pragma unroll 8
-            for (int j = par; j < Tb; j += 2) a += sc[j] * Vb[(size_t)j * DXA + dd];
-            red[8 + tid] = a;
-            lds_sync();
-            if (tid < DXA) act[b * K + tid] = (red[8 + tid] + red[8 + DXA + tid]) / l;
-            lds_sync();
-        }
     } else if constexpr (PRO == PRO_LTX_LN && NB >= 2) {
         const int lane = tid & 63, w = tid >> 6;
         for (int b = w; b < NB; b += MP_NWAVES) {
@@ -494,15 +422,6 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             act[b * K + tid] = a / l;
             lds_sync();
         }
-    } else if constexpr (PRO == PRO_ARGMAX_EMB) {
-        static_assert(K == D, "embedding is d_model wide");
-        for (int b = 0; b < NB; ++b) {
-            const int i0 = block_masked_argmax(p, b, red);
-            if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb] = i0;
-            const float *e = p.emb + ((size_t)p.cb * VCB + i0) * D;
-            for (int k = tid; k < K; k += MP_BLOCK) act[b * K + k] = e[k];
-        }
-        lds_sync();
     } else if constexpr (PRO == PRO_LTARG_LN) {
         static_assert(K == LTD, "LT is 256 wide");
         const int lane = tid & 63, w = tid >> 6;
@@ -551,12 +470,11 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     constexpr int VW = K >= 256 ? 4 : K / 64;
     constexpr int NV = K / (64 * VW);
     using VT = typename vecf<VW>::T;
-    constexpr int SC = (PRO == PRO_XA) ? TMAX_LIMIT
-                       : (PRO == PRO_LT_ATTN) ? 16
+    constexpr int SC = (PRO == PRO_LT_ATTN) ? 16
                        : (PRO == PRO_LTARG_LN) ? (NB >= 2 ? MP_NWAVES : 1) * 2 * VCB
                        : 1;
     __shared__ __attribute__((aligned(16))) float act[NB * K];
-    __shared__ float red[8 + 2 * DXA];
+    __shared__ float red[8];
     __shared__ float sc[SC];
 
     // The weight rows do not depend on the prologue: issue the whole stream first
@@ -615,14 +533,16 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 
 // ---------------------------------------------------------------- SA decode attention
 // Split-K over the key axis: workgroup (chunk, head, slot) handles 64 keys and
-// writes (max, sum, o[64]) for the combine in the O-projection prologue.
+// writes (max, sum, o[64]); the last of a head's active chunks to arrive
+// combines them in-launch (a[d] = sum_c e^(m_c-M) o_c[d] / sum_c e^(m_c-M) l_c)
+// and writes the head's 64 outputs, so the O-projection reads a plain vector.
 // 16 lanes x float4 cover one 64-dim key row (256 B, coalesced); a wave does 4
 // keys per instruction. Keys j > pos are masked (L = pos + 1, magpie.cpp:3412).
-__global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
+__global__ __launch_bounds__(MP_BLOCK) void sa_attn_kernel(AttnP p) {
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    __shared__ float sc[SA_CHUNK];
-    __shared__ float ow[MP_NWAVES][DH];
+    __shared__ float sc[SA_CHUNK + MP_NWAVES * DH + 4];
+    float *ow = sc + SA_CHUNK;  // [MP_NWAVES][DH]
     const int j0 = c * SA_CHUNK;
     const int kk = lane >> 4, dc = lane & 15;
     // Issue q, all 4 K rows and all 4 V rows of this lane first: rows j < max_seq
@@ -637,11 +557,9 @@ __global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
         v4[it] = *(const float4 *)(p.vc + base + (size_t)j * D);
     }
     const int L = p.pos[b] + 1;
+    if (j0 >= L) return;  // inactive chunk: takes no ticket
+    const int nact = (L + SA_CHUNK - 1) / SA_CHUNK;
     float *P = p.part + ((size_t)(b * NH + h) * p.nch + c) * PART_STRIDE;
-    if (j0 >= L) {
-        if (tid < PART_STRIDE) P[tid] = tid == 0 ? -INFINITY : 0.f;
-        return;
-    }
     float s[4];
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -671,46 +589,40 @@ __global__ __launch_bounds__(MP_BLOCK) void sa_attn_partial_kernel(AttnP p) {
         o.x += __shfl_xor(o.x, msk, 64); o.y += __shfl_xor(o.y, msk, 64);
         o.z += __shfl_xor(o.z, msk, 64); o.w += __shfl_xor(o.w, msk, 64);
     }
-    if (lane < 16) *(float4 *)(&ow[w][4 * lane]) = o;
+    if (lane < 16) *(float4 *)(&ow[w * DH + 4 * lane]) = o;
     lds_sync();
-    if (tid < DH) P[16 + tid] = (ow[0][tid] + ow[1][tid]) + (ow[2][tid] + ow[3][tid]);
-    if (tid == 64) {
-        P[0] = m;
-        P[1] = l;
+    if (tid < DH / 2) {
+        const int d = 2 * tid;
+        st_sc1(P + 16 + d, (ow[d] + ow[DH + d]) + (ow[2 * DH + d] + ow[3 * DH + d]),
+               (ow[d + 1] + ow[DH + d + 1]) + (ow[2 * DH + d + 1] + ow[3 * DH + d + 1]));
+    } else if (tid == 64) {
+        st_sc1(P, m, l);
     }
-}
-
-// ---------------------------------------------------------------- SA combine (NB > 1)
-// One wave per (head, slot): a[d] = sum_c e^(m_c - M) o_c[d] / sum_c e^(m_c - M) l_c.
-// At batch > 1 this runs once instead of redundantly in every O-proj workgroup.
-__global__ __launch_bounds__(64) void sa_combine_kernel(const float *part, int nch, float *out) {
-    const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-    const float *P = part + (size_t)(b * NH + h) * nch * PART_STRIDE;
+    if (!arrive_last(p.cnt + b * NH + h, (unsigned)nact, sc + SA_CHUNK + MP_NWAVES * DH, p.sc1_loads != 0)) return;
+    if (tid >= DH) return;
+    const float *Pb = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
     float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
 #pragma unroll
-    for (int c = 0; c < NCH_MAX; ++c) {
-        const bool ok = c < nch;
-        mv[c] = ok ? P[c * PART_STRIDE] : -INFINITY;
-        lv[c] = ok ? P[c * PART_STRIDE + 1] : 0.f;
-        ov[c] = ok ? P[c * PART_STRIDE + 16 + d] : 0.f;
+    for (int cc = 0; cc < NCH_MAX; ++cc) {  // unconditional (clamped) loads: no branch per load
+        const float *Pc = Pb + min(cc, nact - 1) * PART_STRIDE;
+        mv[cc] = ld_sc1(Pc);
+        lv[cc] = ld_sc1(Pc + 1);
+        ov[cc] = ld_sc1(Pc + 16 + tid);
     }
+#pragma unroll
+    for (int cc = 0; cc < NCH_MAX; ++cc)
+        if (cc >= nact) { mv[cc] = -INFINITY; lv[cc] = 0.f; ov[cc] = 0.f; }
     float M = -INFINITY;
 #pragma unroll
-    for (int c = 0; c < NCH_MAX; ++c) M = fmaxf(M, mv[c]);
+    for (int cc = 0; cc < NCH_MAX; ++cc) M = fmaxf(M, mv[cc]);
     float num = 0.f, den = 0.f;
 #pragma unroll
-    for (int c = 0; c < NCH_MAX; ++c) {
-        const float e = mv[c] == -INFINITY ? 0.f : expf(mv[c] - M);
-        den += e * lv[c];
-        num += e * ov[c];
+    for (int cc = 0; cc < NCH_MAX; ++cc) {
+        const float e = mv[cc] == -INFINITY ? 0.f : expf(mv[cc] - M);
+        den += e * lv[cc];
+        num += e * ov[cc];
     }
-    out[(size_t)b * D + h * DH + d] = num / den;
-}
-
-hipError_t op_sa_combine(const float *part, int nch, float *out, int B, hipStream_t s) {
-    if (!part || !out || nch < 1 || nch > NCH_MAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sa_combine_kernel, dim3(NH, B), dim3(64), 0, s, part, nch, out);
-    return hipGetLastError();
+    p.out[(size_t)b * D + h * DH + tid] = num / den;
 }
 
 // ---------------------------------------------------------------- fused XA
@@ -857,11 +769,8 @@ static bool gemv_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
-    if constexpr (PRO == PRO_SA_COMBINE) ok &= p.part && p.nch > 0 && p.nch <= NCH_MAX;
-    if constexpr (PRO == PRO_XA) ok &= p.qx && p.xak && p.xav && p.T;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
     if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
-    if constexpr (PRO == PRO_ARGMAX_EMB) ok &= p.logits && p.codes_cur && p.emb && p.step;
     if constexpr (PRO == PRO_LTARG_LN) ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step && p.smp.cfg && p.smp.argeos;
     if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
     if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
@@ -886,10 +795,7 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
 #define MP_DECODE_OPS(NB)                                                                                        \
     hipError_t op_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
-    hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_SA_COMBINE, EPI_RESID>(p, s); } \
-    hipError_t op_oprojp_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_PLAIN, EPI_RESID>(p, s); }   \
-    hipError_t op_xq_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_STORE>(p, s); }            \
-    hipError_t op_xo_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DXA, PRO_XA, EPI_RESID>(p, s); }          \
+    hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_PLAIN, EPI_RESID>(p, s); }    \
     hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_GELU>(p, s); }            \
     hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \
     hipError_t op_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_BIAS>(p, s); }         \
@@ -907,8 +813,10 @@ MP_DECODE_OPS(4)
 MP_DECODE_OPS(8)
 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
-    if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || p.nch < 1 || p.nch * SA_CHUNK > p.max_seq) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sa_attn_partial_kernel, dim3(p.nch, NH, B), dim3(MP_BLOCK), 0, s, p);
+    if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || !p.out || !p.cnt || p.nch < 1 || p.nch > NCH_MAX ||
+        p.nch * SA_CHUNK > p.max_seq)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sa_attn_kernel, dim3(p.nch, NH, B), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 

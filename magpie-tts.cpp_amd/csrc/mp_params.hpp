@@ -27,11 +27,8 @@ enum Pro {
     PRO_PLAIN = 0,      // act = src
     PRO_LN = 1,         // act = LN(src) * lnw                          (magpie.cpp:2237-2259)
     PRO_EMBED_LN = 2,   // x = sum_cb emb[cb][code]/8 + pos; act = LN(x)*lnw (2746-2787, 4376-4379)
-    PRO_SA_COMBINE = 3, // act = split-K softmax combine of SA partials (3457-3476)
-    PRO_XA = 4,         // act = softmax(K q / sqrt(128)) V over the text memory (1713-1767)
     PRO_LTX_LN = 5,     // X = s_cb + lt_pos[cb]; act = LN(X)*lnw       (1015-1034, 946-958)
     PRO_LT_ATTN = 6,    // act = causal 1x256 attention over LT positions 0..cb (965-966)
-    PRO_ARGMAX_EMB = 7, // code = masked argmax(logits); act = audio_emb[cb][code] (1243-1291)
     PRO_LTARG_LN = 8,   // code_{cb-1} = masked argmax(logits); X = P[cb-1][code] + lt_pos[cb];
                         // act = LN(X)*lnw, with P[c][v] = in_proj(audio_emb[c][v]) + b
                         // precomputed at load (1274-1313 depend only on (c, v))
@@ -92,12 +89,7 @@ struct GemvP {
     const float *pos_emb;
     const int *pos;      // [B] decoder position
     float *xres;         // [B][768] residual stream
-    const float *part;   // SA partials
-    int nch;
-    const float *qx;     // XA query [B][128]
-    const float *xak, *xav;  // [B][L][Tmax][128]
-    const int *T;
-    int Tmax, layer, nlayers;
+    int layer, nlayers;
     const float *lt_s;   // [B][9][256]
     const float *ptab;   // [8][2024][256] in_proj(audio_emb) + b
     int cb;
@@ -153,6 +145,9 @@ struct AttnP {  // split-K decode self-attention (one query per utterance)
     int nch;
     const int *ndone;
     int nslots;
+    float *out;          // [B][768] combined attention output
+    unsigned *cnt;       // [B][12] arrival tickets (zero between launches)
+    int sc1_loads;       // combiner reads partials with sc1 loads (1 workgroup/CU) instead of an acquire
 };
 
 }  // namespace mp

@@ -29,11 +29,10 @@ namespace mp {
 using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
 #define MP_DECL_OPS(NB)                                                                                     \
     hipError_t op_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t op_qkv_##NB(const GemvP &, hipStream_t);        \
-    hipError_t op_oproj_##NB(const GemvP &, hipStream_t); hipError_t op_xq_##NB(const GemvP &, hipStream_t);             \
-    hipError_t op_xo_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);               \
+    hipError_t op_oproj_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
     hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
-    hipError_t op_lt_ag_##NB(const GemvP &, hipStream_t); hipError_t op_oprojp_##NB(const GemvP &, hipStream_t);        \
+    hipError_t op_lt_ag_##NB(const GemvP &, hipStream_t);                                                              \
     hipError_t op_lt_c_##NB(const GemvP &, hipStream_t); hipError_t op_lt_d_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_lt_e_##NB(const GemvP &, hipStream_t);
 MP_DECL_OPS(1)
@@ -42,7 +41,6 @@ MP_DECL_OPS(4)
 MP_DECL_OPS(8)
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
-hipError_t op_sa_combine(const float *, int, float *, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 }  // namespace mp
@@ -51,8 +49,8 @@ hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 namespace mp {
 
-struct OpTable { GemvFn qkv_embed, qkv, oproj, oprojp, ff1, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
-#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_oprojp_##NB, op_ff1_##NB, op_ff2_##NB, \
+struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
+#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_ag_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
 static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
 static const OpTable &table_for(int NB) { return kTables[NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : 3]; }
@@ -76,7 +74,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_COMB = 4 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3 };
 struct OpRec {
     std::string name;
     int kind;
@@ -102,7 +100,9 @@ struct mp_dev {
     mp_params params{};
     // device state (one allocation per buffer, sized for the configuration)
     std::vector<void *> allocs;
-    float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *part = nullptr, *qx = nullptr, *h = nullptr, *hidden = nullptr;
+    float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *part = nullptr, *sa_out = nullptr,
+          *h = nullptr, *hidden = nullptr;
+    unsigned *sa_cnt = nullptr;
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
@@ -353,7 +353,8 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     int rc = MP_OK;
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
-    A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(part, (size_t)NB * 12 * dev->nch * mp::PART_STRIDE); A(qx, NB * 128);
+    A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(part, (size_t)NB * 12 * dev->nch * mp::PART_STRIDE);
+    A(sa_out, NB * 768); A(sa_cnt, NB * 12);
     A(h, NB * 3072); A(hidden, NB * D);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -376,8 +377,6 @@ mp::GemvP gemv_base(mp_dev *dev) {
     g.eps = dev->m.eps;
     g.nlayers = dev->m.dec_layers;
     g.max_seq = dev->max_seq;
-    g.Tmax = dev->Tmax;
-    g.T = dev->T;
     g.pos = dev->pos;
     g.step = dev->step;
     g.ndone = dev->ndone;
@@ -418,8 +417,9 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         if (l == 0) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
         if ((rc = run(l == 0 ? "qkv_embed" : "qkv", l == 0 ? tb.qkv_embed : tb.qkv, g,
                       F * (2304.0 * 768 + act * (768 + 2304)))) != MP_OK) return rc;
-        // split-K self-attention over the cache (3457-3476)
-        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->part, dev->nch, dev->ndone, NB};
+        // split-K self-attention over the cache, combined in-launch (3457-3476)
+        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->part, dev->nch, dev->ndone, NB,
+                    dev->sa_out, dev->sa_cnt, dev->nch * 12 * NB <= 256};
         if (record) {
             mp::OpRec r{};
             r.name = "sa_attn"; r.kind = mp::K_ATTN; r.a = a; r.B = NB;
@@ -427,23 +427,10 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             dev->ops.push_back(r);
         }
         HIPCHK(mp::op_sa_attn(a, NB, s));
-        // O-proj + residual (3479, 3509). Batch 1: chunk combine fused in the
-        // prologue; batch > 1: one combine pass, then a plain GEMV.
+        // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
-        g.W = W.o; g.N = 768; g.resid = dev->x;
-        if (NB == 1) {
-            g.part = dev->part; g.nch = dev->nch;
-            if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768 + act * (768 * 2 + 12.0 * dev->nch * 80)))) != MP_OK) return rc;
-        } else {
-            if (record) {
-                mp::OpRec r{};
-                r.name = "sa_combine"; r.kind = mp::K_COMB; r.B = NB; r.bytes = F * act * (12.0 * dev->nch * 80 + 768);
-                dev->ops.push_back(r);
-            }
-            HIPCHK(mp::op_sa_combine(dev->part, dev->nch, dev->q, NB, s));  // q is free once attention ran
-            g.src = dev->q; g.src_ld = 768;
-            if ((rc = run("oproj", tb.oprojp, g, F * (768.0 * 768 + act * 768 * 3))) != MP_OK) return rc;
-        }
+        g.W = W.o; g.N = 768; g.resid = dev->x; g.src = dev->sa_out; g.src_ld = 768;
+        if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768 + act * 768 * 3))) != MP_OK) return rc;
         // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
         mp::XaP xp{dev->x, dev->x2, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
         if (record) {
@@ -710,6 +697,7 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
         mp::SmpCfg cfg{params->temperature, params->top_k, (unsigned long long)params->seed};
         HIPCHK(hipMemcpyAsync(dev->smpcfg, &cfg, sizeof cfg, hipMemcpyHostToDevice, dev->stream));
         HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
     }
     if (int rc = run_preamble(dev)) return rc;
     HIPCHK(hipStreamSynchronize(dev->stream));
@@ -736,6 +724,7 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
     HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
     // MAGPIE_EAGER=1: launch the iteration's kernels directly instead of replaying
     // the captured graph (identical kernels and arguments; used under rocprofv3,
     // whose kernel tracer crashes on graph replays on this image).
@@ -754,7 +743,9 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
             HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
             HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
             HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
     HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
         }
     } else if (!dev->exec) {
         // capture one iteration; the op list is recorded for measurement
@@ -850,7 +841,6 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     auto launch = [&]() -> hipError_t {
         if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
         if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
-        if (r.kind == mp::K_COMB) return mp::op_sa_combine(dev->part, dev->nch, dev->h, r.B, dev->stream);
         if (r.kind == mp::K_XA) {
             mp::XaP xp = r.x;
             xp.x_out = dev->q;  // scratch: timing must not disturb the residual stream

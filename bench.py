@@ -43,11 +43,16 @@ FRAMES = 256
 TEXT_TOKENS = 64
 
 
-def decoder_bytes_per_frame(B: int, L_mean: float, T: int, dec_layers: int = 12) -> float:
-    """Algorithmic HBM bytes per frame, f32 weights and f32 KV."""
+def decoder_bytes_per_frame(B: int, L_mean: float, T: int, dec_layers: int = 12, weights: str = "f32") -> float:
+    """Algorithmic HBM bytes per frame, f32 KV. weights="bf16": the
+    decode projections (decoder qkv/o/ff1/ff2 = 7,077,888 params per layer; LT
+    layer + 8 heads = 4,931,584 params) at 2 B, the rest f32."""
     W_dec = dec_layers * 7_276_800 + 768
     W_lt = 5_147_200
     per_utt = 73_728 * L_mean * dec_layers / 12 + 12_288 * T * dec_layers / 12 + 49_152 + 73_728 * dec_layers / 12
+    if weights == "bf16":
+        half = dec_layers * 7_077_888 + 4_931_584
+        return (2.0 * half + 4.0 * (W_dec + W_lt - half)) / B + per_utt
     return 4.0 * (W_dec + W_lt) / B + per_utt
 
 
@@ -64,6 +69,8 @@ def main() -> None:
                     help="oracle threads for cpu_baseline (ggml's default n_threads, magpie.h:298,306)")
     ap.add_argument("--profile-ops", type=int, default=30, help="event-timed launches per op for the roofline")
     ap.add_argument("--no-codec", action="store_true")
+    ap.add_argument("--weights", choices=["f32", "bf16"], default="f32",
+                    help="f32 = configs[1]; bf16 = configs[2]/[3] (decode projections on bf16 MFMA, batch <= 16)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -83,7 +90,7 @@ def main() -> None:
         dist.barrier()
         ma.synth_gguf(model_path)  # no-op once rank 0 wrote it
 
-    dev = ma.Device(model_path, device=local)
+    dev = ma.Device(model_path, device=local, weights=args.weights)
     B = args.batch
     toks = [ma.synthetic_tokens(args.tokens, seed=1000 + rank * B + b) for b in range(B)]
     speakers = [(rank * B + b) % 5 for b in range(B)]
@@ -187,7 +194,7 @@ def main() -> None:
 
     if rank == 0:
         L_mean = 110 + (args.frames + 1) / 2.0  # keys 111..366 over BOS + 255 steps
-        bpf = decoder_bytes_per_frame(B, L_mean, args.tokens)
+        bpf = decoder_bytes_per_frame(B, L_mean, args.tokens, weights=args.weights)
         fps_per_gpu = value / world
         line = {
             "metric": "audio-codec frames/sec (decode loop), Magpie-357M",
@@ -200,10 +207,11 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.weights,
             "data": "synthetic (deterministic random weights, exact GGUF layout; synthetic T=64 prompts)",
-            "config": {"workload": f"Magpie-357M f32, batch={B}/GPU, {args.frames} frames/utterance, "
-                                   f"T={args.tokens}, greedy, EOS masked (configs[1])",
+            "config": {"workload": f"Magpie-357M {args.weights}, batch={B}/GPU, {args.frames} frames/utterance, "
+                                   f"T={args.tokens}, greedy, EOS masked "
+                                   f"({'configs[1]' if args.weights == 'f32' else 'configs[2]/[3] shape'})",
                        "global_batch": B * world, "frames_per_utterance": args.frames, "text_tokens": args.tokens,
                        "parallelism": f"replicas x{world} (utterance-partitioned, no collectives)"},
             "rtf_per_stream": round(value / world / B / ma.FRAMES_PER_SECOND, 2),

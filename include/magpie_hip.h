@@ -64,13 +64,25 @@ int mp_hip_init(int device, mp_dev **out);
  * (magpie.cpp:73-121, 572-718, 781-880): parses the GGUF (F32/F16/Q8_0 tensors,
  * same names and layout) and uploads resident weights once. */
 int mp_hip_load_model(mp_dev *dev, const char *gguf_path);
+/* Weight modes of mp_hip_load_model_ex. AS_STORED streams the GGUF's weights
+ * as f32 (F16/BF16/Q8_0 tensors are widened at load). BF16 additionally repacks
+ * the decode-step projections (decoder qkv/o/ff1/ff2, LT layer, LT heads) into
+ * bf16 MFMA fragments: half the bytes per frame, activations rounded to bf16
+ * like ggml's BF16 mul_mat; batches up to 16 (BASELINE configs 3-4). The
+ * preamble and cross-attention stay f32. No reference counterpart (the
+ * reference converter writes F32/F16/Q8_0/Q4_0, convert_magpie_to_gguf.py:197-206). */
+#define MP_WEIGHTS_AS_STORED 0
+#define MP_WEIGHTS_BF16 1
+int mp_hip_load_model_ex(mp_dev *dev, const char *gguf_path, int weight_mode);
+int mp_hip_weight_mode(mp_dev *dev);
 int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes);
 /* replaces magpie_free (magpie.cpp:882-910) */
 void mp_hip_free(mp_dev *dev);
 const char *mp_hip_error(mp_dev *dev);
 
 /* --- synthesis ------------------------------------------------------------ */
-/* Per-utterance preamble for B independent utterances: text encoder
+/* Per-utterance preamble for B independent utterances (B <= 8; <= 16 in the
+ * BF16 weight mode): text encoder
  * (magpie_encode_text, magpie.cpp:2284-2374), cross-attention K/V
  * (magpie.cpp:4098-4136), baked speaker context + 110-frame prefill
  * (magpie.cpp:4138-4238). tokens: [B][tmax] row-major (padding ignored),

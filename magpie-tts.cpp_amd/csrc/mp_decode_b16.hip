@@ -1,0 +1,177 @@
+// bf16 weight mode of the decode projections on MFMA (gfx950).
+//
+// Every fused projection of the decode step (qkv, O, FFN up/down of the 12
+// decoder layers; the LT layer and its 8 output heads) as a skinny GEMM
+//   out[b][n] = sum_k W[n][k] * bf16(act[b][k]),  b < NB <= 16
+// on v_mfma_f32_16x16x32_bf16: the A operand is a 16-row x 32-k weight
+// fragment, the B operand 32 k x 16 utterance columns (columns >= NB are zero),
+// f32 accumulation. Activations are rounded to bf16 exactly as ggml rounds src1
+// for a BF16 mul_mat (vec_dot_type BF16); the products are exact in f32.
+//
+// Layout in HBM: weights are repacked once at load into fragment order,
+// [N/16][K/32][64 lanes][8 bf16], so each wave-instruction of the weight stream
+// is one contiguous 1 KiB global_load_dwordx4 (lane l holds row l&15, k
+// 8(l>>4)..+8 of the fragment). One workgroup owns one 16-row tile; its four
+// waves split K in four and reduce their 16x16 accumulators through LDS in a
+// fixed order, so every output's arithmetic is independent of NB (a batch
+// reproduces its utterances run alone bit for bit).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "mp_device.hpp"
+#include "mp_fused.hpp"
+#include "mp_params.hpp"
+
+namespace mp {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// f32 -> bf16 bits, round to nearest even (ggml_compute_fp32_to_bf16)
+__device__ __forceinline__ unsigned short f2bf(float x) {
+    unsigned u = __float_as_uint(x);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 64);
+    return (unsigned short)((u + (0x7fffu + ((u >> 16) & 1u))) >> 16);
+}
+
+template <int NB, int K, int PRO, int EPI>
+__global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
+    static_assert(NB >= 1 && NB <= 16, "one 16-column MFMA tile of utterances");
+    static_assert(K % 128 == 0, "K splits into 4 waves x 32-wide chunks");
+    constexpr int KC = K / 32, KW = KC / MP_NWAVES;
+    constexpr int KP = K + 8;  // padded bf16 row: rows land 16 B apart in the banks
+    constexpr int NR = NB + 1;  // NB activation rows + one zero row for the unused MFMA columns
+    constexpr bool STAGE = PRO != PRO_PLAIN;
+    constexpr int SC = (PRO == PRO_LT_ATTN) ? 16 : (PRO == PRO_LTARG_LN) ? (NB < MP_NWAVES ? NB : MP_NWAVES) * 2 * VCB : 1;
+    __shared__ __attribute__((aligned(16))) float actf[STAGE ? NB * K : 4];
+    __shared__ __attribute__((aligned(16))) unsigned short actb[NR * KP];
+    __shared__ __attribute__((aligned(16))) floatx4 part[MP_NWAVES][64];
+    __shared__ float red[8];
+    __shared__ float sc[SC];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = blockIdx.x;
+
+    // weight fragments of this wave's K slice, issued before the prologue
+    const uint4 *wf = (const uint4 *)p.Wb + ((size_t)rt * KC + w * KW) * 64 + lane;
+    uint4 a[KW];
+#pragma unroll
+    for (int i = 0; i < KW; ++i) a[i] = wf[(size_t)i * 64];
+
+    // activation rows -> bf16 in LDS; row NB is zero and feeds MFMA columns NB..15
+    if constexpr (STAGE) {
+        prologue<NB, K, PRO>(p, actf, red, sc);
+        for (int e = tid; e < NR * (K / 8); e += MP_BLOCK) {
+            const int b = e / (K / 8), k = (e % (K / 8)) * 8;
+            uint4 o = make_uint4(0, 0, 0, 0);
+            if (b < NB) {
+                const float4 x0 = *(const float4 *)(actf + b * K + k), x1 = *(const float4 *)(actf + b * K + k + 4);
+                o.x = f2bf(x0.x) | ((unsigned)f2bf(x0.y) << 16);
+                o.y = f2bf(x0.z) | ((unsigned)f2bf(x0.w) << 16);
+                o.z = f2bf(x1.x) | ((unsigned)f2bf(x1.y) << 16);
+                o.w = f2bf(x1.z) | ((unsigned)f2bf(x1.w) << 16);
+            }
+            *(uint4 *)(actb + b * KP + k) = o;
+        }
+    } else {
+        for (int e = tid; e < NR * (K / 8); e += MP_BLOCK) {
+            const int b = e / (K / 8), k = (e % (K / 8)) * 8;
+            uint4 o = make_uint4(0, 0, 0, 0);
+            if (b < NB) {
+                const float *src = p.src + (size_t)b * p.src_ld + k;
+                const float4 x0 = *(const float4 *)src, x1 = *(const float4 *)(src + 4);
+                o.x = f2bf(x0.x) | ((unsigned)f2bf(x0.y) << 16);
+                o.y = f2bf(x0.z) | ((unsigned)f2bf(x0.w) << 16);
+                o.z = f2bf(x1.x) | ((unsigned)f2bf(x1.y) << 16);
+                o.w = f2bf(x1.z) | ((unsigned)f2bf(x1.w) << 16);
+            }
+            *(uint4 *)(actb + b * KP + k) = o;
+        }
+    }
+    lds_sync();
+
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const unsigned short *brow = actb + min(lane & 15, NB) * KP + 8 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < KW; ++i) {
+        const int kc = w * KW + i;
+        const uint4 bv = *(const uint4 *)(brow + kc * 32);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i]), __builtin_bit_cast(bf16x8, bv),
+                                                     acc, 0, 0, 0);
+    }
+    part[w][lane] = acc;
+    lds_sync();
+    // thread t -> (row t/16, column t%16); D[row][col] sits in lane (row/4)*16 + col, register row%4
+    const int row = tid >> 4, col = tid & 15;
+    if (col >= NB) return;
+    const int ls = (row >> 2) * 16 + col, rg = row & 3;
+    const float v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
+    const int n = rt * 16 + row;
+    if (n >= p.N) return;
+    epi_store<EPI>(p, v, n, col);
+}
+
+template <int PRO, int EPI>
+static bool b16_args_ok(const GemvP &p) {
+    if (!p.Wb || p.N <= 0) return false;
+    bool ok = true;
+    if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
+    if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
+    if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
+    if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
+    if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
+    if constexpr (PRO == PRO_LTARG_LN)
+        ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step && p.smp.cfg && p.smp.argeos;
+    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
+    if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
+    if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
+    if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
+    if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
+    return ok;
+}
+
+template <int NB, int K, int PRO, int EPI>
+static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
+    if (!b16_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_b16_kernel<NB, K, PRO, EPI>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
+#define MP_B16_OPS(NB)                                                                                                  \
+    hipError_t b16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
+    hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
+    hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_PLAIN, EPI_RESID>(p, s); }      \
+    hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_GELU>(p, s); }            \
+    hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \
+    hipError_t b16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
+    hipError_t b16_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \
+    hipError_t b16_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
+    hipError_t b16_lt_c_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LN, EPI_GELU>(p, s); }         \
+    hipError_t b16_lt_d_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTF, PRO_PLAIN, EPI_ADD_STORE>(p, s); } \
+    hipError_t b16_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }
+
+MP_B16_OPS(1)
+MP_B16_OPS(2)
+MP_B16_OPS(4)
+MP_B16_OPS(8)
+MP_B16_OPS(16)
+
+// f32 [N][K] -> bf16 fragment order [ceil(N/16)][K/32][64][8], rows >= N zero.
+__global__ void pack_b16_kernel(const float *W, int N, int K, unsigned short *out) {
+    const size_t total = (size_t)((N + 15) / 16) * (K / 32) * 64;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(e % 64);
+        const size_t frag = e / 64;
+        const int kc = (int)(frag % (K / 32)), rt = (int)(frag / (K / 32));
+        const int n = rt * 16 + (lane & 15), k0 = kc * 32 + 8 * (lane >> 4);
+        unsigned short *o = out + e * 8;
+        for (int j = 0; j < 8; ++j) o[j] = n < N ? f2bf(W[(size_t)n * K + k0 + j]) : (unsigned short)0;
+    }
+}
+
+hipError_t pack_b16(const float *W, int N, int K, unsigned short *out, hipStream_t s) {
+    if (!W || !out || N <= 0 || K % 32) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pack_b16_kernel, dim3(1024), dim3(256), 0, s, W, N, K, out);
+    return hipGetLastError();
+}
+
+}  // namespace mp

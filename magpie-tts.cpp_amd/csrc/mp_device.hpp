@@ -126,6 +126,50 @@ __device__ __forceinline__ void block_meanvar(const float (&v)[PER], float *red,
     var = Q * (1.0f / (4.f * nw));
 }
 
+// block_meanvar<PER> of a 256-thread block, computed by ONE wave bit for bit:
+// x[j] holds element lane + 64 j (j < 4 PER), i.e. virtual thread 64 (j%4) + lane's
+// value i = j/4. The four virtual waves run the same DPP trees, then the same
+// final combination, so a batched prologue (one wave per slot) reproduces the
+// batch-1 statistics exactly. Uniform result, no barrier.
+template <int PER>
+__device__ __forceinline__ void wave_block_meanvar(const float (&x)[4 * PER], float &mean, float &var) {
+    float mw[4], qw[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) m += x[v + 4 * i];
+        m *= 1.0f / PER;
+        float M2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) { const float d = x[v + 4 * i] - m; M2 += d * d; }
+        float n = (float)PER;
+        auto comb = [&](float mb, float M2b) {
+            const float d = mb - m;
+            m = m + 0.5f * d;
+            M2 = M2 + M2b + d * d * (0.5f * n);
+            n *= 2.f;
+        };
+        comb(dpp_mov<0xB1>(m), dpp_mov<0xB1>(M2));
+        comb(dpp_mov<0x4E>(m), dpp_mov<0x4E>(M2));
+        comb(dpp_mov<0x141>(m), dpp_mov<0x141>(M2));
+        comb(dpp_mov<0x140>(m), dpp_mov<0x140>(M2));
+        comb(dpp_mov<0x142, 0xA>(m), dpp_mov<0x142, 0xA>(M2));
+        comb(dpp_mov<0x143, 0xC>(m), dpp_mov<0x143, 0xC>(M2));
+        mw[v] = bcast_lane63(m);
+        qw[v] = bcast_lane63(M2);
+    }
+    const float nw = 64.f * PER;
+    float d = mw[1] - mw[0];
+    const float ma = mw[0] + 0.5f * d, Qa = qw[0] + qw[1] + d * d * (0.5f * nw);
+    d = mw[3] - mw[2];
+    const float mb = mw[2] + 0.5f * d, Qb = qw[2] + qw[3] + d * d * (0.5f * nw);
+    d = mb - ma;
+    mean = ma + 0.5f * d;
+    const float Q = Qa + Qb + d * d * nw;
+    var = Q * (1.0f / (4.f * nw));
+}
+
 // Wave-level LayerNorm statistics of 64*PER elements (PER per lane), same
 // pairwise (mean, M2) combination as block_meanvar; uniform result, no barrier.
 template <int PER>

@@ -1,0 +1,445 @@
+// Fused-projection building blocks shared by the f32 GEMV kernels
+// (mp_decode.hip) and the bf16 MFMA kernels (mp_decode_b16.hip): the prologues
+// that build the activation rows in LDS, the code pick (argmax / top-k draw) of
+// the local transformer, and the epilogues.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "mp_device.hpp"
+#include "mp_params.hpp"
+
+namespace mp {
+
+// ---------------------------------------------------------------- prologues
+// Each prologue fills act[NB][K] (LDS) with the activation vector of every slot.
+
+template <int NB, int K>
+__device__ __forceinline__ void pro_ln_vec(const float *x, const float *lnw, float eps, float *act, float *red,
+                                           float *store) {
+    // ggml_norm + ggml_mul (magpie.cpp:2255-2258): (x - mean) / sqrt(var + eps) * w
+    constexpr int PER = K / MP_BLOCK;
+    float v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = x[threadIdx.x + MP_BLOCK * i];
+    float mean, var;
+    block_meanvar<PER>(v, red, mean, var);
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int k = threadIdx.x + MP_BLOCK * i;
+        const float y = ((v[i] - mean) * rstd) * lnw[k];
+        act[k] = y;
+        if (store) store[k] = y;
+    }
+}
+
+// Masked first-max argmax of slot b's logits (magpie.cpp:1133-1145, 1243-1259):
+// 2016 and 2018..2023 always forbidden, 2017 (EOS) too while step < 4 or in
+// fixed-length mode. Every thread returns the winner.
+__device__ __forceinline__ int block_masked_argmax(const GemvP &p, int b, float *red) {
+    const int tid = threadIdx.x;
+    const float *lg = p.logits + (size_t)b * VCB;
+    const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
+    constexpr int R = (VCB + MP_BLOCK - 1) / MP_BLOCK;
+    float lv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = tid + MP_BLOCK * r;
+        lv[r] = i < VCB ? lg[i] : -INFINITY;
+    }
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = tid + MP_BLOCK * r;
+        float v = lv[r];
+        if (i >= VCB || (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos))) v = -INFINITY;
+        argmax_merge(bv, bi, v, i);
+    }
+    wave_argmax(bv, bi);
+    if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
+    lds_sync();
+    float v0 = red[0];
+    int i0 = ((int *)red)[4];
+    for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
+    lds_sync();
+    if (i0 < 0 || i0 >= VCB) i0 = 0;  // all -inf / NaN: the reference's argmax stays 0
+    return i0;
+}
+
+// One wave picks slot b's code for codebook `cb` of this frame: masked first-max
+// argmax (always, for EOS detection, magpie.cpp:1250-1259), and at temperature
+// >= 0.01 a top-k draw with the reference's sample_top_k arithmetic
+// (magpie.cpp:1072-1109): the k largest masked logits in descending order (ties by
+// ascending index), p_i = exp((l_i - l_max) / T) summed sequentially, normalised,
+// and the first i with u < cumsum_i (fallback: the k-th). Radix-select finds the
+// k-th key, a ballot compaction gathers the k candidates into LDS, a counting rank
+// orders them, lane 0 runs the two sequential float loops. scratch: 2*VCB floats.
+__device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos, int audio_eos, const Sampling &smp,
+                         int stream, int step, int cb, float *scratch, int &amax) {
+    const int lane = threadIdx.x & 63;
+    constexpr int R = (VCB + 63) / 64;
+    float lv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        lv[r] = i < VCB ? lg[i] : -INFINITY;
+    }
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        if (i >= VCB || (i >= audio_bos && i <= audio_bos + 7 && (i != audio_eos || forbid_eos))) lv[r] = -INFINITY;
+        argmax_merge(bv, bi, lv[r], i);
+    }
+    wave_argmax(bv, bi);
+    if (bi < 0 || bi >= VCB) bi = 0;
+    amax = bi;
+    if (!smp.on) return bi;
+    const float temp = smp.cfg->temperature;
+    const float M = bv;
+    const int k = min(max(smp.cfg->top_k, 1), VCB);
+    // order-preserving keys; padding lanes get 0 (below every real key)
+    unsigned key[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const unsigned u = __float_as_uint(lv[r]);
+        key[r] = (lane + 64 * r) < VCB ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0u;
+    }
+    unsigned t = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = t | (1u << bit);
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) c += key[r] >= cand;
+        if ((int)wave_sum((float)c) >= k) t = cand;
+    }
+    int cgt = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) cgt += key[r] > t;
+    const int need = k - (int)wave_sum((float)cgt);
+    float *sv = scratch;
+    int *si = (int *)(scratch + VCB);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int ties = 0, base = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const bool tie = key[r] == t;
+        const unsigned long long bt = __ballot(tie);
+        const bool sel = key[r] > t || (tie && ties + __popcll(bt & below) < need);
+        ties += __popcll(bt);
+        const unsigned long long bs = __ballot(sel);
+        if (sel) {
+            const int q = base + __popcll(bs & below);
+            sv[q] = lv[r];
+            si[q] = lane + 64 * r;
+        }
+        base += __popcll(bs);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // counting rank (descending value, ascending index), then scatter in place
+    constexpr int RK = (VCB + 63) / 64;
+    float ev[RK];
+    int ei[RK], rk[RK];
+    for (int j = 0; j < RK; ++j) {
+        const int e = lane + 64 * j;
+        if (j * 64 >= k) break;
+        if (e < k) {
+            const float v = sv[e];
+            const int i = si[e];
+            int rank = 0;
+            for (int e2 = 0; e2 < k; ++e2) {
+                const float v2 = sv[e2];
+                rank += (v2 > v) || (v2 == v && si[e2] < i);
+            }
+            rk[j] = rank;
+            ev[j] = expf((v - M) / temp);
+            ei[j] = i;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    for (int j = 0; j < RK; ++j) {
+        if (j * 64 >= k) break;
+        if (lane + 64 * j < k) { sv[rk[j]] = ev[j]; si[rk[j]] = ei[j]; }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    int code = 0;
+    if (lane == 0) {
+        float sum = 0.f;
+        for (int i = 0; i < k; ++i) sum += sv[i];
+        const float u = mp_uniform(smp.cfg->seed, stream, step, cb);
+        float cum = 0.f;
+        code = si[k - 1];
+        for (int i = 0; i < k; ++i) {
+            cum += sv[i] / sum;
+            if (u < cum) { code = si[i]; break; }
+        }
+    }
+    code = __shfl(code, 0, 64);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    return code;
+}
+
+template <int NB, int K, int PRO>
+__device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
+    const int tid = threadIdx.x;
+    if constexpr (PRO == PRO_PLAIN) {
+        for (int b = 0; b < NB; ++b)
+            for (int k = tid * 4; k < K; k += MP_BLOCK * 4)
+                *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
+        lds_sync();
+    } else if constexpr (PRO == PRO_LN && NB >= 2) {
+        // batched: wave w owns slots w, w+4, ...; wave_block_meanvar reproduces the
+        // batch-1 block statistics bit for bit (DPP only, one barrier)
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            constexpr int PER = K / 64;
+            float v[PER];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) v[i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
+            float mean, var;
+            wave_block_meanvar<PER / 4>(v, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            const bool st = p.hidden_out && blockIdx.x == 0;
+            const int s = (p.trace && blockIdx.x == 0) ? p.step[b] : 0;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int k = lane + 64 * i;
+                const float y = ((v[i] - mean) * rstd) * p.lnw[k];
+                act[b * K + k] = y;
+                if (st) p.hidden_out[(size_t)b * K + k] = y;
+                if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[((size_t)b * p.trace_steps + s) * K + k] = y;
+            }
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LN) {
+        for (int b = 0; b < NB; ++b) {
+            float *store = nullptr;
+            if (p.hidden_out && blockIdx.x == 0) store = p.hidden_out + (size_t)b * K;
+            pro_ln_vec<NB, K>(p.src + (size_t)b * p.src_ld, p.lnw, p.eps, act + b * K, red, store);
+            if (p.trace && blockIdx.x == 0) {
+                lds_sync();
+                const int s = p.step[b];
+                if (s < p.trace_steps)
+                    for (int k = tid; k < K; k += MP_BLOCK)
+                        p.trace[((size_t)b * p.trace_steps + s) * K + k] = act[b * K + k];
+            }
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_EMBED_LN && NB >= 2) {
+        static_assert(K == D, "embed prologue is d_model wide");
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            const int *c = p.codes + b * NCB;
+            const int ps = p.pos[b];
+            float x[K / 64];
+#pragma unroll
+            for (int i = 0; i < K / 64; ++i) {
+                const int k = lane + 64 * i;
+                float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
+#pragma unroll
+                for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
+                x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
+                if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
+            }
+            float mean, var;
+            wave_block_meanvar<K / 256>(x, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+            for (int i = 0; i < K / 64; ++i) {
+                const int k = lane + 64 * i;
+                act[b * K + k] = ((x[i] - mean) * rstd) * p.lnw[k];
+            }
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_EMBED_LN) {
+        static_assert(K == D, "embed prologue is d_model wide");
+        for (int b = 0; b < NB; ++b) {
+            const int *c = p.codes + b * NCB;
+            const int ps = p.pos[b];
+            float x[K / MP_BLOCK];
+#pragma unroll
+            for (int i = 0; i < K / MP_BLOCK; ++i) {
+                const int k = tid + MP_BLOCK * i;
+                float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
+#pragma unroll
+                for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
+                x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
+                if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
+            }
+            // LN over the freshly built x
+            float mean, var;
+            block_meanvar<K / MP_BLOCK>(x, red, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+            for (int i = 0; i < K / MP_BLOCK; ++i) {
+                const int k = tid + MP_BLOCK * i;
+                act[b * K + k] = ((x[i] - mean) * rstd) * p.lnw[k];
+            }
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LTX_LN && NB >= 2) {
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            float X[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = lane + 64 * i;
+                X[i] = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+                if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X[i];
+            }
+            float mean, var;
+            wave_block_meanvar<1>(X, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LTARG_LN && NB >= 2) {
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            int amax;
+            const int code = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos,
+                                       p.smp, b, p.step[b], p.cb - 1, sc + w * 2 * VCB, amax);
+            if (blockIdx.x == 0 && lane == 0) {
+                p.codes_cur[b * NCB + p.cb - 1] = code;
+                if (amax == p.audio_eos) p.smp.argeos[b] = 1;
+            }
+            float X[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = lane + 64 * i;
+                X[i] = p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+                if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X[i];
+            }
+            float mean, var;
+            wave_block_meanvar<1>(X, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LT_ATTN && NB >= 2) {
+        const int lane = tid & 63, w = tid >> 6;
+        const int nk = p.cb + 1;
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            const float4 q4 = *(const float4 *)(p.ltq + (size_t)b * LTD + 4 * lane);
+            float sj[NCB];
+#pragma unroll
+            for (int j = 0; j < NCB; ++j)
+                sj[j] = j < nk ? wave_sum(dotv(q4, *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane))) *
+                                     (1.0f / 16.0f)
+                               : -INFINITY;
+            float m = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < NCB; ++j) m = fmaxf(m, sj[j]);
+            float l = 0.f;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < NCB; ++j) {
+                if (j >= nk) break;
+                const float e = expf(sj[j] - m);
+                l += e;
+                const float4 v4 = *(const float4 *)(p.ltv + ((size_t)b * NCB + j) * LTD + 4 * lane);
+                a.x += e * v4.x; a.y += e * v4.y; a.z += e * v4.z; a.w += e * v4.w;
+            }
+            *(float4 *)(act + b * K + 4 * lane) = make_float4(a.x / l, a.y / l, a.z / l, a.w / l);
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LTX_LN) {
+        static_assert(K == LTD, "LT is 256 wide");
+        for (int b = 0; b < NB; ++b) {
+            const int k = tid;
+            const float X = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+            if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X;
+            const float xv[1] = {X};
+            float mean, var;
+            block_meanvar<1>(xv, red, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LT_ATTN) {
+        static_assert(K == LTD, "LT is 256 wide");
+        const int lane = tid & 63, w = tid >> 6;
+        const int nk = p.cb + 1;
+        for (int b = 0; b < NB; ++b) {
+            const float4 q4 = *(const float4 *)(p.ltq + (size_t)b * LTD + 4 * lane);
+            for (int j = w; j < nk; j += MP_NWAVES) {
+                float v = dotv(q4, *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane));
+                v = wave_sum(v);
+                if (lane == 0) sc[j] = v * (1.0f / 16.0f);  // 1/sqrt(256)
+            }
+            lds_sync();
+            float m = -INFINITY;
+            for (int j = 0; j < nk; ++j) m = fmaxf(m, sc[j]);
+            float l = 0.f, a = 0.f;
+            for (int j = 0; j < nk; ++j) {
+                const float e = expf(sc[j] - m);
+                l += e;
+                a += e * p.ltv[((size_t)b * NCB + j) * LTD + tid];
+            }
+            act[b * K + tid] = a / l;
+            lds_sync();
+        }
+    } else if constexpr (PRO == PRO_LTARG_LN) {
+        static_assert(K == LTD, "LT is 256 wide");
+        const int lane = tid & 63, w = tid >> 6;
+        for (int b = 0; b < NB; ++b) {
+            int code;
+            if (p.smp.on) {
+                if (w == 0) {
+                    int amax;
+                    code = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos,
+                                     p.audio_eos, p.smp, b, p.step[b], p.cb - 1, sc, amax);
+                    if (lane == 0) {
+                        red[0] = __int_as_float(code);
+                        if (blockIdx.x == 0 && amax == p.audio_eos) p.smp.argeos[b] = 1;
+                    }
+                }
+                lds_sync();
+                code = __float_as_int(red[0]);
+                lds_sync();
+            } else {
+                code = block_masked_argmax(p, b, red);  // codebook cb-1's code
+            }
+            if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb - 1] = code;
+            const int k = tid;
+            const float X = p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
+            if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X;
+            const float xv[1] = {X};
+            float mean, var;
+            block_meanvar<1>(xv, red, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
+        }
+        lds_sync();
+    }
+}
+
+// Epilogue of output (row n, slot b) of a fused projection.
+template <int EPI>
+__device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b) {
+    if constexpr (EPI == EPI_STORE) p.out[(size_t)b * p.out_ld + n] = v;
+    else if constexpr (EPI == EPI_BIAS) p.out[(size_t)b * p.out_ld + n] = v + p.bias[n];
+    else if constexpr (EPI == EPI_GELU) p.out[(size_t)b * p.out_ld + n] = gelu_tanh(v);
+    else if constexpr (EPI == EPI_RESID) p.resid[(size_t)b * D + n] = v + p.resid[(size_t)b * D + n];
+    else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
+    else if constexpr (EPI == EPI_QKV) {
+        const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + p.pos[b]) * D;
+        if (n < D) p.out[(size_t)b * D + n] = v;
+        else if (n < 2 * D) p.kc[slot + n - D] = v;
+        else p.vc[slot + n - 2 * D] = v;
+    } else if constexpr (EPI == EPI_LTQKV) {
+        if (n < LTD) p.lq[(size_t)b * LTD + n] = v;
+        else if (n < 2 * LTD) p.lk[((size_t)b * NCB + p.cb) * LTD + n - LTD] = v;
+        else p.lv[((size_t)b * NCB + p.cb) * LTD + n - 2 * LTD] = v;
+    }
+}
+
+}  // namespace mp

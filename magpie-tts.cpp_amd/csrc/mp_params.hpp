@@ -74,6 +74,7 @@ __host__ __device__ inline float mp_uniform(unsigned long long seed, int stream,
 
 struct GemvP {
     const float *W;
+    const unsigned short *Wb;  // bf16 weights in MFMA fragment order (mp_decode_b16.hip), or null
     int N;
     const float *bias;
     // prologue inputs

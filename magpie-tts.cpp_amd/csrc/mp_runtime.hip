@@ -39,6 +39,20 @@ MP_DECL_OPS(1)
 MP_DECL_OPS(2)
 MP_DECL_OPS(4)
 MP_DECL_OPS(8)
+hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
+#define MP_DECL_B16(NB)                                                                                      \
+    hipError_t b16_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t b16_qkv_##NB(const GemvP &, hipStream_t);      \
+    hipError_t b16_oproj_##NB(const GemvP &, hipStream_t); hipError_t b16_ff1_##NB(const GemvP &, hipStream_t);          \
+    hipError_t b16_ff2_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_a_##NB(const GemvP &, hipStream_t);           \
+    hipError_t b16_lt_ag_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_b_##NB(const GemvP &, hipStream_t);         \
+    hipError_t b16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_d_##NB(const GemvP &, hipStream_t);          \
+    hipError_t b16_lt_e_##NB(const GemvP &, hipStream_t);
+MP_DECL_B16(1)
+MP_DECL_B16(2)
+MP_DECL_B16(4)
+MP_DECL_B16(8)
+MP_DECL_B16(16)
+hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
@@ -53,7 +67,14 @@ struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff2, lt_in0, lt_a, lt_ag, lt
 #define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_ag_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
 static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
-static const OpTable &table_for(int NB) { return kTables[NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : 3]; }
+// bf16 weight mode: every projection on MFMA except the f32 LT in_proj
+#define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, b16_ff1_##NB, b16_ff2_##NB, \
+                           op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_ag_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
+                           b16_lt_d_##NB, b16_lt_e_##NB }
+static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
+                                      MP_TABLE_B16(16)};
+static int nb_index(int NB) { return NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : NB == 8 ? 3 : 4; }
+static const OpTable &table_for(int NB, bool b16) { return b16 ? kTablesB16[nb_index(NB)] : kTables[nb_index(NB)]; }
 
 struct EncLayerW { const float *norm_self, *qkv, *o, *norm_ff, *ff1, *ff2; };
 struct DecLayerW { const float *norm_self, *qkv, *o, *norm_xq, *xq, *xkv, *xo, *norm_xmem, *norm_ff, *ff1, *ff2; };
@@ -70,6 +91,12 @@ struct Model {
         *lt_out_b;
     float *lt_ptab = nullptr;  // [8][2024][256] = in_proj(audio_emb[c][v]) + b, built at load
     std::vector<float *> xq_t;  // per layer W_q^T [768][128] (for K' = K W_q)
+    // weight mode MP_WEIGHTS_BF16: decode projections repacked as bf16 MFMA fragments
+    int weight_mode = 0;
+    unsigned short *pk_arena = nullptr;
+    std::vector<const unsigned short *> pk_qkv, pk_o, pk_ff1, pk_ff2;
+    const unsigned short *pk_lt_qkv = nullptr, *pk_lt_o = nullptr, *pk_lt_ff1 = nullptr, *pk_lt_ff2 = nullptr,
+                         *pk_lt_out = nullptr;  // lt_out: [8][127 tiles][8][64][8]
     float *arena = nullptr;
     size_t arena_bytes = 0;
 };
@@ -165,6 +192,43 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 // ------------------------------------------------------------------ weights
 // Tensor names and mapping: create_tensors (magpie.cpp:572-672).
+// Size (elements) of one packed [N][K] matrix: [ceil(N/16)][K/32][64][8].
+size_t pk_elems(int N, int K) { return (size_t)((N + 15) / 16) * 16 * K; }
+
+int pack_weights(mp_dev *dev) {
+    mp::Model &m = dev->m;
+    if (m.pk_arena) { hipFree(m.pk_arena); m.pk_arena = nullptr; }
+    const int L = m.dec_layers;
+    const size_t per_layer = pk_elems(2304, 768) + pk_elems(768, 768) + pk_elems(3072, 768) + pk_elems(768, 3072);
+    const size_t lt = pk_elems(768, 256) + pk_elems(256, 256) + pk_elems(1024, 256) + pk_elems(256, 1024) +
+                      8 * pk_elems(2024, 256);
+    HIPCHK(hipMalloc(&m.pk_arena, (per_layer * L + lt) * 2));
+    unsigned short *cur = m.pk_arena;
+    auto pack = [&](const float *W, int N, int K) -> const unsigned short * {
+        unsigned short *dst = cur;
+        cur += pk_elems(N, K);
+        return mp::pack_b16(W, N, K, dst, dev->stream) == hipSuccess ? dst : nullptr;
+    };
+    m.pk_qkv.assign(L, nullptr); m.pk_o.assign(L, nullptr); m.pk_ff1.assign(L, nullptr); m.pk_ff2.assign(L, nullptr);
+    for (int l = 0; l < L; ++l) {
+        m.pk_qkv[l] = pack(m.dec[l].qkv, 2304, 768);
+        m.pk_o[l] = pack(m.dec[l].o, 768, 768);
+        m.pk_ff1[l] = pack(m.dec[l].ff1, 3072, 768);
+        m.pk_ff2[l] = pack(m.dec[l].ff2, 768, 3072);
+        if (!m.pk_qkv[l] || !m.pk_o[l] || !m.pk_ff1[l] || !m.pk_ff2[l]) return fail(dev, MP_ERR_HIP, "bf16 pack failed");
+    }
+    m.pk_lt_qkv = pack(m.lt_qkv, 768, 256);
+    m.pk_lt_o = pack(m.lt_o, 256, 256);
+    m.pk_lt_ff1 = pack(m.lt_ff1, 1024, 256);
+    m.pk_lt_ff2 = pack(m.lt_ff2, 256, 1024);
+    m.pk_lt_out = cur;
+    for (int c = 0; c < 8; ++c)
+        if (!pack(m.lt_out_w + (size_t)c * 2024 * 256, 2024, 256)) return fail(dev, MP_ERR_HIP, "bf16 pack failed");
+    if (!m.pk_lt_qkv || !m.pk_lt_o || !m.pk_lt_ff1 || !m.pk_lt_ff2) return fail(dev, MP_ERR_HIP, "bf16 pack failed");
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    return MP_OK;
+}
+
 int load_model(mp_dev *dev, const char *path) {
     mp::Gguf g;
     std::string err;
@@ -340,7 +404,7 @@ int load_model(mp_dev *dev, const char *path) {
 // ------------------------------------------------------------------ batch state
 int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     free_batch(dev);
-    const int NB = B <= 1 ? 1 : B <= 2 ? 2 : B <= 4 ? 4 : 8;
+    const int NB = B <= 1 ? 1 : B <= 2 ? 2 : B <= 4 ? 4 : B <= 8 ? 8 : 16;
     const int L = dev->m.dec_layers;
     dev->B = B;
     dev->NB = NB;
@@ -394,8 +458,10 @@ mp::GemvP gemv_base(mp_dev *dev) {
 int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     const mp::Model &m = dev->m;
     const int NB = dev->NB, L = m.dec_layers;
-    const mp::OpTable &tb = mp::table_for(NB);
-    const double F = 4.0, act = (double)NB;
+    const bool b16 = m.weight_mode == MP_WEIGHTS_BF16;
+    const mp::OpTable &tb = mp::table_for(NB, b16);
+    // algorithmic bytes: weights at their stored width, activations f32
+    const double F = b16 ? 2.0 : 4.0, A = 4.0, act = (double)NB;
     if (record) dev->ops.clear();
     auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
         if (record) {
@@ -412,11 +478,11 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         mp::GemvP g = gemv_base(dev);
         g.layer = l;
         // LN + QKV (+ frame embedding on layer 0) + KV append   (3415-3442)
-        g.W = W.qkv; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
+        g.W = W.qkv; g.Wb = b16 ? m.pk_qkv[l] : nullptr; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
         g.kc = dev->kc; g.vc = dev->vc;
         if (l == 0) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
         if ((rc = run(l == 0 ? "qkv_embed" : "qkv", l == 0 ? tb.qkv_embed : tb.qkv, g,
-                      F * (2304.0 * 768 + act * (768 + 2304)))) != MP_OK) return rc;
+                      F * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
         // split-K self-attention over the cache, combined in-launch (3457-3476)
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->part, dev->nch, dev->ndone, NB,
                     dev->sa_out, dev->sa_cnt, dev->nch * 12 * NB <= 256};
@@ -429,25 +495,25 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         HIPCHK(mp::op_sa_attn(a, NB, s));
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
-        g.W = W.o; g.N = 768; g.resid = dev->x; g.src = dev->sa_out; g.src_ld = 768;
-        if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768 + act * 768 * 3))) != MP_OK) return rc;
+        g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.src = dev->sa_out; g.src_ld = 768;
+        if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) return rc;
         // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
         mp::XaP xp{dev->x, dev->x2, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
         if (record) {
             mp::OpRec r{};
             r.name = "xa"; r.kind = mp::K_XA; r.x = xp; r.B = NB;
-            r.bytes = F * act * (768.0 * 2 + 2.0 * 768 * dev->Tmax);
+            r.bytes = A * act * (768.0 * 2 + 2.0 * 768 * dev->Tmax);
             dev->ops.push_back(r);
         }
         HIPCHK(mp::op_xa(xp, NB, s));
         // LN + FFN up + GELU (1796-1799)
         g = gemv_base(dev); g.layer = l;
-        g.W = W.ff1; g.N = 3072; g.lnw = W.norm_ff; g.src = dev->x2; g.src_ld = 768; g.out = dev->h; g.out_ld = 3072;
-        if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768 + act * (768 + 3072)))) != MP_OK) return rc;
+        g.W = W.ff1; g.Wb = b16 ? m.pk_ff1[l] : nullptr; g.N = 3072; g.lnw = W.norm_ff; g.src = dev->x2; g.src_ld = 768; g.out = dev->h; g.out_ld = 3072;
+        if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
         // FFN down + residual (1805, 3525): x = x2 + W2 h
         g = gemv_base(dev); g.layer = l;
-        g.W = W.ff2; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.out = dev->x; g.out_ld = 768; g.addsrc = dev->x2;
-        if ((rc = run("ff2", tb.ff2, g, F * (768.0 * 3072 + act * (3072 + 2 * 768)))) != MP_OK) return rc;
+        g.W = W.ff2; g.Wb = b16 ? m.pk_ff2[l] : nullptr; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.out = dev->x; g.out_ld = 768; g.addsrc = dev->x2;
+        if ((rc = run("ff2", tb.ff2, g, F * (768.0 * 3072) + A * act * ((3072 + 2 * 768)))) != MP_OK) return rc;
     }
     // final LN -> hidden (4394) fused into LT in_proj (1162-1163)
     {
@@ -455,38 +521,39 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.lnw = m.dec_norm_out; g.src = dev->x; g.src_ld = 768;
         g.hidden_out = dev->hidden; g.out = dev->lt_s; g.out_ld = 9 * 256;
         if (dev->trace) { g.trace = dev->trace; g.trace_steps = dev->max_steps + 1; }
-        if ((rc = run("lt_in0", tb.lt_in0, g, F * (256.0 * 768 + act * (768 + 768 + 256)))) != MP_OK) return rc;
+        if ((rc = run("lt_in0", tb.lt_in0, g, A * (256.0 * 768 + 256) + A * act * ((768 + 768 + 256)))) != MP_OK) return rc;
     }
     for (int cb = 0; cb < 8; ++cb) {
         // cb > 0: codebook cb-1's masked argmax + table gather fused into this prologue
         mp::GemvP g = gemv_base(dev);
         g.cb = cb;
-        g.W = m.lt_qkv; g.N = 768; g.lt_s = dev->lt_s; g.lt_pos = m.lt_pos; g.ltX = dev->ltX; g.lnw = m.lt_norm_self;
+        g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = dev->lt_s; g.lt_pos = m.lt_pos; g.ltX = dev->ltX; g.lnw = m.lt_norm_self;
         g.lq = dev->ltq; g.lk = dev->ltk; g.lv = dev->ltv;
         if (cb > 0) { g.logits = dev->logits; g.codes_cur = dev->codes_cur; g.ptab = m.lt_ptab; }
         if ((rc = run(cb == 0 ? "lt_a" : "lt_ag", cb == 0 ? tb.lt_a : tb.lt_ag, g,
-                      F * (768.0 * 256 + act * (256 * 3 + 768 + (cb > 0 ? 2024 + 256 : 256))))) != MP_OK) return rc;
+                      F * (768.0 * 256) + A * act * ((256 * 3 + 768 + (cb > 0 ? 2024 + 256 : 256))))) != MP_OK) return rc;
         g = gemv_base(dev); g.cb = cb;
-        g.W = m.lt_o; g.N = 256; g.ltq = dev->ltq; g.ltk = dev->ltk; g.ltv = dev->ltv; g.out = dev->ltY; g.out_ld = 256;
+        g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = dev->ltq; g.ltk = dev->ltk; g.ltv = dev->ltv; g.out = dev->ltY; g.out_ld = 256;
         g.addsrc = dev->ltX;
-        if ((rc = run("lt_b", tb.lt_b, g, F * (256.0 * 256 + act * (256 * (2 * cb + 5))))) != MP_OK) return rc;
+        if ((rc = run("lt_b", tb.lt_b, g, F * (256.0 * 256) + A * act * ((256 * (2 * cb + 5))))) != MP_OK) return rc;
         g = gemv_base(dev); g.cb = cb;
-        g.W = m.lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = dev->ltY; g.src_ld = 256; g.out = dev->ltf; g.out_ld = 1024;
-        if ((rc = run("lt_c", tb.lt_c, g, F * (1024.0 * 256 + act * (256 + 1024)))) != MP_OK) return rc;
+        g.W = m.lt_ff1; g.Wb = m.pk_lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = dev->ltY; g.src_ld = 256; g.out = dev->ltf; g.out_ld = 1024;
+        if ((rc = run("lt_c", tb.lt_c, g, F * (1024.0 * 256) + A * act * ((256 + 1024)))) != MP_OK) return rc;
         g = gemv_base(dev); g.cb = cb;
-        g.W = m.lt_ff2; g.N = 256; g.src = dev->ltf; g.src_ld = 1024; g.out = dev->lty2; g.out_ld = 256; g.addsrc = dev->ltY;
-        if ((rc = run("lt_d", tb.lt_d, g, F * (256.0 * 1024 + act * (1024 + 512)))) != MP_OK) return rc;
+        g.W = m.lt_ff2; g.Wb = m.pk_lt_ff2; g.N = 256; g.src = dev->ltf; g.src_ld = 1024; g.out = dev->lty2; g.out_ld = 256; g.addsrc = dev->ltY;
+        if ((rc = run("lt_d", tb.lt_d, g, F * (256.0 * 1024) + A * act * ((1024 + 512)))) != MP_OK) return rc;
         g = gemv_base(dev); g.cb = cb;
-        g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024; g.bias = m.lt_out_b + (size_t)cb * 2024;
+        g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024;
+        g.Wb = b16 ? m.pk_lt_out + (size_t)cb * pk_elems(2024, 256) : nullptr; g.bias = m.lt_out_b + (size_t)cb * 2024;
         g.src = dev->lty2; g.src_ld = 256; g.out = dev->logits; g.out_ld = 2024;
-        if ((rc = run("lt_e", tb.lt_e, g, F * (2024.0 * 256 + 2024 + act * (256 + 2024)))) != MP_OK) return rc;
+        if ((rc = run("lt_e", tb.lt_e, g, F * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK) return rc;
     }
     mp::FinP f{dev->logits, dev->codes_cur, dev->codes_prev, dev->codes_out, dev->step, dev->pos, dev->done,
                dev->nframes, dev->ndone, dev->max_steps, dev->params.ignore_eos, m.audio_bos, m.audio_eos, NB,
                mp::Sampling{dev->params.temperature >= 0.01f, dev->smpcfg, dev->argeos}};
     if (record) {
         mp::OpRec r{};
-        r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = F * act * 2024;
+        r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = A * act * 2024;
         dev->ops.push_back(r);
     }
     HIPCHK(mp::op_finalize(f, NB, s));
@@ -619,12 +686,25 @@ int mp_hip_init(int device, mp_dev **out) {
     return MP_OK;
 }
 
-int mp_hip_load_model(mp_dev *dev, const char *path) {
+int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     if (!dev || !path) return MP_ERR_ARG;
+    if (weight_mode != MP_WEIGHTS_AS_STORED && weight_mode != MP_WEIGHTS_BF16)
+        return fail(dev, MP_ERR_ARG, "unknown weight mode");
     HIPCHK(hipSetDevice(dev->device));
     free_batch(dev);
-    return load_model(dev, path);
+    dev->loaded = false;
+    dev->m.weight_mode = MP_WEIGHTS_AS_STORED;
+    if (int rc = load_model(dev, path)) return rc;
+    if (weight_mode == MP_WEIGHTS_BF16) {
+        dev->loaded = false;
+        if (int rc = pack_weights(dev)) return rc;
+        dev->m.weight_mode = MP_WEIGHTS_BF16;
+        dev->loaded = true;
+    }
+    return MP_OK;
 }
+
+int mp_hip_load_model(mp_dev *dev, const char *path) { return mp_hip_load_model_ex(dev, path, MP_WEIGHTS_AS_STORED); }
 
 int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes) {
     if (!dev || !dev->loaded) return MP_ERR_STATE;
@@ -634,6 +714,8 @@ int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *wei
     return MP_OK;
 }
 
+int mp_hip_weight_mode(mp_dev *dev) { return dev && dev->loaded ? dev->m.weight_mode : MP_ERR_STATE; }
+
 void mp_hip_free(mp_dev *dev) {
     if (!dev) return;
     hipSetDevice(dev->device);
@@ -641,6 +723,7 @@ void mp_hip_free(mp_dev *dev) {
     free_batch(dev);
     if (dev->m.arena) hipFree(dev->m.arena);
     if (dev->m.lt_ptab) hipFree(dev->m.lt_ptab);
+    if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
     for (float *p : dev->m.xq_t) hipFree(p);
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
     if (dev->stream) hipStreamDestroy(dev->stream);
@@ -653,8 +736,9 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
                        int tmax, const mp_params *params) {
     if (!dev) return MP_ERR_ARG;
     if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
-    if (!tokens || !n_tokens || !speaker || B < 1 || B > 8 || tmax < 1 || !params)
-        return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..8)");
+    const int bmax = dev->m.weight_mode == MP_WEIGHTS_BF16 ? 16 : 8;
+    if (!tokens || !n_tokens || !speaker || B < 1 || B > bmax || tmax < 1 || !params)
+        return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..8, 1..16 with bf16 weights)");
     if (params->temperature >= 0.01f && (params->top_k < 1 || params->top_k > mp::VCB))
         return fail(dev, MP_ERR_ARG, "top_k must be in 1..2024 when sampling");
     int Tmax = 0;

@@ -57,6 +57,8 @@ SYMBOLS = [
     ("mp_hip_device_count", _I, [ctypes.POINTER(_I)]),
     ("mp_hip_init", _I, [_I, ctypes.POINTER(_P)]),
     ("mp_hip_load_model", _I, [_P, ctypes.c_char_p]),
+    ("mp_hip_load_model_ex", _I, [_P, ctypes.c_char_p, _I]),
+    ("mp_hip_weight_mode", _I, [_P]),
     ("mp_hip_model_info", _I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_size_t)]),
     ("mp_hip_free", None, [_P]),
     ("mp_hip_error", ctypes.c_char_p, [_P]),
@@ -137,14 +139,21 @@ class SynthResult:
 class Device:
     """One GPU with resident Magpie weights (magpie_init_with_backend, magpie.cpp:781)."""
 
-    def __init__(self, model_path: str, device: int = 0):
+    WEIGHT_MODES = {"f32": 0, "as_stored": 0, "bf16": 1}
+
+    def __init__(self, model_path: str, device: int = 0, weights: str = "f32"):
+        """weights: "f32" (as stored, widened to f32) or "bf16" (decode projections
+        on bf16 MFMA, activations rounded to bf16; batches up to 16)."""
+        if weights not in self.WEIGHT_MODES:
+            raise ValueError(f"weights must be one of {sorted(self.WEIGHT_MODES)}")
         self.lib = load_library()
         h = ctypes.c_void_p()
         rc = self.lib.mp_hip_init(device, ctypes.byref(h))
         if rc != MP_OK or not h.value:
             raise MagpieError(f"mp_hip_init(device={device}) failed ({_ERRS.get(rc, rc)}): no usable HIP device")
         self.h = h
-        self._check(self.lib.mp_hip_load_model(self.h, model_path.encode()))
+        self.weights = weights
+        self._check(self.lib.mp_hip_load_model_ex(self.h, model_path.encode(), self.WEIGHT_MODES[weights]))
 
     def _check(self, rc: int) -> None:
         if rc != MP_OK:

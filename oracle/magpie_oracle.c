@@ -60,6 +60,32 @@ static void matmul(const float *W, const float *bias, const float *X, float *Y, 
     }
 }
 
+// f32 -> bf16 -> f32, round-to-nearest-even (ggml_compute_fp32_to_bf16)
+static float bf16r(float x) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    if ((u & 0x7fffffff) > 0x7f800000) u = (u | 0x00400000) & 0xffff0000u;  // NaN stays NaN
+    else u = (u + (0x7fff + ((u >> 16) & 1))) & 0xffff0000u;
+    memcpy(&x, &u, 4);
+    return x;
+}
+static float *bf16_copy(const float *w, size_t n) {
+    float *r = malloc(sizeof(float) * n);
+    for (size_t i = 0; i < n; ++i) r[i] = bf16r(w[i]);
+    return r;
+}
+// Projection in weight mode 1: bf16 weights x bf16-rounded activations,
+// products exact, accumulated like matmul() (ggml's BF16 mul_mat rounds src1 to
+// its vec_dot_type BF16 the same way).
+static void matmul_sel(const float *W, const float *Wh, const float *bias, const float *X, float *Y, int M, int N,
+                       int K) {
+    if (!Wh) { matmul(W, bias, X, Y, M, N, K); return; }
+    float *Xh = malloc(sizeof(float) * (size_t)M * K);
+    for (size_t i = 0; i < (size_t)M * K; ++i) Xh[i] = bf16r(X[i]);
+    matmul(Wh, bias, Xh, Y, M, N, K);
+    free(Xh);
+}
+
 // ggml_norm(eps) * w (magpie.cpp:2237-2259): mean/var accumulated in double.
 static void layernorm(const float *x, const float *w, float *y, int K, float eps) {
     double s = 0.0;
@@ -127,6 +153,7 @@ typedef struct {
 } enc_layer;
 typedef struct {
     float *norm_self, *qkv, *o, *norm_xq, *xq, *xkv, *xo, *norm_xmem, *norm_ff, *ff1, *ff2;
+    float *qkv_h, *o_h, *ff1_h, *ff2_h;  // bf16-rounded copies (weight mode 1)
 } dec_layer;
 
 struct orc_model {
@@ -141,6 +168,9 @@ struct orc_model {
     dec_layer *dec;
     float *lt_in_w, *lt_in_b, *lt_pos, *lt_norm_self, *lt_qkv, *lt_o, *lt_norm_ff, *lt_ff1, *lt_ff2;
     float *lt_out_w[8], *lt_out_b[8];
+    // weight mode 1 (bf16 decode projections): rounded copies, NULL in mode 0
+    int half;
+    float *lt_qkv_h, *lt_o_h, *lt_ff1_h, *lt_ff2_h, *lt_out_w_h[8];
     float **owned;
     int n_owned, cap_owned;
 };
@@ -249,8 +279,42 @@ orc_model *orc_load(const char *path) {
     return m;
 }
 
+static void free_half(orc_model *m) {
+    for (int l = 0; l < m->dec_layers; ++l) {
+        dec_layer *L = &m->dec[l];
+        free(L->qkv_h); free(L->o_h); free(L->ff1_h); free(L->ff2_h);
+        L->qkv_h = L->o_h = L->ff1_h = L->ff2_h = NULL;
+    }
+    free(m->lt_qkv_h); free(m->lt_o_h); free(m->lt_ff1_h); free(m->lt_ff2_h);
+    m->lt_qkv_h = m->lt_o_h = m->lt_ff1_h = m->lt_ff2_h = NULL;
+    for (int c = 0; c < 8; ++c) { free(m->lt_out_w_h[c]); m->lt_out_w_h[c] = NULL; }
+    m->half = 0;
+}
+
+int orc_set_weight_mode(orc_model *m, int mode) {
+    if (!m || mode < 0 || mode > 1) return -1;
+    free_half(m);
+    if (mode == 0) return 0;
+    const int d = m->d, dff = m->dff, D = m->lt_dim, F = m->lt_ffn;
+    for (int l = 0; l < m->dec_layers; ++l) {
+        dec_layer *L = &m->dec[l];
+        L->qkv_h = bf16_copy(L->qkv, (size_t)3 * d * d);
+        L->o_h = bf16_copy(L->o, (size_t)d * d);
+        L->ff1_h = bf16_copy(L->ff1, (size_t)dff * d);
+        L->ff2_h = bf16_copy(L->ff2, (size_t)d * dff);
+    }
+    m->lt_qkv_h = bf16_copy(m->lt_qkv, (size_t)3 * D * D);
+    m->lt_o_h = bf16_copy(m->lt_o, (size_t)D * D);
+    m->lt_ff1_h = bf16_copy(m->lt_ff1, (size_t)F * D);
+    m->lt_ff2_h = bf16_copy(m->lt_ff2, (size_t)D * F);
+    for (int c = 0; c < 8; ++c) m->lt_out_w_h[c] = bf16_copy(m->lt_out_w[c], (size_t)m->vocab_cb * D);
+    m->half = 1;
+    return 0;
+}
+
 void orc_free(orc_model *m) {
     if (!m) return;
+    free_half(m);
     for (int i = 0; i < m->n_owned; ++i) free(m->owned[i]);
     free(m->owned);
     free(m->enc);
@@ -367,14 +431,15 @@ static void decoder_layer(const orc_model *m, dstate *s, int l, float *x, int M,
     float *f = malloc(sizeof(float) * (size_t)M * dff);
     float *Kc = s->kc + (size_t)l * s->max_seq * d, *Vc = s->vc + (size_t)l * s->max_seq * d;
     // self-attention: LN -> qkv -> cache append -> attention over [0, pos] -> o_net (3395-3480)
+    const int hm = m->half && M == 1;  // decode steps only; the 110-frame prefill stays f32
     layernorm_rows(x, L->norm_self, h, M, d, m->eps);
-    matmul(L->qkv, NULL, h, qkv, M, 3 * d, d);
+    matmul_sel(L->qkv, hm ? L->qkv_h : NULL, NULL, h, qkv, M, 3 * d, d);
     for (int r = 0; r < M; ++r) {
         memcpy(Kc + (size_t)(pos0 + r) * d, qkv + (size_t)r * 3 * d + d, sizeof(float) * d);
         memcpy(Vc + (size_t)(pos0 + r) * d, qkv + (size_t)r * 3 * d + 2 * d, sizeof(float) * d);
     }
     causal_mha(qkv, M, d, m->dec_heads, att, pos0, Kc, Vc);
-    matmul(L->o, NULL, att, o, M, d, d);
+    matmul_sel(L->o, hm ? L->o_h : NULL, NULL, att, o, M, d, d);
     for (size_t i = 0; i < (size_t)M * d; ++i) x[i] = o[i] + x[i];
     // cross-attention with cached K/V (1713-1767): 1 head x 128, no mask
     layernorm_rows(x, L->norm_xq, h, M, d, m->eps);
@@ -395,9 +460,9 @@ static void decoder_layer(const orc_model *m, dstate *s, int l, float *x, int M,
     for (size_t i = 0; i < (size_t)M * d; ++i) x[i] = o[i] + x[i];
     // pointwise conv-FFN (1791-1805)
     layernorm_rows(x, L->norm_ff, h, M, d, m->eps);
-    matmul(L->ff1, NULL, h, f, M, dff, d);
+    matmul_sel(L->ff1, hm ? L->ff1_h : NULL, NULL, h, f, M, dff, d);
     gelu_inplace(f, (size_t)M * dff);
-    matmul(L->ff2, NULL, f, o, M, d, dff);
+    matmul_sel(L->ff2, hm ? L->ff2_h : NULL, NULL, f, o, M, d, dff);
     for (size_t i = 0; i < (size_t)M * d; ++i) x[i] = o[i] + x[i];
     free(h); free(qkv); free(att); free(o); free(q); free(f);
 }
@@ -475,18 +540,18 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, f
     for (int cb = 0; cb < 8; ++cb) {
         for (int i = 0; i < D; ++i) X[i] = s[cb][i] + m->lt_pos[(size_t)cb * D + i];
         layernorm(X, m->lt_norm_self, h, D, m->eps);
-        matmul(m->lt_qkv, NULL, h, qkv, 1, 3 * D, D);
+        matmul_sel(m->lt_qkv, m->lt_qkv_h, NULL, h, qkv, 1, 3 * D, D);
         memcpy(kk[cb], qkv + D, sizeof(float) * D);
         memcpy(vv[cb], qkv + 2 * D, sizeof(float) * D);
         attend(qkv, &kk[0][0], &vv[0][0], cb + 1, D, D, 1.0 / sqrt((double)D), a, sb, pb);
-        matmul(m->lt_o, NULL, a, Y, 1, D, D);
+        matmul_sel(m->lt_o, m->lt_o_h, NULL, a, Y, 1, D, D);
         for (int i = 0; i < D; ++i) Y[i] = Y[i] + X[i];
         layernorm(Y, m->lt_norm_ff, h, D, m->eps);
-        matmul(m->lt_ff1, NULL, h, f, 1, F, D);
+        matmul_sel(m->lt_ff1, m->lt_ff1_h, NULL, h, f, 1, F, D);
         gelu_inplace(f, (size_t)F);
-        matmul(m->lt_ff2, NULL, f, y2, 1, D, F);
+        matmul_sel(m->lt_ff2, m->lt_ff2_h, NULL, f, y2, 1, D, F);
         for (int i = 0; i < D; ++i) y2[i] = y2[i] + Y[i];
-        matmul(m->lt_out_w[cb], m->lt_out_b[cb], y2, logits, 1, V, D);
+        matmul_sel(m->lt_out_w[cb], m->lt_out_w_h[cb], m->lt_out_b[cb], y2, logits, 1, V, D);
         // forbidden tokens (1133-1145) and first-max argmax (1250-1259)
         for (int t = m->audio_bos; t <= m->audio_bos + 7 && t < V; ++t)
             if (t != m->audio_eos || forbid_eos) logits[t] = -INFINITY;

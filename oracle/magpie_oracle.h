@@ -28,6 +28,13 @@ typedef struct orc_codec orc_codec;
 void orc_set_mode(int acc64, int gelu_f16, int n_threads);
 
 orc_model *orc_load(const char *gguf_path);
+// Weight mode 1 = this build's bf16 decode path (no reference file format: the
+// reference converter writes F32/F16/Q8_0/Q4_0): in decode steps (BOS included)
+// the projections qkv/o/ff1/ff2 of every decoder layer and of the LT layer, and
+// the 8 LT output projections, use bf16-rounded weights and bf16-rounded input
+// activations (ggml's BF16 mul_mat semantics), f32/f64 accumulation. Encoder,
+// prefill, cross-attention and LT in_proj stay f32. 0 = as stored (f32).
+int orc_set_weight_mode(orc_model *m, int mode);
 void orc_free(orc_model *m);
 int orc_dec_layers(const orc_model *m);
 

@@ -37,6 +37,7 @@ def lib() -> ctypes.CDLL:
         L.orc_synthesize.argtypes = [P, P, I, I, I, I, P, P, P, P]
         L.orc_synthesize_ex.argtypes = [P, P, I, I, I, I, ctypes.c_float, I, ctypes.c_uint64, I, P, P, P, P]
         L.orc_encode.argtypes = [P, P, I, P]
+        L.orc_set_weight_mode.argtypes = [P, I]
         L.orc_draw_u.restype = ctypes.c_float
         L.orc_draw_u.argtypes = [ctypes.c_uint64, I, I, I]
         L.orc_sample_top_k.argtypes = [P, I, ctypes.c_float, I, ctypes.c_float, P]
@@ -70,6 +71,11 @@ class Model:
         self.h = lib().orc_load(path.encode())
         if not self.h:
             raise RuntimeError(f"oracle: cannot load {path}")
+
+    def set_weight_mode(self, mode: int) -> None:
+        """0 = f32 as stored, 1 = bf16 decode projections (see magpie_oracle.h)."""
+        if lib().orc_set_weight_mode(self.h, int(mode)) != 0:
+            raise RuntimeError("oracle: bad weight mode")
 
     def close(self):
         if self.h:

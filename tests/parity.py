@@ -11,7 +11,7 @@ import numpy as np
 TIE_EPS = 2e-4  # logit units; GPU f32 vs oracle f64 logit error is ~1e-6
 
 
-def compare_codes(gpu_codes, orc_codes, orc_margins):
+def compare_codes(gpu_codes, orc_codes, orc_margins, tie_eps=TIE_EPS):
     g = np.asarray(gpu_codes)
     o = np.asarray(orc_codes)
     n = min(len(g), len(o))
@@ -21,6 +21,6 @@ def compare_codes(gpu_codes, orc_codes, orc_margins):
         return {"identical": True, "frames": n}
     f, cb = diff[0]
     margin = float(orc_margins[f, cb])
-    assert margin < TIE_EPS, (f"codes differ at frame {f} cb {cb}: gpu {g[f].tolist()} oracle {o[f].tolist()} "
-                              f"with oracle margin {margin:.3g} >= {TIE_EPS}")
+    assert margin < tie_eps, (f"codes differ at frame {f} cb {cb}: gpu {g[f].tolist()} oracle {o[f].tolist()} "
+                              f"with oracle margin {margin:.3g} >= {tie_eps}")
     return {"identical": False, "frames": int(f), "tie_margin": margin}

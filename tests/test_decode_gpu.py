@@ -168,3 +168,76 @@ def test_sampling_eos_from_argmax(ma, oracle, eos_model):
         assert outs[b]["n_frames"] == 4
         assert r.n_frames[b] == 4
         compare_codes(r.codes[b], outs[b]["codes"], outs[b]["margins"])
+
+
+# ---------------------------------------------------------------- bf16 weight mode
+# Decode projections on bf16 MFMA (mp_decode_b16.hip) vs the oracle's weight
+# mode 1 (bf16-rounded weights and input activations, magpie_oracle.h). Rounding
+# activations to bf16 is discontinuous: an f32-level difference (GPU f32 vs
+# oracle f64 accumulation, ~1e-7 relative) flips an element across a bf16
+# rounding boundary a few times per step, a 2^-8 relative step in that input.
+# On the synthetic weights the residual stream is small (std ~0.03) and every
+# LayerNorm amplifies such a flip ~30x, so hidden states drift apart by ~1e-2
+# over 24 frames (a mis-indexed fragment gives O(1)). The bar is therefore wider
+# than f32's: identical codes up to a decision whose oracle margin is < 1e-2
+# (logits / draw probability), hidden within 3e-2 max abs and 5e-3 relative L2.
+BF16_TIE_EPS = 1e-2
+BF16_HIDDEN_TOL = 3e-2
+BF16_HIDDEN_REL = 5e-3
+
+
+def _check_hidden_b16(h_gpu, h_orc):
+    err = np.abs(h_gpu - h_orc).max()
+    rel = np.linalg.norm(h_gpu - h_orc, axis=-1) / np.linalg.norm(h_orc, axis=-1)
+    assert err < BF16_HIDDEN_TOL, f"hidden max abs err {err}"
+    assert rel.max() < BF16_HIDDEN_REL, f"hidden rel L2 err {rel.max()}"
+
+def _run_both_b16(ma, oracle, model_path, tokens, steps, speaker=0, ignore_eos=False):
+    dev = ma.Device(model_path, weights="bf16")
+    r = dev.synthesize([tokens], speakers=[speaker], max_dec_steps=steps, ignore_eos=ignore_eos, trace=True)
+    dev.close()
+    om = oracle.Model(model_path)
+    om.set_weight_mode(1)
+    o = om.synthesize(tokens, speaker=speaker, max_steps=steps, ignore_eos=ignore_eos, trace=True)
+    om.close()
+    return r, o
+
+
+def test_bf16_small_model_matches_oracle(ma, oracle, small_model):
+    tok = ma.synthetic_tokens(24, seed=1000)
+    r, o = _run_both_b16(ma, oracle, small_model, tok, steps=40, speaker=1)
+    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=BF16_TIE_EPS)
+    n = res["frames"]
+    _check_hidden_b16(r.hidden[0, :n + 1], o["hidden"][:n + 1])
+    assert n >= 10, f"diverged after {n} frames"
+
+
+def test_bf16_full_model_matches_oracle(ma, oracle, full_model):
+    tok = ma.synthetic_tokens(64, seed=1000)
+    r, o = _run_both_b16(ma, oracle, full_model, tok, steps=24, ignore_eos=True)
+    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=BF16_TIE_EPS)
+    n = res["frames"]
+    _check_hidden_b16(r.hidden[0, :n + 1], o["hidden"][:n + 1])
+    assert r.n_frames[0] == 24
+
+
+@pytest.mark.parametrize("B", [3, 16])
+def test_bf16_batch_equals_single(ma, small_model, B):
+    """bf16 batches reach 16 slots; each output's MFMA arithmetic is independent of
+    the batch size, so a batch reproduces its utterances run alone exactly."""
+    toks = [ma.synthetic_tokens(8 + 3 * b, seed=2000 + b) for b in range(B)]
+    spk = [b % 5 for b in range(B)]
+    dev = ma.Device(small_model, weights="bf16")
+    rb = dev.synthesize(toks, speakers=spk, max_dec_steps=24, ignore_eos=True, trace=True)
+    for b in (0, B // 2, B - 1):
+        rs = dev.synthesize([toks[b]], speakers=[spk[b]], max_dec_steps=24, ignore_eos=True, trace=True)
+        assert np.array_equal(rb.codes[b], rs.codes[0]), f"slot {b}"
+        assert np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b} hidden"
+    dev.close()
+
+
+def test_f32_mode_rejects_batch_16(ma, small_model):
+    dev = ma.Device(small_model)
+    with pytest.raises(ma.MagpieError):
+        dev.synthesize([ma.synthetic_tokens(8, seed=b) for b in range(9)], max_dec_steps=4)
+    dev.close()

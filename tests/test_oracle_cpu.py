@@ -174,3 +174,20 @@ def test_sampling_stream_is_reproducible(oracle, small_model):
     assert not np.array_equal(a, c) and not np.array_equal(a, d)
     assert np.array_equal(t1, g)  # top-1 sampling is greedy
     assert a.max() <= 2015 and a.min() >= 0
+
+
+def test_oracle_bf16_mode_close_to_f32(oracle, small_model):
+    """Weight mode 1 changes only rounding: hidden states stay within bf16 noise
+    of the f32 mode over a few steps, and switching back restores f32 exactly."""
+    import magpie_amd as ma
+    m = oracle.Model(small_model)
+    tok = ma.synthetic_tokens(12, seed=4)
+    f = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.set_weight_mode(1)
+    h = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.set_weight_mode(0)
+    g = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.close()
+    d0 = np.abs(f["hidden"][0] - h["hidden"][0]).max()
+    assert 0 < d0 < 0.1, d0
+    assert np.array_equal(f["hidden"], g["hidden"]) and np.array_equal(f["codes"], g["codes"])

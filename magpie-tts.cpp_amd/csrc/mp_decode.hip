@@ -143,6 +143,11 @@ __global__ __launch_bounds__(MP_BLOCK) void sa_attn_kernel(AttnP p) {
     }
     if (lane < 16) *(float4 *)(&ow[w * DH + 4 * lane]) = o;
     lds_sync();
+    if (p.mode == SA_PARTIALS) {  // plain stores; the combine is the next launch
+        if (tid < DH) P[16 + tid] = (ow[tid] + ow[DH + tid]) + (ow[2 * DH + tid] + ow[3 * DH + tid]);
+        else if (tid == 64) { P[0] = m; P[1] = l; }
+        return;
+    }
     if (tid < DH / 2) {
         const int d = 2 * tid;
         st_sc1(P + 16 + d, (ow[d] + ow[DH + d]) + (ow[2 * DH + d] + ow[3 * DH + d]),
@@ -150,7 +155,8 @@ __global__ __launch_bounds__(MP_BLOCK) void sa_attn_kernel(AttnP p) {
     } else if (tid == 64) {
         st_sc1(P, m, l);
     }
-    if (!arrive_last(p.cnt + b * NH + h, (unsigned)nact, sc + SA_CHUNK + MP_NWAVES * DH, p.sc1_loads != 0)) return;
+    if (!arrive_last(p.cnt + b * NH + h, (unsigned)nact, sc + SA_CHUNK + MP_NWAVES * DH, p.mode == SA_COMBINE_SC1))
+        return;
     if (tid >= DH) return;
     const float *Pb = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
     float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
@@ -365,6 +371,42 @@ MP_DECODE_OPS(4)
 MP_DECODE_OPS(8)
 // bf16 weight mode at 16 slots: only the f32 LT in_proj runs on the GEMV family
 hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, D, PRO_LN, EPI_BIAS>(p, s); }
+
+// Combine of the SA_PARTIALS mode: one wave per (head, slot), the same arithmetic
+// as the in-launch combiner (identical results in every mode).
+__global__ __launch_bounds__(64) void sa_combine_kernel(AttnP p) {
+    const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+    const int nact = (p.pos[b] + 1 + SA_CHUNK - 1) / SA_CHUNK;
+    const float *Pb = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
+    float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
+#pragma unroll
+    for (int cc = 0; cc < NCH_MAX; ++cc) {
+        const float *Pc = Pb + min(cc, nact - 1) * PART_STRIDE;
+        mv[cc] = Pc[0];
+        lv[cc] = Pc[1];
+        ov[cc] = Pc[16 + d];
+    }
+#pragma unroll
+    for (int cc = 0; cc < NCH_MAX; ++cc)
+        if (cc >= nact) { mv[cc] = -INFINITY; lv[cc] = 0.f; ov[cc] = 0.f; }
+    float M = -INFINITY;
+#pragma unroll
+    for (int cc = 0; cc < NCH_MAX; ++cc) M = fmaxf(M, mv[cc]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < NCH_MAX; ++cc) {
+        const float e = mv[cc] == -INFINITY ? 0.f : expf(mv[cc] - M);
+        den += e * lv[cc];
+        num += e * ov[cc];
+    }
+    p.out[(size_t)b * D + h * DH + d] = num / den;
+}
+
+hipError_t op_sa_combine(const AttnP &p, int B, hipStream_t s) {
+    if (!p.part || !p.out || !p.pos || p.nch < 1 || p.nch > NCH_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sa_combine_kernel, dim3(NH, B), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
     if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || !p.out || !p.cnt || p.nch < 1 || p.nch > NCH_MAX ||

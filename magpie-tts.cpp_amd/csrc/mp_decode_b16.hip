@@ -72,19 +72,34 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
             *(uint4 *)(actb + b * KP + k) = o;
         }
     } else {
-        for (int e = tid; e < NR * (K / 8); e += MP_BLOCK) {
-            const int b = e / (K / 8), k = (e % (K / 8)) * 8;
-            uint4 o = make_uint4(0, 0, 0, 0);
-            if (b < NB) {
-                const float *src = p.src + (size_t)b * p.src_ld + k;
-                const float4 x0 = *(const float4 *)src, x1 = *(const float4 *)(src + 4);
-                o.x = f2bf(x0.x) | ((unsigned)f2bf(x0.y) << 16);
-                o.y = f2bf(x0.z) | ((unsigned)f2bf(x0.w) << 16);
-                o.z = f2bf(x1.x) | ((unsigned)f2bf(x1.y) << 16);
-                o.w = f2bf(x1.z) | ((unsigned)f2bf(x1.w) << 16);
+        // NB rows straight from HBM/L2, in batches of 8 items per thread with all
+        // 16 loads issued before the first conversion (one latency per batch)
+        constexpr int ITEMS = NB * (K / 8), BATCH = 8;
+        for (int base = 0; base < ITEMS; base += BATCH * MP_BLOCK) {
+            float4 x0[BATCH], x1[BATCH];
+#pragma unroll
+            for (int u = 0; u < BATCH; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                if (e < ITEMS) {
+                    const float *src = p.src + (size_t)(e / (K / 8)) * p.src_ld + (e % (K / 8)) * 8;
+                    x0[u] = *(const float4 *)src;
+                    x1[u] = *(const float4 *)(src + 4);
+                }
             }
-            *(uint4 *)(actb + b * KP + k) = o;
+#pragma unroll
+            for (int u = 0; u < BATCH; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                if (e < ITEMS) {
+                    uint4 o;
+                    o.x = f2bf(x0[u].x) | ((unsigned)f2bf(x0[u].y) << 16);
+                    o.y = f2bf(x0[u].z) | ((unsigned)f2bf(x0[u].w) << 16);
+                    o.z = f2bf(x1[u].x) | ((unsigned)f2bf(x1[u].y) << 16);
+                    o.w = f2bf(x1[u].z) | ((unsigned)f2bf(x1[u].w) << 16);
+                    *(uint4 *)(actb + (e / (K / 8)) * KP + (e % (K / 8)) * 8) = o;
+                }
+            }
         }
+        for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     }
     lds_sync();
 

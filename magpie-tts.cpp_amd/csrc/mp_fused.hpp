@@ -14,26 +14,6 @@ namespace mp {
 // ---------------------------------------------------------------- prologues
 // Each prologue fills act[NB][K] (LDS) with the activation vector of every slot.
 
-template <int NB, int K>
-__device__ __forceinline__ void pro_ln_vec(const float *x, const float *lnw, float eps, float *act, float *red,
-                                           float *store) {
-    // ggml_norm + ggml_mul (magpie.cpp:2255-2258): (x - mean) / sqrt(var + eps) * w
-    constexpr int PER = K / MP_BLOCK;
-    float v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = x[threadIdx.x + MP_BLOCK * i];
-    float mean, var;
-    block_meanvar<PER>(v, red, mean, var);
-    const float rstd = 1.0f / sqrtf(var + eps);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int k = threadIdx.x + MP_BLOCK * i;
-        const float y = ((v[i] - mean) * rstd) * lnw[k];
-        act[k] = y;
-        if (store) store[k] = y;
-    }
-}
-
 // Masked first-max argmax of slot b's logits (magpie.cpp:1133-1145, 1243-1259):
 // 2016 and 2018..2023 always forbidden, 2017 (EOS) too while step < 4 or in
 // fixed-length mode. Every thread returns the winner.
@@ -194,16 +174,25 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
         lds_sync();
     } else if constexpr (PRO == PRO_LN && NB >= 2) {
-        // batched: wave w owns slots w, w+4, ...; wave_block_meanvar reproduces the
-        // batch-1 block statistics bit for bit (DPP only, one barrier)
+        // batched: wave w owns slots w, w+4, ...; the statistics are one wave's DPP
+        // tree over the row, exactly as every wave computes them at batch 1
         const int lane = tid & 63, w = tid >> 6;
-        for (int b = w; b < NB; b += MP_NWAVES) {
-            constexpr int PER = K / 64;
-            float v[PER];
+        constexpr int PER = K / 64, SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
+        float vs[SPW][PER];  // every slot of this wave is loaded before any is reduced
 #pragma unroll
-            for (int i = 0; i < PER; ++i) v[i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b < NB)
+#pragma unroll
+                for (int i = 0; i < PER; ++i) vs[j][i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
+        }
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b >= NB) break;
+            const float(&v)[PER] = vs[j];
             float mean, var;
-            wave_block_meanvar<PER / 4>(v, mean, var);
+            wave_meanvar<PER>(v, mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
             const bool st = p.hidden_out && blockIdx.x == 0;
             const int s = (p.trace && blockIdx.x == 0) ? p.step[b] : 0;
@@ -218,17 +207,26 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LN) {
-        for (int b = 0; b < NB; ++b) {
-            float *store = nullptr;
-            if (p.hidden_out && blockIdx.x == 0) store = p.hidden_out + (size_t)b * K;
-            pro_ln_vec<NB, K>(p.src + (size_t)b * p.src_ld, p.lnw, p.eps, act + b * K, red, store);
-            if (p.trace && blockIdx.x == 0) {
-                lds_sync();
-                const int s = p.step[b];
-                if (s < p.trace_steps)
-                    for (int k = tid; k < K; k += MP_BLOCK)
-                        p.trace[((size_t)b * p.trace_steps + s) * K + k] = act[b * K + k];
-            }
+        // batch 1: every wave loads the whole row and runs the same DPP statistics
+        // (identical results, no barrier), then writes its quarter
+        const int lane = tid & 63, w = tid >> 6;
+        constexpr int PER = K / 64, Q = PER / MP_NWAVES;
+        float v[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) v[i] = p.src[lane + 64 * i];
+        float mean, var;
+        wave_meanvar<PER>(v, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.eps);
+        const bool st = p.hidden_out && blockIdx.x == 0;
+        const int s = (p.trace && blockIdx.x == 0) ? p.step[0] : 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (i / Q != w) continue;
+            const int k = lane + 64 * i;
+            const float y = ((v[i] - mean) * rstd) * p.lnw[k];
+            act[k] = y;
+            if (st) p.hidden_out[k] = y;
+            if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[(size_t)s * K + k] = y;
         }
         lds_sync();
     } else if constexpr (PRO == PRO_EMBED_LN && NB >= 2) {
@@ -248,7 +246,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
             }
             float mean, var;
-            wave_block_meanvar<K / 256>(x, mean, var);
+            wave_meanvar<K / 64>(x, mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
             for (int i = 0; i < K / 64; ++i) {
@@ -259,28 +257,28 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         lds_sync();
     } else if constexpr (PRO == PRO_EMBED_LN) {
         static_assert(K == D, "embed prologue is d_model wide");
-        for (int b = 0; b < NB; ++b) {
-            const int *c = p.codes + b * NCB;
-            const int ps = p.pos[b];
-            float x[K / MP_BLOCK];
+        const int lane = tid & 63, w = tid >> 6;
+        constexpr int PER = K / 64, Q = PER / MP_NWAVES;
+        const int *c = p.codes;
+        const int ps = p.pos[0];
+        float x[PER];
 #pragma unroll
-            for (int i = 0; i < K / MP_BLOCK; ++i) {
-                const int k = tid + MP_BLOCK * i;
-                float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
+        for (int i = 0; i < PER; ++i) {
+            const int k = lane + 64 * i;
+            float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
 #pragma unroll
-                for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
-                x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
-                if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
-            }
-            // LN over the freshly built x
-            float mean, var;
-            block_meanvar<K / MP_BLOCK>(x, red, mean, var);
-            const float rstd = 1.0f / sqrtf(var + p.eps);
+            for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
+            x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
+        }
+        float mean, var;
+        wave_meanvar<PER>(x, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
-            for (int i = 0; i < K / MP_BLOCK; ++i) {
-                const int k = tid + MP_BLOCK * i;
-                act[b * K + k] = ((x[i] - mean) * rstd) * p.lnw[k];
-            }
+        for (int i = 0; i < PER; ++i) {
+            if (i / Q != w) continue;
+            const int k = lane + 64 * i;
+            if (blockIdx.x == 0) p.xres[k] = x[i];
+            act[k] = ((x[i] - mean) * rstd) * p.lnw[k];
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LTX_LN && NB >= 2) {

@@ -148,7 +148,9 @@ struct AttnP {  // split-K decode self-attention (one query per utterance)
     int nslots;
     float *out;          // [B][768] combined attention output
     unsigned *cnt;       // [B][12] arrival tickets (zero between launches)
-    int sc1_loads;       // combiner reads partials with sc1 loads (1 workgroup/CU) instead of an acquire
+    int mode;            // SA_COMBINE_SC1 / SA_COMBINE_ACQ: last arriver combines in-launch;
+                         // SA_PARTIALS: partials only, sa_combine_kernel follows (large batches)
 };
+enum { SA_COMBINE_SC1 = 0, SA_COMBINE_ACQ = 1, SA_PARTIALS = 2 };
 
 }  // namespace mp

@@ -54,6 +54,7 @@ MP_DECL_B16(8)
 MP_DECL_B16(16)
 hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
+hipError_t op_sa_combine(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
 
@@ -101,7 +102,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_COMB = 4 };
 struct OpRec {
     std::string name;
     int kind;
@@ -484,8 +485,11 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         if ((rc = run(l == 0 ? "qkv_embed" : "qkv", l == 0 ? tb.qkv_embed : tb.qkv, g,
                       F * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
         // split-K self-attention over the cache, combined in-launch (3457-3476)
+        // batch <= 2: the last chunk to arrive combines in-launch (sc1 loads while the
+        // grid fits one workgroup per CU); larger batches: partials + a combine launch
+        const int sa_mode = NB >= 4 ? mp::SA_PARTIALS : dev->nch * 12 * NB <= 256 ? mp::SA_COMBINE_SC1 : mp::SA_COMBINE_ACQ;
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->part, dev->nch, dev->ndone, NB,
-                    dev->sa_out, dev->sa_cnt, dev->nch * 12 * NB <= 256};
+                    dev->sa_out, dev->sa_cnt, sa_mode};
         if (record) {
             mp::OpRec r{};
             r.name = "sa_attn"; r.kind = mp::K_ATTN; r.a = a; r.B = NB;
@@ -493,6 +497,15 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             dev->ops.push_back(r);
         }
         HIPCHK(mp::op_sa_attn(a, NB, s));
+        if (sa_mode == mp::SA_PARTIALS) {
+            if (record) {
+                mp::OpRec r{};
+                r.name = "sa_combine"; r.kind = mp::K_COMB; r.a = a; r.B = NB;
+                r.bytes = A * act * 12.0 * (dev->nch * 66 + 64);
+                dev->ops.push_back(r);
+            }
+            HIPCHK(mp::op_sa_combine(a, NB, s));
+        }
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.src = dev->sa_out; g.src_ld = 768;
@@ -925,6 +938,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     auto launch = [&]() -> hipError_t {
         if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
         if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
+        if (r.kind == mp::K_COMB) return mp::op_sa_combine(r.a, r.B, dev->stream);
         if (r.kind == mp::K_XA) {
             mp::XaP xp = r.x;
             xp.x_out = dev->q;  // scratch: timing must not disturb the residual stream

@@ -47,6 +47,10 @@ typedef struct mp_params {
     int ignore_eos;     /* 1: EOS masked at every step (fixed-length bench mode) */
     uint64_t seed;      /* sampling RNG seed (reference: unseeded static mt19937, magpie.cpp:1129) */
     int trace_hidden;   /* 1: keep the decoder hidden state of every step (parity tests) */
+    int stream_base;    /* draw stream of utterance b = stream_base + b (a sentence run alone with
+                           stream_base = i draws exactly what slot i of a batch draws) */
+    int emit_eos_frame; /* 1: the EOS frame's codes are emitted too, as the streaming loop does
+                           (magpie.cpp:4800-4806); 0: dropped, as graph_reuse does (4349-4352) */
 } mp_params;
 
 typedef struct mp_timing {
@@ -54,6 +58,7 @@ typedef struct mp_timing {
     double decode_ms;    /* BOS step + autoregressive loop (gen_time, magpie.cpp:4265,4409) */
     int frames_total;    /* frames produced over all utterances */
     int iterations;      /* decode iterations (graph replays) executed */
+    double first_audio_ms; /* mp_hip_decode_stream: decode start -> first audio callback */
 } mp_timing;
 
 /* --- device + weights ---------------------------------------------------- */
@@ -97,6 +102,23 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames);
 /* decoder hidden state after every step (BOS first): [B][max_dec_steps+1][768];
  * requires params.trace_hidden. */
 int mp_hip_get_trace(mp_dev *dev, float *hidden);
+
+/* Streaming variant of mp_hip_decode (magpie_synthesize_sentence_streaming's
+ * frame loop, magpie.cpp:4762-4838, for every utterance of the batch): every
+ * frames_per_chunk frames (<= 0: 4, magpie.h:621) each utterance's new frames are
+ * decoded by `codec` as one stateless chunk (decode_frames_to_audio,
+ * magpie.cpp:4458-4476; the last chunk may be shorter) and passed to on_audio in
+ * frame order; returning 0 stops that utterance (4820-4824). codes_out /
+ * n_frames / total_samples may be NULL. */
+typedef int (*mp_audio_cb)(int utterance, const float *samples, int n_samples, void *user);
+int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_audio_cb on_audio, void *user,
+                         int32_t *codes_out, int32_t *n_frames, int64_t *total_samples);
+
+/* magpie_local_transformer_sample_all (magpie.cpp:1113-1317) for one normalised
+ * decoder hidden vector [768]: sampled[8] and argmax[8] codes. Independent of any
+ * batch in flight. Draws use stream -1 and a per-device call counter as the step. */
+int mp_hip_lt_sample(mp_dev *dev, const float *hidden, float temperature, int top_k, int forbid_eos, uint64_t seed,
+                     int32_t *sampled, int32_t *argmax);
 int mp_hip_get_timing(mp_dev *dev, mp_timing *t);
 
 /* --- measurement ---------------------------------------------------------- */

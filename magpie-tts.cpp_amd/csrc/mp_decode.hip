@@ -267,8 +267,8 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
     if (p.smp.on) {  // one wave draws
         __shared__ float scratch[2 * VCB];
         if (tid >= 64) return;
-        i0 = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos, p.smp, b,
-                       p.step[b], NCB - 1, scratch, amax);
+        i0 = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos, p.smp,
+                       b, p.step[b], NCB - 1, scratch, amax);
         if (tid != 0) return;
     } else {
         const float *lg = p.logits + (size_t)b * VCB;
@@ -292,15 +292,20 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
     }
     int *cc = p.codes_cur + b * NCB;
     cc[NCB - 1] = i0;
+    if (p.smp.amax) p.smp.amax[b * NCB + NCB - 1] = amax;
     // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
     bool eos = amax == p.audio_eos;
     eos |= p.smp.argeos[b] != 0;
     p.smp.argeos[b] = 0;
+    if (p.lt_only) return;  // magpie_local_transformer_sample_all: codes only
     for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
     const int s = p.step[b];
     if (eos) {
+        // graph_reuse drops the EOS frame (4349-4352); the streaming loop emits it (4800-4806)
+        if (p.emit_eos)
+            for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
         p.done[b] = 1;
-        p.nframes[b] = s;
+        p.nframes[b] = p.emit_eos ? s + 1 : s;
         atomicAdd(p.ndone, 1);
         return;
     }
@@ -369,6 +374,9 @@ MP_DECODE_OPS(1)
 MP_DECODE_OPS(2)
 MP_DECODE_OPS(4)
 MP_DECODE_OPS(8)
+// LT in_proj of a caller-supplied (already normalised) hidden vector, batch 1
+// (magpie_local_transformer_sample_all, magpie.cpp:1161-1163)
+hipError_t op_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 1, D, PRO_PLAIN, EPI_BIAS>(p, s); }
 // bf16 weight mode at 16 slots: only the f32 LT in_proj runs on the GEMV family
 hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, D, PRO_LN, EPI_BIAS>(p, s); }
 

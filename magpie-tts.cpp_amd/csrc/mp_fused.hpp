@@ -56,6 +56,7 @@ __device__ __forceinline__ int block_masked_argmax(const GemvP &p, int b, float 
 // and the first i with u < cumsum_i (fallback: the k-th). Radix-select finds the
 // k-th key, a ballot compaction gathers the k candidates into LDS, a counting rank
 // orders them, lane 0 runs the two sequential float loops. scratch: 2*VCB floats.
+// `stream` is the batch slot; the draw stream is cfg->stream_base + slot.
 __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos, int audio_eos, const Sampling &smp,
                          int stream, int step, int cb, float *scratch, int &amax) {
     const int lane = threadIdx.x & 63;
@@ -151,7 +152,7 @@ __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos,
     if (lane == 0) {
         float sum = 0.f;
         for (int i = 0; i < k; ++i) sum += sv[i];
-        const float u = mp_uniform(smp.cfg->seed, stream, step, cb);
+        const float u = mp_uniform(smp.cfg->seed, smp.cfg->stream_base + stream, step, cb);
         float cum = 0.f;
         code = si[k - 1];
         for (int i = 0; i < k; ++i) {
@@ -307,6 +308,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             if (blockIdx.x == 0 && lane == 0) {
                 p.codes_cur[b * NCB + p.cb - 1] = code;
                 if (amax == p.audio_eos) p.smp.argeos[b] = 1;
+                if (p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
             }
             float X[4];
 #pragma unroll
@@ -398,6 +400,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                     if (lane == 0) {
                         red[0] = __int_as_float(code);
                         if (blockIdx.x == 0 && amax == p.audio_eos) p.smp.argeos[b] = 1;
+                        if (blockIdx.x == 0 && p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
                     }
                 }
                 lds_sync();
@@ -405,6 +408,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 lds_sync();
             } else {
                 code = block_masked_argmax(p, b, red);  // codebook cb-1's code
+                if (blockIdx.x == 0 && tid == 0 && p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = code;
             }
             if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb - 1] = code;
             const int k = tid;

@@ -51,11 +51,13 @@ struct SmpCfg {                // device-resident, so a captured graph serves an
     float temperature;
     int top_k;                 // 1..VCB
     unsigned long long seed;
+    int stream_base;           // draw stream of slot b = stream_base + b
 };
 struct Sampling {
     int on;                    // temperature >= 0.01 (baked into the captured graph)
     const SmpCfg *cfg;
     int *argeos;               // [B] 1 once a codebook's argmax was EOS this frame (4343-4346)
+    int *amax;                 // optional [B][8]: every codebook's argmax (magpie_sample_result.argmax_codes)
 };
 
 // splitmix64 finaliser
@@ -121,6 +123,8 @@ struct FinP {
     int *step, *pos, *done, *nframes, *ndone;
     int max_steps, ignore_eos, audio_bos, audio_eos, nslots;
     Sampling smp;
+    int emit_eos;   // streaming semantics: the EOS frame's codes are emitted too (magpie.cpp:4800-4806)
+    int lt_only;    // magpie_local_transformer_sample_all: pick codebook 7, no loop bookkeeping
 };
 
 // Fused cross-attention for one decode step (replaces the xq GEMV + XA attention

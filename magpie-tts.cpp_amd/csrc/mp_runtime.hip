@@ -17,6 +17,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/magpie_hip.h"
@@ -115,6 +116,17 @@ struct OpRec {
     double bytes;
 };
 
+// Buffers of the local-transformer + bookkeeping part of an iteration
+struct LtIo {
+    float *x, *hidden, *trace;
+    int trace_steps;
+    float *lt_s, *ltX, *ltY, *lty2, *ltq, *ltk, *ltv, *ltf, *logits;
+    int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
+    SmpCfg *cfg;
+    int sampling, ignore_eos, emit_eos, max_steps, lt_only;
+};
+hipError_t op_lt_inh_1(const GemvP &, hipStream_t);
+
 }  // namespace mp
 
 struct mp_dev {
@@ -136,8 +148,12 @@ struct mp_dev {
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
-        *argeos = nullptr;
+        *argeos = nullptr, *amax = nullptr;
     mp::SmpCfg *smpcfg = nullptr;
+    int lt_calls = 0;
+    // magpie_local_transformer_sample_all scratch (batch 1, independent of any batch)
+    std::vector<void *> lt_allocs;
+    mp::LtIo lt_io{};
     // preamble scratch
     float *pX = nullptr, *pH = nullptr, *pQKV = nullptr, *pATT = nullptr, *pF = nullptr, *pXQ = nullptr,
           *pXAO = nullptr, *enc_out = nullptr;
@@ -427,7 +443,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);
-    A(argeos, NB); A(smpcfg, 1);
+    A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
     A(codes_cur, NB * 8); A(codes_prev, NB * 8); A(codes_out, (size_t)NB * max_steps * 8); A(tok, (size_t)NB * Tmax);
     const size_t rows = (size_t)NB * std::max(Tmax, mp::CTX);
     A(pX, rows * D); A(pH, rows * D); A(pQKV, rows * 3 * D); A(pATT, rows * D); A(pF, rows * 3072);
@@ -452,6 +468,8 @@ mp::GemvP gemv_base(mp_dev *dev) {
     g.audio_eos = dev->m.audio_eos;
     return g;
 }
+
+int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vector<mp::OpRec> *ops);
 
 // Enqueue one decode iteration: decoder step at pos (embedding codes_prev), LT
 // over 8 codebooks, finalize. When `record` is set, the op list is rebuilt for
@@ -528,46 +546,97 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.W = W.ff2; g.Wb = b16 ? m.pk_ff2[l] : nullptr; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.out = dev->x; g.out_ld = 768; g.addsrc = dev->x2;
         if ((rc = run("ff2", tb.ff2, g, F * (768.0 * 3072) + A * act * ((3072 + 2 * 768)))) != MP_OK) return rc;
     }
-    // final LN -> hidden (4394) fused into LT in_proj (1162-1163)
+    mp::LtIo io{};
+    io.x = dev->x; io.hidden = dev->hidden; io.trace = dev->trace; io.trace_steps = dev->max_steps + 1;
+    io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
+    io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits;
+    io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
+    io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
+    io.amax = dev->amax; io.cfg = dev->smpcfg;
+    io.sampling = dev->params.temperature >= 0.01f; io.ignore_eos = dev->params.ignore_eos;
+    io.emit_eos = dev->params.emit_eos_frame; io.max_steps = dev->max_steps; io.lt_only = false;
+    return enqueue_lt(dev, io, NB, s, record ? &dev->ops : nullptr);
+}
+
+// The local transformer over one frame (magpie_local_transformer_sample_all,
+// magpie.cpp:1113-1317) + the frame bookkeeping (4320-4358), for NB slots whose
+// buffers `io` names. lt_only: in_proj of a given normalised hidden, codes only.
+int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vector<mp::OpRec> *ops) {
+    const mp::Model &m = dev->m;
+    const bool b16 = m.weight_mode == MP_WEIGHTS_BF16;
+    const mp::OpTable &tb = mp::table_for(NB, b16);
+    const double F = b16 ? 2.0 : 4.0, A = 4.0, act = (double)NB;
+    auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
+        if (ops) {
+            mp::OpRec r{};
+            r.name = name; r.kind = mp::K_GEMV; r.fn = fn; r.g = g; r.B = NB; r.bytes = bytes;
+            ops->push_back(r);
+        }
+        HIPCHK(fn(g, s));
+        return MP_OK;
+    };
+    auto base = [&]() {
+        mp::GemvP g;
+        memset(&g, 0, sizeof g);
+        g.eps = m.eps;
+        g.step = io.step;
+        g.smp = mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax};
+        g.nslots = NB;
+        g.ignore_eos = io.ignore_eos;
+        g.audio_bos = m.audio_bos;
+        g.audio_eos = m.audio_eos;
+        return g;
+    };
+    int rc;
     {
-        mp::GemvP g = gemv_base(dev);
-        g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.lnw = m.dec_norm_out; g.src = dev->x; g.src_ld = 768;
-        g.hidden_out = dev->hidden; g.out = dev->lt_s; g.out_ld = 9 * 256;
-        if (dev->trace) { g.trace = dev->trace; g.trace_steps = dev->max_steps + 1; }
-        if ((rc = run("lt_in0", tb.lt_in0, g, A * (256.0 * 768 + 256) + A * act * ((768 + 768 + 256)))) != MP_OK) return rc;
+        mp::GemvP g = base();
+        g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.out = io.lt_s; g.out_ld = 9 * 256;
+        if (io.lt_only) {
+            // in_proj of the caller's (already normalised) hidden (1161-1163)
+            g.src = io.hidden; g.src_ld = 768;
+            if ((rc = run("lt_inh", mp::op_lt_inh_1, g, A * (256.0 * 768 + 256) + A * (768 + 256))) != MP_OK) return rc;
+        } else {
+            // final LN -> hidden (4394) fused into LT in_proj (1162-1163)
+            g.lnw = m.dec_norm_out; g.src = io.x; g.src_ld = 768; g.hidden_out = io.hidden;
+            if (io.trace) { g.trace = io.trace; g.trace_steps = io.trace_steps; g.step = io.step; }
+            if ((rc = run("lt_in0", tb.lt_in0, g, A * (256.0 * 768 + 256) + A * act * ((768 + 768 + 256)))) != MP_OK)
+                return rc;
+        }
     }
     for (int cb = 0; cb < 8; ++cb) {
-        // cb > 0: codebook cb-1's masked argmax + table gather fused into this prologue
-        mp::GemvP g = gemv_base(dev);
+        // cb > 0: codebook cb-1's pick (argmax / top-k draw) + table gather fused into this prologue
+        mp::GemvP g = base();
         g.cb = cb;
-        g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = dev->lt_s; g.lt_pos = m.lt_pos; g.ltX = dev->ltX; g.lnw = m.lt_norm_self;
-        g.lq = dev->ltq; g.lk = dev->ltk; g.lv = dev->ltv;
-        if (cb > 0) { g.logits = dev->logits; g.codes_cur = dev->codes_cur; g.ptab = m.lt_ptab; }
+        g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX;
+        g.lnw = m.lt_norm_self; g.lq = io.ltq; g.lk = io.ltk; g.lv = io.ltv;
+        if (cb > 0) { g.logits = io.logits; g.codes_cur = io.codes_cur; g.ptab = m.lt_ptab; }
         if ((rc = run(cb == 0 ? "lt_a" : "lt_ag", cb == 0 ? tb.lt_a : tb.lt_ag, g,
                       F * (768.0 * 256) + A * act * ((256 * 3 + 768 + (cb > 0 ? 2024 + 256 : 256))))) != MP_OK) return rc;
-        g = gemv_base(dev); g.cb = cb;
-        g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = dev->ltq; g.ltk = dev->ltk; g.ltv = dev->ltv; g.out = dev->ltY; g.out_ld = 256;
-        g.addsrc = dev->ltX;
+        g = base(); g.cb = cb;
+        g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = io.ltq; g.ltk = io.ltk; g.ltv = io.ltv; g.out = io.ltY;
+        g.out_ld = 256; g.addsrc = io.ltX;
         if ((rc = run("lt_b", tb.lt_b, g, F * (256.0 * 256) + A * act * ((256 * (2 * cb + 5))))) != MP_OK) return rc;
-        g = gemv_base(dev); g.cb = cb;
-        g.W = m.lt_ff1; g.Wb = m.pk_lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = dev->ltY; g.src_ld = 256; g.out = dev->ltf; g.out_ld = 1024;
+        g = base(); g.cb = cb;
+        g.W = m.lt_ff1; g.Wb = m.pk_lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = io.ltY; g.src_ld = 256;
+        g.out = io.ltf; g.out_ld = 1024;
         if ((rc = run("lt_c", tb.lt_c, g, F * (1024.0 * 256) + A * act * ((256 + 1024)))) != MP_OK) return rc;
-        g = gemv_base(dev); g.cb = cb;
-        g.W = m.lt_ff2; g.Wb = m.pk_lt_ff2; g.N = 256; g.src = dev->ltf; g.src_ld = 1024; g.out = dev->lty2; g.out_ld = 256; g.addsrc = dev->ltY;
+        g = base(); g.cb = cb;
+        g.W = m.lt_ff2; g.Wb = m.pk_lt_ff2; g.N = 256; g.src = io.ltf; g.src_ld = 1024; g.out = io.lty2; g.out_ld = 256;
+        g.addsrc = io.ltY;
         if ((rc = run("lt_d", tb.lt_d, g, F * (256.0 * 1024) + A * act * ((1024 + 512)))) != MP_OK) return rc;
-        g = gemv_base(dev); g.cb = cb;
+        g = base(); g.cb = cb;
         g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024;
         g.Wb = b16 ? m.pk_lt_out + (size_t)cb * pk_elems(2024, 256) : nullptr; g.bias = m.lt_out_b + (size_t)cb * 2024;
-        g.src = dev->lty2; g.src_ld = 256; g.out = dev->logits; g.out_ld = 2024;
+        g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
         if ((rc = run("lt_e", tb.lt_e, g, F * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK) return rc;
     }
-    mp::FinP f{dev->logits, dev->codes_cur, dev->codes_prev, dev->codes_out, dev->step, dev->pos, dev->done,
-               dev->nframes, dev->ndone, dev->max_steps, dev->params.ignore_eos, m.audio_bos, m.audio_eos, NB,
-               mp::Sampling{dev->params.temperature >= 0.01f, dev->smpcfg, dev->argeos}};
-    if (record) {
+    mp::FinP f{io.logits, io.codes_cur, io.codes_prev, io.codes_out, io.step, io.pos, io.done, io.nframes, io.ndone,
+               io.max_steps, io.ignore_eos, m.audio_bos, m.audio_eos, NB,
+               mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax}, io.emit_eos, io.lt_only};
+    if (ops) {
         mp::OpRec r{};
         r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = A * act * 2024;
-        dev->ops.push_back(r);
+        ops->push_back(r);
     }
     HIPCHK(mp::op_finalize(f, NB, s));
     return MP_OK;
@@ -737,6 +806,7 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.arena) hipFree(dev->m.arena);
     if (dev->m.lt_ptab) hipFree(dev->m.lt_ptab);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
+    for (void *p : dev->lt_allocs) hipFree(p);
     for (float *p : dev->m.xq_t) hipFree(p);
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
     if (dev->stream) hipStreamDestroy(dev->stream);
@@ -773,7 +843,8 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     const bool trace = params->trace_hidden != 0;
     const bool same = dev->NB > 0 && dev->B == B && dev->Tmax == Tmax && dev->max_steps == max_steps &&
                       (dev->trace != nullptr) == trace && dev->params.ignore_eos == params->ignore_eos &&
-                      (dev->params.temperature >= 0.01f) == (params->temperature >= 0.01f);
+                      (dev->params.temperature >= 0.01f) == (params->temperature >= 0.01f) &&
+                      dev->params.emit_eos_frame == params->emit_eos_frame;
     dev->params = *params;
     if (!same) {
         if (int rc = alloc_batch(dev, B, Tmax, max_steps, trace)) return rc;
@@ -791,7 +862,7 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     HIPCHK(hipMemcpyAsync(dev->T, h_T.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemcpyAsync(dev->spk, h_spk.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
     {   // sampling settings live on the device: the captured graph serves any of them
-        mp::SmpCfg cfg{params->temperature, params->top_k, (unsigned long long)params->seed};
+        mp::SmpCfg cfg{params->temperature, params->top_k, (unsigned long long)params->seed, params->stream_base};
         HIPCHK(hipMemcpyAsync(dev->smpcfg, &cfg, sizeof cfg, hipMemcpyHostToDevice, dev->stream));
         HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
     HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
@@ -804,12 +875,9 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     return MP_OK;
 }
 
-int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
-    if (!dev) return MP_ERR_ARG;
-    if (!dev->batch_ready) return fail(dev, MP_ERR_STATE, "mp_hip_begin_batch must precede mp_hip_decode");
-    HIPCHK(hipSetDevice(dev->device));
+// Per-decode device state: BOS frame at position 110 (magpie.cpp:4243-4318).
+int reset_decode_state(mp_dev *dev) {
     const int NB = dev->NB, B = dev->B;
-    // iteration state: BOS frame at position 110 (magpie.cpp:4243-4318)
     std::vector<int> h_pos(NB, mp::CTX), h_zero(NB, 0), h_done(NB, 0), h_prev((size_t)NB * 8, dev->m.audio_bos);
     for (int b = B; b < NB; ++b) h_done[b] = 1;
     int h_nd[4] = {NB - B, 0, 0, 0};
@@ -822,30 +890,28 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
     HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
     HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
-    // MAGPIE_EAGER=1: launch the iteration's kernels directly instead of replaying
-    // the captured graph (identical kernels and arguments; used under rocprofv3,
-    // whose kernel tracer crashes on graph replays on this image).
-    const char *eager_env = getenv("MAGPIE_EAGER");
-    const bool eager = eager_env && atoi(eager_env) != 0;
-    if (eager) {
+    // the host copies are stack/heap temporaries: finish the uploads before they go
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    return MP_OK;
+}
+
+// MAGPIE_EAGER=1: launch the iteration's kernels directly instead of replaying
+// the captured graph (identical kernels and arguments; used under rocprofv3,
+// whose kernel tracer crashes on graph replays on this image).
+bool eager_mode() {
+    const char *e = getenv("MAGPIE_EAGER");
+    return e && atoi(e) != 0;
+}
+
+// Capture the iteration graph (or, eager, record the op list) once per batch
+// configuration; leaves the decode state reset.
+int prepare_iteration(mp_dev *dev) {
+    if (eager_mode()) {
         if (dev->ops.empty()) {
-            if (int rc = enqueue_iteration(dev, dev->stream, true)) return rc;  // also records op list
+            if (int rc = enqueue_iteration(dev, dev->stream, true)) return rc;  // a real first iteration
             HIPCHK(hipStreamSynchronize(dev->stream));
-            // that was a real first iteration: restore the initial state
-            HIPCHK(hipMemcpyAsync(dev->pos, h_pos.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
-            HIPCHK(hipMemcpyAsync(dev->step, h_zero.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
-            HIPCHK(hipMemcpyAsync(dev->nframes, h_zero.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
-            HIPCHK(hipMemcpyAsync(dev->done, h_done.data(), NB * 4, hipMemcpyHostToDevice, dev->stream));
-            HIPCHK(hipMemcpyAsync(dev->ndone, h_nd, 16, hipMemcpyHostToDevice, dev->stream));
-            HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
-            HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
-            HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
         }
     } else if (!dev->exec) {
-        // capture one iteration; the op list is recorded for measurement
         HIPCHK(hipStreamBeginCapture(dev->stream, hipStreamCaptureModeThreadLocal));
         int rc = enqueue_iteration(dev, dev->stream, true);
         hipGraph_t g = nullptr;
@@ -855,7 +921,21 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
         dev->graph = g;
         HIPCHK(hipGraphInstantiate(&dev->exec, dev->graph, nullptr, nullptr, 0));
     }
-    HIPCHK(hipStreamSynchronize(dev->stream));
+    return reset_decode_state(dev);
+}
+
+int launch_iteration(mp_dev *dev) {
+    if (eager_mode()) return enqueue_iteration(dev, dev->stream, false);
+    HIPCHK(hipGraphLaunch(dev->exec, dev->stream));
+    return MP_OK;
+}
+
+int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
+    if (!dev) return MP_ERR_ARG;
+    if (!dev->batch_ready) return fail(dev, MP_ERR_STATE, "mp_hip_begin_batch must precede mp_hip_decode");
+    HIPCHK(hipSetDevice(dev->device));
+    const int NB = dev->NB, B = dev->B;
+    if (int rc = prepare_iteration(dev)) return rc;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
@@ -863,11 +943,7 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     const int poll = 8;
     int it = 0;
     for (; it < dev->max_steps; ++it) {
-        if (eager) {
-            if (int rc = enqueue_iteration(dev, dev->stream, false)) return rc;
-        } else {
-            HIPCHK(hipGraphLaunch(dev->exec, dev->stream));
-        }
+        if (int rc = launch_iteration(dev)) return rc;
         if (!dev->params.ignore_eos && (it + 1) % poll == 0 && it + 1 < dev->max_steps) {
             HIPCHK(hipMemcpyAsync(dev->h_ndone, dev->ndone, 4, hipMemcpyDeviceToHost, dev->stream));
             HIPCHK(hipStreamSynchronize(dev->stream));
@@ -893,6 +969,121 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     dev->timing.decode_ms = ms;
     dev->timing.frames_total = total;
     dev->timing.iterations = it;
+    return MP_OK;
+}
+
+// Streaming frame loop (magpie_synthesize_sentence_streaming's loop,
+// magpie.cpp:4762-4838) for every utterance of the batch: after each
+// frames_per_chunk iterations the new frames of every utterance are decoded by
+// the codec in chunks of frames_per_chunk (the last chunk of an utterance may
+// be shorter: EOS or max_dec_steps) and handed to `on_audio` in order.
+int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_audio_cb on_audio, void *user,
+                         int32_t *codes_out, int32_t *n_frames, int64_t *total_samples) {
+    if (!dev) return MP_ERR_ARG;
+    if (!dev->batch_ready) return fail(dev, MP_ERR_STATE, "mp_hip_begin_batch must precede mp_hip_decode_stream");
+    if (!codec) return fail(dev, MP_ERR_ARG, "codec is required");
+    const int fpc = frames_per_chunk > 0 ? frames_per_chunk : 4;  // default 4 (magpie.h:621)
+    HIPCHK(hipSetDevice(dev->device));
+    const int NB = dev->NB, B = dev->B, S = dev->max_steps;
+    if (int rc = prepare_iteration(dev)) return rc;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<int> h_step(NB), h_done(NB), h_nf(NB), delivered(B, 0), stopped(B, 0);
+    std::vector<int32_t> chunk((size_t)8 * fpc), fm((size_t)fpc * 8);
+    std::vector<float> audio((size_t)fpc * 1024);
+    int64_t samples = 0;
+    int it = 0;
+    bool first = true;
+    dev->timing = mp_timing{dev->timing.preamble_ms, 0.0, 0, 0, 0.0};
+    for (;;) {
+        int n_it = std::min(fpc, S - it);
+        for (int i = 0; i < n_it; ++i)
+            if (int rc = launch_iteration(dev)) return rc;
+        it += n_it;
+        HIPCHK(hipMemcpyAsync(h_step.data(), dev->step, NB * 4, hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipMemcpyAsync(h_done.data(), dev->done, NB * 4, hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipMemcpyAsync(h_nf.data(), dev->nframes, NB * 4, hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipStreamSynchronize(dev->stream));
+        bool all_done = true;
+        for (int b = 0; b < B; ++b) {
+            const bool done = h_done[b] != 0 || stopped[b];
+            const int produced = h_done[b] ? h_nf[b] : h_step[b];
+            while (!stopped[b] && produced - delivered[b] >= (done ? 1 : fpc)) {
+                const int n = std::min(fpc, produced - delivered[b]);
+                HIPCHK(hipMemcpy(fm.data(), dev->codes_out + ((size_t)b * S + delivered[b]) * 8, (size_t)n * 32,
+                                 hipMemcpyDeviceToHost));
+                for (int t = 0; t < n; ++t)  // frame-major -> codebook-major (decode_frames_to_audio, 4468-4473)
+                    for (int c = 0; c < 8; ++c) chunk[(size_t)c * n + t] = fm[(size_t)t * 8 + c];
+                if (int rc = mp_hip_codec_decode(codec, chunk.data(), n, audio.data()))
+                    return fail(dev, rc, std::string("codec: ") + mp_hip_codec_error(codec));
+                delivered[b] += n;
+                samples += (int64_t)n * 1024;
+                if (first) {
+                    dev->timing.first_audio_ms = ms_since(t0);
+                    first = false;
+                }
+                if (on_audio && !on_audio(b, audio.data(), n * 1024, user)) {
+                    // the callback asked to stop (4820-4824): the utterance ends here
+                    stopped[b] = 1;
+                    const int one = 1;
+                    HIPCHK(hipMemcpy(dev->done + b, &one, 4, hipMemcpyHostToDevice));
+                }
+            }
+            if (!(done || stopped[b])) all_done = false;
+        }
+        if (all_done || it >= S) break;
+    }
+    dev->timing.decode_ms = ms_since(t0);
+    dev->timing.iterations = it;
+    int total = 0;
+    for (int b = 0; b < B; ++b) {
+        if (n_frames) n_frames[b] = delivered[b];
+        total += delivered[b];
+    }
+    dev->timing.frames_total = total;
+    if (codes_out) HIPCHK(hipMemcpy(codes_out, dev->codes_out, (size_t)B * S * 8 * 4, hipMemcpyDeviceToHost));
+    if (total_samples) *total_samples = samples;
+    return MP_OK;
+}
+
+int mp_hip_lt_sample(mp_dev *dev, const float *hidden, float temperature, int top_k, int forbid_eos, uint64_t seed,
+                     int32_t *sampled, int32_t *argmax) {
+    if (!dev || !hidden || !sampled || !argmax) return MP_ERR_ARG;
+    if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
+    if (temperature >= 0.01f && (top_k < 1 || top_k > mp::VCB)) return fail(dev, MP_ERR_ARG, "top_k must be in 1..2024");
+    HIPCHK(hipSetDevice(dev->device));
+    mp::LtIo &io = dev->lt_io;
+    if (dev->lt_allocs.empty()) {
+        auto al = [&](auto **p, size_t n) -> int {
+            void *v = nullptr;
+            HIPCHK(hipMalloc(&v, n * 4 + 256));
+            HIPCHK(hipMemset(v, 0, n * 4 + 256));
+            dev->lt_allocs.push_back(v);
+            *p = (std::remove_reference_t<decltype(**p)> *)v;
+            return MP_OK;
+        };
+        int rc = MP_OK;
+        if ((rc = al(&io.hidden, 768)) || (rc = al(&io.lt_s, 9 * 256)) || (rc = al(&io.ltX, 256)) ||
+            (rc = al(&io.ltY, 256)) || (rc = al(&io.lty2, 256)) || (rc = al(&io.ltq, 256)) ||
+            (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) ||
+            (rc = al(&io.logits, 2024)) || (rc = al(&io.codes_cur, 8)) || (rc = al(&io.step, 1)) ||
+            (rc = al(&io.done, 1)) || (rc = al(&io.argeos, 1)) || (rc = al(&io.amax, 8)) || (rc = al(&io.cfg, 8)))
+            return rc;
+        io.lt_only = 1;
+        io.max_steps = 1;
+    }
+    io.sampling = temperature >= 0.01f;
+    io.ignore_eos = forbid_eos != 0;
+    // step: a call counter >= 4 (so only forbid_eos masks EOS), also the draw's step index
+    const int step = 4 + dev->lt_calls++;
+    mp::SmpCfg cfg{temperature, top_k, (unsigned long long)seed, -1};
+    HIPCHK(hipMemcpyAsync(io.hidden, hidden, 768 * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(io.step, &step, 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(io.cfg, &cfg, sizeof cfg, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemsetAsync(io.argeos, 0, 4, dev->stream));
+    if (int rc = enqueue_lt(dev, io, 1, dev->stream, nullptr)) return rc;
+    HIPCHK(hipMemcpyAsync(sampled, io.codes_cur, 32, hipMemcpyDeviceToHost, dev->stream));
+    HIPCHK(hipMemcpyAsync(argmax, io.amax, 32, hipMemcpyDeviceToHost, dev->stream));
+    HIPCHK(hipStreamSynchronize(dev->stream));
     return MP_OK;
 }
 

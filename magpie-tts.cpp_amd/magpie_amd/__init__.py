@@ -42,12 +42,17 @@ class MagpieError(RuntimeError):
 
 class mp_params(ctypes.Structure):
     _fields_ = [("temperature", ctypes.c_float), ("top_k", ctypes.c_int), ("max_dec_steps", ctypes.c_int),
-                ("ignore_eos", ctypes.c_int), ("seed", ctypes.c_uint64), ("trace_hidden", ctypes.c_int)]
+                ("ignore_eos", ctypes.c_int), ("seed", ctypes.c_uint64), ("trace_hidden", ctypes.c_int),
+                ("stream_base", ctypes.c_int), ("emit_eos_frame", ctypes.c_int)]
 
 
 class mp_timing(ctypes.Structure):
     _fields_ = [("preamble_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("frames_total", ctypes.c_int),
-                ("iterations", ctypes.c_int)]
+                ("iterations", ctypes.c_int), ("first_audio_ms", ctypes.c_double)]
+
+
+# int (*mp_audio_cb)(int utterance, const float *samples, int n_samples, void *user)
+AUDIO_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_void_p)
 
 
 # (name, restype, argtypes) of every symbol include/magpie_hip.h declares
@@ -66,6 +71,8 @@ SYMBOLS = [
     ("mp_hip_decode", _I, [_P, _P, _P]),
     ("mp_hip_get_trace", _I, [_P, _P]),
     ("mp_hip_get_timing", _I, [_P, ctypes.POINTER(mp_timing)]),
+    ("mp_hip_decode_stream", _I, [_P, _P, _I, AUDIO_CB, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)]),
+    ("mp_hip_lt_sample", _I, [_P, _P, ctypes.c_float, _I, _I, ctypes.c_uint64, _P, _P]),
     ("mp_hip_num_ops", _I, [_P]),
     ("mp_hip_op_name", ctypes.c_char_p, [_P, _I]),
     ("mp_hip_op_bytes", ctypes.c_double, [_P, _I]),
@@ -176,10 +183,10 @@ class Device:
         self._check(self.lib.mp_hip_model_info(self.h, ctypes.byref(dl), ctypes.byref(el), ctypes.byref(wb)))
         return {"dec_layers": dl.value, "enc_layers": el.value, "weight_bytes": wb.value}
 
-    def synthesize(self, tokens: Sequence[Sequence[int]], speakers: Optional[Sequence[int]] = None,
-                   max_dec_steps: int = 500, temperature: float = 0.0, top_k: int = 80, ignore_eos: bool = False,
-                   seed: int = 0, trace: bool = False) -> SynthResult:
-        """Batched magpie_synthesize_codes_graph_reuse over independent utterances."""
+    def begin(self, tokens: Sequence[Sequence[int]], speakers: Optional[Sequence[int]] = None,
+              max_dec_steps: int = 500, temperature: float = 0.0, top_k: int = 80, ignore_eos: bool = False,
+              seed: int = 0, trace: bool = False, stream_base: int = 0, emit_eos_frame: bool = False) -> int:
+        """mp_hip_begin_batch: preamble of B independent utterances; returns B."""
         B = len(tokens)
         tmax = max(len(t) for t in tokens)
         tok = np.zeros((B, tmax), np.int32)
@@ -187,10 +194,49 @@ class Device:
             tok[b, :len(t)] = np.asarray(t, np.int32)
         nt = np.array([len(t) for t in tokens], np.int32)
         spk = np.zeros(B, np.int32) if speakers is None else np.asarray(speakers, np.int32)
-        p = mp_params(temperature, top_k, max_dec_steps, int(ignore_eos), seed, int(trace))
+        p = mp_params(temperature, top_k, max_dec_steps, int(ignore_eos), seed, int(trace), int(stream_base),
+                      int(emit_eos_frame))
         self._check(self.lib.mp_hip_begin_batch(self.h, tok.ctypes.data, nt.ctypes.data, spk.ctypes.data, B, tmax,
                                                 ctypes.byref(p)))
+        return B
+
+    def synthesize(self, tokens: Sequence[Sequence[int]], speakers: Optional[Sequence[int]] = None,
+                   max_dec_steps: int = 500, temperature: float = 0.0, top_k: int = 80, ignore_eos: bool = False,
+                   seed: int = 0, trace: bool = False, stream_base: int = 0) -> SynthResult:
+        """Batched magpie_synthesize_codes_graph_reuse over independent utterances."""
+        B = self.begin(tokens, speakers, max_dec_steps, temperature, top_k, ignore_eos, seed, trace, stream_base)
         return self.decode(B, max_dec_steps, trace)
+
+    def synthesize_stream(self, codec: "Codec", tokens: Sequence[Sequence[int]], on_audio,
+                          speakers: Optional[Sequence[int]] = None, max_dec_steps: int = 500,
+                          temperature: float = 0.0, top_k: int = 80, seed: int = 0, frames_per_chunk: int = 4,
+                          stream_base: int = 0):
+        """magpie_synthesize_sentence_streaming over a batch: on_audio(utt, np.ndarray) -> bool
+        (False stops that utterance). The EOS frame is emitted, as the reference's streaming
+        loop does. Returns (codes per utterance, total samples, timing)."""
+        B = self.begin(tokens, speakers, max_dec_steps, temperature, top_k, False, seed, False, stream_base, True)
+
+        def _cb(utt, ptr, n, _user):
+            return 1 if on_audio(utt, np.ctypeslib.as_array(ptr, shape=(n,)).copy()) is not False else 0
+
+        cb = AUDIO_CB(_cb)
+        codes = np.zeros((B, max_dec_steps, 8), np.int32)
+        nf = np.zeros(B, np.int32)
+        total = ctypes.c_int64()
+        self._check(self.lib.mp_hip_decode_stream(self.h, codec.h, frames_per_chunk, cb, None, codes.ctypes.data,
+                                                  nf.ctypes.data, ctypes.byref(total)))
+        tm = mp_timing()
+        self._check(self.lib.mp_hip_get_timing(self.h, ctypes.byref(tm)))
+        return [codes[b, :nf[b]].copy() for b in range(B)], int(total.value), tm
+
+    def lt_sample(self, hidden, temperature: float = 0.0, top_k: int = 80, forbid_eos: bool = False, seed: int = 0):
+        """magpie_local_transformer_sample_all: (sampled[8], argmax[8]) for one hidden[768]."""
+        h = np.ascontiguousarray(hidden, np.float32)
+        assert h.shape == (768,)
+        smp, amx = np.zeros(8, np.int32), np.zeros(8, np.int32)
+        self._check(self.lib.mp_hip_lt_sample(self.h, h.ctypes.data, temperature, top_k, int(forbid_eos), seed,
+                                              smp.ctypes.data, amx.ctypes.data))
+        return smp, amx
 
     def decode(self, B: int, max_dec_steps: int, trace: bool = False) -> SynthResult:
         codes = np.zeros((B, max_dec_steps, 8), np.int32)

@@ -531,7 +531,8 @@ int orc_sample_top_k(const float *logits, int n, float temperature, int top_k, f
 // per-codebook recompute). temperature < 0.01 => argmax (1263-1264).
 // *argeos is set when any codebook's argmax is EOS (the loop's EOS test, 4340-4346).
 static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, float temperature, int top_k,
-                      uint64_t seed, int stream, int step, int32_t *codes, float *margins, int *argeos) {
+                      uint64_t seed, int stream, int step, int32_t *codes, float *margins, int *argeos,
+                      int32_t *argmax) {
     const int D = m->lt_dim, F = m->lt_ffn, V = m->vocab_cb, d = m->d;
     float s[9][256], X[256], h[256], qkv[768], kk[8][256], vv[8][256], a[256], Y[256], f[1024], y2[256];
     float *logits = malloc(sizeof(float) * (size_t)V);
@@ -561,6 +562,7 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, f
         float second = -INFINITY;
         for (int i = 0; i < V; ++i) if (i != am && logits[i] > second) second = logits[i];
         int code = am;
+        if (argmax) argmax[cb] = am;
         float mg = mx - second;
         if (am == m->audio_eos && argeos) *argeos = 1;
         if (temperature >= 0.01f) {
@@ -580,12 +582,19 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, f
 
 int orc_synthesize(orc_model *m, const int32_t *tokens, int T, int speaker, int max_steps, int ignore_eos,
                    int32_t *codes_out, float *margins_out, float *hidden_out, double *timing_out) {
-    return orc_synthesize_ex(m, tokens, T, speaker, max_steps, ignore_eos, 0.0f, 80, 0, 0, codes_out, margins_out,
+    return orc_synthesize_ex(m, tokens, T, speaker, max_steps, ignore_eos, 0.0f, 80, 0, 0, 0, codes_out, margins_out,
                              hidden_out, timing_out);
 }
 
+int orc_lt_sample(orc_model *m, const float *hidden, float temperature, int top_k, int forbid_eos, uint64_t seed,
+                  int stream, int step, int32_t *sampled, int32_t *argmax, float *margins) {
+    if (!m || !hidden || !sampled || (temperature >= 0.01f && top_k < 1)) return -1;
+    lt_sample(m, hidden, forbid_eos, temperature, top_k, seed, stream, step, sampled, margins, NULL, argmax);
+    return 0;
+}
+
 int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, int max_steps, int ignore_eos,
-                      float temperature, int top_k, uint64_t seed, int stream, int32_t *codes_out,
+                      float temperature, int top_k, uint64_t seed, int stream, int emit_eos, int32_t *codes_out,
                       float *margins_out, float *hidden_out, double *timing_out) {
     if (temperature >= 0.01f && top_k < 1) return -1;
     if (!m || !tokens || T <= 0 || speaker < 0 || speaker >= m->n_spk) return -1;
@@ -638,9 +647,13 @@ int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, i
         const int forbid = ignore_eos || step < 4;  // min_generated_frames (4267,4325)
         int eos = 0;
         lt_sample(m, hid, forbid, temperature, top_k, seed, stream, step, codes,
-                  margins_out ? margins_out + (size_t)step * 8 : NULL, &eos);
+                  margins_out ? margins_out + (size_t)step * 8 : NULL, &eos, NULL);
         for (int c = 0; c < 8; ++c) if (codes[c] == m->audio_eos) eos = 1;
-        if (eos) break;
+        if (eos) {
+            // the streaming loop emits the EOS frame too (magpie.cpp:4800-4806)
+            if (emit_eos) { memcpy(codes_out + (size_t)step * 8, codes, sizeof codes); n_frames = step + 1; }
+            break;
+        }
         memcpy(codes_out + (size_t)step * 8, codes, sizeof codes);
         n_frames = step + 1;
         if (step + 1 >= max_steps) break;

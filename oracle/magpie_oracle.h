@@ -51,9 +51,15 @@ int orc_synthesize(orc_model *m, const int32_t *tokens, int n_tokens, int speake
 // magpie.cpp:1072-1109). Draws use this repo's counter-based stream
 // u(seed, stream, step, codebook) (see magpie_oracle.c); stream = batch slot.
 // margins_out then holds min(argmax gap, distance of u to the chosen interval).
+// emit_eos = 1: the EOS frame is emitted too (the streaming loop, magpie.cpp:4800-4806).
 int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int n_tokens, int speaker_id, int max_steps,
-                      int ignore_eos, float temperature, int top_k, uint64_t seed, int stream,
+                      int ignore_eos, float temperature, int top_k, uint64_t seed, int stream, int emit_eos,
                       int32_t *codes_out, float *margins_out, float *hidden_out, double *timing_out);
+
+// magpie_local_transformer_sample_all (magpie.cpp:1113-1317) for one hidden[768]:
+// sampled[8], argmax[8] (nullable), margins[8] (nullable).
+int orc_lt_sample(orc_model *m, const float *hidden, float temperature, int top_k, int forbid_eos, uint64_t seed,
+                  int stream, int step, int32_t *sampled, int32_t *argmax, float *margins);
 
 // Component entry points used by unit tests.
 float orc_draw_u(uint64_t seed, int stream, int step, int cb);

@@ -35,9 +35,10 @@ def lib() -> ctypes.CDLL:
         L.orc_free.argtypes = [P]
         L.orc_dec_layers.argtypes = [P]
         L.orc_synthesize.argtypes = [P, P, I, I, I, I, P, P, P, P]
-        L.orc_synthesize_ex.argtypes = [P, P, I, I, I, I, ctypes.c_float, I, ctypes.c_uint64, I, P, P, P, P]
+        L.orc_synthesize_ex.argtypes = [P, P, I, I, I, I, ctypes.c_float, I, ctypes.c_uint64, I, I, P, P, P, P]
         L.orc_encode.argtypes = [P, P, I, P]
         L.orc_set_weight_mode.argtypes = [P, I]
+        L.orc_lt_sample.argtypes = [P, P, ctypes.c_float, I, I, ctypes.c_uint64, I, I, P, P, P]
         L.orc_draw_u.restype = ctypes.c_float
         L.orc_draw_u.argtypes = [ctypes.c_uint64, I, I, I]
         L.orc_sample_top_k.argtypes = [P, I, ctypes.c_float, I, ctypes.c_float, P]
@@ -83,7 +84,7 @@ class Model:
             self.h = None
 
     def synthesize(self, tokens, speaker=0, max_steps=32, ignore_eos=False, trace=True,
-                   temperature=0.0, top_k=80, seed=0, stream=0):
+                   temperature=0.0, top_k=80, seed=0, stream=0, emit_eos=False):
         """magpie_synthesize_codes_graph_reuse restated (magpie.cpp:4063-4432).
         temperature >= 0.01 samples with sample_top_k's arithmetic (1072-1109) from
         the counter-based stream u(seed, stream, step, cb); stream = batch slot."""
@@ -94,12 +95,22 @@ class Model:
         tim = np.zeros(2, np.float64)
         n = lib().orc_synthesize_ex(self.h, tok.ctypes.data, len(tok), speaker, max_steps, int(ignore_eos),
                                     float(temperature), int(top_k), int(seed) & (2**64 - 1), int(stream),
-                                    codes.ctypes.data, marg.ctypes.data,
+                                    int(emit_eos), codes.ctypes.data, marg.ctypes.data,
                                     hid.ctypes.data if trace else None, tim.ctypes.data)
         if n < 0:
             raise RuntimeError(f"oracle synthesize failed ({n})")
         return {"n_frames": n, "codes": codes[:n], "margins": marg[:max(n + 1, 0)],
                 "hidden": hid, "preamble_ms": tim[0], "decode_ms": tim[1]}
+
+    def lt_sample(self, hidden, temperature=0.0, top_k=80, forbid_eos=False, seed=0, stream=-1, step=4):
+        """magpie_local_transformer_sample_all restated: (sampled[8], argmax[8], margins[8])."""
+        h = np.ascontiguousarray(hidden, np.float32)
+        smp, amx, mg = np.zeros(8, np.int32), np.zeros(8, np.int32), np.zeros(8, np.float32)
+        if lib().orc_lt_sample(self.h, h.ctypes.data, float(temperature), int(top_k), int(forbid_eos),
+                               int(seed) & (2**64 - 1), int(stream), int(step), smp.ctypes.data, amx.ctypes.data,
+                               mg.ctypes.data) != 0:
+            raise RuntimeError("oracle lt_sample failed")
+        return smp, amx, mg
 
     def encode(self, tokens):
         tok = np.ascontiguousarray(tokens, np.int32)

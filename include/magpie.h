@@ -8,12 +8,14 @@
 // below is implemented over the C-ABI in magpie_hip.h (one HIP device per
 // context, no multi-backend dispatch).
 //
-// Out of scope here: graph-builder entry points
-// (magpie_build_*), the tokenizer, streaming API and CLI.
+// Also provided: the streaming API (magpie.h:596-648) and the text
+// front end / tokenizer (magpie.h:86-110). Out of scope: graph-builder entry
+// points (magpie_build_*) and the CLI.
 #ifndef MAGPIE_H
 #define MAGPIE_H
 
 #include <cstdint>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -61,8 +63,27 @@ struct magpie_hparams {
     float eps = 1e-5f;
 };
 
+// magpie.h:86-104 (same fields)
+struct magpie_tokenizer {
+    std::vector<std::string> vocab;               // token id -> token string
+    std::map<std::string, int32_t> token_to_id;   // token string -> id
+    std::map<std::string, std::string> dict;      // word -> IPA pronunciation
+    int32_t pad_id = -1;
+    int32_t oov_id = -1;
+    int32_t space_id = -1;
+    int32_t bos_id = -1;
+    int32_t eos_id = -1;
+    bool loaded = false;
+};
+// magpie_tokenizer_init (magpie.h:107) takes a ggml gguf_context there; here the
+// GGUF path (strings magpie.tokenizer.vocab / .dict, ids magpie.tokenizer.*).
+bool magpie_tokenizer_load(magpie_tokenizer *tok, const char *gguf_path);
+// magpie.h:110: normalise, lower-case, dictionary/IPA or letter fallback, BOS..EOS
+std::vector<int32_t> magpie_tokenize(const magpie_tokenizer *tok, const std::string &text);
+
 struct magpie_model {
     magpie_hparams hparams;
+    magpie_tokenizer tokenizer;  // loaded by magpie_init when the GGUF carries one
     magpie_backend_type backend_type = MAGPIE_BACKEND_CUDA;
     mp_dev *dev = nullptr;  // resident weights + device state (replaces ggml ctx/buffers)
 };
@@ -134,6 +155,35 @@ magpie_codec *magpie_codec_init_with_backend(const char *codec_path, magpie_back
 void magpie_codec_free(magpie_codec *codec);
 // codes: [num_codebooks][n_frames] codebook-major; returns n_frames * 1024 samples
 std::vector<float> magpie_codec_decode(magpie_codec *codec, const int32_t *codes, int n_frames);
+
+// magpie.h:372-377: the 8-codebook local transformer for one normalised decoder
+// hidden state [768] (sampled + argmax codes), on the device.
+magpie_sample_result magpie_local_transformer_sample_all(magpie_context *ctx, const float *decoder_hidden,
+                                                        float temperature, int top_k, bool forbid_eos = false);
+
+// ---- streaming (magpie.h:596-648, same types and defaults)
+typedef bool (*magpie_audio_callback)(const float *samples, int n_samples, void *user_data);
+typedef void (*magpie_progress_callback)(int frames_generated, int sentence_index, int total_sentences,
+                                         void *user_data);
+struct magpie_stream_params {
+    float temperature = 0.7f;
+    int top_k = 80;
+    int speaker_id = 0;
+    int frames_per_chunk = 4;
+    bool sentence_chunking = true;
+    magpie_audio_callback on_audio = nullptr;
+    magpie_progress_callback on_progress = nullptr;
+    void *user_data = nullptr;
+    // added: sentences synthesised concurrently as one device batch (audio still
+    // delivered in sentence order; identical samples). 1 = the reference's order.
+    int max_parallel_sentences = 8;
+};
+std::vector<std::string> magpie_split_sentences(const char *text);
+// total samples, or -1 on error
+int magpie_synthesize_streaming(magpie_context *ctx, magpie_codec *codec, const char *text,
+                                const magpie_stream_params &params);
+int magpie_synthesize_sentence_streaming(magpie_context *ctx, magpie_codec *codec, const int32_t *tokens,
+                                         int n_tokens, const magpie_stream_params &params);
 
 // magpie.h:823 utility
 bool magpie_is_eos(const std::vector<int32_t> &frame_codes, int32_t eos_id);

@@ -108,8 +108,9 @@ int mp_hip_get_trace(mp_dev *dev, float *hidden);
  * frames_per_chunk frames (<= 0: 4, magpie.h:621) each utterance's new frames are
  * decoded by `codec` as one stateless chunk (decode_frames_to_audio,
  * magpie.cpp:4458-4476; the last chunk may be shorter) and passed to on_audio in
- * frame order; returning 0 stops that utterance (4820-4824). codes_out /
- * n_frames / total_samples may be NULL. */
+ * frame order; returning 0 stops that utterance (4820-4824). Once an utterance
+ * has ended (EOS, max_dec_steps or stopped) on_audio(utt, NULL, 0, user) is called
+ * once. codes_out / n_frames / total_samples may be NULL. */
 typedef int (*mp_audio_cb)(int utterance, const float *samples, int n_samples, void *user);
 int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_audio_cb on_audio, void *user,
                          int32_t *codes_out, int32_t *n_frames, int64_t *total_samples);
@@ -131,6 +132,18 @@ double mp_hip_op_bytes(mp_dev *dev, int op);
  * stream (same arguments as in the captured graph), one hipEvent pair around
  * the whole run; returns the mean per-launch time in us (kernel + dispatch gap). */
 int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us);
+
+/* --- text front end (host) ---------------------------------------------------- */
+/* magpie_tokenizer_init + magpie_tokenize (magpie.cpp:124-495): vocabulary and
+ * pronunciation dictionary from the GGUF strings magpie.tokenizer.vocab / .dict.
+ * mp_tokenize returns the token count (writing at most cap ids) or < 0. */
+typedef struct mp_tokenizer mp_tokenizer;
+int mp_tokenizer_load(const char *gguf_path, mp_tokenizer **out);
+int mp_tokenize(mp_tokenizer *tok, const char *text, int32_t *out, int cap);
+void mp_tokenizer_free(mp_tokenizer *tok);
+/* magpie_split_sentences (magpie.cpp:4439-4480): byte offset/length of each
+ * sentence (at most cap written); returns the sentence count or < 0. */
+int mp_split_sentences(const char *text, int32_t *offsets, int32_t *lengths, int cap);
 
 /* --- nano-codec ----------------------------------------------------------- */
 /* replaces magpie_codec_init / magpie_codec_load (nano-codec.cpp:205-352) */

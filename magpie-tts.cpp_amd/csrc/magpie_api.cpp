@@ -3,8 +3,11 @@
 // kernels behind mp_hip_*.
 #include "../../include/magpie.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <deque>
 
 static int env_device() {
     const char *s = getenv("MAGPIE_DEVICE");
@@ -23,7 +26,10 @@ magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_
         delete ctx;
         return nullptr;
     }
-    if (mp_hip_load_model(ctx->model.dev, model_path) != MP_OK) {
+    // MAGPIE_WEIGHTS=bf16 selects the bf16 decode projections (magpie_hip.h weight modes)
+    const char *wm = getenv("MAGPIE_WEIGHTS");
+    const int mode = wm && !strcmp(wm, "bf16") ? MP_WEIGHTS_BF16 : MP_WEIGHTS_AS_STORED;
+    if (mp_hip_load_model_ex(ctx->model.dev, model_path, mode) != MP_OK) {
         fprintf(stderr, "magpie: failed to load '%s': %s\n", model_path, mp_hip_error(ctx->model.dev));
         mp_hip_free(ctx->model.dev);
         delete ctx;
@@ -31,6 +37,9 @@ magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_
     }
     int dec = 12, enc = 6;
     mp_hip_model_info(ctx->model.dev, &dec, &enc, nullptr);
+    // the text front end rides in the same GGUF (magpie.cpp:853-858); optional
+    if (!magpie_tokenizer_load(&ctx->model.tokenizer, model_path))
+        fprintf(stderr, "magpie: no tokenizer in '%s' (token-id entry points only)\n", model_path);
     ctx->model.hparams.dec_layers = dec;
     ctx->model.hparams.enc_layers = enc;
     return ctx;
@@ -148,4 +157,166 @@ bool magpie_is_eos(const std::vector<int32_t> &frame_codes, int32_t eos_id) {
     for (int32_t c : frame_codes)
         if (c == eos_id) return true;
     return false;
+}
+
+// magpie_local_transformer_sample_all (magpie.cpp:1113-1317) on the device.
+magpie_sample_result magpie_local_transformer_sample_all(magpie_context *ctx, const float *decoder_hidden,
+                                                        float temperature, int top_k, bool forbid_eos) {
+    magpie_sample_result r;
+    if (!ctx || !ctx->model.dev || !decoder_hidden) return r;
+    int32_t smp[8], amx[8];
+    if (mp_hip_lt_sample(ctx->model.dev, decoder_hidden, temperature, top_k, forbid_eos ? 1 : 0, ctx->seed, smp, amx) !=
+        MP_OK) {
+        fprintf(stderr, "magpie: local transformer failed: %s\n", mp_hip_error(ctx->model.dev));
+        return r;  // empty: the reference's failure signal (sampled_codes.size() != 8)
+    }
+    r.sampled_codes.assign(smp, smp + 8);
+    r.argmax_codes.assign(amx, amx + 8);
+    return r;
+}
+
+// ---------------------------------------------------------------- streaming
+// magpie_split_sentences (magpie.cpp:4439-4480), over mp_split_sentences
+std::vector<std::string> magpie_split_sentences(const char *text) {
+    std::vector<std::string> out;
+    if (!text) return out;
+    const int n = mp_split_sentences(text, nullptr, nullptr, 0);
+    std::vector<int32_t> off(std::max(n, 0)), len(std::max(n, 0));
+    mp_split_sentences(text, off.data(), len.data(), n);
+    for (int i = 0; i < n; ++i) out.emplace_back(text + off[i], (size_t)len[i]);
+    return out;
+}
+
+namespace {
+
+// Runs one device batch of sentences through mp_hip_decode_stream and hands the
+// audio to the caller's callback in sentence order: sentence `next` streams
+// live, later ones are buffered until every earlier sentence has ended.
+struct OrderedStream {
+    const magpie_stream_params *prm;
+    int B = 0, next = 0, sentence0 = 0, n_sentences = 1;
+    std::vector<std::deque<std::vector<float>>> pending;
+    std::vector<int> ended, stopped, frames;
+    long long delivered = 0;
+
+    bool deliver(int u, const float *x, int n) {
+        delivered += n;
+        frames[u] += n / 1024;
+        bool go = prm->on_audio ? prm->on_audio(x, n, prm->user_data) : true;
+        if (prm->on_progress) prm->on_progress(frames[u], 0, 1, prm->user_data);  // (4826-4828)
+        return go;
+    }
+    void drain() {
+        while (next < B) {
+            auto &q = pending[next];
+            while (!q.empty() && !stopped[next]) {
+                std::vector<float> a = std::move(q.front());
+                q.pop_front();
+                if (!deliver(next, a.data(), (int)a.size())) stopped[next] = 1;
+            }
+            q.clear();
+            if (!ended[next]) break;
+            ++next;
+        }
+    }
+    static int cb(int u, const float *x, int n, void *self_) {
+        OrderedStream &s = *(OrderedStream *)self_;
+        if (n == 0) {
+            s.ended[u] = 1;
+            s.drain();
+            return 1;
+        }
+        if (s.stopped[u]) return 0;
+        if (u == s.next) {
+            if (!s.deliver(u, x, n)) { s.stopped[u] = 1; return 0; }
+            return 1;
+        }
+        s.pending[u].emplace_back(x, x + n);
+        return 1;  // a buffered sentence's stop is applied when it is delivered
+    }
+};
+
+long long stream_batch(magpie_context *ctx, magpie_codec *codec, const std::vector<std::vector<int32_t>> &sents,
+                       int sentence0, const magpie_stream_params &prm) {
+    const int B = (int)sents.size();
+    int tmax = 0;
+    for (auto &t : sents) tmax = std::max(tmax, (int)t.size());
+    std::vector<int32_t> tok((size_t)B * tmax, 0), nt(B), spk(B, prm.speaker_id);
+    for (int b = 0; b < B; ++b) {
+        nt[b] = (int32_t)sents[b].size();
+        std::copy(sents[b].begin(), sents[b].end(), tok.begin() + (size_t)b * tmax);
+    }
+    mp_params p{};
+    p.temperature = prm.temperature;
+    p.top_k = prm.top_k;
+    p.max_dec_steps = ctx->model.hparams.max_dec_steps;
+    p.seed = ctx->seed;
+    p.stream_base = sentence0;  // sentence i draws from stream i, batched or not
+    p.emit_eos_frame = 1;       // the streaming loop emits the EOS frame (magpie.cpp:4800-4806)
+    if (mp_hip_begin_batch(ctx->model.dev, tok.data(), nt.data(), spk.data(), B, tmax, &p) != MP_OK) {
+        fprintf(stderr, "magpie: %s\n", mp_hip_error(ctx->model.dev));
+        return -1;
+    }
+    OrderedStream os;
+    os.prm = &prm;
+    os.B = B;
+    os.pending.resize(B);
+    os.ended.assign(B, 0);
+    os.stopped.assign(B, 0);
+    os.frames.assign(B, 0);
+    if (mp_hip_decode_stream(ctx->model.dev, codec->dev, prm.frames_per_chunk, OrderedStream::cb, &os, nullptr,
+                             nullptr, nullptr) != MP_OK) {
+        fprintf(stderr, "magpie: %s\n", mp_hip_error(ctx->model.dev));
+        return -1;
+    }
+    os.drain();
+    return os.delivered;
+}
+
+}  // namespace
+
+// magpie_synthesize_sentence_streaming (magpie.cpp:4479-4840)
+int magpie_synthesize_sentence_streaming(magpie_context *ctx, magpie_codec *codec, const int32_t *tokens,
+                                         int n_tokens, const magpie_stream_params &params) {
+    if (!ctx || !ctx->model.dev || !codec || !codec->dev || !tokens || n_tokens <= 0) return -1;
+    ctx->temperature = params.temperature;  // as the reference does (4497-4499)
+    ctx->top_k = params.top_k;
+    ctx->speaker_id = params.speaker_id;
+    const long long n = stream_batch(ctx, codec, {std::vector<int32_t>(tokens, tokens + n_tokens)}, 0, params);
+    return n < 0 ? -1 : (int)n;
+}
+
+// magpie_synthesize_streaming (magpie.cpp:4843-4863). Sentences of the text run
+// as device batches of up to max_parallel_sentences; the audio reaches on_audio
+// in sentence order, sample for sample what the sentence-by-sentence loop gives.
+int magpie_synthesize_streaming(magpie_context *ctx, magpie_codec *codec, const char *text,
+                                const magpie_stream_params &params) {
+    if (!ctx || !ctx->model.dev || !codec || !codec->dev || !text) return -1;
+    std::vector<std::vector<int32_t>> sents;
+    if (params.sentence_chunking) {
+        std::vector<std::string> ss = magpie_split_sentences(text);
+        if (ss.empty()) ss.push_back(text);
+        for (auto &s : ss) {
+            std::vector<int32_t> t = magpie_tokenize(&ctx->model.tokenizer, s);
+            if (!t.empty()) sents.push_back(std::move(t));
+        }
+    } else {
+        std::vector<int32_t> t = magpie_tokenize(&ctx->model.tokenizer, text);
+        if (t.empty()) return -1;
+        sents.push_back(std::move(t));
+    }
+    ctx->temperature = params.temperature;
+    ctx->top_k = params.top_k;
+    ctx->speaker_id = params.speaker_id;
+    const int bmax = mp_hip_weight_mode(ctx->model.dev) == MP_WEIGHTS_BF16 ? 16 : 8;
+    const int P = std::max(1, std::min(params.max_parallel_sentences, bmax));
+    long long total = 0;
+    for (size_t s0 = 0; s0 < sents.size(); s0 += P) {
+        const size_t s1 = std::min(sents.size(), s0 + P);
+        if (params.on_progress) params.on_progress(0, (int)s0, (int)sents.size(), params.user_data);
+        const long long n = stream_batch(ctx, codec, {sents.begin() + s0, sents.begin() + s1}, (int)s0, params);
+        if (n < 0) return -1;
+        total += n;
+    }
+    return (int)total;
 }

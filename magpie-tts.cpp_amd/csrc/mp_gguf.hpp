@@ -104,6 +104,12 @@ public:
         auto it = u32_.find(key);
         return it == u32_.end() ? def : (int64_t)it->second;
     }
+    bool get_str(const std::string &key, std::string &out) const {
+        auto it = str_.find(key);
+        if (it == str_.end()) return false;
+        out = it->second;
+        return true;
+    }
     double get_f32(const std::string &key, double def) const {
         auto it = f32_.find(key);
         return it == f32_.end() ? def : it->second;
@@ -163,7 +169,11 @@ private:
     }
     void read_value(const std::string &key, uint32_t type) {
         static const int sz[13] = {1, 1, 2, 2, 4, 4, 4, 1, 0, 0, 8, 8, 8};
-        if (type == 8) { rd_str(); return; }
+        if (type == 8) {
+            std::string v = rd_str();
+            if (!key.empty()) str_[key] = std::move(v);
+            return;
+        }
         if (type == 9) {
             const uint32_t et = rd<uint32_t>();
             const uint64_t n = rd<uint64_t>();
@@ -191,6 +201,7 @@ private:
     std::map<std::string, GgufTensor> tensors_;
     std::map<std::string, uint64_t> u32_;
     std::map<std::string, double> f32_;
+    std::map<std::string, std::string> str_;
 };
 
 }  // namespace mp

@@ -987,7 +987,7 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
     const int NB = dev->NB, B = dev->B, S = dev->max_steps;
     if (int rc = prepare_iteration(dev)) return rc;
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<int> h_step(NB), h_done(NB), h_nf(NB), delivered(B, 0), stopped(B, 0);
+    std::vector<int> h_step(NB), h_done(NB), h_nf(NB), delivered(B, 0), stopped(B, 0), ended(B, 0);
     std::vector<int32_t> chunk((size_t)8 * fpc), fm((size_t)fpc * 8);
     std::vector<float> audio((size_t)fpc * 1024);
     int64_t samples = 0;
@@ -1029,6 +1029,10 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
                 }
             }
             if (!(done || stopped[b])) all_done = false;
+            else if (!ended[b]) {  // end-of-utterance notice: (utt, NULL, 0)
+                ended[b] = 1;
+                if (on_audio) on_audio(b, nullptr, 0, user);
+            }
         }
         if (all_done || it >= S) break;
     }

@@ -77,6 +77,10 @@ SYMBOLS = [
     ("mp_hip_op_name", ctypes.c_char_p, [_P, _I]),
     ("mp_hip_op_bytes", ctypes.c_double, [_P, _I]),
     ("mp_hip_time_op", _I, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+    ("mp_tokenizer_load", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
+    ("mp_tokenize", _I, [_P, ctypes.c_char_p, _P, _I]),
+    ("mp_tokenizer_free", None, [_P]),
+    ("mp_split_sentences", _I, [ctypes.c_char_p, _P, _P, _I]),
     ("mp_hip_codec_init", _I, [_I, ctypes.c_char_p, ctypes.POINTER(_P)]),
     ("mp_hip_codec_decode", _I, [_P, _P, _I, _P]),
     ("mp_hip_codec_decode_chunks", _I, [_P, _P, _I, _I, _P]),
@@ -217,6 +221,8 @@ class Device:
         B = self.begin(tokens, speakers, max_dec_steps, temperature, top_k, False, seed, False, stream_base, True)
 
         def _cb(utt, ptr, n, _user):
+            if n == 0:  # end-of-utterance notice
+                return 1
             return 1 if on_audio(utt, np.ctypeslib.as_array(ptr, shape=(n,)).copy()) is not False else 0
 
         cb = AUDIO_CB(_cb)
@@ -262,6 +268,49 @@ class Device:
         us = ctypes.c_float()
         self._check(self.lib.mp_hip_time_op(self.h, op, reps, ctypes.byref(us)))
         return us.value
+
+
+class Tokenizer:
+    """Text front end of the reference (magpie_tokenizer_init / magpie_tokenize,
+    magpie.cpp:124-495), host C++ in libmagpie_hip.so."""
+
+    def __init__(self, gguf_path: str):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.mp_tokenizer_load(gguf_path.encode(), ctypes.byref(h))
+        if rc != MP_OK or not h.value:
+            raise MagpieError(f"{gguf_path}: no tokenizer ({_ERRS.get(rc, rc)})")
+        self.h = h
+
+    def __call__(self, text: str) -> List[int]:
+        raw = text.encode("utf-8")
+        n = self.lib.mp_tokenize(self.h, raw, None, 0)
+        if n < 0:
+            raise MagpieError(f"mp_tokenize failed ({n})")
+        out = (ctypes.c_int32 * max(n, 1))()
+        self.lib.mp_tokenize(self.h, raw, out, n)
+        return list(out[:n])
+
+    def close(self) -> None:
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.mp_tokenizer_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def split_sentences(text: str) -> List[str]:
+    """magpie_split_sentences (magpie.cpp:4439-4480) via the C-ABI."""
+    lib = load_library()
+    raw = text.encode("utf-8")
+    n = lib.mp_split_sentences(raw, None, None, 0)
+    off, ln = (ctypes.c_int32 * max(n, 1))(), (ctypes.c_int32 * max(n, 1))()
+    lib.mp_split_sentences(raw, off, ln, n)
+    return [raw[off[i]:off[i] + ln[i]].decode("utf-8") for i in range(n)]
 
 
 class Codec:

@@ -238,6 +238,50 @@ static void plan_magpie(int dtype, int dec_layers, int enc_layers, int dec_pos) 
     kv_u32("magpie.decoder_layers", 12);
     kv_u32("magpie.text_bos_id", 2378);
     kv_u32("magpie.text_eos_id", 2379);
+    // synthetic text front end (the real one ships NeMo's IPA vocabulary and CMU-style
+    // dictionary as magpie.tokenizer.vocab / .dict): ids 0-25 upper-case letters
+    // (out-of-dictionary fallback), 26-31 punctuation, IPA symbols (some multi-byte,
+    // some two-symbol tokens for the longest-match rule), 93 space, 94 pad, 95 oov
+    {
+        static const char *ipa[] = {"a", "b", "d", "e", "f", "h", "i", "j", "k", "l", "m", "n", "o", "p", "r",
+                                    "s", "t", "u", "v", "w", "z", "\xc9\x99" /*ə*/, "\xc9\xaa" /*ɪ*/,
+                                    "\xca\x8a" /*ʊ*/, "\xc9\x9b" /*ɛ*/, "\xc3\xa6" /*æ*/, "\xc9\x91" /*ɑ*/,
+                                    "\xc9\x94" /*ɔ*/, "\xca\x83" /*ʃ*/, "\xca\x92" /*ʒ*/, "\xce\xb8" /*θ*/,
+                                    "\xc3\xb0" /*ð*/, "\xc5\x8b" /*ŋ*/, "\xcb\x88" /*ˈ*/, "\xcb\x8c" /*ˌ*/,
+                                    "\xc9\xb9" /*ɹ*/, "\xc9\x9d" /*ɝ*/, "\xc9\x9a" /*ɚ*/, "o\xca\x8a" /*oʊ*/,
+                                    "a\xc9\xaa" /*aɪ*/, "e\xc9\xaa" /*eɪ*/, "a\xca\x8a" /*aʊ*/,
+                                    "\xc9\x94\xc9\xaa" /*ɔɪ*/, "t\xca\x83" /*tʃ*/, "d\xca\x92" /*dʒ*/, "'", "-"};
+        static char vocab[4096];
+        size_t n = 0;
+        const int nipa = (int)(sizeof ipa / sizeof ipa[0]);
+        for (int id = 0; id < 96; ++id) {
+            char tok[32];
+            if (id < 26) snprintf(tok, sizeof tok, "%c", 'A' + id);
+            else if (id < 32) snprintf(tok, sizeof tok, "%c", ",.!?:;"[id - 26]);
+            else if (id - 32 < nipa) snprintf(tok, sizeof tok, "%s", ipa[id - 32]);
+            else if (id == 93) snprintf(tok, sizeof tok, " ");
+            else if (id == 94) snprintf(tok, sizeof tok, "<pad>");
+            else if (id == 95) snprintf(tok, sizeof tok, "<oov>");
+            else snprintf(tok, sizeof tok, "<unused%d>", id);
+            n += (size_t)snprintf(vocab + n, sizeof vocab - n, id ? "\n%s" : "%s", tok);
+        }
+        kv_str("magpie.tokenizer.vocab", vocab);
+        kv_str("magpie.tokenizer.dict",
+               "hello\th\xc9\x99\xcb\x88lo\xca\x8a\n"            /* həˈloʊ */
+               "world\tw\xcb\x88\xc9\x9dld\n"                      /* wˈɝld */
+               "the\t\xc3\xb0\xc9\x99\n"                           /* ðə */
+               "and\t\xc3\xa6nd\n"                                  /* ænd */
+               "twenty\tt w\xcb\x88\xc9\x9bnti\n"                  /* a space inside: no token, skipped */
+               "four\tf\xcb\x88\xc9\x94\xc9\xb9\n"                /* fˈɔɹ */
+               "dollars\td\xcb\x88\xc9\x91l\xc9\x9az\n"          /* dˈɑlɚz */
+               "percent\tp\xc9\x9a\xcb\x88s\xc9\x9bnt\n"         /* pɚˈsɛnt */
+               "first\tf\xcb\x88\xc9\x9dst\n"                      /* fˈɝst */
+               "voice\tv\xcb\x88\xc9\x94\xc9\xaas\n"             /* vˈɔɪs */
+               "joy\td\xca\x92\xcb\x88\xc9\x94\xc9\xaa\xe2\x82\xac");  /* dʒˈɔɪ + an unknown 3-byte char */
+        kv_u32("magpie.tokenizer.space", 93);
+        kv_u32("magpie.tokenizer.pad", 94);
+        kv_u32("magpie.tokenizer.oov", 95);
+    }
     kv_u32("magpie.audio_bos_id", 2016);
     kv_u32("magpie.audio_eos_id", 2017);
     // keys the reader actually honours (magpie.cpp:85-120); only written when a

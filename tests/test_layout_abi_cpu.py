@@ -179,7 +179,7 @@ def test_generator_is_deterministic(tmp_path):
 
 def _declared_symbols():
     src = open(HDR).read()
-    return sorted(set(re.findall(r"\b(mp_hip_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(mp_\w+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -194,7 +194,14 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-DC", ma.LIB_PATH], capture_output=True, text=True).stdout
     for fn in ["magpie_init(char const*)", "magpie_free(magpie_context*)",
                "magpie_synthesize_codes_graph_reuse(magpie_context*, int const*, int)",
-               "magpie_codec_decode(magpie_codec*, int const*, int)", "magpie_codec_init(char const*)"]:
+               "magpie_codec_decode(magpie_codec*, int const*, int)", "magpie_codec_init(char const*)",
+               "magpie_local_transformer_sample_all(magpie_context*, float const*, float, int, bool)",
+               "magpie_split_sentences[abi:cxx11](char const*)",
+               "magpie_synthesize_streaming(magpie_context*, magpie_codec*, char const*, magpie_stream_params const&)",
+               "magpie_synthesize_sentence_streaming(magpie_context*, magpie_codec*, int const*, int, "
+               "magpie_stream_params const&)",
+               "magpie_tokenize(magpie_tokenizer const*, std::__cxx11::basic_string<char, std::char_traits<char>, "
+               "std::allocator<char> > const&)"]:
         assert fn in out, fn
 
 

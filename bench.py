@@ -56,6 +56,47 @@ def decoder_bytes_per_frame(B: int, L_mean: float, T: int, dec_layers: int = 12,
     return 4.0 * (W_dec + W_lt) / B + per_utt
 
 
+def _decode_fps(dev, B, frames, steps=2):
+    ms = []
+    for _ in range(steps):
+        ms.append(dev.decode(B, frames).decode_ms)
+    return B * frames * 1e3 / float(np.median(ms))
+
+
+def measure_extra(model_path: str, codec_path, args) -> dict:
+    """Throughput of the BASELINE configs' other shapes on this one GPU (fixed-length
+    greedy decode, same synthetic prompts): bf16 projections at batch 1, 8
+    (configs[3]'s per-GPU share of batch 64) and 16 (configs[2]); and the streaming
+    path (sentence streaming, 4-frame codec chunks): time to first audio and
+    real-time factor of one utterance."""
+    out = {}
+    dev = ma.Device(model_path, weights="bf16")
+    for B in (1, 8, 16):
+        toks = [ma.synthetic_tokens(args.tokens, seed=1000 + b) for b in range(B)]
+        dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=args.frames, ignore_eos=True)
+        out[f"bf16_batch{B}_fps"] = round(_decode_fps(dev, B, args.frames), 1)
+    dev.close()
+    if codec_path:
+        dev = ma.Device(model_path)
+        cdc = ma.Codec(codec_path)
+        tok = [ma.synthetic_tokens(args.tokens, seed=1000)]
+        dev.synthesize_stream(cdc, tok, lambda u, a: True, max_dec_steps=32)  # warm-up
+        t0 = time.perf_counter()
+        n = [0]
+
+        def on_audio(u, a):
+            n[0] += len(a)
+            return True
+        codes, total, tm = dev.synthesize_stream(cdc, tok, on_audio, max_dec_steps=args.frames)
+        wall = time.perf_counter() - t0
+        out["stream_f32_batch1"] = {"frames": int(len(codes[0])), "first_audio_ms": round(tm.preamble_ms +
+                                    tm.first_audio_ms, 2), "preamble_ms": round(tm.preamble_ms, 2),
+                                    "rtf": round(total / 22050.0 / wall, 1), "chunk_frames": 4}
+        cdc.close()
+        dev.close()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,6 +110,7 @@ def main() -> None:
                     help="oracle threads for cpu_baseline (ggml's default n_threads, magpie.h:298,306)")
     ap.add_argument("--profile-ops", type=int, default=30, help="event-timed launches per op for the roofline")
     ap.add_argument("--no-codec", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the bf16 batch / streaming measurements")
     ap.add_argument("--weights", choices=["f32", "bf16"], default="f32",
                     help="f32 = configs[1]; bf16 = configs[2]/[3] (decode projections on bf16 MFMA, batch <= 16)")
     args = ap.parse_args()
@@ -131,8 +173,8 @@ def main() -> None:
 
     # ---- nano-codec on the device: every utterance's 256 frames as 32-frame chunks
     codec = None
+    codec_path = os.path.join(cache, "nano_codec.gguf")
     if not args.no_codec:
-        codec_path = os.path.join(cache, "nano_codec.gguf")
         if rank == 0 or world == 1:
             ma.synth_gguf(codec_path, kind="codec")
         if dist is not None:
@@ -159,10 +201,14 @@ def main() -> None:
                  "tflops": round(tfs, 1), "mfma_f16_peak_tflops": MFMA_F16_PEAK_TFS,
                  "frac": round(tfs / MFMA_F16_PEAK_TFS, 4), "audio_peak": round(float(np.abs(audio).max()), 4)}
 
-    # ---- roofline of the dominant kernel (event-timed live, same stream as the graph)
+    # ---- roofline of the dominant kernel (event-timed live, same stream as the graph).
+    # The ops are re-timed at the mid-utterance state (cache length L = 110 + frames/2
+    # + 1, the mean over the decode) so that length-dependent kernels (attention)
+    # match the per-launch average a kernel trace of the whole decode reports.
     roofline = None
     op_table = {}
     if rank == 0:
+        dev.synthesize(toks, speakers=speakers, max_dec_steps=args.frames // 2, ignore_eos=True)
         names = dev.ops()
         groups = {}
         for i, n in enumerate(names):
@@ -191,6 +237,11 @@ def main() -> None:
                "kind": "port",
                "sample": f"1 utterance x {res['frames']} frames (T={args.tokens}), decode loop only "
                          f"(preamble {res['preamble_s']:.2f}s excluded), oracle f32-accumulate mode"}
+
+    # ---- the other BASELINE configs' shapes on this GPU (rank 0 at N=1 only)
+    extra = None
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = measure_extra(model_path, codec_path if not args.no_codec else None, args)
 
     if rank == 0:
         L_mean = 110 + (args.frames + 1) / 2.0  # keys 111..366 over BOS + 255 steps
@@ -228,6 +279,7 @@ def main() -> None:
             "roofline": roofline,
             "cpu_baseline": cpu,
             "ops": op_table,
+            "extra_configs": extra,
         }
         print(json.dumps(line), flush=True)
     dev.close()

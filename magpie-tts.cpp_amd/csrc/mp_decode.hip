@@ -84,173 +84,176 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 }
 
 // ---------------------------------------------------------------- SA decode attention
-// Split-K over the key axis: workgroup (chunk, head, slot) handles 64 keys and
-// writes (max, sum, o[64]); the last of a head's active chunks to arrive
-// combines them in-launch (a[d] = sum_c e^(m_c-M) o_c[d] / sum_c e^(m_c-M) l_c)
-// and writes the head's 64 outputs, so the O-projection reads a plain vector.
-// 16 lanes x float4 cover one 64-dim key row (256 B, coalesced); a wave does 4
-// keys per instruction. Keys j > pos are masked (L = pos + 1, magpie.cpp:3412).
-__global__ __launch_bounds__(MP_BLOCK) void sa_attn_kernel(AttnP p) {
-    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+// One workgroup of 16 waves per (head, slot) over the whole live cache, no
+// split-K and no combine pass: wave w takes keys 4(w + 16 r) + kk (16 lanes x
+// float4 cover one 64-dim row, a wave does 4 keys per instruction) with four
+// iterations' K and V loads in flight, keeps an online softmax (m, l, o[64]),
+// and the 16 wave states are merged through LDS. Keys j > pos are masked
+// (L = pos + 1, magpie.cpp:3412); softmax(K q / 8) V per head (3457-3476).
+constexpr int SA_WAVES = 16, SA_THREADS = SA_WAVES * 64, SA_IF = 4;  // iterations in flight
+__global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
+    const int h = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    __shared__ float sc[SA_CHUNK + MP_NWAVES * DH + 4];
-    float *ow = sc + SA_CHUNK;  // [MP_NWAVES][DH]
-    const int j0 = c * SA_CHUNK;
     const int kk = lane >> 4, dc = lane & 15;
-    // Issue q, all 4 K rows and all 4 V rows of this lane first: rows j < max_seq
-    // are always valid memory, so no load waits for the live length L = pos + 1.
+    __shared__ float wm[SA_WAVES], wl[SA_WAVES];
+    __shared__ __attribute__((aligned(16))) float wo[SA_WAVES][DH];
     const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
-    float4 k4[4], v4[4];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int j = j0 + w * 16 + it * 4 + kk;
-        k4[it] = *(const float4 *)(p.kc + base + (size_t)j * D);
-        v4[it] = *(const float4 *)(p.vc + base + (size_t)j * D);
-    }
     const int L = p.pos[b] + 1;
-    if (j0 >= L) return;  // inactive chunk: takes no ticket
-    const int nact = (L + SA_CHUNK - 1) / SA_CHUNK;
-    float *P = p.part + ((size_t)(b * NH + h) * p.nch + c) * PART_STRIDE;
-    float s[4];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int j = j0 + w * 16 + it * 4 + kk;
-        const float v = group_sum<16>(dotv(q4, k4[it]));
-        s[it] = j < L ? v * 0.125f : -INFINITY;  // 1/sqrt(64)
-    }
-    if (dc == 0)
-#pragma unroll
-        for (int it = 0; it < 4; ++it) sc[w * 16 + it * 4 + kk] = s[it];
-    lds_sync();
-    // every wave reduces the chunk's 64 scores itself: lane i holds key i
-    const float si = sc[lane];
-    const float m = wave_max(si);
-    const float l = wave_sum(si == -INFINITY ? 0.f : expf(si - m));
+    float m = -INFINITY, l = 0.f;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r0 = 0; 64 * r0 < L; r0 += SA_IF) {
+        float4 k4[SA_IF], v4[SA_IF];
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int j = j0 + w * 16 + it * 4 + kk;
-        if (j < L) {
-            const float e = expf(s[it] - m);
-            o.x += e * v4[it].x; o.y += e * v4[it].y; o.z += e * v4[it].z; o.w += e * v4[it].w;
+        for (int u = 0; u < SA_IF; ++u) {
+            // rows < max_seq are always valid memory: no load waits for the mask
+            const int j = min(4 * (w + SA_WAVES * (r0 + u)) + kk, p.max_seq - 1);
+            k4[u] = *(const float4 *)(p.kc + base + (size_t)j * D);
+            v4[u] = *(const float4 *)(p.vc + base + (size_t)j * D);
         }
+        float s[SA_IF];
+        float mb = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < SA_IF; ++u) {
+            const int j = 4 * (w + SA_WAVES * (r0 + u)) + kk;
+            const float v = group_sum<16>(dotv(q4, k4[u])) * 0.125f;  // 1/sqrt(64)
+            s[u] = j < L ? v : -INFINITY;
+            mb = fmaxf(mb, s[u]);
+        }
+        mb = wave_max(mb);
+        if (mb == -INFINITY) continue;  // nothing live for this wave in this batch
+        const float mn = fmaxf(m, mb), c = expf(m - mn);
+        l *= c;
+        o.x *= c; o.y *= c; o.z *= c; o.w *= c;
+#pragma unroll
+        for (int u = 0; u < SA_IF; ++u) {
+            const float e = s[u] == -INFINITY ? 0.f : expf(s[u] - mn);
+            l += e;  // per lane: its key group's keys; summed over the wave below
+            o.x += e * v4[u].x; o.y += e * v4[u].y; o.z += e * v4[u].z; o.w += e * v4[u].w;
+        }
+        m = mn;
     }
+    // merge the 4 key groups of the wave (lanes l, l^16, l^32, l^48 share dims)
 #pragma unroll
     for (int msk = 16; msk <= 32; msk <<= 1) {
         o.x += __shfl_xor(o.x, msk, 64); o.y += __shfl_xor(o.y, msk, 64);
         o.z += __shfl_xor(o.z, msk, 64); o.w += __shfl_xor(o.w, msk, 64);
+        l += __shfl_xor(l, msk, 64);
     }
-    if (lane < 16) *(float4 *)(&ow[w * DH + 4 * lane]) = o;
+    if (lane < 16) *(float4 *)(&wo[w][4 * lane]) = o;
+    if (lane == 0) { wm[w] = m; wl[w] = l; }
     lds_sync();
-    if (p.mode == SA_PARTIALS) {  // plain stores; the combine is the next launch
-        if (tid < DH) P[16 + tid] = (ow[tid] + ow[DH + tid]) + (ow[2 * DH + tid] + ow[3 * DH + tid]);
-        else if (tid == 64) { P[0] = m; P[1] = l; }
-        return;
-    }
-    if (tid < DH / 2) {
-        const int d = 2 * tid;
-        st_sc1(P + 16 + d, (ow[d] + ow[DH + d]) + (ow[2 * DH + d] + ow[3 * DH + d]),
-               (ow[d + 1] + ow[DH + d + 1]) + (ow[2 * DH + d + 1] + ow[3 * DH + d + 1]));
-    } else if (tid == 64) {
-        st_sc1(P, m, l);
-    }
-    if (!arrive_last(p.cnt + b * NH + h, (unsigned)nact, sc + SA_CHUNK + MP_NWAVES * DH, p.mode == SA_COMBINE_SC1))
-        return;
     if (tid >= DH) return;
-    const float *Pb = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
-    float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
-#pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc) {  // unconditional (clamped) loads: no branch per load
-        const float *Pc = Pb + min(cc, nact - 1) * PART_STRIDE;
-        mv[cc] = ld_sc1(Pc);
-        lv[cc] = ld_sc1(Pc + 1);
-        ov[cc] = ld_sc1(Pc + 16 + tid);
-    }
-#pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc)
-        if (cc >= nact) { mv[cc] = -INFINITY; lv[cc] = 0.f; ov[cc] = 0.f; }
     float M = -INFINITY;
 #pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc) M = fmaxf(M, mv[cc]);
+    for (int q = 0; q < SA_WAVES; ++q) M = fmaxf(M, wm[q]);
     float num = 0.f, den = 0.f;
 #pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc) {
-        const float e = mv[cc] == -INFINITY ? 0.f : expf(mv[cc] - M);
-        den += e * lv[cc];
-        num += e * ov[cc];
+    for (int q = 0; q < SA_WAVES; ++q) {
+        const float e = wm[q] == -INFINITY ? 0.f : expf(wm[q] - M);
+        den += e * wl[q];
+        num += e * wo[q][tid];
     }
     p.out[(size_t)b * D + h * DH + tid] = num / den;
 }
 
 // ---------------------------------------------------------------- fused XA
-// grid (768/64, B): every workgroup recomputes LN(x) and all T scores (K' rows
-// are L2-resident after the first workgroup), then owns 64 output dims.
-__global__ __launch_bounds__(MP_BLOCK) void xa_fused_kernel(XaP p) {
-    __shared__ __attribute__((aligned(16))) float act[D];
-    __shared__ float red[8];
+// grid (768/64, B), 16 waves per workgroup. Every wave normalises x itself (the
+// same DPP statistics in every wave: no barrier) and scores keys t = w, w+16, ...
+// with all of its K' loads in flight at once (12 scalar loads per key per lane,
+// each a coalesced 256 B wave access), so the score phase costs one L2 round trip
+// instead of one per group of keys. The workgroup then owns 64 output dims:
+// out[d] = x[d] + sum_t e_t V'_t[d] / l (K' rows are L2-resident after the first
+// workgroup; the 12 workgroups of a slot share them).
+constexpr int XA_WAVES = 16, XA_THREADS = XA_WAVES * 64, XA_KPW = 4;  // keys in flight per wave
+constexpr int XA_VPW = 8;  // V' values prefetched per lane (keys t = w + 16 u)
+__global__ __launch_bounds__(XA_THREADS) void xa_fused_kernel(XaP p) {
     __shared__ float sc[TMAX_LIMIT];
-    __shared__ float part[MP_NWAVES][64];
+    __shared__ float part[XA_WAVES][64];
     const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int d0 = blockIdx.x * 64;
     const int Tb = p.T[b];
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
     const float *Kp = p.kp + base, *Vp = p.vp + base;
-    // LN(x) (magpie.cpp:3513)
-    {
-        float v[3];
+    // Nothing below the loads depends on x: issue the first keys' K' rows and this
+    // lane's V' values, then x, so the three fetches share one memory round trip.
+    float k[XA_KPW][D / 64];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) v[i] = p.x[(size_t)b * D + tid + MP_BLOCK * i];
+    for (int u = 0; u < XA_KPW; ++u) {
+        const int t = w + XA_WAVES * u;
+        const float *kr = Kp + (size_t)(t < Tb ? t : 0) * D + lane;
+#pragma unroll
+        for (int i = 0; i < D / 64; ++i) k[u][i] = kr[64 * i];
+    }
+    float vv[XA_VPW];
+#pragma unroll
+    for (int u = 0; u < XA_VPW; ++u) {
+        const int t = w + XA_WAVES * u;
+        vv[u] = Vp[(size_t)(t < Tb ? t : 0) * D + d0 + lane];
+    }
+    asm volatile("" ::: "memory");  // keep these loads ahead of the x fetch and the loop below
+    // LN(x) (magpie.cpp:3513): lane owns elements lane + 64 i
+    float h[D / 64];
+    {
+        float v[D / 64];
+#pragma unroll
+        for (int i = 0; i < D / 64; ++i) v[i] = p.x[(size_t)b * D + lane + 64 * i];
         float mean, var;
-        block_meanvar<3>(v, red, mean, var);
+        wave_meanvar<D / 64>(v, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) act[tid + MP_BLOCK * i] = ((v[i] - mean) * rstd) * p.lnw[tid + MP_BLOCK * i];
+        for (int i = 0; i < D / 64; ++i) h[i] = ((v[i] - mean) * rstd) * p.lnw[lane + 64 * i];
     }
-    lds_sync();
-    const float4 a0 = *(const float4 *)(act + 4 * lane), a1 = *(const float4 *)(act + 256 + 4 * lane),
-                 a2 = *(const float4 *)(act + 512 + 4 * lane);
     const float scale = 1.0f / sqrtf((float)DXA);
-    // scores: wave w takes rows w, w+4, ...; 4 rows (12 float4 per lane) in flight
-    for (int tb = w; tb < Tb; tb += 16) {
-        float4 k[4][3];
+    for (int t0 = w;; t0 += XA_WAVES * XA_KPW) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = tb + 4 * u;
-            const float *kr = Kp + (size_t)(t < Tb ? t : 0) * D;
-            k[u][0] = *(const float4 *)(kr + 4 * lane);
-            k[u][1] = *(const float4 *)(kr + 256 + 4 * lane);
-            k[u][2] = *(const float4 *)(kr + 512 + 4 * lane);
-        }
+        for (int u = 0; u < XA_KPW; ++u) {
+            float acc = 0.f;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = tb + 4 * u;
-            const float sv = wave_sum(dotv(k[u][0], a0) + dotv(k[u][1], a1) + dotv(k[u][2], a2));
+            for (int i = 0; i < D / 64; ++i) acc += k[u][i] * h[i];
+            const float sv = wave_sum(acc);
+            const int t = t0 + XA_WAVES * u;
             if (lane == 0 && t < Tb) sc[t] = sv * scale;
         }
+        const int t1 = t0 + XA_WAVES * XA_KPW;
+        if (t1 >= Tb) break;
+#pragma unroll
+        for (int u = 0; u < XA_KPW; ++u) {  // next keys (long texts)
+            const int t = t1 + XA_WAVES * u;
+            const float *kr = Kp + (size_t)(t < Tb ? t : 0) * D + lane;
+#pragma unroll
+            for (int i = 0; i < D / 64; ++i) k[u][i] = kr[64 * i];
+        }
     }
     lds_sync();
+    // softmax statistics: every wave reduces the T scores itself
     float m = -INFINITY;
-    for (int t = tid; t < Tb; t += MP_BLOCK) m = fmaxf(m, sc[t]);
-    m = block_max(m, red);
+    for (int t = lane; t < Tb; t += 64) m = fmaxf(m, sc[t]);
+    m = wave_max(m);
     float l = 0.f;
-    for (int t = tid; t < Tb; t += MP_BLOCK) { const float e = expf(sc[t] - m); sc[t] = e; l += e; }
-    l = block_sum(l, red);
-    // out[d] = sum_t e_t V'_t[d] / l for the workgroup's 64 dims; 4 time groups
+    for (int t = lane; t < Tb; t += 64) l += expf(sc[t] - m);
+    l = wave_sum(l);
+    // out[d] = sum_t e_t V'_t[d] / l for this workgroup's 64 dims; wave w takes t = w (mod 16)
     float acc = 0.f;
-#pragma unroll 8
-    for (int t = w; t < Tb; t += MP_NWAVES) acc += sc[t] * Vp[(size_t)t * D + d0 + lane];
+#pragma unroll
+    for (int u = 0; u < XA_VPW; ++u) {
+        const int t = w + XA_WAVES * u;
+        if (t < Tb) acc += expf(sc[t] - m) * vv[u];
+    }
+    for (int t = w + XA_WAVES * XA_VPW; t < Tb; t += XA_WAVES) acc += expf(sc[t] - m) * Vp[(size_t)t * D + d0 + lane];
     part[w][lane] = acc;
     lds_sync();
     if (tid < 64) {
-        const float o = ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid])) / l;
-        p.x_out[(size_t)b * D + d0 + tid] = o + p.x[(size_t)b * D + d0 + tid];
+        float o = 0.f;
+#pragma unroll
+        for (int q = 0; q < XA_WAVES; ++q) o += part[q][tid];
+        p.x_out[(size_t)b * D + d0 + tid] = o / l + p.x[(size_t)b * D + d0 + tid];
     }
 }
 
 hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
     if (!p.x || !p.x_out || !p.lnw || !p.kp || !p.vp || !p.T || p.Tmax < 1 || p.Tmax > TMAX_LIMIT) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(xa_fused_kernel, dim3(D / 64, B), dim3(MP_BLOCK), 0, s, p);
+    hipLaunchKernelGGL(xa_fused_kernel, dim3(D / 64, B), dim3(XA_THREADS), 0, s, p);
     return hipGetLastError();
 }
 
@@ -380,47 +383,11 @@ hipError_t op_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 1,
 // bf16 weight mode at 16 slots: only the f32 LT in_proj runs on the GEMV family
 hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, D, PRO_LN, EPI_BIAS>(p, s); }
 
-// Combine of the SA_PARTIALS mode: one wave per (head, slot), the same arithmetic
-// as the in-launch combiner (identical results in every mode).
-__global__ __launch_bounds__(64) void sa_combine_kernel(AttnP p) {
-    const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-    const int nact = (p.pos[b] + 1 + SA_CHUNK - 1) / SA_CHUNK;
-    const float *Pb = p.part + (size_t)(b * NH + h) * p.nch * PART_STRIDE;
-    float mv[NCH_MAX], lv[NCH_MAX], ov[NCH_MAX];
-#pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc) {
-        const float *Pc = Pb + min(cc, nact - 1) * PART_STRIDE;
-        mv[cc] = Pc[0];
-        lv[cc] = Pc[1];
-        ov[cc] = Pc[16 + d];
-    }
-#pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc)
-        if (cc >= nact) { mv[cc] = -INFINITY; lv[cc] = 0.f; ov[cc] = 0.f; }
-    float M = -INFINITY;
-#pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc) M = fmaxf(M, mv[cc]);
-    float num = 0.f, den = 0.f;
-#pragma unroll
-    for (int cc = 0; cc < NCH_MAX; ++cc) {
-        const float e = mv[cc] == -INFINITY ? 0.f : expf(mv[cc] - M);
-        den += e * lv[cc];
-        num += e * ov[cc];
-    }
-    p.out[(size_t)b * D + h * DH + d] = num / den;
-}
-
-hipError_t op_sa_combine(const AttnP &p, int B, hipStream_t s) {
-    if (!p.part || !p.out || !p.pos || p.nch < 1 || p.nch > NCH_MAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sa_combine_kernel, dim3(NH, B), dim3(64), 0, s, p);
-    return hipGetLastError();
-}
 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
-    if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || !p.out || !p.cnt || p.nch < 1 || p.nch > NCH_MAX ||
-        p.nch * SA_CHUNK > p.max_seq)
+    if (!p.q || !p.kc || !p.vc || !p.pos || !p.out || p.max_seq < 1 || p.max_seq > NCH_MAX * SA_CHUNK)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sa_attn_kernel, dim3(p.nch, NH, B), dim3(MP_BLOCK), 0, s, p);
+    hipLaunchKernelGGL(sa_attn_kernel, dim3(NH, B), dim3(SA_THREADS), 0, s, p);
     return hipGetLastError();
 }
 

@@ -17,9 +17,8 @@ constexpr int LTF = 1024;     // LT ffn dim                   (magpie.h:55)
 constexpr int NCB = 8;        // codebooks                    (magpie.h:61)
 constexpr int VCB = 2024;     // vocab per codebook           (magpie.h:63)
 constexpr int CTX = 110;      // baked context frames         (magpie.h:67)
-constexpr int SA_CHUNK = 64;  // keys per split-K attention workgroup
-constexpr int NCH_MAX = 16;   // split-K chunks -> max_seq <= 1024 (reference: 626, magpie.cpp:4077)
-constexpr int PART_STRIDE = 80;  // [m, l, pad.., o[64] at +16]
+constexpr int SA_CHUNK = 64;  // cache rows are allocated in whole 64-key chunks
+constexpr int NCH_MAX = 16;   // -> max_seq <= 1024 (reference: 626, magpie.cpp:4077)
 constexpr int TMAX_LIMIT = 1024;  // text tokens per utterance (LDS score buffer)
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
@@ -141,20 +140,12 @@ struct XaP {
     int Tmax, layer, nlayers;
 };
 
-struct AttnP {  // split-K decode self-attention (one query per utterance)
+struct AttnP {  // decode self-attention (one query per utterance)
     const float *q;
     const float *kc, *vc;
     int layer, nlayers, max_seq;
     const int *pos;
-    float *part;
-    int nch;
-    const int *ndone;
-    int nslots;
-    float *out;          // [B][768] combined attention output
-    unsigned *cnt;       // [B][12] arrival tickets (zero between launches)
-    int mode;            // SA_COMBINE_SC1 / SA_COMBINE_ACQ: last arriver combines in-launch;
-                         // SA_PARTIALS: partials only, sa_combine_kernel follows (large batches)
+    float *out;          // [B][768] attention output
 };
-enum { SA_COMBINE_SC1 = 0, SA_COMBINE_ACQ = 1, SA_PARTIALS = 2 };
 
 }  // namespace mp

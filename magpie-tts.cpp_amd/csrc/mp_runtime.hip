@@ -55,7 +55,6 @@ MP_DECL_B16(8)
 MP_DECL_B16(16)
 hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
-hipError_t op_sa_combine(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
 
@@ -103,7 +102,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_COMB = 4 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3 };
 struct OpRec {
     std::string name;
     int kind;
@@ -140,9 +139,8 @@ struct mp_dev {
     mp_params params{};
     // device state (one allocation per buffer, sized for the configuration)
     std::vector<void *> allocs;
-    float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *part = nullptr, *sa_out = nullptr,
+    float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *sa_out = nullptr,
           *h = nullptr, *hidden = nullptr;
-    unsigned *sa_cnt = nullptr;
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
@@ -434,8 +432,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     int rc = MP_OK;
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
-    A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(part, (size_t)NB * 12 * dev->nch * mp::PART_STRIDE);
-    A(sa_out, NB * 768); A(sa_cnt, NB * 12);
+    A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(sa_out, NB * 768);
     A(h, NB * 3072); A(hidden, NB * D);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -502,12 +499,8 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         if (l == 0) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
         if ((rc = run(l == 0 ? "qkv_embed" : "qkv", l == 0 ? tb.qkv_embed : tb.qkv, g,
                       F * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
-        // split-K self-attention over the cache, combined in-launch (3457-3476)
-        // batch <= 2: the last chunk to arrive combines in-launch (sc1 loads while the
-        // grid fits one workgroup per CU); larger batches: partials + a combine launch
-        const int sa_mode = NB >= 4 ? mp::SA_PARTIALS : dev->nch * 12 * NB <= 256 ? mp::SA_COMBINE_SC1 : mp::SA_COMBINE_ACQ;
-        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->part, dev->nch, dev->ndone, NB,
-                    dev->sa_out, dev->sa_cnt, sa_mode};
+        // self-attention over the cache, one workgroup per (head, slot) (3457-3476)
+        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->sa_out};
         if (record) {
             mp::OpRec r{};
             r.name = "sa_attn"; r.kind = mp::K_ATTN; r.a = a; r.B = NB;
@@ -515,15 +508,6 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             dev->ops.push_back(r);
         }
         HIPCHK(mp::op_sa_attn(a, NB, s));
-        if (sa_mode == mp::SA_PARTIALS) {
-            if (record) {
-                mp::OpRec r{};
-                r.name = "sa_combine"; r.kind = mp::K_COMB; r.a = a; r.B = NB;
-                r.bytes = A * act * 12.0 * (dev->nch * 66 + 64);
-                dev->ops.push_back(r);
-            }
-            HIPCHK(mp::op_sa_combine(a, NB, s));
-        }
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.src = dev->sa_out; g.src_ld = 768;
@@ -865,7 +849,6 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
         mp::SmpCfg cfg{params->temperature, params->top_k, (unsigned long long)params->seed, params->stream_base};
         HIPCHK(hipMemcpyAsync(dev->smpcfg, &cfg, sizeof cfg, hipMemcpyHostToDevice, dev->stream));
         HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
     }
     if (int rc = run_preamble(dev)) return rc;
     HIPCHK(hipStreamSynchronize(dev->stream));
@@ -889,7 +872,6 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
     HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->sa_cnt, 0, NB * 12 * 4, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go
     HIPCHK(hipStreamSynchronize(dev->stream));
     return MP_OK;
@@ -1118,7 +1100,7 @@ double mp_hip_op_bytes(mp_dev *dev, int op) {
         // live cache length of slot 0 after the run: keys 0..pos
         int pos = 0;
         hipMemcpy(&pos, dev->pos, 4, hipMemcpyDeviceToHost);
-        return 4.0 * dev->NB * ((double)(pos + 1) * 768 * 2 + 768 + 12.0 * dev->nch * 80);
+        return 4.0 * dev->NB * ((double)(pos + 1) * 768 * 2 + 768 * 2);  // K, V rows + q in + out
     }
     return r.bytes;
 }
@@ -1128,12 +1110,10 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     HIPCHK(hipSetDevice(dev->device));
     mp::OpRec r = dev->ops[op];
     r.g.ndone = nullptr;
-    r.a.ndone = nullptr;
     r.g.trace = nullptr;
     auto launch = [&]() -> hipError_t {
         if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
         if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
-        if (r.kind == mp::K_COMB) return mp::op_sa_combine(r.a, r.B, dev->stream);
         if (r.kind == mp::K_XA) {
             mp::XaP xp = r.x;
             xp.x_out = dev->q;  // scratch: timing must not disturb the residual stream

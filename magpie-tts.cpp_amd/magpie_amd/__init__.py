@@ -23,7 +23,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmagpie_hip.so")
+LIB_PATH = os.environ.get("MAGPIE_LIB") or os.path.join(PKG_DIR, "lib", "libmagpie_hip.so")  # MAGPIE_LIB: A/B builds
 SYNTH_BIN = os.path.join(PKG_DIR, "bin", "mp_synth_gguf")
 
 MP_OK = 0

@@ -66,15 +66,48 @@ def _decode_fps(dev, B, frames, steps=2):
 def measure_extra(model_path: str, codec_path, args) -> dict:
     """Throughput of the BASELINE configs' other shapes on this one GPU (fixed-length
     greedy decode, same synthetic prompts): bf16 projections at batch 1, 8
-    (configs[3]'s per-GPU share of batch 64) and 16 (configs[2]); and the streaming
-    path (sentence streaming, 4-frame codec chunks): time to first audio and
-    real-time factor of one utterance."""
+    (configs[3]'s per-GPU share of batch 64) and 16 (configs[2]); Q8_0 weights at
+    batch 1 and 60 s of long-form streaming (configs[4]); and the streaming path
+    (sentence streaming, 4-frame codec chunks): time to first audio and real-time
+    factor of one utterance."""
     out = {}
     dev = ma.Device(model_path, weights="bf16")
     for B in (1, 8, 16):
         toks = [ma.synthetic_tokens(args.tokens, seed=1000 + b) for b in range(B)]
         dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=args.frames, ignore_eos=True)
         out[f"bf16_batch{B}_fps"] = round(_decode_fps(dev, B, args.frames), 1)
+    dev.close()
+    # configs[4]: Q8_0 GGUF (the reference converter's default patterns), 60 s of
+    # long-form audio streamed sentence by sentence with 4-frame codec chunks; the
+    # sentences run as one device batch (magpie_synthesize_streaming's sentence
+    # batching), fixed 216 frames each (EOS masked) -> 6 x 216 = 1296 frames = 60.2 s.
+    q8_path = os.path.join(os.path.dirname(model_path), "magpie_357m_q8.gguf")
+    ma.synth_gguf(q8_path, dtype="q8_0")
+    dev = ma.Device(q8_path, weights="q8")
+    tok1 = [ma.synthetic_tokens(args.tokens, seed=1000)]
+    dev.synthesize(tok1, speakers=[0], max_dec_steps=args.frames, ignore_eos=True)
+    out["q8_batch1_fps"] = round(_decode_fps(dev, 1, args.frames), 1)
+    if codec_path:
+        cdc = ma.Codec(codec_path)
+        sents = [ma.synthetic_tokens(40, seed=5000 + i) for i in range(6)]
+        dev.synthesize_stream(cdc, sents[:1], lambda u, a: True, max_dec_steps=8, ignore_eos=True)  # warm-up
+        n = [0]
+        first = [None]
+        t0 = time.perf_counter()
+
+        def on_audio_q8(u, a):
+            if first[0] is None:
+                first[0] = time.perf_counter() - t0
+            n[0] += len(a)
+            return True
+        codes, total, tm = dev.synthesize_stream(cdc, sents, on_audio_q8, max_dec_steps=216, ignore_eos=True)
+        wall = time.perf_counter() - t0
+        audio_s = total / 22050.0
+        out["q8_longform_60s"] = {"sentences": len(sents), "frames": int(sum(len(c) for c in codes)),
+                                  "audio_s": round(audio_s, 1), "wall_s": round(wall, 3),
+                                  "rtf": round(audio_s / wall, 1), "first_audio_ms": round(first[0] * 1e3, 2),
+                                  "chunk_frames": 4}
+        cdc.close()
     dev.close()
     if codec_path:
         dev = ma.Device(model_path)

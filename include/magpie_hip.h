@@ -78,6 +78,15 @@ int mp_hip_load_model(mp_dev *dev, const char *gguf_path);
  * reference converter writes F32/F16/Q8_0/Q4_0, convert_magpie_to_gguf.py:197-206). */
 #define MP_WEIGHTS_AS_STORED 0
 #define MP_WEIGHTS_BF16 1
+/* Q8: the GGUF's Q8_0 tensors (the reference converter's Q8 file quantises the
+ * attention, cross-attention and LT projections, convert_magpie_to_gguf.py:155-176)
+ * stay int8 in HBM and are multiplied the way ggml multiplies Q8_0:
+ * every activation row is quantised to Q8_0 (quantize_row_q8_0_ref) and each
+ * 32-block contributes its exact integer dot times d_w*d_a — in the encoder, the
+ * XA K/V precompute, the prefill, every decode step and the LT. F32 tensors (the
+ * pos_ff convs) keep the f32 path. Batches up to 8. MP_ERR_UNSUPPORTED for a file
+ * without Q8_0 tensors (BASELINE config 5). */
+#define MP_WEIGHTS_Q8 2
 int mp_hip_load_model_ex(mp_dev *dev, const char *gguf_path, int weight_mode);
 int mp_hip_weight_mode(mp_dev *dev);
 int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes);

@@ -26,10 +26,19 @@ magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_
         delete ctx;
         return nullptr;
     }
-    // MAGPIE_WEIGHTS=bf16 selects the bf16 decode projections (magpie_hip.h weight modes)
+    // Weight mode (magpie_hip.h): a GGUF with Q8_0 tensors runs them as ggml does
+    // (MP_WEIGHTS_Q8), any other file as stored; MAGPIE_WEIGHTS=f32|bf16|q8 overrides.
     const char *wm = getenv("MAGPIE_WEIGHTS");
-    const int mode = wm && !strcmp(wm, "bf16") ? MP_WEIGHTS_BF16 : MP_WEIGHTS_AS_STORED;
-    if (mp_hip_load_model_ex(ctx->model.dev, model_path, mode) != MP_OK) {
+    int mode = MP_WEIGHTS_Q8;
+    bool forced = false;
+    if (wm && *wm) {
+        forced = true;
+        mode = !strcmp(wm, "bf16") ? MP_WEIGHTS_BF16 : !strcmp(wm, "q8") ? MP_WEIGHTS_Q8 : MP_WEIGHTS_AS_STORED;
+    }
+    int rc = mp_hip_load_model_ex(ctx->model.dev, model_path, mode);
+    if (rc == MP_ERR_UNSUPPORTED && !forced)  // no Q8_0 tensors in the file: as stored
+        rc = mp_hip_load_model_ex(ctx->model.dev, model_path, MP_WEIGHTS_AS_STORED);
+    if (rc != MP_OK) {
         fprintf(stderr, "magpie: failed to load '%s': %s\n", model_path, mp_hip_error(ctx->model.dev));
         mp_hip_free(ctx->model.dev);
         delete ctx;

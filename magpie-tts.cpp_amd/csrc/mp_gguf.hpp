@@ -151,6 +151,8 @@ public:
         return false;
     }
     const std::map<std::string, GgufTensor> &tensors() const { return tensors_; }
+    // the tensor's bytes as stored in the file (e.g. Q8_0 blocks)
+    const uint8_t *data(const GgufTensor &t) const { return map_ + data_off_ + t.offset; }
 
 private:
     template <class T> T rd() {

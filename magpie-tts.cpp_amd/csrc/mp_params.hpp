@@ -76,6 +76,8 @@ __host__ __device__ inline float mp_uniform(unsigned long long seed, int stream,
 struct GemvP {
     const float *W;
     const unsigned short *Wb;  // bf16 weights in MFMA fragment order (mp_decode_b16.hip), or null
+    const signed char *Wq;     // Q8_0 weights as stored: int8 [N][K] (mp_decode_q8.hip), or null
+    const unsigned short *Wd;  //   and their fp16 block scales [N][K/32]
     int N;
     const float *bias;
     // prologue inputs

@@ -8,6 +8,7 @@
 // tiny neighbouring ops fused into its operand loader (causal k=3 conv taps) or
 // its epilogue (residual, GELU, KV-cache scatter, XA K/V split).
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 #include <math.h>
 
 #include "mp_device.hpp"
@@ -15,6 +16,38 @@
 #include "mp_prefill_api.hpp"
 
 namespace mp {
+
+// Epilogue of a 4x4 register tile at rows m0.., columns n0.. (bias, residual,
+// GELU, KV-cache scatter, XA K/V split).
+template <int EPI>
+__device__ __forceinline__ void gemm_store(const GemmP &p, const float (&acc)[4][4], int m0, int n0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + i;
+        if (m >= p.M) continue;
+        const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + j;
+            if (n >= p.N) continue;
+            float v = acc[i][j];
+            if (p.bias) v += p.bias[n];
+            if constexpr (EPI == GE_STORE) p.C[(size_t)m * p.ldc + n] = v;
+            else if constexpr (EPI == GE_RESID) p.C[(size_t)m * p.ldc + n] = v + p.C[(size_t)m * p.ldc + n];
+            else if constexpr (EPI == GE_GELU) p.C[(size_t)m * p.ldc + n] = gelu_tanh(v);
+            else if constexpr (EPI == GE_QKV_CACHE) {
+                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + t) * D;
+                if (n < D) p.C[(size_t)m * p.ldc + n] = v;
+                else if (n < 2 * D) p.kc[slot + n - D] = v;
+                else p.vc[slot + n - 2 * D] = v;
+            } else if constexpr (EPI == GE_XAKV) {
+                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.Tmax + t) * DXA;
+                if (n < DXA) p.xak[slot + n] = v;
+                else p.xav[slot + n - DXA] = v;
+            }
+        }
+    }
+}
 
 template <int EPI, int TAPS>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
@@ -68,32 +101,84 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
         }
         __syncthreads();
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int m = m0 + ty * 4 + i;
-        if (m >= p.M) continue;
-        const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + tx * 4 + j;
-            if (n >= p.N) continue;
-            float v = acc[i][j];
-            if (p.bias) v += p.bias[n];
-            if constexpr (EPI == GE_STORE) p.C[(size_t)m * p.ldc + n] = v;
-            else if constexpr (EPI == GE_RESID) p.C[(size_t)m * p.ldc + n] = v + p.C[(size_t)m * p.ldc + n];
-            else if constexpr (EPI == GE_GELU) p.C[(size_t)m * p.ldc + n] = gelu_tanh(v);
-            else if constexpr (EPI == GE_QKV_CACHE) {
-                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + t) * D;
-                if (n < D) p.C[(size_t)m * p.ldc + n] = v;
-                else if (n < 2 * D) p.kc[slot + n - D] = v;
-                else p.vc[slot + n - 2 * D] = v;
-            } else if constexpr (EPI == GE_XAKV) {
-                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.Tmax + t) * DXA;
-                if (n < DXA) p.xak[slot + n] = v;
-                else p.xav[slot + n - DXA] = v;
+    gemm_store<EPI>(p, acc, m0 + ty * 4, n0 + tx * 4);
+}
+
+// Q8_0 weights (weight mode MP_WEIGHTS_Q8): ggml's quantised mul_mat. Every K
+// step is one 32-wide Q8_0 block; the A tile is quantised as it is loaded
+// (quantize_row_q8_0_ref: d = amax/127, id = 1/d, q = roundf(x*id), d kept as
+// fp16; the four loader lanes of a row share amax through DPP), the block dot
+// products are exact int32 (v_dot4c_i32_i8) and are scaled by d_w * d_a
+// (ggml_vec_dot_q8_0_q8_0).
+__device__ __forceinline__ int pack_i8x4(float a, float b, float c, float d) {
+    return (int)(((unsigned)(int)a & 0xffu) | (((unsigned)(int)b & 0xffu) << 8) | (((unsigned)(int)c & 0xffu) << 16) |
+                 ((unsigned)(int)d << 24));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_q8_kernel(GemmP p) {
+    constexpr int BM = 64, BN = 64;
+    __shared__ int Aq[BM][9];
+    __shared__ int Wq[BN][9];
+    __shared__ float Ad[BM], Wd[BN];
+    const int tid = threadIdx.x;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int tx = tid & 15, ty = tid >> 4;
+    const int lr = tid >> 2, part = tid & 3;  // loader: row lr, elements 8 part .. 8 part + 7 of the block
+    const int nblk = p.K / 32;
+    float acc[4][4] = {};
+    for (int kb = 0; kb < nblk; ++kb) {
+        const int k0 = kb * 32 + part * 8;
+        {   // A rows -> Q8_0
+            float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            const int m = m0 + lr;
+            if (m < p.M) {
+                const float4 v0 = *(const float4 *)(p.A + (size_t)m * p.lda + k0);
+                const float4 v1 = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + 4);
+                a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w; a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
             }
+            float amax = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(a[e]));
+            amax = fmaxf(amax, dpp_mov<0xB1>(amax));
+            amax = fmaxf(amax, dpp_mov<0x4E>(amax));
+            const float dd = amax / 127.0f;
+            const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+            Aq[lr][2 * part] = pack_i8x4(roundf(a[0] * id), roundf(a[1] * id), roundf(a[2] * id), roundf(a[3] * id));
+            Aq[lr][2 * part + 1] = pack_i8x4(roundf(a[4] * id), roundf(a[5] * id), roundf(a[6] * id), roundf(a[7] * id));
+            if (part == 0) Ad[lr] = __half2float(__float2half(dd));
         }
+        {   // W rows: int8 + block scale
+            const int n = n0 + lr;
+            uint2 wv = make_uint2(0u, 0u);
+            float wd = 0.f;
+            if (n < p.N) {
+                wv = *(const uint2 *)(p.Wq + (size_t)n * p.K + k0);
+                wd = __half2float(__ushort_as_half(p.Wd[(size_t)n * nblk + kb]));
+            }
+            Wq[lr][2 * part] = (int)wv.x;
+            Wq[lr][2 * part + 1] = (int)wv.y;
+            if (part == 0) Wd[lr] = wd;
+        }
+        __syncthreads();
+        int s[4][4] = {};
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            int av[4], wv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { av[i] = Aq[ty * 4 + i][w]; wv[i] = Wq[tx * 4 + i][w]; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s[i][j] = __builtin_amdgcn_sdot4(av[i], wv[j], s[i][j], false);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] += (float)s[i][j] * (Wd[tx * 4 + j] * Ad[ty * 4 + i]);
+        __syncthreads();
     }
+    gemm_store<EPI>(p, acc, m0 + ty * 4, n0 + tx * 4);
 }
 
 // Y[m] = LN(X[m]) * w for rows of width 768 (ggml_norm + ggml_mul).
@@ -205,7 +290,23 @@ static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, p);
     return hipGetLastError();
 }
+template <int EPI>
+static hipError_t launch_gemm_q8(const GemmP &p, hipStream_t s) {
+    if (!p.Wd || p.K % 32 || p.conv_taps) return hipErrorInvalidValue;
+    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64);
+    hipLaunchKernelGGL((gemm_q8_kernel<EPI>), grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
 hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s) {
+    if (p.Wq) {
+        switch (epi) {
+        case GE_STORE: return launch_gemm_q8<GE_STORE>(p, s);
+        case GE_RESID: return launch_gemm_q8<GE_RESID>(p, s);
+        case GE_QKV_CACHE: return launch_gemm_q8<GE_QKV_CACHE>(p, s);
+        case GE_XAKV: return launch_gemm_q8<GE_XAKV>(p, s);
+        }
+        return hipErrorInvalidValue;
+    }
     if (p.conv_taps == 3) {
         if (epi == GE_GELU) return launch_gemm<GE_GELU, 3>(p, s);
         if (epi == GE_RESID) return launch_gemm<GE_RESID, 3>(p, s);

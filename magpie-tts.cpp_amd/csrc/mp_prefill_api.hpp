@@ -18,6 +18,8 @@ struct GemmP {
     const float *A;  // [M][lda]
     int lda;
     const float *W;  // [N][K]
+    const signed char *Wq;     // Q8_0 weight mode: int8 [N][K] + fp16 block scales [N][K/32]
+    const unsigned short *Wd;  //   (ggml's quantised mul_mat, gemm_q8_kernel); null: f32 W
     const float *bias;
     float *C;
     int ldc;

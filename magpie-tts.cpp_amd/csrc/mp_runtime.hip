@@ -54,6 +54,17 @@ MP_DECL_B16(4)
 MP_DECL_B16(8)
 MP_DECL_B16(16)
 hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t);
+#define MP_DECL_Q8(NB)                                                                                       \
+    hipError_t q8_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t q8_qkv_##NB(const GemvP &, hipStream_t);        \
+    hipError_t q8_oproj_##NB(const GemvP &, hipStream_t); hipError_t q8_xq_##NB(const GemvP &, hipStream_t);             \
+    hipError_t q8_xo_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_in0_##NB(const GemvP &, hipStream_t);           \
+    hipError_t q8_lt_a_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_ag_##NB(const GemvP &, hipStream_t);           \
+    hipError_t q8_lt_b_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_e_##NB(const GemvP &, hipStream_t);
+MP_DECL_Q8(1)
+MP_DECL_Q8(2)
+MP_DECL_Q8(4)
+MP_DECL_Q8(8)
+hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
@@ -74,11 +85,27 @@ static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TAB
                            b16_lt_d_##NB, b16_lt_e_##NB }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
+// Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
+struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, xo, lt_in0, lt_a, lt_ag, lt_b, lt_e; };
+#define MP_TABLE_Q8(NB) { q8_qkv_embed_##NB, q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_xo_##NB, q8_lt_in0_##NB, \
+                          q8_lt_a_##NB, q8_lt_ag_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
+static const OpTableQ8 kTablesQ8[4] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8)};
 static int nb_index(int NB) { return NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : NB == 8 ? 3 : 4; }
 static const OpTable &table_for(int NB, bool b16) { return b16 ? kTablesB16[nb_index(NB)] : kTables[nb_index(NB)]; }
+static const OpTableQ8 &table_q8(int NB) { return kTablesQ8[nb_index(NB) < 4 ? nb_index(NB) : 3]; }
 
-struct EncLayerW { const float *norm_self, *qkv, *o, *norm_ff, *ff1, *ff2; };
-struct DecLayerW { const float *norm_self, *qkv, *o, *norm_xq, *xq, *xkv, *xo, *norm_xmem, *norm_ff, *ff1, *ff2; };
+// A Q8_0 tensor as stored (weight mode MP_WEIGHTS_Q8): int8 [N][K] + fp16 scales [N][K/32]
+struct QW {
+    const signed char *q = nullptr;
+    const unsigned short *d = nullptr;
+    explicit operator bool() const { return q != nullptr; }
+};
+
+struct EncLayerW { const float *norm_self, *qkv, *o, *norm_ff, *ff1, *ff2; QW qkv8, o8; };
+struct DecLayerW {
+    const float *norm_self, *qkv, *o, *norm_xq, *xq, *xkv, *xo, *norm_xmem, *norm_ff, *ff1, *ff2;
+    QW qkv8, o8, xq8, xkv8, xo8;
+};
 
 struct Model {
     int enc_layers = 6, dec_layers = 12, n_spk = 5, dec_pos_rows = 0, text_vocab = 2380;
@@ -98,11 +125,15 @@ struct Model {
     std::vector<const unsigned short *> pk_qkv, pk_o, pk_ff1, pk_ff2;
     const unsigned short *pk_lt_qkv = nullptr, *pk_lt_o = nullptr, *pk_lt_ff1 = nullptr, *pk_lt_ff2 = nullptr,
                          *pk_lt_out = nullptr;  // lt_out: [8][127 tiles][8][64][8]
+    // weight mode MP_WEIGHTS_Q8: the file's Q8_0 tensors as stored (ggml's quantised mul_mat)
+    void *q8_arena = nullptr;
+    size_t q8_bytes = 0;
+    QW lt_in8, lt_qkv8, lt_o8, lt_out8;  // lt_out8: [8][2024][256] (+ [8][2024][8] scales)
     float *arena = nullptr;
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_ROWXA = 4 };
 struct OpRec {
     std::string name;
     int kind;
@@ -111,6 +142,7 @@ struct OpRec {
     AttnP a;
     FinP f;
     XaP x;
+    RowXaP rx;
     int B;
     double bytes;
 };
@@ -141,6 +173,7 @@ struct mp_dev {
     std::vector<void *> allocs;
     float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *sa_out = nullptr,
           *h = nullptr, *hidden = nullptr;
+    float *xqb = nullptr, *xab = nullptr;  // Q8 mode (unfused XA): q_net output, attention output [NB][128]
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
@@ -276,7 +309,7 @@ int load_model(mp_dev *dev, const char *path) {
     const int64_t D = 768;
     need("text_embedding.weight", (int64_t)m.text_vocab * D, &m.text_emb);
     need("encoder.position_embeddings.weight", -1, &m.enc_pos);
-    m.enc.resize(m.enc_layers);
+    m.enc.assign(m.enc_layers, mp::EncLayerW{});
     for (int l = 0; l < m.enc_layers; ++l) {
         const std::string p = "encoder.layers." + std::to_string(l) + ".";
         mp::EncLayerW &L = m.enc[l];
@@ -289,7 +322,7 @@ int load_model(mp_dev *dev, const char *path) {
     }
     need("encoder.norm_out.weight", D, &m.enc_norm_out);
     need("decoder.position_embeddings.weight", -1, &m.dec_pos);
-    m.dec.resize(m.dec_layers);
+    m.dec.assign(m.dec_layers, mp::DecLayerW{});
     for (int l = 0; l < m.dec_layers; ++l) {
         const std::string p = "decoder.layers." + std::to_string(l) + ".";
         mp::DecLayerW &L = m.dec[l];
@@ -401,18 +434,111 @@ int load_model(mp_dev *dev, const char *path) {
             HIPCHK(hipMemcpy(m.xq_t[l], wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
         }
     }
-    // P[c][v] = in_proj(audio_emb[c][v]) + b: the LT's per-codebook re-embedding
-    // (magpie.cpp:1274-1313) depends only on (c, v) -> one GEMM at load time.
+    dev->loaded = true;
+    return MP_OK;
+}
+
+// P[c][v] = in_proj(audio_emb[c][v]) + b: the LT's per-codebook re-embedding
+// (magpie.cpp:1274-1313) depends only on (c, v) -> one GEMM at load time (with
+// ggml's Q8_0 arithmetic when in_proj is a Q8_0 tensor in Q8 mode).
+int build_ptab(mp_dev *dev) {
+    mp::Model &m = dev->m;
     if (m.lt_ptab) { hipFree(m.lt_ptab); m.lt_ptab = nullptr; }
     HIPCHK(hipMalloc(&m.lt_ptab, (size_t)8 * 2024 * 256 * 4));
-    {
-        mp::GemmP gp{};
-        gp.A = m.audio_emb; gp.lda = 768; gp.W = m.lt_in_w; gp.bias = m.lt_in_b; gp.C = m.lt_ptab; gp.ldc = 256;
-        gp.M = 8 * 2024; gp.N = 256; gp.K = 768; gp.rows_per_utt = 8 * 2024;
-        HIPCHK(mp::pre_gemm(gp, mp::GE_STORE, dev->stream));
-        HIPCHK(hipStreamSynchronize(dev->stream));
+    mp::GemmP gp{};
+    gp.A = m.audio_emb; gp.lda = 768; gp.W = m.lt_in_w; gp.Wq = m.lt_in8.q; gp.Wd = m.lt_in8.d; gp.bias = m.lt_in_b;
+    gp.C = m.lt_ptab; gp.ldc = 256; gp.M = 8 * 2024; gp.N = 256; gp.K = 768; gp.rows_per_utt = 8 * 2024;
+    HIPCHK(mp::pre_gemm(gp, mp::GE_STORE, dev->stream));
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    return MP_OK;
+}
+
+// Weight mode MP_WEIGHTS_Q8: upload every Q8_0 tensor the decode path uses as
+// stored (scripts/convert_magpie_to_gguf.py:155-176 decides which: attention,
+// cross-attention and LT projections), repacked to int8 [N][K] + fp16 scales
+// [N][K/32] (34 B per 32 weights, as in the file). F32 tensors keep the f32 path.
+int load_q8(mp_dev *dev, const char *path) {
+    mp::Gguf g;
+    std::string err;
+    if (!g.open(path, err)) return fail(dev, MP_ERR_IO, err);
+    mp::Model &m = dev->m;
+    struct Item { const mp::GgufTensor *t; mp::QW *dst; int group; };
+    std::vector<Item> items;
+    auto want = [&](const std::string &name, mp::QW *dst) {
+        const mp::GgufTensor *t = g.find(name);
+        if (t && t->type == 8 && t->ne[0] % 32 == 0) items.push_back({t, dst, -1});
+    };
+    for (int l = 0; l < m.enc_layers; ++l) {
+        const std::string p = "encoder.layers." + std::to_string(l) + ".self_attention.";
+        want(p + "qkv_net.weight", &m.enc[l].qkv8);
+        want(p + "o_net.weight", &m.enc[l].o8);
     }
-    dev->loaded = true;
+    for (int l = 0; l < m.dec_layers; ++l) {
+        const std::string p = "decoder.layers." + std::to_string(l) + ".";
+        want(p + "self_attention.qkv_net.weight", &m.dec[l].qkv8);
+        want(p + "self_attention.o_net.weight", &m.dec[l].o8);
+        want(p + "cross_attention.q_net.weight", &m.dec[l].xq8);
+        want(p + "cross_attention.kv_net.weight", &m.dec[l].xkv8);
+        want(p + "cross_attention.o_net.weight", &m.dec[l].xo8);
+    }
+    want("local_transformer_in_projection.weight", &m.lt_in8);
+    want("local_transformer.layers.0.self_attention.qkv_net.weight", &m.lt_qkv8);
+    want("local_transformer.layers.0.self_attention.o_net.weight", &m.lt_o8);
+    int nout = 0;
+    for (int c = 0; c < 8; ++c) {
+        const mp::GgufTensor *t = g.find("local_transformer_out_projections." + std::to_string(c) + ".weight");
+        if (t && t->type == 8) { items.push_back({t, &m.lt_out8, c}); ++nout; }
+    }
+    if (nout != 0 && nout != 8) return fail(dev, MP_ERR_UNSUPPORTED, "mixed Q8_0/F32 LT output projections");
+    if (items.empty()) return fail(dev, MP_ERR_UNSUPPORTED, "Q8 weight mode needs a GGUF with Q8_0 tensors");
+    // the reassociated XA (K' = K W_q, V' = W_o V) is an f32 identity: with Q8_0
+    // q_net / o_net the activations must be quantised where ggml quantises them
+    for (int l = 0; l < m.dec_layers; ++l)
+        if ((bool)m.dec[l].xq8 != (bool)m.dec[l].xo8)
+            return fail(dev, MP_ERR_UNSUPPORTED, "cross-attention q_net / o_net must both be Q8_0 or both F32");
+    auto align_up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    size_t total = 0;
+    for (auto &it : items) {
+        const size_t n = (size_t)it.t->nelements();
+        total += align_up(n) + align_up(n / 32 * 2);
+    }
+    if (m.q8_arena) { hipFree(m.q8_arena); m.q8_arena = nullptr; }
+    HIPCHK(hipMalloc(&m.q8_arena, total));
+    m.q8_bytes = total;
+    char *cur = (char *)m.q8_arena;
+    std::vector<signed char> hq;
+    std::vector<unsigned short> hd;
+    signed char *out_q = nullptr;
+    unsigned short *out_d = nullptr;
+    const size_t out_n = (size_t)2024 * 256;
+    for (auto &it : items) {
+        const size_t n = (size_t)it.t->nelements();
+        const uint8_t *src = g.data(*it.t);
+        hq.resize(n);
+        hd.resize(n / 32);
+        for (size_t b = 0; b < n / 32; ++b) {
+            memcpy(&hd[b], src + b * 34, 2);
+            memcpy(&hq[b * 32], src + b * 34 + 2, 32);
+        }
+        signed char *dq;
+        unsigned short *dd;
+        if (it.group < 0) {
+            dq = (signed char *)cur; cur += align_up(n);
+            dd = (unsigned short *)cur; cur += align_up(n / 32 * 2);
+            it.dst->q = dq; it.dst->d = dd;
+        } else {  // the 8 LT heads as one [8][2024][256] array (indexed by a device codebook)
+            if (n != out_n) return fail(dev, MP_ERR_FORMAT, "unexpected LT output projection shape");
+            if (!out_q) {
+                out_q = (signed char *)cur; cur += align_up(8 * n);
+                out_d = (unsigned short *)cur; cur += align_up(8 * (n / 32) * 2);
+            }
+            dq = out_q + (size_t)it.group * n;
+            dd = out_d + (size_t)it.group * (n / 32);
+            it.dst->q = out_q; it.dst->d = out_d;
+        }
+        HIPCHK(hipMemcpy(dq, hq.data(), n, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dd, hd.data(), n / 32 * 2, hipMemcpyHostToDevice));
+    }
     return MP_OK;
 }
 
@@ -433,7 +559,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
     A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(sa_out, NB * 768);
-    A(h, NB * 3072); A(hidden, NB * D);
+    A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(xab, NB * 128);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
@@ -476,8 +602,9 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     const int NB = dev->NB, L = m.dec_layers;
     const bool b16 = m.weight_mode == MP_WEIGHTS_BF16;
     const mp::OpTable &tb = mp::table_for(NB, b16);
-    // algorithmic bytes: weights at their stored width, activations f32
-    const double F = b16 ? 2.0 : 4.0, A = 4.0, act = (double)NB;
+    const mp::OpTableQ8 &tq = mp::table_q8(NB);
+    // algorithmic bytes: weights at their stored width (Q8_0: 34 B per 32), activations f32
+    const double F = b16 ? 2.0 : 4.0, Fq = 34.0 / 32.0, A = 4.0, act = (double)NB;
     if (record) dev->ops.clear();
     auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
         if (record) {
@@ -495,10 +622,14 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.layer = l;
         // LN + QKV (+ frame embedding on layer 0) + KV append   (3415-3442)
         g.W = W.qkv; g.Wb = b16 ? m.pk_qkv[l] : nullptr; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
+        g.Wq = W.qkv8.q; g.Wd = W.qkv8.d;
         g.kc = dev->kc; g.vc = dev->vc;
         if (l == 0) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
-        if ((rc = run(l == 0 ? "qkv_embed" : "qkv", l == 0 ? tb.qkv_embed : tb.qkv, g,
-                      F * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
+        {
+            const mp::GemvFn fn = W.qkv8 ? (l == 0 ? tq.qkv_embed : tq.qkv) : (l == 0 ? tb.qkv_embed : tb.qkv);
+            if ((rc = run(l == 0 ? "qkv_embed" : "qkv", fn, g,
+                          (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
+        }
         // self-attention over the cache, one workgroup per (head, slot) (3457-3476)
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->sa_out};
         if (record) {
@@ -511,16 +642,40 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.src = dev->sa_out; g.src_ld = 768;
-        if ((rc = run("oproj", tb.oproj, g, F * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) return rc;
-        // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
-        mp::XaP xp{dev->x, dev->x2, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
-        if (record) {
-            mp::OpRec r{};
-            r.name = "xa"; r.kind = mp::K_XA; r.x = xp; r.B = NB;
-            r.bytes = A * act * (768.0 * 2 + 2.0 * 768 * dev->Tmax);
-            dev->ops.push_back(r);
+        g.Wq = W.o8.q; g.Wd = W.o8.d;
+        if ((rc = run("oproj", W.o8 ? tq.oproj : tb.oproj, g, (W.o8 ? Fq : F) * (768.0 * 768) + A * act * (768 * 3))) !=
+            MP_OK)
+            return rc;
+        if (W.xq8) {
+            // cross-attention with Q8_0 q_net / o_net, as ggml computes it (1713-1767):
+            // q = Q8(q_net) LN(x); a = attn(q, K, V); x2 = x + Q8(o_net) a
+            g = gemv_base(dev); g.layer = l;
+            g.W = W.xq; g.Wq = W.xq8.q; g.Wd = W.xq8.d; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
+            g.out = dev->xqb; g.out_ld = 128;
+            if ((rc = run("xq", tq.xq, g, Fq * (128.0 * 768) + A * act * (768 + 128))) != MP_OK) return rc;
+            mp::RowXaP rx{dev->xqb, dev->xak, dev->xav, l, L, dev->Tmax, 1, NB, dev->T, dev->xab};
+            if (record) {
+                mp::OpRec r{};
+                r.name = "xattn"; r.kind = mp::K_ROWXA; r.rx = rx; r.B = NB;
+                r.bytes = A * act * (128.0 * 2 + 2.0 * 128 * dev->Tmax);
+                dev->ops.push_back(r);
+            }
+            HIPCHK(mp::pre_row_xa(rx, s));
+            g = gemv_base(dev); g.layer = l;
+            g.W = W.xo; g.Wq = W.xo8.q; g.Wd = W.xo8.d; g.N = 768; g.src = dev->xab; g.src_ld = 128;
+            g.out = dev->x2; g.out_ld = 768; g.addsrc = dev->x;
+            if ((rc = run("xo", tq.xo, g, Fq * (768.0 * 128) + A * act * (128 + 2 * 768))) != MP_OK) return rc;
+        } else {
+            // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
+            mp::XaP xp{dev->x, dev->x2, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
+            if (record) {
+                mp::OpRec r{};
+                r.name = "xa"; r.kind = mp::K_XA; r.x = xp; r.B = NB;
+                r.bytes = A * act * (768.0 * 2 + 2.0 * 768 * dev->Tmax);
+                dev->ops.push_back(r);
+            }
+            HIPCHK(mp::op_xa(xp, NB, s));
         }
-        HIPCHK(mp::op_xa(xp, NB, s));
         // LN + FFN up + GELU (1796-1799)
         g = gemv_base(dev); g.layer = l;
         g.W = W.ff1; g.Wb = b16 ? m.pk_ff1[l] : nullptr; g.N = 3072; g.lnw = W.norm_ff; g.src = dev->x2; g.src_ld = 768; g.out = dev->h; g.out_ld = 3072;
@@ -549,7 +704,8 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     const mp::Model &m = dev->m;
     const bool b16 = m.weight_mode == MP_WEIGHTS_BF16;
     const mp::OpTable &tb = mp::table_for(NB, b16);
-    const double F = b16 ? 2.0 : 4.0, A = 4.0, act = (double)NB;
+    const mp::OpTableQ8 &tq = mp::table_q8(NB);
+    const double F = b16 ? 2.0 : 4.0, Fq = 34.0 / 32.0, A = 4.0, act = (double)NB;
     auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
         if (ops) {
             mp::OpRec r{};
@@ -575,15 +731,20 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     {
         mp::GemvP g = base();
         g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.out = io.lt_s; g.out_ld = 9 * 256;
+        g.Wq = m.lt_in8.q; g.Wd = m.lt_in8.d;
+        const double Fi = m.lt_in8 ? Fq : A;
         if (io.lt_only) {
             // in_proj of the caller's (already normalised) hidden (1161-1163)
             g.src = io.hidden; g.src_ld = 768;
-            if ((rc = run("lt_inh", mp::op_lt_inh_1, g, A * (256.0 * 768 + 256) + A * (768 + 256))) != MP_OK) return rc;
+            if ((rc = run("lt_inh", m.lt_in8 ? mp::q8_lt_inh_1 : mp::op_lt_inh_1, g,
+                          Fi * 256.0 * 768 + A * 256 + A * (768 + 256))) != MP_OK)
+                return rc;
         } else {
             // final LN -> hidden (4394) fused into LT in_proj (1162-1163)
             g.lnw = m.dec_norm_out; g.src = io.x; g.src_ld = 768; g.hidden_out = io.hidden;
             if (io.trace) { g.trace = io.trace; g.trace_steps = io.trace_steps; g.step = io.step; }
-            if ((rc = run("lt_in0", tb.lt_in0, g, A * (256.0 * 768 + 256) + A * act * ((768 + 768 + 256)))) != MP_OK)
+            if ((rc = run("lt_in0", m.lt_in8 ? tq.lt_in0 : tb.lt_in0, g,
+                          Fi * 256.0 * 768 + A * 256 + A * act * ((768 + 768 + 256)))) != MP_OK)
                 return rc;
         }
     }
@@ -592,14 +753,23 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         mp::GemvP g = base();
         g.cb = cb;
         g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX;
+        g.Wq = m.lt_qkv8.q; g.Wd = m.lt_qkv8.d;
         g.lnw = m.lt_norm_self; g.lq = io.ltq; g.lk = io.ltk; g.lv = io.ltv;
         if (cb > 0) { g.logits = io.logits; g.codes_cur = io.codes_cur; g.ptab = m.lt_ptab; }
-        if ((rc = run(cb == 0 ? "lt_a" : "lt_ag", cb == 0 ? tb.lt_a : tb.lt_ag, g,
-                      F * (768.0 * 256) + A * act * ((256 * 3 + 768 + (cb > 0 ? 2024 + 256 : 256))))) != MP_OK) return rc;
+        {
+            const mp::GemvFn fn = m.lt_qkv8 ? (cb == 0 ? tq.lt_a : tq.lt_ag) : (cb == 0 ? tb.lt_a : tb.lt_ag);
+            if ((rc = run(cb == 0 ? "lt_a" : "lt_ag", fn, g,
+                          (m.lt_qkv8 ? Fq : F) * (768.0 * 256) + A * act * ((256 * 3 + 768 + (cb > 0 ? 2024 + 256 : 256))))) !=
+                MP_OK)
+                return rc;
+        }
         g = base(); g.cb = cb;
         g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = io.ltq; g.ltk = io.ltk; g.ltv = io.ltv; g.out = io.ltY;
+        g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
         g.out_ld = 256; g.addsrc = io.ltX;
-        if ((rc = run("lt_b", tb.lt_b, g, F * (256.0 * 256) + A * act * ((256 * (2 * cb + 5))))) != MP_OK) return rc;
+        if ((rc = run("lt_b", m.lt_o8 ? tq.lt_b : tb.lt_b, g,
+                      (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * ((256 * (2 * cb + 5))))) != MP_OK)
+            return rc;
         g = base(); g.cb = cb;
         g.W = m.lt_ff1; g.Wb = m.pk_lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = io.ltY; g.src_ld = 256;
         g.out = io.ltf; g.out_ld = 1024;
@@ -612,7 +782,13 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024;
         g.Wb = b16 ? m.pk_lt_out + (size_t)cb * pk_elems(2024, 256) : nullptr; g.bias = m.lt_out_b + (size_t)cb * 2024;
         g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
-        if ((rc = run("lt_e", tb.lt_e, g, F * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK) return rc;
+        if (m.lt_out8) {
+            g.Wq = m.lt_out8.q + (size_t)cb * 2024 * 256;
+            g.Wd = m.lt_out8.d + (size_t)cb * 2024 * 8;
+        }
+        if ((rc = run("lt_e", m.lt_out8 ? tq.lt_e : tb.lt_e, g,
+                      (m.lt_out8 ? Fq : F) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
+            return rc;
     }
     mp::FinP f{io.logits, io.codes_cur, io.codes_prev, io.codes_out, io.step, io.pos, io.done, io.nframes, io.ndone,
                io.max_steps, io.ignore_eos, m.audio_bos, m.audio_eos, NB,
@@ -639,7 +815,7 @@ int run_preamble(mp_dev *dev) {
         const EncLayerW &W = m.enc[l];
         HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_self, dev->pH, 768, Me, m.eps, s));
         GemmP gp{};
-        gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Me; gp.N = 2304; gp.K = 768;
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.Wq = W.qkv8.q; gp.Wd = W.qkv8.d; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Me; gp.N = 2304; gp.K = 768;
         gp.rows_per_utt = Tmax; gp.T = dev->T;
         HIPCHK(pre_gemm(gp, GE_STORE, s));
         RowAttnP ra{};
@@ -648,7 +824,7 @@ int run_preamble(mp_dev *dev) {
         ra.heads = 12; ra.T = dev->T;
         HIPCHK(pre_row_attn(ra, s));
         gp = GemmP{};
-        gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.C = dev->pX; gp.ldc = 768; gp.M = Me; gp.N = 768; gp.K = 768;
+        gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.Wq = W.o8.q; gp.Wd = W.o8.d; gp.C = dev->pX; gp.ldc = 768; gp.M = Me; gp.N = 768; gp.K = 768;
         gp.rows_per_utt = Tmax; gp.T = dev->T;
         HIPCHK(pre_gemm(gp, GE_RESID, s));
         HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_ff, dev->pH, 768, Me, m.eps, s));
@@ -666,13 +842,15 @@ int run_preamble(mp_dev *dev) {
     for (int l = 0; l < L; ++l) {
         HIPCHK(pre_ln_rows(dev->enc_out, 768, m.dec[l].norm_xmem, dev->pH, 768, Me, m.eps, s));
         GemmP gp{};
-        gp.A = dev->pH; gp.lda = 768; gp.W = m.dec[l].xkv; gp.M = Me; gp.N = 256; gp.K = 768; gp.rows_per_utt = Tmax;
+        gp.A = dev->pH; gp.lda = 768; gp.W = m.dec[l].xkv; gp.Wq = m.dec[l].xkv8.q; gp.Wd = m.dec[l].xkv8.d; gp.M = Me; gp.N = 256; gp.K = 768; gp.rows_per_utt = Tmax;
         gp.T = dev->T; gp.xak = dev->xak; gp.xav = dev->xav; gp.layer = l; gp.nlayers = L; gp.Tmax = Tmax;
         HIPCHK(pre_gemm(gp, GE_XAKV, s));
     }
-    // --- K'_t = W_q^T K_t, V'_t = W_o V_t per utterance and layer (decode-time fused XA)
+    // --- K'_t = W_q^T K_t, V'_t = W_o V_t per utterance and layer (decode-time fused XA;
+    //     not with Q8_0 q_net / o_net, whose activations ggml quantises: unfused XA there)
     for (int b = 0; b < NB; ++b)
         for (int l = 0; l < L; ++l) {
+            if (m.dec[l].xq8) continue;
             const size_t xo = ((size_t)(b * L + l) * Tmax) * 128, po = ((size_t)(b * L + l) * Tmax) * 768;
             GemmP gp{};
             gp.A = dev->xak + xo; gp.lda = 128; gp.W = m.xq_t[l]; gp.C = dev->kp + po; gp.ldc = 768;
@@ -688,7 +866,7 @@ int run_preamble(mp_dev *dev) {
         const DecLayerW &W = m.dec[l];
         HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_self, dev->pH, 768, Mc, m.eps, s));
         GemmP gp{};
-        gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Mc; gp.N = 2304; gp.K = 768;
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.Wq = W.qkv8.q; gp.Wd = W.qkv8.d; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Mc; gp.N = 2304; gp.K = 768;
         gp.rows_per_utt = CTX; gp.kc = dev->kc; gp.vc = dev->vc; gp.layer = l; gp.nlayers = L; gp.max_seq = dev->max_seq;
         HIPCHK(pre_gemm(gp, GE_QKV_CACHE, s));
         RowAttnP ra{};
@@ -698,18 +876,18 @@ int run_preamble(mp_dev *dev) {
         ra.rows_per_utt = CTX; ra.heads = 12; ra.T = dev->T;
         HIPCHK(pre_row_attn(ra, s));
         gp = GemmP{};
-        gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 768;
+        gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.Wq = W.o8.q; gp.Wd = W.o8.d; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 768;
         gp.rows_per_utt = CTX;
         HIPCHK(pre_gemm(gp, GE_RESID, s));
         HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_xq, dev->pH, 768, Mc, m.eps, s));
         gp = GemmP{};
-        gp.A = dev->pH; gp.lda = 768; gp.W = W.xq; gp.C = dev->pXQ; gp.ldc = 128; gp.M = Mc; gp.N = 128; gp.K = 768;
+        gp.A = dev->pH; gp.lda = 768; gp.W = W.xq; gp.Wq = W.xq8.q; gp.Wd = W.xq8.d; gp.C = dev->pXQ; gp.ldc = 128; gp.M = Mc; gp.N = 128; gp.K = 768;
         gp.rows_per_utt = CTX;
         HIPCHK(pre_gemm(gp, GE_STORE, s));
         RowXaP rx{dev->pXQ, dev->xak, dev->xav, l, L, Tmax, CTX, Mc, dev->T, dev->pXAO};
         HIPCHK(pre_row_xa(rx, s));
         gp = GemmP{};
-        gp.A = dev->pXAO; gp.lda = 128; gp.W = W.xo; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 128;
+        gp.A = dev->pXAO; gp.lda = 128; gp.W = W.xo; gp.Wq = W.xo8.q; gp.Wd = W.xo8.d; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 128;
         gp.rows_per_utt = CTX;
         HIPCHK(pre_gemm(gp, GE_RESID, s));
         HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_ff, dev->pH, 768, Mc, m.eps, s));
@@ -754,19 +932,32 @@ int mp_hip_init(int device, mp_dev **out) {
 
 int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     if (!dev || !path) return MP_ERR_ARG;
-    if (weight_mode != MP_WEIGHTS_AS_STORED && weight_mode != MP_WEIGHTS_BF16)
+    if (weight_mode != MP_WEIGHTS_AS_STORED && weight_mode != MP_WEIGHTS_BF16 && weight_mode != MP_WEIGHTS_Q8)
         return fail(dev, MP_ERR_ARG, "unknown weight mode");
     HIPCHK(hipSetDevice(dev->device));
     free_batch(dev);
     dev->loaded = false;
     dev->m.weight_mode = MP_WEIGHTS_AS_STORED;
-    if (int rc = load_model(dev, path)) return rc;
-    if (weight_mode == MP_WEIGHTS_BF16) {
-        dev->loaded = false;
-        if (int rc = pack_weights(dev)) return rc;
-        dev->m.weight_mode = MP_WEIGHTS_BF16;
-        dev->loaded = true;
+    // drop the Q8_0 views of a previous model
+    if (dev->m.q8_arena) { hipFree(dev->m.q8_arena); dev->m.q8_arena = nullptr; dev->m.q8_bytes = 0; }
+    dev->m.lt_in8 = dev->m.lt_qkv8 = dev->m.lt_o8 = dev->m.lt_out8 = mp::QW{};
+    if (weight_mode == MP_WEIGHTS_Q8) {  // cheap header check before any upload
+        mp::Gguf g;
+        std::string err;
+        if (!g.open(path, err)) return fail(dev, MP_ERR_IO, err);
+        const mp::GgufTensor *t = g.find("decoder.layers.0.self_attention.qkv_net.weight");
+        if (!t || t->type != 8) return fail(dev, MP_ERR_UNSUPPORTED, "Q8 weight mode needs a GGUF with Q8_0 tensors");
     }
+    if (int rc = load_model(dev, path)) return rc;
+    dev->loaded = false;
+    if (weight_mode == MP_WEIGHTS_BF16) {
+        if (int rc = pack_weights(dev)) return rc;
+    } else if (weight_mode == MP_WEIGHTS_Q8) {
+        if (int rc = load_q8(dev, path)) return rc;
+    }
+    if (int rc = build_ptab(dev)) return rc;
+    dev->m.weight_mode = weight_mode;
+    dev->loaded = true;
     return MP_OK;
 }
 
@@ -790,6 +981,7 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.arena) hipFree(dev->m.arena);
     if (dev->m.lt_ptab) hipFree(dev->m.lt_ptab);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
+    if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
     for (void *p : dev->lt_allocs) hipFree(p);
     for (float *p : dev->m.xq_t) hipFree(p);
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
@@ -1119,6 +1311,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
             xp.x_out = dev->q;  // scratch: timing must not disturb the residual stream
             return mp::op_xa(xp, r.B, dev->stream);
         }
+        if (r.kind == mp::K_ROWXA) return mp::pre_row_xa(r.rx, dev->stream);
         return hipErrorInvalidValue;
     };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");

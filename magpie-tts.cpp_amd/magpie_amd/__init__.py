@@ -150,11 +150,13 @@ class SynthResult:
 class Device:
     """One GPU with resident Magpie weights (magpie_init_with_backend, magpie.cpp:781)."""
 
-    WEIGHT_MODES = {"f32": 0, "as_stored": 0, "bf16": 1}
+    WEIGHT_MODES = {"f32": 0, "as_stored": 0, "bf16": 1, "q8": 2}
 
     def __init__(self, model_path: str, device: int = 0, weights: str = "f32"):
-        """weights: "f32" (as stored, widened to f32) or "bf16" (decode projections
-        on bf16 MFMA, activations rounded to bf16; batches up to 16)."""
+        """weights: "f32" (as stored, widened to f32), "bf16" (decode projections
+        on bf16 MFMA, activations rounded to bf16; batches up to 16) or "q8" (the
+        file's Q8_0 tensors kept int8, multiplied with ggml's Q8_0 semantics:
+        activations quantised to Q8_0 per 32-block; batches up to 8)."""
         if weights not in self.WEIGHT_MODES:
             raise ValueError(f"weights must be one of {sorted(self.WEIGHT_MODES)}")
         self.lib = load_library()
@@ -214,11 +216,11 @@ class Device:
     def synthesize_stream(self, codec: "Codec", tokens: Sequence[Sequence[int]], on_audio,
                           speakers: Optional[Sequence[int]] = None, max_dec_steps: int = 500,
                           temperature: float = 0.0, top_k: int = 80, seed: int = 0, frames_per_chunk: int = 4,
-                          stream_base: int = 0):
+                          stream_base: int = 0, ignore_eos: bool = False):
         """magpie_synthesize_sentence_streaming over a batch: on_audio(utt, np.ndarray) -> bool
         (False stops that utterance). The EOS frame is emitted, as the reference's streaming
         loop does. Returns (codes per utterance, total samples, timing)."""
-        B = self.begin(tokens, speakers, max_dec_steps, temperature, top_k, False, seed, False, stream_base, True)
+        B = self.begin(tokens, speakers, max_dec_steps, temperature, top_k, ignore_eos, seed, False, stream_base, True)
 
         def _cb(utt, ptr, n, _user):
             if n == 0:  # end-of-utterance notice

@@ -60,6 +60,60 @@ static void matmul(const float *W, const float *bias, const float *X, float *Y, 
     }
 }
 
+// ------------------------------------------------------------------ Q8_0 (weight mode 2)
+// A Q8_0 tensor of the GGUF (scripts/convert_magpie_to_gguf.py:79-104: per 32
+// weights an fp16 scale d and 32 int8 q, value q*d) kept as stored.
+typedef struct {
+    const float *w;  // the dequantised f32 copy this entry shadows (lookup key)
+    int8_t *q;       // [N][K]
+    float *d;        // [N][K/32] (fp16 values, exact in f32)
+} q8w_t;
+
+// ggml's Q8_0 mul_mat (assumed; ggml is absent here): the activation
+// row is itself quantised to Q8_0 (quantize_row_q8_0_ref: d = amax/127,
+// id = 1/d, q = roundf(x*id), d stored as fp16), then per block the exact
+// integer dot is scaled by d_w*d_a and the blocks are summed
+// (ggml_vec_dot_q8_0_q8_0: sumf += sumi*(d_w*d_a)).
+static void quant_row_q8(const float *x, int K, int8_t *q, float *d) {
+    for (int b = 0; b < K / 32; ++b) {
+        float amax = 0.f;
+        for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(x[b * 32 + j]));
+        const float dd = amax / 127.0f;
+        const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+        d[b] = orc_f16_to_f32(orc_f32_to_f16(dd));
+        for (int j = 0; j < 32; ++j) q[b * 32 + j] = (int8_t)roundf(x[b * 32 + j] * id);
+    }
+}
+
+static void matmul_q8(const q8w_t *W, const float *bias, const float *X, float *Y, int M, int N, int K) {
+    const int nb = K / 32;
+    int8_t *xq = malloc((size_t)M * K);
+    float *xd = malloc(sizeof(float) * (size_t)M * nb);
+    for (int m = 0; m < M; ++m) quant_row_q8(X + (size_t)m * K, K, xq + (size_t)m * K, xd + (size_t)m * nb);
+#pragma omp parallel for schedule(static) if ((long)N * K * M > 200000)
+    for (int n = 0; n < N; ++n) {
+        const int8_t *wq = W->q + (size_t)n * K;
+        const float *wd = W->d + (size_t)n * nb;
+        for (int m = 0; m < M; ++m) {
+            const int8_t *aq = xq + (size_t)m * K;
+            const float *ad = xd + (size_t)m * nb;
+            double v64 = 0.0;
+            float v32 = 0.f;
+            for (int b = 0; b < nb; ++b) {
+                int s = 0;
+                for (int j = 0; j < 32; ++j) s += (int)wq[b * 32 + j] * (int)aq[b * 32 + j];
+                if (g_acc64) v64 += (double)s * ((double)wd[b] * (double)ad[b]);
+                else v32 += (float)s * (wd[b] * ad[b]);
+            }
+            float v = g_acc64 ? (float)v64 : v32;
+            if (bias) v = v + bias[n];
+            Y[(size_t)m * N + n] = v;
+        }
+    }
+    free(xq);
+    free(xd);
+}
+
 // f32 -> bf16 -> f32, round-to-nearest-even (ggml_compute_fp32_to_bf16)
 static float bf16r(float x) {
     uint32_t u;
@@ -73,17 +127,6 @@ static float *bf16_copy(const float *w, size_t n) {
     float *r = malloc(sizeof(float) * n);
     for (size_t i = 0; i < n; ++i) r[i] = bf16r(w[i]);
     return r;
-}
-// Projection in weight mode 1: bf16 weights x bf16-rounded activations,
-// products exact, accumulated like matmul() (ggml's BF16 mul_mat rounds src1 to
-// its vec_dot_type BF16 the same way).
-static void matmul_sel(const float *W, const float *Wh, const float *bias, const float *X, float *Y, int M, int N,
-                       int K) {
-    if (!Wh) { matmul(W, bias, X, Y, M, N, K); return; }
-    float *Xh = malloc(sizeof(float) * (size_t)M * K);
-    for (size_t i = 0; i < (size_t)M * K; ++i) Xh[i] = bf16r(X[i]);
-    matmul(Wh, bias, Xh, Y, M, N, K);
-    free(Xh);
 }
 
 // ggml_norm(eps) * w (magpie.cpp:2237-2259): mean/var accumulated in double.
@@ -171,9 +214,40 @@ struct orc_model {
     // weight mode 1 (bf16 decode projections): rounded copies, NULL in mode 0
     int half;
     float *lt_qkv_h, *lt_o_h, *lt_ff1_h, *lt_ff2_h, *lt_out_w_h[8];
+    // weight mode 2 (ggml Q8_0 mul_mat for the file's Q8_0 tensors): the raw blocks
+    int q8mode;
+    q8w_t *q8;
+    int n_q8, cap_q8;
     float **owned;
     int n_owned, cap_owned;
 };
+
+static const q8w_t *find_q8(const orc_model *m, const float *W) {
+    if (!m->q8mode) return NULL;
+    for (int i = 0; i < m->n_q8; ++i)
+        if (m->q8[i].w == W) return &m->q8[i];
+    return NULL;
+}
+
+// ggml_mul_mat(W, X) (+ bias) with W's stored type: Q8_0 tensors in weight
+// mode 2 take ggml's quantised path, everything else the f32 dot.
+static void mm(const orc_model *m, const float *W, const float *bias, const float *X, float *Y, int M, int N, int K) {
+    const q8w_t *q = find_q8(m, W);
+    if (q) matmul_q8(q, bias, X, Y, M, N, K);
+    else matmul(W, bias, X, Y, M, N, K);
+}
+
+// Projection in weight mode 1: bf16 weights x bf16-rounded activations,
+// products exact, accumulated like matmul() (ggml's BF16 mul_mat rounds src1 to
+// its vec_dot_type BF16 the same way). Wh == NULL: mm().
+static void matmul_sel(const orc_model *m, const float *W, const float *Wh, const float *bias, const float *X, float *Y,
+                       int M, int N, int K) {
+    if (!Wh) { mm(m, W, bias, X, Y, M, N, K); return; }
+    float *Xh = malloc(sizeof(float) * (size_t)M * K);
+    for (size_t i = 0; i < (size_t)M * K; ++i) Xh[i] = bf16r(X[i]);
+    matmul(Wh, bias, Xh, Y, M, N, K);
+    free(Xh);
+}
 
 static float *take(orc_model *m, const orc_gguf *g, const char *name, int *ok) {
     float *p = orc_gguf_f32(g, name, NULL);
@@ -183,6 +257,25 @@ static float *take(orc_model *m, const orc_gguf *g, const char *name, int *ok) {
         m->owned = realloc(m->owned, sizeof(float *) * (size_t)m->cap_owned);
     }
     m->owned[m->n_owned++] = p;
+    const orc_tinfo *t = orc_gguf_find(g, name);
+    if (t && t->type == 8) {  // keep the stored Q8_0 blocks for weight mode 2
+        const int64_t n = t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3];
+        const uint8_t *src = g->map + g->data_off + t->offset;
+        if (m->n_q8 == m->cap_q8) {
+            m->cap_q8 = m->cap_q8 ? 2 * m->cap_q8 : 64;
+            m->q8 = realloc(m->q8, sizeof(q8w_t) * (size_t)m->cap_q8);
+        }
+        q8w_t *e = &m->q8[m->n_q8++];
+        e->w = p;
+        e->q = malloc((size_t)n);
+        e->d = malloc(sizeof(float) * (size_t)(n / 32));
+        for (int64_t b = 0; b < n / 32; ++b) {
+            uint16_t h;
+            memcpy(&h, src + b * 34, 2);
+            e->d[b] = orc_f16_to_f32(h);
+            memcpy(e->q + b * 32, src + b * 34 + 2, 32);
+        }
+    }
     return p;
 }
 
@@ -292,9 +385,15 @@ static void free_half(orc_model *m) {
 }
 
 int orc_set_weight_mode(orc_model *m, int mode) {
-    if (!m || mode < 0 || mode > 1) return -1;
+    if (!m || mode < 0 || mode > 2) return -1;
     free_half(m);
+    m->q8mode = 0;
     if (mode == 0) return 0;
+    if (mode == 2) {  // ggml Q8_0 semantics for the file's Q8_0 tensors
+        if (m->n_q8 == 0) return -1;
+        m->q8mode = 1;
+        return 0;
+    }
     const int d = m->d, dff = m->dff, D = m->lt_dim, F = m->lt_ffn;
     for (int l = 0; l < m->dec_layers; ++l) {
         dec_layer *L = &m->dec[l];
@@ -315,6 +414,8 @@ int orc_set_weight_mode(orc_model *m, int mode) {
 void orc_free(orc_model *m) {
     if (!m) return;
     free_half(m);
+    for (int i = 0; i < m->n_q8; ++i) { free(m->q8[i].q); free(m->q8[i].d); }
+    free(m->q8);
     for (int i = 0; i < m->n_owned; ++i) free(m->owned[i]);
     free(m->owned);
     free(m->enc);
@@ -396,9 +497,9 @@ int orc_encode(orc_model *m, const int32_t *tok, int T, float *enc_out) {
     for (int l = 0; l < m->enc_layers; ++l) {
         const enc_layer *L = &m->enc[l];
         layernorm_rows(x, L->norm_self, h, T, d, m->eps);
-        matmul(L->qkv, NULL, h, qkv, T, 3 * d, d);
+        mm(m, L->qkv, NULL, h, qkv, T, 3 * d, d);
         causal_mha(qkv, T, d, m->enc_heads, att, 0, NULL, NULL);
-        matmul(L->o, NULL, att, o, T, d, d);
+        mm(m, L->o, NULL, att, o, T, d, d);
         for (size_t i = 0; i < (size_t)T * d; ++i) x[i] = o[i] + x[i];
         layernorm_rows(x, L->norm_ff, h, T, d, m->eps);
         conv_ffn_k(L->ff1, h, f, T, dff, d, m->enc_kernel);
@@ -433,17 +534,17 @@ static void decoder_layer(const orc_model *m, dstate *s, int l, float *x, int M,
     // self-attention: LN -> qkv -> cache append -> attention over [0, pos] -> o_net (3395-3480)
     const int hm = m->half && M == 1;  // decode steps only; the 110-frame prefill stays f32
     layernorm_rows(x, L->norm_self, h, M, d, m->eps);
-    matmul_sel(L->qkv, hm ? L->qkv_h : NULL, NULL, h, qkv, M, 3 * d, d);
+    matmul_sel(m, L->qkv, hm ? L->qkv_h : NULL, NULL, h, qkv, M, 3 * d, d);
     for (int r = 0; r < M; ++r) {
         memcpy(Kc + (size_t)(pos0 + r) * d, qkv + (size_t)r * 3 * d + d, sizeof(float) * d);
         memcpy(Vc + (size_t)(pos0 + r) * d, qkv + (size_t)r * 3 * d + 2 * d, sizeof(float) * d);
     }
     causal_mha(qkv, M, d, m->dec_heads, att, pos0, Kc, Vc);
-    matmul_sel(L->o, hm ? L->o_h : NULL, NULL, att, o, M, d, d);
+    matmul_sel(m, L->o, hm ? L->o_h : NULL, NULL, att, o, M, d, d);
     for (size_t i = 0; i < (size_t)M * d; ++i) x[i] = o[i] + x[i];
     // cross-attention with cached K/V (1713-1767): 1 head x 128, no mask
     layernorm_rows(x, L->norm_xq, h, M, d, m->eps);
-    matmul(L->xq, NULL, h, q, M, dxa, d);
+    mm(m, L->xq, NULL, h, q, M, dxa, d);
     {
         const int dh = m->xa_dh;
         const double scale = 1.0 / sqrt((double)dh);
@@ -454,15 +555,15 @@ static void decoder_layer(const orc_model *m, dstate *s, int l, float *x, int M,
             for (int hh = 0; hh < m->xa_heads; ++hh)
                 attend(q + (size_t)r * dxa + hh * dh, XK + hh * dh, XV + hh * dh, s->T, dxa, dh, scale,
                        ax + (size_t)r * dxa + hh * dh, sb, pb);
-        matmul(L->xo, NULL, ax, o, M, d, dxa);
+        mm(m, L->xo, NULL, ax, o, M, d, dxa);
         free(sb); free(pb); free(ax);
     }
     for (size_t i = 0; i < (size_t)M * d; ++i) x[i] = o[i] + x[i];
     // pointwise conv-FFN (1791-1805)
     layernorm_rows(x, L->norm_ff, h, M, d, m->eps);
-    matmul_sel(L->ff1, hm ? L->ff1_h : NULL, NULL, h, f, M, dff, d);
+    matmul_sel(m, L->ff1, hm ? L->ff1_h : NULL, NULL, h, f, M, dff, d);
     gelu_inplace(f, (size_t)M * dff);
-    matmul_sel(L->ff2, hm ? L->ff2_h : NULL, NULL, f, o, M, d, dff);
+    matmul_sel(m, L->ff2, hm ? L->ff2_h : NULL, NULL, f, o, M, d, dff);
     for (size_t i = 0; i < (size_t)M * d; ++i) x[i] = o[i] + x[i];
     free(h); free(qkv); free(att); free(o); free(q); free(f);
 }
@@ -537,22 +638,22 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, f
     float s[9][256], X[256], h[256], qkv[768], kk[8][256], vv[8][256], a[256], Y[256], f[1024], y2[256];
     float *logits = malloc(sizeof(float) * (size_t)V);
     double sb[8], pb[8];
-    matmul(m->lt_in_w, m->lt_in_b, hidden, s[0], 1, D, d);
+    mm(m, m->lt_in_w, m->lt_in_b, hidden, s[0], 1, D, d);
     for (int cb = 0; cb < 8; ++cb) {
         for (int i = 0; i < D; ++i) X[i] = s[cb][i] + m->lt_pos[(size_t)cb * D + i];
         layernorm(X, m->lt_norm_self, h, D, m->eps);
-        matmul_sel(m->lt_qkv, m->lt_qkv_h, NULL, h, qkv, 1, 3 * D, D);
+        matmul_sel(m, m->lt_qkv, m->lt_qkv_h, NULL, h, qkv, 1, 3 * D, D);
         memcpy(kk[cb], qkv + D, sizeof(float) * D);
         memcpy(vv[cb], qkv + 2 * D, sizeof(float) * D);
         attend(qkv, &kk[0][0], &vv[0][0], cb + 1, D, D, 1.0 / sqrt((double)D), a, sb, pb);
-        matmul_sel(m->lt_o, m->lt_o_h, NULL, a, Y, 1, D, D);
+        matmul_sel(m, m->lt_o, m->lt_o_h, NULL, a, Y, 1, D, D);
         for (int i = 0; i < D; ++i) Y[i] = Y[i] + X[i];
         layernorm(Y, m->lt_norm_ff, h, D, m->eps);
-        matmul_sel(m->lt_ff1, m->lt_ff1_h, NULL, h, f, 1, F, D);
+        matmul_sel(m, m->lt_ff1, m->lt_ff1_h, NULL, h, f, 1, F, D);
         gelu_inplace(f, (size_t)F);
-        matmul_sel(m->lt_ff2, m->lt_ff2_h, NULL, f, y2, 1, D, F);
+        matmul_sel(m, m->lt_ff2, m->lt_ff2_h, NULL, f, y2, 1, D, F);
         for (int i = 0; i < D; ++i) y2[i] = y2[i] + Y[i];
-        matmul_sel(m->lt_out_w[cb], m->lt_out_w_h[cb], m->lt_out_b[cb], y2, logits, 1, V, D);
+        matmul_sel(m, m->lt_out_w[cb], m->lt_out_w_h[cb], m->lt_out_b[cb], y2, logits, 1, V, D);
         // forbidden tokens (1133-1145) and first-max argmax (1250-1259)
         for (int t = m->audio_bos; t <= m->audio_bos + 7 && t < V; ++t)
             if (t != m->audio_eos || forbid_eos) logits[t] = -INFINITY;
@@ -574,7 +675,7 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, f
         if (margins) margins[cb] = mg;
         if (cb < 7) {
             const float *e = m->audio_emb[cb] + (size_t)code * d;  // no 1/8 here (1284-1291)
-            matmul(m->lt_in_w, m->lt_in_b, e, s[cb + 1], 1, D, d);
+            mm(m, m->lt_in_w, m->lt_in_b, e, s[cb + 1], 1, D, d);
         }
     }
     free(logits);
@@ -614,7 +715,7 @@ int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, i
         float *hn = malloc(sizeof(float) * (size_t)T * d), *kv = malloc(sizeof(float) * (size_t)T * 2 * dxa);
         for (int l = 0; l < L; ++l) {
             layernorm_rows(enc, m->dec[l].norm_xmem, hn, T, d, m->eps);
-            matmul(m->dec[l].xkv, NULL, hn, kv, T, 2 * dxa, d);
+            mm(m, m->dec[l].xkv, NULL, hn, kv, T, 2 * dxa, d);
             for (int t = 0; t < T; ++t) {
                 memcpy(s.xa_k + ((size_t)l * T + t) * dxa, kv + (size_t)t * 2 * dxa, sizeof(float) * dxa);
                 memcpy(s.xa_v + ((size_t)l * T + t) * dxa, kv + (size_t)t * 2 * dxa + dxa, sizeof(float) * dxa);
@@ -892,4 +993,21 @@ int orc_codec_decode(orc_codec *c, const int32_t *codes, int F, float *audio, in
     for (int t = 0; t < T; ++t) audio[t] = tanhf(h2[t]);
     free(x); free(h); free(h2); free(acc); free(rb); free(lat);
     return T;
+}
+
+// Unit-test entry: y[N] = ggml Q8_0 mul_mat of the raw GGUF Q8_0 blocks
+// (34 bytes per 32 weights, row-major [N][K]) with the activation x[K].
+int orc_q8_matvec(const uint8_t *blocks, int N, int K, const float *x, float *y) {
+    if (!blocks || !x || !y || N <= 0 || K <= 0 || K % 32) return -1;
+    q8w_t w = {NULL, malloc((size_t)N * K), malloc(sizeof(float) * (size_t)N * (K / 32))};
+    for (int64_t b = 0; b < (int64_t)N * K / 32; ++b) {
+        uint16_t h;
+        memcpy(&h, blocks + b * 34, 2);
+        w.d[b] = orc_f16_to_f32(h);
+        memcpy(w.q + b * 32, blocks + b * 34 + 2, 32);
+    }
+    matmul_q8(&w, NULL, x, y, 1, N, K);
+    free(w.q);
+    free(w.d);
+    return 0;
 }

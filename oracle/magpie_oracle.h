@@ -33,7 +33,12 @@ orc_model *orc_load(const char *gguf_path);
 // the projections qkv/o/ff1/ff2 of every decoder layer and of the LT layer, and
 // the 8 LT output projections, use bf16-rounded weights and bf16-rounded input
 // activations (ggml's BF16 mul_mat semantics), f32/f64 accumulation. Encoder,
-// prefill, cross-attention and LT in_proj stay f32. 0 = as stored (f32).
+// prefill, cross-attention and LT in_proj stay f32. 0 = as stored (Q8_0/F16
+// tensors dequantised to f32, f32 activations). Weight mode 2 = ggml's Q8_0
+// mul_mat for every Q8_0 tensor of the file, everywhere it is used (encoder,
+// XA K/V, prefill, decode steps, LT): the activation row is quantised to Q8_0
+// (quantize_row_q8_0_ref), per-block integer dots scaled by d_w*d_a (SURVEY A.7,
+// assumed); -1 if the file has no Q8_0 tensor.
 int orc_set_weight_mode(orc_model *m, int mode);
 void orc_free(orc_model *m);
 int orc_dec_layers(const orc_model *m);
@@ -65,6 +70,8 @@ int orc_lt_sample(orc_model *m, const float *hidden, float temperature, int top_
 float orc_draw_u(uint64_t seed, int stream, int step, int cb);
 int orc_sample_top_k(const float *logits, int n, float temperature, int top_k, float u, float *margin);
 int orc_encode(orc_model *m, const int32_t *tokens, int n_tokens, float *enc_out /*[T][768]*/);
+// ggml Q8_0 mul_mat of raw GGUF Q8_0 blocks ([N][K], 34 B per 32 weights) with x[K].
+int orc_q8_matvec(const uint8_t *blocks, int N, int K, const float *x, float *y);
 
 orc_codec *orc_codec_load(const char *gguf_path);
 void orc_codec_free(orc_codec *c);

@@ -47,6 +47,7 @@ def lib() -> ctypes.CDLL:
         L.orc_codec_free.argtypes = [P]
         L.orc_codec_decode.argtypes = [P, P, I, P, I]
         L.orc_fsq.argtypes = [P, I, P]
+        L.orc_q8_matvec.argtypes = [P, I, I, P, P]
         _lib = L
     return _lib
 
@@ -74,7 +75,8 @@ class Model:
             raise RuntimeError(f"oracle: cannot load {path}")
 
     def set_weight_mode(self, mode: int) -> None:
-        """0 = f32 as stored, 1 = bf16 decode projections (see magpie_oracle.h)."""
+        """0 = f32 (dequantised), 1 = bf16 decode projections, 2 = ggml Q8_0 mul_mat
+        for the file's Q8_0 tensors (see magpie_oracle.h)."""
         if lib().orc_set_weight_mode(self.h, int(mode)) != 0:
             raise RuntimeError("oracle: bad weight mode")
 
@@ -138,6 +140,17 @@ class Codec:
         if self.h:
             lib().orc_codec_free(self.h)
             self.h = None
+
+
+def q8_matvec(blocks: bytes, N: int, K: int, x) -> np.ndarray:
+    """ggml Q8_0 mul_mat (activation quantised to Q8_0) of raw GGUF blocks with x[K]."""
+    buf = np.frombuffer(blocks, np.uint8)
+    assert buf.size == N * K // 32 * 34
+    xv = np.ascontiguousarray(x, np.float32)
+    y = np.zeros(N, np.float32)
+    if lib().orc_q8_matvec(buf.ctypes.data, N, K, xv.ctypes.data, y.ctypes.data) != 0:
+        raise RuntimeError("oracle q8_matvec failed")
+    return y
 
 
 def fsq(codes_cb_major):

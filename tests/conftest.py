@@ -56,6 +56,12 @@ def q8_model():
 
 
 @pytest.fixture(scope="session")
+def q8_full_model():
+    """Magpie-357M shapes, the reference converter's default Q8_0 patterns."""
+    return _gguf("magpie_357m_q8.gguf", dtype="q8_0")
+
+
+@pytest.fixture(scope="session")
 def codec_model():
     return _gguf("nano_codec.gguf", kind="codec")
 

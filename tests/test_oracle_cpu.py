@@ -191,3 +191,76 @@ def test_oracle_bf16_mode_close_to_f32(oracle, small_model):
     d0 = np.abs(f["hidden"][0] - h["hidden"][0]).max()
     assert 0 < d0 < 0.1, d0
     assert np.array_equal(f["hidden"], g["hidden"]) and np.array_equal(f["codes"], g["codes"])
+
+
+# ---------------------------------------------------------------- Q8_0 (weight mode 2)
+def _q8_blocks_like_converter(W):
+    """convert_magpie_to_gguf.py:79-104 in numpy: fp16 d = amax/127, q = round-half-even(x/d)."""
+    x = W.astype(np.float32).reshape(-1, 32)
+    amax = np.abs(x).max(axis=1)
+    d = np.where(amax != 0, amax / 127.0, 0.0).astype(np.float16)
+    ds = np.where(d != 0, d.astype(np.float32), 1.0)[:, None]
+    q = np.where(d[:, None] != 0, np.round(x / ds), 0).astype(np.int8)
+    blk = np.empty(len(x), np.dtype([("d", "<f2"), ("q", "i1", 32)]))
+    blk["d"], blk["q"] = d, q
+    return blk.tobytes(), q.astype(np.int64), d.astype(np.float64)
+
+
+def _ggml_q8_matvec_numpy(q, d, N, K, x):
+    """ggml Q8_0 mul_mat restated independently: quantize_row_q8_0_ref on x
+    (d = amax/127 in f32, id = 1/d, q = roundf(x*id) half away from zero, d kept
+    as fp16), then sum over blocks of int dot * (d_w * d_a)."""
+    xb = x.astype(np.float32).reshape(-1, 32)
+    amax = np.abs(xb).max(axis=1)
+    da = amax / np.float32(127.0)
+    ida = np.where(da != 0, np.float32(1.0) / np.where(da != 0, da, 1), 0).astype(np.float32)
+    v = xb * ida[:, None]
+    qa = (np.sign(v) * np.floor(np.abs(v) + np.float32(0.5))).astype(np.int64)
+    da16 = da.astype(np.float16).astype(np.float64)
+    qw = q.reshape(N, K // 32, 32)
+    dw = d.reshape(N, K // 32)
+    sumi = (qw * qa[None]).sum(axis=2)
+    return (sumi * (dw * da16[None])).sum(axis=1)
+
+
+def test_q8_matvec_matches_numpy_restatement(oracle):
+    rng = np.random.default_rng(8)
+    N, K = 96, 256
+    W = rng.normal(0, 0.02, (N, K)).astype(np.float32)
+    W[3, :32] = 0.0  # an all-zero block: d = 0, q = 0
+    blocks, q, d = _q8_blocks_like_converter(W)
+    for trial in range(3):
+        x = rng.normal(0, 1.0, K).astype(np.float32)
+        if trial == 1:
+            x[32:64] = 0.0  # zero activation block
+        if trial == 2:
+            x[:32] = np.round(x[:32] * 4) / 4  # exact halves after scaling are possible
+        y = oracle.q8_matvec(blocks, N, K, x)
+        ref = _ggml_q8_matvec_numpy(q, d, N, K, x)
+        np.testing.assert_allclose(y, ref.astype(np.float32), rtol=2e-6, atol=1e-9)
+    # activation quantisation is visible: differs from the dequantised f32 product
+    deq = (q.reshape(N, K // 32, 32) * d.reshape(N, K // 32, 1)).reshape(N, K)
+    assert np.abs(y - deq @ x.astype(np.float64)).max() > 1e-6
+
+
+def test_oracle_q8_mode(oracle, q8_model, small_model):
+    """Weight mode 2 (ggml Q8_0 mul_mat) stays within quantisation noise of the
+    dequantised-f32 mode, is deterministic, and needs a file with Q8_0 tensors."""
+    import magpie_amd as ma
+    tok = ma.synthetic_tokens(12, seed=4)
+    m = oracle.Model(q8_model)
+    f = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.set_weight_mode(2)
+    a = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    b = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.set_weight_mode(0)
+    g = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.close()
+    assert np.array_equal(a["hidden"], b["hidden"]) and np.array_equal(a["codes"], b["codes"])
+    d0 = np.abs(f["hidden"][0] - a["hidden"][0]).max()
+    assert 0 < d0 < 0.2, d0
+    assert np.array_equal(f["hidden"], g["hidden"])
+    m = oracle.Model(small_model)
+    with pytest.raises(RuntimeError):
+        m.set_weight_mode(2)  # F32 file: nothing to run as Q8_0
+    m.close()

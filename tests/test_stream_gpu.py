@@ -115,3 +115,19 @@ def test_lt_sample_matches_oracle(ma, oracle, small_model):
             assert np.array_equal(smp, amx)
     dev.close()
     om.close()
+
+
+def test_lt_sample_q8_matches_oracle(ma, oracle, q8_model):
+    """magpie_local_transformer_sample_all with the Q8_0 LT projections (weight mode q8)."""
+    rng = np.random.default_rng(6)
+    dev = ma.Device(q8_model, weights="q8")
+    om = oracle.Model(q8_model)
+    om.set_weight_mode(2)
+    for call in range(4):
+        h = rng.normal(0, 1, 768).astype(np.float32)
+        temp = 0.0 if call < 2 else 0.8
+        smp, amx = dev.lt_sample(h, temperature=temp, top_k=50, seed=12)
+        o_smp, o_amx, o_mg = om.lt_sample(h, temperature=temp, top_k=50, seed=12, stream=-1, step=4 + call)
+        compare_codes(smp[None], o_smp[None], o_mg[None], tie_eps=1e-2)
+    dev.close()
+    om.close()

@@ -17,6 +17,6 @@ fi
 timeout -k 10 300 python -u bench.py > "$OUT/${TAG}_bench.log" 2>&1
 tail -1 "$OUT/${TAG}_bench.log" > "$OUT/${TAG}_bench.json"
 echo "bench ok"
-MAGPIE_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o prof \
+MAGPIE_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/${TAG}_prof" -o prof \
   -- python3 -u bench.py --no-cpu-baseline --no-extra > "$OUT/${TAG}_prof_bench.log" 2>&1
 echo "rocprof ok"

@@ -141,6 +141,13 @@ double mp_hip_op_bytes(mp_dev *dev, int op);
  * stream (same arguments as in the captured graph), one hipEvent pair around
  * the whole run; returns the mean per-launch time in us (kernel + dispatch gap). */
 int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us);
+/* In-situ per-op timing: run `iters` whole decode iterations with every kernel
+ * launched directly (not from the graph), each launch bracketed by a hipEvent
+ * pair on the decode stream, so every op sees the caches a real frame leaves it
+ * (weights streamed by the ops before it). avg_us[op] = mean per launch of op
+ * (mp_hip_num_ops entries). Continues from the batch's current state; after
+ * every utterance is done the iteration recomputes the same frame. */
+int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us);
 
 /* --- text front end (host) ---------------------------------------------------- */
 /* magpie_tokenizer_init + magpie_tokenize (magpie.cpp:124-495): vocabulary and

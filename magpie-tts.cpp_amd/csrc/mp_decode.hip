@@ -84,15 +84,18 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 }
 
 // ---------------------------------------------------------------- SA decode attention
-// One workgroup of 16 waves per (head, slot) over the whole live cache, no
-// split-K and no combine pass: wave w takes keys 4(w + 16 r) + kk (16 lanes x
-// float4 cover one 64-dim row, a wave does 4 keys per instruction) with four
+// Split-K over the live cache: grid (head, split, slot), 8 waves per workgroup.
+// Split s of head h takes keys [s*chunk, (s+1)*chunk) of L = pos + 1
+// (magpie.cpp:3412); wave w takes keys 4(w + 8 r) + kk of it (16 lanes x float4
+// cover one 64-dim row, a wave does 4 keys per instruction) with four
 // iterations' K and V loads in flight, keeps an online softmax (m, l, o[64]),
-// and the 16 wave states are merged through LDS. Keys j > pos are masked
-// (L = pos + 1, magpie.cpp:3412); softmax(K q / 8) V per head (3457-3476).
-constexpr int SA_WAVES = 16, SA_THREADS = SA_WAVES * 64, SA_IF = 4;  // iterations in flight
+// the 8 wave states are merged in LDS, and the split's state (m, l, unnormalised
+// O) is stored; the O-projection's PRO_SA_MERGE prologue merges the splits
+// (softmax(K q / 8) V per head, 3457-3476). At batch 1 that is 48 workgroups of
+// ~L/4 keys each instead of one workgroup streaming a whole head.
+constexpr int SA_WAVES = 8, SA_THREADS = SA_WAVES * 64, SA_IF = 4;  // iterations in flight
 __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
-    const int h = blockIdx.x, b = blockIdx.y;
+    const int h = blockIdx.x, sp = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kk = lane >> 4, dc = lane & 15;
     __shared__ float wm[SA_WAVES], wl[SA_WAVES];
@@ -100,25 +103,27 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
     const int L = p.pos[b] + 1;
+    const int chunk = (L + SA_SPLITS - 1) / SA_SPLITS;
+    const int j0 = sp * chunk, j1 = min(L, j0 + chunk);
     float m = -INFINITY, l = 0.f;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r0 = 0; 64 * r0 < L; r0 += SA_IF) {
+    for (int r0 = 0; j0 + 4 * SA_WAVES * r0 < j1; r0 += SA_IF) {
         float4 k4[SA_IF], v4[SA_IF];
 #pragma unroll
         for (int u = 0; u < SA_IF; ++u) {
             // rows < max_seq are always valid memory: no load waits for the mask
-            const int j = min(4 * (w + SA_WAVES * (r0 + u)) + kk, p.max_seq - 1);
+            const int j = min(j0 + 4 * (w + SA_WAVES * (r0 + u)) + kk, p.max_seq - 1);
             k4[u] = *(const float4 *)(p.kc + base + (size_t)j * D);
             v4[u] = *(const float4 *)(p.vc + base + (size_t)j * D);
         }
-        float s[SA_IF];
+        float sv[SA_IF];
         float mb = -INFINITY;
 #pragma unroll
         for (int u = 0; u < SA_IF; ++u) {
-            const int j = 4 * (w + SA_WAVES * (r0 + u)) + kk;
+            const int j = j0 + 4 * (w + SA_WAVES * (r0 + u)) + kk;
             const float v = group_sum<16>(dotv(q4, k4[u])) * 0.125f;  // 1/sqrt(64)
-            s[u] = j < L ? v : -INFINITY;
-            mb = fmaxf(mb, s[u]);
+            sv[u] = j < j1 ? v : -INFINITY;
+            mb = fmaxf(mb, sv[u]);
         }
         mb = wave_max(mb);
         if (mb == -INFINITY) continue;  // nothing live for this wave in this batch
@@ -127,7 +132,7 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
         o.x *= c; o.y *= c; o.z *= c; o.w *= c;
 #pragma unroll
         for (int u = 0; u < SA_IF; ++u) {
-            const float e = s[u] == -INFINITY ? 0.f : expf(s[u] - mn);
+            const float e = sv[u] == -INFINITY ? 0.f : expf(sv[u] - mn);
             l += e;  // per lane: its key group's keys; summed over the wave below
             o.x += e * v4[u].x; o.y += e * v4[u].y; o.z += e * v4[u].z; o.w += e * v4[u].w;
         }
@@ -154,47 +159,42 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
         den += e * wl[q];
         num += e * wo[q][tid];
     }
-    p.out[(size_t)b * D + h * DH + tid] = num / den;
+    float *pp = p.part + ((size_t)(b * NH + h) * SA_SPLITS + sp) * SA_PART;
+    pp[4 + tid] = num;  // relative to M (an empty split stores M = -inf, l = 0, O = 0)
+    if (tid == 0) { pp[0] = M; pp[1] = den; }
 }
 
 // ---------------------------------------------------------------- fused XA
-// grid (768/64, B), 16 waves per workgroup. Every wave normalises x itself (the
-// same DPP statistics in every wave: no barrier) and scores keys t = w, w+16, ...
-// with all of its K' loads in flight at once (12 scalar loads per key per lane,
-// each a coalesced 256 B wave access), so the score phase costs one L2 round trip
-// instead of one per group of keys. The workgroup then owns 64 output dims:
-// out[d] = x[d] + sum_t e_t V'_t[d] / l (K' rows are L2-resident after the first
-// workgroup; the 12 workgroups of a slot share them).
-constexpr int XA_WAVES = 16, XA_THREADS = XA_WAVES * 64, XA_KPW = 4;  // keys in flight per wave
-constexpr int XA_VPW = 8;  // V' values prefetched per lane (keys t = w + 16 u)
-__global__ __launch_bounds__(XA_THREADS) void xa_fused_kernel(XaP p) {
-    __shared__ float sc[TMAX_LIMIT];
-    __shared__ float part[XA_WAVES][64];
-    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int d0 = blockIdx.x * 64;
+// XA reassociated: with K'_t = W_q^T K_t and V'_t = W_o V_t precomputed per
+// utterance and layer, x += sum_t softmax_t(K'_t . LN(x) / sqrt(128)) V'_t.
+// Split over text keys: grid (split, slot), 8 waves. Split s takes keys
+// [s*chunk, (s+1)*chunk) of T; wave w takes t = t0 + w, t0 + w + 8, ... with its
+// first keys' K' and V' rows issued before x is fetched (one round trip), every
+// wave normalises x itself (DPP statistics, no barrier), keeps an online softmax
+// (m, l, o[768] in 12 registers per lane); the 8 wave states merge in LDS and
+// the split's state (m, l, unnormalised O[768]) is stored. The next op (FFN up,
+// PRO_XA_LN) merges the XA_SPLITS states, adds x and normalises.
+constexpr int XA_WAVES = 8, XA_THREADS = XA_WAVES * 64, XA_KPW = 2;  // keys in flight per wave
+__global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
+    __shared__ float wm[XA_WAVES], wl[XA_WAVES];
+    __shared__ float wo[XA_WAVES][D];
+    const int sp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int Tb = p.T[b];
+    const int chunk = (Tb + XA_SPLITS - 1) / XA_SPLITS;
+    const int t0 = sp * chunk, t1 = min(Tb, t0 + chunk);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
     const float *Kp = p.kp + base, *Vp = p.vp + base;
-    // Nothing below the loads depends on x: issue the first keys' K' rows and this
-    // lane's V' values, then x, so the three fetches share one memory round trip.
-    float k[XA_KPW][D / 64];
+    float k[XA_KPW][D / 64], vv[XA_KPW][D / 64];
 #pragma unroll
     for (int u = 0; u < XA_KPW; ++u) {
-        const int t = w + XA_WAVES * u;
-        const float *kr = Kp + (size_t)(t < Tb ? t : 0) * D + lane;
+        const int t = t0 + w + XA_WAVES * u;
+        const size_t r = (size_t)(t < t1 ? t : 0) * D + lane;
 #pragma unroll
-        for (int i = 0; i < D / 64; ++i) k[u][i] = kr[64 * i];
+        for (int i = 0; i < D / 64; ++i) { k[u][i] = Kp[r + 64 * i]; vv[u][i] = Vp[r + 64 * i]; }
     }
-    float vv[XA_VPW];
-#pragma unroll
-    for (int u = 0; u < XA_VPW; ++u) {
-        const int t = w + XA_WAVES * u;
-        vv[u] = Vp[(size_t)(t < Tb ? t : 0) * D + d0 + lane];
-    }
-    asm volatile("" ::: "memory");  // keep these loads ahead of the x fetch and the loop below
-    // LN(x) (magpie.cpp:3513): lane owns elements lane + 64 i
+    asm volatile("" ::: "memory");  // keep these loads ahead of the x fetch
     float h[D / 64];
-    {
+    {   // LN(x) (magpie.cpp:3513): lane owns elements lane + 64 i
         float v[D / 64];
 #pragma unroll
         for (int i = 0; i < D / 64; ++i) v[i] = p.x[(size_t)b * D + lane + 64 * i];
@@ -205,55 +205,60 @@ __global__ __launch_bounds__(XA_THREADS) void xa_fused_kernel(XaP p) {
         for (int i = 0; i < D / 64; ++i) h[i] = ((v[i] - mean) * rstd) * p.lnw[lane + 64 * i];
     }
     const float scale = 1.0f / sqrtf((float)DXA);
-    for (int t0 = w;; t0 += XA_WAVES * XA_KPW) {
+    float m = -INFINITY, l = 0.f, o[D / 64];
+#pragma unroll
+    for (int i = 0; i < D / 64; ++i) o[i] = 0.f;
+    for (int tb = t0 + w; tb < t1; tb += XA_WAVES * XA_KPW) {
 #pragma unroll
         for (int u = 0; u < XA_KPW; ++u) {
+            const int t = tb + XA_WAVES * u;
+            if (t >= t1) break;  // wave-uniform
             float acc = 0.f;
 #pragma unroll
             for (int i = 0; i < D / 64; ++i) acc += k[u][i] * h[i];
-            const float sv = wave_sum(acc);
-            const int t = t0 + XA_WAVES * u;
-            if (lane == 0 && t < Tb) sc[t] = sv * scale;
+            const float sv = wave_sum(acc) * scale;
+            const float mn = fmaxf(m, sv), c = expf(m - mn), e = expf(sv - mn);
+            l = l * c + e;
+#pragma unroll
+            for (int i = 0; i < D / 64; ++i) o[i] = o[i] * c + e * vv[u][i];
+            m = mn;
         }
-        const int t1 = t0 + XA_WAVES * XA_KPW;
-        if (t1 >= Tb) break;
+        const int tn = tb + XA_WAVES * XA_KPW;
+        if (tn >= t1) break;
 #pragma unroll
         for (int u = 0; u < XA_KPW; ++u) {  // next keys (long texts)
-            const int t = t1 + XA_WAVES * u;
-            const float *kr = Kp + (size_t)(t < Tb ? t : 0) * D + lane;
+            const int t = tn + XA_WAVES * u;
+            const size_t r = (size_t)(t < t1 ? t : 0) * D + lane;
 #pragma unroll
-            for (int i = 0; i < D / 64; ++i) k[u][i] = kr[64 * i];
+            for (int i = 0; i < D / 64; ++i) { k[u][i] = Kp[r + 64 * i]; vv[u][i] = Vp[r + 64 * i]; }
         }
     }
-    lds_sync();
-    // softmax statistics: every wave reduces the T scores itself
-    float m = -INFINITY;
-    for (int t = lane; t < Tb; t += 64) m = fmaxf(m, sc[t]);
-    m = wave_max(m);
-    float l = 0.f;
-    for (int t = lane; t < Tb; t += 64) l += expf(sc[t] - m);
-    l = wave_sum(l);
-    // out[d] = sum_t e_t V'_t[d] / l for this workgroup's 64 dims; wave w takes t = w (mod 16)
-    float acc = 0.f;
 #pragma unroll
-    for (int u = 0; u < XA_VPW; ++u) {
-        const int t = w + XA_WAVES * u;
-        if (t < Tb) acc += expf(sc[t] - m) * vv[u];
-    }
-    for (int t = w + XA_WAVES * XA_VPW; t < Tb; t += XA_WAVES) acc += expf(sc[t] - m) * Vp[(size_t)t * D + d0 + lane];
-    part[w][lane] = acc;
+    for (int i = 0; i < D / 64; ++i) wo[w][lane + 64 * i] = o[i];
+    if (lane == 0) { wm[w] = m; wl[w] = l; }
     lds_sync();
-    if (tid < 64) {
-        float o = 0.f;
+    float M = -INFINITY;
 #pragma unroll
-        for (int q = 0; q < XA_WAVES; ++q) o += part[q][tid];
-        p.x_out[(size_t)b * D + d0 + tid] = o / l + p.x[(size_t)b * D + d0 + tid];
+    for (int q = 0; q < XA_WAVES; ++q) M = fmaxf(M, wm[q]);
+    float den = 0.f, e[XA_WAVES];
+#pragma unroll
+    for (int q = 0; q < XA_WAVES; ++q) {
+        e[q] = wm[q] == -INFINITY ? 0.f : expf(wm[q] - M);
+        den += e[q] * wl[q];
     }
+    float *pp = p.part + ((size_t)b * XA_SPLITS + sp) * XA_PART;
+    for (int kx = tid; kx < D; kx += XA_THREADS) {
+        float num = 0.f;
+#pragma unroll
+        for (int q = 0; q < XA_WAVES; ++q) num += e[q] * wo[q][kx];
+        pp[4 + kx] = num;
+    }
+    if (tid == 0) { pp[0] = M; pp[1] = den; }
 }
 
 hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
-    if (!p.x || !p.x_out || !p.lnw || !p.kp || !p.vp || !p.T || p.Tmax < 1 || p.Tmax > TMAX_LIMIT) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(xa_fused_kernel, dim3(D / 64, B), dim3(XA_THREADS), 0, s, p);
+    if (!p.x || !p.part || !p.lnw || !p.kp || !p.vp || !p.T || p.Tmax < 1 || p.Tmax > TMAX_LIMIT) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xa_part_kernel, dim3(XA_SPLITS, B), dim3(XA_THREADS), 0, s, p);
     return hipGetLastError();
 }
 
@@ -333,6 +338,8 @@ static bool gemv_args_ok(const GemvP &p) {
     if (!p.W || p.N <= 0) return false;
     bool ok = true;
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
+    if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
+    if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
@@ -361,8 +368,9 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
 #define MP_DECODE_OPS(NB)                                                                                        \
     hipError_t op_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
-    hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_PLAIN, EPI_RESID>(p, s); }    \
+    hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_SA_MERGE, EPI_RESID>(p, s); } \
     hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_GELU>(p, s); }            \
+    hipError_t op_ff1x_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_XA_LN, EPI_GELU>(p, s); }        \
     hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \
     hipError_t op_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_BIAS>(p, s); }         \
     hipError_t op_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
@@ -385,9 +393,9 @@ hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 
 
 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
-    if (!p.q || !p.kc || !p.vc || !p.pos || !p.out || p.max_seq < 1 || p.max_seq > NCH_MAX * SA_CHUNK)
+    if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || p.max_seq < 1 || p.max_seq > NCH_MAX * SA_CHUNK)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sa_attn_kernel, dim3(NH, B), dim3(SA_THREADS), 0, s, p);
+    hipLaunchKernelGGL(sa_attn_kernel, dim3(NH, SA_SPLITS, B), dim3(SA_THREADS), 0, s, p);
     return hipGetLastError();
 }
 

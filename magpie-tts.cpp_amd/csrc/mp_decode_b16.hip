@@ -129,6 +129,8 @@ static bool b16_args_ok(const GemvP &p) {
     if (!p.Wb || p.N <= 0) return false;
     bool ok = true;
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
+    if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
+    if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
@@ -154,8 +156,8 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
 #define MP_B16_OPS(NB)                                                                                                  \
     hipError_t b16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
-    hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_PLAIN, EPI_RESID>(p, s); }      \
-    hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_GELU>(p, s); }            \
+    hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }   \
+    hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU>(p, s); }         \
     hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \
     hipError_t b16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
     hipError_t b16_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \

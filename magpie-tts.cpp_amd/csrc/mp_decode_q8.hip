@@ -119,6 +119,8 @@ static bool q8_args_ok(const GemvP &p) {
     if (!p.Wq || !p.Wd || p.N <= 0) return false;
     bool ok = true;
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
+    if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
+    if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
@@ -148,7 +150,7 @@ static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
 #define MP_Q8_OPS(NB)                                                                                                  \
     hipError_t q8_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t q8_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_QKV>(p, s); }             \
-    hipError_t q8_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_PLAIN, EPI_RESID>(p, s); }      \
+    hipError_t q8_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_SA_MERGE, EPI_RESID>(p, s); }      \
     hipError_t q8_xq_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_STORE>(p, s); }            \
     hipError_t q8_xo_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, DXA, 8, PRO_PLAIN, EPI_ADD_STORE>(p, s); }   \
     hipError_t q8_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_BIAS>(p, s); }         \

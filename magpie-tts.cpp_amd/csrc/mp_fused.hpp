@@ -166,10 +166,94 @@ __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos,
     return code;
 }
 
+// Merge of NS partial softmax states (m_s, l_s, O_s relative to m_s):
+// sum_s e^{m_s - M} O_s / sum_s e^{m_s - M} l_s, M = max_s m_s. An empty split has
+// m = -inf, l = 0, O = 0. `pp` points at split 0's state, states `stride` apart,
+// O at +4; returns the four consecutive outputs starting at offset `k` of O.
+template <int NS>
+__device__ __forceinline__ float4 merge_states(const float *pp, int stride, int k) {
+    float ms[NS], ls[NS];
+    float4 os[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        ms[s] = pp[(size_t)s * stride];
+        ls[s] = pp[(size_t)s * stride + 1];
+        os[s] = *(const float4 *)(pp + (size_t)s * stride + 4 + k);
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) M = fmaxf(M, ms[s]);
+    float den = 0.f;
+    float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const float e = ms[s] == -INFINITY ? 0.f : expf(ms[s] - M);
+        den += e * ls[s];
+        num.x += e * os[s].x; num.y += e * os[s].y; num.z += e * os[s].z; num.w += e * os[s].w;
+    }
+    return make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
+}
+
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
     const int tid = threadIdx.x;
-    if constexpr (PRO == PRO_PLAIN) {
+    if constexpr (PRO == PRO_SA_MERGE) {
+        // self-attention output of every head: its SA_SPLITS key-split states merged
+        static_assert(K == D, "SA output is d_model wide");
+        for (int e = tid; e < NB * (K / 4); e += MP_BLOCK) {
+            const int b = e / (K / 4), k = (e % (K / 4)) * 4, h = k / DH;
+            const float4 v = merge_states<SA_SPLITS>(p.part + ((size_t)(b * NH + h) * SA_SPLITS) * SA_PART, SA_PART, k % DH);
+            *(float4 *)(act + b * K + k) = v;
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_XA_LN) {
+        // x2 = x + XA (its XA_SPLITS text-key split states merged, magpie.cpp:3519); block 0
+        // stores x2 (the FFN's residual input); act = LN(x2) * lnw with the same one-wave
+        // DPP statistics as PRO_LN, so batch 1 and batched prologues agree bit for bit
+        static_assert(K == D, "XA output is d_model wide");
+        for (int e = tid; e < NB * (K / 4); e += MP_BLOCK) {
+            const int b = e / (K / 4), k = (e % (K / 4)) * 4;
+            const float4 a = merge_states<XA_SPLITS>(p.part + (size_t)b * XA_SPLITS * XA_PART, XA_PART, k);
+            const float4 xv = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
+            const float4 x2 = make_float4(a.x + xv.x, a.y + xv.y, a.z + xv.z, a.w + xv.w);
+            *(float4 *)(act + b * K + k) = x2;
+            if (blockIdx.x == 0) *(float4 *)(p.xres + (size_t)b * D + k) = x2;
+        }
+        lds_sync();
+        const int lane = tid & 63, w = tid >> 6;
+        constexpr int PER = K / 64;
+        if constexpr (NB == 1) {
+            constexpr int Q = PER / MP_NWAVES;
+            float v[PER];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) v[i] = act[lane + 64 * i];
+            float mean, var;
+            wave_meanvar<PER>(v, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            lds_sync();  // every wave has read the row before any overwrites its quarter
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                if (i / Q != w) continue;
+                const int k = lane + 64 * i;
+                act[k] = ((v[i] - mean) * rstd) * p.lnw[k];
+            }
+        } else {
+            for (int b = w; b < NB; b += MP_NWAVES) {  // a wave owns its slots' rows
+                float v[PER];
+#pragma unroll
+                for (int i = 0; i < PER; ++i) v[i] = act[b * K + lane + 64 * i];
+                float mean, var;
+                wave_meanvar<PER>(v, mean, var);
+                const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int k = lane + 64 * i;
+                    act[b * K + k] = ((v[i] - mean) * rstd) * p.lnw[k];
+                }
+            }
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_PLAIN) {
         for (int b = 0; b < NB; ++b)
             for (int k = tid * 4; k < K; k += MP_BLOCK * 4)
                 *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);

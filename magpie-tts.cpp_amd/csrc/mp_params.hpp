@@ -20,6 +20,11 @@ constexpr int CTX = 110;      // baked context frames         (magpie.h:67)
 constexpr int SA_CHUNK = 64;  // cache rows are allocated in whole 64-key chunks
 constexpr int NCH_MAX = 16;   // -> max_seq <= 1024 (reference: 626, magpie.cpp:4077)
 constexpr int TMAX_LIMIT = 1024;  // text tokens per utterance (LDS score buffer)
+// split-K decode attention: partial softmax states, merged in the next op's prologue
+constexpr int SA_SPLITS = 4;        // key splits of each SA head (sa_attn_kernel)
+constexpr int SA_PART = 4 + DH;     // per (slot, head, split): m, l, -, -, O[64] (unnormalised)
+constexpr int XA_SPLITS = 4;        // text-key splits of the fused cross-attention (xa_part_kernel)
+constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
 enum Pro {
@@ -31,6 +36,9 @@ enum Pro {
     PRO_LTARG_LN = 8,   // code_{cb-1} = masked argmax(logits); X = P[cb-1][code] + lt_pos[cb];
                         // act = LN(X)*lnw, with P[c][v] = in_proj(audio_emb[c][v]) + b
                         // precomputed at load (1274-1313 depend only on (c, v))
+    PRO_SA_MERGE = 9,   // act = SA output: the SA_SPLITS partial softmax states of each head merged
+    PRO_XA_LN = 10,     // x2 = src + XA output (XA_SPLITS partial states merged), block 0 stores
+                        // x2 to xres; act = LN(x2)*lnw              (3513-3525)
 };
 enum Epi {
     EPI_STORE = 0,      // out = v
@@ -116,6 +124,7 @@ struct GemvP {
     // early exit once every slot is done (count >= nslots)
     const int *ndone;
     int nslots;
+    const float *part;   // PRO_SA_MERGE: [B][NH][SA_SPLITS][SA_PART]; PRO_XA_LN: [B][XA_SPLITS][XA_PART]
 };
 
 struct FinP {
@@ -134,7 +143,8 @@ struct FinP {
 // (= o_net(attn(q_net(LN(x)), K, V)), magpie.cpp:1713-1767, by associativity).
 struct XaP {
     const float *x;        // [B][768] residual in
-    float *x_out;          // [B][768] = x + XA(x) (separate buffer: every workgroup reads all of x)
+    float *part;           // [B][XA_SPLITS][XA_PART] partial softmax states over text-key splits
+                           // (merged + added to x in the next op's PRO_XA_LN prologue)
     const float *lnw;      // norm_xattn_query
     float eps;
     const float *kp, *vp;  // K', V': [B][L][Tmax][768]
@@ -147,7 +157,8 @@ struct AttnP {  // decode self-attention (one query per utterance)
     const float *kc, *vc;
     int layer, nlayers, max_seq;
     const int *pos;
-    float *out;          // [B][768] attention output
+    float *part;         // [B][NH][SA_SPLITS][SA_PART] partial softmax states over key splits
+                         // (merged in the O-projection's PRO_SA_MERGE prologue)
 };
 
 }  // namespace mp

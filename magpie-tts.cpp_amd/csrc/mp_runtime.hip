@@ -31,6 +31,7 @@ using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
 #define MP_DECL_OPS(NB)                                                                                     \
     hipError_t op_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t op_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t op_oproj_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);            \
+    hipError_t op_ff1x_##NB(const GemvP &, hipStream_t);                                                                \
     hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
     hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_lt_ag_##NB(const GemvP &, hipStream_t);                                                              \
@@ -75,12 +76,13 @@ hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 namespace mp {
 
-struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
-#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff2_##NB, \
+// ff1: LN(x2) prologue (x2 materialised: Q8 unfused XA); ff1x: the fused XA's split states merged into x2 first
+struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
+#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_ag_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
 static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
-#define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, b16_ff1_##NB, b16_ff2_##NB, \
+#define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, nullptr, b16_ff1_##NB, b16_ff2_##NB, \
                            op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_ag_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
                            b16_lt_d_##NB, b16_lt_e_##NB }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
@@ -174,6 +176,7 @@ struct mp_dev {
     float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *sa_out = nullptr,
           *h = nullptr, *hidden = nullptr;
     float *xqb = nullptr, *xab = nullptr;  // Q8 mode (unfused XA): q_net output, attention output [NB][128]
+    float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
@@ -560,6 +563,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
     A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(sa_out, NB * 768);
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(xab, NB * 128);
+    A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
@@ -631,7 +635,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
                           (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
         }
         // self-attention over the cache, one workgroup per (head, slot) (3457-3476)
-        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->sa_out};
+        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->sa_part};
         if (record) {
             mp::OpRec r{};
             r.name = "sa_attn"; r.kind = mp::K_ATTN; r.a = a; r.B = NB;
@@ -641,7 +645,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         HIPCHK(mp::op_sa_attn(a, NB, s));
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
-        g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.src = dev->sa_out; g.src_ld = 768;
+        g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.part = dev->sa_part;
         g.Wq = W.o8.q; g.Wd = W.o8.d;
         if ((rc = run("oproj", W.o8 ? tq.oproj : tb.oproj, g, (W.o8 ? Fq : F) * (768.0 * 768) + A * act * (768 * 3))) !=
             MP_OK)
@@ -667,19 +671,27 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             if ((rc = run("xo", tq.xo, g, Fq * (768.0 * 128) + A * act * (128 + 2 * 768))) != MP_OK) return rc;
         } else {
             // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
-            mp::XaP xp{dev->x, dev->x2, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
+            mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
             if (record) {
                 mp::OpRec r{};
                 r.name = "xa"; r.kind = mp::K_XA; r.x = xp; r.B = NB;
-                r.bytes = A * act * (768.0 * 2 + 2.0 * 768 * dev->Tmax);
+                r.bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
                 dev->ops.push_back(r);
             }
             HIPCHK(mp::op_xa(xp, NB, s));
         }
         // LN + FFN up + GELU (1796-1799)
         g = gemv_base(dev); g.layer = l;
-        g.W = W.ff1; g.Wb = b16 ? m.pk_ff1[l] : nullptr; g.N = 3072; g.lnw = W.norm_ff; g.src = dev->x2; g.src_ld = 768; g.out = dev->h; g.out_ld = 3072;
-        if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
+        g.W = W.ff1; g.Wb = b16 ? m.pk_ff1[l] : nullptr; g.N = 3072; g.lnw = W.norm_ff; g.out = dev->h; g.out_ld = 3072;
+        if (W.xq8) {  // x2 materialised by the Q8 o_net
+            g.src = dev->x2; g.src_ld = 768;
+            if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
+        } else {      // x2 = x + merged XA split states, stored by block 0 for the FFN residual
+            g.src = dev->x; g.src_ld = 768; g.part = dev->xa_part; g.xres = dev->x2;
+            if ((rc = run("ff1", tb.ff1x, g,
+                          F * (3072.0 * 768) + A * act * (768 * 2 + 3072 + mp::XA_SPLITS * mp::XA_PART))) != MP_OK)
+                return rc;
+        }
         // FFN down + residual (1805, 3525): x = x2 + W2 h
         g = gemv_base(dev); g.layer = l;
         g.W = W.ff2; g.Wb = b16 ? m.pk_ff2[l] : nullptr; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.out = dev->x; g.out_ld = 768; g.addsrc = dev->x2;
@@ -1292,9 +1304,47 @@ double mp_hip_op_bytes(mp_dev *dev, int op) {
         // live cache length of slot 0 after the run: keys 0..pos
         int pos = 0;
         hipMemcpy(&pos, dev->pos, 4, hipMemcpyDeviceToHost);
-        return 4.0 * dev->NB * ((double)(pos + 1) * 768 * 2 + 768 * 2);  // K, V rows + q in + out
+        // K, V rows + q in + the split states out
+        return 4.0 * dev->NB * ((double)(pos + 1) * 768 * 2 + 768 + mp::NH * mp::SA_SPLITS * mp::SA_PART);
     }
     return r.bytes;
+}
+
+int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
+    if (!dev || !avg_us || iters < 1) return MP_ERR_ARG;
+    if (!dev->batch_ready || dev->ops.empty())
+        return fail(dev, MP_ERR_STATE, "mp_hip_profile_ops needs a decoded batch (mp_hip_decode first)");
+    HIPCHK(hipSetDevice(dev->device));
+    const int n = (int)dev->ops.size();
+    std::vector<hipEvent_t> ev(2 * (size_t)n);
+    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+    std::vector<double> sum(n, 0.0);
+    int rc = MP_OK;
+    for (int it = 0; it < iters && rc == MP_OK; ++it) {
+        for (int i = 0; i < n; ++i) {
+            const mp::OpRec &r = dev->ops[i];
+            HIPCHK(hipEventRecord(ev[2 * i], dev->stream));
+            hipError_t e = hipErrorInvalidValue;
+            switch (r.kind) {
+            case mp::K_GEMV: e = r.fn(r.g, dev->stream); break;
+            case mp::K_ATTN: e = mp::op_sa_attn(r.a, r.B, dev->stream); break;
+            case mp::K_XA: e = mp::op_xa(r.x, r.B, dev->stream); break;
+            case mp::K_ROWXA: e = mp::pre_row_xa(r.rx, dev->stream); break;
+            case mp::K_FIN: e = mp::op_finalize(r.f, r.B, dev->stream); break;
+            }
+            HIPCHK(e);
+            HIPCHK(hipEventRecord(ev[2 * i + 1], dev->stream));
+        }
+        HIPCHK(hipStreamSynchronize(dev->stream));
+        for (int i = 0; i < n; ++i) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+            sum[i] += ms;
+        }
+    }
+    for (auto &e : ev) hipEventDestroy(e);
+    for (int i = 0; i < n; ++i) avg_us[i] = (float)(sum[i] * 1000.0 / iters);
+    return rc;
 }
 
 int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
@@ -1307,9 +1357,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
         if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
         if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
         if (r.kind == mp::K_XA) {
-            mp::XaP xp = r.x;
-            xp.x_out = dev->q;  // scratch: timing must not disturb the residual stream
-            return mp::op_xa(xp, r.B, dev->stream);
+            return mp::op_xa(r.x, r.B, dev->stream);  // rewrites this layer's split states only
         }
         if (r.kind == mp::K_ROWXA) return mp::pre_row_xa(r.rx, dev->stream);
         return hipErrorInvalidValue;

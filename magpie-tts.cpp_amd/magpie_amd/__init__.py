@@ -77,6 +77,7 @@ SYMBOLS = [
     ("mp_hip_op_name", ctypes.c_char_p, [_P, _I]),
     ("mp_hip_op_bytes", ctypes.c_double, [_P, _I]),
     ("mp_hip_time_op", _I, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+    ("mp_hip_profile_ops", _I, [_P, _I, _P]),
     ("mp_tokenizer_load", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
     ("mp_tokenize", _I, [_P, ctypes.c_char_p, _P, _I]),
     ("mp_tokenizer_free", None, [_P]),
@@ -265,6 +266,13 @@ class Device:
 
     def op_bytes(self, op: int) -> float:
         return float(self.lib.mp_hip_op_bytes(self.h, op))
+
+    def profile_ops(self, iters: int = 32) -> np.ndarray:
+        """In-situ mean launch time (us) of every op of the decode iteration."""
+        n = self.lib.mp_hip_num_ops(self.h)
+        out = np.zeros(max(n, 1), np.float32)
+        self._check(self.lib.mp_hip_profile_ops(self.h, iters, out.ctypes.data))
+        return out[:n]
 
     def time_op(self, op: int, reps: int = 50) -> float:
         us = ctypes.c_float()

@@ -34,9 +34,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     constexpr int VW = K >= 256 ? 4 : K / 64;
     constexpr int NV = K / (64 * VW);
     using VT = typename vecf<VW>::T;
-    constexpr int SC = (PRO == PRO_LT_ATTN) ? 16
-                       : (PRO == PRO_LTARG_LN) ? (NB < MP_NWAVES ? NB : MP_NWAVES) * 2 * VCB
-                       : 1;
+    constexpr int SC = pro_scratch<NB, PRO>();
     __shared__ __attribute__((aligned(16))) float act[NB * K];
     __shared__ float red[8];
     __shared__ float sc[SC];

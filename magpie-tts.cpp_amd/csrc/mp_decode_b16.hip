@@ -42,7 +42,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     constexpr int KP = K + 8;  // padded bf16 row: rows land 16 B apart in the banks
     constexpr int NR = NB + 1;  // NB activation rows + one zero row for the unused MFMA columns
     constexpr bool STAGE = PRO != PRO_PLAIN;
-    constexpr int SC = (PRO == PRO_LT_ATTN) ? 16 : (PRO == PRO_LTARG_LN) ? (NB < MP_NWAVES ? NB : MP_NWAVES) * 2 * VCB : 1;
+    constexpr int SC = pro_scratch<NB, PRO>();
     __shared__ __attribute__((aligned(16))) float actf[STAGE ? NB * K : 4];
     __shared__ __attribute__((aligned(16))) unsigned short actb[NR * KP];
     __shared__ __attribute__((aligned(16))) floatx4 part[MP_NWAVES][64];

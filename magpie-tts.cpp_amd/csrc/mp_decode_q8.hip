@@ -39,9 +39,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_q8_kernel(GemvP p) {
     constexpr int J = R * CPR / 64;
     static_assert(R * CPR % 64 == 0, "a wave's rows must fill whole wave-instructions");
     static_assert(R * NB <= 64, "one lane per output");
-    constexpr int SC = (PRO == PRO_LT_ATTN) ? 16
-                       : (PRO == PRO_LTARG_LN) ? (NB < MP_NWAVES ? NB : MP_NWAVES) * 2 * VCB
-                       : 1;
+    constexpr int SC = pro_scratch<NB, PRO>();
     __shared__ __attribute__((aligned(16))) float act[NB * K];
     __shared__ __attribute__((aligned(16))) signed char actq[NB * K];
     __shared__ float actd[NB * NBLK];

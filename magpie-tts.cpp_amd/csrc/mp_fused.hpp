@@ -57,16 +57,20 @@ __device__ __forceinline__ int block_masked_argmax(const GemvP &p, int b, float 
 // k-th key, a ballot compaction gathers the k candidates into LDS, a counting rank
 // orders them, lane 0 runs the two sequential float loops. scratch: 2*VCB floats.
 // `stream` is the batch slot; the draw stream is cfg->stream_base + slot.
-__device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos, int audio_eos, const Sampling &smp,
-                         int stream, int step, int cb, float *scratch, int &amax) {
+constexpr int PICK_R = (VCB + 63) / 64;  // logits per lane
+__device__ __forceinline__ void load_logits(const float *lg, float (&lv)[PICK_R]) {
     const int lane = threadIdx.x & 63;
-    constexpr int R = (VCB + 63) / 64;
-    float lv[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < PICK_R; ++r) {
         const int i = lane + 64 * r;
         lv[r] = i < VCB ? lg[i] : -INFINITY;
     }
+}
+// wave_pick on logits already loaded by load_logits (lv is modified)
+__device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audio_bos, int audio_eos,
+                                  const Sampling &smp, int stream, int step, int cb, float *scratch, int &amax) {
+    const int lane = threadIdx.x & 63;
+    constexpr int R = PICK_R;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
 #pragma unroll
@@ -165,45 +169,86 @@ __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos,
     __builtin_amdgcn_wave_barrier();
     return code;
 }
+__device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos, int audio_eos, const Sampling &smp,
+                                int stream, int step, int cb, float *scratch, int &amax) {
+    float lv[PICK_R];
+    load_logits(lg, lv);
+    return wave_pick_v(lv, forbid_eos, audio_bos, audio_eos, smp, stream, step, cb, scratch, amax);
+}
 
-// Merge of NS partial softmax states (m_s, l_s, O_s relative to m_s):
-// sum_s e^{m_s - M} O_s / sum_s e^{m_s - M} l_s, M = max_s m_s. An empty split has
-// m = -inf, l = 0, O = 0. `pp` points at split 0's state, states `stride` apart,
-// O at +4; returns the four consecutive outputs starting at offset `k` of O.
+// LDS scratch (floats) a prologue needs besides the activation rows
+template <int NB, int PRO>
+constexpr int pro_scratch() {
+    return PRO == PRO_LT_ATTN ? 16
+           : PRO == PRO_LTARG_LN ? (NB < MP_NWAVES ? NB : MP_NWAVES) * 2 * VCB
+           : PRO == PRO_SA_MERGE ? NB * NH * (SA_SPLITS + 1)
+           : PRO == PRO_XA_LN ? NB * (XA_SPLITS + 1)
+           : 1;
+}
+
+// Weights of NS partial softmax states (m_s, l_s, O_s relative to m_s) of `nq`
+// groups (group q's split s at pp + (q*NS + s)*stride): e_s = exp(m_s - M),
+// M = max_s m_s, den = sum_s e_s l_s (an empty split has m = -inf, l = 0, O = 0);
+// sc[q*(NS+1) + s] = e_s, sc[q*(NS+1) + NS] = den. The merged output is
+// sum_s e_s O_s / den. Computed once per group, not per element.
 template <int NS>
-__device__ __forceinline__ float4 merge_states(const float *pp, int stride, int k) {
-    float ms[NS], ls[NS];
-    float4 os[NS];
+__device__ __forceinline__ void merge_weights(const float *pp, int stride, int nq, float *sc) {
+    for (int q = threadIdx.x; q < nq; q += MP_BLOCK) {
+        float ms[NS], ls[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        ms[s] = pp[(size_t)s * stride];
-        ls[s] = pp[(size_t)s * stride + 1];
-        os[s] = *(const float4 *)(pp + (size_t)s * stride + 4 + k);
+        for (int s = 0; s < NS; ++s) {
+            ms[s] = pp[((size_t)q * NS + s) * stride];
+            ls[s] = pp[((size_t)q * NS + s) * stride + 1];
+        }
+        float M = -INFINITY;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) M = fmaxf(M, ms[s]);
+        float den = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const float e = ms[s] == -INFINITY ? 0.f : expf(ms[s] - M);
+            sc[q * (NS + 1) + s] = e;
+            den += e * ls[s];
+        }
+        sc[q * (NS + 1) + NS] = den;
     }
-    float M = -INFINITY;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) M = fmaxf(M, ms[s]);
-    float den = 0.f;
-    float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        const float e = ms[s] == -INFINITY ? 0.f : expf(ms[s] - M);
-        den += e * ls[s];
-        num.x += e * os[s].x; num.y += e * os[s].y; num.z += e * os[s].z; num.w += e * os[s].w;
-    }
-    return make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
 }
 
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
     const int tid = threadIdx.x;
+    constexpr int IB = 4;  // merge items per thread with all their loads in flight
     if constexpr (PRO == PRO_SA_MERGE) {
         // self-attention output of every head: its SA_SPLITS key-split states merged
         static_assert(K == D, "SA output is d_model wide");
-        for (int e = tid; e < NB * (K / 4); e += MP_BLOCK) {
-            const int b = e / (K / 4), k = (e % (K / 4)) * 4, h = k / DH;
-            const float4 v = merge_states<SA_SPLITS>(p.part + ((size_t)(b * NH + h) * SA_SPLITS) * SA_PART, SA_PART, k % DH);
-            *(float4 *)(act + b * K + k) = v;
+        merge_weights<SA_SPLITS>(p.part, SA_PART, NB * NH, sc);
+        lds_sync();
+        constexpr int ITEMS = NB * (K / 4);
+        for (int base = 0; base < ITEMS; base += MP_BLOCK * IB) {
+            float4 o[IB][SA_SPLITS];
+#pragma unroll
+            for (int u = 0; u < IB; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                if (e >= ITEMS) break;
+                const int b = e / (K / 4), k = (e % (K / 4)) * 4, q = b * NH + k / DH;
+#pragma unroll
+                for (int s2 = 0; s2 < SA_SPLITS; ++s2)
+                    o[u][s2] = *(const float4 *)(p.part + ((size_t)q * SA_SPLITS + s2) * SA_PART + 4 + k % DH);
+            }
+#pragma unroll
+            for (int u = 0; u < IB; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                if (e >= ITEMS) break;
+                const int b = e / (K / 4), k = (e % (K / 4)) * 4, q = b * NH + k / DH;
+                float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int s2 = 0; s2 < SA_SPLITS; ++s2) {
+                    const float w = sc[q * (SA_SPLITS + 1) + s2];
+                    num.x += w * o[u][s2].x; num.y += w * o[u][s2].y; num.z += w * o[u][s2].z; num.w += w * o[u][s2].w;
+                }
+                const float den = sc[q * (SA_SPLITS + 1) + SA_SPLITS];
+                *(float4 *)(act + b * K + k) = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
+            }
         }
         lds_sync();
     } else if constexpr (PRO == PRO_XA_LN) {
@@ -211,13 +256,38 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         // stores x2 (the FFN's residual input); act = LN(x2) * lnw with the same one-wave
         // DPP statistics as PRO_LN, so batch 1 and batched prologues agree bit for bit
         static_assert(K == D, "XA output is d_model wide");
-        for (int e = tid; e < NB * (K / 4); e += MP_BLOCK) {
-            const int b = e / (K / 4), k = (e % (K / 4)) * 4;
-            const float4 a = merge_states<XA_SPLITS>(p.part + (size_t)b * XA_SPLITS * XA_PART, XA_PART, k);
-            const float4 xv = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
-            const float4 x2 = make_float4(a.x + xv.x, a.y + xv.y, a.z + xv.z, a.w + xv.w);
-            *(float4 *)(act + b * K + k) = x2;
-            if (blockIdx.x == 0) *(float4 *)(p.xres + (size_t)b * D + k) = x2;
+        merge_weights<XA_SPLITS>(p.part, XA_PART, NB, sc);
+        lds_sync();
+        constexpr int ITEMS = NB * (K / 4);
+        for (int base = 0; base < ITEMS; base += MP_BLOCK * IB) {
+            float4 o[IB][XA_SPLITS], xv[IB];
+#pragma unroll
+            for (int u = 0; u < IB; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                if (e >= ITEMS) break;
+                const int b = e / (K / 4), k = (e % (K / 4)) * 4;
+                xv[u] = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
+#pragma unroll
+                for (int s2 = 0; s2 < XA_SPLITS; ++s2)
+                    o[u][s2] = *(const float4 *)(p.part + ((size_t)b * XA_SPLITS + s2) * XA_PART + 4 + k);
+            }
+#pragma unroll
+            for (int u = 0; u < IB; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                if (e >= ITEMS) break;
+                const int b = e / (K / 4), k = (e % (K / 4)) * 4;
+                float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int s2 = 0; s2 < XA_SPLITS; ++s2) {
+                    const float w = sc[b * (XA_SPLITS + 1) + s2];
+                    num.x += w * o[u][s2].x; num.y += w * o[u][s2].y; num.z += w * o[u][s2].z; num.w += w * o[u][s2].w;
+                }
+                const float den = sc[b * (XA_SPLITS + 1) + XA_SPLITS];
+                const float4 x2 = make_float4(num.x / den + xv[u].x, num.y / den + xv[u].y, num.z / den + xv[u].z,
+                                              num.w / den + xv[u].w);
+                *(float4 *)(act + b * K + k) = x2;
+                if (blockIdx.x == 0) *(float4 *)(p.xres + (size_t)b * D + k) = x2;
+            }
         }
         lds_sync();
         const int lane = tid & 63, w = tid >> 6;
@@ -384,28 +454,54 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LTARG_LN && NB >= 2) {
+        // wave w owns slots w, w+4, ...: all their logits are loaded before the first pick,
+        // all table rows gathered before the first LayerNorm (one latency per phase)
         const int lane = tid & 63, w = tid >> 6;
-        for (int b = w; b < NB; b += MP_NWAVES) {
+        constexpr int SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
+        float cur[PICK_R], nxt[PICK_R];
+        if (w < NB) load_logits(p.logits + (size_t)w * VCB, cur);
+        unsigned long long codes = 0ull;  // 16 bits per slot of this wave (codes < 2048)
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b >= NB) break;  // wave-uniform
+            const int bn = b + MP_NWAVES;
+            if (bn < NB) load_logits(p.logits + (size_t)bn * VCB, nxt);  // next slot's logits in flight
             int amax;
-            const int code = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos,
-                                       p.smp, b, p.step[b], p.cb - 1, sc + w * 2 * VCB, amax);
+            const int code = wave_pick_v(cur, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos, p.smp, b,
+                                         p.step[b], p.cb - 1, sc + w * 2 * VCB, amax);
             if (blockIdx.x == 0 && lane == 0) {
                 p.codes_cur[b * NCB + p.cb - 1] = code;
                 if (amax == p.audio_eos) p.smp.argeos[b] = 1;
                 if (p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
             }
-            float X[4];
+            codes |= (unsigned long long)code << (16 * j);
+#pragma unroll
+            for (int r = 0; r < PICK_R; ++r) cur[r] = nxt[r];
+        }
+        int code[SPW];
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) code[j] = (int)((codes >> (16 * j)) & 0xffffull);
+        float X[SPW][4];
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int k = lane + 64 * i;
-                X[i] = p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
-                if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X[i];
+                X[j][i] = p.ptab[((size_t)(p.cb - 1) * VCB + code[j]) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
             }
+        }
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b >= NB) continue;
+            if (blockIdx.x == 0)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) p.ltX[(size_t)b * LTD + lane + 64 * i] = X[j][i];
             float mean, var;
-            wave_block_meanvar<1>(X, mean, var);
+            wave_block_meanvar<1>(X[j], mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[j][i] - mean) * rstd) * p.lnw[lane + 64 * i];
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LT_ATTN && NB >= 2) {

@@ -41,6 +41,7 @@ CODEC_FLOP_PER_FRAME = 2.447e9  # 1.2234 G MAC per codec frame
 CODEC_CHUNK = 32  # the CLI decodes stateless 32-frame chunks (magpie-tts.cpp:181-206)
 FRAMES = 256
 TEXT_TOKENS = 64
+PMC_TRAFFIC = "r01_pmc_traffic.json"  # per-op HBM bytes of the N=1 workload (tools_dev/pmc_parse.py)
 
 
 def decoder_bytes_per_frame(B: int, L_mean: float, T: int, dec_layers: int = 12, weights: str = "f32") -> float:
@@ -262,6 +263,17 @@ def main() -> None:
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "algorithmic_bytes_per_launch": rec["bytes"], "avg_launch_us": rec["avg_us"],
                     "timing": "in-situ hipEvent pair per launch (mp_hip_profile_ops)"}
+        # HBM bytes per launch from the committed PMC passes (tools_dev/pmc_traffic.sh +
+        # pmc_parse.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE x2 on gfx950)
+        pmc_path = os.path.join(REPO, "profiles", PMC_TRAFFIC)
+        if args.weights == "f32" and B == 1 and os.path.exists(pmc_path):
+            pmc = json.load(open(pmc_path))["ops"].get(name)
+            if pmc:
+                roofline["traffic"] = pmc["traffic_bytes"]
+                roofline["traffic_source"] = f"profiles/{PMC_TRAFFIC} ({pmc['kernel']})"
+                for n, r in op_table.items():
+                    if n in json.load(open(pmc_path))["ops"]:
+                        r["pmc_traffic_bytes"] = json.load(open(pmc_path))["ops"][n]["traffic_bytes"]
 
     # ---- CPU baseline: the oracle (C restatement, f32 accumulation) on the host cores
     cpu = None

@@ -109,8 +109,9 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
         float4 k4[SA_IF], v4[SA_IF];
 #pragma unroll
         for (int u = 0; u < SA_IF; ++u) {
-            // rows < max_seq are always valid memory: no load waits for the mask
-            const int j = min(j0 + 4 * (w + SA_WAVES * (r0 + u)) + kk, p.max_seq - 1);
+            // keys past the split re-read its last row (an L1/L2 hit, no extra HBM
+            // traffic); rows < max_seq are valid memory: no load waits for the mask
+            const int j = min(j0 + 4 * (w + SA_WAVES * (r0 + u)) + kk, max(j1 - 1, 0));
             k4[u] = *(const float4 *)(p.kc + base + (size_t)j * D);
             v4[u] = *(const float4 *)(p.vc + base + (size_t)j * D);
         }

@@ -14,15 +14,22 @@
 //    step is 64 contiguous bytes, so an input tile is staged once into LDS (with
 //    its causal halo) as f16 and reused by all ks taps -> the B fragment of every
 //    tap is one ds_read_b128.
-//  * The op before each conv is fused into its operand loader: HalfSnake
-//    (nano-codec.cpp:376-426), the FSQ dequant (721-752) for the pre-conv, and the
-//    3-branch ResLayer mean (619-641) for the next stage's input. Bias and the
-//    residual add (568-599) are fused into the epilogue. The 3 HiFiGAN branches
-//    of a ResLayer run in one launch (grid.z).
+//  * Each conv's input activation is produced ONCE, by the epilogue of the op
+//    that writes its input: HalfSnake (nano-codec.cpp:376-426) with the
+//    consumer's alpha, rounded to f16 exactly as ggml's F16 im2col rounds it, is
+//    stored next to (or instead of) the f32 output, so a conv's operand loader is
+//    a plain 16-byte f16 copy into LDS (no sinf per M-tile and per halo row). The
+//    FSQ dequant (721-752) stays in the pre-conv's loader. Bias and the residual
+//    add (568-599) are fused into the epilogue. The 3 HiFiGAN branches of a
+//    ResLayer run in one launch (grid.z). The A fragments of all taps of a
+//    32-channel block are issued before the block's input rows are staged.
 //  * Weight-norm is already folded in the GGUF (convert_codec_to_gguf.py:169-221);
 //    weights are re-laid out once at init as f16 [Cout_p][tap][Cin_p].
-//  * The grouped ConvTranspose1d (481-565) is 4 MACs per output: an elementwise
-//    f32 kernel (ggml's conv_transpose_1d with F32 weights is an f32 dot, A.7).
+//  * The grouped ConvTranspose1d (481-565) is 4 MACs per output: an f32 kernel
+//    (ggml's conv_transpose_1d with F32 weights is an f32 dot, A.7) with one
+//    thread per (input step, group): the 3-branch ResLayer mean (619-641) and
+//    HalfSnake of its 4 inputs are computed once and reused by its s outputs;
+//    it emits the k=0 in_conv activations of the 3 branches.
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -46,23 +53,23 @@ constexpr int KS[3] = {3, 7, 11};
 constexpr int DIL[3] = {1, 3, 5};
 constexpr int HOP = 1024;
 
-enum InMode { IN_PLAIN = 0, IN_FSQ = 1, IN_AVG3 = 2 };
+enum InMode { IN_F16 = 0, IN_FSQ = 1 };
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 struct ConvP {
     // per-branch (grid.z) operands
-    const _Float16 *W[3];   // [Coutp][ks][Cinp] f16
-    const float *bias[3];   // [Coutp] (zero padded)
-    const float *alpha[3];  // HalfSnake alpha (nullptr: no activation)
-    const float *x[3];      // input [chunk][T][Cinp]
-    float *out[3];          // output [chunk][T][Coutp]
-    const float *resid[3];  // optional residual [chunk][T][Coutp]
+    const _Float16 *W[3];    // [Coutp][ks][Cinp] f16
+    const float *bias[3];    // [Coutp] (zero padded)
+    const _Float16 *x[3];    // input activation [chunk][T][Cinp] f16 (already HalfSnake'd)
+    float *out[3];           // optional f32 output [chunk][T][Coutp]
+    const float *resid[3];   // optional residual [chunk][T][Coutp]
+    _Float16 *act[3];        // optional f16 HalfSnake(output) for the next conv [chunk][T][Coutp]
+    const float *act_alpha[3];
     int ks[3];
-    const float *xa, *xb;   // IN_AVG3: second and third branch inputs (x[] = first)
-    const int *codes;       // IN_FSQ: [chunk][8][T]
-    int n_snake, cin_real;
+    const int *codes;        // IN_FSQ: [chunk][8][T]
+    int act_nsnake, cout_real;
     int Cinp, Coutp, T, dil;
     int tiles_per_chunk;
 };
@@ -87,6 +94,7 @@ __device__ __forceinline__ float fsq(int code, int d) {
 }
 
 // Implicit-GEMM causal conv. Block tile BM (out ch) x BN (time), 4 waves.
+constexpr int MAXTAPS = 11;
 template <int BM, int BN, int MODE>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     constexpr int RW = BM / 16;          // row blocks of 16
@@ -107,8 +115,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     const int rw = w % RW, cw = w / RW;
     const int kg = lane >> 4, l16 = lane & 15;
     const size_t chunk_in = (size_t)chunk * p.T * p.Cinp;
-    const float *xin = p.x[br] + chunk_in;
-    const float *alpha = p.alpha[br];
+    const _Float16 *xin = p.x[br] + chunk_in;
     const _Float16 *W = p.W[br];
     const int Kw = ks * p.Cinp;
     const int orow = m0 + rw * 16 + l16;
@@ -119,48 +126,45 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
 
     const int rows = BN + pad;
     for (int i0 = 0; i0 < p.Cinp; i0 += 32) {
+        // ---- A fragments of every tap of this channel block (L2-resident weight
+        //      image), in flight while the input rows are staged
+        half8 af[MAXTAPS];
+#pragma unroll
+        for (int k = 0; k < MAXTAPS; ++k)
+            if (k < ks) af[k] = *(const half8 *)(W + (size_t)orow * Kw + k * p.Cinp + i0 + 8 * kg);
         // ---- stage input rows [t0 - pad, t0 + BN) x channels [i0, i0+32) as f16
-        for (int e = tid; e < rows * 8; e += 256) {
-            const int r = e >> 3, c4 = (e & 7) * 4;
-            const int t = t0 - pad + r;
-            float v[4] = {0.f, 0.f, 0.f, 0.f};
-            if (t >= 0 && t < p.T) {
-                if constexpr (MODE == IN_FSQ) {
+        if constexpr (MODE == IN_FSQ) {
+            for (int e = tid; e < rows * 8; e += 256) {
+                const int r = e >> 3, c4 = (e & 7) * 4;
+                const int t = t0 - pad + r;
+                _Float16 *dst = (_Float16 *)(xs + r * ROWB) + c4;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int c = i0 + c4 + u;
-                        v[u] = fsq(p.codes[((size_t)chunk * 8 + (c >> 2)) * p.T + t], c & 3);
-                    }
-                } else {
-                    float4 a = *(const float4 *)(xin + (size_t)t * p.Cinp + i0 + c4);
-                    if constexpr (MODE == IN_AVG3) {
-                        const float4 b = *(const float4 *)(p.xa + chunk_in + (size_t)t * p.Cinp + i0 + c4);
-                        const float4 c = *(const float4 *)(p.xb + chunk_in + (size_t)t * p.Cinp + i0 + c4);
-                        // magpie_codec_build_reslayer: (b0 + b1) + b2, then * (1/3)
-                        a.x = ((a.x + b.x) + c.x) * (1.0f / 3.0f);
-                        a.y = ((a.y + b.y) + c.y) * (1.0f / 3.0f);
-                        a.z = ((a.z + b.z) + c.z) * (1.0f / 3.0f);
-                        a.w = ((a.w + b.w) + c.w) * (1.0f / 3.0f);
-                    }
-                    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-                    if (alpha) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) v[u] = half_snake(v[u], i0 + c4 + u, p.n_snake, p.cin_real, alpha);
-                    }
+                for (int u = 0; u < 4; ++u) {
+                    const int c = i0 + c4 + u;
+                    dst[u] = (t >= 0 && t < p.T) ? (_Float16)fsq(p.codes[((size_t)chunk * 8 + (c >> 2)) * p.T + t], c & 3)
+                                                 : (_Float16)0.f;
                 }
             }
-            _Float16 *dst = (_Float16 *)(xs + r * ROWB) + c4;
-            dst[0] = (_Float16)v[0]; dst[1] = (_Float16)v[1]; dst[2] = (_Float16)v[2]; dst[3] = (_Float16)v[3];
+        } else {
+            for (int e = tid; e < rows * 4; e += 256) {
+                const int r = e >> 2, q = e & 3;
+                const int t = t0 - pad + r;
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (t >= 0 && t < p.T) v = *(const uint4 *)(xin + (size_t)t * p.Cinp + i0 + 8 * q);
+                *(uint4 *)(xs + r * ROWB + 16 * q) = v;
+            }
         }
         __syncthreads();
-        // ---- ks taps: A from the f16 weight image (L2-resident), B from LDS
-        for (int k = 0; k < ks; ++k) {
-            const half8 a = *(const half8 *)(W + (size_t)orow * Kw + k * p.Cinp + i0 + 8 * kg);
+        // ---- ks taps: A from registers, B (one ds_read_b128 per fragment) from LDS
 #pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const int col = cw * WCOLS + j * 16 + l16;
-                const half8 b = *(const half8 *)(xs + (col + k * p.dil) * ROWB + 16 * kg);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[j], 0, 0, 0);
+        for (int k = 0; k < MAXTAPS; ++k) {
+            if (k < ks) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const int col = cw * WCOLS + j * 16 + l16;
+                    const half8 b = *(const half8 *)(xs + (col + k * p.dil) * ROWB + 16 * kg);
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k], b, acc[j], 0, 0, 0);
+                }
             }
         }
         __syncthreads();
@@ -169,6 +173,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     const int o = m0 + rw * 16 + 4 * kg;
     const float4 bb = *(const float4 *)(p.bias[br] + o);
     const size_t chunk_out = (size_t)chunk * p.T * p.Coutp;
+    const float *aal = p.act_alpha[br];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         const int t = t0 + cw * WCOLS + j * 16 + l16;
@@ -179,7 +184,16 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
             const float4 r = *(const float4 *)(p.resid[br] + off);
             v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;  // input + h (568-599)
         }
-        *(float4 *)(p.out[br] + off) = v;
+        if (p.out[br]) *(float4 *)(p.out[br] + off) = v;
+        if (p.act[br]) {  // the next conv's operand: f16(HalfSnake(v)) (ggml F16 im2col)
+            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+            half4 h;
+            h[0] = (_Float16)half_snake(v.x, o + 0, p.act_nsnake, p.cout_real, aal);
+            h[1] = (_Float16)half_snake(v.y, o + 1, p.act_nsnake, p.cout_real, aal);
+            h[2] = (_Float16)half_snake(v.z, o + 2, p.act_nsnake, p.cout_real, aal);
+            h[3] = (_Float16)half_snake(v.w, o + 3, p.act_nsnake, p.cout_real, aal);
+            *(half4 *)(p.act[br] + off) = h;
+        }
     }
 }
 
@@ -193,33 +207,56 @@ struct ConvTP {
     const float *w;            // [Cin_real][2s] f32
     const float *bias;         // [Cout_real]
     float *out;                // [chunk][Tin*s][Coutp]
+    _Float16 *act[3];          // f16 HalfSnake_{act_alpha[j]}(out): the k=0 in_conv operands
+    const float *act_alpha[3];
     int cout_real, Coutp, Tin, s, nchunk;
 };
+// One thread per (chunk, input step tau, output group g): its outputs are
+// t in [tau*s, tau*s + s), fed by inputs tau-1 and tau of channels 2g, 2g+1
+// (the 3-branch mean and HalfSnake of those 4 values computed once).
 template <bool AVG>
 __global__ __launch_bounds__(256) void conv_transpose_kernel(ConvTP p) {
-    const size_t total = (size_t)p.nchunk * p.Tin * p.s * p.Coutp;
+    const size_t total = (size_t)p.nchunk * p.Tin * p.Coutp;
     for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (size_t)gridDim.x * 256) {
         const int g = (int)(e % p.Coutp);
         const size_t tt = e / p.Coutp;
-        const int t = (int)(tt % ((size_t)p.Tin * p.s));
-        const int chunk = (int)(tt / ((size_t)p.Tin * p.s));
-        float acc = 0.f;
+        const int tau = (int)(tt % p.Tin), chunk = (int)(tt / p.Tin);
+        const int K = 2 * p.s;
+        float in[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // [tau-1, tau][channel 2g, 2g+1]
         if (g < p.cout_real) {
-            const int K = 2 * p.s;
-            for (int ci = 0; ci < 2; ++ci) {
-                const int c = 2 * g + ci;
-                for (int tau = t / p.s - 1; tau <= t / p.s; ++tau) {
-                    if (tau < 0 || tau >= p.Tin) continue;
-                    const size_t xo = ((size_t)chunk * p.Tin + tau) * p.Cinp + c;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const int ta = tau - 1 + dt;
+                if (ta < 0) continue;
+#pragma unroll
+                for (int ci = 0; ci < 2; ++ci) {
+                    const int c = 2 * g + ci;
+                    const size_t xo = ((size_t)chunk * p.Tin + ta) * p.Cinp + c;
                     float v = p.x[xo];
                     if constexpr (AVG) v = ((v + p.xa[xo]) + p.xb[xo]) * (1.0f / 3.0f);
-                    v = half_snake(v, c, p.n_snake, p.cin_real, p.alpha);
-                    acc += v * p.w[(size_t)c * K + (t - tau * p.s)];
+                    in[dt][ci] = half_snake(v, c, p.n_snake, p.cin_real, p.alpha);
                 }
             }
-            acc += p.bias[g];
         }
-        p.out[e] = acc;
+        for (int u = 0; u < p.s; ++u) {
+            const int t = tau * p.s + u;
+            float acc = 0.f;
+            if (g < p.cout_real) {
+                // ggml order: channel c outer, tau = t/s - 1 then t/s inner
+#pragma unroll
+                for (int ci = 0; ci < 2; ++ci) {
+                    const int c = 2 * g + ci;
+                    if (tau >= 1) acc += in[0][ci] * p.w[(size_t)c * K + (t - (tau - 1) * p.s)];
+                    acc += in[1][ci] * p.w[(size_t)c * K + (t - tau * p.s)];
+                }
+                acc += p.bias[g];
+            }
+            const size_t oo = ((size_t)chunk * p.Tin * p.s + t) * p.Coutp + g;
+            p.out[oo] = acc;
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                p.act[j][oo] = (_Float16)half_snake(acc, g, p.cout_real / 2, p.cout_real, p.act_alpha[j]);
+        }
     }
 }
 
@@ -280,7 +317,8 @@ struct mp_codec {
     std::vector<void *> weight_allocs;
     // activations (grown on demand)
     size_t cap_elems = 0;
-    float *x_pre = nullptr, *x0 = nullptr, *brb[3] = {}, *tmp[3] = {}, *audio = nullptr;
+    float *x_pre = nullptr, *x0 = nullptr, *brb[3] = {}, *audio = nullptr;
+    _Float16 *a16[3] = {}, *b16[3] = {};  // f16 conv operands: in_conv (HS_in x), sk_conv (HS_sk h)
     int *codes = nullptr;
     size_t codes_cap = 0, audio_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -381,9 +419,12 @@ int ensure_buffers(mp_codec *c, int nchunk, int F) {
     }
     need = std::max(need, (size_t)nchunk * F * CP_PRE);
     if (need > c->cap_elems) {
-        float **bufs[8] = {&c->x_pre, &c->x0, &c->brb[0], &c->brb[1], &c->brb[2], &c->tmp[0], &c->tmp[1], &c->tmp[2]};
+        float **bufs[5] = {&c->x_pre, &c->x0, &c->brb[0], &c->brb[1], &c->brb[2]};
         for (auto b : bufs) if (*b) { hipFree(*b); *b = nullptr; }
         for (auto b : bufs) CHK(hipMalloc((void **)b, need * 4 + 256));
+        _Float16 **hb[6] = {&c->a16[0], &c->a16[1], &c->a16[2], &c->b16[0], &c->b16[1], &c->b16[2]};
+        for (auto b : hb) if (*b) { hipFree(*b); *b = nullptr; }
+        for (auto b : hb) CHK(hipMalloc((void **)b, need * 2 + 256));
         c->cap_elems = need;
     }
     const size_t ncodes = (size_t)nchunk * 8 * F, naudio = (size_t)nchunk * F * HOP;
@@ -411,9 +452,9 @@ hipError_t run_conv(const mpc::ConvP &p, int BM, int mode, int nchunk, int nbran
     using namespace mpc;
     if (BM == 64) {
         if (mode == IN_FSQ) return launch_conv<64, 64, IN_FSQ>(p, nchunk, nbranch, s);
-        return launch_conv<64, 64, IN_PLAIN>(p, nchunk, nbranch, s);
+        return launch_conv<64, 64, IN_F16>(p, nchunk, nbranch, s);
     }
-    return launch_conv<32, 128, IN_PLAIN>(p, nchunk, nbranch, s);
+    return launch_conv<32, 128, IN_F16>(p, nchunk, nbranch, s);
 }
 
 // Decode nchunk independent chunks of F frames each (codes [chunk][8][F]).
@@ -423,22 +464,24 @@ int codec_run(mp_codec *c, int nchunk, int F) {
     // pre-conv with the FSQ dequant in its loader
     {
         ConvP p{};
-        p.W[0] = c->pre.w; p.bias[0] = c->pre.b; p.alpha[0] = nullptr; p.x[0] = nullptr; p.out[0] = c->x_pre;
-        p.resid[0] = nullptr; p.ks[0] = 7; p.codes = c->codes; p.n_snake = 0; p.cin_real = 32;
+        p.W[0] = c->pre.w; p.bias[0] = c->pre.b; p.x[0] = nullptr; p.out[0] = c->x_pre;
+        p.resid[0] = nullptr; p.act[0] = nullptr; p.ks[0] = 7; p.codes = c->codes; p.cout_real = 864;
         p.Cinp = 32; p.Coutp = CP_PRE; p.T = F; p.dil = 1; p.tiles_per_chunk = (F + 63) / 64;
         CHK(run_conv(p, 64, IN_FSQ, nchunk, 1, s));
     }
     int T = F;
     for (int i = 0; i < NSTAGE; ++i) {
         const int cin = CH[i], C = CH[i + 1], Cin_p = i == 0 ? CP_PRE : CP[i - 1], Cp = CP[i];
-        // HalfSnake -> grouped convT (input: pre-conv, or mean of the previous ResLayer's branches)
+        // HalfSnake -> grouped convT (input: pre-conv, or mean of the previous ResLayer's
+        // branches); emits x0 and the 3 branches' first in_conv operands HS_in(x0)
         ConvTP tp{};
         tp.x = i == 0 ? c->x_pre : c->brb[0];
         tp.xa = c->brb[1]; tp.xb = c->brb[2];
         tp.alpha = c->up_alpha[i]; tp.n_snake = cin / 2; tp.cin_real = cin; tp.Cinp = Cin_p;
         tp.w = c->up_w[i]; tp.bias = c->up_b[i]; tp.out = c->x0; tp.cout_real = C; tp.Coutp = Cp;
+        for (int j = 0; j < 3; ++j) { tp.act[j] = c->a16[j]; tp.act_alpha[j] = c->rb_alpha[i][j][0][0]; }
         tp.Tin = T; tp.s = RATE[i]; tp.nchunk = nchunk;
-        const size_t total = (size_t)nchunk * T * RATE[i] * Cp;
+        const size_t total = (size_t)nchunk * T * Cp;
         const int grid = (int)std::min<size_t>((total + 255) / 256, 65536);
         if (i == 0) hipLaunchKernelGGL(conv_transpose_kernel<false>, dim3(grid), dim3(256), 0, s, tp);
         else hipLaunchKernelGGL(conv_transpose_kernel<true>, dim3(grid), dim3(256), 0, s, tp);
@@ -446,24 +489,26 @@ int codec_run(mp_codec *c, int nchunk, int F) {
         T *= RATE[i];
         const int BM = BMS[i], BN = BM == 64 ? 64 : 128;
         for (int k = 0; k < 3; ++k) {
-            // h = conv_{ks_j, d_k}(HS_in(x)) for the 3 branches j
+            // h = conv_{ks_j, d_k}(HS_in(x)) for the 3 branches j; only HS_sk(h) (f16) is kept
             ConvP p{};
             for (int j = 0; j < 3; ++j) {
                 const mp_codec::Conv &cv = c->rb[i][j][k][0];
-                p.W[j] = cv.w; p.bias[j] = cv.b; p.alpha[j] = c->rb_alpha[i][j][k][0];
-                p.x[j] = k == 0 ? c->x0 : c->brb[j]; p.out[j] = c->tmp[j]; p.resid[j] = nullptr; p.ks[j] = KS[j];
+                p.W[j] = cv.w; p.bias[j] = cv.b; p.x[j] = c->a16[j]; p.out[j] = nullptr; p.resid[j] = nullptr;
+                p.act[j] = c->b16[j]; p.act_alpha[j] = c->rb_alpha[i][j][k][1]; p.ks[j] = KS[j];
             }
-            p.n_snake = C / 2; p.cin_real = C; p.Cinp = Cp; p.Coutp = Cp; p.T = T; p.dil = DIL[k];
+            p.act_nsnake = C / 2; p.cout_real = C; p.Cinp = Cp; p.Coutp = Cp; p.T = T; p.dil = DIL[k];
             p.tiles_per_chunk = (T + BN - 1) / BN;
-            CHK(run_conv(p, BM, IN_PLAIN, nchunk, 3, s));
-            // x' = x + conv_{ks_j, 1}(HS_sk(h))
+            CHK(run_conv(p, BM, IN_F16, nchunk, 3, s));
+            // x' = x + conv_{ks_j, 1}(HS_sk(h)); plus the next block's operand HS_in(x')
             for (int j = 0; j < 3; ++j) {
                 const mp_codec::Conv &cv = c->rb[i][j][k][1];
-                p.W[j] = cv.w; p.bias[j] = cv.b; p.alpha[j] = c->rb_alpha[i][j][k][1];
-                p.x[j] = c->tmp[j]; p.out[j] = c->brb[j]; p.resid[j] = k == 0 ? c->x0 : c->brb[j];
+                p.W[j] = cv.w; p.bias[j] = cv.b; p.x[j] = c->b16[j];
+                p.out[j] = c->brb[j]; p.resid[j] = k == 0 ? c->x0 : c->brb[j];
+                p.act[j] = k < 2 ? c->a16[j] : nullptr;
+                p.act_alpha[j] = k < 2 ? c->rb_alpha[i][j][k + 1][0] : nullptr;
             }
             p.dil = 1;
-            CHK(run_conv(p, BM, IN_PLAIN, nchunk, 3, s));
+            CHK(run_conv(p, BM, IN_F16, nchunk, 3, s));
         }
     }
     PostP pp{c->brb[0], c->brb[1], c->brb[2], c->post_alpha, c->post_w, c->post_b, c->audio, T, nchunk};
@@ -527,8 +572,12 @@ void mp_hip_codec_free(mp_codec *c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void *p : c->weight_allocs) hipFree(p);
-    float *bufs[8] = {c->x_pre, c->x0, c->brb[0], c->brb[1], c->brb[2], c->tmp[0], c->tmp[1], c->tmp[2]};
+    float *bufs[5] = {c->x_pre, c->x0, c->brb[0], c->brb[1], c->brb[2]};
     for (float *b : bufs) if (b) hipFree(b);
+    for (int j = 0; j < 3; ++j) {
+        if (c->a16[j]) hipFree(c->a16[j]);
+        if (c->b16[j]) hipFree(c->b16[j]);
+    }
     if (c->codes) hipFree(c->codes);
     if (c->audio) hipFree(c->audio);
     if (c->ev0) hipEventDestroy(c->ev0);

@@ -33,6 +33,13 @@ __device__ __forceinline__ unsigned short f2bf(float x) {
     if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 64);
     return (unsigned short)((u + (0x7fffu + ((u >> 16) & 1u))) >> 16);
 }
+// two f32 -> packed bf16 pair on one v_cvt_pk_bf16_f32 (round to nearest even,
+// identical to f2bf for every non-NaN input)
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(unsigned, v);
+}
 
 template <int NB, int K, int PRO, int EPI>
 __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
@@ -64,10 +71,10 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
             uint4 o = make_uint4(0, 0, 0, 0);
             if (b < NB) {
                 const float4 x0 = *(const float4 *)(actf + b * K + k), x1 = *(const float4 *)(actf + b * K + k + 4);
-                o.x = f2bf(x0.x) | ((unsigned)f2bf(x0.y) << 16);
-                o.y = f2bf(x0.z) | ((unsigned)f2bf(x0.w) << 16);
-                o.z = f2bf(x1.x) | ((unsigned)f2bf(x1.y) << 16);
-                o.w = f2bf(x1.z) | ((unsigned)f2bf(x1.w) << 16);
+                o.x = pk_bf16(x0.x, x0.y);
+                o.y = pk_bf16(x0.z, x0.w);
+                o.z = pk_bf16(x1.x, x1.y);
+                o.w = pk_bf16(x1.z, x1.w);
             }
             *(uint4 *)(actb + b * KP + k) = o;
         }
@@ -91,10 +98,10 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
                 const int e = base + u * MP_BLOCK + tid;
                 if (e < ITEMS) {
                     uint4 o;
-                    o.x = f2bf(x0[u].x) | ((unsigned)f2bf(x0[u].y) << 16);
-                    o.y = f2bf(x0[u].z) | ((unsigned)f2bf(x0[u].w) << 16);
-                    o.z = f2bf(x1[u].x) | ((unsigned)f2bf(x1[u].y) << 16);
-                    o.w = f2bf(x1[u].z) | ((unsigned)f2bf(x1[u].w) << 16);
+                    o.x = pk_bf16(x0[u].x, x0[u].y);
+                    o.y = pk_bf16(x0[u].z, x0[u].w);
+                    o.z = pk_bf16(x1[u].x, x1[u].y);
+                    o.w = pk_bf16(x1[u].z, x1[u].w);
                     *(uint4 *)(actb + (e / (K / 8)) * KP + (e % (K / 8)) * 8) = o;
                 }
             }

@@ -189,8 +189,8 @@ constexpr int pro_scratch() {
 // Weights of NS partial softmax states (m_s, l_s, O_s relative to m_s) of `nq`
 // groups (group q's split s at pp + (q*NS + s)*stride): e_s = exp(m_s - M),
 // M = max_s m_s, den = sum_s e_s l_s (an empty split has m = -inf, l = 0, O = 0);
-// sc[q*(NS+1) + s] = e_s, sc[q*(NS+1) + NS] = den. The merged output is
-// sum_s e_s O_s / den. Computed once per group, not per element.
+// sc[q*(NS+1) + s] = e_s, sc[q*(NS+1) + NS] = 1/den. The merged output is
+// (sum_s e_s O_s) * (1/den). Computed once per group, not per element.
 template <int NS>
 __device__ __forceinline__ void merge_weights(const float *pp, int stride, int nq, float *sc) {
     for (int q = threadIdx.x; q < nq; q += MP_BLOCK) {
@@ -210,7 +210,7 @@ __device__ __forceinline__ void merge_weights(const float *pp, int stride, int n
             sc[q * (NS + 1) + s] = e;
             den += e * ls[s];
         }
-        sc[q * (NS + 1) + NS] = den;
+        sc[q * (NS + 1) + NS] = 1.0f / den;
     }
 }
 
@@ -246,8 +246,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                     const float w = sc[q * (SA_SPLITS + 1) + s2];
                     num.x += w * o[u][s2].x; num.y += w * o[u][s2].y; num.z += w * o[u][s2].z; num.w += w * o[u][s2].w;
                 }
-                const float den = sc[q * (SA_SPLITS + 1) + SA_SPLITS];
-                *(float4 *)(act + b * K + k) = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
+                const float rd = sc[q * (SA_SPLITS + 1) + SA_SPLITS];
+                *(float4 *)(act + b * K + k) = make_float4(num.x * rd, num.y * rd, num.z * rd, num.w * rd);
             }
         }
         lds_sync();
@@ -282,9 +282,9 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                     const float w = sc[b * (XA_SPLITS + 1) + s2];
                     num.x += w * o[u][s2].x; num.y += w * o[u][s2].y; num.z += w * o[u][s2].z; num.w += w * o[u][s2].w;
                 }
-                const float den = sc[b * (XA_SPLITS + 1) + XA_SPLITS];
-                const float4 x2 = make_float4(num.x / den + xv[u].x, num.y / den + xv[u].y, num.z / den + xv[u].z,
-                                              num.w / den + xv[u].w);
+                const float rd = sc[b * (XA_SPLITS + 1) + XA_SPLITS];
+                const float4 x2 = make_float4(num.x * rd + xv[u].x, num.y * rd + xv[u].y, num.z * rd + xv[u].z,
+                                              num.w * rd + xv[u].w);
                 *(float4 *)(act + b * K + k) = x2;
                 if (blockIdx.x == 0) *(float4 *)(p.xres + (size_t)b * D + k) = x2;
             }

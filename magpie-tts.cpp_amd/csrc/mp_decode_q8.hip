@@ -112,6 +112,134 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_q8_kernel(GemvP p) {
     epi_store<EPI>(p, v, n, b);
 }
 
+// ---------------------------------------------------------------- fused Q8 XA tail
+// Cross-attention with Q8_0 q_net / o_net: q = Q8(q_net) LN(x) is one GEMV
+// launch (q8_xq, 8 workgroups: q_net's 98 KB spread over CUs); this kernel then
+// does attention + o_net + residual: grid (768/64, B), a workgroup owns 64 rows
+// of o_net and recomputes the slot's attention over the text (K, V: 2 x T x 128
+// f32, coalesced: half a wave per key row), quantises it to Q8_0 and finishes
+// x2 = x + Q8(o_net) a for its rows with gemv_q8<.., 128, 8, PRO_PLAIN,
+// EPI_ADD_STORE>'s arithmetic. The o_net rows are issued first.
+constexpr int XQ8_ROWS = 64;  // o_net rows per workgroup
+__global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
+    constexpr int OR = 8, OCPR = DXA / 16;                 // o_net: groups of 8 rows
+    constexpr int OG = XQ8_ROWS / MP_NWAVES / OR;          // 2 groups per wave
+    __shared__ float pr[TMAX_LIMIT];
+    __shared__ __attribute__((aligned(16))) signed char aq[DXA];
+    __shared__ float ad[DXA / 32];
+    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r0 = blockIdx.x * XQ8_ROWS;
+    uint4 wo[OG];
+    float wos[OG];
+#pragma unroll
+    for (int g = 0; g < OG; ++g) {
+        const int row = r0 + (w * OG + g) * OR + lane / OCPR, kc = lane % OCPR;
+        wo[g] = *(const uint4 *)(p.wo + (size_t)row * DXA + kc * 16);
+        wos[g] = __half2float(__ushort_as_half(p.wod[(size_t)row * (DXA / 32) + kc / 2]));
+    }
+    // ---- attention over the utterance's text, coalesced: a half-wave (32 lanes x
+    //      float4) covers one 128-dim key row; wave w scores keys t = w + 4 u
+    __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
+    __shared__ float wred[2 * MP_NWAVES];
+    {
+        const int Tb = p.T[b];
+        const int h = lane >> 5, d4 = 4 * (lane & 31);
+        const float4 q4 = *(const float4 *)(p.q + (size_t)b * DXA + d4);
+        const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+        const float *Vb = p.xav + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+        const float scale = 1.0f / sqrtf((float)DXA);
+        float mx = -INFINITY;
+        for (int t0 = 2 * w; t0 < Tb; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
+            float4 k4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = min(t0 + 2 * MP_NWAVES * u + h, Tb - 1);
+                k4[u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 2 * MP_NWAVES * u + h;
+                const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
+                if (t < Tb) {
+                    if ((lane & 31) == 0) pr[t] = sv;
+                    mx = fmaxf(mx, sv);
+                }
+            }
+        }
+        mx = wave_max(mx);
+        if (lane == 0) wred[w] = mx;
+        lds_sync();
+        const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
+        // o[d] = sum_t e_t V_t[d]: wave w takes keys t = w + 4 u, lane owns dims lane, 64 + lane
+        float l = 0.f, o0 = 0.f, o1 = 0.f;
+        for (int t0 = w; t0 < Tb; t0 += MP_NWAVES * 4) {
+            float v0[4], v1[4], e[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = min(t0 + MP_NWAVES * u, Tb - 1);
+                v0[u] = Vb[(size_t)t * DXA + lane];
+                v1[u] = Vb[(size_t)t * DXA + 64 + lane];
+                e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { l += e[u]; o0 += e[u] * v0[u]; o1 += e[u] * v1[u]; }
+        }
+        pv[w][lane] = o0;
+        pv[w][64 + lane] = o1;
+        if (lane == 0) wred[MP_NWAVES + w] = l;
+        lds_sync();
+        if (w == 0) {
+            const float den = ((wred[4] + wred[5]) + wred[6]) + wred[7];
+            float av[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int d = lane + 64 * i;
+                av[i] = (((pv[0][d] + pv[1][d]) + pv[2][d]) + pv[3][d]) / den;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {  // element lane + 64 i; its Q8_0 block = this half-wave
+                float a = row_max16(fabsf(av[i]));
+                a = fmaxf(a, __shfl_xor(a, 16, 64));
+                const float dd = a / 127.0f;
+                const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+                aq[lane + 64 * i] = (signed char)(int)roundf(av[i] * id);
+                if ((lane & 31) == 0) ad[(lane + 64 * i) / 32] = __half2float(__float2half(dd));
+            }
+        }
+    }
+    lds_sync();
+    // ---- x2 = x + Q8(o_net) a for this workgroup's 64 rows (8 per group)
+#pragma unroll
+    for (int g = 0; g < OG; ++g) {
+        const int r = lane / OCPR, kc = lane % OCPR;
+        const int4 a4 = *(const int4 *)(aq + kc * 16);
+        int s = __builtin_amdgcn_sdot4((int)wo[g].x, a4.x, 0, false);
+        s = __builtin_amdgcn_sdot4((int)wo[g].y, a4.y, s, false);
+        s = __builtin_amdgcn_sdot4((int)wo[g].z, a4.z, s, false);
+        s = __builtin_amdgcn_sdot4((int)wo[g].w, a4.w, s, false);
+        s += __builtin_amdgcn_update_dpp(0, s, 0xB1, 0xF, 0xF, false);
+        const float f = (lane & 1) ? 0.f : (float)s * (wos[g] * ad[kc >> 1]);
+        float v = 0.f;
+#pragma unroll
+        for (int rr = 0; rr < OR; ++rr) {
+            const float t = wave_sum((r == rr) ? f : 0.f);
+            if (lane == rr) v = t;
+        }
+        if (lane < OR) {
+            const int row = r0 + (w * OG + g) * OR + lane;
+            p.x2[(size_t)b * D + row] = v + p.x[(size_t)b * D + row];
+        }
+    }
+}
+
+hipError_t op_xa_q8(const XaQ8P &p, int B, hipStream_t s) {
+    if (!p.x || !p.x2 || !p.q || !p.wo || !p.wod || !p.xak || !p.xav || !p.T || p.Tmax < 1 ||
+        p.Tmax > TMAX_LIMIT)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xa_q8_kernel, dim3(D / XQ8_ROWS, B), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
 template <int PRO, int EPI>
 static bool q8_args_ok(const GemvP &p) {
     if (!p.Wq || !p.Wd || p.N <= 0) return false;
@@ -150,7 +278,6 @@ static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     hipError_t q8_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t q8_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_SA_MERGE, EPI_RESID>(p, s); }      \
     hipError_t q8_xq_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_STORE>(p, s); }            \
-    hipError_t q8_xo_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, DXA, 8, PRO_PLAIN, EPI_ADD_STORE>(p, s); }   \
     hipError_t q8_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_BIAS>(p, s); }         \
     hipError_t q8_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
     hipError_t q8_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \

@@ -152,6 +152,20 @@ struct XaP {
     int Tmax, layer, nlayers;
 };
 
+// Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the
+// q GEMV: x2 = x + Q8(o_net) attn(q, K, V), the attention output quantised where
+// ggml quantises it (magpie.cpp:1713-1767, 3513-3519).
+struct XaQ8P {
+    const float *x;                 // [B][768]
+    float *x2;                      // [B][768]
+    const float *q;                 // [B][128] = Q8(q_net) LN(x)
+    const signed char *wo;          // o_net int8 [768][128]
+    const unsigned short *wod;      //   fp16 block scales [768][4]
+    const float *xak, *xav;         // XA K, V [B][L][Tmax][128]
+    const int *T;
+    int Tmax, layer, nlayers;
+};
+
 struct AttnP {  // decode self-attention (one query per utterance)
     const float *q;
     const float *kc, *vc;

@@ -258,9 +258,20 @@ __global__ __launch_bounds__(256) void row_xa_kernel(RowXaP p) {
     l = wave_sum(l);
     __builtin_amdgcn_wave_barrier();
     float o0 = 0.f, o1 = 0.f;
-    for (int j = 0; j < Tb; ++j) {
-        o0 += pr[w][j] * Vb[(size_t)j * DXA + lane];
-        o1 += pr[w][j] * Vb[(size_t)j * DXA + 64 + lane];
+    for (int j0 = 0; j0 < Tb; j0 += 8) {  // 8 keys' V rows in flight, summed in key order
+        float v0[8], v1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = min(j0 + u, Tb - 1);
+            v0[u] = Vb[(size_t)j * DXA + lane];
+            v1[u] = Vb[(size_t)j * DXA + 64 + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (j0 + u < Tb) {
+                o0 += pr[w][j0 + u] * v0[u];
+                o1 += pr[w][j0 + u] * v1[u];
+            }
     }
     p.O[(size_t)m * DXA + lane] = o0 / l;
     p.O[(size_t)m * DXA + 64 + lane] = o1 / l;

@@ -58,7 +58,7 @@ hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t);
 #define MP_DECL_Q8(NB)                                                                                       \
     hipError_t q8_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t q8_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t q8_oproj_##NB(const GemvP &, hipStream_t); hipError_t q8_xq_##NB(const GemvP &, hipStream_t);             \
-    hipError_t q8_xo_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_in0_##NB(const GemvP &, hipStream_t);           \
+    hipError_t q8_lt_in0_##NB(const GemvP &, hipStream_t);                                                             \
     hipError_t q8_lt_a_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_ag_##NB(const GemvP &, hipStream_t);           \
     hipError_t q8_lt_b_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_e_##NB(const GemvP &, hipStream_t);
 MP_DECL_Q8(1)
@@ -68,6 +68,7 @@ MP_DECL_Q8(8)
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
+hipError_t op_xa_q8(const XaQ8P &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
 
 }  // namespace mp
@@ -88,8 +89,8 @@ static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TAB
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
-struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, xo, lt_in0, lt_a, lt_ag, lt_b, lt_e; };
-#define MP_TABLE_Q8(NB) { q8_qkv_embed_##NB, q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_xo_##NB, q8_lt_in0_##NB, \
+struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, lt_in0, lt_a, lt_ag, lt_b, lt_e; };
+#define MP_TABLE_Q8(NB) { q8_qkv_embed_##NB, q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_lt_in0_##NB, \
                           q8_lt_a_##NB, q8_lt_ag_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
 static const OpTableQ8 kTablesQ8[4] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8)};
 static int nb_index(int NB) { return NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : NB == 8 ? 3 : 4; }
@@ -135,7 +136,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_ROWXA = 4 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5 };
 struct OpRec {
     std::string name;
     int kind;
@@ -144,7 +145,7 @@ struct OpRec {
     AttnP a;
     FinP f;
     XaP x;
-    RowXaP rx;
+    XaQ8P xq;
     int B;
     double bytes;
 };
@@ -175,7 +176,7 @@ struct mp_dev {
     std::vector<void *> allocs;
     float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *sa_out = nullptr,
           *h = nullptr, *hidden = nullptr;
-    float *xqb = nullptr, *xab = nullptr;  // Q8 mode (unfused XA): q_net output, attention output [NB][128]
+    float *xqb = nullptr;  // Q8 mode: q_net output [NB][128]
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
@@ -562,7 +563,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
     A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(sa_out, NB * 768);
-    A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(xab, NB * 128);
+    A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -652,23 +653,19 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             return rc;
         if (W.xq8) {
             // cross-attention with Q8_0 q_net / o_net, as ggml computes it (1713-1767):
-            // q = Q8(q_net) LN(x); a = attn(q, K, V); x2 = x + Q8(o_net) a
+            // q = Q8(q_net) LN(x) (GEMV), then x2 = x + Q8(o_net) attn(q, K, V) (xa_q8_kernel)
             g = gemv_base(dev); g.layer = l;
             g.W = W.xq; g.Wq = W.xq8.q; g.Wd = W.xq8.d; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
             g.out = dev->xqb; g.out_ld = 128;
             if ((rc = run("xq", tq.xq, g, Fq * (128.0 * 768) + A * act * (768 + 128))) != MP_OK) return rc;
-            mp::RowXaP rx{dev->xqb, dev->xak, dev->xav, l, L, dev->Tmax, 1, NB, dev->T, dev->xab};
+            mp::XaQ8P xq{dev->x, dev->x2, dev->xqb, W.xo8.q, W.xo8.d, dev->xak, dev->xav, dev->T, dev->Tmax, l, L};
             if (record) {
                 mp::OpRec r{};
-                r.name = "xattn"; r.kind = mp::K_ROWXA; r.rx = rx; r.B = NB;
-                r.bytes = A * act * (128.0 * 2 + 2.0 * 128 * dev->Tmax);
+                r.name = "xa_q8"; r.kind = mp::K_XAQ8; r.xq = xq; r.B = NB;
+                r.bytes = Fq * (768.0 * 128) + A * act * (128.0 + 768 * 2 + 2.0 * 128 * dev->Tmax);
                 dev->ops.push_back(r);
             }
-            HIPCHK(mp::pre_row_xa(rx, s));
-            g = gemv_base(dev); g.layer = l;
-            g.W = W.xo; g.Wq = W.xo8.q; g.Wd = W.xo8.d; g.N = 768; g.src = dev->xab; g.src_ld = 128;
-            g.out = dev->x2; g.out_ld = 768; g.addsrc = dev->x;
-            if ((rc = run("xo", tq.xo, g, Fq * (768.0 * 128) + A * act * (128 + 2 * 768))) != MP_OK) return rc;
+            HIPCHK(mp::op_xa_q8(xq, NB, s));
         } else {
             // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
             mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
@@ -1329,7 +1326,7 @@ int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
             case mp::K_GEMV: e = r.fn(r.g, dev->stream); break;
             case mp::K_ATTN: e = mp::op_sa_attn(r.a, r.B, dev->stream); break;
             case mp::K_XA: e = mp::op_xa(r.x, r.B, dev->stream); break;
-            case mp::K_ROWXA: e = mp::pre_row_xa(r.rx, dev->stream); break;
+            case mp::K_XAQ8: e = mp::op_xa_q8(r.xq, r.B, dev->stream); break;
             case mp::K_FIN: e = mp::op_finalize(r.f, r.B, dev->stream); break;
             }
             HIPCHK(e);
@@ -1359,7 +1356,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
         if (r.kind == mp::K_XA) {
             return mp::op_xa(r.x, r.B, dev->stream);  // rewrites this layer's split states only
         }
-        if (r.kind == mp::K_ROWXA) return mp::pre_row_xa(r.rx, dev->stream);
+        if (r.kind == mp::K_XAQ8) return mp::op_xa_q8(r.xq, r.B, dev->stream);  // rewrites x2 with the same values
         return hipErrorInvalidValue;
     };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");

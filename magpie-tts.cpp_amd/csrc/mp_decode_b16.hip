@@ -48,7 +48,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     constexpr int KC = K / 32, KW = KC / MP_NWAVES;
     constexpr int KP = K + 8;  // padded bf16 row: rows land 16 B apart in the banks
     constexpr int NR = NB + 1;  // NB activation rows + one zero row for the unused MFMA columns
-    constexpr bool STAGE = PRO != PRO_PLAIN;
+    constexpr bool STAGE = PRO != PRO_PLAIN && PRO != PRO_PLAIN_B16;
     constexpr int SC = pro_scratch<NB, PRO>();
     __shared__ __attribute__((aligned(16))) float actf[STAGE ? NB * K : 4];
     __shared__ __attribute__((aligned(16))) unsigned short actb[NR * KP];
@@ -78,6 +78,25 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
             }
             *(uint4 *)(actb + b * KP + k) = o;
         }
+    } else if constexpr (PRO == PRO_PLAIN_B16) {
+        // bf16 rows (written by the FFN-up epilogue): copied as they are, 12 uint4
+        // per thread in flight
+        constexpr int ITEMS = NB * (K / 8), BATCH = 12;
+        for (int base = 0; base < ITEMS; base += BATCH * MP_BLOCK) {
+            uint4 v[BATCH];
+#pragma unroll
+            for (int u = 0; u < BATCH; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                v[u] = e < ITEMS ? *(const uint4 *)(p.src_b16 + (size_t)(e / (K / 8)) * p.src_ld + (e % (K / 8)) * 8)
+                                 : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int u = 0; u < BATCH; ++u) {
+                const int e = base + u * MP_BLOCK + tid;
+                if (e < ITEMS) *(uint4 *)(actb + (e / (K / 8)) * KP + (e % (K / 8)) * 8) = v[u];
+            }
+        }
+        for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     } else {
         // NB rows straight from HBM/L2, in batches of 8 items per thread with all
         // 16 loads issued before the first conversion (one latency per batch)
@@ -136,6 +155,7 @@ static bool b16_args_ok(const GemvP &p) {
     if (!p.Wb || p.N <= 0) return false;
     bool ok = true;
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
+    if constexpr (PRO == PRO_PLAIN_B16) ok &= p.src_b16 != nullptr;
     if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
@@ -145,6 +165,7 @@ static bool b16_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_LTARG_LN)
         ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step && p.smp.cfg && p.smp.argeos;
     if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
+    if constexpr (EPI == EPI_GELU_B16) ok &= p.out_b16 != nullptr;
     if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
     if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
@@ -164,8 +185,8 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     hipError_t b16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }   \
-    hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU>(p, s); }         \
-    hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \
+    hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_B16>(p, s); }     \
+    hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE>(p, s); }  \
     hipError_t b16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
     hipError_t b16_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \
     hipError_t b16_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \

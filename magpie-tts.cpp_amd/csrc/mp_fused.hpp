@@ -610,6 +610,10 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b)
     if constexpr (EPI == EPI_STORE) p.out[(size_t)b * p.out_ld + n] = v;
     else if constexpr (EPI == EPI_BIAS) p.out[(size_t)b * p.out_ld + n] = v + p.bias[n];
     else if constexpr (EPI == EPI_GELU) p.out[(size_t)b * p.out_ld + n] = gelu_tanh(v);
+    else if constexpr (EPI == EPI_GELU_B16) {
+        const __bf16 h = (__bf16)gelu_tanh(v);  // round to nearest even, as the consumer's staging would
+        p.out_b16[(size_t)b * p.out_ld + n] = __builtin_bit_cast(unsigned short, h);
+    }
     else if constexpr (EPI == EPI_RESID) p.resid[(size_t)b * D + n] = v + p.resid[(size_t)b * D + n];
     else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
     else if constexpr (EPI == EPI_QKV) {

@@ -39,6 +39,7 @@ enum Pro {
     PRO_SA_MERGE = 9,   // act = SA output: the SA_SPLITS partial softmax states of each head merged
     PRO_XA_LN = 10,     // x2 = src + XA output (XA_SPLITS partial states merged), block 0 stores
                         // x2 to xres; act = LN(x2)*lnw              (3513-3525)
+    PRO_PLAIN_B16 = 11, // bf16 kernels only: act = src_b16 (rows already bf16, EPI_GELU_B16 output)
 };
 enum Epi {
     EPI_STORE = 0,      // out = v
@@ -48,6 +49,7 @@ enum Epi {
     EPI_QKV = 4,        // q -> out, k/v -> SA cache at pos       (3415-3442)
     EPI_LTQKV = 5,      // q -> lq, k/v -> LT position cb
     EPI_ADD_STORE = 6,  // out = v + addsrc
+    EPI_GELU_B16 = 7,   // out_b16 = bf16(gelu(v)): the bf16 FFN-down operand, rounded once here
 };
 
 // Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
@@ -91,6 +93,7 @@ struct GemvP {
     // prologue inputs
     const float *src;
     int src_ld;
+    const unsigned short *src_b16;  // PRO_PLAIN in the bf16 kernels: rows already bf16 (EPI_GELU_B16 output)
     const float *lnw;
     float eps;
     float *hidden_out;   // PRO_LN: block 0 stores the normalised vector (decoder hidden)
@@ -116,6 +119,7 @@ struct GemvP {
     // epilogue outputs
     float *out;
     int out_ld;
+    unsigned short *out_b16;        // EPI_GELU_B16
     float *resid;
     const float *addsrc;
     float *kc, *vc;

@@ -177,6 +177,7 @@ struct mp_dev {
     float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *sa_out = nullptr,
           *h = nullptr, *hidden = nullptr;
     float *xqb = nullptr;  // Q8 mode: q_net output [NB][128]
+    unsigned short *h_b16 = nullptr;  // bf16 mode: GELU(FFN up) as the bf16 FFN-down operand [NB][3072]
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
@@ -563,7 +564,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
     A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(sa_out, NB * 768);
-    A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128);
+    A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -685,6 +686,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
         } else {      // x2 = x + merged XA split states, stored by block 0 for the FFN residual
             g.src = dev->x; g.src_ld = 768; g.part = dev->xa_part; g.xres = dev->x2;
+            if (b16) g.out_b16 = dev->h_b16;  // GELU output stored bf16 (what FFN down rounds it to)
             if ((rc = run("ff1", tb.ff1x, g,
                           F * (3072.0 * 768) + A * act * (768 * 2 + 3072 + mp::XA_SPLITS * mp::XA_PART))) != MP_OK)
                 return rc;
@@ -692,6 +694,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // FFN down + residual (1805, 3525): x = x2 + W2 h
         g = gemv_base(dev); g.layer = l;
         g.W = W.ff2; g.Wb = b16 ? m.pk_ff2[l] : nullptr; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.out = dev->x; g.out_ld = 768; g.addsrc = dev->x2;
+        if (b16) { g.src = nullptr; g.src_b16 = dev->h_b16; }
         if ((rc = run("ff2", tb.ff2, g, F * (768.0 * 3072) + A * act * ((3072 + 2 * 768)))) != MP_OK) return rc;
     }
     mp::LtIo io{};

@@ -504,7 +504,9 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[j][i] - mean) * rstd) * p.lnw[lane + 64 * i];
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_LT_ATTN && NB >= 2) {
+    } else if constexpr (PRO == PRO_LT_ATTN) {
+        // wave w owns slots w, w+4, ... at every batch size (batch 1 included), so a
+        // slot's attention is the same instruction sequence whatever the batch
         const int lane = tid & 63, w = tid >> 6;
         const int nk = p.cb + 1;
         for (int b = w; b < NB; b += MP_NWAVES) {
@@ -526,7 +528,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 const float e = expf(sj[j] - m);
                 l += e;
                 const float4 v4 = *(const float4 *)(p.ltv + ((size_t)b * NCB + j) * LTD + 4 * lane);
-                a.x += e * v4.x; a.y += e * v4.y; a.z += e * v4.z; a.w += e * v4.w;
+                a.x = fmaf(e, v4.x, a.x); a.y = fmaf(e, v4.y, a.y); a.z = fmaf(e, v4.z, a.z); a.w = fmaf(e, v4.w, a.w);
             }
             *(float4 *)(act + b * K + 4 * lane) = make_float4(a.x / l, a.y / l, a.z / l, a.w / l);
         }
@@ -544,29 +546,6 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_LT_ATTN) {
-        static_assert(K == LTD, "LT is 256 wide");
-        const int lane = tid & 63, w = tid >> 6;
-        const int nk = p.cb + 1;
-        for (int b = 0; b < NB; ++b) {
-            const float4 q4 = *(const float4 *)(p.ltq + (size_t)b * LTD + 4 * lane);
-            for (int j = w; j < nk; j += MP_NWAVES) {
-                float v = dotv(q4, *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane));
-                v = wave_sum(v);
-                if (lane == 0) sc[j] = v * (1.0f / 16.0f);  // 1/sqrt(256)
-            }
-            lds_sync();
-            float m = -INFINITY;
-            for (int j = 0; j < nk; ++j) m = fmaxf(m, sc[j]);
-            float l = 0.f, a = 0.f;
-            for (int j = 0; j < nk; ++j) {
-                const float e = expf(sc[j] - m);
-                l += e;
-                a += e * p.ltv[((size_t)b * NCB + j) * LTD + tid];
-            }
-            act[b * K + tid] = a / l;
-            lds_sync();
-        }
     } else if constexpr (PRO == PRO_LTARG_LN) {
         static_assert(K == LTD, "LT is 256 wide");
         const int lane = tid & 63, w = tid >> 6;

@@ -11,41 +11,60 @@
 #include <hip/hip_fp16.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "mp_device.hpp"
 #include "mp_params.hpp"
 #include "mp_prefill_api.hpp"
 
 namespace mp {
 
-// Epilogue of a 4x4 register tile at rows m0.., columns n0.. (bias, residual,
-// GELU, KV-cache scatter, XA K/V split).
+// Epilogue of output (m, n) (bias, residual, GELU, KV-cache scatter, XA K/V split).
+template <int EPI>
+__device__ __forceinline__ void gemm_store1(const GemmP &p, int m, int n, float v) {
+    const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
+    if (p.bias) v += p.bias[n];
+    if constexpr (EPI == GE_STORE) p.C[(size_t)m * p.ldc + n] = v;
+    else if constexpr (EPI == GE_RESID) p.C[(size_t)m * p.ldc + n] = v + p.C[(size_t)m * p.ldc + n];
+    else if constexpr (EPI == GE_GELU) p.C[(size_t)m * p.ldc + n] = gelu_tanh(v);
+    else if constexpr (EPI == GE_QKV_CACHE) {
+        const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + t) * D;
+        if (n < D) p.C[(size_t)m * p.ldc + n] = v;
+        else if (n < 2 * D) p.kc[slot + n - D] = v;
+        else p.vc[slot + n - 2 * D] = v;
+    } else if constexpr (EPI == GE_XAKV) {
+        const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.Tmax + t) * DXA;
+        if (n < DXA) p.xak[slot + n] = v;
+        else p.xav[slot + n - DXA] = v;
+    }
+}
+
+// A 4x4 register tile at rows m0.., columns n0..: the epilogue, or (split-K)
+// the raw partial sums into split blockIdx.z's slice of p.part.
 template <int EPI>
 __device__ __forceinline__ void gemm_store(const GemmP &p, const float (&acc)[4][4], int m0, int n0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + i;
         if (m >= p.M) continue;
-        const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int n = n0 + j;
             if (n >= p.N) continue;
-            float v = acc[i][j];
-            if (p.bias) v += p.bias[n];
-            if constexpr (EPI == GE_STORE) p.C[(size_t)m * p.ldc + n] = v;
-            else if constexpr (EPI == GE_RESID) p.C[(size_t)m * p.ldc + n] = v + p.C[(size_t)m * p.ldc + n];
-            else if constexpr (EPI == GE_GELU) p.C[(size_t)m * p.ldc + n] = gelu_tanh(v);
-            else if constexpr (EPI == GE_QKV_CACHE) {
-                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + t) * D;
-                if (n < D) p.C[(size_t)m * p.ldc + n] = v;
-                else if (n < 2 * D) p.kc[slot + n - D] = v;
-                else p.vc[slot + n - 2 * D] = v;
-            } else if constexpr (EPI == GE_XAKV) {
-                const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.Tmax + t) * DXA;
-                if (n < DXA) p.xak[slot + n] = v;
-                else p.xav[slot + n - DXA] = v;
-            }
+            if (p.part) p.part[((size_t)blockIdx.z * p.M + m) * p.N + n] = acc[i][j];
+            else gemm_store1<EPI>(p, m, n, acc[i][j]);
         }
+    }
+}
+
+// Split-K reduction: v = sum of the splits in order, then the epilogue.
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmP p, int splits) {
+    const size_t total = (size_t)p.M * p.N;
+    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (size_t)gridDim.x * 256) {
+        float v = p.part[e];
+        for (int s = 1; s < splits; ++s) v += p.part[(size_t)s * total + e];
+        gemm_store1<EPI>(p, (int)(e / p.N), (int)(e % p.N), v);
     }
 }
 
@@ -59,7 +78,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
     const int tx = tid & 15, ty = tid >> 4;
     float acc[4][4] = {};
     const int lr = tid >> 2, lk = (tid & 3) * 4;  // loader: row lr, k lk..lk+3
-    for (int k0 = 0; k0 < p.K; k0 += BK) {
+    const int ks = p.K / gridDim.z, kbeg = blockIdx.z * ks;  // split-K slice (gridDim.z == 1: all of K)
+    for (int k0 = kbeg; k0 < kbeg + ks; k0 += BK) {
         {   // A tile
             const int m = m0 + lr;
             float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -126,8 +146,9 @@ __global__ __launch_bounds__(256) void gemm_q8_kernel(GemmP p) {
     const int tx = tid & 15, ty = tid >> 4;
     const int lr = tid >> 2, part = tid & 3;  // loader: row lr, elements 8 part .. 8 part + 7 of the block
     const int nblk = p.K / 32;
+    const int bs = nblk / gridDim.z, bbeg = blockIdx.z * bs;  // split-K slice in whole blocks
     float acc[4][4] = {};
-    for (int kb = 0; kb < nblk; ++kb) {
+    for (int kb = bbeg; kb < bbeg + bs; ++kb) {
         const int k0 = kb * 32 + part * 8;
         {   // A rows -> Q8_0
             float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -295,18 +316,34 @@ __global__ void embed_context_kernel(const int *spk, const float *baked, const f
 }
 
 // ---------------------------------------------------------------- launchers
+template <int EPI>
+static hipError_t launch_reduce(const GemmP &p, int splits, hipStream_t s) {
+    const size_t total = (size_t)p.M * p.N;
+    const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3(grid), dim3(256), 0, s, p, splits);
+    return hipGetLastError();
+}
 template <int EPI, int TAPS>
 static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
-    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64);
-    hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, p);
-    return hipGetLastError();
+    const int splits = p.part ? gemm_splits(p.K) : 1;
+    if (p.K % (16 * splits)) return hipErrorInvalidValue;
+    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits);
+    GemmP q = p;
+    if (splits == 1) q.part = nullptr;
+    hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess || splits == 1) return e;
+    return launch_reduce<EPI>(p, splits, s);
 }
 template <int EPI>
 static hipError_t launch_gemm_q8(const GemmP &p, hipStream_t s) {
     if (!p.Wd || p.K % 32 || p.conv_taps) return hipErrorInvalidValue;
-    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64);
-    hipLaunchKernelGGL((gemm_q8_kernel<EPI>), grid, dim3(256), 0, s, p);
-    return hipGetLastError();
+    const int splits = p.part ? gemm_splits(p.K) : 1;
+    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits);
+    GemmP q = p;
+    if (splits == 1) q.part = nullptr;
+    hipLaunchKernelGGL((gemm_q8_kernel<EPI>), grid, dim3(256), 0, s, q);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess || splits == 1) return e;
+    return launch_reduce<EPI>(p, splits, s);
 }
 hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s) {
     if (p.Wq) {

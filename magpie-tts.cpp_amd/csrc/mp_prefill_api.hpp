@@ -32,7 +32,21 @@ struct GemmP {
     int layer, nlayers, max_seq;
     float *xak, *xav;
     int Tmax;
+    // deterministic split-K: with part != nullptr the K range is cut into
+    // gemm_splits(K) pieces (a function of K only, so the arithmetic does not
+    // depend on M, i.e. on the batch), each written raw to part[s][M][N], then
+    // summed in split order by a second launch that applies the epilogue.
+    float *part;
 };
+
+// Split count of a preamble GEMM over K (fixed per K: batch-invariant results).
+inline int gemm_splits(int K) {
+    int s = K / 384;
+    if (s < 1) s = 1;
+    if (s > 16) s = 16;
+    while (s > 1 && (K % (s * 32)) != 0) --s;  // whole 32-wide (Q8_0) blocks per split
+    return s;
+}
 
 // Causal multi-head attention for every (row, head) of a block of rows.
 struct RowAttnP {

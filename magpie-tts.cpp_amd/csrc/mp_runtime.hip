@@ -178,6 +178,7 @@ struct mp_dev {
           *h = nullptr, *hidden = nullptr;
     float *xqb = nullptr;  // Q8 mode: q_net output [NB][128]
     unsigned short *h_b16 = nullptr;  // bf16 mode: GELU(FFN up) as the bf16 FFN-down operand [NB][3072]
+    float *gpart = nullptr;            // preamble split-K partial sums (mp::gemm_splits)
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
@@ -577,6 +578,14 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     const size_t rows = (size_t)NB * std::max(Tmax, mp::CTX);
     A(pX, rows * D); A(pH, rows * D); A(pQKV, rows * 3 * D); A(pATT, rows * D); A(pF, rows * 3072);
     A(pXQ, rows * 128); A(pXAO, rows * 128); A(enc_out, (size_t)NB * Tmax * D);
+    {   // largest S x M x N of the preamble GEMMs (encoder FFN up/down, prefill FFN)
+        const size_t Me = (size_t)NB * Tmax, Mc = (size_t)NB * mp::CTX;
+        size_t cap = 0;
+        auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits(K) * M * N); };
+        need(Me, 2304, 768); need(Me, 3072, 768 * 3); need(Me, 768, 3072 * 3); need(Me, 256, 768);
+        need(Mc, 2304, 768); need(Mc, 3072, 768); need(Mc, 768, 3072); need(Mc, 768, 768);
+        A(gpart, cap);
+    }
 #undef A
     return MP_OK;
 }
@@ -821,6 +830,11 @@ int run_preamble(mp_dev *dev) {
     const int NB = dev->NB, Tmax = dev->Tmax, L = m.dec_layers;
     hipStream_t s = dev->stream;
     const int Me = NB * Tmax;
+    // every preamble GEMM runs split-K over K (deterministic, batch-invariant)
+    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) {
+        gp.part = dev->gpart;
+        return mp::pre_gemm(gp, epi, st);
+    };
     // --- text encoder (magpie_build_full_encoder, 1960-1995)
     HIPCHK(pre_embed_text(dev->tok, dev->T, NB, Tmax, m.text_emb, m.enc_pos, dev->pX, s));
     for (int l = 0; l < m.enc_layers; ++l) {

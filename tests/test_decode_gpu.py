@@ -86,6 +86,23 @@ def test_batch_equals_single(ma, small_model, B):
     dev.close()
 
 
+@pytest.mark.parametrize("weights", ["f32", "bf16", "q8"])
+def test_sampled_batch_equals_single(ma, small_model, q8_model, weights):
+    """Sampling is what exposes ulp-level batch variance (a near-tie in the top-k
+    order flips a draw), so a sampled batch over many frames must reproduce each
+    utterance run alone bit for bit: codes, decoder hidden, every codebook draw."""
+    path = q8_model if weights == "q8" else small_model
+    toks = [ma.synthetic_tokens(9 + 7 * b, seed=3000 + b) for b in range(4)]
+    kw = dict(max_dec_steps=96, temperature=0.7, top_k=80, seed=17, ignore_eos=True, trace=True)
+    dev = ma.Device(path, weights=weights)
+    rb = dev.synthesize(toks, speakers=[0, 1, 2, 3], **kw)
+    for b in range(4):
+        rs = dev.synthesize([toks[b]], speakers=[b], stream_base=b, **kw)
+        assert np.array_equal(rb.codes[b], rs.codes[0]), f"slot {b}"
+        assert np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b} hidden"
+    dev.close()
+
+
 def test_q8_model_loads_and_matches_oracle(ma, oracle, q8_model):
     """Q8_0 attention/LT projections (convert_magpie_to_gguf.py:155-176) are
     dequantised on load; the oracle dequantises the same blocks."""

@@ -285,6 +285,11 @@ def main() -> None:
                "kind": "port",
                "sample": f"1 utterance x {res['frames']} frames (T={args.tokens}), decode loop only "
                          f"(preamble {res['preamble_s']:.2f}s excluded), oracle f32-accumulate mode"}
+        # also at every core this process may use (the box's CPU share)
+        nall = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+        if nall != args.cpu_threads:
+            ra = orc.time_decode_fps(model_path, toks[0], args.frames, threads=nall, acc64=False)
+            cpu["all_cores"] = {"value": round(ra["frames"] / ra["decode_s"], 2), "cores": nall}
 
     # ---- the other BASELINE configs' shapes on this GPU (rank 0 at N=1 only)
     extra = None

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const float v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
     const int n = rt * 16 + row;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, col);
+    epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? ((const int *)sc)[col] : 0);
 }
 
 template <int PRO, int EPI>
@@ -162,13 +162,14 @@ static bool b16_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
     if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
-    if constexpr (PRO == PRO_LTARG_LN)
-        ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step && p.smp.cfg && p.smp.argeos;
+    if constexpr (PRO == PRO_LTARG_ATTN)
+        ok &= p.logits && p.codes_cur && p.qkvtab && p.lk && p.lv && p.ltk && p.ltv && p.step && p.smp.cfg && p.smp.argeos;
     if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
     if constexpr (EPI == EPI_GELU_B16) ok &= p.out_b16 != nullptr;
     if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
     if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
+    if constexpr (EPI == EPI_LTX_ADD) ok &= p.out && p.ptab && p.lt_pos && p.cb >= 1;
     if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
     return ok;
@@ -188,7 +189,7 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_B16>(p, s); }     \
     hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE>(p, s); }  \
     hipError_t b16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
-    hipError_t b16_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \
+    hipError_t b16_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_ATTN, EPI_LTX_ADD>(p, s); } \
     hipError_t b16_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
     hipError_t b16_lt_c_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LN, EPI_GELU>(p, s); }         \
     hipError_t b16_lt_d_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTF, PRO_PLAIN, EPI_ADD_STORE>(p, s); } \

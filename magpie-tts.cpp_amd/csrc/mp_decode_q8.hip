@@ -109,7 +109,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_q8_kernel(GemvP p) {
     if (lane >= R * NB) return;
     const int b = lane % NB, n = row0 + lane / NB;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, b);
+    epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? ((const int *)sc)[b] : 0);
 }
 
 // ---------------------------------------------------------------- fused Q8 XA tail
@@ -251,12 +251,13 @@ static bool q8_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
     if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
-    if constexpr (PRO == PRO_LTARG_LN)
-        ok &= p.logits && p.codes_cur && p.ptab && p.lt_pos && p.ltX && p.lnw && p.step && p.smp.cfg && p.smp.argeos;
+    if constexpr (PRO == PRO_LTARG_ATTN)
+        ok &= p.logits && p.codes_cur && p.qkvtab && p.lk && p.lv && p.ltk && p.ltv && p.step && p.smp.cfg && p.smp.argeos;
     if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
     if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
     if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
+    if constexpr (EPI == EPI_LTX_ADD) ok &= p.out && p.ptab && p.lt_pos && p.cb >= 1;
     if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
     return ok;
@@ -280,7 +281,7 @@ static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     hipError_t q8_xq_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_STORE>(p, s); }            \
     hipError_t q8_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_BIAS>(p, s); }         \
     hipError_t q8_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
-    hipError_t q8_lt_ag_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LTARG_LN, EPI_LTQKV>(p, s); } \
+    hipError_t q8_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LTARG_ATTN, EPI_LTX_ADD>(p, s); } \
     hipError_t q8_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
     hipError_t q8_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_PLAIN, EPI_BIAS>(p, s); }
 

@@ -14,39 +14,6 @@ namespace mp {
 // ---------------------------------------------------------------- prologues
 // Each prologue fills act[NB][K] (LDS) with the activation vector of every slot.
 
-// Masked first-max argmax of slot b's logits (magpie.cpp:1133-1145, 1243-1259):
-// 2016 and 2018..2023 always forbidden, 2017 (EOS) too while step < 4 or in
-// fixed-length mode. Every thread returns the winner.
-__device__ __forceinline__ int block_masked_argmax(const GemvP &p, int b, float *red) {
-    const int tid = threadIdx.x;
-    const float *lg = p.logits + (size_t)b * VCB;
-    const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
-    constexpr int R = (VCB + MP_BLOCK - 1) / MP_BLOCK;
-    float lv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = tid + MP_BLOCK * r;
-        lv[r] = i < VCB ? lg[i] : -INFINITY;
-    }
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = tid + MP_BLOCK * r;
-        float v = lv[r];
-        if (i >= VCB || (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos))) v = -INFINITY;
-        argmax_merge(bv, bi, v, i);
-    }
-    wave_argmax(bv, bi);
-    if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
-    lds_sync();
-    float v0 = red[0];
-    int i0 = ((int *)red)[4];
-    for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
-    lds_sync();
-    if (i0 < 0 || i0 >= VCB) i0 = 0;  // all -inf / NaN: the reference's argmax stays 0
-    return i0;
-}
 
 // One wave picks slot b's code for codebook `cb` of this frame: masked first-max
 // argmax (always, for EOS detection, magpie.cpp:1250-1259), and at temperature
@@ -176,11 +143,52 @@ __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos,
     return wave_pick_v(lv, forbid_eos, audio_bos, audio_eos, smp, stream, step, cb, scratch, amax);
 }
 
+// PRO_LTARG_ATTN keeps each slot's drawn code in sc[0..NB) (the EPI_LTX_ADD
+// epilogue adds that code's residual row); the wave pick scratch follows
+template <int NB>
+constexpr int ltc_off() { return (NB + 15) / 16 * 16; }
+
+// Causal 1-head attention of LT position cb over positions 0..cb for slot b,
+// one wave: lane l owns elements 4l..4l+3; scores are wave-wide DPP sums
+// (softmax(K q / 16) V, magpie.cpp:965-966). Position cb's k/v come from
+// registers when CUR (gathered this launch), from ltk/ltv otherwise; the
+// arithmetic is the same either way, at every batch size.
+template <bool CUR>
+__device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4) {
+    const int lane = threadIdx.x & 63;
+    const int nk = p.cb + 1;
+    float sj[NCB];
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+        if (j < nk) {
+            const float4 k4 = (CUR && j == p.cb) ? kc4 : *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane);
+            sj[j] = wave_sum(dotv(q4, k4)) * (1.0f / 16.0f);
+        } else {
+            sj[j] = -INFINITY;
+        }
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) m = fmaxf(m, sj[j]);
+    float l = 0.f;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+        if (j < nk) {
+            const float e = expf(sj[j] - m);
+            l += e;
+            const float4 v4 = (CUR && j == p.cb) ? vc4 : *(const float4 *)(p.ltv + ((size_t)b * NCB + j) * LTD + 4 * lane);
+            a.x = fmaf(e, v4.x, a.x); a.y = fmaf(e, v4.y, a.y); a.z = fmaf(e, v4.z, a.z); a.w = fmaf(e, v4.w, a.w);
+        }
+    }
+    return make_float4(a.x / l, a.y / l, a.z / l, a.w / l);
+}
+
 // LDS scratch (floats) a prologue needs besides the activation rows
 template <int NB, int PRO>
 constexpr int pro_scratch() {
     return PRO == PRO_LT_ATTN ? 16
-           : PRO == PRO_LTARG_LN ? (NB < MP_NWAVES ? NB : MP_NWAVES) * 2 * VCB
+           : PRO == PRO_LTARG_ATTN ? ltc_off<NB>() + (NB < MP_NWAVES ? NB : MP_NWAVES) * 2 * VCB
            : PRO == PRO_SA_MERGE ? NB * NH * (SA_SPLITS + 1)
            : PRO == PRO_XA_LN ? NB * (XA_SPLITS + 1)
            : 1;
@@ -453,84 +461,49 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * p.lnw[lane + 64 * i];
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_LTARG_LN && NB >= 2) {
-        // wave w owns slots w, w+4, ...: all their logits are loaded before the first pick,
-        // all table rows gathered before the first LayerNorm (one latency per phase)
+    } else if constexpr (PRO == PRO_LTARG_ATTN) {
+        // wave w owns slots w, w+4, ... at every batch size: pick codebook cb-1's code
+        // (the next slot's logits already in flight), gather q|k|v of position cb from
+        // the load-time table, attend over positions 0..cb
+        static_assert(K == LTD, "LT is 256 wide");
         const int lane = tid & 63, w = tid >> 6;
-        constexpr int SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
+        int *scode = (int *)sc;
+        float *wsc = sc + ltc_off<NB>() + w * 2 * VCB;
         float cur[PICK_R], nxt[PICK_R];
         if (w < NB) load_logits(p.logits + (size_t)w * VCB, cur);
-        unsigned long long codes = 0ull;  // 16 bits per slot of this wave (codes < 2048)
-        for (int j = 0; j < SPW; ++j) {
-            const int b = w + MP_NWAVES * j;
-            if (b >= NB) break;  // wave-uniform
+        for (int b = w; b < NB; b += MP_NWAVES) {  // wave-uniform
             const int bn = b + MP_NWAVES;
-            if (bn < NB) load_logits(p.logits + (size_t)bn * VCB, nxt);  // next slot's logits in flight
+            if (bn < NB) load_logits(p.logits + (size_t)bn * VCB, nxt);
             int amax;
             const int code = wave_pick_v(cur, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos, p.smp, b,
-                                         p.step[b], p.cb - 1, sc + w * 2 * VCB, amax);
-            if (blockIdx.x == 0 && lane == 0) {
-                p.codes_cur[b * NCB + p.cb - 1] = code;
-                if (amax == p.audio_eos) p.smp.argeos[b] = 1;
-                if (p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
+                                         p.step[b], p.cb - 1, wsc, amax);
+            if (lane == 0) {
+                scode[b] = code;
+                if (blockIdx.x == 0) {
+                    p.codes_cur[b * NCB + p.cb - 1] = code;
+                    if (amax == p.audio_eos) p.smp.argeos[b] = 1;
+                    if (p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
+                }
             }
-            codes |= (unsigned long long)code << (16 * j);
+            const float *row = p.qkvtab + ((size_t)(p.cb - 1) * VCB + code) * (3 * LTD) + 4 * lane;
+            const float4 q4 = *(const float4 *)row, k4 = *(const float4 *)(row + LTD),
+                         v4 = *(const float4 *)(row + 2 * LTD);
+            if (blockIdx.x == 0) {  // position cb's k/v for the later codebooks
+                *(float4 *)(p.lk + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = k4;
+                *(float4 *)(p.lv + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = v4;
+            }
+            *(float4 *)(act + b * K + 4 * lane) = lt_attend<true>(p, b, q4, k4, v4);
 #pragma unroll
             for (int r = 0; r < PICK_R; ++r) cur[r] = nxt[r];
         }
-        int code[SPW];
-#pragma unroll
-        for (int j = 0; j < SPW; ++j) code[j] = (int)((codes >> (16 * j)) & 0xffffull);
-        float X[SPW][4];
-#pragma unroll
-        for (int j = 0; j < SPW; ++j) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int k = lane + 64 * i;
-                X[j][i] = p.ptab[((size_t)(p.cb - 1) * VCB + code[j]) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < SPW; ++j) {
-            const int b = w + MP_NWAVES * j;
-            if (b >= NB) continue;
-            if (blockIdx.x == 0)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) p.ltX[(size_t)b * LTD + lane + 64 * i] = X[j][i];
-            float mean, var;
-            wave_block_meanvar<1>(X[j], mean, var);
-            const float rstd = 1.0f / sqrtf(var + p.eps);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[j][i] - mean) * rstd) * p.lnw[lane + 64 * i];
-        }
         lds_sync();
     } else if constexpr (PRO == PRO_LT_ATTN) {
-        // wave w owns slots w, w+4, ... at every batch size (batch 1 included), so a
-        // slot's attention is the same instruction sequence whatever the batch
+        // codebook 0 (q|k|v from the lt_a GEMV): the same per-slot wave code
+        static_assert(K == LTD, "LT is 256 wide");
         const int lane = tid & 63, w = tid >> 6;
-        const int nk = p.cb + 1;
         for (int b = w; b < NB; b += MP_NWAVES) {
             const float4 q4 = *(const float4 *)(p.ltq + (size_t)b * LTD + 4 * lane);
-            float sj[NCB];
-#pragma unroll
-            for (int j = 0; j < NCB; ++j)
-                sj[j] = j < nk ? wave_sum(dotv(q4, *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane))) *
-                                     (1.0f / 16.0f)
-                               : -INFINITY;
-            float m = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < NCB; ++j) m = fmaxf(m, sj[j]);
-            float l = 0.f;
-            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int j = 0; j < NCB; ++j) {
-                if (j >= nk) break;
-                const float e = expf(sj[j] - m);
-                l += e;
-                const float4 v4 = *(const float4 *)(p.ltv + ((size_t)b * NCB + j) * LTD + 4 * lane);
-                a.x = fmaf(e, v4.x, a.x); a.y = fmaf(e, v4.y, a.y); a.z = fmaf(e, v4.z, a.z); a.w = fmaf(e, v4.w, a.w);
-            }
-            *(float4 *)(act + b * K + 4 * lane) = make_float4(a.x / l, a.y / l, a.z / l, a.w / l);
+            *(float4 *)(act + b * K + 4 * lane) = lt_attend<false>(p, b, q4, q4, q4);
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LTX_LN) {
@@ -546,46 +519,12 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_LTARG_LN) {
-        static_assert(K == LTD, "LT is 256 wide");
-        const int lane = tid & 63, w = tid >> 6;
-        for (int b = 0; b < NB; ++b) {
-            int code;
-            if (p.smp.on) {
-                if (w == 0) {
-                    int amax;
-                    code = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos,
-                                     p.audio_eos, p.smp, b, p.step[b], p.cb - 1, sc, amax);
-                    if (lane == 0) {
-                        red[0] = __int_as_float(code);
-                        if (blockIdx.x == 0 && amax == p.audio_eos) p.smp.argeos[b] = 1;
-                        if (blockIdx.x == 0 && p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
-                    }
-                }
-                lds_sync();
-                code = __float_as_int(red[0]);
-                lds_sync();
-            } else {
-                code = block_masked_argmax(p, b, red);  // codebook cb-1's code
-                if (blockIdx.x == 0 && tid == 0 && p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = code;
-            }
-            if (blockIdx.x == 0 && tid == 0) p.codes_cur[b * NCB + p.cb - 1] = code;
-            const int k = tid;
-            const float X = p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
-            if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X;
-            const float xv[1] = {X};
-            float mean, var;
-            block_meanvar<1>(xv, red, mean, var);
-            const float rstd = 1.0f / sqrtf(var + p.eps);
-            act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
-        }
-        lds_sync();
     }
 }
 
 // Epilogue of output (row n, slot b) of a fused projection.
 template <int EPI>
-__device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b) {
+__device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b, int code = 0) {
     if constexpr (EPI == EPI_STORE) p.out[(size_t)b * p.out_ld + n] = v;
     else if constexpr (EPI == EPI_BIAS) p.out[(size_t)b * p.out_ld + n] = v + p.bias[n];
     else if constexpr (EPI == EPI_GELU) p.out[(size_t)b * p.out_ld + n] = gelu_tanh(v);
@@ -595,6 +534,9 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b)
     }
     else if constexpr (EPI == EPI_RESID) p.resid[(size_t)b * D + n] = v + p.resid[(size_t)b * D + n];
     else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
+    else if constexpr (EPI == EPI_LTX_ADD)
+        p.out[(size_t)b * p.out_ld + n] =
+            v + (p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + n] + p.lt_pos[(size_t)p.cb * LTD + n]);
     else if constexpr (EPI == EPI_QKV) {
         const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + p.pos[b]) * D;
         if (n < D) p.out[(size_t)b * D + n] = v;

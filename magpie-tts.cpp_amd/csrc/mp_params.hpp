@@ -33,9 +33,11 @@ enum Pro {
     PRO_EMBED_LN = 2,   // x = sum_cb emb[cb][code]/8 + pos; act = LN(x)*lnw (2746-2787, 4376-4379)
     PRO_LTX_LN = 5,     // X = s_cb + lt_pos[cb]; act = LN(X)*lnw       (1015-1034, 946-958)
     PRO_LT_ATTN = 6,    // act = causal 1x256 attention over LT positions 0..cb (965-966)
-    PRO_LTARG_LN = 8,   // code_{cb-1} = masked argmax(logits); X = P[cb-1][code] + lt_pos[cb];
-                        // act = LN(X)*lnw, with P[c][v] = in_proj(audio_emb[c][v]) + b
-                        // precomputed at load (1274-1313 depend only on (c, v))
+    PRO_LTARG_ATTN = 8, // cb >= 1: code_{cb-1} = top-k draw / masked argmax of the logits; q|k|v of
+                        // LT position cb = Q[cb-1][code], gathered; act = PRO_LT_ATTN's attention.
+                        // Q[c][v] = qkv_net(LN(P[c][v] + lt_pos[c+1])) and P[c][v] =
+                        // in_proj(audio_emb[c][v]) + b depend only on (c, v) (magpie.cpp:1274-1313,
+                        // 946-958): both tables are built at load
     PRO_SA_MERGE = 9,   // act = SA output: the SA_SPLITS partial softmax states of each head merged
     PRO_XA_LN = 10,     // x2 = src + XA output (XA_SPLITS partial states merged), block 0 stores
                         // x2 to xres; act = LN(x2)*lnw              (3513-3525)
@@ -50,6 +52,7 @@ enum Epi {
     EPI_LTQKV = 5,      // q -> lq, k/v -> LT position cb
     EPI_ADD_STORE = 6,  // out = v + addsrc
     EPI_GELU_B16 = 7,   // out_b16 = bf16(gelu(v)): the bf16 FFN-down operand, rounded once here
+    EPI_LTX_ADD = 8,    // out = v + (P[cb-1][code] + lt_pos[cb]): LT residual of PRO_LTARG_ATTN's code
 };
 
 // Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
@@ -107,6 +110,7 @@ struct GemvP {
     int layer, nlayers;
     const float *lt_s;   // [B][9][256]
     const float *ptab;   // [8][2024][256] in_proj(audio_emb) + b
+    const float *qkvtab; // [7][2024][768] LT q|k|v of codebook c's code v at position c+1
     int cb;
     const float *lt_pos;
     float *ltX;

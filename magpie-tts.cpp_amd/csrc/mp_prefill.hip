@@ -315,6 +315,26 @@ __global__ void embed_context_kernel(const int *spk, const float *baked, const f
     for (int k = threadIdx.x; k < D; k += blockDim.x) X[(size_t)m * D + k] = src[k] + dec_pos[(size_t)t * D + k];
 }
 
+// LT table rows (see pre_lt_tab_rows): one 256-thread block per row, the
+// block statistics PRO_LTARG_ATTN's per-wave statistics reproduce
+__global__ __launch_bounds__(256) void lt_tab_rows_kernel(const float *P, const float *lt_pos, const float *w, float eps,
+                                                          float *Y, int b16) {
+    __shared__ float red[8];
+    const int r = blockIdx.x, k = threadIdx.x, cb = r / VCB + 1;
+    const float X = P[(size_t)r * LTD + k] + lt_pos[(size_t)cb * LTD + k];
+    const float xv[1] = {X};
+    float mean, var;
+    block_meanvar<1>(xv, red, mean, var);
+    const float rstd = 1.0f / sqrtf(var + eps);
+    float y = ((X - mean) * rstd) * w[k];
+    if (b16) y = (float)(__bf16)y;
+    Y[(size_t)r * LTD + k] = y;
+}
+__global__ void round_bf16_kernel(const float *src, float *dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        dst[i] = (float)(__bf16)src[i];
+}
+
 // ---------------------------------------------------------------- launchers
 template <int EPI>
 static hipError_t launch_reduce(const GemmP &p, int splits, hipStream_t s) {
@@ -371,6 +391,16 @@ hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s) {
 }
 hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ldy, int M, float eps, hipStream_t s) {
     hipLaunchKernelGGL(ln_rows_kernel, dim3(M), dim3(256), 0, s, X, ldx, w, Y, ldy, eps);
+    return hipGetLastError();
+}
+hipError_t pre_lt_tab_rows(const float *P, const float *lt_pos, const float *w, float eps, float *Y, bool b16,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(lt_tab_rows_kernel, dim3(7 * VCB), dim3(256), 0, s, P, lt_pos, w, eps, Y, (int)b16);
+    return hipGetLastError();
+}
+hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s) {
+    hipLaunchKernelGGL(round_bf16_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, s, src,
+                       dst, n);
     return hipGetLastError();
 }
 hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s) {

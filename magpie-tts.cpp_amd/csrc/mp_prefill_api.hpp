@@ -71,6 +71,12 @@ struct RowXaP {
 
 hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s);
 hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ldy, int M, float eps, hipStream_t s);
+// LT table rows: Y[r] = LN(P[r] + lt_pos[r / VCB + 1]) * w for r < 7 * VCB (the LN of
+// PRO_LTARG_ATTN's position, bit for bit), rounded to bf16 when `b16`
+hipError_t pre_lt_tab_rows(const float *P, const float *lt_pos, const float *w, float eps, float *Y, bool b16,
+                           hipStream_t s);
+// dst = bf16(src) held as f32 (a bf16-mode weight for an f32 GEMM)
+hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s);
 hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s);
 hipError_t pre_row_xa(const RowXaP &p, hipStream_t s);
 hipError_t pre_embed_text(const int *tok, const int *T, int B, int Tmax, const float *te, const float *ep, float *X,

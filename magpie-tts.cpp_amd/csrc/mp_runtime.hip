@@ -34,7 +34,7 @@ using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
     hipError_t op_ff1x_##NB(const GemvP &, hipStream_t);                                                                \
     hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
     hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
-    hipError_t op_lt_ag_##NB(const GemvP &, hipStream_t);                                                              \
+    hipError_t op_lt_bg_##NB(const GemvP &, hipStream_t);                                                              \
     hipError_t op_lt_c_##NB(const GemvP &, hipStream_t); hipError_t op_lt_d_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_lt_e_##NB(const GemvP &, hipStream_t);
 MP_DECL_OPS(1)
@@ -46,7 +46,7 @@ hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
     hipError_t b16_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t b16_qkv_##NB(const GemvP &, hipStream_t);      \
     hipError_t b16_oproj_##NB(const GemvP &, hipStream_t); hipError_t b16_ff1_##NB(const GemvP &, hipStream_t);          \
     hipError_t b16_ff2_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_a_##NB(const GemvP &, hipStream_t);           \
-    hipError_t b16_lt_ag_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_b_##NB(const GemvP &, hipStream_t);         \
+    hipError_t b16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_b_##NB(const GemvP &, hipStream_t);         \
     hipError_t b16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_d_##NB(const GemvP &, hipStream_t);          \
     hipError_t b16_lt_e_##NB(const GemvP &, hipStream_t);
 MP_DECL_B16(1)
@@ -59,7 +59,7 @@ hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t);
     hipError_t q8_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t q8_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t q8_oproj_##NB(const GemvP &, hipStream_t); hipError_t q8_xq_##NB(const GemvP &, hipStream_t);             \
     hipError_t q8_lt_in0_##NB(const GemvP &, hipStream_t);                                                             \
-    hipError_t q8_lt_a_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_ag_##NB(const GemvP &, hipStream_t);           \
+    hipError_t q8_lt_a_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_bg_##NB(const GemvP &, hipStream_t);           \
     hipError_t q8_lt_b_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_e_##NB(const GemvP &, hipStream_t);
 MP_DECL_Q8(1)
 MP_DECL_Q8(2)
@@ -78,20 +78,20 @@ hipError_t op_finalize(const FinP &, int, hipStream_t);
 namespace mp {
 
 // ff1: LN(x2) prologue (x2 materialised: Q8 unfused XA); ff1x: the fused XA's split states merged into x2 first
-struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_ag, lt_b, lt_c, lt_d, lt_e; };
+struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e; };
 #define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
-                       op_lt_in0_##NB, op_lt_a_##NB, op_lt_ag_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
+                       op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
 static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
 #define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, nullptr, b16_ff1_##NB, b16_ff2_##NB, \
-                           op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_ag_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
+                           op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_bg_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
                            b16_lt_d_##NB, b16_lt_e_##NB }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
-struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, lt_in0, lt_a, lt_ag, lt_b, lt_e; };
+struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, lt_in0, lt_a, lt_bg, lt_b, lt_e; };
 #define MP_TABLE_Q8(NB) { q8_qkv_embed_##NB, q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_lt_in0_##NB, \
-                          q8_lt_a_##NB, q8_lt_ag_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
+                          q8_lt_a_##NB, q8_lt_bg_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
 static const OpTableQ8 kTablesQ8[4] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8)};
 static int nb_index(int NB) { return NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : NB == 8 ? 3 : 4; }
 static const OpTable &table_for(int NB, bool b16) { return b16 ? kTablesB16[nb_index(NB)] : kTables[nb_index(NB)]; }
@@ -121,6 +121,7 @@ struct Model {
     const float *lt_in_w, *lt_in_b, *lt_pos, *lt_norm_self, *lt_qkv, *lt_o, *lt_norm_ff, *lt_ff1, *lt_ff2, *lt_out_w,
         *lt_out_b;
     float *lt_ptab = nullptr;  // [8][2024][256] = in_proj(audio_emb[c][v]) + b, built at load
+    float *lt_qkvtab = nullptr;  // [7][2024][768] = qkv_net(LN(ptab[c][v] + lt_pos[c+1])), built at load
     std::vector<float *> xq_t;  // per layer W_q^T [768][128] (for K' = K W_q)
     // weight mode MP_WEIGHTS_BF16: decode projections repacked as bf16 MFMA fragments
     int weight_mode = 0;
@@ -447,7 +448,7 @@ int load_model(mp_dev *dev, const char *path) {
 // P[c][v] = in_proj(audio_emb[c][v]) + b: the LT's per-codebook re-embedding
 // (magpie.cpp:1274-1313) depends only on (c, v) -> one GEMM at load time (with
 // ggml's Q8_0 arithmetic when in_proj is a Q8_0 tensor in Q8 mode).
-int build_ptab(mp_dev *dev) {
+int build_ptab(mp_dev *dev, int weight_mode) {
     mp::Model &m = dev->m;
     if (m.lt_ptab) { hipFree(m.lt_ptab); m.lt_ptab = nullptr; }
     HIPCHK(hipMalloc(&m.lt_ptab, (size_t)8 * 2024 * 256 * 4));
@@ -455,7 +456,30 @@ int build_ptab(mp_dev *dev) {
     gp.A = m.audio_emb; gp.lda = 768; gp.W = m.lt_in_w; gp.Wq = m.lt_in8.q; gp.Wd = m.lt_in8.d; gp.bias = m.lt_in_b;
     gp.C = m.lt_ptab; gp.ldc = 256; gp.M = 8 * 2024; gp.N = 256; gp.K = 768; gp.rows_per_utt = 8 * 2024;
     HIPCHK(mp::pre_gemm(gp, mp::GE_STORE, dev->stream));
-    HIPCHK(hipStreamSynchronize(dev->stream));
+    // LT q|k|v of position c+1 for every code v of codebook c < 7: the rows PRO_LTARG_ATTN
+    // gathers instead of running the q|k|v GEMV per codebook. The projection uses the
+    // weights the decode-time GEMV would (f32, Q8_0 with activations quantised per
+    // block, or bf16 weights and bf16 activations, f32 accumulation).
+    if (m.lt_qkvtab) { hipFree(m.lt_qkvtab); m.lt_qkvtab = nullptr; }
+    const size_t R = (size_t)7 * 2024;
+    HIPCHK(hipMalloc(&m.lt_qkvtab, R * 768 * 4));
+    float *rows = nullptr, *wq = nullptr;
+    HIPCHK(hipMalloc(&rows, R * 256 * 4));
+    const bool b16 = weight_mode == MP_WEIGHTS_BF16;
+    HIPCHK(mp::pre_lt_tab_rows(m.lt_ptab, m.lt_pos, m.lt_norm_self, m.eps, rows, b16, dev->stream));
+    if (b16) {
+        HIPCHK(hipMalloc(&wq, (size_t)768 * 256 * 4));
+        HIPCHK(mp::pre_round_bf16(m.lt_qkv, wq, (size_t)768 * 256, dev->stream));
+    }
+    gp = mp::GemmP{};
+    gp.A = rows; gp.lda = 256; gp.W = b16 ? wq : m.lt_qkv; gp.Wq = m.lt_qkv8.q; gp.Wd = m.lt_qkv8.d;
+    gp.C = m.lt_qkvtab; gp.ldc = 768; gp.M = (int)R; gp.N = 768; gp.K = 256; gp.rows_per_utt = (int)R;
+    const hipError_t ge = mp::pre_gemm(gp, mp::GE_STORE, dev->stream);
+    const hipError_t se = hipStreamSynchronize(dev->stream);
+    hipFree(rows);
+    if (wq) hipFree(wq);
+    HIPCHK(ge);
+    HIPCHK(se);
     return MP_OK;
 }
 
@@ -770,27 +794,36 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         }
     }
     for (int cb = 0; cb < 8; ++cb) {
-        // cb > 0: codebook cb-1's pick (argmax / top-k draw) + table gather fused into this prologue
-        mp::GemvP g = base();
-        g.cb = cb;
-        g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX;
-        g.Wq = m.lt_qkv8.q; g.Wd = m.lt_qkv8.d;
-        g.lnw = m.lt_norm_self; g.lq = io.ltq; g.lk = io.ltk; g.lv = io.ltv;
-        if (cb > 0) { g.logits = io.logits; g.codes_cur = io.codes_cur; g.ptab = m.lt_ptab; }
-        {
-            const mp::GemvFn fn = m.lt_qkv8 ? (cb == 0 ? tq.lt_a : tq.lt_ag) : (cb == 0 ? tb.lt_a : tb.lt_ag);
-            if ((rc = run(cb == 0 ? "lt_a" : "lt_ag", fn, g,
-                          (m.lt_qkv8 ? Fq : F) * (768.0 * 256) + A * act * ((256 * 3 + 768 + (cb > 0 ? 2024 + 256 : 256))))) !=
-                MP_OK)
+        mp::GemvP g;
+        if (cb == 0) {
+            // position 0 (the hidden's in_proj): LN + q|k|v GEMV, then attention + o_net
+            g = base(); g.cb = 0;
+            g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX;
+            g.Wq = m.lt_qkv8.q; g.Wd = m.lt_qkv8.d;
+            g.lnw = m.lt_norm_self; g.lq = io.ltq; g.lk = io.ltk; g.lv = io.ltv;
+            if ((rc = run("lt_a", m.lt_qkv8 ? tq.lt_a : tb.lt_a, g,
+                          (m.lt_qkv8 ? Fq : F) * (768.0 * 256) + A * act * (256 * 3 + 768 + 256))) != MP_OK)
+                return rc;
+            g = base(); g.cb = 0;
+            g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = io.ltq; g.ltk = io.ltk; g.ltv = io.ltv; g.out = io.ltY;
+            g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
+            g.out_ld = 256; g.addsrc = io.ltX;
+            if ((rc = run("lt_b", m.lt_o8 ? tq.lt_b : tb.lt_b, g,
+                          (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * (256 * 5))) != MP_OK)
+                return rc;
+        } else {
+            // position cb: codebook cb-1's pick, its q|k|v row gathered from the load-time
+            // table (no q|k|v GEMV), attention + o_net + residual, one launch
+            g = base(); g.cb = cb;
+            g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.out = io.ltY; g.out_ld = 256;
+            g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
+            g.logits = io.logits; g.codes_cur = io.codes_cur; g.qkvtab = m.lt_qkvtab; g.ptab = m.lt_ptab;
+            g.lt_pos = m.lt_pos; g.ltk = io.ltk; g.ltv = io.ltv; g.lk = io.ltk; g.lv = io.ltv;
+            if ((rc = run("lt_bg", m.lt_o8 ? tq.lt_bg : tb.lt_bg, g,
+                          (m.lt_o8 ? Fq : F) * (256.0 * 256) +
+                              A * act * (2024 + 3 * 256 + 2 * 256 * cb + 2 * 256 + 256))) != MP_OK)
                 return rc;
         }
-        g = base(); g.cb = cb;
-        g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = io.ltq; g.ltk = io.ltk; g.ltv = io.ltv; g.out = io.ltY;
-        g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
-        g.out_ld = 256; g.addsrc = io.ltX;
-        if ((rc = run("lt_b", m.lt_o8 ? tq.lt_b : tb.lt_b, g,
-                      (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * ((256 * (2 * cb + 5))))) != MP_OK)
-            return rc;
         g = base(); g.cb = cb;
         g.W = m.lt_ff1; g.Wb = m.pk_lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = io.ltY; g.src_ld = 256;
         g.out = io.ltf; g.out_ld = 1024;
@@ -981,7 +1014,7 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     } else if (weight_mode == MP_WEIGHTS_Q8) {
         if (int rc = load_q8(dev, path)) return rc;
     }
-    if (int rc = build_ptab(dev)) return rc;
+    if (int rc = build_ptab(dev, weight_mode)) return rc;
     dev->m.weight_mode = weight_mode;
     dev->loaded = true;
     return MP_OK;
@@ -1006,6 +1039,7 @@ void mp_hip_free(mp_dev *dev) {
     free_batch(dev);
     if (dev->m.arena) hipFree(dev->m.arena);
     if (dev->m.lt_ptab) hipFree(dev->m.lt_ptab);
+    if (dev->m.lt_qkvtab) hipFree(dev->m.lt_qkvtab);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
     if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
     for (void *p : dev->lt_allocs) hipFree(p);

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     if (lane >= RW * NB) return;
     const int b = lane % NB, n = row0 + lane / NB;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? ((const int *)sc)[b] : 0);
+    epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
 }
 
 // ---------------------------------------------------------------- SA decode attention

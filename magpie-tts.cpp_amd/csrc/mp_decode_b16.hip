@@ -147,7 +147,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const float v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
     const int n = rt * 16 + row;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? ((const int *)sc)[col] : 0);
+    epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
 }
 
 template <int PRO, int EPI>

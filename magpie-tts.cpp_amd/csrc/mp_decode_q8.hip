@@ -109,7 +109,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_q8_kernel(GemvP p) {
     if (lane >= R * NB) return;
     const int b = lane % NB, n = row0 + lane / NB;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? ((const int *)sc)[b] : 0);
+    epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
 }
 
 // ---------------------------------------------------------------- fused Q8 XA tail

@@ -143,25 +143,28 @@ __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos,
     return wave_pick_v(lv, forbid_eos, audio_bos, audio_eos, smp, stream, step, cb, scratch, amax);
 }
 
-// PRO_LTARG_ATTN keeps each slot's drawn code in sc[0..NB) (the EPI_LTX_ADD
-// epilogue adds that code's residual row); the wave pick scratch follows
+// PRO_LTARG_ATTN keeps each slot's residual row X = P[cb-1][code] + lt_pos[cb] in
+// sc[b*LTD ..] (the EPI_LTX_ADD epilogue adds it); the wave pick scratch follows.
 template <int NB>
-constexpr int ltc_off() { return (NB + 15) / 16 * 16; }
+constexpr int ltc_off() { return NB * LTD; }
 
 // Causal 1-head attention of LT position cb over positions 0..cb for slot b,
 // one wave: lane l owns elements 4l..4l+3; scores are wave-wide DPP sums
-// (softmax(K q / 16) V, magpie.cpp:965-966). Position cb's k/v come from
-// registers when CUR (gathered this launch), from ltk/ltv otherwise; the
+// (softmax(K q / 16) V, magpie.cpp:965-966). Position cb's k/v are kc4/vc4
+// (gathered this launch) when CUR, else row cb of ltk/ltv; earlier positions come
+// from kr/vr when PRE (loaded ahead by the caller), else from ltk/ltv. The
 // arithmetic is the same either way, at every batch size.
-template <bool CUR>
-__device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4) {
+template <bool CUR, bool PRE>
+__device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4,
+                                            const float4 (&kr)[NCB], const float4 (&vr)[NCB]) {
     const int lane = threadIdx.x & 63;
     const int nk = p.cb + 1;
+    const float *kb = p.ltk + (size_t)b * NCB * LTD + 4 * lane, *vb = p.ltv + (size_t)b * NCB * LTD + 4 * lane;
     float sj[NCB];
 #pragma unroll
     for (int j = 0; j < NCB; ++j) {
         if (j < nk) {
-            const float4 k4 = (CUR && j == p.cb) ? kc4 : *(const float4 *)(p.ltk + ((size_t)b * NCB + j) * LTD + 4 * lane);
+            const float4 k4 = (CUR && j == p.cb) ? kc4 : PRE ? kr[j] : *(const float4 *)(kb + j * LTD);
             sj[j] = wave_sum(dotv(q4, k4)) * (1.0f / 16.0f);
         } else {
             sj[j] = -INFINITY;
@@ -177,7 +180,7 @@ __device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, fl
         if (j < nk) {
             const float e = expf(sj[j] - m);
             l += e;
-            const float4 v4 = (CUR && j == p.cb) ? vc4 : *(const float4 *)(p.ltv + ((size_t)b * NCB + j) * LTD + 4 * lane);
+            const float4 v4 = (CUR && j == p.cb) ? vc4 : PRE ? vr[j] : *(const float4 *)(vb + j * LTD);
             a.x = fmaf(e, v4.x, a.x); a.y = fmaf(e, v4.y, a.y); a.z = fmaf(e, v4.z, a.z); a.w = fmaf(e, v4.w, a.w);
         }
     }
@@ -462,48 +465,83 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LTARG_ATTN) {
-        // wave w owns slots w, w+4, ... at every batch size: pick codebook cb-1's code
-        // (the next slot's logits already in flight), gather q|k|v of position cb from
-        // the load-time table, attend over positions 0..cb
+        // wave w owns slots w, w+4, ... at every batch size. Phase 1 picks codebook
+        // cb-1's code of each (the next slot's logits in flight); phase 2 issues every
+        // gather at once: q|k|v of position cb from the load-time table and the residual
+        // row P[cb-1][code] + lt_pos[cb]; phase 3 attends over positions 0..cb. At one
+        // slot per wave the earlier positions' k/v are loaded before the pick.
         static_assert(K == LTD, "LT is 256 wide");
+        constexpr int SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
         const int lane = tid & 63, w = tid >> 6;
-        int *scode = (int *)sc;
         float *wsc = sc + ltc_off<NB>() + w * 2 * VCB;
         float cur[PICK_R], nxt[PICK_R];
         if (w < NB) load_logits(p.logits + (size_t)w * VCB, cur);
-        for (int b = w; b < NB; b += MP_NWAVES) {  // wave-uniform
+        float4 kr[NCB], vr[NCB];
+        if constexpr (SPW == 1) {
+            if (w < NB) {
+                const float *kb = p.ltk + (size_t)w * NCB * LTD + 4 * lane, *vb = p.ltv + (size_t)w * NCB * LTD + 4 * lane;
+#pragma unroll
+                for (int j = 0; j < NCB - 1; ++j)
+                    if (j < p.cb) { kr[j] = *(const float4 *)(kb + j * LTD); vr[j] = *(const float4 *)(vb + j * LTD); }
+            }
+        }
+        int stp[SPW];  // every owned slot's step up front, not one dependent load per pick
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) stp[j] = w + MP_NWAVES * j < NB ? p.step[w + MP_NWAVES * j] : 0;
+        unsigned long long codes = 0ull;  // 16 bits per owned slot (codes < 2048)
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b >= NB) break;  // wave-uniform
             const int bn = b + MP_NWAVES;
             if (bn < NB) load_logits(p.logits + (size_t)bn * VCB, nxt);
             int amax;
-            const int code = wave_pick_v(cur, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos, p.smp, b,
-                                         p.step[b], p.cb - 1, wsc, amax);
-            if (lane == 0) {
-                scode[b] = code;
-                if (blockIdx.x == 0) {
-                    p.codes_cur[b * NCB + p.cb - 1] = code;
-                    if (amax == p.audio_eos) p.smp.argeos[b] = 1;
-                    if (p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
-                }
+            const int code = wave_pick_v(cur, p.ignore_eos || stp[j] < 4, p.audio_bos, p.audio_eos, p.smp, b,
+                                         stp[j], p.cb - 1, wsc, amax);
+            if (blockIdx.x == 0 && lane == 0) {
+                p.codes_cur[b * NCB + p.cb - 1] = code;
+                if (amax == p.audio_eos) p.smp.argeos[b] = 1;
+                if (p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
             }
-            const float *row = p.qkvtab + ((size_t)(p.cb - 1) * VCB + code) * (3 * LTD) + 4 * lane;
-            const float4 q4 = *(const float4 *)row, k4 = *(const float4 *)(row + LTD),
-                         v4 = *(const float4 *)(row + 2 * LTD);
-            if (blockIdx.x == 0) {  // position cb's k/v for the later codebooks
-                *(float4 *)(p.lk + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = k4;
-                *(float4 *)(p.lv + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = v4;
-            }
-            *(float4 *)(act + b * K + 4 * lane) = lt_attend<true>(p, b, q4, k4, v4);
+            codes |= (unsigned long long)code << (16 * j);
 #pragma unroll
             for (int r = 0; r < PICK_R; ++r) cur[r] = nxt[r];
+        }
+        float4 q4[SPW], k4[SPW], v4[SPW], x4[SPW];
+        const float4 pos4 = *(const float4 *)(p.lt_pos + (size_t)p.cb * LTD + 4 * lane);
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            if (w + MP_NWAVES * j < NB) {
+                const int code = (int)((codes >> (16 * j)) & 0xffffull);
+                const size_t r = (size_t)(p.cb - 1) * VCB + code;
+                const float *row = p.qkvtab + r * (3 * LTD) + 4 * lane;
+                q4[j] = *(const float4 *)row;
+                k4[j] = *(const float4 *)(row + LTD);
+                v4[j] = *(const float4 *)(row + 2 * LTD);
+                x4[j] = *(const float4 *)(p.ptab + r * LTD + 4 * lane);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b >= NB) continue;
+            if (blockIdx.x == 0) {  // position cb's k/v for the later codebooks
+                *(float4 *)(p.lk + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = k4[j];
+                *(float4 *)(p.lv + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = v4[j];
+            }
+            *(float4 *)(sc + b * LTD + 4 * lane) =
+                make_float4(x4[j].x + pos4.x, x4[j].y + pos4.y, x4[j].z + pos4.z, x4[j].w + pos4.w);
+            *(float4 *)(act + b * K + 4 * lane) = lt_attend<true, SPW == 1>(p, b, q4[j], k4[j], v4[j], kr, vr);
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LT_ATTN) {
         // codebook 0 (q|k|v from the lt_a GEMV): the same per-slot wave code
         static_assert(K == LTD, "LT is 256 wide");
         const int lane = tid & 63, w = tid >> 6;
+        float4 kr[NCB], vr[NCB];
         for (int b = w; b < NB; b += MP_NWAVES) {
             const float4 q4 = *(const float4 *)(p.ltq + (size_t)b * LTD + 4 * lane);
-            *(float4 *)(act + b * K + 4 * lane) = lt_attend<false>(p, b, q4, q4, q4);
+            *(float4 *)(act + b * K + 4 * lane) = lt_attend<false, false>(p, b, q4, q4, q4, kr, vr);
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LTX_LN) {
@@ -524,7 +562,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
 
 // Epilogue of output (row n, slot b) of a fused projection.
 template <int EPI>
-__device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b, int code = 0) {
+__device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b, float extra = 0.f) {
     if constexpr (EPI == EPI_STORE) p.out[(size_t)b * p.out_ld + n] = v;
     else if constexpr (EPI == EPI_BIAS) p.out[(size_t)b * p.out_ld + n] = v + p.bias[n];
     else if constexpr (EPI == EPI_GELU) p.out[(size_t)b * p.out_ld + n] = gelu_tanh(v);
@@ -534,9 +572,7 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b,
     }
     else if constexpr (EPI == EPI_RESID) p.resid[(size_t)b * D + n] = v + p.resid[(size_t)b * D + n];
     else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
-    else if constexpr (EPI == EPI_LTX_ADD)
-        p.out[(size_t)b * p.out_ld + n] =
-            v + (p.ptab[((size_t)(p.cb - 1) * VCB + code) * LTD + n] + p.lt_pos[(size_t)p.cb * LTD + n]);
+    else if constexpr (EPI == EPI_LTX_ADD) p.out[(size_t)b * p.out_ld + n] = v + extra;  // extra = X[b][n]
     else if constexpr (EPI == EPI_QKV) {
         const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + p.pos[b]) * D;
         if (n < D) p.out[(size_t)b * D + n] = v;

@@ -180,6 +180,9 @@ struct mp_dev {
     float *xqb = nullptr;  // Q8 mode: q_net output [NB][128]
     unsigned short *h_b16 = nullptr;  // bf16 mode: GELU(FFN up) as the bf16 FFN-down operand [NB][3072]
     float *gpart = nullptr;            // preamble split-K partial sums (mp::gemm_splits)
+    hipEvent_t sev[2] = {nullptr, nullptr};  // streaming: the two chunk snapshots landed
+    int32_t *h_codes = nullptr;              // streaming: pinned host mirror of codes_out [NB][S][8] + snapshots
+    size_t h_codes_n = 0;
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
@@ -1045,6 +1048,9 @@ void mp_hip_free(mp_dev *dev) {
     for (void *p : dev->lt_allocs) hipFree(p);
     for (float *p : dev->m.xq_t) hipFree(p);
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
+    for (hipEvent_t e : dev->sev)
+        if (e) hipEventDestroy(e);
+    if (dev->h_codes) hipHostFree(dev->h_codes);
     if (dev->stream) hipStreamDestroy(dev->stream);
     delete dev;
 }
@@ -1211,6 +1217,9 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
 // frames_per_chunk iterations the new frames of every utterance are decoded by
 // the codec in chunks of frames_per_chunk (the last chunk of an utterance may
 // be shorter: EOS or max_dec_steps) and handed to `on_audio` in order.
+// Every full chunk of a round goes through the codec in one launch sequence
+// (chunks are independent, magpie.cpp:4739-4742: the audio is the same); the
+// frames reach the host through a pinned mirror filled on the decode stream.
 int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_audio_cb on_audio, void *user,
                          int32_t *codes_out, int32_t *n_frames, int64_t *total_samples) {
     if (!dev) return MP_ERR_ARG;
@@ -1220,56 +1229,122 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
     HIPCHK(hipSetDevice(dev->device));
     const int NB = dev->NB, B = dev->B, S = dev->max_steps;
     if (int rc = prepare_iteration(dev)) return rc;
+    if (!dev->sev[0]) {
+        HIPCHK(hipEventCreateWithFlags(&dev->sev[0], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&dev->sev[1], hipEventDisableTiming));
+    }
+    // pinned: a copy into pageable memory would block the host until the chunk's kernels finish
+    if (dev->h_codes_n < (size_t)NB * S * 8 + 6 * NB) {
+        if (dev->h_codes) hipHostFree(dev->h_codes);
+        dev->h_codes = nullptr;
+        dev->h_codes_n = 0;
+        HIPCHK(hipHostMalloc((void **)&dev->h_codes, ((size_t)NB * S * 8 + 6 * NB) * 4, hipHostMallocDefault));
+        dev->h_codes_n = (size_t)NB * S * 8 + 6 * NB;
+    }
+    int *const snap = dev->h_codes + (size_t)NB * S * 8;  // two snapshots of (step, done, nframes)
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<int> h_step(NB), h_done(NB), h_nf(NB), delivered(B, 0), stopped(B, 0), ended(B, 0);
-    std::vector<int32_t> chunk((size_t)8 * fpc), fm((size_t)fpc * 8);
-    std::vector<float> audio((size_t)fpc * 1024);
+    // two snapshots of (step, done, nframes): the host reads one while the next chunk's land in the other
+    std::vector<int> delivered(B, 0), stopped(B, 0), ended(B, 0);
+    std::vector<int32_t> cbm;
+    std::vector<float> audio;
     int64_t samples = 0;
     int it = 0;
     bool first = true;
     dev->timing = mp_timing{dev->timing.preamble_ms, 0.0, 0, 0, 0.0};
-    for (;;) {
-        int n_it = std::min(fpc, S - it);
+    auto enqueue_chunk = [&](int slot) -> int {
+        const int n_it = std::min(fpc, S - it);
         for (int i = 0; i < n_it; ++i)
             if (int rc = launch_iteration(dev)) return rc;
+        // the frames these iterations wrote (columns it..it+n_it of every slot) to the
+        // pinned mirror, on the decode stream: no host copy waits on the GPU later
+        HIPCHK(hipMemcpy2DAsync(dev->h_codes + (size_t)it * 8, (size_t)S * 32, dev->codes_out + (size_t)it * 8,
+                                (size_t)S * 32, (size_t)n_it * 32, NB, hipMemcpyDeviceToHost, dev->stream));
         it += n_it;
-        HIPCHK(hipMemcpyAsync(h_step.data(), dev->step, NB * 4, hipMemcpyDeviceToHost, dev->stream));
-        HIPCHK(hipMemcpyAsync(h_done.data(), dev->done, NB * 4, hipMemcpyDeviceToHost, dev->stream));
-        HIPCHK(hipMemcpyAsync(h_nf.data(), dev->nframes, NB * 4, hipMemcpyDeviceToHost, dev->stream));
-        HIPCHK(hipStreamSynchronize(dev->stream));
-        bool all_done = true;
+        int *h = snap + (size_t)slot * 3 * NB;
+        HIPCHK(hipMemcpyAsync(h, dev->step, NB * 4, hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipMemcpyAsync(h + NB, dev->done, NB * 4, hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipMemcpyAsync(h + 2 * NB, dev->nframes, NB * 4, hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipEventRecord(dev->sev[slot], dev->stream));
+        return MP_OK;
+    };
+    struct Job { int b, f0, n; };
+    std::vector<Job> jobs;
+    int slot = 0;
+    if (int rc = enqueue_chunk(0)) return rc;
+    for (;;) {
+        HIPCHK(hipEventSynchronize(dev->sev[slot]));
+        const int *h_step = snap + (size_t)slot * 3 * NB, *h_done = h_step + NB, *h_nf = h_step + 2 * NB;
+        bool more = false;
+        for (int b = 0; b < B; ++b) more |= !(h_done[b] != 0 || stopped[b]);
+        more &= it < S;
+        // this round's chunks, utterance by utterance, in delivery order
+        jobs.clear();
         for (int b = 0; b < B; ++b) {
-            const bool done = h_done[b] != 0 || stopped[b];
-            const int produced = h_done[b] ? h_nf[b] : h_step[b];
-            while (!stopped[b] && produced - delivered[b] >= (done ? 1 : fpc)) {
-                const int n = std::min(fpc, produced - delivered[b]);
-                HIPCHK(hipMemcpy(fm.data(), dev->codes_out + ((size_t)b * S + delivered[b]) * 8, (size_t)n * 32,
-                                 hipMemcpyDeviceToHost));
-                for (int t = 0; t < n; ++t)  // frame-major -> codebook-major (decode_frames_to_audio, 4468-4473)
-                    for (int c = 0; c < 8; ++c) chunk[(size_t)c * n + t] = fm[(size_t)t * 8 + c];
-                if (int rc = mp_hip_codec_decode(codec, chunk.data(), n, audio.data()))
+            if (stopped[b]) continue;
+            const bool done = h_done[b] != 0;
+            const int produced = done ? h_nf[b] : h_step[b];
+            for (int d = delivered[b]; produced - d >= (done ? 1 : fpc);) {
+                const int n = std::min(fpc, produced - d);
+                jobs.push_back({b, d, n});
+                d += n;
+            }
+        }
+        // full chunks through the codec together, a shorter final chunk on its own
+        size_t nfull = 0;
+        for (const Job &j : jobs) nfull += j.n == fpc;
+        cbm.assign(jobs.size() * 8 * fpc, 0);
+        audio.resize(jobs.size() * fpc * 1024);
+        std::vector<size_t> at(jobs.size());
+        {
+            size_t kf = 0, ks = nfull;
+            for (size_t q = 0; q < jobs.size(); ++q) at[q] = jobs[q].n == fpc ? kf++ : ks++;
+        }
+        for (size_t q = 0; q < jobs.size(); ++q) {
+            const Job &j = jobs[q];
+            const int32_t *fm = dev->h_codes + ((size_t)j.b * S + j.f0) * 8;
+            int32_t *dst = cbm.data() + at[q] * 8 * fpc;
+            for (int t = 0; t < j.n; ++t)  // frame-major -> codebook-major (decode_frames_to_audio, 4468-4473)
+                for (int c = 0; c < 8; ++c) dst[(size_t)c * j.n + t] = fm[(size_t)t * 8 + c];
+        }
+        if (nfull)
+            if (int rc = mp_hip_codec_decode_chunks(codec, cbm.data(), (int)nfull, fpc, audio.data()))
+                return fail(dev, rc, std::string("codec: ") + mp_hip_codec_error(codec));
+        for (size_t q = 0; q < jobs.size(); ++q)
+            if (jobs[q].n != fpc)
+                if (int rc = mp_hip_codec_decode(codec, cbm.data() + at[q] * 8 * fpc, jobs[q].n,
+                                                 audio.data() + at[q] * fpc * 1024))
                     return fail(dev, rc, std::string("codec: ") + mp_hip_codec_error(codec));
-                delivered[b] += n;
-                samples += (int64_t)n * 1024;
+        for (size_t q = 0, b = 0; b < (size_t)B; ++b) {
+            for (; q < jobs.size() && jobs[q].b == (int)b; ++q) {
+                const Job &j = jobs[q];
+                if (stopped[b]) continue;  // a callback of this round stopped the utterance
+                delivered[b] += j.n;
+                samples += (int64_t)j.n * 1024;
                 if (first) {
                     dev->timing.first_audio_ms = ms_since(t0);
                     first = false;
                 }
-                if (on_audio && !on_audio(b, audio.data(), n * 1024, user)) {
+                if (on_audio && !on_audio((int)b, audio.data() + at[q] * fpc * 1024, j.n * 1024, user)) {
                     // the callback asked to stop (4820-4824): the utterance ends here
                     stopped[b] = 1;
                     const int one = 1;
-                    HIPCHK(hipMemcpy(dev->done + b, &one, 4, hipMemcpyHostToDevice));
+                    HIPCHK(hipMemcpyAsync(dev->done + b, &one, 4, hipMemcpyHostToDevice, dev->stream));
+                    HIPCHK(hipStreamSynchronize(dev->stream));
                 }
             }
-            if (!(done || stopped[b])) all_done = false;
-            else if (!ended[b]) {  // end-of-utterance notice: (utt, NULL, 0)
+            if ((h_done[b] != 0 || stopped[b]) && !ended[b]) {  // end-of-utterance notice: (utt, NULL, 0)
                 ended[b] = 1;
-                if (on_audio) on_audio(b, nullptr, 0, user);
+                if (on_audio) on_audio((int)b, nullptr, 0, user);
             }
         }
-        if (all_done || it >= S) break;
+        if (!more) break;
+        // The next chunk is queued only now, after the codec: with the codec's kernels
+        // running beside the decode iterations the decoded frames were observed to
+        // change (open item), so the two do not overlap.
+        if (int rc = enqueue_chunk(slot ^ 1)) return rc;
+        slot ^= 1;
     }
+    HIPCHK(hipStreamSynchronize(dev->stream));
     dev->timing.decode_ms = ms_since(t0);
     dev->timing.iterations = it;
     int total = 0;

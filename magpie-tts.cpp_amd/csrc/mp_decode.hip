@@ -338,6 +338,7 @@ static bool gemv_args_ok(const GemvP &p) {
     bool ok = true;
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
     if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
+    if constexpr (PRO == PRO_LTFFN_MERGE) ok &= p.part && p.addsrc;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
@@ -399,6 +400,91 @@ hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
     hipLaunchKernelGGL(sa_attn_kernel, dim3(NH, SA_SPLITS, B), dim3(SA_THREADS), 0, s, p);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------- LT FFN
+// FFN up + GELU + FFN down of the local transformer in one launch
+// (magpie.cpp:983-992): workgroup p owns hidden units j in [32p, 32p+32). Its
+// weights (32 rows of W1, the 32-column slice of W2 that row n = thread n
+// reads) are issued first; every slot's LN(y) row is built by one wave (DPP
+// statistics, the same code at every batch size), a wave computes 8 units per
+// slot (float4 lanes, DPP sum, GELU) into LDS, then thread n adds its 32 units'
+// contributions to output n in ascending order. The LT_FFN_P partial sums are
+// merged (ascending p) by the head's prologue at batch 1 or by lt_merge_kernel.
+template <int NB>
+__global__ __launch_bounds__(MP_BLOCK) void lt_ffn_kernel(LtFfnP p) {
+    constexpr int U = LTF / LT_FFN_P, UPW = U / MP_NWAVES;
+    static_assert(U % MP_NWAVES == 0 && U % 4 == 0 && LTD == MP_BLOCK, "unit split");
+    __shared__ __attribute__((aligned(16))) float xs[NB][LTD];
+    __shared__ __attribute__((aligned(16))) float fs[NB][U];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = blockIdx.x * U;
+    float4 a1[UPW], a2[U / 4];
+#pragma unroll
+    for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
+#pragma unroll
+    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.w2 + (size_t)tid * LTF + j0 + 4 * i);
+    for (int b = w; b < NB; b += MP_NWAVES) {
+        float x[LTD / 64];
+#pragma unroll
+        for (int i = 0; i < LTD / 64; ++i) x[i] = p.y[(size_t)b * LTD + lane + 64 * i];
+        float mean, var;
+        wave_meanvar<LTD / 64>(x, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+        for (int i = 0; i < LTD / 64; ++i) xs[b][lane + 64 * i] = ((x[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+    }
+    lds_sync();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const float4 xv = *(const float4 *)&xs[b][4 * lane];
+#pragma unroll
+        for (int r = 0; r < UPW; ++r) {
+            const float v = wave_sum(dotv(a1[r], xv));
+            if (lane == 0) fs[b][w * UPW + r] = gelu_tanh(v);
+        }
+    }
+    lds_sync();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < U / 4; ++i) {
+            const float4 f4 = *(const float4 *)&fs[b][4 * i];
+            acc = fmaf(a2[i].x, f4.x, acc);
+            acc = fmaf(a2[i].y, f4.y, acc);
+            acc = fmaf(a2[i].z, f4.z, acc);
+            acc = fmaf(a2[i].w, f4.w, acc);
+        }
+        p.part[((size_t)b * LT_FFN_P + blockIdx.x) * LTD + tid] = acc;
+    }
+}
+template <int NB>
+__global__ __launch_bounds__(MP_BLOCK) void lt_merge_kernel(LtFfnP p) {
+    for (int e = threadIdx.x; e < NB * LTD; e += MP_BLOCK) p.out[e] = lt_ffn_merge(p.part, p.y, e / LTD, e % LTD);
+}
+hipError_t op_lt_ffn(const LtFfnP &p, int NB, hipStream_t s) {
+    if (!p.y || !p.lnw || !p.w1 || !p.w2 || !p.part) return hipErrorInvalidValue;
+    switch (NB) {
+    case 1: hipLaunchKernelGGL(lt_ffn_kernel<1>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(lt_ffn_kernel<2>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(lt_ffn_kernel<4>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 8: hipLaunchKernelGGL(lt_ffn_kernel<8>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t op_lt_merge(const LtFfnP &p, int NB, hipStream_t s) {
+    if (!p.y || !p.part || !p.out) return hipErrorInvalidValue;
+    switch (NB) {
+    case 1: hipLaunchKernelGGL(lt_merge_kernel<1>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(lt_merge_kernel<2>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(lt_merge_kernel<4>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 8: hipLaunchKernelGGL(lt_merge_kernel<8>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+// the LT head at batch 1 with the FFN merge as its prologue
+hipError_t op_lt_em_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 2, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 
 hipError_t op_finalize(const FinP &p, int B, hipStream_t s) {
     if (!p.smp.cfg || !p.smp.argeos) return hipErrorInvalidValue;

@@ -246,6 +246,7 @@ static bool q8_args_ok(const GemvP &p) {
     bool ok = true;
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
     if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
+    if constexpr (PRO == PRO_LTFFN_MERGE) ok &= p.part && p.addsrc;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
@@ -291,5 +292,7 @@ MP_Q8_OPS(4)
 MP_Q8_OPS(8)
 // LT in_proj of a caller-supplied normalised hidden (magpie_local_transformer_sample_all)
 hipError_t q8_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_q8<1, D, 4, PRO_PLAIN, EPI_BIAS>(p, s); }
+// the LT head at batch 1 with the LT FFN merge as its prologue (lt_ffn_kernel)
+hipError_t q8_lt_em_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, 4, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 
 }  // namespace mp

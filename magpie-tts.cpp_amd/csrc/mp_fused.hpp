@@ -187,6 +187,17 @@ __device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, fl
     return make_float4(a.x / l, a.y / l, a.z / l, a.w / l);
 }
 
+// LT FFN output element k of slot b: the LT_FFN_P partial FFN-down sums added in
+// ascending order, then the residual (the same arithmetic in the head's prologue
+// at batch 1 and in lt_merge_kernel otherwise)
+__device__ __forceinline__ float lt_ffn_merge(const float *part, const float *y, int b, int k) {
+    const float *pp = part + (size_t)b * LT_FFN_P * LTD + k;
+    float s = pp[0];
+#pragma unroll
+    for (int q = 1; q < LT_FFN_P; ++q) s += pp[(size_t)q * LTD];
+    return s + y[(size_t)b * LTD + k];
+}
+
 // LDS scratch (floats) a prologue needs besides the activation rows
 template <int NB, int PRO>
 constexpr int pro_scratch() {
@@ -333,6 +344,10 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 }
             }
         }
+        lds_sync();
+    } else if constexpr (PRO == PRO_LTFFN_MERGE) {
+        static_assert(K == LTD, "LT is 256 wide");
+        for (int e = tid; e < NB * K; e += MP_BLOCK) act[e] = lt_ffn_merge(p.part, p.addsrc, e / K, e % K);
         lds_sync();
     } else if constexpr (PRO == PRO_PLAIN) {
         for (int b = 0; b < NB; ++b)

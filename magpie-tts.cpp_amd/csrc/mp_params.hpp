@@ -25,6 +25,7 @@ constexpr int SA_SPLITS = 4;        // key splits of each SA head (sa_attn_kerne
 constexpr int SA_PART = 4 + DH;     // per (slot, head, split): m, l, -, -, O[64] (unnormalised)
 constexpr int XA_SPLITS = 4;        // text-key splits of the fused cross-attention (xa_part_kernel)
 constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
+constexpr int LT_FFN_P = 32;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
 enum Pro {
@@ -42,6 +43,8 @@ enum Pro {
     PRO_XA_LN = 10,     // x2 = src + XA output (XA_SPLITS partial states merged), block 0 stores
                         // x2 to xres; act = LN(x2)*lnw              (3513-3525)
     PRO_PLAIN_B16 = 11, // bf16 kernels only: act = src_b16 (rows already bf16, EPI_GELU_B16 output)
+    PRO_LTFFN_MERGE = 12, // act = (sum over p of the LT_FFN_P partial FFN-down sums, p ascending)
+                          //       + addsrc: the LT FFN output (lt_ffn_kernel, 983-992)
 };
 enum Epi {
     EPI_STORE = 0,      // out = v
@@ -70,6 +73,18 @@ struct Sampling {
     const SmpCfg *cfg;
     int *argeos;               // [B] 1 once a codebook's argmax was EOS this frame (4343-4346)
     int *amax;                 // optional [B][8]: every codebook's argmax (magpie_sample_result.argmax_codes)
+};
+
+// LT FFN up + GELU + FFN down in one launch (lt_ffn_kernel): workgroup p owns
+// hidden units [p*32, p*32+32) and writes its share of FFN down, part[b][p][256]
+struct LtFfnP {
+    const float *y;      // [B][256] LT residual stream after attention (ltY)
+    const float *lnw;    // norm_pos_ff weight
+    const float *w1;     // [1024][256] FFN up
+    const float *w2;     // [256][1024] FFN down
+    float eps;
+    float *part;         // [B][LT_FFN_P][256]
+    float *out;          // lt_merge_kernel: [B][256] = ltY + merged FFN down
 };
 
 // splitmix64 finaliser

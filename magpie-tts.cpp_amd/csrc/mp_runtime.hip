@@ -66,6 +66,10 @@ MP_DECL_Q8(2)
 MP_DECL_Q8(4)
 MP_DECL_Q8(8)
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
+hipError_t q8_lt_em_1(const GemvP &, hipStream_t);
+hipError_t op_lt_em_1(const GemvP &, hipStream_t);
+hipError_t op_lt_ffn(const LtFfnP &, int, hipStream_t);
+hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_xa_q8(const XaQ8P &, int, hipStream_t);
@@ -137,7 +141,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7 };
 struct OpRec {
     std::string name;
     int kind;
@@ -147,6 +151,7 @@ struct OpRec {
     FinP f;
     XaP x;
     XaQ8P xq;
+    LtFfnP lf;
     int B;
     double bytes;
 };
@@ -156,6 +161,7 @@ struct LtIo {
     float *x, *hidden, *trace;
     int trace_steps;
     float *lt_s, *ltX, *ltY, *lty2, *ltq, *ltk, *ltv, *ltf, *logits;
+    float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel)
     int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
     SmpCfg *cfg;
     int sampling, ignore_eos, emit_eos, max_steps, lt_only;
@@ -186,7 +192,7 @@ struct mp_dev {
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
-          *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr;
+          *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
         *argeos = nullptr, *amax = nullptr;
@@ -598,6 +604,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
+    A(ltp, (size_t)NB * mp::LT_FFN_P * 256);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -736,7 +743,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     mp::LtIo io{};
     io.x = dev->x; io.hidden = dev->hidden; io.trace = dev->trace; io.trace_steps = dev->max_steps + 1;
     io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
-    io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits;
+    io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits; io.ltp = dev->ltp;
     io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
     io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
     io.amax = dev->amax; io.cfg = dev->smpcfg;
@@ -827,14 +834,37 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                               A * act * (2024 + 3 * 256 + 2 * 256 * cb + 2 * 256 + 256))) != MP_OK)
                 return rc;
         }
-        g = base(); g.cb = cb;
-        g.W = m.lt_ff1; g.Wb = m.pk_lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = io.ltY; g.src_ld = 256;
-        g.out = io.ltf; g.out_ld = 1024;
-        if ((rc = run("lt_c", tb.lt_c, g, F * (1024.0 * 256) + A * act * ((256 + 1024)))) != MP_OK) return rc;
-        g = base(); g.cb = cb;
-        g.W = m.lt_ff2; g.Wb = m.pk_lt_ff2; g.N = 256; g.src = io.ltf; g.src_ld = 1024; g.out = io.lty2; g.out_ld = 256;
-        g.addsrc = io.ltY;
-        if ((rc = run("lt_d", tb.lt_d, g, F * (256.0 * 1024) + A * act * ((1024 + 512)))) != MP_OK) return rc;
+        // FFN up + GELU + FFN down: one launch of partial sums (f32 FFN weights), merged by
+        // the head's prologue at batch 1 or by a one-workgroup merge; bf16 mode: two GEMVs
+        const bool ffn1 = !b16;
+        if (ffn1) {
+            mp::LtFfnP lf{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2, m.eps, io.ltp, io.lty2};
+            if (ops) {
+                mp::OpRec r{};
+                r.name = "lt_ffn"; r.kind = mp::K_LTFFN; r.lf = lf; r.B = NB;
+                r.bytes = A * (1024.0 * 256 * 2) + A * act * (256 + mp::LT_FFN_P * 256);
+                ops->push_back(r);
+            }
+            HIPCHK(mp::op_lt_ffn(lf, NB, s));
+            if (NB > 1) {
+                if (ops) {
+                    mp::OpRec r{};
+                    r.name = "lt_merge"; r.kind = mp::K_LTMERGE; r.lf = lf; r.B = NB;
+                    r.bytes = A * act * (mp::LT_FFN_P * 256 + 512);
+                    ops->push_back(r);
+                }
+                HIPCHK(mp::op_lt_merge(lf, NB, s));
+            }
+        } else {
+            g = base(); g.cb = cb;
+            g.W = m.lt_ff1; g.Wb = m.pk_lt_ff1; g.N = 1024; g.lnw = m.lt_norm_ff; g.src = io.ltY; g.src_ld = 256;
+            g.out = io.ltf; g.out_ld = 1024;
+            if ((rc = run("lt_c", tb.lt_c, g, F * (1024.0 * 256) + A * act * ((256 + 1024)))) != MP_OK) return rc;
+            g = base(); g.cb = cb;
+            g.W = m.lt_ff2; g.Wb = m.pk_lt_ff2; g.N = 256; g.src = io.ltf; g.src_ld = 1024; g.out = io.lty2;
+            g.out_ld = 256; g.addsrc = io.ltY;
+            if ((rc = run("lt_d", tb.lt_d, g, F * (256.0 * 1024) + A * act * ((1024 + 512)))) != MP_OK) return rc;
+        }
         g = base(); g.cb = cb;
         g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024;
         g.Wb = b16 ? m.pk_lt_out + (size_t)cb * pk_elems(2024, 256) : nullptr; g.bias = m.lt_out_b + (size_t)cb * 2024;
@@ -843,7 +873,12 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             g.Wq = m.lt_out8.q + (size_t)cb * 2024 * 256;
             g.Wd = m.lt_out8.d + (size_t)cb * 2024 * 8;
         }
-        if ((rc = run("lt_e", m.lt_out8 ? tq.lt_e : tb.lt_e, g,
+        mp::GemvFn efn = m.lt_out8 ? tq.lt_e : tb.lt_e;
+        if (ffn1 && NB == 1) {  // the FFN merge is the head's prologue
+            g.part = io.ltp; g.addsrc = io.ltY;
+            efn = m.lt_out8 ? mp::q8_lt_em_1 : mp::op_lt_em_1;
+        }
+        if ((rc = run("lt_e", efn, g,
                       (m.lt_out8 ? Fq : F) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
             return rc;
     }
@@ -1377,7 +1412,7 @@ int mp_hip_lt_sample(mp_dev *dev, const float *hidden, float temperature, int to
         int rc = MP_OK;
         if ((rc = al(&io.hidden, 768)) || (rc = al(&io.lt_s, 9 * 256)) || (rc = al(&io.ltX, 256)) ||
             (rc = al(&io.ltY, 256)) || (rc = al(&io.lty2, 256)) || (rc = al(&io.ltq, 256)) ||
-            (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) ||
+            (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) || (rc = al(&io.ltp, mp::LT_FFN_P * 256)) ||
             (rc = al(&io.logits, 2024)) || (rc = al(&io.codes_cur, 8)) || (rc = al(&io.step, 1)) ||
             (rc = al(&io.done, 1)) || (rc = al(&io.argeos, 1)) || (rc = al(&io.amax, 8)) || (rc = al(&io.cfg, 8)))
             return rc;
@@ -1453,6 +1488,8 @@ int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
             case mp::K_ATTN: e = mp::op_sa_attn(r.a, r.B, dev->stream); break;
             case mp::K_XA: e = mp::op_xa(r.x, r.B, dev->stream); break;
             case mp::K_XAQ8: e = mp::op_xa_q8(r.xq, r.B, dev->stream); break;
+            case mp::K_LTFFN: e = mp::op_lt_ffn(r.lf, r.B, dev->stream); break;
+            case mp::K_LTMERGE: e = mp::op_lt_merge(r.lf, r.B, dev->stream); break;
             case mp::K_FIN: e = mp::op_finalize(r.f, r.B, dev->stream); break;
             }
             HIPCHK(e);
@@ -1483,6 +1520,8 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
             return mp::op_xa(r.x, r.B, dev->stream);  // rewrites this layer's split states only
         }
         if (r.kind == mp::K_XAQ8) return mp::op_xa_q8(r.xq, r.B, dev->stream);  // rewrites x2 with the same values
+        if (r.kind == mp::K_LTFFN) return mp::op_lt_ffn(r.lf, r.B, dev->stream);
+        if (r.kind == mp::K_LTMERGE) return mp::op_lt_merge(r.lf, r.B, dev->stream);
         return hipErrorInvalidValue;
     };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");

@@ -401,6 +401,55 @@ hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- LT pick (large batches)
+// PRO_LTARG_ATTN's per-slot work as its own launch, one wave per slot, for
+// NB >= 8 (where the fused prologue would run several slots' picks in sequence
+// per wave): codebook cb-1's pick, the gathers of position cb's q|k|v and
+// residual rows, the causal attention. The attention output goes to ltq (out),
+// the residual row to ltX; the o_net GEMV (PRO_PLAIN + EPI_ADD_STORE) follows.
+// Same functions, same arithmetic as the fused path: batches stay bit-identical.
+__global__ __launch_bounds__(64) void lt_pick_kernel(GemvP p) {
+    __shared__ float wsc[2 * VCB];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    float4 kr[NCB], vr[NCB];
+    {
+        const float *kb = p.ltk + (size_t)b * NCB * LTD + 4 * lane, *vb = p.ltv + (size_t)b * NCB * LTD + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < NCB - 1; ++j)
+            if (j < p.cb) { kr[j] = *(const float4 *)(kb + j * LTD); vr[j] = *(const float4 *)(vb + j * LTD); }
+    }
+    float lv[PICK_R];
+    load_logits(p.logits + (size_t)b * VCB, lv);
+    const int stp = p.step[b];
+    int amax;
+    const int code = wave_pick_v(lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, p.cb - 1, wsc,
+                                 amax);
+    if (lane == 0) {
+        p.codes_cur[b * NCB + p.cb - 1] = code;
+        if (amax == p.audio_eos) p.smp.argeos[b] = 1;
+        if (p.smp.amax) p.smp.amax[b * NCB + p.cb - 1] = amax;
+    }
+    const size_t r = (size_t)(p.cb - 1) * VCB + code;
+    const float *row = p.qkvtab + r * (3 * LTD) + 4 * lane;
+    const float4 q4 = *(const float4 *)row, k4 = *(const float4 *)(row + LTD), v4 = *(const float4 *)(row + 2 * LTD);
+    const float4 x4 = *(const float4 *)(p.ptab + r * LTD + 4 * lane);
+    const float4 pos4 = *(const float4 *)(p.lt_pos + (size_t)p.cb * LTD + 4 * lane);
+    *(float4 *)(p.lk + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = k4;
+    *(float4 *)(p.lv + ((size_t)b * NCB + p.cb) * LTD + 4 * lane) = v4;
+    *(float4 *)(p.ltX + (size_t)b * LTD + 4 * lane) =
+        make_float4(x4.x + pos4.x, x4.y + pos4.y, x4.z + pos4.z, x4.w + pos4.w);
+    *(float4 *)(p.out + (size_t)b * LTD + 4 * lane) = lt_attend<true, true>(p, b, q4, k4, v4, kr, vr);
+}
+hipError_t op_lt_pick(const GemvP &p, int NB, hipStream_t s) {
+    if (!p.logits || !p.codes_cur || !p.qkvtab || !p.ptab || !p.lt_pos || !p.ltk || !p.ltv || !p.lk || !p.lv ||
+        !p.ltX || !p.out || !p.step || !p.smp.cfg || !p.smp.argeos || p.cb < 1)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lt_pick_kernel, dim3(NB), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+// o_net + residual after lt_pick_kernel (its attention output in src, residual in addsrc)
+hipError_t op_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_gemv<8, 1, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
+
 // ---------------------------------------------------------------- LT FFN
 // FFN up + GELU + FFN down of the local transformer in one launch
 // (magpie.cpp:983-992): workgroup p owns hidden units j in [32p, 32p+32). Its

@@ -200,6 +200,9 @@ MP_B16_OPS(2)
 MP_B16_OPS(4)
 MP_B16_OPS(8)
 MP_B16_OPS(16)
+// o_net + residual after lt_pick_kernel (large batches)
+hipError_t b16_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_b16<8, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
+hipError_t b16_lt_bo_16(const GemvP &p, hipStream_t s) { return launch_b16<16, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 
 // f32 [N][K] -> bf16 fragment order [ceil(N/16)][K/32][64][8], rows >= N zero.
 __global__ void pack_b16_kernel(const float *W, int N, int K, unsigned short *out) {

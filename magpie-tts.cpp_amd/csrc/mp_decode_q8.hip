@@ -292,6 +292,8 @@ MP_Q8_OPS(4)
 MP_Q8_OPS(8)
 // LT in_proj of a caller-supplied normalised hidden (magpie_local_transformer_sample_all)
 hipError_t q8_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_q8<1, D, 4, PRO_PLAIN, EPI_BIAS>(p, s); }
+// o_net + residual after lt_pick_kernel (large batches)
+hipError_t q8_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_q8<8, LTD, 4, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 // the LT head at batch 1 with the LT FFN merge as its prologue (lt_ffn_kernel)
 hipError_t q8_lt_em_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, 4, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 

@@ -67,6 +67,11 @@ MP_DECL_Q8(4)
 MP_DECL_Q8(8)
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
 hipError_t q8_lt_em_1(const GemvP &, hipStream_t);
+hipError_t op_lt_pick(const GemvP &, int, hipStream_t);
+hipError_t op_lt_bo_8(const GemvP &, hipStream_t);
+hipError_t b16_lt_bo_8(const GemvP &, hipStream_t);
+hipError_t b16_lt_bo_16(const GemvP &, hipStream_t);
+hipError_t q8_lt_bo_8(const GemvP &, hipStream_t);
 hipError_t op_lt_em_1(const GemvP &, hipStream_t);
 hipError_t op_lt_ffn(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
@@ -141,7 +146,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8 };
 struct OpRec {
     std::string name;
     int kind;
@@ -821,6 +826,26 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             if ((rc = run("lt_b", m.lt_o8 ? tq.lt_b : tb.lt_b, g,
                           (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * (256 * 5))) != MP_OK)
                 return rc;
+        } else if (NB >= 8) {
+            // large batches: the per-slot pick + gathers + attention as one wave per slot
+            // (lt_pick_kernel), then o_net + residual; the same arithmetic as lt_bg
+            g = base(); g.cb = cb;
+            g.logits = io.logits; g.codes_cur = io.codes_cur; g.qkvtab = m.lt_qkvtab; g.ptab = m.lt_ptab;
+            g.lt_pos = m.lt_pos; g.ltk = io.ltk; g.ltv = io.ltv; g.lk = io.ltk; g.lv = io.ltv; g.ltX = io.ltX;
+            g.out = io.ltq;
+            if (ops) {
+                mp::OpRec r{};
+                r.name = "lt_pick"; r.kind = mp::K_LTPICK; r.g = g; r.B = NB;
+                r.bytes = A * act * (2024 + 4 * 256 + 2 * 256 * cb + 4 * 256);
+                ops->push_back(r);
+            }
+            HIPCHK(mp::op_lt_pick(g, NB, s));
+            g = base(); g.cb = cb;
+            g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.src = io.ltq; g.src_ld = 256; g.out = io.ltY; g.out_ld = 256;
+            g.addsrc = io.ltX; g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
+            const mp::GemvFn bo = m.lt_o8 ? mp::q8_lt_bo_8 : b16 ? (NB == 16 ? mp::b16_lt_bo_16 : mp::b16_lt_bo_8)
+                                                                : mp::op_lt_bo_8;
+            if ((rc = run("lt_bo", bo, g, (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * (256 * 3))) != MP_OK) return rc;
         } else {
             // position cb: codebook cb-1's pick, its q|k|v row gathered from the load-time
             // table (no q|k|v GEMV), attention + o_net + residual, one launch
@@ -1490,6 +1515,7 @@ int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
             case mp::K_XAQ8: e = mp::op_xa_q8(r.xq, r.B, dev->stream); break;
             case mp::K_LTFFN: e = mp::op_lt_ffn(r.lf, r.B, dev->stream); break;
             case mp::K_LTMERGE: e = mp::op_lt_merge(r.lf, r.B, dev->stream); break;
+            case mp::K_LTPICK: e = mp::op_lt_pick(r.g, r.B, dev->stream); break;
             case mp::K_FIN: e = mp::op_finalize(r.f, r.B, dev->stream); break;
             }
             HIPCHK(e);
@@ -1522,6 +1548,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
         if (r.kind == mp::K_XAQ8) return mp::op_xa_q8(r.xq, r.B, dev->stream);  // rewrites x2 with the same values
         if (r.kind == mp::K_LTFFN) return mp::op_lt_ffn(r.lf, r.B, dev->stream);
         if (r.kind == mp::K_LTMERGE) return mp::op_lt_merge(r.lf, r.B, dev->stream);
+        if (r.kind == mp::K_LTPICK) return mp::op_lt_pick(r.g, r.B, dev->stream);
         return hipErrorInvalidValue;
     };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");

@@ -86,18 +86,19 @@ def test_batch_equals_single(ma, small_model, B):
     dev.close()
 
 
-@pytest.mark.parametrize("weights", ["f32", "bf16", "q8"])
-def test_sampled_batch_equals_single(ma, small_model, q8_model, weights):
+@pytest.mark.parametrize("weights,B", [("f32", 4), ("bf16", 4), ("q8", 4), ("f32", 8), ("bf16", 16), ("q8", 8)])
+def test_sampled_batch_equals_single(ma, small_model, q8_model, weights, B):
     """Sampling is what exposes ulp-level batch variance (a near-tie in the top-k
     order flips a draw), so a sampled batch over many frames must reproduce each
-    utterance run alone bit for bit: codes, decoder hidden, every codebook draw."""
+    utterance run alone bit for bit: codes, decoder hidden, every codebook draw.
+    B >= 8 runs the LT pick as its own per-slot launch (lt_pick_kernel)."""
     path = q8_model if weights == "q8" else small_model
-    toks = [ma.synthetic_tokens(9 + 7 * b, seed=3000 + b) for b in range(4)]
-    kw = dict(max_dec_steps=96, temperature=0.7, top_k=80, seed=17, ignore_eos=True, trace=True)
+    toks = [ma.synthetic_tokens(9 + 7 * (b % 6), seed=3000 + b) for b in range(B)]
+    kw = dict(max_dec_steps=64, temperature=0.7, top_k=80, seed=17, ignore_eos=True, trace=True)
     dev = ma.Device(path, weights=weights)
-    rb = dev.synthesize(toks, speakers=[0, 1, 2, 3], **kw)
-    for b in range(4):
-        rs = dev.synthesize([toks[b]], speakers=[b], stream_base=b, **kw)
+    rb = dev.synthesize(toks, speakers=[b % 5 for b in range(B)], **kw)
+    for b in (range(B) if B <= 4 else (0, 3, B - 1)):
+        rs = dev.synthesize([toks[b]], speakers=[b % 5], stream_base=b, **kw)
         assert np.array_equal(rb.codes[b], rs.codes[0]), f"slot {b}"
         assert np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b} hidden"
     dev.close()

@@ -20,7 +20,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 ops = json.load(open(os.path.join(REPO, "gpurun_out", "pmc_ops.json")))["ops"]
 DECODE = ("gemv_kernel", "sa_attn_kernel", "xa_part_kernel", "lt_finalize_kernel", "gemm_b16_kernel",
-          "gemv_q8_kernel", "row_xa_kernel")
+          "gemv_q8_kernel", "row_xa_kernel", "lt_ffn_kernel", "lt_merge_kernel", "lt_pick_kernel", "xa_q8_kernel")
 
 
 def per_op(kind):

@@ -17,7 +17,7 @@ p = ma.synth_gguf(C + "/magpie_small_l2e1.gguf", dec_layers=2, enc_layers=1)
 ma.synth_gguf(C + "/nano_codec.gguf", kind="codec")
 NBT = int(os.environ.get("DIAG_B", "2"))
 toks = [ma.synthetic_tokens(16 + 9 * b, seed=50 + b) for b in range(NBT)]
-dev = ma.Device(p)
+dev = ma.Device(p, weights=os.environ.get("DIAG_W", "f32"))
 kw = dict(speakers=[0] * NBT, max_dec_steps=96, ignore_eos=True, trace=True)
 ref = dev.synthesize(toks, **kw)
 for f in ("/tmp/codec_child_ready", "/tmp/codec_child_stop"):

@@ -95,7 +95,9 @@ __device__ __forceinline__ float fsq(int code, int d) {
 
 // Implicit-GEMM causal conv. Block tile BM (out ch) x BN (time), 4 waves.
 constexpr int MAXTAPS = 11;
-template <int BM, int BN, int MODE>
+// PIPE: the software-pipelined channel loop (twice the registers: 2 waves/SIMD),
+// for grids too small to hide latency by occupancy; same arithmetic either way.
+template <int BM, int BN, int MODE, bool PIPE>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     constexpr int RW = BM / 16;          // row blocks of 16
     constexpr int CWN = 4 / RW;          // column groups
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     constexpr int NT = WCOLS / 16;       // MFMA column tiles per wave
     constexpr int ROWB = 80;             // LDS bytes per time row: 32 halves + 16 B pad
     constexpr int MAXHALO = 50;          // (11 - 1) * 5
-    __shared__ __attribute__((aligned(16))) char xs[(BN + MAXHALO) * ROWB];
+    __shared__ __attribute__((aligned(16))) char xs[PIPE ? 2 : 1][(BN + MAXHALO) * ROWB];
 
     const int br = blockIdx.z;
     const int ks = p.ks[br];
@@ -125,49 +127,97 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     const int rows = BN + pad;
-    for (int i0 = 0; i0 < p.Cinp; i0 += 32) {
-        // ---- A fragments of every tap of this channel block (L2-resident weight
-        //      image), in flight while the input rows are staged
-        half8 af[MAXTAPS];
+    if constexpr (!PIPE) {
+        // single-buffered: A fragments and input rows of a channel block issued
+        // together, one wait, MFMAs; latency hidden by other resident workgroups
+        for (int i0 = 0; i0 < p.Cinp; i0 += 32) {
+            half8 af[MAXTAPS];
 #pragma unroll
-        for (int k = 0; k < MAXTAPS; ++k)
-            if (k < ks) af[k] = *(const half8 *)(W + (size_t)orow * Kw + k * p.Cinp + i0 + 8 * kg);
-        // ---- stage input rows [t0 - pad, t0 + BN) x channels [i0, i0+32) as f16
-        if constexpr (MODE == IN_FSQ) {
-            for (int e = tid; e < rows * 8; e += 256) {
-                const int r = e >> 3, c4 = (e & 7) * 4;
-                const int t = t0 - pad + r;
-                _Float16 *dst = (_Float16 *)(xs + r * ROWB) + c4;
+            for (int k = 0; k < MAXTAPS; ++k)
+                if (k < ks) af[k] = *(const half8 *)(W + (size_t)orow * Kw + k * p.Cinp + i0 + 8 * kg);
+            if constexpr (MODE == IN_FSQ) {
+                for (int e = tid; e < rows * 8; e += 256) {
+                    const int r = e >> 3, c4 = (e & 7) * 4;
+                    const int t = t0 - pad + r;
+                    _Float16 *dst = (_Float16 *)(xs[0] + r * ROWB) + c4;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int c = i0 + c4 + u;
-                    dst[u] = (t >= 0 && t < p.T) ? (_Float16)fsq(p.codes[((size_t)chunk * 8 + (c >> 2)) * p.T + t], c & 3)
-                                                 : (_Float16)0.f;
+                    for (int u = 0; u < 4; ++u) {
+                        const int c = i0 + c4 + u;
+                        dst[u] = (t >= 0 && t < p.T)
+                                     ? (_Float16)fsq(p.codes[((size_t)chunk * 8 + (c >> 2)) * p.T + t], c & 3)
+                                     : (_Float16)0.f;
+                    }
+                }
+            } else {
+                for (int e = tid; e < rows * 4; e += 256) {
+                    const int r = e >> 2, q = e & 3;
+                    const int t = t0 - pad + r;
+                    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                    if (t >= 0 && t < p.T) v = *(const uint4 *)(xin + (size_t)t * p.Cinp + i0 + 8 * q);
+                    *(uint4 *)(xs[0] + r * ROWB + 16 * q) = v;
                 }
             }
-        } else {
-            for (int e = tid; e < rows * 4; e += 256) {
-                const int r = e >> 2, q = e & 3;
-                const int t = t0 - pad + r;
-                uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                if (t >= 0 && t < p.T) v = *(const uint4 *)(xin + (size_t)t * p.Cinp + i0 + 8 * q);
-                *(uint4 *)(xs + r * ROWB + 16 * q) = v;
-            }
-        }
-        __syncthreads();
-        // ---- ks taps: A from registers, B (one ds_read_b128 per fragment) from LDS
+            __syncthreads();
 #pragma unroll
-        for (int k = 0; k < MAXTAPS; ++k) {
-            if (k < ks) {
+            for (int k = 0; k < MAXTAPS; ++k) {
+                if (k < ks) {
 #pragma unroll
-                for (int j = 0; j < NT; ++j) {
-                    const int col = cw * WCOLS + j * 16 + l16;
-                    const half8 b = *(const half8 *)(xs + (col + k * p.dil) * ROWB + 16 * kg);
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k], b, acc[j], 0, 0, 0);
+                    for (int j = 0; j < NT; ++j) {
+                        const int col = cw * WCOLS + j * 16 + l16;
+                        const half8 b = *(const half8 *)(xs[0] + (col + k * p.dil) * ROWB + 16 * kg);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k], b, acc[j], 0, 0, 0);
+                    }
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
+    } else {
+        static_assert(MODE == IN_F16, "pipelined loop: f16 inputs");
+        // software pipeline over 32-channel blocks: block i+1's A fragments and input
+        // rows are loaded into registers while block i's MFMAs run on the LDS buffer
+        // filled last iteration (two LDS buffers, one barrier per block)
+        constexpr int RPT = ((BN + MAXHALO) * 4 + 255) / 256;  // 16-byte row pieces per thread
+        const int items = rows * 4;
+        half8 an[MAXTAPS];
+        uint4 xv[RPT];
+        auto load_blk = [&](int i0) {
+#pragma unroll
+            for (int k = 0; k < MAXTAPS; ++k)
+                if (k < ks) an[k] = *(const half8 *)(W + (size_t)orow * Kw + k * p.Cinp + i0 + 8 * kg);
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int e = tid + 256 * u;
+                const int t = t0 - pad + (e >> 2);
+                xv[u] = make_uint4(0u, 0u, 0u, 0u);
+                if (e < items && t >= 0 && t < p.T) xv[u] = *(const uint4 *)(xin + (size_t)t * p.Cinp + i0 + 8 * (e & 3));
+            }
+        };
+        load_blk(0);
+        int buf = 0;
+        for (int i0 = 0; i0 < p.Cinp; i0 += 32) {
+            half8 af[MAXTAPS];
+#pragma unroll
+            for (int k = 0; k < MAXTAPS; ++k) af[k] = an[k];
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int e = tid + 256 * u;
+                if (e < items) *(uint4 *)(xs[buf] + (e >> 2) * ROWB + 16 * (e & 3)) = xv[u];
+            }
+            if (i0 + 32 < p.Cinp) load_blk(i0 + 32);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < MAXTAPS; ++k) {
+                if (k < ks) {
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        const int col = cw * WCOLS + j * 16 + l16;
+                        const half8 b = *(const half8 *)(xs[buf] + (col + k * p.dil) * ROWB + 16 * kg);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k], b, acc[j], 0, 0, 0);
+                    }
+                }
+            }
+            buf ^= 1;
+        }
     }
     // ---- epilogue: C[row = 4*kg + r][col = l16] -> 4 consecutive channels of one time step
     const int o = m0 + rw * 16 + 4 * kg;
@@ -444,7 +494,11 @@ int ensure_buffers(mp_codec *c, int nchunk, int F) {
 template <int BM, int BN, int MODE>
 hipError_t launch_conv(const mpc::ConvP &p, int nchunk, int nbranch, hipStream_t s) {
     dim3 grid(p.Coutp / BM, nchunk * p.tiles_per_chunk, nbranch);
-    hipLaunchKernelGGL((mpc::conv_mfma_kernel<BM, BN, MODE>), grid, dim3(256), 0, s, p);
+    // fewer workgroups than ~4 per CU cannot hide the channel loop's load latency by
+    // occupancy: pipeline it instead (streaming chunks, the small early stages)
+    const bool pipe = MODE == mpc::IN_F16 && (size_t)grid.x * grid.y * grid.z < 1024;
+    if (pipe) hipLaunchKernelGGL((mpc::conv_mfma_kernel<BM, BN, mpc::IN_F16, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((mpc::conv_mfma_kernel<BM, BN, MODE, false>), grid, dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -450,6 +450,28 @@ hipError_t op_lt_pick(const GemvP &p, int NB, hipStream_t s) {
 // o_net + residual after lt_pick_kernel (its attention output in src, residual in addsrc)
 hipError_t op_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_gemv<8, 1, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 
+// ---------------------------------------------------------------- frame embedding
+// One workgroup per slot; each element summed over the 8 codebooks in order, /8,
+// + position: PRO_EMBED_LN's arithmetic, whose LayerNorm then runs in the qkv
+// GEMV's PRO_LN prologue (batches of 8+, where every qkv workgroup re-gathering
+// 9 rows per slot would cost more than this launch).
+__global__ __launch_bounds__(MP_BLOCK) void embed_kernel(EmbP p) {
+    const int b = blockIdx.x;
+    const int *c = p.codes + b * NCB;
+    const int ps = p.pos[b];
+    for (int k = threadIdx.x; k < D; k += MP_BLOCK) {
+        float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
+#pragma unroll
+        for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
+        p.x[(size_t)b * D + k] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
+    }
+}
+hipError_t op_embed(const EmbP &p, int NB, hipStream_t s) {
+    if (!p.emb || !p.codes || !p.pos_emb || !p.pos || !p.x) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(embed_kernel, dim3(NB), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- LT FFN
 // FFN up + GELU + FFN down of the local transformer in one launch
 // (magpie.cpp:983-992): workgroup p owns hidden units j in [32p, 32p+32). Its

@@ -87,6 +87,16 @@ struct LtFfnP {
     float *out;          // lt_merge_kernel: [B][256] = ltY + merged FFN down
 };
 
+// Frame embedding of every slot (layer 0's residual input, magpie.cpp:2746-2787,
+// 4376-4379): x[b] = (sum_cb emb[cb][code_cb]) / 8 + pos_emb[pos[b]]
+struct EmbP {
+    const float *emb;      // [8][2024][768]
+    const int *codes;      // [B][8] (codes_prev)
+    const float *pos_emb;
+    const int *pos;        // [B]
+    float *x;              // [B][768]
+};
+
 // splitmix64 finaliser
 __host__ __device__ inline unsigned long long mp_mix64(unsigned long long x) {
     x += 0x9E3779B97F4A7C15ull;

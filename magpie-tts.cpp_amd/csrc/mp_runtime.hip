@@ -68,6 +68,7 @@ MP_DECL_Q8(8)
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
 hipError_t q8_lt_em_1(const GemvP &, hipStream_t);
 hipError_t op_lt_pick(const GemvP &, int, hipStream_t);
+hipError_t op_embed(const EmbP &, int, hipStream_t);
 hipError_t op_lt_bo_8(const GemvP &, hipStream_t);
 hipError_t b16_lt_bo_8(const GemvP &, hipStream_t);
 hipError_t b16_lt_bo_16(const GemvP &, hipStream_t);
@@ -146,7 +147,7 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9 };
 struct OpRec {
     std::string name;
     int kind;
@@ -157,6 +158,7 @@ struct OpRec {
     XaP x;
     XaQ8P xq;
     LtFfnP lf;
+    EmbP e;
     int B;
     double bytes;
 };
@@ -678,10 +680,23 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.W = W.qkv; g.Wb = b16 ? m.pk_qkv[l] : nullptr; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
         g.Wq = W.qkv8.q; g.Wd = W.qkv8.d;
         g.kc = dev->kc; g.vc = dev->vc;
-        if (l == 0) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
+        // layer 0 embeds the frame (2746-2787) in the prologue; batches of 8+ embed it once
+        // in a separate launch instead of in every workgroup (the same arithmetic)
+        const bool embed_in = l == 0 && NB < 8;
+        if (l == 0 && !embed_in) {
+            mp::EmbP ep{m.audio_emb, dev->codes_prev, m.dec_pos, dev->pos, dev->x};
+            if (record) {
+                mp::OpRec r{};
+                r.name = "embed"; r.kind = mp::K_EMBED; r.e = ep; r.B = NB;
+                r.bytes = A * act * (9.0 * 768 + 768);
+                dev->ops.push_back(r);
+            }
+            HIPCHK(mp::op_embed(ep, NB, s));
+        }
+        if (embed_in) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
         {
-            const mp::GemvFn fn = W.qkv8 ? (l == 0 ? tq.qkv_embed : tq.qkv) : (l == 0 ? tb.qkv_embed : tb.qkv);
-            if ((rc = run(l == 0 ? "qkv_embed" : "qkv", fn, g,
+            const mp::GemvFn fn = W.qkv8 ? (embed_in ? tq.qkv_embed : tq.qkv) : (embed_in ? tb.qkv_embed : tb.qkv);
+            if ((rc = run(embed_in ? "qkv_embed" : "qkv", fn, g,
                           (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
         }
         // self-attention over the cache, one workgroup per (head, slot) (3457-3476)
@@ -1516,6 +1531,7 @@ int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
             case mp::K_LTFFN: e = mp::op_lt_ffn(r.lf, r.B, dev->stream); break;
             case mp::K_LTMERGE: e = mp::op_lt_merge(r.lf, r.B, dev->stream); break;
             case mp::K_LTPICK: e = mp::op_lt_pick(r.g, r.B, dev->stream); break;
+            case mp::K_EMBED: e = mp::op_embed(r.e, r.B, dev->stream); break;
             case mp::K_FIN: e = mp::op_finalize(r.f, r.B, dev->stream); break;
             }
             HIPCHK(e);
@@ -1549,6 +1565,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
         if (r.kind == mp::K_LTFFN) return mp::op_lt_ffn(r.lf, r.B, dev->stream);
         if (r.kind == mp::K_LTMERGE) return mp::op_lt_merge(r.lf, r.B, dev->stream);
         if (r.kind == mp::K_LTPICK) return mp::op_lt_pick(r.g, r.B, dev->stream);
+        if (r.kind == mp::K_EMBED) return mp::op_embed(r.e, r.B, dev->stream);
         return hipErrorInvalidValue;
     };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");

@@ -12,17 +12,22 @@ __global__ __launch_bounds__(256) void fill(float *sink, int iters) {
     __shared__ float s[16384];
     const float nan = __int_as_float(0x7fc00000);
     for (int i = threadIdx.x; i < 16384; i += 256) s[i] = nan;
-    float r[96];
+    float r[240];
 #pragma unroll
-    for (int i = 0; i < 96; ++i) r[i] = nan;
+    for (int i = 0; i < 240; ++i) r[i] = nan;
+    float ag[192];  // accumulation registers too (MFMA neighbours leave values there)
+#pragma unroll
+    for (int i = 0; i < 192; ++i) asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(ag[i]) : "v"(nan));
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
-        for (int i = 0; i < 96; ++i) asm volatile("" : "+v"(r[i]));
+        for (int i = 0; i < 240; ++i) asm volatile("" : "+v"(r[i]));
+#pragma unroll
+        for (int i = 0; i < 192; ++i) asm volatile("" : "+a"(ag[i]));
     }
     __syncthreads();
     float acc = 0.f;
 #pragma unroll
-    for (int i = 0; i < 96; ++i) acc += r[i];
+    for (int i = 0; i < 240; ++i) acc += r[i];
     if (acc == 1.0f) sink[threadIdx.x] = s[threadIdx.x];  // never true: keeps r and s live
 }
 int main(int argc, char **argv) {

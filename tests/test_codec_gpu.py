@@ -53,11 +53,15 @@ def test_codec_32_frame_chunk(gpu_codec, cpu_codec):
     assert np.abs(g - o).max() < WAVE_TOL
 
 
-def test_chunked_equals_independent(gpu_codec):
-    rng = np.random.default_rng(3)
-    chunks = rng.integers(0, 2016, (3, 8, 16)).astype(np.int32)
+@pytest.mark.parametrize("n,F", [(3, 16), (16, 32), (12, 4)])
+def test_chunked_equals_independent(gpu_codec, n, F):
+    """Chunks decoded together equal each chunk decoded alone, bit for bit: small
+    grids take the software-pipelined conv loop, large ones the occupancy-bound
+    loop, with the same arithmetic (16 x 32 frames puts every stage on the latter)."""
+    rng = np.random.default_rng(3 + n)
+    chunks = rng.integers(0, 2016, (n, 8, F)).astype(np.int32)
     batched = gpu_codec.decode_chunks(chunks)
-    for i in range(3):
+    for i in (range(n) if n <= 4 else (0, n // 2, n - 1)):
         np.testing.assert_array_equal(batched[i], gpu_codec.decode(chunks[i]))
 
 

@@ -77,9 +77,12 @@ struct ConvP {
 __device__ __forceinline__ float half_snake(float v, int c, int n_snake, int cin_real, const float *alpha) {
     // nano-codec.cpp:401-417 in ggml op order: mul, sin, sqr, div, add | leaky 0.01
     if (c < n_snake) {
+        // hardware sin (v_sin_f32) and a reciprocal instead of the libm sinf and an
+        // IEEE division: ~1e-7 relative, far below the f16 rounding every HalfSnake
+        // output gets next (the next conv's operand)
         const float a = alpha[c];
-        const float s = sinf(v * a);
-        return v + (s * s) / a;
+        const float s = __sinf(v * a);
+        return v + __fdividef(s * s, a);
     }
     if (c < cin_real) return v > 0.f ? v : 0.01f * v;
     return 0.f;

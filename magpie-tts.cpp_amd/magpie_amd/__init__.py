@@ -124,10 +124,16 @@ def synth_gguf(path: str, kind: str = "magpie", seed: int = 0x4D414750, dtype: s
     """Write (or reuse) a deterministic synthetic GGUF with the reference's layout."""
     if os.path.exists(path):
         return path
-    cmd = [SYNTH_BIN, kind, path, "--seed", str(seed)]
+    tmp = f"{path}.tmp{os.getpid()}"  # written aside, then renamed: never a partial file at `path`
+    cmd = [SYNTH_BIN, kind, tmp, "--seed", str(seed)]
     if kind == "magpie":
         cmd += ["--dtype", dtype, "--dec-layers", str(dec_layers), "--enc-layers", str(enc_layers)]
-    subprocess.run(cmd, check=True)
+    try:
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, path)
+    finally:
+        if os.path.exists(tmp):
+            os.remove(tmp)
     return path
 
 

@@ -198,38 +198,6 @@ __device__ __forceinline__ void wave_meanvar(const float (&v)[PER], float &mean,
     var = bcast_lane63(M2) * (1.0f / (64.f * PER));
 }
 
-// ---- in-launch hand-off (cdna_hip_programming.md §5 "In-launch split-K
-// reduction", sc1 form, and §6 Guideline 16): partials are stored write-through
-// (sc1, relaxed agent-scope atomics), every storing wave drains vmcnt, the
-// workgroup barriers, lane 0 draws an arrival ticket; the workgroup that draws
-// n-1 combines, reading the partials with sc1 loads or behind an agent acquire.
-__device__ __forceinline__ void st_sc1(float *p, float a, float b) {
-    const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
-    __hip_atomic_store((unsigned long long *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float *p) {
-    return __uint_as_float(__hip_atomic_load((const unsigned *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-// Returns true in every thread of the last-arriving workgroup (uniform).
-// flag: one LDS word of the caller's existing shared array.
-__device__ __forceinline__ bool arrive_last(unsigned *cnt, unsigned n, float *flag, bool sc1_loads) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = t == n - 1;
-        if (last) {
-            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-            if (!sc1_loads) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *flag = last ? 1.f : 0.f;
-    }
-    __syncthreads();
-    return *flag != 0.f;
-}
-
 // (value, index) argmax with the reference's tie rule: the FIRST maximal index
 // wins (strict '>' scan from index 0, magpie.cpp:1250-1258).
 __device__ __forceinline__ void argmax_merge(float &v, int &i, float v2, int i2) {

@@ -97,6 +97,30 @@ def test_batched_longform_equals_sequential(ma, small_model, codec):
     dev.close()
 
 
+def test_batched_stream_stop_one_utterance(ma, small_model, codec):
+    """A callback stopping one utterance of a batch ends that utterance only (its
+    chunks already decoded this round are dropped); the others stream on unchanged."""
+    sents = [ma.synthetic_tokens(8 + 3 * i, seed=500 + i) for i in range(3)]
+    kw = dict(max_dec_steps=16, frames_per_chunk=4, ignore_eos=True)
+    dev = ma.Device(small_model)
+    got = {0: [], 1: [], 2: []}
+
+    def cb(utt, audio):
+        got[utt].append(audio)
+        return utt != 1
+
+    codes_b, total, _ = dev.synthesize_stream(codec, sents, cb, speakers=[0, 1, 2], **kw)
+    assert len(got[1]) == 1 and len(codes_b[1]) == 4
+    assert total == (16 + 4 + 16) * 1024
+    for i in (0, 2):
+        chunks_s, cbs = _collect(1)
+        codes_s, _, _ = dev.synthesize_stream(codec, [sents[i]], cbs, speakers=[i], stream_base=i, **kw)
+        assert np.array_equal(codes_s[0], codes_b[i])
+        assert len(chunks_s[0]) == len(got[i]) == 4
+        assert all(np.array_equal(x, y) for x, y in zip(chunks_s[0], got[i]))
+    dev.close()
+
+
 def test_lt_sample_matches_oracle(ma, oracle, small_model):
     rng = np.random.default_rng(5)
     dev = ma.Device(small_model)

@@ -474,11 +474,11 @@ hipError_t op_embed(const EmbP &p, int NB, hipStream_t s) {
 
 // ---------------------------------------------------------------- LT FFN
 // FFN up + GELU + FFN down of the local transformer in one launch
-// (magpie.cpp:983-992): workgroup p owns hidden units j in [32p, 32p+32). Its
-// weights (32 rows of W1, the 32-column slice of W2 that row n = thread n
+// (magpie.cpp:983-992): workgroup p owns hidden units j in [16p, 16p+16). Its
+// weights (16 rows of W1, the 16-column slice of W2 that row n = thread n
 // reads) are issued first; every slot's LN(y) row is built by one wave (DPP
-// statistics, the same code at every batch size), a wave computes 8 units per
-// slot (float4 lanes, DPP sum, GELU) into LDS, then thread n adds its 32 units'
+// statistics, the same code at every batch size), a wave computes 4 units per
+// slot (float4 lanes, DPP sum, GELU) into LDS, then thread n adds its 16 units'
 // contributions to output n in ascending order. The LT_FFN_P partial sums are
 // merged (ascending p) by the head's prologue at batch 1 or by lt_merge_kernel.
 template <int NB>

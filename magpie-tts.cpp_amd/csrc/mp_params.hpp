@@ -25,7 +25,7 @@ constexpr int SA_SPLITS = 4;        // key splits of each SA head (sa_attn_kerne
 constexpr int SA_PART = 4 + DH;     // per (slot, head, split): m, l, -, -, O[64] (unnormalised)
 constexpr int XA_SPLITS = 4;        // text-key splits of the fused cross-attention (xa_part_kernel)
 constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
-constexpr int LT_FFN_P = 32;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
+constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
 enum Pro {
@@ -76,7 +76,7 @@ struct Sampling {
 };
 
 // LT FFN up + GELU + FFN down in one launch (lt_ffn_kernel): workgroup p owns
-// hidden units [p*32, p*32+32) and writes its share of FFN down, part[b][p][256]
+// hidden units [p*16, p*16+16) and writes its share of FFN down, part[b][p][256]
 struct LtFfnP {
     const float *y;      // [B][256] LT residual stream after attention (ltY)
     const float *lnw;    // norm_pos_ff weight

@@ -111,6 +111,13 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames);
 /* decoder hidden state after every step (BOS first): [B][max_dec_steps+1][768];
  * requires params.trace_hidden. */
 int mp_hip_get_trace(mp_dev *dev, float *hidden);
+/* Diagnostics: copy a per-batch device buffer to host after mp_hip_begin_batch /
+ * mp_hip_decode. name: "enc_out" [NB][Tmax][768] (magpie_encode_text's output),
+ * "xak"/"xav" [NB][L][Tmax][128] (XA K/V, magpie.cpp:1663-1711), "kc"/"vc"
+ * [NB][L][max_seq][768] (SA cache), "x" [NB][768] (residual stream). Writes at
+ * most `bytes`; returns the buffer's size in bytes (host may be NULL to query),
+ * or a negative MP_ERR_*. */
+int64_t mp_hip_debug_buffer(mp_dev *dev, const char *name, void *host, int64_t bytes);
 
 /* Streaming variant of mp_hip_decode (magpie_synthesize_sentence_streaming's
  * frame loop, magpie.cpp:4762-4838, for every utterance of the batch): every

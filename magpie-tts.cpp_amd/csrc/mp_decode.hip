@@ -100,7 +100,7 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     __shared__ __attribute__((aligned(16))) float wo[SA_WAVES][DH];
     const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
-    const int L = p.pos[b] + 1;
+    const int L = ld_fresh_u(p.pos + b) + 1;
     const int chunk = (L + SA_SPLITS - 1) / SA_SPLITS;
     const int j0 = sp * chunk, j1 = min(L, j0 + chunk);
     float m = -INFINITY, l = 0.f;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
     __shared__ float wm[XA_WAVES], wl[XA_WAVES];
     __shared__ float wo[XA_WAVES][D];
     const int sp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int Tb = p.T[b];
+    const int Tb = ld_fresh_u(p.T + b);
     const int chunk = (Tb + XA_SPLITS - 1) / XA_SPLITS;
     const int t0 = sp * chunk, t1 = min(Tb, t0 + chunk);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
@@ -268,18 +268,19 @@ hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
 // decoder input and the position advances.
 __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
     const int b = blockIdx.x, tid = threadIdx.x;
-    if (p.done[b]) return;
+    if (ld_fresh_u(p.done + b)) return;
     __shared__ float red[8];
     int i0, amax;
     if (p.smp.on) {  // one wave draws
         __shared__ float scratch[2 * VCB];
         if (tid >= 64) return;
-        i0 = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || p.step[b] < 4, p.audio_bos, p.audio_eos, p.smp,
-                       b, p.step[b], NCB - 1, scratch, amax);
+        const int stp = ld_fresh_u(p.step + b);
+        i0 = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp,
+                       NCB - 1, scratch, amax);
         if (tid != 0) return;
     } else {
         const float *lg = p.logits + (size_t)b * VCB;
-        const bool forbid_eos = p.ignore_eos || p.step[b] < 4;
+        const bool forbid_eos = p.ignore_eos || ld_fresh_u(p.step + b) < 4;
         float bv = -INFINITY;
         int bi = 0x7fffffff;
         for (int i = tid; i < VCB; i += MP_BLOCK) {
@@ -297,16 +298,20 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
         if (i0 < 0 || i0 >= VCB) i0 = 0;
         amax = i0;
     }
-    int *cc = p.codes_cur + b * NCB;
+    int *ccp = p.codes_cur + b * NCB;
+    ccp[NCB - 1] = i0;
+    int cc[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB - 1; ++cb) cc[cb] = ld_fresh_u(ccp + cb);
     cc[NCB - 1] = i0;
     if (p.smp.amax) p.smp.amax[b * NCB + NCB - 1] = amax;
     // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
     bool eos = amax == p.audio_eos;
-    eos |= p.smp.argeos[b] != 0;
+    eos |= ld_fresh_u(p.smp.argeos + b) != 0;
     p.smp.argeos[b] = 0;
     if (p.lt_only) return;  // magpie_local_transformer_sample_all: codes only
     for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
-    const int s = p.step[b];
+    const int s = ld_fresh_u(p.step + b);
     if (eos) {
         // graph_reuse drops the EOS frame (4349-4352); the streaming loop emits it (4800-4806)
         if (p.emit_eos)
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
         return;
     }
     for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
-    p.pos[b] += 1;
+    p.pos[b] = ld_fresh_u(p.pos + b) + 1;
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -420,7 +425,7 @@ __global__ __launch_bounds__(64) void lt_pick_kernel(GemvP p) {
     }
     float lv[PICK_R];
     load_logits(p.logits + (size_t)b * VCB, lv);
-    const int stp = p.step[b];
+    const int stp = ld_fresh_u(p.step + b);
     int amax;
     const int code = wave_pick_v(lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, p.cb - 1, wsc,
                                  amax);
@@ -457,8 +462,10 @@ hipError_t op_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_gemv<8, 1, 
 // 9 rows per slot would cost more than this launch).
 __global__ __launch_bounds__(MP_BLOCK) void embed_kernel(EmbP p) {
     const int b = blockIdx.x;
-    const int *c = p.codes + b * NCB;
-    const int ps = p.pos[b];
+    int c[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) c[cb] = ld_fresh_u(p.codes + b * NCB + cb);
+    const int ps = ld_fresh_u(p.pos + b);
     for (int k = threadIdx.x; k < D; k += MP_BLOCK) {
         float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
 #pragma unroll

@@ -58,11 +58,46 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
-// (lgkmcnt) but NOT for outstanding global loads, so a weight stream issued
-// before a prologue stays in flight across it (__syncthreads() would drain it).
-// The "memory" clobber keeps the compiler from moving memory ops across.
-__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Workgroup barrier for LDS hand-offs only: LDS-scoped release/acquire fences
+// around s_barrier lower to `s_waitcnt lgkmcnt(0); s_barrier` and do NOT wait
+// for outstanding global loads, so a weight stream issued before a prologue
+// stays in flight across it (__syncthreads() would drain it with vmcnt(0)).
+// Compiler-visible (no inline asm): the waitcnt and scheduling passes see it.
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// LDS ordering among the lanes of one wave (wave-private LDS scratch)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Read of a value another launch of the same decode iteration wrote (positions,
+// steps, done flags, codes, split softmax states, the sampling config): always a
+// VECTOR load at agent scope (`global_load … sc1`, served by L2/MALL). A plain
+// load of a wave-uniform address is compiled to `s_load` through the scalar
+// cache, and inside a replayed hipGraph such reads were observed to return the
+// previous frame's value (a sampled batch of 16 drew with a stale step and left
+// its single-utterance runs; tests/test_decode_gpu.py::test_sampled_batch_equals_single),
+// so no mutable cross-launch datum goes through the scalar cache.
+template <class T>
+__device__ __forceinline__ T ld_fresh(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// ld_fresh of a wave-uniform address, returned in an SGPR (readfirstlane) so the
+// compiler can use it in scalar address arithmetic and batch the loads it feeds
+__device__ __forceinline__ int ld_fresh_u(const int *p) { return __builtin_amdgcn_readfirstlane(ld_fresh(p)); }
+__device__ __forceinline__ float ld_fresh_u(const float *p) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ld_fresh(p))));
+}
+__device__ __forceinline__ unsigned long long ld_fresh_u(const unsigned long long *p) {
+    const unsigned long long v = ld_fresh(p);
+    return (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v) |
+           ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32)) << 32);
+}
 
 // Block-wide reduction for 256 threads; `red` is an LDS scratch of >= 4 floats.
 // Every thread returns the total. Contains two barriers.

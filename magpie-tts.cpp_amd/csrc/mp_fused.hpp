@@ -50,9 +50,9 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
     if (bi < 0 || bi >= VCB) bi = 0;
     amax = bi;
     if (!smp.on) return bi;
-    const float temp = smp.cfg->temperature;
+    const float temp = ld_fresh_u(&smp.cfg->temperature);
     const float M = bv;
-    const int k = min(max(smp.cfg->top_k, 1), VCB);
+    const int k = min(max(ld_fresh_u(&smp.cfg->top_k), 1), VCB);
     // order-preserving keys; padding lanes get 0 (below every real key)
     unsigned key[R];
 #pragma unroll
@@ -90,7 +90,7 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
         }
         base += __popcll(bs);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wave_lds_sync();
     // counting rank (descending value, ascending index), then scatter in place
     constexpr int RK = (VCB + 63) / 64;
     float ev[RK];
@@ -111,19 +111,17 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
             ei[j] = i;
         }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     for (int j = 0; j < RK; ++j) {
         if (j * 64 >= k) break;
         if (lane + 64 * j < k) { sv[rk[j]] = ev[j]; si[rk[j]] = ei[j]; }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     int code = 0;
     if (lane == 0) {
         float sum = 0.f;
         for (int i = 0; i < k; ++i) sum += sv[i];
-        const float u = mp_uniform(smp.cfg->seed, smp.cfg->stream_base + stream, step, cb);
+        const float u = mp_uniform(ld_fresh_u(&smp.cfg->seed), ld_fresh_u(&smp.cfg->stream_base) + stream, step, cb);
         float cum = 0.f;
         code = si[k - 1];
         for (int i = 0; i < k; ++i) {
@@ -132,8 +130,7 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
         }
     }
     code = __shfl(code, 0, 64);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     return code;
 }
 __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos, int audio_eos, const Sampling &smp,
@@ -155,7 +152,7 @@ constexpr int ltc_off() { return NB * LTD; }
 // from kr/vr when PRE (loaded ahead by the caller), else from ltk/ltv. The
 // arithmetic is the same either way, at every batch size.
 template <bool CUR, bool PRE>
-__device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4,
+__device__ __noinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4,
                                             const float4 (&kr)[NCB], const float4 (&vr)[NCB]) {
     const int lane = threadIdx.x & 63;
     const int nk = p.cb + 1;
@@ -219,8 +216,8 @@ __device__ __forceinline__ void merge_weights(const float *pp, int stride, int n
         float ms[NS], ls[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            ms[s] = pp[((size_t)q * NS + s) * stride];
-            ls[s] = pp[((size_t)q * NS + s) * stride + 1];
+            ms[s] = ld_fresh(pp + ((size_t)q * NS + s) * stride);
+            ls[s] = ld_fresh(pp + ((size_t)q * NS + s) * stride + 1);
         }
         float M = -INFINITY;
 #pragma unroll
@@ -376,7 +373,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             wave_meanvar<PER>(v, mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
             const bool st = p.hidden_out && blockIdx.x == 0;
-            const int s = (p.trace && blockIdx.x == 0) ? p.step[b] : 0;
+            const int s = (p.trace && blockIdx.x == 0) ? ld_fresh_u(p.step + b) : 0;
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int k = lane + 64 * i;
@@ -399,7 +396,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         wave_meanvar<PER>(v, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.eps);
         const bool st = p.hidden_out && blockIdx.x == 0;
-        const int s = (p.trace && blockIdx.x == 0) ? p.step[0] : 0;
+        const int s = (p.trace && blockIdx.x == 0) ? ld_fresh_u(p.step) : 0;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             if (i / Q != w) continue;
@@ -414,8 +411,10 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         static_assert(K == D, "embed prologue is d_model wide");
         const int lane = tid & 63, w = tid >> 6;
         for (int b = w; b < NB; b += MP_NWAVES) {
-            const int *c = p.codes + b * NCB;
-            const int ps = p.pos[b];
+            int c[NCB];
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) c[cb] = ld_fresh_u(p.codes + b * NCB + cb);
+            const int ps = ld_fresh_u(p.pos + b);
             float x[K / 64];
 #pragma unroll
             for (int i = 0; i < K / 64; ++i) {
@@ -440,8 +439,10 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         static_assert(K == D, "embed prologue is d_model wide");
         const int lane = tid & 63, w = tid >> 6;
         constexpr int PER = K / 64, Q = PER / MP_NWAVES;
-        const int *c = p.codes;
-        const int ps = p.pos[0];
+        int c[NCB];
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) c[cb] = ld_fresh_u(p.codes + cb);
+        const int ps = ld_fresh_u(p.pos);
         float x[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -462,7 +463,9 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             act[k] = ((x[i] - mean) * rstd) * p.lnw[k];
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_LTX_LN && NB >= 2) {
+    } else if constexpr (PRO == PRO_LTX_LN) {
+        // one wave per slot at every batch size (wave_block_meanvar), so a batch
+        // reproduces its utterances run alone bit for bit
         const int lane = tid & 63, w = tid >> 6;
         for (int b = w; b < NB; b += MP_NWAVES) {
             float X[4];
@@ -502,7 +505,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         }
         int stp[SPW];  // every owned slot's step up front, not one dependent load per pick
 #pragma unroll
-        for (int j = 0; j < SPW; ++j) stp[j] = w + MP_NWAVES * j < NB ? p.step[w + MP_NWAVES * j] : 0;
+        for (int j = 0; j < SPW; ++j) stp[j] = w + MP_NWAVES * j < NB ? ld_fresh_u(p.step + w + MP_NWAVES * j) : 0;
         unsigned long long codes = 0ull;  // 16 bits per owned slot (codes < 2048)
 #pragma unroll
         for (int j = 0; j < SPW; ++j) {
@@ -559,19 +562,6 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             *(float4 *)(act + b * K + 4 * lane) = lt_attend<false, false>(p, b, q4, q4, q4, kr, vr);
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_LTX_LN) {
-        static_assert(K == LTD, "LT is 256 wide");
-        for (int b = 0; b < NB; ++b) {
-            const int k = tid;
-            const float X = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
-            if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X;
-            const float xv[1] = {X};
-            float mean, var;
-            block_meanvar<1>(xv, red, mean, var);
-            const float rstd = 1.0f / sqrtf(var + p.eps);
-            act[b * K + k] = ((X - mean) * rstd) * p.lnw[k];
-        }
-        lds_sync();
     }
 }
 
@@ -589,7 +579,7 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b,
     else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
     else if constexpr (EPI == EPI_LTX_ADD) p.out[(size_t)b * p.out_ld + n] = v + extra;  // extra = X[b][n]
     else if constexpr (EPI == EPI_QKV) {
-        const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + p.pos[b]) * D;
+        const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + ld_fresh(p.pos + b)) * D;
         if (n < D) p.out[(size_t)b * D + n] = v;
         else if (n < 2 * D) p.kc[slot + n - D] = v;
         else p.vc[slot + n - 2 * D] = v;

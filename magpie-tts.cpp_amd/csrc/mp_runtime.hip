@@ -775,6 +775,30 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
 // The local transformer over one frame (magpie_local_transformer_sample_all,
 // magpie.cpp:1113-1317) + the frame bookkeeping (4320-4358), for NB slots whose
 // buffers `io` names. lt_only: in_proj of a given normalised hidden, codes only.
+// MAGPIE_EAGER=1: launch the iteration's kernels directly instead of replaying
+// the captured graph (identical kernels and arguments; used under rocprofv3,
+// whose kernel tracer crashes on graph replays on this image).
+bool eager_mode() {
+    const char *e = getenv("MAGPIE_EAGER");
+    return e && atoi(e) != 0;
+}
+
+// Diagnostics (MAGPIE_EAGER=1 and MAGPIE_DUMP_LT=file): after every launch of
+// the local transformer, slot 0's LT state is appended to the file as f32
+// records [logits 2024 | codes_cur 8 (int bits) | ltX | ltY | lty2 | ltq 256 each].
+void dump_lt(const mp::LtIo &io, hipStream_t s) {
+    const char *path = getenv("MAGPIE_DUMP_LT");
+    if (!path || !eager_mode() || hipStreamSynchronize(s) != hipSuccess) return;
+    std::vector<float> rec(2024 + 8 + 4 * 256);
+    float *p = rec.data();
+    auto get = [&](const void *src, size_t n) {
+        if (hipMemcpy(p, src, n * 4, hipMemcpyDeviceToHost) != hipSuccess) return;
+        p += n;
+    };
+    get(io.logits, 2024); get(io.codes_cur, 8); get(io.ltX, 256); get(io.ltY, 256); get(io.lty2, 256); get(io.ltq, 256);
+    if (FILE *fp = fopen(path, "ab")) { fwrite(rec.data(), 4, rec.size(), fp); fclose(fp); }
+}
+
 int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vector<mp::OpRec> *ops) {
     const mp::Model &m = dev->m;
     const bool b16 = m.weight_mode == MP_WEIGHTS_BF16;
@@ -788,6 +812,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             ops->push_back(r);
         }
         HIPCHK(fn(g, s));
+        dump_lt(io, s);
         return MP_OK;
     };
     auto base = [&]() {
@@ -855,6 +880,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                 ops->push_back(r);
             }
             HIPCHK(mp::op_lt_pick(g, NB, s));
+            dump_lt(io, s);
             g = base(); g.cb = cb;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.src = io.ltq; g.src_ld = 256; g.out = io.ltY; g.out_ld = 256;
             g.addsrc = io.ltX; g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
@@ -1210,13 +1236,6 @@ int reset_decode_state(mp_dev *dev) {
     return MP_OK;
 }
 
-// MAGPIE_EAGER=1: launch the iteration's kernels directly instead of replaying
-// the captured graph (identical kernels and arguments; used under rocprofv3,
-// whose kernel tracer crashes on graph replays on this image).
-bool eager_mode() {
-    const char *e = getenv("MAGPIE_EAGER");
-    return e && atoi(e) != 0;
-}
 
 // Capture the iteration graph (or, eager, record the op list) once per batch
 // configuration; leaves the decode state reset.
@@ -1352,6 +1371,12 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
         bool more = false;
         for (int b = 0; b < B; ++b) more |= !(h_done[b] != 0 || stopped[b]);
         more &= it < S;
+        // the next chunk's iterations are queued before this round's codec work, so
+        // the decode runs on its stream while the codec runs on the codec's (bit-exact
+        // beside it: tests/test_concurrency_gpu.py); a stop requested by a callback
+        // below takes effect after that chunk, whose frames are then not delivered
+        if (more)
+            if (int rc = enqueue_chunk(slot ^ 1)) return rc;
         // this round's chunks, utterance by utterance, in delivery order
         jobs.clear();
         for (int b = 0; b < B; ++b) {
@@ -1413,10 +1438,6 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
             }
         }
         if (!more) break;
-        // The next chunk is queued only now, after the codec: with the codec's kernels
-        // running beside the decode iterations the decoded frames were observed to
-        // change (open item), so the two do not overlap.
-        if (int rc = enqueue_chunk(slot ^ 1)) return rc;
         slot ^= 1;
     }
     HIPCHK(hipStreamSynchronize(dev->stream));
@@ -1480,6 +1501,28 @@ int mp_hip_get_trace(mp_dev *dev, float *hidden) {
     if (!dev->trace) return fail(dev, MP_ERR_STATE, "trace_hidden was not enabled");
     HIPCHK(hipMemcpy(hidden, dev->trace, (size_t)dev->B * (dev->max_steps + 1) * 768 * 4, hipMemcpyDeviceToHost));
     return MP_OK;
+}
+
+int64_t mp_hip_debug_buffer(mp_dev *dev, const char *name, void *host, int64_t bytes) {
+    if (!dev || !name || bytes < 0) return MP_ERR_ARG;
+    if (!dev->batch_ready) return fail(dev, MP_ERR_STATE, "no batch");
+    const size_t NB = dev->NB, L = dev->m.dec_layers, T = dev->Tmax, S = dev->max_seq;
+    const std::string n(name);
+    const void *src = nullptr;
+    size_t sz = 0;
+    if (n == "enc_out") { src = dev->enc_out; sz = NB * T * 768 * 4; }
+    else if (n == "xak") { src = dev->xak; sz = NB * L * T * 128 * 4; }
+    else if (n == "xav") { src = dev->xav; sz = NB * L * T * 128 * 4; }
+    else if (n == "kc") { src = dev->kc; sz = NB * L * S * 768 * 4; }
+    else if (n == "vc") { src = dev->vc; sz = NB * L * S * 768 * 4; }
+    else if (n == "x") { src = dev->x; sz = NB * 768 * 4; }
+    else return fail(dev, MP_ERR_ARG, "unknown buffer " + n);
+    if (host) {
+        HIPCHK(hipSetDevice(dev->device));
+        HIPCHK(hipStreamSynchronize(dev->stream));
+        HIPCHK(hipMemcpy(host, src, std::min<size_t>(sz, (size_t)bytes), hipMemcpyDeviceToHost));
+    }
+    return (int64_t)sz;
 }
 
 int mp_hip_get_timing(mp_dev *dev, mp_timing *t) {

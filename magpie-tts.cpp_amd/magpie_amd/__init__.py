@@ -70,6 +70,7 @@ SYMBOLS = [
     ("mp_hip_begin_batch", _I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(mp_params)]),
     ("mp_hip_decode", _I, [_P, _P, _P]),
     ("mp_hip_get_trace", _I, [_P, _P]),
+    ("mp_hip_debug_buffer", ctypes.c_int64, [_P, ctypes.c_char_p, _P, ctypes.c_int64]),
     ("mp_hip_get_timing", _I, [_P, ctypes.POINTER(mp_timing)]),
     ("mp_hip_decode_stream", _I, [_P, _P, _I, AUDIO_CB, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)]),
     ("mp_hip_lt_sample", _I, [_P, _P, ctypes.c_float, _I, _I, ctypes.c_uint64, _P, _P]),
@@ -265,6 +266,15 @@ class Device:
             self._check(self.lib.mp_hip_get_trace(self.h, hidden.ctypes.data))
         return SynthResult([codes[b, :nf[b]].copy() for b in range(B)], nf, tm.preamble_ms, tm.decode_ms,
                            tm.iterations, hidden)
+
+    def debug_buffer(self, name: str) -> np.ndarray:
+        """mp_hip_debug_buffer: a per-batch device buffer (flat f32) for diagnostics."""
+        n = self.lib.mp_hip_debug_buffer(self.h, name.encode(), None, 0)
+        if n < 0:
+            self._check(int(n))
+        out = np.zeros(n // 4, np.float32)
+        self._check(0 if self.lib.mp_hip_debug_buffer(self.h, name.encode(), out.ctypes.data, n) == n else -5)
+        return out
 
     # ---- measurement
     def ops(self) -> List[str]:

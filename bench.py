@@ -82,8 +82,8 @@ def measure_extra(model_path: str, codec_path, args) -> dict:
     # long-form audio streamed sentence by sentence with 4-frame codec chunks; the
     # sentences run as one device batch (magpie_synthesize_streaming's sentence
     # batching), fixed 216 frames each (EOS masked) -> 6 x 216 = 1296 frames = 60.2 s.
-    q8_path = os.path.join(os.path.dirname(model_path), "magpie_357m_q8.gguf")
-    ma.synth_gguf(q8_path, dtype="q8_0")
+    q8_path = os.path.join(os.path.dirname(model_path), "magpie_357m_q8_k32.gguf")
+    ma.synth_gguf(q8_path, dtype="q8_0", lt_head_scale=ma.DECISIVE)
     dev = ma.Device(q8_path, weights="q8")
     tok1 = [ma.synthetic_tokens(args.tokens, seed=1000)]
     dev.synthesize(tok1, speakers=[0], max_dec_steps=args.frames, ignore_eos=True)
@@ -131,12 +131,28 @@ def measure_extra(model_path: str, codec_path, args) -> dict:
     return out
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly (no torchrun env): start N ranks, one
+    process per GPU, through torch.distributed.run on 127.0.0.1 as CHILD
+    processes (this process never touches the GPU) and return their exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs of this node, one rank each")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU (configs[1]: 1)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="utterances per GPU (default: configs[1]'s 1 at N=1, configs[3]'s 8 at N>1)")
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--tokens", type=int, default=TEXT_TOKENS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -145,28 +161,57 @@ def main() -> None:
     ap.add_argument("--profile-ops", type=int, default=32, help="in-situ event-timed iterations for the op table")
     ap.add_argument("--no-codec", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the bf16 batch / streaming measurements")
-    ap.add_argument("--weights", choices=["f32", "bf16"], default="f32",
-                    help="f32 = configs[1]; bf16 = configs[2]/[3] (decode projections on bf16 MFMA, batch <= 16)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="resolve ranks / workload, rendezvous over gloo, print one line per rank, no GPU work")
+    ap.add_argument("--weights", choices=["f32", "bf16"], default=None,
+                    help="f32 = configs[1]; bf16 = configs[2]/[3] (decode projections on bf16 MFMA, batch <= 16); "
+                         "default f32 at N=1, bf16 at N>1")
     args = ap.parse_args()
-
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    # N=1: configs[1] (f32, one utterance); N>1: configs[3] (bf16, 8 utterances per GPU)
+    if args.weights is None:
+        args.weights = "f32" if world == 1 else "bf16"
+    if args.batch is None:
+        args.batch = 1 if world == 1 else 8
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: E402  (gloo: barrier + max only)
         dist.init_process_group("gloo")
+    if args.dry_run:
+        seen = [None] * world
+        if dist is not None:
+            dist.all_gather_object(seen, rank)
+            dist.destroy_process_group()
+        else:
+            seen = [rank]
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world, "ranks_seen": seen,
+                          "weights": args.weights, "batch_per_gpu": args.batch}), flush=True)
+        return
+    # one rank per GPU; with fewer GPUs than ranks (a rehearsal) ranks share devices
+    ndev = ma.device_count()
+    if ndev < 1:
+        sys.exit("bench.py: no HIP device visible")
+    device = local % ndev
 
     cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
     os.makedirs(cache, exist_ok=True)
-    model_path = os.path.join(cache, "magpie_357m_f32.gguf")
+    # the parity tests' model (decisive LT heads; the shapes, bytes and timings are those of any Magpie-357M)
+    model_path = os.path.join(cache, "magpie_357m_f32_k32.gguf")
     if rank == 0 or world == 1:
-        ma.synth_gguf(model_path)
+        ma.synth_gguf(model_path, lt_head_scale=ma.DECISIVE)
     if dist is not None:
         dist.barrier()
-        ma.synth_gguf(model_path)  # no-op once rank 0 wrote it
+        ma.synth_gguf(model_path, lt_head_scale=ma.DECISIVE)  # no-op once rank 0 wrote it
 
-    dev = ma.Device(model_path, device=local, weights=args.weights)
+    dev = ma.Device(model_path, device=device, weights=args.weights)
     B = args.batch
     toks = [ma.synthetic_tokens(args.tokens, seed=1000 + rank * B + b) for b in range(B)]
     speakers = [(rank * B + b) % 5 for b in range(B)]
@@ -196,12 +241,17 @@ def main() -> None:
     assert frames == args.steps * B * args.frames, f"expected fixed-length output, got {frames} frames"
 
     t_max = elapsed
+    per_rank = [{"rank": rank, "device": device, "frames": frames, "s": round(elapsed, 4),
+                 "fps": round(frames / elapsed, 1)}]
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
-    total_frames = frames * world
+        allr = [None] * world
+        dist.all_gather_object(allr, per_rank[0])
+        per_rank = allr
+    total_frames = sum(r["frames"] for r in per_rank)
     value = total_frames / t_max
     ms_per_step = 1e3 * t_max / args.steps
 
@@ -213,7 +263,7 @@ def main() -> None:
             ma.synth_gguf(codec_path, kind="codec")
         if dist is not None:
             dist.barrier()
-        cdc = ma.Codec(codec_path, device=local)
+        cdc = ma.Codec(codec_path, device=device)
         chunks = []
         for b in range(B):
             c = rr.codes[b]
@@ -318,6 +368,7 @@ def main() -> None:
                                    f"({'configs[1]' if args.weights == 'f32' else 'configs[2]/[3] shape'})",
                        "global_batch": B * world, "frames_per_utterance": args.frames, "text_tokens": args.tokens,
                        "parallelism": f"replicas x{world} (utterance-partitioned, no collectives)"},
+            "ranks": {"seen": len(per_rank), "devices_visible": ndev, "per_rank": per_rank},
             "rtf_per_stream": round(value / world / B / ma.FRAMES_PER_SECOND, 2),
             "decode_fps_events": round(B * args.frames * 1e3 / float(np.mean(decode_ms)), 2),
             "e2e_fps_first_call": round(B * args.frames / e2e_first_s, 2),

@@ -120,15 +120,22 @@ def build(jobs: int = 8) -> None:
     subprocess.run(["make", "-C", PKG_DIR, f"-j{jobs}"], check=True)
 
 
+# LT output-head scale of the parity/bench models: logits wide enough that >= 98 % of
+# greedy decisions have a top-1/top-2 gap above 1e-2 (1.0 leaves 58 % below it)
+DECISIVE = 32.0
+
+
 def synth_gguf(path: str, kind: str = "magpie", seed: int = 0x4D414750, dtype: str = "f32",
-               dec_layers: int = 12, enc_layers: int = 6) -> str:
-    """Write (or reuse) a deterministic synthetic GGUF with the reference's layout."""
+               dec_layers: int = 12, enc_layers: int = 6, lt_head_scale: float = 1.0) -> str:
+    """Write (or reuse) a deterministic synthetic GGUF with the reference's layout.
+    lt_head_scale multiplies the std of the LT output heads (weights and bias)."""
     if os.path.exists(path):
         return path
     tmp = f"{path}.tmp{os.getpid()}"  # written aside, then renamed: never a partial file at `path`
     cmd = [SYNTH_BIN, kind, tmp, "--seed", str(seed)]
     if kind == "magpie":
-        cmd += ["--dtype", dtype, "--dec-layers", str(dec_layers), "--enc-layers", str(enc_layers)]
+        cmd += ["--dtype", dtype, "--dec-layers", str(dec_layers), "--enc-layers", str(enc_layers),
+                "--lt-head-scale", repr(float(lt_head_scale))]
     try:
         subprocess.run(cmd, check=True)
         os.replace(tmp, path)

@@ -11,6 +11,7 @@
 //
 // usage: mp_synth_gguf magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|f16]
 //                      [--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V]
+//                      [--lt-head-scale K]  (LT output head weights N(0, (0.02 K)^2): decisive logits)
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -22,6 +23,7 @@ enum { KV_U32 = 4, KV_F32 = 6, KV_STR = 8 };
 
 static uint64_t g_seed = 0x4D414750ull;  // "MAGP"
 static float g_eos_bias = 0.f;            // test-only: added to out_proj[3].bias[2017]
+static float g_lt_head_scale = 1.f;       // LT output heads std = 0.02 * this
 
 static uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -216,9 +218,11 @@ static void plan_magpie(int dtype, int dec_layers, int enc_layers, int dec_pos) 
     LNW("local_transformer.layers.0.norm_pos_ff.weight", 256);
     MAT3("local_transformer.layers.0.pos_ff.proj.conv.weight", 1024, 256, 1);
     MAT3("local_transformer.layers.0.pos_ff.o_net.conv.weight", 256, 1024, 1);
-    for (int c = 0; c < 8; ++c) {
-        snprintf(nm, sizeof nm, "local_transformer_out_projections.%d.weight", c); MAT(nm, 2024, 256);
-        snprintf(nm, sizeof nm, "local_transformer_out_projections.%d.bias", c); VEC(nm, 2024);
+    for (int c = 0; c < 8; ++c) {  // --lt-head-scale: wider logits, so greedy decisions are not near-ties
+        snprintf(nm, sizeof nm, "local_transformer_out_projections.%d.weight", c);
+        add(nm, 2, 2024, 256, 1, T_F32, I_NORMAL, S * g_lt_head_scale, 0);
+        snprintf(nm, sizeof nm, "local_transformer_out_projections.%d.bias", c);
+        add(nm, 1, 2024, 1, 1, T_F32, I_NORMAL, S, 0);
     }
     for (int i = 0; i < g_nt; ++i) {
         if (dtype == T_Q8_0 && should_q8(g_t[i].name) && nel(&g_t[i]) % 32 == 0) g_t[i].type = T_Q8_0;
@@ -353,7 +357,7 @@ static void plan_codec(void) {
 int main(int argc, char **argv) {
     if (argc < 3) {
         fprintf(stderr, "usage: %s magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|f16] "
-                        "[--dec-layers N] [--enc-layers N] [--dec-pos P]\n", argv[0]);
+                        "[--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V] [--lt-head-scale K]\n", argv[0]);
         return 2;
     }
     const char *kind = argv[1], *out = argv[2];
@@ -365,6 +369,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--enc-layers")) enc_layers = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--dec-pos")) dec_pos = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--eos-bias")) g_eos_bias = (float)atof(argv[i + 1]);
+        else if (!strcmp(argv[i], "--lt-head-scale")) g_lt_head_scale = (float)atof(argv[i + 1]);
         else { fprintf(stderr, "unknown option %s\n", argv[i]); return 2; }
     }
     if (!strcmp(kind, "magpie")) plan_magpie(dtype, dec_layers, enc_layers, dec_pos);

@@ -27,15 +27,20 @@ def _gguf(name, kind="magpie", **kw):
     return ma.synth_gguf(os.path.join(CACHE, name), kind=kind, **kw)
 
 
+# Parity models use decisive LT heads (magpie_amd.DECISIVE): >= 98 % of greedy
+# decisions have an oracle top-1/top-2 gap above 1e-2, so code identity is a real
+# test, not a run of near-ties.
 @pytest.fixture(scope="session")
 def small_model():
     """2 decoder layers / 1 encoder layer: same kernels, fast oracle."""
-    return _gguf("magpie_small_l2e1.gguf", dec_layers=2, enc_layers=1)
+    import magpie_amd as ma
+    return _gguf("magpie_small_l2e1_k32.gguf", dec_layers=2, enc_layers=1, lt_head_scale=ma.DECISIVE)
 
 
 @pytest.fixture(scope="session")
 def full_model():
-    return _gguf("magpie_357m_f32.gguf")
+    import magpie_amd as ma
+    return _gguf("magpie_357m_f32_k32.gguf", lt_head_scale=ma.DECISIVE)
 
 
 @pytest.fixture(scope="session")
@@ -52,13 +57,15 @@ def eos_model():
 
 @pytest.fixture(scope="session")
 def q8_model():
-    return _gguf("magpie_small_q8.gguf", dtype="q8_0", dec_layers=2, enc_layers=1)
+    import magpie_amd as ma
+    return _gguf("magpie_small_q8_k32.gguf", dtype="q8_0", dec_layers=2, enc_layers=1, lt_head_scale=ma.DECISIVE)
 
 
 @pytest.fixture(scope="session")
 def q8_full_model():
     """Magpie-357M shapes, the reference converter's default Q8_0 patterns."""
-    return _gguf("magpie_357m_q8.gguf", dtype="q8_0")
+    import magpie_amd as ma
+    return _gguf("magpie_357m_q8_k32.gguf", dtype="q8_0", lt_head_scale=ma.DECISIVE)
 
 
 @pytest.fixture(scope="session")

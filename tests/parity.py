@@ -11,16 +11,25 @@ import numpy as np
 TIE_EPS = 2e-4  # logit units; GPU f32 vs oracle f64 logit error is ~1e-6
 
 
-def compare_codes(gpu_codes, orc_codes, orc_margins, tie_eps=TIE_EPS):
+def compare_codes(gpu_codes, orc_codes, orc_margins, tie_eps=TIE_EPS, min_frames=None):
+    """Returns {"identical", "frames" (frames compared before the first difference),
+    "decisions"}. min_frames: the comparison must cover at least that many frames
+    (None: every frame the oracle produced), so a near-tie in an early frame cannot
+    make a test pass vacuously."""
     g = np.asarray(gpu_codes)
     o = np.asarray(orc_codes)
     n = min(len(g), len(o))
+    need = len(o) if min_frames is None else min_frames
     diff = np.argwhere(g[:n] != o[:n])
     if len(diff) == 0:
         assert len(g) == len(o), f"frame counts differ: gpu {len(g)} vs oracle {len(o)}"
-        return {"identical": True, "frames": n}
+        print(f"codes identical over {n} frames ({n * 8} decisions)")
+        assert n >= need, f"only {n} frames compared, {need} required"
+        return {"identical": True, "frames": n, "decisions": n * 8}
     f, cb = diff[0]
     margin = float(orc_margins[f, cb])
     assert margin < tie_eps, (f"codes differ at frame {f} cb {cb}: gpu {g[f].tolist()} oracle {o[f].tolist()} "
                               f"with oracle margin {margin:.3g} >= {tie_eps}")
-    return {"identical": False, "frames": int(f), "tie_margin": margin}
+    print(f"codes identical over {f} frames, then a near-tie at frame {f} cb {cb} (margin {margin:.3g})")
+    assert f >= need, f"near-tie at frame {f}: only {f} frames compared, {need} required"
+    return {"identical": False, "frames": int(f), "decisions": int(f) * 8 + int(cb), "tie_margin": margin}

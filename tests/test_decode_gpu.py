@@ -54,6 +54,28 @@ def test_full_model_codes_and_hidden(ma, oracle, full_model):
     assert r.n_frames[0] == 24
 
 
+def test_small_model_matches_committed_golden(ma, small_model):
+    """GPU codes vs the committed oracle fixture (tests/golden/small_model_codes.json,
+    tests/golden/make_golden.py), independent of a live oracle run: every frame
+    identical, hidden states (first 8 elements, L1 norm) within the f32 bar."""
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "small_model_codes.json")))
+    dev = ma.Device(small_model)
+    for case in gold["cases"]:
+        r = dev.synthesize([case["tokens"]], speakers=[case["speaker"]], max_dec_steps=case["max_steps"],
+                           trace=True)
+        n = case["n_frames"]
+        assert r.n_frames[0] == n
+        np.testing.assert_array_equal(r.codes[0], np.asarray(case["codes"], np.int32).reshape(-1, 8))
+        h = r.hidden[0, :n + 1]
+        assert np.abs(h[:, :8] - np.asarray(case["hidden_first8"])).max() < HIDDEN_TOL
+        l1 = np.abs(h).sum(axis=1)
+        assert np.abs(l1 - np.asarray(case["hidden_l1"])).max() < HIDDEN_TOL * 768
+        print(f"golden case (T={len(case['tokens'])}, speaker {case['speaker']}): {n} frames identical")
+    dev.close()
+
+
 def test_eos_stops_like_reference(ma, oracle, eos_model):
     """EOS is forbidden for the first 4 frames (magpie.cpp:4267,4325); the EOS
     frame itself is not emitted (4349-4352)."""
@@ -232,16 +254,15 @@ def _run_both_b16(ma, oracle, model_path, tokens, steps, speaker=0, ignore_eos=F
 def test_bf16_small_model_matches_oracle(ma, oracle, small_model):
     tok = ma.synthetic_tokens(24, seed=1000)
     r, o = _run_both_b16(ma, oracle, small_model, tok, steps=40, speaker=1)
-    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=BF16_TIE_EPS)
+    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=BF16_TIE_EPS, min_frames=32)
     n = res["frames"]
     _check_hidden_b16(r.hidden[0, :n + 1], o["hidden"][:n + 1])
-    assert n >= 10, f"diverged after {n} frames"
 
 
 def test_bf16_full_model_matches_oracle(ma, oracle, full_model):
     tok = ma.synthetic_tokens(64, seed=1000)
     r, o = _run_both_b16(ma, oracle, full_model, tok, steps=24, ignore_eos=True)
-    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=BF16_TIE_EPS)
+    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=BF16_TIE_EPS, min_frames=20)
     n = res["frames"]
     _check_hidden_b16(r.hidden[0, :n + 1], o["hidden"][:n + 1])
     assert r.n_frames[0] == 24
@@ -304,19 +325,17 @@ def _check_hidden_q8(h_gpu, h_orc):
 def test_q8_small_model_matches_oracle(ma, oracle, q8_model):
     tok = ma.synthetic_tokens(24, seed=1000)
     r, o = _run_both_q8(ma, oracle, q8_model, tok, steps=40, speaker=1)
-    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=Q8_TIE_EPS)
+    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=Q8_TIE_EPS, min_frames=32)
     n = res["frames"]
     _check_hidden_q8(r.hidden[0, :n + 1], o["hidden"][:n + 1])
     # the oracle itself moves ~3e-3 between f64 and f32 accumulation in this mode
-    # (quantisation flips), and synthetic-weight decisions have ~1e-3 margins, so
-    # trajectories part at the first near-tie after a few frames
-    assert n >= 3, f"diverged after {n} frames"
+    # (quantisation flips); with decisive heads the codes still agree for >= 32 frames
 
 
 def test_q8_full_model_matches_oracle(ma, oracle, q8_full_model):
     tok = ma.synthetic_tokens(64, seed=1000)
     r, o = _run_both_q8(ma, oracle, q8_full_model, tok, steps=24, ignore_eos=True)
-    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=Q8_TIE_EPS)
+    res = compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=Q8_TIE_EPS, min_frames=20)
     n = res["frames"]
     _check_hidden_q8(r.hidden[0, :n + 1], o["hidden"][:n + 1])
     assert r.n_frames[0] == 24
@@ -357,7 +376,7 @@ def test_q8_sampling_matches_oracle(ma, oracle, q8_model):
     om.set_weight_mode(2)
     o = om.synthesize(toks[0], speaker=0, max_steps=24, trace=False, temperature=0.7, top_k=80, seed=77, stream=0)
     om.close()
-    compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=Q8_TIE_EPS)
+    compare_codes(r.codes[0], o["codes"], o["margins"], tie_eps=Q8_TIE_EPS, min_frames=20)
 
 
 def test_q8_mode_needs_q8_file(ma, small_model):

@@ -53,3 +53,34 @@ def test_gloo_world_size_2():
     assert res[0][1] == list(range(32)) and res[1][1] == list(range(32, 64))
     assert res[0][2] == res[1][2] == 2.0
     assert res[0][3] == res[1][3] == 64.0
+
+
+def test_bench_gpus_2_spawns_two_ranks():
+    """`bench.py --gpus 2` (what the driver runs for N=2 when it does not wrap it in
+    torchrun itself) starts two ranks over 127.0.0.1 and selects configs[3]'s
+    per-GPU shape (bf16, 8 utterances)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == [0, 1]
+    for x in lines:
+        assert x["world"] == 2 and x["ranks_seen"] == [0, 1]
+        assert x["weights"] == "bf16" and x["batch_per_gpu"] == 8
+
+
+def test_bench_rejects_mismatched_world():
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr

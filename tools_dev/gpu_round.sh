@@ -10,7 +10,7 @@ OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ "${2:-}" != "skip-tests" ]; then
-  timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread \
     > "$OUT/${TAG}_gpu_tests.log" 2>&1
   echo "gpu tests ok"
 fi

@@ -631,9 +631,12 @@ int orc_sample_top_k(const float *logits, int n, float temperature, int top_k, f
 // incrementally over positions (causal => identical to the reference's
 // per-codebook recompute). temperature < 0.01 => argmax (1263-1264).
 // *argeos is set when any codebook's argmax is EOS (the loop's EOS test, 4340-4346).
+// force (nullable): teacher forcing; codes[] still receives this oracle's own
+// decisions (and margins[] their margins), but codebook cb+1 is conditioned on
+// force[cb] (the trajectory under test), so every decision can be checked.
 static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, float temperature, int top_k,
                       uint64_t seed, int stream, int step, int32_t *codes, float *margins, int *argeos,
-                      int32_t *argmax) {
+                      int32_t *argmax, const int32_t *force) {
     const int D = m->lt_dim, F = m->lt_ffn, V = m->vocab_cb, d = m->d;
     float s[9][256], X[256], h[256], qkv[768], kk[8][256], vv[8][256], a[256], Y[256], f[1024], y2[256];
     float *logits = malloc(sizeof(float) * (size_t)V);
@@ -674,7 +677,8 @@ static void lt_sample(const orc_model *m, const float *hidden, int forbid_eos, f
         codes[cb] = code;
         if (margins) margins[cb] = mg;
         if (cb < 7) {
-            const float *e = m->audio_emb[cb] + (size_t)code * d;  // no 1/8 here (1284-1291)
+            const int next = force ? force[cb] : code;
+            const float *e = m->audio_emb[cb] + (size_t)next * d;  // no 1/8 here (1284-1291)
             mm(m, m->lt_in_w, m->lt_in_b, e, s[cb + 1], 1, D, d);
         }
     }
@@ -690,13 +694,13 @@ int orc_synthesize(orc_model *m, const int32_t *tokens, int T, int speaker, int 
 int orc_lt_sample(orc_model *m, const float *hidden, float temperature, int top_k, int forbid_eos, uint64_t seed,
                   int stream, int step, int32_t *sampled, int32_t *argmax, float *margins) {
     if (!m || !hidden || !sampled || (temperature >= 0.01f && top_k < 1)) return -1;
-    lt_sample(m, hidden, forbid_eos, temperature, top_k, seed, stream, step, sampled, margins, NULL, argmax);
+    lt_sample(m, hidden, forbid_eos, temperature, top_k, seed, stream, step, sampled, margins, NULL, argmax, NULL);
     return 0;
 }
 
-int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, int max_steps, int ignore_eos,
-                      float temperature, int top_k, uint64_t seed, int stream, int emit_eos, int32_t *codes_out,
-                      float *margins_out, float *hidden_out, double *timing_out) {
+static int synthesize(orc_model *m, const int32_t *tokens, int T, int speaker, int max_steps, int ignore_eos,
+                      float temperature, int top_k, uint64_t seed, int stream, int emit_eos, const int32_t *force,
+                      int32_t *codes_out, float *margins_out, float *hidden_out, double *timing_out) {
     if (temperature >= 0.01f && top_k < 1) return -1;
     if (!m || !tokens || T <= 0 || speaker < 0 || speaker >= m->n_spk) return -1;
     if (max_steps <= 0) max_steps = m->max_dec_steps;
@@ -747,9 +751,21 @@ int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, i
         int32_t codes[8];
         const int forbid = ignore_eos || step < 4;  // min_generated_frames (4267,4325)
         int eos = 0;
+        const int32_t *fc = force ? force + (size_t)step * 8 : NULL;
         lt_sample(m, hid, forbid, temperature, top_k, seed, stream, step, codes,
-                  margins_out ? margins_out + (size_t)step * 8 : NULL, &eos, NULL);
+                  margins_out ? margins_out + (size_t)step * 8 : NULL, &eos, NULL, fc);
         for (int c = 0; c < 8; ++c) if (codes[c] == m->audio_eos) eos = 1;
+        if (fc) {  // forced: the trajectory under test decides what comes next
+            memcpy(codes_out + (size_t)step * 8, codes, sizeof codes);
+            n_frames = step + 1;
+            if (step + 1 >= max_steps) break;
+            frame_embed(m, fc, pos, x);
+            for (int l = 0; l < L; ++l) decoder_layer(m, &s, l, x, 1, pos);
+            layernorm(x, m->dec_norm_out, hid, d, m->eps);
+            if (hidden_out) memcpy(hidden_out + (size_t)(step + 1) * d, hid, sizeof hid);
+            pos++;
+            continue;
+        }
         if (eos) {
             // the streaming loop emits the EOS frame too (magpie.cpp:4800-4806)
             if (emit_eos) { memcpy(codes_out + (size_t)step * 8, codes, sizeof codes); n_frames = step + 1; }
@@ -768,6 +784,21 @@ int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, i
     if (timing_out) { timing_out[0] = t1 - t0; timing_out[1] = t2 - t1; }
     free(enc); free(s.xa_k); free(s.xa_v); free(s.kc); free(s.vc);
     return n_frames;
+}
+
+int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int T, int speaker, int max_steps, int ignore_eos,
+                      float temperature, int top_k, uint64_t seed, int stream, int emit_eos, int32_t *codes_out,
+                      float *margins_out, float *hidden_out, double *timing_out) {
+    return synthesize(m, tokens, T, speaker, max_steps, ignore_eos, temperature, top_k, seed, stream, emit_eos, NULL,
+                      codes_out, margins_out, hidden_out, timing_out);
+}
+
+int orc_synthesize_forced(orc_model *m, const int32_t *tokens, int T, int speaker, int n_frames, int ignore_eos,
+                          float temperature, int top_k, uint64_t seed, int stream, const int32_t *forced,
+                          int32_t *codes_out, float *margins_out, float *hidden_out) {
+    if (!forced || n_frames <= 0) return -1;
+    return synthesize(m, tokens, T, speaker, n_frames, ignore_eos, temperature, top_k, seed, stream, 0, forced,
+                      codes_out, margins_out, hidden_out, NULL);
 }
 
 // ------------------------------------------------------------------ codec

@@ -61,6 +61,15 @@ int orc_synthesize_ex(orc_model *m, const int32_t *tokens, int n_tokens, int spe
                       int ignore_eos, float temperature, int top_k, uint64_t seed, int stream, int emit_eos,
                       int32_t *codes_out, float *margins_out, float *hidden_out, double *timing_out);
 
+// Teacher-forced run of the same loop for exactly n_frames frames: at every
+// codebook decision the oracle records ITS OWN pick (codes_out) and margin, then
+// continues with forced[step][cb] (the codes of the run under test, [n_frames][8]),
+// so every decision of a GPU run is checked against the oracle, not only those
+// before the first near-tie. EOS does not stop the loop (the forced run decides).
+int orc_synthesize_forced(orc_model *m, const int32_t *tokens, int n_tokens, int speaker_id, int n_frames,
+                          int ignore_eos, float temperature, int top_k, uint64_t seed, int stream,
+                          const int32_t *forced, int32_t *codes_out, float *margins_out, float *hidden_out);
+
 // magpie_local_transformer_sample_all (magpie.cpp:1113-1317) for one hidden[768]:
 // sampled[8], argmax[8] (nullable), margins[8] (nullable).
 int orc_lt_sample(orc_model *m, const float *hidden, float temperature, int top_k, int forbid_eos, uint64_t seed,

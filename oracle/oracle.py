@@ -37,6 +37,7 @@ def lib() -> ctypes.CDLL:
         L.orc_synthesize.argtypes = [P, P, I, I, I, I, P, P, P, P]
         L.orc_synthesize_ex.argtypes = [P, P, I, I, I, I, ctypes.c_float, I, ctypes.c_uint64, I, I, P, P, P, P]
         L.orc_encode.argtypes = [P, P, I, P]
+        L.orc_synthesize_forced.argtypes = [P, P, I, I, I, I, ctypes.c_float, I, ctypes.c_uint64, I, P, P, P, P]
         L.orc_set_weight_mode.argtypes = [P, I]
         L.orc_lt_sample.argtypes = [P, P, ctypes.c_float, I, I, ctypes.c_uint64, I, I, P, P, P]
         L.orc_draw_u.restype = ctypes.c_float
@@ -103,6 +104,24 @@ class Model:
             raise RuntimeError(f"oracle synthesize failed ({n})")
         return {"n_frames": n, "codes": codes[:n], "margins": marg[:max(n + 1, 0)],
                 "hidden": hid, "preamble_ms": tim[0], "decode_ms": tim[1]}
+
+    def synthesize_forced(self, tokens, forced, speaker=0, ignore_eos=True, temperature=0.0, top_k=80, seed=0,
+                          stream=0):
+        """Teacher-forced oracle run along `forced` ([n][8], the codes under test):
+        the oracle's own decision and margin at every codebook of every frame, and the
+        hidden state along the forced trajectory ([n+1][768], BOS first)."""
+        tok = np.ascontiguousarray(tokens, np.int32)
+        fc = np.ascontiguousarray(forced, np.int32).reshape(-1, 8)
+        n = len(fc)
+        codes = np.zeros((n, 8), np.int32)
+        marg = np.zeros((n, 8), np.float32)
+        hid = np.zeros((n + 1, 768), np.float32)
+        r = lib().orc_synthesize_forced(self.h, tok.ctypes.data, len(tok), speaker, n, int(ignore_eos),
+                                        float(temperature), int(top_k), int(seed) & (2**64 - 1), int(stream),
+                                        fc.ctypes.data, codes.ctypes.data, marg.ctypes.data, hid.ctypes.data)
+        if r != n:
+            raise RuntimeError(f"oracle forced synthesize failed ({r})")
+        return {"codes": codes, "margins": marg, "hidden": hid}
 
     def lt_sample(self, hidden, temperature=0.0, top_k=80, forbid_eos=False, seed=0, stream=-1, step=4):
         """magpie_local_transformer_sample_all restated: (sampled[8], argmax[8], margins[8])."""

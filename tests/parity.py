@@ -33,3 +33,23 @@ def compare_codes(gpu_codes, orc_codes, orc_margins, tie_eps=TIE_EPS, min_frames
     print(f"codes identical over {f} frames, then a near-tie at frame {f} cb {cb} (margin {margin:.3g})")
     assert f >= need, f"near-tie at frame {f}: only {f} frames compared, {need} required"
     return {"identical": False, "frames": int(f), "decisions": int(f) * 8 + int(cb), "tie_margin": margin}
+
+
+def compare_forced(gpu_codes, forced_orc, tie_eps=TIE_EPS, max_ties=None):
+    """Every decision of a GPU run against a teacher-forced oracle run along the GPU's
+    own codes (oracle.Model.synthesize_forced): a decision may differ only where the
+    oracle's margin is below tie_eps (a genuine near-tie). max_ties bounds how many
+    such decisions are tolerated (None: no bound beyond the margin rule)."""
+    g = np.asarray(gpu_codes).reshape(-1, 8)
+    o = np.asarray(forced_orc["codes"])
+    m = np.asarray(forced_orc["margins"])
+    assert g.shape == o.shape, f"{g.shape} vs {o.shape}"
+    diff = np.argwhere(g != o)
+    for f, cb in diff:
+        assert m[f, cb] < tie_eps, (f"frame {f} cb {cb}: gpu {g[f, cb]} oracle {o[f, cb]} "
+                                    f"with oracle margin {m[f, cb]:.3g} >= {tie_eps}")
+    if max_ties is not None:
+        assert len(diff) <= max_ties, f"{len(diff)} near-tie decisions, at most {max_ties} expected"
+    print(f"teacher-forced: {g.size} decisions checked over {len(g)} frames, {len(diff)} near-tie differences"
+          f" (margins {[round(float(m[f, c]), 5) for f, c in diff[:4]]})")
+    return {"decisions": int(g.size), "differences": int(len(diff))}

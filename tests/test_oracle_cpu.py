@@ -264,3 +264,21 @@ def test_oracle_q8_mode(oracle, q8_model, small_model):
     with pytest.raises(RuntimeError):
         m.set_weight_mode(2)  # F32 file: nothing to run as Q8_0
     m.close()
+
+
+def test_teacher_forced_run_reproduces_free_run(oracle, small_model):
+    """Forced along its own codes, the oracle reproduces its free run exactly (codes,
+    margins, hidden); forced along other codes it follows them."""
+    import magpie_amd as ma
+    tok = ma.synthetic_tokens(16, seed=21)
+    m = oracle.Model(small_model)
+    r = m.synthesize(tok, speaker=2, max_steps=12, ignore_eos=True, trace=True)
+    f = m.synthesize_forced(tok, r["codes"], speaker=2, ignore_eos=True)
+    np.testing.assert_array_equal(f["codes"], r["codes"])
+    np.testing.assert_array_equal(f["margins"], r["margins"][:12])
+    np.testing.assert_array_equal(f["hidden"], r["hidden"])
+    other = (r["codes"] + 7) % 2016
+    g = m.synthesize_forced(tok, other, speaker=2, ignore_eos=True)
+    np.testing.assert_array_equal(g["hidden"][0], r["hidden"][0])   # BOS step precedes any code
+    assert np.abs(g["hidden"][2] - r["hidden"][2]).max() > 1e-3     # the frame embedding follows the forced codes
+    m.close()

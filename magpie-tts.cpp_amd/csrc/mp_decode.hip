@@ -358,6 +358,7 @@ static bool gemv_args_ok(const GemvP &p) {
     if constexpr (EPI == EPI_LTX_ADD) ok &= p.out && p.ptab && p.lt_pos && p.cb >= 1;
     if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
+    if constexpr (EPI == EPI_LTKVO) ok &= p.lk && p.lv && p.N == 2 * LTD;
     return ok;
 }
 
@@ -561,8 +562,148 @@ hipError_t op_lt_merge(const LtFfnP &p, int NB, hipStream_t s) {
     }
     return hipGetLastError();
 }
+// ---------------------------------------------------------------- LT, f32 mode
+// One wave computes slot b's LT residual row y at position cb (LtFfn2P): cb = 0:
+// y = X_0 + vo_0; cb >= 1: codebook cb-1's pick (wave_pick_v, the same draw as
+// every other path), the q|k|vo gathers of that code's table rows, the causal
+// softmax over positions 0..cb and y = X_cb + sum_j p_j vo_j. Lane l returns
+// elements 4l..4l+3. `wb0`: this is workgroup 0, which publishes the code and the
+// position's k / vo rows for the later codebooks. One body for every batch size
+// (one wave per slot), so a batch reproduces its utterances run alone.
+__device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, float *wsc) {
+    const int lane = threadIdx.x & 63, cb = p.cb;
+    const size_t row = (size_t)b * NCB * LTD + 4 * lane;
+    if (cb == 0) {
+        const float4 x = *(const float4 *)(p.ltX + (size_t)b * LTD + 4 * lane), v = *(const float4 *)(p.ltv + row);
+        return make_float4(x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w);
+    }
+    float4 kr[NCB - 1], vr[NCB - 1];  // earlier positions' k / vo, in flight during the pick
+#pragma unroll
+    for (int j = 0; j < NCB - 1; ++j)
+        if (j < cb) { kr[j] = *(const float4 *)(p.ltk + row + j * LTD); vr[j] = *(const float4 *)(p.ltv + row + j * LTD); }
+    float lv[PICK_R];
+    load_logits(p.logits + (size_t)b * VCB, lv);
+    const int stp = ld_fresh_u(p.step + b);
+    int amax;
+    const int code = wave_pick_v(lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, cb - 1, wsc,
+                                 amax);
+    const size_t r = (size_t)(cb - 1) * VCB + code;
+    const float *qkv = p.qkvtab + r * (3 * LTD) + 4 * lane;
+    const float4 q4 = *(const float4 *)qkv, k4 = *(const float4 *)(qkv + LTD);
+    const float4 vo4 = *(const float4 *)(p.votab + r * LTD + 4 * lane);
+    const float4 x4 = *(const float4 *)(p.ptab + r * LTD + 4 * lane);
+    const float4 pos4 = *(const float4 *)(p.lt_pos + (size_t)cb * LTD + 4 * lane);
+    if (wb0) {
+        if (lane == 0) {
+            p.codes_cur[b * NCB + cb - 1] = code;
+            if (amax == p.audio_eos) p.smp.argeos[b] = 1;
+            if (p.smp.amax) p.smp.amax[b * NCB + cb - 1] = amax;
+        }
+        *(float4 *)(p.ltk + row + cb * LTD) = k4;
+        *(float4 *)(p.ltv + row + cb * LTD) = vo4;
+    }
+    float sj[NCB];
+#pragma unroll
+    for (int j = 0; j < NCB; ++j)
+        sj[j] = j < cb ? wave_sum(dotv(q4, kr[j < NCB - 1 ? j : 0])) * (1.0f / 16.0f)
+                       : j == cb ? wave_sum(dotv(q4, k4)) * (1.0f / 16.0f) : -INFINITY;
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) m = fmaxf(m, sj[j]);
+    float l = 0.f;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+        if (j > cb) break;
+        const float e = expf(sj[j] - m);
+        l += e;
+        const float4 v4 = j == cb ? vo4 : vr[j < NCB - 1 ? j : 0];
+        a.x = fmaf(e, v4.x, a.x); a.y = fmaf(e, v4.y, a.y); a.z = fmaf(e, v4.z, a.z); a.w = fmaf(e, v4.w, a.w);
+    }
+    return make_float4(x4.x + pos4.x + a.x / l, x4.y + pos4.y + a.y / l, x4.z + pos4.z + a.z / l,
+                       x4.w + pos4.w + a.w / l);
+}
+
+// The LT step of codebook cb in f32 mode, one launch: y (lt_y_slot, every workgroup
+// for itself; workgroup 0 stores it as the head's residual), then LN + FFN up +
+// GELU + FFN down partial sums exactly as lt_ffn_kernel (workgroup p owns hidden
+// units [16p, 16p+16)).
+template <int NB>
+__global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
+    constexpr int U = LTF / LT_FFN_P, UPW = U / MP_NWAVES;
+    static_assert(U % MP_NWAVES == 0 && U % 4 == 0 && LTD == MP_BLOCK, "unit split");
+    __shared__ __attribute__((aligned(16))) float xs[NB][LTD];
+    __shared__ __attribute__((aligned(16))) float fs[NB][U];
+    __shared__ __attribute__((aligned(16))) float wsc_all[MP_NWAVES][2 * VCB];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = blockIdx.x * U;
+    float4 a1[UPW], a2[U / 4];
+#pragma unroll
+    for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
+#pragma unroll
+    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.f.w2 + (size_t)tid * LTF + j0 + 4 * i);
+    for (int b = w; b < NB; b += MP_NWAVES) {
+        const float4 y = lt_y_slot(p, b, blockIdx.x == 0, wsc_all[w]);
+        if (blockIdx.x == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
+        const float x[4] = {y.x, y.y, y.z, y.w};
+        float mean, var;
+        wave_meanvar<4>(x, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.f.eps);
+        const float4 g = *(const float4 *)(p.f.lnw + 4 * lane);
+        *(float4 *)&xs[b][4 * lane] = make_float4(((x[0] - mean) * rstd) * g.x, ((x[1] - mean) * rstd) * g.y,
+                                                  ((x[2] - mean) * rstd) * g.z, ((x[3] - mean) * rstd) * g.w);
+    }
+    lds_sync();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const float4 xv = *(const float4 *)&xs[b][4 * lane];
+#pragma unroll
+        for (int r = 0; r < UPW; ++r) {
+            const float v = wave_sum(dotv(a1[r], xv));
+            if (lane == 0) fs[b][w * UPW + r] = gelu_tanh(v);
+        }
+    }
+    lds_sync();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < U / 4; ++i) {
+            const float4 f4 = *(const float4 *)&fs[b][4 * i];
+            acc = fmaf(a2[i].x, f4.x, acc);
+            acc = fmaf(a2[i].y, f4.y, acc);
+            acc = fmaf(a2[i].z, f4.z, acc);
+            acc = fmaf(a2[i].w, f4.w, acc);
+        }
+        p.f.part[((size_t)b * LT_FFN_P + blockIdx.x) * LTD + tid] = acc;
+    }
+}
+hipError_t op_lt_ffn2(const LtFfn2P &p, int NB, hipStream_t s) {
+    if (!p.f.y || !p.f.lnw || !p.f.w1 || !p.f.w2 || !p.f.part || !p.ltX || !p.ltk || !p.ltv || !p.qkvtab ||
+        !p.votab || !p.ptab || !p.lt_pos || !p.logits || !p.codes_cur || !p.step || !p.smp.cfg || !p.smp.argeos ||
+        p.cb < 0 || p.cb >= NCB)
+        return hipErrorInvalidValue;
+    switch (NB) {
+    case 1: hipLaunchKernelGGL(lt_ffn2_kernel<1>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(lt_ffn2_kernel<2>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(lt_ffn2_kernel<4>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 8: hipLaunchKernelGGL(lt_ffn2_kernel<8>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // the LT head at batch 1 with the FFN merge as its prologue
 hipError_t op_lt_em_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 2, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
+// f32 LT position 0: LN(X_0) -> [k_0 | vo_0] (W = [W_k ; W_o W_v], 512 x 256)
+hipError_t op_lt_kvo(const GemvP &p, int NB, hipStream_t s) {
+    switch (NB) {
+    case 1: return launch_gemv<1, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
+    case 2: return launch_gemv<2, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
+    case 4: return launch_gemv<4, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
+    case 8: return launch_gemv<8, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
+    }
+    return hipErrorInvalidValue;
+}
 
 hipError_t op_finalize(const FinP &p, int B, hipStream_t s) {
     if (!p.smp.cfg || !p.smp.argeos) return hipErrorInvalidValue;

@@ -38,15 +38,22 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
                                   const Sampling &smp, int stream, int step, int cb, float *scratch, int &amax) {
     const int lane = threadIdx.x & 63;
     constexpr int R = PICK_R;
+    // masked first-max argmax: the wave's max by DPP, then the first index holding it
+    // (ballots in index order: r-major, lane-minor = ascending i)
     float bv = -INFINITY;
-    int bi = 0x7fffffff;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int i = lane + 64 * r;
         if (i >= VCB || (i >= audio_bos && i <= audio_bos + 7 && (i != audio_eos || forbid_eos))) lv[r] = -INFINITY;
-        argmax_merge(bv, bi, lv[r], i);
+        bv = fmaxf(bv, lv[r]);
     }
-    wave_argmax(bv, bi);
+    bv = wave_max(bv);
+    int bi = VCB;
+#pragma unroll
+    for (int r = R - 1; r >= 0; --r) {
+        const unsigned long long bal = __ballot(lv[r] == bv);
+        if (bal) bi = 64 * r + __builtin_ctzll(bal);
+    }
     if (bi < 0 || bi >= VCB) bi = 0;
     amax = bi;
     if (!smp.on) return bi;
@@ -583,6 +590,9 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b,
         if (n < D) p.out[(size_t)b * D + n] = v;
         else if (n < 2 * D) p.kc[slot + n - D] = v;
         else p.vc[slot + n - 2 * D] = v;
+    } else if constexpr (EPI == EPI_LTKVO) {
+        if (n < LTD) p.lk[(size_t)b * NCB * LTD + n] = v;
+        else p.lv[(size_t)b * NCB * LTD + n - LTD] = v;
     } else if constexpr (EPI == EPI_LTQKV) {
         if (n < LTD) p.lq[(size_t)b * LTD + n] = v;
         else if (n < 2 * LTD) p.lk[((size_t)b * NCB + p.cb) * LTD + n - LTD] = v;

@@ -56,6 +56,7 @@ enum Epi {
     EPI_ADD_STORE = 6,  // out = v + addsrc
     EPI_GELU_B16 = 7,   // out_b16 = bf16(gelu(v)): the bf16 FFN-down operand, rounded once here
     EPI_LTX_ADD = 8,    // out = v + (P[cb-1][code] + lt_pos[cb]): LT residual of PRO_LTARG_ATTN's code
+    EPI_LTKVO = 9,      // f32 LT position 0: rows [0,256) k_0 -> lk[b][0], rows [256,512) vo_0 -> lv[b][0]
 };
 
 // Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
@@ -85,6 +86,28 @@ struct LtFfnP {
     float eps;
     float *part;         // [B][LT_FFN_P][256]
     float *out;          // lt_merge_kernel: [B][256] = ltY + merged FFN down
+};
+
+// f32 weight mode: the LT's attention + o_net + residual folded into the FFN launch
+// (lt_ffn2_kernel). Position j's o_net contribution is W_o v_j: for j >= 1 a
+// load-time table row VO[j-1][code] = W_o V[j-1][code] (V = the v third of the q|k|v
+// table), for j = 0 the per-frame vo_0 = (W_o W_v) LN(X_0) (lt_a's epilogue), so
+// y = X_c + sum_j softmax_j(q_c k_j / 16) vo_j  (= X_c + o_net(attn), magpie.cpp:946-966,
+// reassociated; o_net is linear).
+struct LtFfn2P {
+    LtFfnP f;             // y = ltY (written by block 0), FFN weights, partials
+    int cb;
+    const float *ltX;     // [B][256] X_0 (cb 0)
+    float *ltk, *ltv;     // [B][8][256] k_j and vo_j rows of the frame's positions
+    const float *qkvtab;  // [7][2024][768] q|k|v of codebook c's code at position c+1
+    const float *votab;   // [7][2024][256] W_o v of the same rows
+    const float *ptab;    // [8][2024][256] in_proj(audio_emb) + b
+    const float *lt_pos;
+    const float *logits;  // [B][2024] codebook cb-1's logits
+    int *codes_cur;       // [B][8]
+    const int *step;
+    int ignore_eos, audio_bos, audio_eos;
+    Sampling smp;
 };
 
 // Frame embedding of every slot (layer 0's residual input, magpie.cpp:2746-2787,

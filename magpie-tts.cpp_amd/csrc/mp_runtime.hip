@@ -76,6 +76,8 @@ hipError_t q8_lt_bo_8(const GemvP &, hipStream_t);
 hipError_t op_lt_em_1(const GemvP &, hipStream_t);
 hipError_t op_lt_ffn(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
+hipError_t op_lt_ffn2(const LtFfn2P &, int, hipStream_t);
+hipError_t op_lt_kvo(const GemvP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_xa_q8(const XaQ8P &, int, hipStream_t);
@@ -132,6 +134,9 @@ struct Model {
         *lt_out_b;
     float *lt_ptab = nullptr;  // [8][2024][256] = in_proj(audio_emb[c][v]) + b, built at load
     float *lt_qkvtab = nullptr;  // [7][2024][768] = qkv_net(LN(ptab[c][v] + lt_pos[c+1])), built at load
+    // f32 weight mode (lt_ffn2_kernel): [7][2024][256] = o_net(v third of lt_qkvtab), and
+    // [512][256] = [W_k ; W_o W_v] for position 0 (W_o W_v formed in double on the host)
+    float *lt_votab = nullptr, *lt_kvo = nullptr;
     std::vector<float *> xq_t;  // per layer W_q^T [768][128] (for K' = K W_q)
     // weight mode MP_WEIGHTS_BF16: decode projections repacked as bf16 MFMA fragments
     int weight_mode = 0;
@@ -147,7 +152,8 @@ struct Model {
     size_t arena_bytes = 0;
 };
 
-enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9 };
+enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9,
+              K_LTFFN2 = 10, K_LTKVO = 11 };
 struct OpRec {
     std::string name;
     int kind;
@@ -158,6 +164,7 @@ struct OpRec {
     XaP x;
     XaQ8P xq;
     LtFfnP lf;
+    LtFfn2P l2;
     EmbP e;
     int B;
     double bytes;
@@ -461,6 +468,36 @@ int load_model(mp_dev *dev, const char *path) {
     return MP_OK;
 }
 
+// f32 mode's LT (lt_ffn2_kernel) needs o_net applied to v rows ahead of time:
+// VO[c][v] = W_o V[c][v] for every table row, and [W_k ; W_o W_v] for position 0.
+bool f32_lt_mode(const mp::Model &m) { return m.weight_mode == MP_WEIGHTS_AS_STORED; }
+
+int build_vo_tables(mp_dev *dev) {
+    mp::Model &m = dev->m;
+    if (m.lt_votab) { hipFree(m.lt_votab); m.lt_votab = nullptr; }
+    if (m.lt_kvo) { hipFree(m.lt_kvo); m.lt_kvo = nullptr; }
+    const size_t R = (size_t)7 * 2024;
+    HIPCHK(hipMalloc(&m.lt_votab, R * 256 * 4));
+    mp::GemmP gp{};
+    gp.A = m.lt_qkvtab + 512; gp.lda = 768; gp.W = m.lt_o; gp.C = m.lt_votab; gp.ldc = 256;
+    gp.M = (int)R; gp.N = 256; gp.K = 256; gp.rows_per_utt = (int)R;
+    HIPCHK(mp::pre_gemm(gp, mp::GE_STORE, dev->stream));
+    std::vector<float> qkv((size_t)768 * 256), o((size_t)256 * 256), kvo((size_t)512 * 256);
+    HIPCHK(hipMemcpy(qkv.data(), m.lt_qkv, qkv.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(o.data(), m.lt_o, o.size() * 4, hipMemcpyDeviceToHost));
+    memcpy(kvo.data(), qkv.data() + (size_t)256 * 256, (size_t)256 * 256 * 4);  // W_k rows
+    for (int n = 0; n < 256; ++n)
+        for (int k = 0; k < 256; ++k) {
+            double acc = 0.0;
+            for (int j = 0; j < 256; ++j) acc += (double)o[(size_t)n * 256 + j] * qkv[(size_t)(512 + j) * 256 + k];
+            kvo[(size_t)(256 + n) * 256 + k] = (float)acc;
+        }
+    HIPCHK(hipMalloc(&m.lt_kvo, kvo.size() * 4));
+    HIPCHK(hipMemcpy(m.lt_kvo, kvo.data(), kvo.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    return MP_OK;
+}
+
 // P[c][v] = in_proj(audio_emb[c][v]) + b: the LT's per-codebook re-embedding
 // (magpie.cpp:1274-1313) depends only on (c, v) -> one GEMM at load time (with
 // ggml's Q8_0 arithmetic when in_proj is a Q8_0 tensor in Q8 mode).
@@ -496,7 +533,7 @@ int build_ptab(mp_dev *dev, int weight_mode) {
     if (wq) hipFree(wq);
     HIPCHK(ge);
     HIPCHK(se);
-    return MP_OK;
+    return f32_lt_mode(m) ? build_vo_tables(dev) : MP_OK;
 }
 
 // Weight mode MP_WEIGHTS_Q8: upload every Q8_0 tensor the decode path uses as
@@ -848,6 +885,58 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                 return rc;
         }
     }
+    if (f32_lt_mode(m)) {
+        // f32 mode: LN + [k_0 | vo_0] for position 0, then per codebook ONE launch for
+        // pick + attention + o_net + residual + FFN (lt_ffn2_kernel) and the head
+        mp::GemvP g = base(); g.cb = 0;
+        g.W = m.lt_kvo; g.N = 512; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX; g.lnw = m.lt_norm_self;
+        g.lk = io.ltk; g.lv = io.ltv;
+        if (ops) {
+            mp::OpRec r{};
+            r.name = "lt_kvo"; r.kind = mp::K_LTKVO; r.g = g; r.B = NB;
+            r.bytes = A * (512.0 * 256) + A * act * (256 * 4);
+            ops->push_back(r);
+        }
+        HIPCHK(mp::op_lt_kvo(g, NB, s));
+        dump_lt(io, s);
+        for (int cb = 0; cb < 8; ++cb) {
+            mp::LtFfn2P l2{};
+            l2.f = mp::LtFfnP{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2, m.eps, io.ltp, io.lty2};
+            l2.cb = cb; l2.ltX = io.ltX; l2.ltk = io.ltk; l2.ltv = io.ltv; l2.qkvtab = m.lt_qkvtab;
+            l2.votab = m.lt_votab; l2.ptab = m.lt_ptab; l2.lt_pos = m.lt_pos; l2.logits = io.logits;
+            l2.codes_cur = io.codes_cur; l2.step = io.step; l2.ignore_eos = io.ignore_eos;
+            l2.audio_bos = m.audio_bos; l2.audio_eos = m.audio_eos;
+            l2.smp = mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax};
+            if (ops) {
+                mp::OpRec r{};
+                r.name = "lt_ffn2"; r.kind = mp::K_LTFFN2; r.l2 = l2; r.B = NB;
+                r.bytes = A * (1024.0 * 256 * 2) + A * act * (cb ? 2024 + 4 * 256 + 2 * 256 * cb : 512) +
+                          A * act * (mp::LT_FFN_P * 256 + 256);
+                ops->push_back(r);
+            }
+            HIPCHK(mp::op_lt_ffn2(l2, NB, s));
+            dump_lt(io, s);
+            if (NB > 1) {
+                if (ops) {
+                    mp::OpRec r{};
+                    r.name = "lt_merge"; r.kind = mp::K_LTMERGE; r.lf = l2.f; r.B = NB;
+                    r.bytes = A * act * (mp::LT_FFN_P * 256 + 512);
+                    ops->push_back(r);
+                }
+                HIPCHK(mp::op_lt_merge(l2.f, NB, s));
+            }
+            g = base(); g.cb = cb;
+            g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024; g.bias = m.lt_out_b + (size_t)cb * 2024;
+            g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
+            mp::GemvFn efn = tb.lt_e;
+            if (NB == 1) {  // the FFN merge is the head's prologue
+                g.part = io.ltp; g.addsrc = io.ltY;
+                efn = mp::op_lt_em_1;
+            }
+            if ((rc = run("lt_e", efn, g, A * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
+                return rc;
+        }
+    } else
     for (int cb = 0; cb < 8; ++cb) {
         mp::GemvP g;
         if (cb == 0) {
@@ -1144,6 +1233,8 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.arena) hipFree(dev->m.arena);
     if (dev->m.lt_ptab) hipFree(dev->m.lt_ptab);
     if (dev->m.lt_qkvtab) hipFree(dev->m.lt_qkvtab);
+    if (dev->m.lt_votab) hipFree(dev->m.lt_votab);
+    if (dev->m.lt_kvo) hipFree(dev->m.lt_kvo);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
     if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
     for (void *p : dev->lt_allocs) hipFree(p);
@@ -1574,6 +1665,8 @@ int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
             case mp::K_LTFFN: e = mp::op_lt_ffn(r.lf, r.B, dev->stream); break;
             case mp::K_LTMERGE: e = mp::op_lt_merge(r.lf, r.B, dev->stream); break;
             case mp::K_LTPICK: e = mp::op_lt_pick(r.g, r.B, dev->stream); break;
+            case mp::K_LTFFN2: e = mp::op_lt_ffn2(r.l2, r.B, dev->stream); break;
+            case mp::K_LTKVO: e = mp::op_lt_kvo(r.g, r.B, dev->stream); break;
             case mp::K_EMBED: e = mp::op_embed(r.e, r.B, dev->stream); break;
             case mp::K_FIN: e = mp::op_finalize(r.f, r.B, dev->stream); break;
             }
@@ -1608,6 +1701,8 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
         if (r.kind == mp::K_LTFFN) return mp::op_lt_ffn(r.lf, r.B, dev->stream);
         if (r.kind == mp::K_LTMERGE) return mp::op_lt_merge(r.lf, r.B, dev->stream);
         if (r.kind == mp::K_LTPICK) return mp::op_lt_pick(r.g, r.B, dev->stream);
+        if (r.kind == mp::K_LTFFN2) return mp::op_lt_ffn2(r.l2, r.B, dev->stream);
+        if (r.kind == mp::K_LTKVO) return mp::op_lt_kvo(r.g, r.B, dev->stream);
         if (r.kind == mp::K_EMBED) return mp::op_embed(r.e, r.B, dev->stream);
         return hipErrorInvalidValue;
     };

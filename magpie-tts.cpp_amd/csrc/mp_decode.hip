@@ -100,7 +100,7 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     __shared__ __attribute__((aligned(16))) float wo[SA_WAVES][DH];
     const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
-    const int L = ld_fresh_u(p.pos + b) + 1;
+    const int L = p.pos[b] + 1;
     const int chunk = (L + SA_SPLITS - 1) / SA_SPLITS;
     const int j0 = sp * chunk, j1 = min(L, j0 + chunk);
     float m = -INFINITY, l = 0.f;
@@ -173,40 +173,56 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
 // (m, l, o[768] in 12 registers per lane); the 8 wave states merge in LDS and
 // the split's state (m, l, unnormalised O[768]) is stored. The next op (FFN up,
 // PRO_XA_LN) merges the XA_SPLITS states, adds x and normalises.
-constexpr int XA_WAVES = 8, XA_THREADS = XA_WAVES * 64, XA_KPW = 2;  // keys in flight per wave
+#ifndef MP_XA_WAVES
+#define MP_XA_WAVES 4
+#define MP_XA_KPW 4
+#endif
+constexpr int XA_WAVES = MP_XA_WAVES, XA_THREADS = XA_WAVES * 64, XA_KPW = MP_XA_KPW;  // keys in flight per wave
+constexpr int XA_V = D / 256;  // float4 per lane per 768-row: lane owns elements 4 lane + 256 i + (0..3)
 __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
     __shared__ float wm[XA_WAVES], wl[XA_WAVES];
-    __shared__ float wo[XA_WAVES][D];
+    __shared__ __attribute__((aligned(16))) float wo[XA_WAVES][D];
     const int sp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int Tb = ld_fresh_u(p.T + b);
+    const int Tb = p.T[b];
     const int chunk = (Tb + XA_SPLITS - 1) / XA_SPLITS;
     const int t0 = sp * chunk, t1 = min(Tb, t0 + chunk);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
-    const float *Kp = p.kp + base, *Vp = p.vp + base;
-    float k[XA_KPW][D / 64], vv[XA_KPW][D / 64];
+    const float *Kp = p.kp + base + 4 * lane, *Vp = p.vp + base + 4 * lane;
+    float4 k[XA_KPW][XA_V], vv[XA_KPW][XA_V];
 #pragma unroll
     for (int u = 0; u < XA_KPW; ++u) {
         const int t = t0 + w + XA_WAVES * u;
-        const size_t r = (size_t)(t < t1 ? t : 0) * D + lane;
+        const size_t r = (size_t)(t < t1 ? t : 0) * D;
 #pragma unroll
-        for (int i = 0; i < D / 64; ++i) { k[u][i] = Kp[r + 64 * i]; vv[u][i] = Vp[r + 64 * i]; }
+        for (int i = 0; i < XA_V; ++i) {
+            k[u][i] = *(const float4 *)(Kp + r + 256 * i);
+            vv[u][i] = *(const float4 *)(Vp + r + 256 * i);
+        }
     }
-    asm volatile("" ::: "memory");  // keep these loads ahead of the x fetch
-    float h[D / 64];
-    {   // LN(x) (magpie.cpp:3513): lane owns elements lane + 64 i
-        float v[D / 64];
+    float4 h[XA_V];
+    {   // LN(x) (magpie.cpp:3513), every wave for itself (DPP statistics, no barrier)
+        float4 x4[XA_V], g4[XA_V];
 #pragma unroll
-        for (int i = 0; i < D / 64; ++i) v[i] = p.x[(size_t)b * D + lane + 64 * i];
+        for (int i = 0; i < XA_V; ++i) {
+            x4[i] = *(const float4 *)(p.x + (size_t)b * D + 4 * lane + 256 * i);
+            g4[i] = *(const float4 *)(p.lnw + 4 * lane + 256 * i);
+        }
+        float v[4 * XA_V];
+#pragma unroll
+        for (int i = 0; i < XA_V; ++i) { v[4 * i] = x4[i].x; v[4 * i + 1] = x4[i].y; v[4 * i + 2] = x4[i].z; v[4 * i + 3] = x4[i].w; }
         float mean, var;
-        wave_meanvar<D / 64>(v, mean, var);
+        wave_meanvar<4 * XA_V>(v, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
-        for (int i = 0; i < D / 64; ++i) h[i] = ((v[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+        for (int i = 0; i < XA_V; ++i)
+            h[i] = make_float4(((x4[i].x - mean) * rstd) * g4[i].x, ((x4[i].y - mean) * rstd) * g4[i].y,
+                               ((x4[i].z - mean) * rstd) * g4[i].z, ((x4[i].w - mean) * rstd) * g4[i].w);
     }
     const float scale = 1.0f / sqrtf((float)DXA);
-    float m = -INFINITY, l = 0.f, o[D / 64];
+    float m = -INFINITY, l = 0.f;
+    float4 o[XA_V];
 #pragma unroll
-    for (int i = 0; i < D / 64; ++i) o[i] = 0.f;
+    for (int i = 0; i < XA_V; ++i) o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int tb = t0 + w; tb < t1; tb += XA_WAVES * XA_KPW) {
 #pragma unroll
         for (int u = 0; u < XA_KPW; ++u) {
@@ -214,12 +230,15 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
             if (t >= t1) break;  // wave-uniform
             float acc = 0.f;
 #pragma unroll
-            for (int i = 0; i < D / 64; ++i) acc += k[u][i] * h[i];
+            for (int i = 0; i < XA_V; ++i) acc += dotv(k[u][i], h[i]);
             const float sv = wave_sum(acc) * scale;
             const float mn = fmaxf(m, sv), c = expf(m - mn), e = expf(sv - mn);
             l = l * c + e;
 #pragma unroll
-            for (int i = 0; i < D / 64; ++i) o[i] = o[i] * c + e * vv[u][i];
+            for (int i = 0; i < XA_V; ++i) {
+                o[i].x = o[i].x * c + e * vv[u][i].x; o[i].y = o[i].y * c + e * vv[u][i].y;
+                o[i].z = o[i].z * c + e * vv[u][i].z; o[i].w = o[i].w * c + e * vv[u][i].w;
+            }
             m = mn;
         }
         const int tn = tb + XA_WAVES * XA_KPW;
@@ -227,13 +246,16 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
 #pragma unroll
         for (int u = 0; u < XA_KPW; ++u) {  // next keys (long texts)
             const int t = tn + XA_WAVES * u;
-            const size_t r = (size_t)(t < t1 ? t : 0) * D + lane;
+            const size_t r = (size_t)(t < t1 ? t : 0) * D;
 #pragma unroll
-            for (int i = 0; i < D / 64; ++i) { k[u][i] = Kp[r + 64 * i]; vv[u][i] = Vp[r + 64 * i]; }
+            for (int i = 0; i < XA_V; ++i) {
+                k[u][i] = *(const float4 *)(Kp + r + 256 * i);
+                vv[u][i] = *(const float4 *)(Vp + r + 256 * i);
+            }
         }
     }
 #pragma unroll
-    for (int i = 0; i < D / 64; ++i) wo[w][lane + 64 * i] = o[i];
+    for (int i = 0; i < XA_V; ++i) *(float4 *)&wo[w][4 * lane + 256 * i] = o[i];
     if (lane == 0) { wm[w] = m; wl[w] = l; }
     lds_sync();
     float M = -INFINITY;
@@ -246,11 +268,14 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
         den += e[q] * wl[q];
     }
     float *pp = p.part + ((size_t)b * XA_SPLITS + sp) * XA_PART;
-    for (int kx = tid; kx < D; kx += XA_THREADS) {
-        float num = 0.f;
+    if (tid < D / 4) {
+        float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int q = 0; q < XA_WAVES; ++q) num += e[q] * wo[q][kx];
-        pp[4 + kx] = num;
+        for (int q = 0; q < XA_WAVES; ++q) {
+            const float4 v4 = *(const float4 *)&wo[q][4 * tid];
+            num.x += e[q] * v4.x; num.y += e[q] * v4.y; num.z += e[q] * v4.z; num.w += e[q] * v4.w;
+        }
+        *(float4 *)(pp + 4 + 4 * tid) = num;
     }
     if (tid == 0) { pp[0] = M; pp[1] = den; }
 }
@@ -266,52 +291,33 @@ hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
 // (magpie.cpp:4340-4358): stop on EOS in any codebook (frame not emitted), else
 // append the frame; stop at max_dec_steps; otherwise the frame becomes the next
 // decoder input and the position advances.
-__global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
+__global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
+    // one wave per slot: codebook 7's pick with the same wave_pick as every other
+    // codebook (masked first-max argmax; top-k draw when sampling)
     const int b = blockIdx.x, tid = threadIdx.x;
-    if (ld_fresh_u(p.done + b)) return;
-    __shared__ float red[8];
+    if (p.done[b]) return;
+    __shared__ float scratch[2 * VCB];
     int i0, amax;
-    if (p.smp.on) {  // one wave draws
-        __shared__ float scratch[2 * VCB];
-        if (tid >= 64) return;
-        const int stp = ld_fresh_u(p.step + b);
+    {
+        const int stp = p.step[b];
         i0 = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp,
                        NCB - 1, scratch, amax);
         if (tid != 0) return;
-    } else {
-        const float *lg = p.logits + (size_t)b * VCB;
-        const bool forbid_eos = p.ignore_eos || ld_fresh_u(p.step + b) < 4;
-        float bv = -INFINITY;
-        int bi = 0x7fffffff;
-        for (int i = tid; i < VCB; i += MP_BLOCK) {
-            float v = lg[i];
-            if (i >= p.audio_bos && i <= p.audio_bos + 7 && (i != p.audio_eos || forbid_eos)) v = -INFINITY;
-            argmax_merge(bv, bi, v, i);
-        }
-        wave_argmax(bv, bi);
-        if ((tid & 63) == 0) { red[tid >> 6] = bv; ((int *)red)[4 + (tid >> 6)] = bi; }
-        lds_sync();
-        if (tid != 0) return;
-        float v0 = red[0];
-        i0 = ((int *)red)[4];
-        for (int w = 1; w < MP_NWAVES; ++w) argmax_merge(v0, i0, red[w], ((int *)red)[4 + w]);
-        if (i0 < 0 || i0 >= VCB) i0 = 0;
-        amax = i0;
     }
     int *ccp = p.codes_cur + b * NCB;
     ccp[NCB - 1] = i0;
     int cc[NCB];
 #pragma unroll
-    for (int cb = 0; cb < NCB - 1; ++cb) cc[cb] = ld_fresh_u(ccp + cb);
+    for (int cb = 0; cb < NCB - 1; ++cb) cc[cb] = ccp[cb];
     cc[NCB - 1] = i0;
     if (p.smp.amax) p.smp.amax[b * NCB + NCB - 1] = amax;
     // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
     bool eos = amax == p.audio_eos;
-    eos |= ld_fresh_u(p.smp.argeos + b) != 0;
+    eos |= p.smp.argeos[b] != 0;
     p.smp.argeos[b] = 0;
     if (p.lt_only) return;  // magpie_local_transformer_sample_all: codes only
     for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
-    const int s = ld_fresh_u(p.step + b);
+    const int s = p.step[b];
     if (eos) {
         // graph_reuse drops the EOS frame (4349-4352); the streaming loop emits it (4800-4806)
         if (p.emit_eos)
@@ -330,7 +336,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_finalize_kernel(FinP p) {
         return;
     }
     for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
-    p.pos[b] = ld_fresh_u(p.pos + b) + 1;
+    p.pos[b] += 1;
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -426,7 +432,7 @@ __global__ __launch_bounds__(64) void lt_pick_kernel(GemvP p) {
     }
     float lv[PICK_R];
     load_logits(p.logits + (size_t)b * VCB, lv);
-    const int stp = ld_fresh_u(p.step + b);
+    const int stp = p.step[b];
     int amax;
     const int code = wave_pick_v(lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, p.cb - 1, wsc,
                                  amax);
@@ -465,8 +471,8 @@ __global__ __launch_bounds__(MP_BLOCK) void embed_kernel(EmbP p) {
     const int b = blockIdx.x;
     int c[NCB];
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) c[cb] = ld_fresh_u(p.codes + b * NCB + cb);
-    const int ps = ld_fresh_u(p.pos + b);
+    for (int cb = 0; cb < NCB; ++cb) c[cb] = p.codes[b * NCB + cb];
+    const int ps = p.pos[b];
     for (int k = threadIdx.x; k < D; k += MP_BLOCK) {
         float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
 #pragma unroll
@@ -583,7 +589,7 @@ __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, f
         if (j < cb) { kr[j] = *(const float4 *)(p.ltk + row + j * LTD); vr[j] = *(const float4 *)(p.ltv + row + j * LTD); }
     float lv[PICK_R];
     load_logits(p.logits + (size_t)b * VCB, lv);
-    const int stp = ld_fresh_u(p.step + b);
+    const int stp = p.step[b];
     int amax;
     const int code = wave_pick_v(lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, cb - 1, wsc,
                                  amax);
@@ -707,7 +713,7 @@ hipError_t op_lt_kvo(const GemvP &p, int NB, hipStream_t s) {
 
 hipError_t op_finalize(const FinP &p, int B, hipStream_t s) {
     if (!p.smp.cfg || !p.smp.argeos) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lt_finalize_kernel, dim3(B), dim3(MP_BLOCK), 0, s, p);
+    hipLaunchKernelGGL(lt_finalize_kernel, dim3(B), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
     __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
     __shared__ float wred[2 * MP_NWAVES];
     {
-        const int Tb = ld_fresh_u(p.T + b);
+        const int Tb = p.T[b];
         const int h = lane >> 5, d4 = 4 * (lane & 31);
         const float4 q4 = *(const float4 *)(p.q + (size_t)b * DXA + d4);
         const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;

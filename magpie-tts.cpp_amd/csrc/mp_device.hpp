@@ -75,30 +75,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Read of a value another launch of the same decode iteration wrote (positions,
-// steps, done flags, codes, split softmax states, the sampling config): always a
-// VECTOR load at agent scope (`global_load … sc1`, served by L2/MALL). A plain
-// load of a wave-uniform address is compiled to `s_load` through the scalar
-// cache, and inside a replayed hipGraph such reads were observed to return the
-// previous frame's value (a sampled batch of 16 drew with a stale step and left
-// its single-utterance runs; tests/test_decode_gpu.py::test_sampled_batch_equals_single),
-// so no mutable cross-launch datum goes through the scalar cache.
-template <class T>
-__device__ __forceinline__ T ld_fresh(const T *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// ld_fresh of a wave-uniform address, returned in an SGPR (readfirstlane) so the
-// compiler can use it in scalar address arithmetic and batch the loads it feeds
-__device__ __forceinline__ int ld_fresh_u(const int *p) { return __builtin_amdgcn_readfirstlane(ld_fresh(p)); }
-__device__ __forceinline__ float ld_fresh_u(const float *p) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ld_fresh(p))));
-}
-__device__ __forceinline__ unsigned long long ld_fresh_u(const unsigned long long *p) {
-    const unsigned long long v = ld_fresh(p);
-    return (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v) |
-           ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32)) << 32);
-}
-
 // Block-wide reduction for 256 threads; `red` is an LDS scratch of >= 4 floats.
 // Every thread returns the total. Contains two barriers.
 __device__ __forceinline__ float block_sum(float v, float *red) {

@@ -57,9 +57,9 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
     if (bi < 0 || bi >= VCB) bi = 0;
     amax = bi;
     if (!smp.on) return bi;
-    const float temp = ld_fresh_u(&smp.cfg->temperature);
+    const float temp = smp.cfg->temperature;
     const float M = bv;
-    const int k = min(max(ld_fresh_u(&smp.cfg->top_k), 1), VCB);
+    const int k = min(max(smp.cfg->top_k, 1), VCB);
     // order-preserving keys; padding lanes get 0 (below every real key)
     unsigned key[R];
 #pragma unroll
@@ -128,7 +128,7 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
     if (lane == 0) {
         float sum = 0.f;
         for (int i = 0; i < k; ++i) sum += sv[i];
-        const float u = mp_uniform(ld_fresh_u(&smp.cfg->seed), ld_fresh_u(&smp.cfg->stream_base) + stream, step, cb);
+        const float u = mp_uniform(smp.cfg->seed, smp.cfg->stream_base + stream, step, cb);
         float cum = 0.f;
         code = si[k - 1];
         for (int i = 0; i < k; ++i) {
@@ -223,8 +223,8 @@ __device__ __forceinline__ void merge_weights(const float *pp, int stride, int n
         float ms[NS], ls[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            ms[s] = ld_fresh(pp + ((size_t)q * NS + s) * stride);
-            ls[s] = ld_fresh(pp + ((size_t)q * NS + s) * stride + 1);
+            ms[s] = pp[((size_t)q * NS + s) * stride];
+            ls[s] = pp[((size_t)q * NS + s) * stride + 1];
         }
         float M = -INFINITY;
 #pragma unroll
@@ -380,7 +380,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             wave_meanvar<PER>(v, mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
             const bool st = p.hidden_out && blockIdx.x == 0;
-            const int s = (p.trace && blockIdx.x == 0) ? ld_fresh_u(p.step + b) : 0;
+            const int s = (p.trace && blockIdx.x == 0) ? p.step[b] : 0;
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int k = lane + 64 * i;
@@ -403,7 +403,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         wave_meanvar<PER>(v, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.eps);
         const bool st = p.hidden_out && blockIdx.x == 0;
-        const int s = (p.trace && blockIdx.x == 0) ? ld_fresh_u(p.step) : 0;
+        const int s = (p.trace && blockIdx.x == 0) ? p.step[0] : 0;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             if (i / Q != w) continue;
@@ -420,8 +420,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         for (int b = w; b < NB; b += MP_NWAVES) {
             int c[NCB];
 #pragma unroll
-            for (int cb = 0; cb < NCB; ++cb) c[cb] = ld_fresh_u(p.codes + b * NCB + cb);
-            const int ps = ld_fresh_u(p.pos + b);
+            for (int cb = 0; cb < NCB; ++cb) c[cb] = p.codes[b * NCB + cb];
+            const int ps = p.pos[b];
             float x[K / 64];
 #pragma unroll
             for (int i = 0; i < K / 64; ++i) {
@@ -448,8 +448,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         constexpr int PER = K / 64, Q = PER / MP_NWAVES;
         int c[NCB];
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) c[cb] = ld_fresh_u(p.codes + cb);
-        const int ps = ld_fresh_u(p.pos);
+        for (int cb = 0; cb < NCB; ++cb) c[cb] = p.codes[cb];
+        const int ps = p.pos[0];
         float x[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -512,7 +512,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         }
         int stp[SPW];  // every owned slot's step up front, not one dependent load per pick
 #pragma unroll
-        for (int j = 0; j < SPW; ++j) stp[j] = w + MP_NWAVES * j < NB ? ld_fresh_u(p.step + w + MP_NWAVES * j) : 0;
+        for (int j = 0; j < SPW; ++j) stp[j] = w + MP_NWAVES * j < NB ? p.step[w + MP_NWAVES * j] : 0;
         unsigned long long codes = 0ull;  // 16 bits per owned slot (codes < 2048)
 #pragma unroll
         for (int j = 0; j < SPW; ++j) {
@@ -586,7 +586,7 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b,
     else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
     else if constexpr (EPI == EPI_LTX_ADD) p.out[(size_t)b * p.out_ld + n] = v + extra;  // extra = X[b][n]
     else if constexpr (EPI == EPI_QKV) {
-        const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + ld_fresh(p.pos + b)) * D;
+        const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + p.pos[b]) * D;
         if (n < D) p.out[(size_t)b * D + n] = v;
         else if (n < 2 * D) p.kc[slot + n - D] = v;
         else p.vc[slot + n - 2 * D] = v;

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void row_xa_kernel(RowXaP p) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int m = blockIdx.x * 4 + w;
     if (m >= p.M) return;
-    const int b = m / p.rows_per_utt, Tb = ld_fresh_u(p.T + b);
+    const int b = m / p.rows_per_utt, Tb = p.T[b];
     const float *q = p.Q + (size_t)m * DXA;
     const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
     const float *Vb = p.xav + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
@@ -302,8 +302,8 @@ __global__ __launch_bounds__(256) void row_xa_kernel(RowXaP p) {
 __global__ void embed_text_kernel(const int *tok, const int *T, int Tmax, const float *text_emb,
                                   const float *enc_pos, float *X) {
     const int m = blockIdx.x, b = m / Tmax, t = m % Tmax;
-    const bool valid = t < ld_fresh_u(T + b);
-    const int id = valid ? ld_fresh_u(tok + m) : 0;
+    const bool valid = t < T[b];
+    const int id = valid ? tok[m] : 0;
     for (int k = threadIdx.x; k < D; k += blockDim.x)
         X[(size_t)m * D + k] = valid ? text_emb[(size_t)id * D + k] + enc_pos[(size_t)t * D + k] : 0.f;
 }
@@ -311,7 +311,7 @@ __global__ void embed_text_kernel(const int *tok, const int *T, int Tmax, const 
 // x[b][t] = baked_context[spk_b][t] + dec_pos[t] for the 110 context frames (4138-4189).
 __global__ void embed_context_kernel(const int *spk, const float *baked, const float *dec_pos, float *X) {
     const int m = blockIdx.x, b = m / CTX, t = m % CTX;
-    const float *src = baked + (size_t)ld_fresh_u(spk + b) * CTX * D + (size_t)t * D;
+    const float *src = baked + (size_t)spk[b] * CTX * D + (size_t)t * D;
     for (int k = threadIdx.x; k < D; k += blockDim.x) X[(size_t)m * D + k] = src[k] + dec_pos[(size_t)t * D + k];
 }
 

@@ -192,8 +192,9 @@ def main() -> None:
             dist.destroy_process_group()
         else:
             seen = [rank]
-        print(json.dumps({"rank": rank, "local_rank": local, "world": world, "ranks_seen": seen,
-                          "weights": args.weights, "batch_per_gpu": args.batch}), flush=True)
+        # one write(2) per line: the ranks share the launcher's stdout pipe
+        os.write(1, (json.dumps({"rank": rank, "local_rank": local, "world": world, "ranks_seen": seen,
+                                 "weights": args.weights, "batch_per_gpu": args.batch}) + "\n").encode())
         return
     # one rank per GPU; with fewer GPUs than ranks (a rehearsal) ranks share devices
     ndev = ma.device_count()
@@ -286,25 +287,37 @@ def main() -> None:
                  "frac": round(tfs / MFMA_F16_PEAK_TFS, 4), "audio_peak": round(float(np.abs(audio).max()), 4)}
 
     # ---- roofline of the dominant kernel, timed in situ: whole decode iterations
-    # with every kernel launched on the decode stream between a hipEvent pair, so
-    # each op sees the caches a real frame leaves it (mp_hip_profile_ops). The
-    # batch is first decoded to mid-utterance (cache length L = 110 + frames/2 + 1,
-    # the mean over the decode), so length-dependent kernels (attention) run at
-    # the average length of the timed decode.
+    # launched eagerly on the decode stream, each kernel through hipExtLaunchKernel
+    # with a start/stop event pair that the dispatch itself stamps
+    # (mp_hip_profile_ops_kev): the interval rocprofv3's kernel trace reports, in
+    # the cache state a real frame leaves each op. The batch is first decoded to
+    # mid-utterance (cache length L = 110 + frames/2 + 1, the mean over the decode),
+    # so length-dependent kernels (attention) run at the average length of the
+    # timed decode. Also recorded per op: the first-wave-start to last-wave-end span
+    # from in-kernel timestamps (wave_span_us, mp_hip_profile_ops_ts) and a plain
+    # event pair around the launch (event_pair_us, mp_hip_profile_ops).
     roofline = None
     op_table = {}
     if rank == 0:
         dev.synthesize(toks, speakers=speakers, max_dec_steps=args.frames // 2, ignore_eos=True)
         names = dev.ops()
+        kev = dev.profile_ops_kev(iters=args.profile_ops)
+        tsu = dev.profile_ops_ts(iters=args.profile_ops)
         us = dev.profile_ops(iters=args.profile_ops)
         groups = {}
         for i, n in enumerate(names):
             groups.setdefault(n, []).append(i)
         for n, idxs in groups.items():
-            avg = float(np.mean([us[i] for i in idxs]))
-            rec = {"launches_per_frame": len(idxs), "avg_us": round(avg, 3), "us_per_frame": round(avg * len(idxs), 2)}
+            dur = float(np.mean([kev[i] for i in idxs]))
+            own = [tsu[i] for i in idxs if tsu[i] > 0]
+            rec = {"launches_per_frame": len(idxs), "avg_us": round(dur, 3),
+                   "wave_span_us": round(float(np.mean(own)), 3) if own else None,
+                   "event_pair_us": round(float(np.mean([us[i] for i in idxs])), 3),
+                   "us_per_frame": round(dur * len(idxs), 2)}
             if n != "finalize":
                 rec["bytes"] = dev.op_bytes(idxs[0])
+                # back to back (one event pair around 50 launches; weights warm in L2/MALL)
+                rec["b2b_us"] = round(dev.time_op(idxs[0], reps=50), 3)
             op_table[n] = rec
         dom = max(((n, r) for n, r in op_table.items() if "bytes" in r), key=lambda kv: kv[1]["us_per_frame"])
         name, rec = dom
@@ -312,18 +325,21 @@ def main() -> None:
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "algorithmic_bytes_per_launch": rec["bytes"], "avg_launch_us": rec["avg_us"],
-                    "timing": "in-situ hipEvent pair per launch (mp_hip_profile_ops)"}
+                    "timing": "dispatch begin/end stamped on the kernel's own start/stop events "
+                              "(hipExtLaunchKernel; the rocprofv3 kernel-trace interval), whole eager "
+                              "iterations at the mid-utterance state (mp_hip_profile_ops_kev)"}
         # HBM bytes per launch from the committed PMC passes (tools_dev/pmc_traffic.sh +
-        # pmc_parse.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE x2 on gfx950)
+        # pmc_parse.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE correction)
         pmc_path = os.path.join(REPO, "profiles", PMC_TRAFFIC)
         if args.weights == "f32" and B == 1 and os.path.exists(pmc_path):
-            pmc = json.load(open(pmc_path))["ops"].get(name)
+            pmc_ops = json.load(open(pmc_path))["ops"]
+            pmc = pmc_ops.get(name)
             if pmc:
                 roofline["traffic"] = pmc["traffic_bytes"]
                 roofline["traffic_source"] = f"profiles/{PMC_TRAFFIC} ({pmc['kernel']})"
-                for n, r in op_table.items():
-                    if n in json.load(open(pmc_path))["ops"]:
-                        r["pmc_traffic_bytes"] = json.load(open(pmc_path))["ops"][n]["traffic_bytes"]
+            for n, r in op_table.items():
+                if n in pmc_ops:
+                    r["pmc_traffic_bytes"] = pmc_ops[n]["traffic_bytes"]
 
     # ---- CPU baseline: the oracle (C restatement, f32 accumulation) on the host cores
     cpu = None

@@ -155,6 +155,19 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us);
  * (mp_hip_num_ops entries). Continues from the batch's current state; after
  * every utterance is done the iteration recomputes the same frame. */
 int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us);
+/* mp_hip_profile_ops plus, per op, the time of an EMPTY event pair recorded right
+ * after it (pair_us, nullable): avg_us - pair_us estimates the launch's own
+ * duration without the event-pair overhead. */
+int mp_hip_profile_ops_ex(mp_dev *dev, int iters, float *avg_us, float *pair_us);
+/* Per-op duration from in-kernel timestamps (first wave start to last wave end
+ * after its stores, s_memrealtime), eager launches of whole iterations with no
+ * event in the stream: the launch's own time in the decode's cache state. -1 for
+ * an op whose kernel records no timestamps. */
+int mp_hip_profile_ops_ts(mp_dev *dev, int iters, float *avg_us);
+/* Per-op duration from the kernel dispatch's own begin/end timestamps
+ * (hipExtLaunchKernel start/stop events: the interval rocprofv3's kernel trace
+ * reports), eager launches of whole iterations in the decode's cache state. */
+int mp_hip_profile_ops_kev(mp_dev *dev, int iters, float *avg_us);
 
 /* --- text front end (host) ---------------------------------------------------- */
 /* magpie_tokenizer_init + magpie_tokenize (magpie.cpp:124-495): vocabulary and

@@ -27,6 +27,7 @@ namespace mp {
 // wave-instruction; activations come from LDS with conflict-free ds_read_b128.
 template <int NB, int RW, int K, int PRO, int EPI>
 __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
+    const unsigned long long t_start = ts_begin(p.ts);
     // No early exit on the done counter: a dependent load there would sit in
     // front of the weight stream of every launch. Once every slot is done the
     // iteration recomputes identical values (codes_prev / pos are frozen) and
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     // The weight rows do not depend on the prologue: issue the whole stream first
     // so the HBM latency overlaps the prologue's own dependent loads/reductions.
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int row0 = (blockIdx.x * MP_NWAVES + w) * RW;
+    const int row0 = (blockIdx.x * MP_NWAVES + w) * RW + ts_dep(t_start);
     VT wv[RW][NV];
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
@@ -79,6 +80,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     const int b = lane % NB, n = row0 + lane / NB;
     if (n >= p.N) return;
     epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
+    ts_end(p.ts, t_start);
 }
 
 // ---------------------------------------------------------------- SA decode attention
@@ -93,13 +95,14 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 // ~L/4 keys each instead of one workgroup streaming a whole head.
 constexpr int SA_WAVES = 8, SA_THREADS = SA_WAVES * 64, SA_IF = 4;  // iterations in flight
 __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
+    const unsigned long long t_start = ts_begin(p.ts);
     const int h = blockIdx.x, sp = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kk = lane >> 4, dc = lane & 15;
     __shared__ float wm[SA_WAVES], wl[SA_WAVES];
     __shared__ __attribute__((aligned(16))) float wo[SA_WAVES][DH];
     const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
-    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc;
+    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc + ts_dep(t_start);
     const int L = p.pos[b] + 1;
     const int chunk = (L + SA_SPLITS - 1) / SA_SPLITS;
     const int j0 = sp * chunk, j1 = min(L, j0 + chunk);
@@ -161,6 +164,7 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     float *pp = p.part + ((size_t)(b * NH + h) * SA_SPLITS + sp) * SA_PART;
     pp[4 + tid] = num;  // relative to M (an empty split stores M = -inf, l = 0, O = 0)
     if (tid == 0) { pp[0] = M; pp[1] = den; }
+    ts_end(p.ts, t_start);
 }
 
 // ---------------------------------------------------------------- fused XA
@@ -180,6 +184,7 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
 constexpr int XA_WAVES = MP_XA_WAVES, XA_THREADS = XA_WAVES * 64, XA_KPW = MP_XA_KPW;  // keys in flight per wave
 constexpr int XA_V = D / 256;  // float4 per lane per 768-row: lane owns elements 4 lane + 256 i + (0..3)
 __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
+    const unsigned long long t_start = ts_begin(p.ts);
     __shared__ float wm[XA_WAVES], wl[XA_WAVES];
     __shared__ __attribute__((aligned(16))) float wo[XA_WAVES][D];
     const int sp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
     const int chunk = (Tb + XA_SPLITS - 1) / XA_SPLITS;
     const int t0 = sp * chunk, t1 = min(Tb, t0 + chunk);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
-    const float *Kp = p.kp + base + 4 * lane, *Vp = p.vp + base + 4 * lane;
+    const float *Kp = p.kp + base + 4 * lane + ts_dep(t_start), *Vp = p.vp + base + 4 * lane;
     float4 k[XA_KPW][XA_V], vv[XA_KPW][XA_V];
 #pragma unroll
     for (int u = 0; u < XA_KPW; ++u) {
@@ -278,11 +283,12 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
         *(float4 *)(pp + 4 + 4 * tid) = num;
     }
     if (tid == 0) { pp[0] = M; pp[1] = den; }
+    ts_end(p.ts, t_start);
 }
 
 hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
     if (!p.x || !p.part || !p.lnw || !p.kp || !p.vp || !p.T || p.Tmax < 1 || p.Tmax > TMAX_LIMIT) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(xa_part_kernel, dim3(XA_SPLITS, B), dim3(XA_THREADS), 0, s, p);
+    mp::launch(xa_part_kernel, dim3(XA_SPLITS, B), dim3(XA_THREADS), 0, s, p);
     return hipGetLastError();
 }
 
@@ -292,6 +298,7 @@ hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
 // append the frame; stop at max_dec_steps; otherwise the frame becomes the next
 // decoder input and the position advances.
 __global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
+    const unsigned long long t_start = ts_begin(p.ts);
     // one wave per slot: codebook 7's pick with the same wave_pick as every other
     // codebook (masked first-max argmax; top-k draw when sampling)
     const int b = blockIdx.x, tid = threadIdx.x;
@@ -300,7 +307,7 @@ __global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
     int i0, amax;
     {
         const int stp = p.step[b];
-        i0 = wave_pick(p.logits + (size_t)b * VCB, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp,
+        i0 = wave_pick(p.logits + (size_t)b * VCB + ts_dep(t_start), p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp,
                        NCB - 1, scratch, amax);
         if (tid != 0) return;
     }
@@ -337,6 +344,7 @@ __global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
     }
     for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
     p.pos[b] += 1;
+    ts_end(p.ts, t_start);
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -373,7 +381,7 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
     if (!gemv_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
     const int rows_per_block = MP_NWAVES * RW;
     const int grid = (p.N + rows_per_block - 1) / rows_per_block;
-    hipLaunchKernelGGL((gemv_kernel<NB, RW, K, PRO, EPI>), dim3(grid), dim3(MP_BLOCK), 0, s, p);
+    mp::launch((gemv_kernel<NB, RW, K, PRO, EPI>), dim3(grid), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
@@ -409,7 +417,7 @@ hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
     if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || p.max_seq < 1 || p.max_seq > NCH_MAX * SA_CHUNK)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sa_attn_kernel, dim3(NH, SA_SPLITS, B), dim3(SA_THREADS), 0, s, p);
+    mp::launch(sa_attn_kernel, dim3(NH, SA_SPLITS, B), dim3(SA_THREADS), 0, s, p);
     return hipGetLastError();
 }
 
@@ -456,7 +464,7 @@ hipError_t op_lt_pick(const GemvP &p, int NB, hipStream_t s) {
     if (!p.logits || !p.codes_cur || !p.qkvtab || !p.ptab || !p.lt_pos || !p.ltk || !p.ltv || !p.lk || !p.lv ||
         !p.ltX || !p.out || !p.step || !p.smp.cfg || !p.smp.argeos || p.cb < 1)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lt_pick_kernel, dim3(NB), dim3(64), 0, s, p);
+    mp::launch(lt_pick_kernel, dim3(NB), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 // o_net + residual after lt_pick_kernel (its attention output in src, residual in addsrc)
@@ -482,7 +490,7 @@ __global__ __launch_bounds__(MP_BLOCK) void embed_kernel(EmbP p) {
 }
 hipError_t op_embed(const EmbP &p, int NB, hipStream_t s) {
     if (!p.emb || !p.codes || !p.pos_emb || !p.pos || !p.x) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(embed_kernel, dim3(NB), dim3(MP_BLOCK), 0, s, p);
+    mp::launch(embed_kernel, dim3(NB), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
@@ -549,10 +557,10 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_merge_kernel(LtFfnP p) {
 hipError_t op_lt_ffn(const LtFfnP &p, int NB, hipStream_t s) {
     if (!p.y || !p.lnw || !p.w1 || !p.w2 || !p.part) return hipErrorInvalidValue;
     switch (NB) {
-    case 1: hipLaunchKernelGGL(lt_ffn_kernel<1>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
-    case 2: hipLaunchKernelGGL(lt_ffn_kernel<2>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(lt_ffn_kernel<4>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
-    case 8: hipLaunchKernelGGL(lt_ffn_kernel<8>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 1: mp::launch(lt_ffn_kernel<1>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 2: mp::launch(lt_ffn_kernel<2>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 4: mp::launch(lt_ffn_kernel<4>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 8: mp::launch(lt_ffn_kernel<8>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -560,10 +568,10 @@ hipError_t op_lt_ffn(const LtFfnP &p, int NB, hipStream_t s) {
 hipError_t op_lt_merge(const LtFfnP &p, int NB, hipStream_t s) {
     if (!p.y || !p.part || !p.out) return hipErrorInvalidValue;
     switch (NB) {
-    case 1: hipLaunchKernelGGL(lt_merge_kernel<1>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
-    case 2: hipLaunchKernelGGL(lt_merge_kernel<2>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(lt_merge_kernel<4>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
-    case 8: hipLaunchKernelGGL(lt_merge_kernel<8>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 1: mp::launch(lt_merge_kernel<1>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 2: mp::launch(lt_merge_kernel<2>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 4: mp::launch(lt_merge_kernel<4>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 8: mp::launch(lt_merge_kernel<8>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -636,12 +644,13 @@ __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, f
 // units [16p, 16p+16)).
 template <int NB>
 __global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
+    const unsigned long long t_start = ts_begin(p.f.ts);
     constexpr int U = LTF / LT_FFN_P, UPW = U / MP_NWAVES;
     static_assert(U % MP_NWAVES == 0 && U % 4 == 0 && LTD == MP_BLOCK, "unit split");
     __shared__ __attribute__((aligned(16))) float xs[NB][LTD];
     __shared__ __attribute__((aligned(16))) float fs[NB][U];
     __shared__ __attribute__((aligned(16))) float wsc_all[MP_NWAVES][2 * VCB];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = blockIdx.x * U;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = blockIdx.x * U + ts_dep(t_start);
     float4 a1[UPW], a2[U / 4];
 #pragma unroll
     for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
@@ -682,6 +691,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
         }
         p.f.part[((size_t)b * LT_FFN_P + blockIdx.x) * LTD + tid] = acc;
     }
+    ts_end(p.f.ts, t_start);
 }
 hipError_t op_lt_ffn2(const LtFfn2P &p, int NB, hipStream_t s) {
     if (!p.f.y || !p.f.lnw || !p.f.w1 || !p.f.w2 || !p.f.part || !p.ltX || !p.ltk || !p.ltv || !p.qkvtab ||
@@ -689,10 +699,10 @@ hipError_t op_lt_ffn2(const LtFfn2P &p, int NB, hipStream_t s) {
         p.cb < 0 || p.cb >= NCB)
         return hipErrorInvalidValue;
     switch (NB) {
-    case 1: hipLaunchKernelGGL(lt_ffn2_kernel<1>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
-    case 2: hipLaunchKernelGGL(lt_ffn2_kernel<2>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(lt_ffn2_kernel<4>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
-    case 8: hipLaunchKernelGGL(lt_ffn2_kernel<8>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 1: mp::launch(lt_ffn2_kernel<1>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 2: mp::launch(lt_ffn2_kernel<2>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 4: mp::launch(lt_ffn2_kernel<4>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 8: mp::launch(lt_ffn2_kernel<8>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -713,7 +723,7 @@ hipError_t op_lt_kvo(const GemvP &p, int NB, hipStream_t s) {
 
 hipError_t op_finalize(const FinP &p, int B, hipStream_t s) {
     if (!p.smp.cfg || !p.smp.argeos) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lt_finalize_kernel, dim3(B), dim3(64), 0, s, p);
+    mp::launch(lt_finalize_kernel, dim3(B), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 

@@ -43,6 +43,7 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
 
 template <int NB, int K, int PRO, int EPI>
 __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
+    const unsigned long long t_start = ts_begin(p.ts);
     static_assert(NB >= 1 && NB <= 16, "one 16-column MFMA tile of utterances");
     static_assert(K % 128 == 0, "K splits into 4 waves x 32-wide chunks");
     constexpr int KC = K / 32, KW = KC / MP_NWAVES;
@@ -58,7 +59,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = blockIdx.x;
 
     // weight fragments of this wave's K slice, issued before the prologue
-    const uint4 *wf = (const uint4 *)p.Wb + ((size_t)rt * KC + w * KW) * 64 + lane;
+    const uint4 *wf = (const uint4 *)p.Wb + ((size_t)rt * KC + w * KW) * 64 + lane + ts_dep(t_start);
     uint4 a[KW];
 #pragma unroll
     for (int i = 0; i < KW; ++i) a[i] = wf[(size_t)i * 64];
@@ -148,6 +149,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const int n = rt * 16 + row;
     if (n >= p.N) return;
     epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
+    ts_end(p.ts, t_start);
 }
 
 template <int PRO, int EPI>
@@ -178,7 +180,7 @@ static bool b16_args_ok(const GemvP &p) {
 template <int NB, int K, int PRO, int EPI>
 static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     if (!b16_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_b16_kernel<NB, K, PRO, EPI>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
+    mp::launch((gemm_b16_kernel<NB, K, PRO, EPI>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
@@ -219,7 +221,7 @@ __global__ void pack_b16_kernel(const float *W, int N, int K, unsigned short *ou
 
 hipError_t pack_b16(const float *W, int N, int K, unsigned short *out, hipStream_t s) {
     if (!W || !out || N <= 0 || K % 32) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pack_b16_kernel, dim3(1024), dim3(256), 0, s, W, N, K, out);
+    mp::launch(pack_b16_kernel, dim3(1024), dim3(256), 0, s, W, N, K, out);
     return hipGetLastError();
 }
 

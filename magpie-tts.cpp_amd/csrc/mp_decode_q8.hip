@@ -236,7 +236,7 @@ hipError_t op_xa_q8(const XaQ8P &p, int B, hipStream_t s) {
     if (!p.x || !p.x2 || !p.q || !p.wo || !p.wod || !p.xak || !p.xav || !p.T || p.Tmax < 1 ||
         p.Tmax > TMAX_LIMIT)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(xa_q8_kernel, dim3(D / XQ8_ROWS, B), dim3(MP_BLOCK), 0, s, p);
+    mp::launch(xa_q8_kernel, dim3(D / XQ8_ROWS, B), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
@@ -268,7 +268,7 @@ template <int NB, int K, int R, int PRO, int EPI>
 static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     if (!q8_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
     const int rows = MP_NWAVES * R;
-    hipLaunchKernelGGL((gemv_q8_kernel<NB, K, R, PRO, EPI>), dim3((p.N + rows - 1) / rows), dim3(MP_BLOCK), 0, s, p);
+    mp::launch((gemv_q8_kernel<NB, K, R, PRO, EPI>), dim3((p.N + rows - 1) / rows), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 

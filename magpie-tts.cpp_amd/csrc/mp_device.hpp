@@ -4,9 +4,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <hip/hip_ext.h>
+
 #define MP_WAVE 64
 #define MP_BLOCK 256
 #define MP_NWAVES (MP_BLOCK / MP_WAVE)
+
+namespace mp {
+// Per-launch kernel timing (mp_hip_profile_ops_kev). While g_kev is set on the
+// launching thread, decode launches go through hipExtLaunchKernel with these
+// events, which then carry the dispatch's own begin/end timestamps: the interval
+// rocprofv3's kernel trace reports, measured live without the profiler.
+inline thread_local hipEvent_t g_kev[2] = {nullptr, nullptr};
+template <typename... A, typename... P>
+inline void launch(void (*k)(A...), dim3 grid, dim3 block, unsigned shm, hipStream_t s, P... args) {
+    if (g_kev[0]) hipExtLaunchKernelGGL(k, grid, block, shm, s, g_kev[0], g_kev[1], 0, args...);
+    else hipLaunchKernelGGL(k, grid, block, shm, s, args...);
+}
+}  // namespace mp
 
 // ---- wave64 reductions on DPP (data-parallel primitives move lanes inside the
 // VALU; no LDS round trip per step, unlike __shfl_xor's ds_bpermute).
@@ -73,6 +88,33 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Optional in-kernel timing for the bench's per-op table (ts != nullptr only in
+// mp_hip_profile_ops_ts): every wave records (its workgroup's start, its own end
+// after its stores completed) as one plain 16-byte store into its slot
+// ts[2 * (block * TS_WAVES + wave)]; the host takes min(start) .. max(end). No
+// atomics (no contention, and no store before the kernel's loads, so the compiler
+// keeps its scalar loads), s_memrealtime at 100 MHz.
+constexpr int TS_WAVES = 8, TS_BLOCKS = 1024;
+// The start stamp is a non-volatile asm (no modelled side effect: a volatile one or
+// the builtin would stop the compiler from turning the kernel's later uniform loads
+// into scalar loads); ts_dep(t) (always 0, opaque to the compiler) is added to the
+// kernel's first load address so the stamp stays at the start.
+__device__ __forceinline__ unsigned long long ts_begin(const unsigned long long *ts) {
+    unsigned long long t = 0;
+    if (ts) asm("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "s"(ts));
+    return t;
+}
+__device__ __forceinline__ int ts_dep(unsigned long long t) { return (int)(t >> 63); }
+__device__ __forceinline__ void ts_end(unsigned long long *ts, unsigned long long t0) {
+    if (ts) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const int blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if ((threadIdx.x & 63) == 0 && blk < TS_BLOCKS)
+            *(ulonglong2 *)(ts + 2 * ((size_t)blk * TS_WAVES + (threadIdx.x >> 6))) = make_ulonglong2(t0, t1);
+    }
 }
 
 // Block-wide reduction for 256 threads; `red` is an LDS scratch of >= 4 floats.

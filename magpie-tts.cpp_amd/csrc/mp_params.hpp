@@ -86,6 +86,7 @@ struct LtFfnP {
     float eps;
     float *part;         // [B][LT_FFN_P][256]
     float *out;          // lt_merge_kernel: [B][256] = ltY + merged FFN down
+    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 
 // f32 weight mode: the LT's attention + o_net + residual folded into the FFN launch
@@ -181,6 +182,7 @@ struct GemvP {
     const int *ndone;
     int nslots;
     const float *part;   // PRO_SA_MERGE: [B][NH][SA_SPLITS][SA_PART]; PRO_XA_LN: [B][XA_SPLITS][XA_PART]
+    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 
 struct FinP {
@@ -191,6 +193,7 @@ struct FinP {
     Sampling smp;
     int emit_eos;   // streaming semantics: the EOS frame's codes are emitted too (magpie.cpp:4800-4806)
     int lt_only;    // magpie_local_transformer_sample_all: pick codebook 7, no loop bookkeeping
+    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 
 // Fused cross-attention for one decode step (replaces the xq GEMV + XA attention
@@ -206,6 +209,7 @@ struct XaP {
     const float *kp, *vp;  // K', V': [B][L][Tmax][768]
     const int *T;
     int Tmax, layer, nlayers;
+    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 
 // Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the
@@ -229,6 +233,7 @@ struct AttnP {  // decode self-attention (one query per utterance)
     const int *pos;
     float *part;         // [B][NH][SA_SPLITS][SA_PART] partial softmax states over key splits
                          // (merged in the O-projection's PRO_SA_MERGE prologue)
+    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 
 }  // namespace mp

@@ -22,6 +22,7 @@
 
 #include "../../include/magpie_hip.h"
 #include "mp_gguf.hpp"
+#include "mp_device.hpp"
 #include "mp_params.hpp"
 
 namespace mp {
@@ -1642,37 +1643,130 @@ double mp_hip_op_bytes(mp_dev *dev, int op) {
     return r.bytes;
 }
 
-int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
+// one recorded op, launched on s (profiling and standalone timing)
+static hipError_t launch_rec(const mp::OpRec &r, hipStream_t s) {
+    switch (r.kind) {
+    case mp::K_GEMV: return r.fn(r.g, s);
+    case mp::K_ATTN: return mp::op_sa_attn(r.a, r.B, s);
+    case mp::K_XA: return mp::op_xa(r.x, r.B, s);
+    case mp::K_XAQ8: return mp::op_xa_q8(r.xq, r.B, s);
+    case mp::K_LTFFN: return mp::op_lt_ffn(r.lf, r.B, s);
+    case mp::K_LTMERGE: return mp::op_lt_merge(r.lf, r.B, s);
+    case mp::K_LTPICK: return mp::op_lt_pick(r.g, r.B, s);
+    case mp::K_LTFFN2: return mp::op_lt_ffn2(r.l2, r.B, s);
+    case mp::K_LTKVO: return mp::op_lt_kvo(r.g, r.B, s);
+    case mp::K_EMBED: return mp::op_embed(r.e, r.B, s);
+    case mp::K_FIN: return mp::op_finalize(r.f, r.B, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) { return mp_hip_profile_ops_ex(dev, iters, avg_us, nullptr); }
+
+int mp_hip_profile_ops_ex(mp_dev *dev, int iters, float *avg_us, float *pair_us) {
     if (!dev || !avg_us || iters < 1) return MP_ERR_ARG;
     if (!dev->batch_ready || dev->ops.empty())
         return fail(dev, MP_ERR_STATE, "mp_hip_profile_ops needs a decoded batch (mp_hip_decode first)");
+    HIPCHK(hipSetDevice(dev->device));
+    const int n = (int)dev->ops.size();
+    std::vector<hipEvent_t> ev(3 * (size_t)n);  // [before, after, after + an empty pair's second event]
+    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+    std::vector<double> sum(n, 0.0), psum(n, 0.0);
+    int rc = MP_OK;
+    for (int it = 0; it < iters && rc == MP_OK; ++it) {
+        for (int i = 0; i < n; ++i) {
+            const mp::OpRec &r = dev->ops[i];
+            HIPCHK(hipEventRecord(ev[3 * i], dev->stream));
+            const hipError_t e = launch_rec(r, dev->stream);
+            HIPCHK(e);
+            HIPCHK(hipEventRecord(ev[3 * i + 1], dev->stream));
+            if (pair_us) HIPCHK(hipEventRecord(ev[3 * i + 2], dev->stream));
+        }
+        HIPCHK(hipStreamSynchronize(dev->stream));
+        for (int i = 0; i < n; ++i) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, ev[3 * i], ev[3 * i + 1]));
+            sum[i] += ms;
+            if (pair_us) {
+                HIPCHK(hipEventElapsedTime(&ms, ev[3 * i + 1], ev[3 * i + 2]));
+                psum[i] += ms;
+            }
+        }
+    }
+    for (auto &e : ev) hipEventDestroy(e);
+    for (int i = 0; i < n; ++i) avg_us[i] = (float)(sum[i] * 1000.0 / iters);
+    if (pair_us)
+        for (int i = 0; i < n; ++i) pair_us[i] = (float)(psum[i] * 1000.0 / iters);
+    return rc;
+}
+
+int mp_hip_profile_ops_ts(mp_dev *dev, int iters, float *avg_us) {
+    if (!dev || !avg_us || iters < 1) return MP_ERR_ARG;
+    if (!dev->batch_ready || dev->ops.empty())
+        return fail(dev, MP_ERR_STATE, "mp_hip_profile_ops_ts needs a decoded batch (mp_hip_decode first)");
+    HIPCHK(hipSetDevice(dev->device));
+    const int n = (int)dev->ops.size();
+    const size_t per = (size_t)2 * TS_BLOCKS * TS_WAVES;  // u64 per op
+    unsigned long long *ts = nullptr;
+    HIPCHK(hipMalloc(&ts, (size_t)n * per * 8));
+    std::vector<unsigned long long> h((size_t)n * per);
+    std::vector<double> sum(n, 0.0);
+    std::vector<int> cnt(n, 0);
+    int rc = MP_OK;
+    for (int it = 0; it < iters && rc == MP_OK; ++it) {
+        HIPCHK(hipMemsetAsync(ts, 0, (size_t)n * per * 8, dev->stream));
+        for (int i = 0; i < n; ++i) {
+            mp::OpRec r = dev->ops[i];
+            unsigned long long *t = ts + (size_t)i * per;
+            r.g.ts = t; r.a.ts = t; r.x.ts = t; r.f.ts = t; r.lf.ts = t; r.l2.f.ts = t;
+            const hipError_t e = launch_rec(r, dev->stream);
+            if (e != hipSuccess) { rc = fail(dev, MP_ERR_HIP, std::string("profile launch: ") + hipGetErrorString(e)); break; }
+        }
+        if (rc != MP_OK) break;
+        HIPCHK(hipMemcpyAsync(h.data(), ts, (size_t)n * per * 8, hipMemcpyDeviceToHost, dev->stream));
+        HIPCHK(hipStreamSynchronize(dev->stream));
+        for (int i = 0; i < n; ++i) {
+            unsigned long long t0 = ~0ull, t1 = 0;
+            for (size_t k = 0; k < per / 2; ++k) {
+                const unsigned long long a = h[(size_t)i * per + 2 * k], b = h[(size_t)i * per + 2 * k + 1];
+                if (b == 0) continue;  // slot not written
+                t0 = std::min(t0, a);
+                t1 = std::max(t1, b);
+            }
+            if (t1 > t0 && t0 != ~0ull) { sum[i] += (double)(t1 - t0); ++cnt[i]; }
+        }
+    }
+    hipFree(ts);
+    // s_memrealtime counts at 100 MHz: 10 ns per tick; -1 for ops without timestamps
+    for (int i = 0; i < n; ++i) avg_us[i] = cnt[i] ? (float)(sum[i] / cnt[i] * 0.01) : -1.f;
+    return rc;
+}
+
+// Empty dispatches bracketing mp_hip_profile_ops_kev's launches, so that a
+// rocprofv3 kernel trace of the same command can be cut to exactly those launches
+// (tools_dev/prof_phase.py) and compared with the events' figures.
+__global__ void profile_mark_kernel() {}
+
+int mp_hip_profile_ops_kev(mp_dev *dev, int iters, float *avg_us) {
+    if (!dev || !avg_us || iters < 1) return MP_ERR_ARG;
+    if (!dev->batch_ready || dev->ops.empty())
+        return fail(dev, MP_ERR_STATE, "mp_hip_profile_ops_kev needs a decoded batch (mp_hip_decode first)");
     HIPCHK(hipSetDevice(dev->device));
     const int n = (int)dev->ops.size();
     std::vector<hipEvent_t> ev(2 * (size_t)n);
     for (auto &e : ev) HIPCHK(hipEventCreate(&e));
     std::vector<double> sum(n, 0.0);
     int rc = MP_OK;
+    hipLaunchKernelGGL(profile_mark_kernel, dim3(1), dim3(64), 0, dev->stream);
     for (int it = 0; it < iters && rc == MP_OK; ++it) {
-        for (int i = 0; i < n; ++i) {
-            const mp::OpRec &r = dev->ops[i];
-            HIPCHK(hipEventRecord(ev[2 * i], dev->stream));
-            hipError_t e = hipErrorInvalidValue;
-            switch (r.kind) {
-            case mp::K_GEMV: e = r.fn(r.g, dev->stream); break;
-            case mp::K_ATTN: e = mp::op_sa_attn(r.a, r.B, dev->stream); break;
-            case mp::K_XA: e = mp::op_xa(r.x, r.B, dev->stream); break;
-            case mp::K_XAQ8: e = mp::op_xa_q8(r.xq, r.B, dev->stream); break;
-            case mp::K_LTFFN: e = mp::op_lt_ffn(r.lf, r.B, dev->stream); break;
-            case mp::K_LTMERGE: e = mp::op_lt_merge(r.lf, r.B, dev->stream); break;
-            case mp::K_LTPICK: e = mp::op_lt_pick(r.g, r.B, dev->stream); break;
-            case mp::K_LTFFN2: e = mp::op_lt_ffn2(r.l2, r.B, dev->stream); break;
-            case mp::K_LTKVO: e = mp::op_lt_kvo(r.g, r.B, dev->stream); break;
-            case mp::K_EMBED: e = mp::op_embed(r.e, r.B, dev->stream); break;
-            case mp::K_FIN: e = mp::op_finalize(r.f, r.B, dev->stream); break;
-            }
-            HIPCHK(e);
-            HIPCHK(hipEventRecord(ev[2 * i + 1], dev->stream));
+        for (int i = 0; i < n && rc == MP_OK; ++i) {
+            mp::g_kev[0] = ev[2 * i];
+            mp::g_kev[1] = ev[2 * i + 1];
+            const hipError_t e = launch_rec(dev->ops[i], dev->stream);
+            mp::g_kev[0] = mp::g_kev[1] = nullptr;
+            if (e != hipSuccess) rc = fail(dev, MP_ERR_HIP, std::string("profile launch: ") + hipGetErrorString(e));
         }
+        if (rc != MP_OK) break;
         HIPCHK(hipStreamSynchronize(dev->stream));
         for (int i = 0; i < n; ++i) {
             float ms = 0.f;
@@ -1680,6 +1774,8 @@ int mp_hip_profile_ops(mp_dev *dev, int iters, float *avg_us) {
             sum[i] += ms;
         }
     }
+    hipLaunchKernelGGL(profile_mark_kernel, dim3(1), dim3(64), 0, dev->stream);
+    HIPCHK(hipStreamSynchronize(dev->stream));
     for (auto &e : ev) hipEventDestroy(e);
     for (int i = 0; i < n; ++i) avg_us[i] = (float)(sum[i] * 1000.0 / iters);
     return rc;
@@ -1691,21 +1787,8 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     mp::OpRec r = dev->ops[op];
     r.g.ndone = nullptr;
     r.g.trace = nullptr;
-    auto launch = [&]() -> hipError_t {
-        if (r.kind == mp::K_GEMV) return r.fn(r.g, dev->stream);
-        if (r.kind == mp::K_ATTN) return mp::op_sa_attn(r.a, r.B, dev->stream);
-        if (r.kind == mp::K_XA) {
-            return mp::op_xa(r.x, r.B, dev->stream);  // rewrites this layer's split states only
-        }
-        if (r.kind == mp::K_XAQ8) return mp::op_xa_q8(r.xq, r.B, dev->stream);  // rewrites x2 with the same values
-        if (r.kind == mp::K_LTFFN) return mp::op_lt_ffn(r.lf, r.B, dev->stream);
-        if (r.kind == mp::K_LTMERGE) return mp::op_lt_merge(r.lf, r.B, dev->stream);
-        if (r.kind == mp::K_LTPICK) return mp::op_lt_pick(r.g, r.B, dev->stream);
-        if (r.kind == mp::K_LTFFN2) return mp::op_lt_ffn2(r.l2, r.B, dev->stream);
-        if (r.kind == mp::K_LTKVO) return mp::op_lt_kvo(r.g, r.B, dev->stream);
-        if (r.kind == mp::K_EMBED) return mp::op_embed(r.e, r.B, dev->stream);
-        return hipErrorInvalidValue;
-    };
+    // XA rewrites this layer's split states only; XA-Q8 rewrites x2 with the same values
+    auto launch = [&]() -> hipError_t { return launch_rec(r, dev->stream); };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");
     HIPCHK(launch());  // warm
     hipEvent_t e0, e1;

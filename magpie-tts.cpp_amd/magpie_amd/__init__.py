@@ -79,6 +79,9 @@ SYMBOLS = [
     ("mp_hip_op_bytes", ctypes.c_double, [_P, _I]),
     ("mp_hip_time_op", _I, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mp_hip_profile_ops", _I, [_P, _I, _P]),
+    ("mp_hip_profile_ops_ex", _I, [_P, _I, _P, _P]),
+    ("mp_hip_profile_ops_ts", _I, [_P, _I, _P]),
+    ("mp_hip_profile_ops_kev", _I, [_P, _I, _P]),
     ("mp_tokenizer_load", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
     ("mp_tokenize", _I, [_P, ctypes.c_char_p, _P, _I]),
     ("mp_tokenizer_free", None, [_P]),
@@ -295,6 +298,29 @@ class Device:
         n = self.lib.mp_hip_num_ops(self.h)
         out = np.zeros(max(n, 1), np.float32)
         self._check(self.lib.mp_hip_profile_ops(self.h, iters, out.ctypes.data))
+        return out[:n]
+
+    def profile_ops_ex(self, iters: int = 32):
+        """(event-pair time per op, empty-pair time right after it), us"""
+        n = self.lib.mp_hip_num_ops(self.h)
+        out = np.zeros(max(n, 1), np.float32)
+        pair = np.zeros(max(n, 1), np.float32)
+        self._check(self.lib.mp_hip_profile_ops_ex(self.h, iters, out.ctypes.data, pair.ctypes.data))
+        return out[:n], pair[:n]
+
+    def profile_ops_ts(self, iters: int = 32) -> np.ndarray:
+        """per-op launch duration from in-kernel timestamps (us; -1: not instrumented)"""
+        n = self.lib.mp_hip_num_ops(self.h)
+        out = np.zeros(max(n, 1), np.float32)
+        self._check(self.lib.mp_hip_profile_ops_ts(self.h, iters, out.ctypes.data))
+        return out[:n]
+
+    def profile_ops_kev(self, iters: int = 32) -> np.ndarray:
+        """per-op launch duration from the dispatch's begin/end timestamps (us), the
+        interval rocprofv3's kernel trace reports"""
+        n = self.lib.mp_hip_num_ops(self.h)
+        out = np.zeros(max(n, 1), np.float32)
+        self._check(self.lib.mp_hip_profile_ops_kev(self.h, iters, out.ctypes.data))
         return out[:n]
 
     def time_op(self, op: int, reps: int = 50) -> float:

@@ -19,4 +19,6 @@ tail -1 "$OUT/${TAG}_bench.log" > "$OUT/${TAG}_bench.json"
 echo "bench ok"
 MAGPIE_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/${TAG}_prof" -o prof \
   -- python3 -u bench.py --no-cpu-baseline --no-extra > "$OUT/${TAG}_prof_bench.log" 2>&1
+python3 tools_dev/prof_phase.py "$OUT/${TAG}_prof/prof_kernel_trace.csv" "$OUT/${TAG}_prof/phase_kernel_stats.csv" \
+  > "$OUT/${TAG}_prof_phase.log"
 echo "rocprof ok"

@@ -21,6 +21,10 @@
 
 namespace mp {
 
+template <bool HANDOFF>
+__device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned long long *xh, unsigned tag, int *err,
+                                        int dep, unsigned long long *ts = nullptr, unsigned long long t_start = 0);
+
 // ---------------------------------------------------------------- GEMV core
 // Rows [row0, row0+RW) of W (row-major [N][K]) dotted with act[NB][K].
 // Lane l owns elements 4*(l + 64*i): every weight load is a 1 KiB coalesced
@@ -28,6 +32,16 @@ namespace mp {
 template <int NB, int RW, int K, int PRO, int EPI>
 __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     const unsigned long long t_start = ts_begin(p.ts);
+    if constexpr (EPI == EPI_RESID_XA) {
+        // the launch's last XA_SPLITS x NB workgroups: cross-attention on this launch's x1
+        if ((int)blockIdx.x >= p.nrow_blocks) {
+            const int k = blockIdx.x - p.nrow_blocks;
+            xa_part<true>(p.xa, k % XA_SPLITS, k / XA_SPLITS, p.xh, (unsigned)p.iter[0] * 64u + p.layer + 1u,
+                          p.hx_err, ts_dep(t_start), p.ts, t_start);
+            ts_end(p.ts, t_start);
+            return;
+        }
+    }
     // No early exit on the done counter: a dependent load there would sit in
     // front of the weight stream of every launch. Once every slot is done the
     // iteration recomputes identical values (codes_prev / pos are frozen) and
@@ -79,7 +93,17 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     if (lane >= RW * NB) return;
     const int b = lane % NB, n = row0 + lane / NB;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
+    if constexpr (EPI == EPI_RESID_XA) {
+        float *r = p.resid + (size_t)b * D + n;
+        const float x1 = v + *r;
+        *r = x1;
+        const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned long long *)(p.xh + (size_t)b * D + n),
+                           ((unsigned long long)tag << 32) | __float_as_uint(x1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
+    }
     ts_end(p.ts, t_start);
 }
 
@@ -182,17 +206,29 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
 #define MP_XA_KPW 4
 #endif
 constexpr int XA_WAVES = MP_XA_WAVES, XA_THREADS = XA_WAVES * 64, XA_KPW = MP_XA_KPW;  // keys in flight per wave
-constexpr int XA_V = D / 256;  // float4 per lane per 768-row: lane owns elements 4 lane + 256 i + (0..3)
-__global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
-    const unsigned long long t_start = ts_begin(p.ts);
+constexpr int XA_V = D / 256;
+static_assert(XA_THREADS == MP_BLOCK, "XA workgroups ride in the O-projection launch (EPI_RESID_XA)");  // float4 per lane per 768-row: lane owns elements 4 lane + 256 i + (0..3)
+// Hand-off bound: polls of the x1 granules before an XA workgroup gives up (with
+// s_sleep between polls this is far beyond any O-projection's duration)
+constexpr unsigned HX_SPIN_LIMIT = 1u << 20;
+using gu64 = __attribute__((address_space(1))) unsigned long long;
+using gi32 = __attribute__((address_space(1))) int;
+
+// Split sp of slot b. HANDOFF: x1 comes from the O-projection in the same launch,
+// as {tag, value} granules xh[b][768] (EPI_RESID_XA): every wave sweeps all 768
+// with relaxed agent-scope loads (write-through producer stores, so no fence is
+// needed) until every tag matches, after its K'/V' rows are already in flight.
+template <bool HANDOFF>
+__device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned long long *xh, unsigned tag, int *err,
+                                        int dep, unsigned long long *ts, unsigned long long t_start) {
     __shared__ float wm[XA_WAVES], wl[XA_WAVES];
     __shared__ __attribute__((aligned(16))) float wo[XA_WAVES][D];
-    const int sp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int Tb = p.T[b];
     const int chunk = (Tb + XA_SPLITS - 1) / XA_SPLITS;
     const int t0 = sp * chunk, t1 = min(Tb, t0 + chunk);
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
-    const float *Kp = p.kp + base + 4 * lane + ts_dep(t_start), *Vp = p.vp + base + 4 * lane;
+    const float *Kp = p.kp + base + 4 * lane + dep, *Vp = p.vp + base + 4 * lane;
     float4 k[XA_KPW][XA_V], vv[XA_KPW][XA_V];
 #pragma unroll
     for (int u = 0; u < XA_KPW; ++u) {
@@ -208,9 +244,38 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
     {   // LN(x) (magpie.cpp:3513), every wave for itself (DPP statistics, no barrier)
         float4 x4[XA_V], g4[XA_V];
 #pragma unroll
-        for (int i = 0; i < XA_V; ++i) {
-            x4[i] = *(const float4 *)(p.x + (size_t)b * D + 4 * lane + 256 * i);
-            g4[i] = *(const float4 *)(p.lnw + 4 * lane + 256 * i);
+        for (int i = 0; i < XA_V; ++i) g4[i] = *(const float4 *)(p.lnw + 4 * lane + 256 * i);
+        if constexpr (HANDOFF) {
+            gu64 *g = (gu64 *)(xh + (size_t)b * D);
+            float xv[D / 64];
+            for (unsigned spins = 0;; ++spins) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < D / 64; ++j) {
+                    const unsigned long long u = __hip_atomic_load(g + lane + 64 * j, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    xv[j] = __uint_as_float((unsigned)u);
+                    ok &= (unsigned)(u >> 32) == tag;
+                }
+                if (__all(ok)) break;
+                if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+                    if (lane == 0) __hip_atomic_store((gi32 *)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                    for (int j = 0; j < D / 64; ++j) xv[j] = __builtin_nanf("");
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            ts_mark(ts, t_start);  // profiling: when this wave saw all of x1
+            // to the float4 layout through this wave's own LDS row (reused for o below)
+#pragma unroll
+            for (int j = 0; j < D / 64; ++j) wo[w][lane + 64 * j] = xv[j];
+            wave_lds_sync();
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)&wo[w][4 * lane + 256 * i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)(p.x + (size_t)b * D + 4 * lane + 256 * i);
         }
         float v[4 * XA_V];
 #pragma unroll
@@ -283,6 +348,11 @@ __global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
         *(float4 *)(pp + 4 + 4 * tid) = num;
     }
     if (tid == 0) { pp[0] = M; pp[1] = den; }
+}
+
+__global__ __launch_bounds__(XA_THREADS) void xa_part_kernel(XaP p) {
+    const unsigned long long t_start = ts_begin(p.ts);
+    xa_part<false>(p, blockIdx.x, blockIdx.y, nullptr, 0u, nullptr, ts_dep(t_start));
     ts_end(p.ts, t_start);
 }
 
@@ -302,6 +372,7 @@ __global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
     // one wave per slot: codebook 7's pick with the same wave_pick as every other
     // codebook (masked first-max argmax; top-k draw when sampling)
     const int b = blockIdx.x, tid = threadIdx.x;
+    if (p.iter && b == 0 && tid == 0) p.iter[0] += 1;  // the next iteration's hand-off tags
     if (p.done[b]) return;
     __shared__ float scratch[2 * VCB];
     int i0, amax;
@@ -373,6 +444,9 @@ static bool gemv_args_ok(const GemvP &p) {
     if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
     if constexpr (EPI == EPI_LTKVO) ok &= p.lk && p.lv && p.N == 2 * LTD;
+    if constexpr (EPI == EPI_RESID_XA)
+        ok &= p.resid && p.xh && p.iter && p.hx_err && p.N == D && p.xa.part && p.xa.lnw && p.xa.kp && p.xa.vp &&
+              p.xa.T && p.xa.Tmax >= 1 && p.xa.Tmax <= TMAX_LIMIT;
     return ok;
 }
 
@@ -380,8 +454,10 @@ template <int NB, int RW, int K, int PRO, int EPI>
 static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
     if (!gemv_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
     const int rows_per_block = MP_NWAVES * RW;
-    const int grid = (p.N + rows_per_block - 1) / rows_per_block;
-    mp::launch((gemv_kernel<NB, RW, K, PRO, EPI>), dim3(grid), dim3(MP_BLOCK), 0, s, p);
+    GemvP q = p;
+    q.nrow_blocks = (p.N + rows_per_block - 1) / rows_per_block;
+    const int grid = q.nrow_blocks + (EPI == EPI_RESID_XA ? XA_SPLITS * NB : 0);
+    mp::launch((gemv_kernel<NB, RW, K, PRO, EPI>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();
 }
 
@@ -391,6 +467,9 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
     hipError_t op_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_SA_MERGE, EPI_RESID>(p, s); } \
+    hipError_t op_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                   \
+        return launch_gemv<NB, 1, D, PRO_SA_MERGE, EPI_RESID_XA>(p, s);                                            \
+    }                                                                                                              \
     hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_GELU>(p, s); }            \
     hipError_t op_ff1x_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_XA_LN, EPI_GELU>(p, s); }        \
     hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \

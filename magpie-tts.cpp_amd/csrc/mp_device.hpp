@@ -107,6 +107,16 @@ __device__ __forceinline__ unsigned long long ts_begin(const unsigned long long 
     return t;
 }
 __device__ __forceinline__ int ts_dep(unsigned long long t) { return (int)(t >> 63); }
+// an intermediate stamp (t0, now) of wave w into wave slot TS_WAVES/2 + w (4-wave kernels)
+__device__ __forceinline__ void ts_mark(unsigned long long *ts, unsigned long long t0) {
+    if (ts) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const int blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if ((threadIdx.x & 63) == 0 && blk < TS_BLOCKS && (threadIdx.x >> 6) < TS_WAVES / 2)
+            *(ulonglong2 *)(ts + 2 * ((size_t)blk * TS_WAVES + TS_WAVES / 2 + (threadIdx.x >> 6))) =
+                make_ulonglong2(t0, t1);
+    }
+}
 __device__ __forceinline__ void ts_end(unsigned long long *ts, unsigned long long t0) {
     if (ts) {
         __builtin_amdgcn_s_waitcnt(0);

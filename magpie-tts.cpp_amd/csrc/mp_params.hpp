@@ -57,6 +57,8 @@ enum Epi {
     EPI_GELU_B16 = 7,   // out_b16 = bf16(gelu(v)): the bf16 FFN-down operand, rounded once here
     EPI_LTX_ADD = 8,    // out = v + (P[cb-1][code] + lt_pos[cb]): LT residual of PRO_LTARG_ATTN's code
     EPI_LTKVO = 9,      // f32 LT position 0: rows [0,256) k_0 -> lk[b][0], rows [256,512) vo_0 -> lv[b][0]
+    EPI_RESID_XA = 10,  // resid += v, each new x1 value also published as a tagged granule; the
+                        // launch's last XA_SPLITS x NB workgroups run the fused XA on it (below)
 };
 
 // Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
@@ -135,6 +137,22 @@ __host__ __device__ inline float mp_uniform(unsigned long long seed, int stream,
     return (float)(h >> 40) * (1.0f / 16777216.0f);
 }
 
+// Fused cross-attention for one decode step (replaces the xq GEMV + XA attention
+// + xo GEMV). With K'_t = W_q^T K_t and V'_t = W_o V_t precomputed per utterance
+// and layer:  x += sum_t softmax_t(K'_t . LN(x) / sqrt(128)) V'_t
+// (= o_net(attn(q_net(LN(x)), K, V)), magpie.cpp:1713-1767, by associativity).
+struct XaP {
+    const float *x;        // [B][768] residual in
+    float *part;           // [B][XA_SPLITS][XA_PART] partial softmax states over text-key splits
+                           // (merged + added to x in the next op's PRO_XA_LN prologue)
+    const float *lnw;      // norm_xattn_query
+    float eps;
+    const float *kp, *vp;  // K', V': [B][L][Tmax][768]
+    const int *T;
+    int Tmax, layer, nlayers;
+    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
+};
+
 struct GemvP {
     const float *W;
     const unsigned short *Wb;  // bf16 weights in MFMA fragment order (mp_decode_b16.hip), or null
@@ -183,6 +201,18 @@ struct GemvP {
     int nslots;
     const float *part;   // PRO_SA_MERGE: [B][NH][SA_SPLITS][SA_PART]; PRO_XA_LN: [B][XA_SPLITS][XA_PART]
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
+    // EPI_RESID_XA (O-projection + cross-attention in one launch): the O-projection's
+    // workgroups publish x1 = x + W_o attn as 8-byte {tag, value} granules xh[B][768]
+    // (relaxed agent-scope atomic stores: write-through, no fence); the last
+    // XA_SPLITS x B workgroups prefetch their K'/V' rows, sweep the granules until
+    // every tag equals this launch's (iteration counter * 64 + layer + 1, never 0;
+    // xh is zeroed per batch) and run xa_part on x1. A sweep that never completes
+    // gives up after a bound and raises *hx_err.
+    XaP xa;
+    unsigned long long *xh;
+    const int *iter;
+    int *hx_err;
+    int nrow_blocks;     // set by the launcher: workgroups of the O-projection
 };
 
 struct FinP {
@@ -193,22 +223,7 @@ struct FinP {
     Sampling smp;
     int emit_eos;   // streaming semantics: the EOS frame's codes are emitted too (magpie.cpp:4800-4806)
     int lt_only;    // magpie_local_transformer_sample_all: pick codebook 7, no loop bookkeeping
-    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
-};
-
-// Fused cross-attention for one decode step (replaces the xq GEMV + XA attention
-// + xo GEMV). With K'_t = W_q^T K_t and V'_t = W_o V_t precomputed per utterance
-// and layer:  x += sum_t softmax_t(K'_t . LN(x) / sqrt(128)) V'_t
-// (= o_net(attn(q_net(LN(x)), K, V)), magpie.cpp:1713-1767, by associativity).
-struct XaP {
-    const float *x;        // [B][768] residual in
-    float *part;           // [B][XA_SPLITS][XA_PART] partial softmax states over text-key splits
-                           // (merged + added to x in the next op's PRO_XA_LN prologue)
-    const float *lnw;      // norm_xattn_query
-    float eps;
-    const float *kp, *vp;  // K', V': [B][L][Tmax][768]
-    const int *T;
-    int Tmax, layer, nlayers;
+    int *iter;      // decode iteration counter (tags of the in-launch hand-offs), +1 per iteration
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 

@@ -32,7 +32,7 @@ using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
 #define MP_DECL_OPS(NB)                                                                                     \
     hipError_t op_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t op_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t op_oproj_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);            \
-    hipError_t op_ff1x_##NB(const GemvP &, hipStream_t);                                                                \
+    hipError_t op_ff1x_##NB(const GemvP &, hipStream_t); hipError_t op_oproj_xa_##NB(const GemvP &, hipStream_t);       \
     hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
     hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_lt_bg_##NB(const GemvP &, hipStream_t);                                                              \
@@ -91,14 +91,16 @@ hipError_t op_finalize(const FinP &, int, hipStream_t);
 namespace mp {
 
 // ff1: LN(x2) prologue (x2 materialised: Q8 unfused XA); ff1x: the fused XA's split states merged into x2 first
-struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e; };
+// oproj_xa: O-projection + the fused XA in one launch (EPI_RESID_XA; f32 GEMV family only)
+struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e, oproj_xa; };
 #define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
-                       op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB }
+                       op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, \
+                       op_oproj_xa_##NB }
 static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
 #define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, nullptr, b16_ff1_##NB, b16_ff2_##NB, \
                            op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_bg_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
-                           b16_lt_d_##NB, b16_lt_e_##NB }
+                           b16_lt_d_##NB, b16_lt_e_##NB, nullptr }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
@@ -205,6 +207,7 @@ struct mp_dev {
     int32_t *h_codes = nullptr;              // streaming: pinned host mirror of codes_out [NB][S][8] + snapshots
     size_t h_codes_n = 0;
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
+    unsigned long long *xh = nullptr;  // O-projection -> XA hand-off granules [NB][768] (EPI_RESID_XA)
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
@@ -645,13 +648,14 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(sa_out, NB * 768);
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
+    A(xh, (size_t)NB * D);
     A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
     A(ltp, (size_t)NB * mp::LT_FFN_P * 256);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
-    A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);
+    A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
     A(codes_cur, NB * 8); A(codes_prev, NB * 8); A(codes_out, (size_t)NB * max_steps * 8); A(tok, (size_t)NB * Tmax);
     const size_t rows = (size_t)NB * std::max(Tmax, mp::CTX);
@@ -750,9 +754,18 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.part = dev->sa_part;
         g.Wq = W.o8.q; g.Wd = W.o8.d;
-        if ((rc = run("oproj", W.o8 ? tq.oproj : tb.oproj, g, (W.o8 ? Fq : F) * (768.0 * 768) + A * act * (768 * 3))) !=
-            MP_OK)
+        const mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
+        const double xa_bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
+        const bool xa_in_oproj = tb.oproj_xa && !W.o8 && !W.xq8;
+        if (xa_in_oproj) {
+            // f32: the fused XA rides in the O-projection's launch on a hand-off of x1
+            g.xa = xp; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
+            if ((rc = run("oproj_xa", tb.oproj_xa, g, F * (768.0 * 768) + A * act * (768 * 3) + xa_bytes)) != MP_OK)
+                return rc;
+        } else if ((rc = run("oproj", W.o8 ? tq.oproj : tb.oproj, g,
+                             (W.o8 ? Fq : F) * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) {
             return rc;
+        }
         if (W.xq8) {
             // cross-attention with Q8_0 q_net / o_net, as ggml computes it (1713-1767):
             // q = Q8(q_net) LN(x) (GEMV), then x2 = x + Q8(o_net) attn(q, K, V) (xa_q8_kernel)
@@ -768,13 +781,12 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
                 dev->ops.push_back(r);
             }
             HIPCHK(mp::op_xa_q8(xq, NB, s));
-        } else {
+        } else if (!xa_in_oproj) {
             // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
-            mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
             if (record) {
                 mp::OpRec r{};
                 r.name = "xa"; r.kind = mp::K_XA; r.x = xp; r.B = NB;
-                r.bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
+                r.bytes = xa_bytes;
                 dev->ops.push_back(r);
             }
             HIPCHK(mp::op_xa(xp, NB, s));
@@ -1040,7 +1052,8 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     }
     mp::FinP f{io.logits, io.codes_cur, io.codes_prev, io.codes_out, io.step, io.pos, io.done, io.nframes, io.ndone,
                io.max_steps, io.ignore_eos, m.audio_bos, m.audio_eos, NB,
-               mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax}, io.emit_eos, io.lt_only};
+               mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax}, io.emit_eos, io.lt_only,
+               io.lt_only ? nullptr : io.ndone + 1};
     if (ops) {
         mp::OpRec r{};
         r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = A * act * 2024;
@@ -1323,6 +1336,8 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemcpyAsync(dev->codes_prev, h_prev.data(), h_prev.size() * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemsetAsync(dev->codes_out, 0, (size_t)NB * dev->max_steps * 8 * 4, dev->stream));
     HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
+    // hand-off tags restart with the iteration counter (ndone[1]): no stale tag may match
+    HIPCHK(hipMemsetAsync(dev->xh, 0, (size_t)NB * 768 * 8, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go
     HIPCHK(hipStreamSynchronize(dev->stream));
     return MP_OK;
@@ -1356,6 +1371,15 @@ int launch_iteration(mp_dev *dev) {
     return MP_OK;
 }
 
+// An in-launch hand-off that gave up (EPI_RESID_XA's bounded sweep) poisons its
+// output and raises ndone[2]: report it instead of returning those codes.
+static int check_handoff(mp_dev *dev) {
+    int nd[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpy(nd, dev->ndone, sizeof nd, hipMemcpyDeviceToHost));
+    if (nd[2]) return fail(dev, MP_ERR_HIP, "in-launch hand-off (O-projection -> cross-attention) timed out");
+    return MP_OK;
+}
+
 int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     if (!dev) return MP_ERR_ARG;
     if (!dev->batch_ready) return fail(dev, MP_ERR_STATE, "mp_hip_begin_batch must precede mp_hip_decode");
@@ -1382,6 +1406,7 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     hipEventDestroy(e0);
     hipEventDestroy(e1);
+    if (int rc = check_handoff(dev)) return rc;
     std::vector<int> h_nf(NB);
     HIPCHK(hipMemcpy(h_nf.data(), dev->nframes, NB * 4, hipMemcpyDeviceToHost));
     std::vector<int> h_codes((size_t)NB * dev->max_steps * 8);
@@ -1533,6 +1558,7 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
         slot ^= 1;
     }
     HIPCHK(hipStreamSynchronize(dev->stream));
+    if (int rc = check_handoff(dev)) return rc;
     dev->timing.decode_ms = ms_since(t0);
     dev->timing.iterations = it;
     int total = 0;
@@ -1725,6 +1751,9 @@ int mp_hip_profile_ops_ts(mp_dev *dev, int iters, float *avg_us) {
         if (rc != MP_OK) break;
         HIPCHK(hipMemcpyAsync(h.data(), ts, (size_t)n * per * 8, hipMemcpyDeviceToHost, dev->stream));
         HIPCHK(hipStreamSynchronize(dev->stream));
+        if (const char *dump = getenv("MAGPIE_TS_DUMP")) {  // raw stamps of the last iteration (diagnostics)
+            if (FILE *fp = fopen(dump, "wb")) { fwrite(h.data(), 8, h.size(), fp); fclose(fp); }
+        }
         for (int i = 0; i < n; ++i) {
             unsigned long long t0 = ~0ull, t1 = 0;
             for (size_t k = 0; k < per / 2; ++k) {

@@ -129,6 +129,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
         for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     }
     lds_sync();
+    ts_mark(p.ts, t_start);  // profiling: activation tile staged
 
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     const unsigned short *brow = actb + min(lane & 15, NB) * KP + 8 * (lane >> 4);

@@ -202,6 +202,16 @@ __device__ __forceinline__ float lt_ffn_merge(const float *part, const float *y,
     return s + y[(size_t)b * LTD + k];
 }
 
+// LayerNorm weights of this lane's elements lane + 64 i, loaded before the
+// prologue's first global store (a load behind a store that may alias it waits
+// for the store: one memory round trip per element otherwise)
+template <int PER>
+__device__ __forceinline__ void load_lnw(const float *lnw, float (&g)[PER]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) g[i] = lnw[lane + 64 * i];
+}
+
 // LDS scratch (floats) a prologue needs besides the activation rows
 template <int NB, int PRO>
 constexpr int pro_scratch() {
@@ -312,17 +322,23 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 const float4 x2 = make_float4(num.x * rd + xv[u].x, num.y * rd + xv[u].y, num.z * rd + xv[u].z,
                                               num.w * rd + xv[u].w);
                 *(float4 *)(act + b * K + k) = x2;
-                if (blockIdx.x == 0) *(float4 *)(p.xres + (size_t)b * D + k) = x2;
             }
         }
         lds_sync();
         const int lane = tid & 63, w = tid >> 6;
         constexpr int PER = K / 64;
+        float g[PER];
+        load_lnw<PER>(p.lnw, g);
         if constexpr (NB == 1) {
             constexpr int Q = PER / MP_NWAVES;
             float v[PER];
 #pragma unroll
             for (int i = 0; i < PER; ++i) v[i] = act[lane + 64 * i];
+            // x2 to HBM (block 0) after every global load of the prologue: a store
+            // earlier would order the later loads behind it
+            if (blockIdx.x == 0 && w == 0)
+#pragma unroll
+                for (int i = 0; i < PER; ++i) p.xres[lane + 64 * i] = v[i];
             float mean, var;
             wave_meanvar<PER>(v, mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
@@ -331,20 +347,23 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             for (int i = 0; i < PER; ++i) {
                 if (i / Q != w) continue;
                 const int k = lane + 64 * i;
-                act[k] = ((v[i] - mean) * rstd) * p.lnw[k];
+                act[k] = ((v[i] - mean) * rstd) * g[i];
             }
         } else {
             for (int b = w; b < NB; b += MP_NWAVES) {  // a wave owns its slots' rows
                 float v[PER];
 #pragma unroll
                 for (int i = 0; i < PER; ++i) v[i] = act[b * K + lane + 64 * i];
+                if (blockIdx.x == 0)
+#pragma unroll
+                    for (int i = 0; i < PER; ++i) p.xres[(size_t)b * D + lane + 64 * i] = v[i];
                 float mean, var;
                 wave_meanvar<PER>(v, mean, var);
                 const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
                 for (int i = 0; i < PER; ++i) {
                     const int k = lane + 64 * i;
-                    act[b * K + k] = ((v[i] - mean) * rstd) * p.lnw[k];
+                    act[b * K + k] = ((v[i] - mean) * rstd) * g[i];
                 }
             }
         }
@@ -363,6 +382,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         // tree over the row, exactly as every wave computes them at batch 1
         const int lane = tid & 63, w = tid >> 6;
         constexpr int PER = K / 64, SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
+        float g[PER];  // in registers before any store: a load after a possibly aliasing
+        load_lnw<PER>(p.lnw, g);  // store would wait for it, one round trip per element
         float vs[SPW][PER];  // every slot of this wave is loaded before any is reduced
 #pragma unroll
         for (int j = 0; j < SPW; ++j) {
@@ -384,7 +405,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int k = lane + 64 * i;
-                const float y = ((v[i] - mean) * rstd) * p.lnw[k];
+                const float y = ((v[i] - mean) * rstd) * g[i];
                 act[b * K + k] = y;
                 if (st) p.hidden_out[(size_t)b * K + k] = y;
                 if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[((size_t)b * p.trace_steps + s) * K + k] = y;
@@ -396,9 +417,10 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         // (identical results, no barrier), then writes its quarter
         const int lane = tid & 63, w = tid >> 6;
         constexpr int PER = K / 64, Q = PER / MP_NWAVES;
-        float v[PER];
+        float v[PER], g[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) v[i] = p.src[lane + 64 * i];
+        load_lnw<PER>(p.lnw, g);
         float mean, var;
         wave_meanvar<PER>(v, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.eps);
@@ -408,7 +430,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         for (int i = 0; i < PER; ++i) {
             if (i / Q != w) continue;
             const int k = lane + 64 * i;
-            const float y = ((v[i] - mean) * rstd) * p.lnw[k];
+            const float y = ((v[i] - mean) * rstd) * g[i];
             act[k] = y;
             if (st) p.hidden_out[k] = y;
             if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[(size_t)s * K + k] = y;
@@ -417,6 +439,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
     } else if constexpr (PRO == PRO_EMBED_LN && NB >= 2) {
         static_assert(K == D, "embed prologue is d_model wide");
         const int lane = tid & 63, w = tid >> 6;
+        float g[K / 64];
+        load_lnw<K / 64>(p.lnw, g);
         for (int b = w; b < NB; b += MP_NWAVES) {
             int c[NCB];
 #pragma unroll
@@ -430,15 +454,17 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
 #pragma unroll
                 for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
                 x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
-                if (blockIdx.x == 0) p.xres[(size_t)b * D + k] = x[i];
             }
+            if (blockIdx.x == 0)  // after every load of the row (a store would order the loads behind it)
+#pragma unroll
+                for (int i = 0; i < K / 64; ++i) p.xres[(size_t)b * D + lane + 64 * i] = x[i];
             float mean, var;
             wave_meanvar<K / 64>(x, mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
             for (int i = 0; i < K / 64; ++i) {
                 const int k = lane + 64 * i;
-                act[b * K + k] = ((x[i] - mean) * rstd) * p.lnw[k];
+                act[b * K + k] = ((x[i] - mean) * rstd) * g[i];
             }
         }
         lds_sync();
@@ -446,6 +472,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         static_assert(K == D, "embed prologue is d_model wide");
         const int lane = tid & 63, w = tid >> 6;
         constexpr int PER = K / 64, Q = PER / MP_NWAVES;
+        float g[PER];
+        load_lnw<PER>(p.lnw, g);
         int c[NCB];
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) c[cb] = p.codes[cb];
@@ -467,26 +495,30 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             if (i / Q != w) continue;
             const int k = lane + 64 * i;
             if (blockIdx.x == 0) p.xres[k] = x[i];
-            act[k] = ((x[i] - mean) * rstd) * p.lnw[k];
+            act[k] = ((x[i] - mean) * rstd) * g[i];
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LTX_LN) {
         // one wave per slot at every batch size (wave_block_meanvar), so a batch
         // reproduces its utterances run alone bit for bit
         const int lane = tid & 63, w = tid >> 6;
+        float g[4];
+        load_lnw<4>(p.lnw, g);
         for (int b = w; b < NB; b += MP_NWAVES) {
             float X[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int k = lane + 64 * i;
                 X[i] = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
-                if (blockIdx.x == 0) p.ltX[(size_t)b * LTD + k] = X[i];
             }
+            if (blockIdx.x == 0)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) p.ltX[(size_t)b * LTD + lane + 64 * i] = X[i];
             float mean, var;
             wave_block_meanvar<1>(X, mean, var);
             const float rstd = 1.0f / sqrtf(var + p.eps);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * p.lnw[lane + 64 * i];
+            for (int i = 0; i < 4; ++i) act[b * K + lane + 64 * i] = ((X[i] - mean) * rstd) * g[i];
         }
         lds_sync();
     } else if constexpr (PRO == PRO_LTARG_ATTN) {

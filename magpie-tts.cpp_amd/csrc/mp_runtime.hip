@@ -25,6 +25,7 @@
 #include "mp_device.hpp"
 #include "mp_params.hpp"
 
+
 namespace mp {
 
 // ---- launchers (mp_decode.hip / mp_prefill.hip)

@@ -22,14 +22,16 @@ for B in [int(b) for b in sys.argv[2:]]:
     fps = B * 256 * 1e3 / r.decode_ms
     dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=128, ignore_eos=True)
     names = dev.ops()
-    us = dev.profile_ops(iters=16)
-    groups = {}
+    us = dev.profile_ops_kev(iters=16)
+    span = dev.profile_ops_ts(iters=16)
+    groups, spans = {}, {}
     for i, n in enumerate(names):
         groups.setdefault(n, []).append(us[i])
+        spans.setdefault(n, []).append(span[i])
     print(f"== {weights} B={B}: {fps:.0f} fps, {r.decode_ms / 256 * 1e3:.1f} us/iteration (graph)")
     tot = 0.0
     for n, v in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
         tot += sum(v)
-        print(f"  {n:12s} {len(v):3d} x {np.mean(v):7.2f} us = {sum(v):8.1f} us/iter")
-    print(f"  event-timed total {tot:.1f} us/iter")
+        print(f"  {n:12s} {len(v):3d} x {np.mean(v):7.2f} us (wave span {np.mean(spans[n]):6.2f}) = {sum(v):8.1f} us/iter")
+    print(f"  dispatch-timed total {tot:.1f} us/iter")
 dev.close()

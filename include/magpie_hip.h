@@ -85,8 +85,19 @@ int mp_hip_load_model(mp_dev *dev, const char *gguf_path);
  * 32-block contributes its exact integer dot times d_w*d_a — in the encoder, the
  * XA K/V precompute, the prefill, every decode step and the LT. F32 tensors (the
  * pos_ff convs) keep the f32 path. Batches up to 8. MP_ERR_UNSUPPORTED for a file
- * without Q8_0 tensors (BASELINE config 5). */
+ * without Q8_0 tensors (BASELINE config 5). A Q4_0 file (convert_magpie_to_gguf.py:
+ * 107-138) runs in this mode too: its blocks are repacked losslessly to int8 q - 8
+ * with the same fp16 scale, so the same kernels compute ggml's vec_dot_q4_0_q8_0. */
 #define MP_WEIGHTS_Q8 2
+/* F16: an F16 GGUF (the converter's F16 file: the same projections plus the pos_ff
+ * convs, convert_magpie_to_gguf.py:311-327) computed as ggml computes F16 mul_mat:
+ * every projection's activation rounded to f16, products exact, f32 accumulation.
+ * The decode-step projections (decoder qkv/o/ff1/ff2, LT in_proj/layer/heads) stream
+ * their f16 weights on f16 MFMA (2 B/param); the preamble GEMMs round their operand;
+ * the fused cross-attention rounds its query (LN(x)) to f16, and applies o_net to the
+ * unrounded attention output (reassociated). Batches up to 16.
+ * MP_ERR_UNSUPPORTED for a file whose projections are not F16. */
+#define MP_WEIGHTS_F16 3
 int mp_hip_load_model_ex(mp_dev *dev, const char *gguf_path, int weight_mode);
 int mp_hip_weight_mode(mp_dev *dev);
 int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes);

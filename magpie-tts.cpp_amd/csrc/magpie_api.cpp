@@ -26,17 +26,23 @@ magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_
         delete ctx;
         return nullptr;
     }
-    // Weight mode (magpie_hip.h): a GGUF with Q8_0 tensors runs them as ggml does
-    // (MP_WEIGHTS_Q8), any other file as stored; MAGPIE_WEIGHTS=f32|bf16|q8 overrides.
+    // Weight mode (magpie_hip.h): a GGUF with Q8_0 / Q4_0 tensors runs them as ggml does
+    // (MP_WEIGHTS_Q8), an F16 file with ggml's F16 semantics (MP_WEIGHTS_F16), any other
+    // file as stored; MAGPIE_WEIGHTS=f32|bf16|q8|f16 overrides.
     const char *wm = getenv("MAGPIE_WEIGHTS");
     int mode = MP_WEIGHTS_Q8;
     bool forced = false;
     if (wm && *wm) {
         forced = true;
-        mode = !strcmp(wm, "bf16") ? MP_WEIGHTS_BF16 : !strcmp(wm, "q8") ? MP_WEIGHTS_Q8 : MP_WEIGHTS_AS_STORED;
+        mode = !strcmp(wm, "bf16")  ? MP_WEIGHTS_BF16
+               : !strcmp(wm, "q8") ? MP_WEIGHTS_Q8
+               : !strcmp(wm, "f16") ? MP_WEIGHTS_F16
+                                    : MP_WEIGHTS_AS_STORED;
     }
     int rc = mp_hip_load_model_ex(ctx->model.dev, model_path, mode);
-    if (rc == MP_ERR_UNSUPPORTED && !forced)  // no Q8_0 tensors in the file: as stored
+    if (rc == MP_ERR_UNSUPPORTED && !forced)  // no block-quantised tensors: an F16 file?
+        rc = mp_hip_load_model_ex(ctx->model.dev, model_path, MP_WEIGHTS_F16);
+    if (rc == MP_ERR_UNSUPPORTED && !forced)  // neither: as stored
         rc = mp_hip_load_model_ex(ctx->model.dev, model_path, MP_WEIGHTS_AS_STORED);
     if (rc != MP_OK) {
         fprintf(stderr, "magpie: failed to load '%s': %s\n", model_path, mp_hip_error(ctx->model.dev));

@@ -287,6 +287,11 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
         for (int i = 0; i < XA_V; ++i)
             h[i] = make_float4(((x4[i].x - mean) * rstd) * g4[i].x, ((x4[i].y - mean) * rstd) * g4[i].y,
                                ((x4[i].z - mean) * rstd) * g4[i].z, ((x4[i].w - mean) * rstd) * g4[i].w);
+        if (p.q_f16)  // h . K'_t = q . K_t with q = W_q f16(h): the rounding commutes through K'
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i)
+                h[i] = make_float4((float)(_Float16)h[i].x, (float)(_Float16)h[i].y, (float)(_Float16)h[i].z,
+                                   (float)(_Float16)h[i].w);
     }
     const float scale = 1.0f / sqrtf((float)DXA);
     float m = -INFINITY, l = 0.f;

@@ -25,6 +25,7 @@
 namespace mp {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // f32 -> bf16 bits, round to nearest even (ggml_compute_fp32_to_bf16)
@@ -41,7 +42,27 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
     return __builtin_bit_cast(unsigned, v);
 }
 
-template <int NB, int K, int PRO, int EPI>
+// two f32 -> packed f16 pair, round to nearest even (ggml_fp32_to_fp16)
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    const f16x2 v = {(_Float16)a, (_Float16)b};
+    return __builtin_bit_cast(unsigned, v);
+}
+// the 16-bit element type of a weight mode: F16 = true -> f16, else bf16
+template <bool F16>
+__device__ __forceinline__ unsigned pk16(float a, float b) {
+    if constexpr (F16) return pk_f16(a, b);
+    else return pk_bf16(a, b);
+}
+template <bool F16>
+__device__ __forceinline__ floatx4 mfma16(uint4 a, uint4 b, floatx4 c) {
+    if constexpr (F16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+template <int NB, int K, int PRO, int EPI, bool F16 = false>
 __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     static_assert(NB >= 1 && NB <= 16, "one 16-column MFMA tile of utterances");
@@ -72,10 +93,10 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
             uint4 o = make_uint4(0, 0, 0, 0);
             if (b < NB) {
                 const float4 x0 = *(const float4 *)(actf + b * K + k), x1 = *(const float4 *)(actf + b * K + k + 4);
-                o.x = pk_bf16(x0.x, x0.y);
-                o.y = pk_bf16(x0.z, x0.w);
-                o.z = pk_bf16(x1.x, x1.y);
-                o.w = pk_bf16(x1.z, x1.w);
+                o.x = pk16<F16>(x0.x, x0.y);
+                o.y = pk16<F16>(x0.z, x0.w);
+                o.z = pk16<F16>(x1.x, x1.y);
+                o.w = pk16<F16>(x1.z, x1.w);
             }
             *(uint4 *)(actb + b * KP + k) = o;
         }
@@ -118,10 +139,10 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
                 const int e = base + u * MP_BLOCK + tid;
                 if (e < ITEMS) {
                     uint4 o;
-                    o.x = pk_bf16(x0[u].x, x0[u].y);
-                    o.y = pk_bf16(x0[u].z, x0[u].w);
-                    o.z = pk_bf16(x1[u].x, x1[u].y);
-                    o.w = pk_bf16(x1[u].z, x1[u].w);
+                    o.x = pk16<F16>(x0[u].x, x0[u].y);
+                    o.y = pk16<F16>(x0[u].z, x0[u].w);
+                    o.z = pk16<F16>(x1[u].x, x1[u].y);
+                    o.w = pk16<F16>(x1[u].z, x1[u].w);
                     *(uint4 *)(actb + (e / (K / 8)) * KP + (e % (K / 8)) * 8) = o;
                 }
             }
@@ -137,8 +158,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     for (int i = 0; i < KW; ++i) {
         const int kc = w * KW + i;
         const uint4 bv = *(const uint4 *)(brow + kc * 32);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i]), __builtin_bit_cast(bf16x8, bv),
-                                                     acc, 0, 0, 0);
+        acc = mfma16<F16>(a[i], bv, acc);
     }
     part[w][lane] = acc;
     lds_sync();
@@ -168,7 +188,7 @@ static bool b16_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_LTARG_ATTN)
         ok &= p.logits && p.codes_cur && p.qkvtab && p.lk && p.lv && p.ltk && p.ltv && p.step && p.smp.cfg && p.smp.argeos;
     if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) ok &= p.out != nullptr;
-    if constexpr (EPI == EPI_GELU_B16) ok &= p.out_b16 != nullptr;
+    if constexpr (EPI == EPI_GELU_B16 || EPI == EPI_GELU_F16) ok &= p.out_b16 != nullptr;
     if constexpr (EPI == EPI_BIAS) ok &= p.out && p.bias;
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
     if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
@@ -178,10 +198,10 @@ static bool b16_args_ok(const GemvP &p) {
     return ok;
 }
 
-template <int NB, int K, int PRO, int EPI>
+template <int NB, int K, int PRO, int EPI, bool F16 = false>
 static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     if (!b16_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
-    mp::launch((gemm_b16_kernel<NB, K, PRO, EPI>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
+    mp::launch((gemm_b16_kernel<NB, K, PRO, EPI, F16>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
@@ -198,17 +218,46 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     hipError_t b16_lt_d_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTF, PRO_PLAIN, EPI_ADD_STORE>(p, s); } \
     hipError_t b16_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }
 
+#define MP_F16_OPS(NB)                                                                                                  \
+    hipError_t f16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV, true>(p, s); } \
+    hipError_t f16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV, true>(p, s); }             \
+    hipError_t f16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID, true>(p, s); }   \
+    hipError_t f16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_F16, true>(p, s); }     \
+    hipError_t f16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE, true>(p, s); }  \
+    hipError_t f16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV, true>(p, s); }    \
+    hipError_t f16_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_ATTN, EPI_LTX_ADD, true>(p, s); } \
+    hipError_t f16_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE, true>(p, s); } \
+    hipError_t f16_lt_c_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LN, EPI_GELU, true>(p, s); }         \
+    hipError_t f16_lt_d_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTF, PRO_PLAIN, EPI_ADD_STORE, true>(p, s); } \
+    hipError_t f16_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_PLAIN, EPI_BIAS, true>(p, s); }
+
 MP_B16_OPS(1)
 MP_B16_OPS(2)
 MP_B16_OPS(4)
 MP_B16_OPS(8)
 MP_B16_OPS(16)
+MP_F16_OPS(1)
+MP_F16_OPS(2)
+MP_F16_OPS(4)
+MP_F16_OPS(8)
+MP_F16_OPS(16)
+// the LT in_proj of an F16 file is F16 too (the bf16 mode keeps it f32)
+hipError_t f16_lt_in0_1(const GemvP &p, hipStream_t s) { return launch_b16<1, D, PRO_LN, EPI_BIAS, true>(p, s); }
+hipError_t f16_lt_in0_2(const GemvP &p, hipStream_t s) { return launch_b16<2, D, PRO_LN, EPI_BIAS, true>(p, s); }
+hipError_t f16_lt_in0_4(const GemvP &p, hipStream_t s) { return launch_b16<4, D, PRO_LN, EPI_BIAS, true>(p, s); }
+hipError_t f16_lt_in0_8(const GemvP &p, hipStream_t s) { return launch_b16<8, D, PRO_LN, EPI_BIAS, true>(p, s); }
+hipError_t f16_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_b16<16, D, PRO_LN, EPI_BIAS, true>(p, s); }
+hipError_t f16_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_b16<1, D, PRO_PLAIN, EPI_BIAS, true>(p, s); }
 // o_net + residual after lt_pick_kernel (large batches)
 hipError_t b16_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_b16<8, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 hipError_t b16_lt_bo_16(const GemvP &p, hipStream_t s) { return launch_b16<16, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
+hipError_t f16_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_b16<8, LTD, PRO_PLAIN, EPI_ADD_STORE, true>(p, s); }
+hipError_t f16_lt_bo_16(const GemvP &p, hipStream_t s) { return launch_b16<16, LTD, PRO_PLAIN, EPI_ADD_STORE, true>(p, s); }
 
-// f32 [N][K] -> bf16 fragment order [ceil(N/16)][K/32][64][8], rows >= N zero.
-__global__ void pack_b16_kernel(const float *W, int N, int K, unsigned short *out) {
+// f32 [N][K] -> bf16 (F16: f16) fragment order [ceil(N/16)][K/32][64][8], rows >= N
+// zero. f16: round to nearest even; exact for an F16 file's (widened) values.
+template <bool F16>
+__global__ void pack_16_kernel(const float *W, int N, int K, unsigned short *out) {
     const size_t total = (size_t)((N + 15) / 16) * (K / 32) * 64;
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
         const int lane = (int)(e % 64);
@@ -216,13 +265,17 @@ __global__ void pack_b16_kernel(const float *W, int N, int K, unsigned short *ou
         const int kc = (int)(frag % (K / 32)), rt = (int)(frag / (K / 32));
         const int n = rt * 16 + (lane & 15), k0 = kc * 32 + 8 * (lane >> 4);
         unsigned short *o = out + e * 8;
-        for (int j = 0; j < 8; ++j) o[j] = n < N ? f2bf(W[(size_t)n * K + k0 + j]) : (unsigned short)0;
+        for (int j = 0; j < 8; ++j) {
+            const float w = n < N ? W[(size_t)n * K + k0 + j] : 0.f;
+            o[j] = F16 ? __builtin_bit_cast(unsigned short, (_Float16)w) : f2bf(w);
+        }
     }
 }
 
-hipError_t pack_b16(const float *W, int N, int K, unsigned short *out, hipStream_t s) {
+hipError_t pack_b16(const float *W, int N, int K, unsigned short *out, hipStream_t s, bool f16) {
     if (!W || !out || N <= 0 || K % 32) return hipErrorInvalidValue;
-    mp::launch(pack_b16_kernel, dim3(1024), dim3(256), 0, s, W, N, K, out);
+    if (f16) mp::launch(pack_16_kernel<true>, dim3(1024), dim3(256), 0, s, W, N, K, out);
+    else mp::launch(pack_16_kernel<false>, dim3(1024), dim3(256), 0, s, W, N, K, out);
     return hipGetLastError();
 }
 

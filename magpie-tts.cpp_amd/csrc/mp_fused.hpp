@@ -614,6 +614,10 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b,
         const __bf16 h = (__bf16)gelu_tanh(v);  // round to nearest even, as the consumer's staging would
         p.out_b16[(size_t)b * p.out_ld + n] = __builtin_bit_cast(unsigned short, h);
     }
+    else if constexpr (EPI == EPI_GELU_F16) {
+        const _Float16 h = (_Float16)gelu_tanh(v);
+        p.out_b16[(size_t)b * p.out_ld + n] = __builtin_bit_cast(unsigned short, h);
+    }
     else if constexpr (EPI == EPI_RESID) p.resid[(size_t)b * D + n] = v + p.resid[(size_t)b * D + n];
     else if constexpr (EPI == EPI_ADD_STORE) p.out[(size_t)b * p.out_ld + n] = v + p.addsrc[(size_t)b * p.out_ld + n];
     else if constexpr (EPI == EPI_LTX_ADD) p.out[(size_t)b * p.out_ld + n] = v + extra;  // extra = X[b][n]

@@ -1,7 +1,8 @@
 // Host-side GGUF v3 reader (ggml-free). Replaces the reference's use of
 // gguf_init_from_file / gguf_find_key / gguf_get_tensor_* (magpie.cpp:73-121,
 // 674-718; nano-codec.cpp:205-333). mmap-based; tensors are converted to f32 on
-// demand (F32 / F16 / BF16 / Q8_0; Q8_0 block = fp16 d + 32 x int8,
+// demand (F32 / F16 / BF16 / Q8_0 / Q4_0; Q8_0 block = fp16 d + 32 x int8, Q4_0 block =
+// fp16 d + 16 bytes of nibbles;
 // scripts/convert_magpie_to_gguf.py:79-104).
 #pragma once
 #include <fcntl.h>
@@ -121,6 +122,7 @@ public:
         case 1: return (uint64_t)n * 2;            // F16
         case 30: return (uint64_t)n * 2;           // BF16
         case 8: return (uint64_t)(n / 32) * 34;    // Q8_0
+        case 2: return (uint64_t)(n / 32) * 18;    // Q4_0
         default: return 0;
         }
     }
@@ -145,6 +147,17 @@ public:
                 uint16_t h; memcpy(&h, blk, 2);
                 const float d = half_to_float(h);
                 for (int i = 0; i < 32; ++i) out[b * 32 + i] = (float)(int8_t)blk[2 + i] * d;
+            }
+            return true;
+        case 2:  // Q4_0 (dequantize_row_q4_0): byte j holds q_j (low nibble) and q_{j+16}
+            for (int64_t b = 0; b < n / 32; ++b) {
+                const uint8_t *blk = src + b * 18;
+                uint16_t h; memcpy(&h, blk, 2);
+                const float d = half_to_float(h);
+                for (int j = 0; j < 16; ++j) {
+                    out[b * 32 + j] = (float)((int)(blk[2 + j] & 0x0F) - 8) * d;
+                    out[b * 32 + j + 16] = (float)((int)(blk[2 + j] >> 4) - 8) * d;
+                }
             }
             return true;
         }

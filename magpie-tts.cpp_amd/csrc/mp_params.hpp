@@ -57,6 +57,7 @@ enum Epi {
     EPI_GELU_B16 = 7,   // out_b16 = bf16(gelu(v)): the bf16 FFN-down operand, rounded once here
     EPI_LTX_ADD = 8,    // out = v + (P[cb-1][code] + lt_pos[cb]): LT residual of PRO_LTARG_ATTN's code
     EPI_LTKVO = 9,      // f32 LT position 0: rows [0,256) k_0 -> lk[b][0], rows [256,512) vo_0 -> lv[b][0]
+    EPI_GELU_F16 = 11,  // out_b16 = f16(gelu(v)): EPI_GELU_B16 for the F16 weight mode
     EPI_RESID_XA = 10,  // resid += v, each new x1 value also published as a tagged granule; the
                         // launch's last XA_SPLITS x NB workgroups run the fused XA on it (below)
 };
@@ -150,6 +151,7 @@ struct XaP {
     const float *kp, *vp;  // K', V': [B][L][Tmax][768]
     const int *T;
     int Tmax, layer, nlayers;
+    int q_f16;             // F16 weight mode: LN(x) rounded to f16, the q_net operand ggml multiplies
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 

@@ -99,6 +99,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
                     }
                 }
             }
+            if (p.xround)  // F16 weights: the operand ggml's F16 mul_mat multiplies (uniform branch)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[e] = (float)(_Float16)a[e];
 #pragma unroll
             for (int e = 0; e < 4; ++e) As[lk + e][lr] = a[e];
         }
@@ -318,7 +321,7 @@ __global__ void embed_context_kernel(const int *spk, const float *baked, const f
 // LT table rows (see pre_lt_tab_rows): one 256-thread block per row, the
 // block statistics PRO_LTARG_ATTN's per-wave statistics reproduce
 __global__ __launch_bounds__(256) void lt_tab_rows_kernel(const float *P, const float *lt_pos, const float *w, float eps,
-                                                          float *Y, int b16) {
+                                                          float *Y, int round) {
     __shared__ float red[8];
     const int r = blockIdx.x, k = threadIdx.x, cb = r / VCB + 1;
     const float X = P[(size_t)r * LTD + k] + lt_pos[(size_t)cb * LTD + k];
@@ -327,7 +330,8 @@ __global__ __launch_bounds__(256) void lt_tab_rows_kernel(const float *P, const 
     block_meanvar<1>(xv, red, mean, var);
     const float rstd = 1.0f / sqrtf(var + eps);
     float y = ((X - mean) * rstd) * w[k];
-    if (b16) y = (float)(__bf16)y;
+    if (round == 1) y = (float)(__bf16)y;
+    else if (round == 2) y = (float)(_Float16)y;
     Y[(size_t)r * LTD + k] = y;
 }
 __global__ void round_bf16_kernel(const float *src, float *dst, size_t n) {
@@ -393,9 +397,9 @@ hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ld
     hipLaunchKernelGGL(ln_rows_kernel, dim3(M), dim3(256), 0, s, X, ldx, w, Y, ldy, eps);
     return hipGetLastError();
 }
-hipError_t pre_lt_tab_rows(const float *P, const float *lt_pos, const float *w, float eps, float *Y, bool b16,
+hipError_t pre_lt_tab_rows(const float *P, const float *lt_pos, const float *w, float eps, float *Y, int round,
                            hipStream_t s) {
-    hipLaunchKernelGGL(lt_tab_rows_kernel, dim3(7 * VCB), dim3(256), 0, s, P, lt_pos, w, eps, Y, (int)b16);
+    hipLaunchKernelGGL(lt_tab_rows_kernel, dim3(7 * VCB), dim3(256), 0, s, P, lt_pos, w, eps, Y, round);
     return hipGetLastError();
 }
 hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s) {

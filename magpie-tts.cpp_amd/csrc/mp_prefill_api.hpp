@@ -37,6 +37,8 @@ struct GemmP {
     // depend on M, i.e. on the batch), each written raw to part[s][M][N], then
     // summed in split order by a second launch that applies the epilogue.
     float *part;
+    int xround;        // 2: round every A element to f16 as it is loaded (an F16 weight: ggml's
+                       //    F16 mul_mat rounds src1 to f16; products then exact in f32)
 };
 
 // Split count of a preamble GEMM over K (fixed per K: batch-invariant results).
@@ -73,7 +75,8 @@ hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s);
 hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ldy, int M, float eps, hipStream_t s);
 // LT table rows: Y[r] = LN(P[r] + lt_pos[r / VCB + 1]) * w for r < 7 * VCB (the LN of
 // PRO_LTARG_ATTN's position, bit for bit), rounded to bf16 when `b16`
-hipError_t pre_lt_tab_rows(const float *P, const float *lt_pos, const float *w, float eps, float *Y, bool b16,
+// round: 0 none, 1 bf16, 2 f16 (the rows' operand precision in that weight mode)
+hipError_t pre_lt_tab_rows(const float *P, const float *lt_pos, const float *w, float eps, float *Y, int round,
                            hipStream_t s);
 // dst = bf16(src) held as f32 (a bf16-mode weight for an f32 GEMM)
 hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s);

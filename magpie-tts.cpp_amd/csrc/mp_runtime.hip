@@ -56,7 +56,22 @@ MP_DECL_B16(2)
 MP_DECL_B16(4)
 MP_DECL_B16(8)
 MP_DECL_B16(16)
-hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t);
+#define MP_DECL_F16(NB)                                                                                      \
+    hipError_t f16_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t f16_qkv_##NB(const GemvP &, hipStream_t);      \
+    hipError_t f16_oproj_##NB(const GemvP &, hipStream_t); hipError_t f16_ff1_##NB(const GemvP &, hipStream_t);          \
+    hipError_t f16_ff2_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_a_##NB(const GemvP &, hipStream_t);           \
+    hipError_t f16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_b_##NB(const GemvP &, hipStream_t);         \
+    hipError_t f16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_d_##NB(const GemvP &, hipStream_t);          \
+    hipError_t f16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_in0_##NB(const GemvP &, hipStream_t);
+MP_DECL_F16(1)
+MP_DECL_F16(2)
+MP_DECL_F16(4)
+MP_DECL_F16(8)
+MP_DECL_F16(16)
+hipError_t f16_lt_inh_1(const GemvP &, hipStream_t);
+hipError_t f16_lt_bo_8(const GemvP &, hipStream_t);
+hipError_t f16_lt_bo_16(const GemvP &, hipStream_t);
+hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t, bool f16);
 #define MP_DECL_Q8(NB)                                                                                       \
     hipError_t q8_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t q8_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t q8_oproj_##NB(const GemvP &, hipStream_t); hipError_t q8_xq_##NB(const GemvP &, hipStream_t);             \
@@ -104,13 +119,25 @@ static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TAB
                            b16_lt_d_##NB, b16_lt_e_##NB, nullptr }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
+// F16 weight mode (an F16 GGUF): the same MFMA family on f16, the LT in_proj included
+#define MP_TABLE_F16(NB) { f16_qkv_embed_##NB, f16_qkv_##NB, f16_oproj_##NB, nullptr, f16_ff1_##NB, f16_ff2_##NB, \
+                           f16_lt_in0_##NB, f16_lt_a_##NB, f16_lt_bg_##NB, f16_lt_b_##NB, f16_lt_c_##NB,  \
+                           f16_lt_d_##NB, f16_lt_e_##NB, nullptr }
+static const OpTable kTablesF16[5] = {MP_TABLE_F16(1), MP_TABLE_F16(2), MP_TABLE_F16(4), MP_TABLE_F16(8),
+                                      MP_TABLE_F16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
 struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, lt_in0, lt_a, lt_bg, lt_b, lt_e; };
 #define MP_TABLE_Q8(NB) { q8_qkv_embed_##NB, q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_lt_in0_##NB, \
                           q8_lt_a_##NB, q8_lt_bg_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
 static const OpTableQ8 kTablesQ8[4] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8)};
 static int nb_index(int NB) { return NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : NB == 8 ? 3 : 4; }
-static const OpTable &table_for(int NB, bool b16) { return b16 ? kTablesB16[nb_index(NB)] : kTables[nb_index(NB)]; }
+// the 16-bit MFMA family serves the bf16 and F16 weight modes
+static bool h16_mode(int weight_mode) { return weight_mode == MP_WEIGHTS_BF16 || weight_mode == MP_WEIGHTS_F16; }
+static const OpTable &table_for(int NB, int weight_mode) {
+    return weight_mode == MP_WEIGHTS_F16 ? kTablesF16[nb_index(NB)]
+           : weight_mode == MP_WEIGHTS_BF16 ? kTablesB16[nb_index(NB)]
+                                            : kTables[nb_index(NB)];
+}
 static const OpTableQ8 &table_q8(int NB) { return kTablesQ8[nb_index(NB) < 4 ? nb_index(NB) : 3]; }
 
 // A Q8_0 tensor as stored (weight mode MP_WEIGHTS_Q8): int8 [N][K] + fp16 scales [N][K/32]
@@ -147,7 +174,8 @@ struct Model {
     unsigned short *pk_arena = nullptr;
     std::vector<const unsigned short *> pk_qkv, pk_o, pk_ff1, pk_ff2;
     const unsigned short *pk_lt_qkv = nullptr, *pk_lt_o = nullptr, *pk_lt_ff1 = nullptr, *pk_lt_ff2 = nullptr,
-                         *pk_lt_out = nullptr;  // lt_out: [8][127 tiles][8][64][8]
+                         *pk_lt_out = nullptr,  // lt_out: [8][127 tiles][8][64][8]
+                         *pk_lt_in = nullptr;   // F16 mode only: the LT in_proj [256][768]
     // weight mode MP_WEIGHTS_Q8: the file's Q8_0 tensors as stored (ggml's quantised mul_mat)
     void *q8_arena = nullptr;
     size_t q8_bytes = 0;
@@ -278,19 +306,21 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 // Size (elements) of one packed [N][K] matrix: [ceil(N/16)][K/32][64][8].
 size_t pk_elems(int N, int K) { return (size_t)((N + 15) / 16) * 16 * K; }
 
-int pack_weights(mp_dev *dev) {
+// bf16 weight mode: the f32 weights rounded to bf16 fragments; F16 mode (an F16
+// file): its f16 values (widened exactly at load) repacked as f16 fragments.
+int pack_weights(mp_dev *dev, bool f16) {
     mp::Model &m = dev->m;
     if (m.pk_arena) { hipFree(m.pk_arena); m.pk_arena = nullptr; }
     const int L = m.dec_layers;
     const size_t per_layer = pk_elems(2304, 768) + pk_elems(768, 768) + pk_elems(3072, 768) + pk_elems(768, 3072);
     const size_t lt = pk_elems(768, 256) + pk_elems(256, 256) + pk_elems(1024, 256) + pk_elems(256, 1024) +
-                      8 * pk_elems(2024, 256);
+                      8 * pk_elems(2024, 256) + (f16 ? pk_elems(256, 768) : 0);
     HIPCHK(hipMalloc(&m.pk_arena, (per_layer * L + lt) * 2));
     unsigned short *cur = m.pk_arena;
     auto pack = [&](const float *W, int N, int K) -> const unsigned short * {
         unsigned short *dst = cur;
         cur += pk_elems(N, K);
-        return mp::pack_b16(W, N, K, dst, dev->stream) == hipSuccess ? dst : nullptr;
+        return mp::pack_b16(W, N, K, dst, dev->stream, f16) == hipSuccess ? dst : nullptr;
     };
     m.pk_qkv.assign(L, nullptr); m.pk_o.assign(L, nullptr); m.pk_ff1.assign(L, nullptr); m.pk_ff2.assign(L, nullptr);
     for (int l = 0; l < L; ++l) {
@@ -308,6 +338,8 @@ int pack_weights(mp_dev *dev) {
     for (int c = 0; c < 8; ++c)
         if (!pack(m.lt_out_w + (size_t)c * 2024 * 256, 2024, 256)) return fail(dev, MP_ERR_HIP, "bf16 pack failed");
     if (!m.pk_lt_qkv || !m.pk_lt_o || !m.pk_lt_ff1 || !m.pk_lt_ff2) return fail(dev, MP_ERR_HIP, "bf16 pack failed");
+    m.pk_lt_in = f16 ? pack(m.lt_in_w, 256, 768) : nullptr;
+    if (f16 && !m.pk_lt_in) return fail(dev, MP_ERR_HIP, "f16 pack failed");
     HIPCHK(hipStreamSynchronize(dev->stream));
     return MP_OK;
 }
@@ -513,18 +545,20 @@ int build_ptab(mp_dev *dev, int weight_mode) {
     mp::GemmP gp{};
     gp.A = m.audio_emb; gp.lda = 768; gp.W = m.lt_in_w; gp.Wq = m.lt_in8.q; gp.Wd = m.lt_in8.d; gp.bias = m.lt_in_b;
     gp.C = m.lt_ptab; gp.ldc = 256; gp.M = 8 * 2024; gp.N = 256; gp.K = 768; gp.rows_per_utt = 8 * 2024;
+    gp.xround = weight_mode == MP_WEIGHTS_F16 ? 2 : 0;  // F16 in_proj: the embedding row rounded to f16
     HIPCHK(mp::pre_gemm(gp, mp::GE_STORE, dev->stream));
     // LT q|k|v of position c+1 for every code v of codebook c < 7: the rows PRO_LTARG_ATTN
     // gathers instead of running the q|k|v GEMV per codebook. The projection uses the
     // weights the decode-time GEMV would (f32, Q8_0 with activations quantised per
-    // block, or bf16 weights and bf16 activations, f32 accumulation).
+    // block, or bf16 / f16 weights and activations, f32 accumulation).
     if (m.lt_qkvtab) { hipFree(m.lt_qkvtab); m.lt_qkvtab = nullptr; }
     const size_t R = (size_t)7 * 2024;
     HIPCHK(hipMalloc(&m.lt_qkvtab, R * 768 * 4));
     float *rows = nullptr, *wq = nullptr;
     HIPCHK(hipMalloc(&rows, R * 256 * 4));
-    const bool b16 = weight_mode == MP_WEIGHTS_BF16;
-    HIPCHK(mp::pre_lt_tab_rows(m.lt_ptab, m.lt_pos, m.lt_norm_self, m.eps, rows, b16, dev->stream));
+    const bool b16 = weight_mode == MP_WEIGHTS_BF16;  // F16: the file's weights are already f16 values
+    HIPCHK(mp::pre_lt_tab_rows(m.lt_ptab, m.lt_pos, m.lt_norm_self, m.eps, rows,
+                               b16 ? 1 : weight_mode == MP_WEIGHTS_F16 ? 2 : 0, dev->stream));
     if (b16) {
         HIPCHK(hipMalloc(&wq, (size_t)768 * 256 * 4));
         HIPCHK(mp::pre_round_bf16(m.lt_qkv, wq, (size_t)768 * 256, dev->stream));
@@ -541,10 +575,14 @@ int build_ptab(mp_dev *dev, int weight_mode) {
     return f32_lt_mode(m) ? build_vo_tables(dev) : MP_OK;
 }
 
-// Weight mode MP_WEIGHTS_Q8: upload every Q8_0 tensor the decode path uses as
-// stored (scripts/convert_magpie_to_gguf.py:155-176 decides which: attention,
+// Weight mode MP_WEIGHTS_Q8: upload every block-quantised tensor the decode path
+// uses (scripts/convert_magpie_to_gguf.py:155-176 decides which: attention,
 // cross-attention and LT projections), repacked to int8 [N][K] + fp16 scales
-// [N][K/32] (34 B per 32 weights, as in the file). F32 tensors keep the f32 path.
+// [N][K/32] (34 B per 32 weights). Q8_0 blocks are copied; Q4_0 blocks
+// (convert_magpie_to_gguf.py:107-138: q in 0..15, byte j = q_j | q_{j+16} << 4) become
+// the int8 values q - 8 with the same scale, so the Q8_0 kernels compute exactly
+// ggml's vec_dot_q4_0_q8_0: the integer dot of (q - 8) with the Q8_0-quantised
+// activation times d_w * d_a. F32 tensors keep the f32 path.
 int load_q8(mp_dev *dev, const char *path) {
     mp::Gguf g;
     std::string err;
@@ -554,7 +592,7 @@ int load_q8(mp_dev *dev, const char *path) {
     std::vector<Item> items;
     auto want = [&](const std::string &name, mp::QW *dst) {
         const mp::GgufTensor *t = g.find(name);
-        if (t && t->type == 8 && t->ne[0] % 32 == 0) items.push_back({t, dst, -1});
+        if (t && (t->type == 8 || t->type == 2) && t->ne[0] % 32 == 0) items.push_back({t, dst, -1});
     };
     for (int l = 0; l < m.enc_layers; ++l) {
         const std::string p = "encoder.layers." + std::to_string(l) + ".self_attention.";
@@ -575,10 +613,10 @@ int load_q8(mp_dev *dev, const char *path) {
     int nout = 0;
     for (int c = 0; c < 8; ++c) {
         const mp::GgufTensor *t = g.find("local_transformer_out_projections." + std::to_string(c) + ".weight");
-        if (t && t->type == 8) { items.push_back({t, &m.lt_out8, c}); ++nout; }
+        if (t && (t->type == 8 || t->type == 2)) { items.push_back({t, &m.lt_out8, c}); ++nout; }
     }
-    if (nout != 0 && nout != 8) return fail(dev, MP_ERR_UNSUPPORTED, "mixed Q8_0/F32 LT output projections");
-    if (items.empty()) return fail(dev, MP_ERR_UNSUPPORTED, "Q8 weight mode needs a GGUF with Q8_0 tensors");
+    if (nout != 0 && nout != 8) return fail(dev, MP_ERR_UNSUPPORTED, "mixed quantised/F32 LT output projections");
+    if (items.empty()) return fail(dev, MP_ERR_UNSUPPORTED, "Q8 weight mode needs a GGUF with Q8_0 or Q4_0 tensors");
     // the reassociated XA (K' = K W_q, V' = W_o V) is an f32 identity: with Q8_0
     // q_net / o_net the activations must be quantised where ggml quantises them
     for (int l = 0; l < m.dec_layers; ++l)
@@ -605,8 +643,17 @@ int load_q8(mp_dev *dev, const char *path) {
         hq.resize(n);
         hd.resize(n / 32);
         for (size_t b = 0; b < n / 32; ++b) {
-            memcpy(&hd[b], src + b * 34, 2);
-            memcpy(&hq[b * 32], src + b * 34 + 2, 32);
+            if (it.t->type == 8) {
+                memcpy(&hd[b], src + b * 34, 2);
+                memcpy(&hq[b * 32], src + b * 34 + 2, 32);
+            } else {  // Q4_0
+                const uint8_t *blk = src + b * 18;
+                memcpy(&hd[b], blk, 2);
+                for (int j = 0; j < 16; ++j) {
+                    hq[b * 32 + j] = (signed char)((blk[2 + j] & 0x0F) - 8);
+                    hq[b * 32 + j + 16] = (signed char)((blk[2 + j] >> 4) - 8);
+                }
+            }
         }
         signed char *dq;
         unsigned short *dd;
@@ -699,8 +746,8 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
 int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     const mp::Model &m = dev->m;
     const int NB = dev->NB, L = m.dec_layers;
-    const bool b16 = m.weight_mode == MP_WEIGHTS_BF16;
-    const mp::OpTable &tb = mp::table_for(NB, b16);
+    const bool b16 = mp::h16_mode(m.weight_mode);  // 16-bit MFMA family (bf16 or F16 weights)
+    const mp::OpTable &tb = mp::table_for(NB, m.weight_mode);
     const mp::OpTableQ8 &tq = mp::table_q8(NB);
     // algorithmic bytes: weights at their stored width (Q8_0: 34 B per 32), activations f32
     const double F = b16 ? 2.0 : 4.0, Fq = 34.0 / 32.0, A = 4.0, act = (double)NB;
@@ -755,7 +802,8 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.part = dev->sa_part;
         g.Wq = W.o8.q; g.Wd = W.o8.d;
-        const mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
+        mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
+        xp.q_f16 = m.weight_mode == MP_WEIGHTS_F16;
         const double xa_bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
         const bool xa_in_oproj = tb.oproj_xa && !W.o8 && !W.xq8;
         if (xa_in_oproj) {
@@ -800,7 +848,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
         } else {      // x2 = x + merged XA split states, stored by block 0 for the FFN residual
             g.src = dev->x; g.src_ld = 768; g.part = dev->xa_part; g.xres = dev->x2;
-            if (b16) g.out_b16 = dev->h_b16;  // GELU output stored bf16 (what FFN down rounds it to)
+            if (b16) g.out_b16 = dev->h_b16;  // GELU output stored bf16 / f16 (what FFN down rounds it to)
             if ((rc = run("ff1", tb.ff1x, g,
                           F * (3072.0 * 768) + A * act * (768 * 2 + 3072 + mp::XA_SPLITS * mp::XA_PART))) != MP_OK)
                 return rc;
@@ -852,8 +900,8 @@ void dump_lt(const mp::LtIo &io, hipStream_t s) {
 
 int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vector<mp::OpRec> *ops) {
     const mp::Model &m = dev->m;
-    const bool b16 = m.weight_mode == MP_WEIGHTS_BF16;
-    const mp::OpTable &tb = mp::table_for(NB, b16);
+    const bool b16 = mp::h16_mode(m.weight_mode);
+    const mp::OpTable &tb = mp::table_for(NB, m.weight_mode);
     const mp::OpTableQ8 &tq = mp::table_q8(NB);
     const double F = b16 ? 2.0 : 4.0, Fq = 34.0 / 32.0, A = 4.0, act = (double)NB;
     auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
@@ -882,12 +930,12 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     {
         mp::GemvP g = base();
         g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.out = io.lt_s; g.out_ld = 9 * 256;
-        g.Wq = m.lt_in8.q; g.Wd = m.lt_in8.d;
-        const double Fi = m.lt_in8 ? Fq : A;
+        g.Wq = m.lt_in8.q; g.Wd = m.lt_in8.d; g.Wb = m.pk_lt_in;  // pk_lt_in: F16 mode only
+        const double Fi = m.lt_in8 ? Fq : m.pk_lt_in ? 2.0 : A;
         if (io.lt_only) {
             // in_proj of the caller's (already normalised) hidden (1161-1163)
             g.src = io.hidden; g.src_ld = 768;
-            if ((rc = run("lt_inh", m.lt_in8 ? mp::q8_lt_inh_1 : mp::op_lt_inh_1, g,
+            if ((rc = run("lt_inh", m.lt_in8 ? mp::q8_lt_inh_1 : m.pk_lt_in ? mp::f16_lt_inh_1 : mp::op_lt_inh_1, g,
                           Fi * 256.0 * 768 + A * 256 + A * (768 + 256))) != MP_OK)
                 return rc;
         } else {
@@ -987,8 +1035,11 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             g = base(); g.cb = cb;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.src = io.ltq; g.src_ld = 256; g.out = io.ltY; g.out_ld = 256;
             g.addsrc = io.ltX; g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
-            const mp::GemvFn bo = m.lt_o8 ? mp::q8_lt_bo_8 : b16 ? (NB == 16 ? mp::b16_lt_bo_16 : mp::b16_lt_bo_8)
-                                                                : mp::op_lt_bo_8;
+            const bool f16 = m.weight_mode == MP_WEIGHTS_F16;
+            const mp::GemvFn bo = m.lt_o8 ? mp::q8_lt_bo_8
+                                  : f16   ? (NB == 16 ? mp::f16_lt_bo_16 : mp::f16_lt_bo_8)
+                                  : b16   ? (NB == 16 ? mp::b16_lt_bo_16 : mp::b16_lt_bo_8)
+                                          : mp::op_lt_bo_8;
             if ((rc = run("lt_bo", bo, g, (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * (256 * 3))) != MP_OK) return rc;
         } else {
             // position cb: codebook cb-1's pick, its q|k|v row gathered from the load-time
@@ -1072,8 +1123,12 @@ int run_preamble(mp_dev *dev) {
     hipStream_t s = dev->stream;
     const int Me = NB * Tmax;
     // every preamble GEMM runs split-K over K (deterministic, batch-invariant)
+    // F16 file: every projection's operand rounded to f16 as ggml's F16 mul_mat does
+    // (the K'/V' precompute below is weight algebra, not a mul_mat of the file)
+    const int xr = m.weight_mode == MP_WEIGHTS_F16 ? 2 : 0;
     auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) {
         gp.part = dev->gpart;
+        gp.xround = gp.xround < 0 ? 0 : xr;  // -1: opted out
         return mp::pre_gemm(gp, epi, st);
     };
     // --- text encoder (magpie_build_full_encoder, 1960-1995)
@@ -1122,6 +1177,7 @@ int run_preamble(mp_dev *dev) {
             GemmP gp{};
             gp.A = dev->xak + xo; gp.lda = 128; gp.W = m.xq_t[l]; gp.C = dev->kp + po; gp.ldc = 768;
             gp.M = Tmax; gp.N = 768; gp.K = 128; gp.rows_per_utt = Tmax;
+            gp.xround = -1;
             HIPCHK(pre_gemm(gp, GE_STORE, s));
             gp.A = dev->xav + xo; gp.W = m.dec[l].xo; gp.C = dev->vp + po;
             HIPCHK(pre_gemm(gp, GE_STORE, s));
@@ -1199,7 +1255,8 @@ int mp_hip_init(int device, mp_dev **out) {
 
 int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     if (!dev || !path) return MP_ERR_ARG;
-    if (weight_mode != MP_WEIGHTS_AS_STORED && weight_mode != MP_WEIGHTS_BF16 && weight_mode != MP_WEIGHTS_Q8)
+    if (weight_mode != MP_WEIGHTS_AS_STORED && weight_mode != MP_WEIGHTS_BF16 && weight_mode != MP_WEIGHTS_Q8 &&
+        weight_mode != MP_WEIGHTS_F16)
         return fail(dev, MP_ERR_ARG, "unknown weight mode");
     HIPCHK(hipSetDevice(dev->device));
     free_batch(dev);
@@ -1208,17 +1265,31 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     // drop the Q8_0 views of a previous model
     if (dev->m.q8_arena) { hipFree(dev->m.q8_arena); dev->m.q8_arena = nullptr; dev->m.q8_bytes = 0; }
     dev->m.lt_in8 = dev->m.lt_qkv8 = dev->m.lt_o8 = dev->m.lt_out8 = mp::QW{};
-    if (weight_mode == MP_WEIGHTS_Q8) {  // cheap header check before any upload
+    dev->m.pk_lt_in = nullptr;  // set again by an F16 load
+    if (weight_mode == MP_WEIGHTS_Q8 || weight_mode == MP_WEIGHTS_F16) {  // cheap header check before any upload
         mp::Gguf g;
         std::string err;
         if (!g.open(path, err)) return fail(dev, MP_ERR_IO, err);
         const mp::GgufTensor *t = g.find("decoder.layers.0.self_attention.qkv_net.weight");
-        if (!t || t->type != 8) return fail(dev, MP_ERR_UNSUPPORTED, "Q8 weight mode needs a GGUF with Q8_0 tensors");
+        if (weight_mode == MP_WEIGHTS_Q8 && (!t || (t->type != 8 && t->type != 2)))
+            return fail(dev, MP_ERR_UNSUPPORTED, "Q8 weight mode needs a GGUF with Q8_0 or Q4_0 tensors");
+        // every tensor the F16 mode streams as f16 must be stored F16 (the converter's
+        // pattern set, convert_magpie_to_gguf.py:155-176, 311-327)
+        if (weight_mode == MP_WEIGHTS_F16)
+            for (const auto &kv : g.tensors()) {
+                const std::string &n = kv.first;
+                const bool proj = n.find(".self_attention.") != std::string::npos ||
+                                  n.find(".pos_ff.") != std::string::npos ||
+                                  n.find("local_transformer_out_projections.") == 0 ||
+                                  n == "local_transformer_in_projection.weight";
+                if (proj && n.size() > 7 && n.compare(n.size() - 7, 7, ".weight") == 0 && kv.second.type != 1)
+                    return fail(dev, MP_ERR_UNSUPPORTED, "F16 weight mode needs a GGUF with F16 projections (" + n + ")");
+            }
     }
     if (int rc = load_model(dev, path)) return rc;
     dev->loaded = false;
-    if (weight_mode == MP_WEIGHTS_BF16) {
-        if (int rc = pack_weights(dev)) return rc;
+    if (weight_mode == MP_WEIGHTS_BF16 || weight_mode == MP_WEIGHTS_F16) {
+        if (int rc = pack_weights(dev, weight_mode == MP_WEIGHTS_F16)) return rc;
     } else if (weight_mode == MP_WEIGHTS_Q8) {
         if (int rc = load_q8(dev, path)) return rc;
     }
@@ -1268,7 +1339,7 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
                        int tmax, const mp_params *params) {
     if (!dev) return MP_ERR_ARG;
     if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
-    const int bmax = dev->m.weight_mode == MP_WEIGHTS_BF16 ? 16 : 8;
+    const int bmax = mp::h16_mode(dev->m.weight_mode) ? 16 : 8;
     if (!tokens || !n_tokens || !speaker || B < 1 || B > bmax || tmax < 1 || !params)
         return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..8, 1..16 with bf16 weights)");
     if (params->temperature >= 0.01f && (params->top_k < 1 || params->top_k > mp::VCB))

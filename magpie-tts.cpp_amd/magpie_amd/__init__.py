@@ -168,13 +168,16 @@ class SynthResult:
 class Device:
     """One GPU with resident Magpie weights (magpie_init_with_backend, magpie.cpp:781)."""
 
-    WEIGHT_MODES = {"f32": 0, "as_stored": 0, "bf16": 1, "q8": 2}
+    WEIGHT_MODES = {"f32": 0, "as_stored": 0, "bf16": 1, "q8": 2, "q4": 2, "f16": 3}
 
     def __init__(self, model_path: str, device: int = 0, weights: str = "f32"):
         """weights: "f32" (as stored, widened to f32), "bf16" (decode projections
-        on bf16 MFMA, activations rounded to bf16; batches up to 16) or "q8" (the
-        file's Q8_0 tensors kept int8, multiplied with ggml's Q8_0 semantics:
-        activations quantised to Q8_0 per 32-block; batches up to 8)."""
+        on bf16 MFMA, activations rounded to bf16; batches up to 16) or "q8" / "q4"
+        (the file's Q8_0 / Q4_0 tensors kept as int8 (Q4_0: q - 8, losslessly),
+        multiplied with ggml's semantics: activations quantised to Q8_0 per
+        32-block, integer dots scaled by d_w * d_a; batches up to 8) or "f16" (an
+        F16 file with ggml's F16 mul_mat semantics: activations rounded to f16,
+        decode projections on f16 MFMA; batches up to 16)."""
         if weights not in self.WEIGHT_MODES:
             raise ValueError(f"weights must be one of {sorted(self.WEIGHT_MODES)}")
         self.lib = load_library()

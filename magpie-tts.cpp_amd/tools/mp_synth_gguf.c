@@ -9,7 +9,7 @@
 // `name` depends only on (seed, name, i), so the GPU box regenerates identical
 // bytes from the seed instead of shipping ~1 GB of weights.
 //
-// usage: mp_synth_gguf magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|f16]
+// usage: mp_synth_gguf magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|q4_0|f16]
 //                      [--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V]
 //                      [--lt-head-scale K]  (LT output head weights N(0, (0.02 K)^2): decisive logits)
 #include <math.h>
@@ -18,7 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { T_F32 = 0, T_F16 = 1, T_Q8_0 = 8 };
+enum { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q8_0 = 8 };
 enum { KV_U32 = 4, KV_F32 = 6, KV_STR = 8 };
 
 static uint64_t g_seed = 0x4D414750ull;  // "MAGP"
@@ -107,6 +107,7 @@ static int64_t nel(const tdesc *t) { int64_t n = 1; for (int i = 0; i < t->n_dim
 static uint64_t nbytes(const tdesc *t) {
     int64_t n = nel(t);
     if (t->type == T_Q8_0) return (uint64_t)(n / 32) * 34u;
+    if (t->type == T_Q4_0) return (uint64_t)(n / 32) * 18u;
     if (t->type == T_F16) return (uint64_t)n * 2u;
     return (uint64_t)n * 4u;
 }
@@ -160,6 +161,27 @@ static void quant_q8_0(const float *x, int64_t n, uint8_t *out) {
     }
 }
 
+// Q4_0 exactly as scripts/convert_magpie_to_gguf.py:107-138 (numpy): fp16 scale =
+// amax/7, q = clip(round-half-even(x / f32(scale)), -8, 7) + 8, byte j = q_j | q_{j+16} << 4.
+static void quant_q4_0(const float *x, int64_t n, uint8_t *out) {
+    for (int64_t b = 0; b < n / 32; ++b) {
+        const float *blk = x + b * 32;
+        float amax = 0.f;
+        for (int i = 0; i < 32; ++i) { float a = fabsf(blk[i]); if (a > amax) amax = a; }
+        uint16_t hs = f32_to_f16(amax != 0.f ? amax / 7.0f : 0.f);
+        float s = f16_to_f32(hs);
+        uint8_t *o = out + b * 18, qv[32];
+        memcpy(o, &hs, 2);
+        for (int i = 0; i < 32; ++i) {
+            int q = 0;
+            if (s != 0.f) q = (int)nearbyintf(blk[i] / s);
+            q = q < -8 ? -8 : q > 7 ? 7 : q;
+            qv[i] = (uint8_t)(q + 8);
+        }
+        for (int j = 0; j < 16; ++j) o[2 + j] = (uint8_t)((qv[j] & 0x0F) | (qv[j + 16] << 4));
+    }
+}
+
 static int should_q8(const char *name) {
     // scripts/convert_magpie_to_gguf.py:155-176 default patterns
     if (strstr(name, ".self_attention.qkv_net.weight") || strstr(name, ".self_attention.o_net.weight")) return 1;
@@ -169,6 +191,12 @@ static int should_q8(const char *name) {
     if (!strncmp(name, "local_transformer_out_projections.", 34) && strstr(name, ".weight")) return 1;
     if (!strcmp(name, "local_transformer_in_projection.weight")) return 1;
     return 0;  // pos_ff conv weights: inner dim 1 or 3 < 32 -> stay F32 (convert_magpie_to_gguf.py:311-320)
+}
+// F16 (convert_magpie_to_gguf.py:155-176, 311-322): the same pattern set plus the
+// pos_ff conv weights (F16 has no block constraint), tensors of >= 256 elements
+static int should_f16(const char *name) {
+    if (strstr(name, ".pos_ff.proj.conv.weight") || strstr(name, ".pos_ff.o_net.conv.weight")) return 1;
+    return should_q8(name);
 }
 
 // ---------------------------------------------------------------- plans
@@ -225,8 +253,9 @@ static void plan_magpie(int dtype, int dec_layers, int enc_layers, int dec_pos) 
         add(nm, 1, 2024, 1, 1, T_F32, I_NORMAL, S, 0);
     }
     for (int i = 0; i < g_nt; ++i) {
-        if (dtype == T_Q8_0 && should_q8(g_t[i].name) && nel(&g_t[i]) % 32 == 0) g_t[i].type = T_Q8_0;
-        if (dtype == T_F16 && g_t[i].n_dims >= 2) g_t[i].type = T_F16;
+        if ((dtype == T_Q8_0 || dtype == T_Q4_0) && should_q8(g_t[i].name) && nel(&g_t[i]) % 32 == 0)
+            g_t[i].type = dtype;
+        if (dtype == T_F16 && g_t[i].n_dims >= 2 && nel(&g_t[i]) >= 256 && should_f16(g_t[i].name)) g_t[i].type = T_F16;
     }
     // keys written by the converter (convert_magpie_to_gguf.py:207-230)
     kv_str("general.architecture", "magpie-tts");
@@ -356,7 +385,7 @@ static void plan_codec(void) {
 
 int main(int argc, char **argv) {
     if (argc < 3) {
-        fprintf(stderr, "usage: %s magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|f16] "
+        fprintf(stderr, "usage: %s magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|q4_0|f16] "
                         "[--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V] [--lt-head-scale K]\n", argv[0]);
         return 2;
     }
@@ -364,7 +393,10 @@ int main(int argc, char **argv) {
     int dtype = T_F32, dec_layers = 12, enc_layers = 6, dec_pos = 2048;
     for (int i = 3; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--seed")) g_seed = strtoull(argv[i + 1], NULL, 0);
-        else if (!strcmp(argv[i], "--dtype")) dtype = !strcmp(argv[i + 1], "q8_0") ? T_Q8_0 : !strcmp(argv[i + 1], "f16") ? T_F16 : T_F32;
+        else if (!strcmp(argv[i], "--dtype")) dtype = !strcmp(argv[i + 1], "q8_0")   ? T_Q8_0
+                                                          : !strcmp(argv[i + 1], "q4_0") ? T_Q4_0
+                                                          : !strcmp(argv[i + 1], "f16")  ? T_F16
+                                                                                         : T_F32;
         else if (!strcmp(argv[i], "--dec-layers")) dec_layers = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--enc-layers")) enc_layers = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--dec-pos")) dec_pos = atoi(argv[i + 1]);
@@ -421,7 +453,8 @@ int main(int argc, char **argv) {
             for (int64_t k = 0; k < n; ++k) h[k] = f32_to_f16(buf[k]);
             fwrite(h, 2, (size_t)n, f);
         } else {
-            quant_q8_0(buf, n, qbuf);
+            if (t->type == T_Q4_0) quant_q4_0(buf, n, qbuf);
+            else quant_q8_0(buf, n, qbuf);
             fwrite(qbuf, 1, nbytes(t), f);
         }
     }

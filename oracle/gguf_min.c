@@ -158,6 +158,16 @@ float *orc_gguf_f32(const orc_gguf *g, const char *name, int64_t *n_out) {
             const float d = orc_f16_to_f32(h);
             for (int i = 0; i < 32; ++i) out[b * 32 + i] = (float)(int8_t)blk[2 + i] * d;
         }
+    } else if (t->type == 2) {  // Q4_0 (dequantize_row_q4_0): byte j = q_j | q_{j+16} << 4, value (q - 8) d
+        for (int64_t b = 0; b < n / 32; ++b) {
+            const uint8_t *blk = src + b * 18;
+            uint16_t h; memcpy(&h, blk, 2);
+            const float d = orc_f16_to_f32(h);
+            for (int j = 0; j < 16; ++j) {
+                out[b * 32 + j] = (float)((int)(blk[2 + j] & 0x0F) - 8) * d;
+                out[b * 32 + j + 16] = (float)((int)(blk[2 + j] >> 4) - 8) * d;
+            }
+        }
     } else { free(out); return NULL; }
     if (n_out) *n_out = n;
     return out;

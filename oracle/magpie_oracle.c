@@ -214,6 +214,11 @@ struct orc_model {
     // weight mode 1 (bf16 decode projections): rounded copies, NULL in mode 0
     int half;
     float *lt_qkv_h, *lt_o_h, *lt_ff1_h, *lt_ff2_h, *lt_out_w_h[8];
+    // weight mode 3 (an F16 file, ggml's F16 mul_mat): the tensors stored F16 (their
+    // widened values are exact); every mul_mat with one rounds its src1 to f16
+    int f16mode;
+    const float **f16w;
+    int n_f16, cap_f16;
     // weight mode 2 (ggml Q8_0 mul_mat for the file's Q8_0 tensors): the raw blocks
     int q8mode;
     q8w_t *q8;
@@ -221,6 +226,19 @@ struct orc_model {
     float **owned;
     int n_owned, cap_owned;
 };
+
+static int is_f16(const orc_model *m, const float *W) {
+    if (!m->f16mode) return 0;
+    for (int i = 0; i < m->n_f16; ++i)
+        if (m->f16w[i] == W) return 1;
+    return 0;
+}
+static float f16r(float x) { return orc_f16_to_f32(orc_f32_to_f16(x)); }
+static float *f16_rows(const float *X, size_t n) {
+    float *r = malloc(sizeof(float) * n);
+    for (size_t i = 0; i < n; ++i) r[i] = f16r(X[i]);
+    return r;
+}
 
 static const q8w_t *find_q8(const orc_model *m, const float *W) {
     if (!m->q8mode) return NULL;
@@ -233,8 +251,14 @@ static const q8w_t *find_q8(const orc_model *m, const float *W) {
 // mode 2 take ggml's quantised path, everything else the f32 dot.
 static void mm(const orc_model *m, const float *W, const float *bias, const float *X, float *Y, int M, int N, int K) {
     const q8w_t *q = find_q8(m, W);
-    if (q) matmul_q8(q, bias, X, Y, M, N, K);
-    else matmul(W, bias, X, Y, M, N, K);
+    if (q) { matmul_q8(q, bias, X, Y, M, N, K); return; }
+    if (is_f16(m, W)) {  // ggml F16 mul_mat: src1 rounded to f16 (vec_dot_type F16), products exact in f32
+        float *Xh = f16_rows(X, (size_t)M * K);
+        matmul(W, bias, Xh, Y, M, N, K);
+        free(Xh);
+        return;
+    }
+    matmul(W, bias, X, Y, M, N, K);
 }
 
 // Projection in weight mode 1: bf16 weights x bf16-rounded activations,
@@ -258,7 +282,14 @@ static float *take(orc_model *m, const orc_gguf *g, const char *name, int *ok) {
     }
     m->owned[m->n_owned++] = p;
     const orc_tinfo *t = orc_gguf_find(g, name);
-    if (t && t->type == 8) {  // keep the stored Q8_0 blocks for weight mode 2
+    if (t && t->type == 1) {  // F16: remembered for weight mode 3
+        if (m->n_f16 == m->cap_f16) {
+            m->cap_f16 = m->cap_f16 ? 2 * m->cap_f16 : 128;
+            m->f16w = realloc(m->f16w, sizeof(float *) * (size_t)m->cap_f16);
+        }
+        m->f16w[m->n_f16++] = p;
+    }
+    if (t && (t->type == 8 || t->type == 2)) {  // keep the stored Q8_0 / Q4_0 blocks for weight mode 2
         const int64_t n = t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3];
         const uint8_t *src = g->map + g->data_off + t->offset;
         if (m->n_q8 == m->cap_q8) {
@@ -271,9 +302,18 @@ static float *take(orc_model *m, const orc_gguf *g, const char *name, int *ok) {
         e->d = malloc(sizeof(float) * (size_t)(n / 32));
         for (int64_t b = 0; b < n / 32; ++b) {
             uint16_t h;
-            memcpy(&h, src + b * 34, 2);
+            if (t->type == 8) {
+                memcpy(&h, src + b * 34, 2);
+                memcpy(e->q + b * 32, src + b * 34 + 2, 32);
+            } else {  // Q4_0 as ggml's vec_dot_q4_0_q8_0 reads it: (nibble - 8), same integer dot
+                const uint8_t *blk = src + b * 18;
+                memcpy(&h, blk, 2);
+                for (int j = 0; j < 16; ++j) {
+                    e->q[b * 32 + j] = (int8_t)((blk[2 + j] & 0x0F) - 8);
+                    e->q[b * 32 + j + 16] = (int8_t)((blk[2 + j] >> 4) - 8);
+                }
+            }
             e->d[b] = orc_f16_to_f32(h);
-            memcpy(e->q + b * 32, src + b * 34 + 2, 32);
         }
     }
     return p;
@@ -385,10 +425,16 @@ static void free_half(orc_model *m) {
 }
 
 int orc_set_weight_mode(orc_model *m, int mode) {
-    if (!m || mode < 0 || mode > 2) return -1;
+    if (!m || mode < 0 || mode > 3) return -1;
     free_half(m);
     m->q8mode = 0;
+    m->f16mode = 0;
     if (mode == 0) return 0;
+    if (mode == 3) {  // ggml F16 semantics for the file's F16 tensors
+        if (m->n_f16 == 0) return -1;
+        m->f16mode = 1;
+        return 0;
+    }
     if (mode == 2) {  // ggml Q8_0 semantics for the file's Q8_0 tensors
         if (m->n_q8 == 0) return -1;
         m->q8mode = 1;
@@ -416,6 +462,7 @@ void orc_free(orc_model *m) {
     free_half(m);
     for (int i = 0; i < m->n_q8; ++i) { free(m->q8[i].q); free(m->q8[i].d); }
     free(m->q8);
+    free(m->f16w);
     for (int i = 0; i < m->n_owned; ++i) free(m->owned[i]);
     free(m->owned);
     free(m->enc);
@@ -455,7 +502,11 @@ static void causal_mha(const float *qkv, int M, int d, int heads, float *attn, i
 
 // magpie_build_conv_ffn kernel_size=3 branch (magpie.cpp:1806-1917): tap k of
 // W[j][i][k] multiplies input row t-2+k (zero left padding).
-static void conv_ffn_k(const float *W, const float *X, float *Y, int M, int N, int K, int ks) {
+static void conv_ffn_k(const orc_model *m, const float *W, const float *X0, float *Y, int M, int N, int K, int ks) {
+    // F16 conv weights (weight mode 3): ggml's im2col takes the kernel's type, so the
+    // input is rounded to f16 before the F16 mul_mat
+    float *Xh = is_f16(m, W) ? f16_rows(X0, (size_t)M * K) : NULL;
+    const float *X = Xh ? Xh : X0;
 #pragma omp parallel for schedule(static)
     for (int n = 0; n < N; ++n) {
         const float *w = W + (size_t)n * K * ks;
@@ -478,6 +529,7 @@ static void conv_ffn_k(const float *W, const float *X, float *Y, int M, int N, i
             Y[(size_t)t * N + n] = (float)acc;
         }
     }
+    free(Xh);
 }
 
 // magpie_encode_text (magpie.cpp:2284-2374) -> magpie_build_full_encoder (1960-1995)
@@ -502,9 +554,9 @@ int orc_encode(orc_model *m, const int32_t *tok, int T, float *enc_out) {
         mm(m, L->o, NULL, att, o, T, d, d);
         for (size_t i = 0; i < (size_t)T * d; ++i) x[i] = o[i] + x[i];
         layernorm_rows(x, L->norm_ff, h, T, d, m->eps);
-        conv_ffn_k(L->ff1, h, f, T, dff, d, m->enc_kernel);
+        conv_ffn_k(m, L->ff1, h, f, T, dff, d, m->enc_kernel);
         gelu_inplace(f, (size_t)T * dff);
-        conv_ffn_k(L->ff2, f, o, T, d, dff, m->enc_kernel);
+        conv_ffn_k(m, L->ff2, f, o, T, d, dff, m->enc_kernel);
         for (size_t i = 0; i < (size_t)T * d; ++i) x[i] = o[i] + x[i];
     }
     layernorm_rows(x, m->enc_norm_out, enc_out, T, d, m->eps);

@@ -38,7 +38,11 @@ orc_model *orc_load(const char *gguf_path);
 // mul_mat for every Q8_0 tensor of the file, everywhere it is used (encoder,
 // XA K/V, prefill, decode steps, LT): the activation row is quantised to Q8_0
 // (quantize_row_q8_0_ref), per-block integer dots scaled by d_w*d_a (SURVEY A.7,
-// assumed); -1 if the file has no Q8_0 tensor.
+// assumed); Q4_0 tensors the same way with q - 8 (vec_dot_q4_0_q8_0); -1 if the
+// file has no Q8_0 / Q4_0 tensor. Weight mode 3 = ggml's F16 mul_mat for every F16
+// tensor of the file, everywhere (encoder incl. its k=3 conv FFN, XA q/kv/o,
+// prefill, decode steps, LT in_proj/layer/heads): src1 rounded to f16, products
+// exact, f32/f64 accumulation; -1 if the file has no F16 tensor.
 int orc_set_weight_mode(orc_model *m, int mode);
 void orc_free(orc_model *m);
 int orc_dec_layers(const orc_model *m);

@@ -77,7 +77,8 @@ class Model:
 
     def set_weight_mode(self, mode: int) -> None:
         """0 = f32 (dequantised), 1 = bf16 decode projections, 2 = ggml Q8_0 mul_mat
-        for the file's Q8_0 tensors (see magpie_oracle.h)."""
+        for the file's Q8_0 / Q4_0 tensors, 3 = ggml F16 mul_mat for the file's F16
+        tensors (see magpie_oracle.h)."""
         if lib().orc_set_weight_mode(self.h, int(mode)) != 0:
             raise RuntimeError("oracle: bad weight mode")
 

@@ -62,6 +62,18 @@ def q8_model():
 
 
 @pytest.fixture(scope="session")
+def q4_model():
+    import magpie_amd as ma
+    return _gguf("magpie_small_q4_k32.gguf", dtype="q4_0", dec_layers=2, enc_layers=1, lt_head_scale=ma.DECISIVE)
+
+
+@pytest.fixture(scope="session")
+def f16_model():
+    import magpie_amd as ma
+    return _gguf("magpie_small_f16_k32.gguf", dtype="f16", dec_layers=2, enc_layers=1, lt_head_scale=ma.DECISIVE)
+
+
+@pytest.fixture(scope="session")
 def q8_full_model():
     """Magpie-357M shapes, the reference converter's default Q8_0 patterns."""
     import magpie_amd as ma

@@ -307,6 +307,57 @@ def test_bf16_batch_equals_single(ma, small_model, B):
     dev.close()
 
 
+# ---------------------------------------------------------------- F16 weight mode
+# An F16 GGUF (the converter's --outtype f16) with ggml's F16 mul_mat semantics
+# (MP_WEIGHTS_F16) vs the oracle's weight mode 3. Every decision teacher forced;
+# f16 rounding is 8x finer than bf16, the bars are the bf16 ones (the fused XA
+# applies o_net to the unrounded attention output, a documented deviation).
+def test_f16_small_model_matches_oracle(ma, oracle, f16_model):
+    tok = ma.synthetic_tokens(24, seed=1000)
+    dev = ma.Device(f16_model, weights="f16")
+    r = dev.synthesize([tok], speakers=[1], max_dec_steps=40, ignore_eos=True, trace=True)
+    dev.close()
+    om = oracle.Model(f16_model)
+    om.set_weight_mode(3)
+    o = om.synthesize_forced(tok, r.codes[0], speaker=1, ignore_eos=True)
+    om.close()
+    res = compare_forced(r.codes[0], o, tie_eps=BF16_TIE_EPS, max_ties=8)
+    assert res["decisions"] == 320
+    _check_hidden_b16(r.hidden[0, :41], o["hidden"][:41])
+    err = np.abs(r.hidden[0, :41] - o["hidden"][:41]).max()
+    print(f"f16 vs oracle mode 3: hidden max abs err {err:.3g}")
+
+
+def test_f16_mode_rounds_like_ggml(ma, f16_model):
+    """The F16 mode is not the widened-f32 mode (activations really are rounded)."""
+    tok = ma.synthetic_tokens(16, seed=3)
+    d16 = ma.Device(f16_model, weights="f16")
+    a = d16.synthesize([tok], max_dec_steps=4, ignore_eos=True, trace=True)
+    d16.close()
+    d32 = ma.Device(f16_model)
+    b = d32.synthesize([tok], max_dec_steps=4, ignore_eos=True, trace=True)
+    d32.close()
+    d = np.abs(a.hidden[0, 0] - b.hidden[0, 0]).max()
+    assert 1e-6 < d < 2e-2, d
+
+
+@pytest.mark.parametrize("B", [3, 16])
+def test_f16_batch_equals_single(ma, f16_model, B):
+    toks = [ma.synthetic_tokens(8 + 3 * b, seed=2500 + b) for b in range(B)]
+    spk = [b % 5 for b in range(B)]
+    dev = ma.Device(f16_model, weights="f16")
+    rb = dev.synthesize(toks, speakers=spk, max_dec_steps=16, ignore_eos=True, trace=True)
+    for b in (0, B - 1):
+        rs = dev.synthesize([toks[b]], speakers=[spk[b]], max_dec_steps=16, ignore_eos=True, trace=True)
+        assert np.array_equal(rb.codes[b], rs.codes[0]) and np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b}"
+    dev.close()
+
+
+def test_f16_mode_needs_f16_file(ma, small_model):
+    with pytest.raises(ma.MagpieError):
+        ma.Device(small_model, weights="f16")
+
+
 def test_f32_mode_rejects_batch_16(ma, small_model):
     dev = ma.Device(small_model)
     with pytest.raises(ma.MagpieError):
@@ -405,6 +456,25 @@ def test_q8_sampling_matches_oracle(ma, oracle, q8_model):
     batch-invariance tests (test_sampled_batch_equals_single[q8-*])."""
     tok = ma.synthetic_tokens(12, seed=41)
     _q8_forced(ma, oracle, q8_model, tok, steps=24, tie_frac=0.5, temperature=0.7, top_k=80, seed=77)
+
+
+def test_q4_small_model_matches_oracle(ma, oracle, q4_model):
+    """Q4_0 file (convert_magpie_to_gguf.py:107-138): its blocks run on the Q8_0
+    kernels as int8 (q - 8) = ggml's vec_dot_q4_0_q8_0; teacher forced against the
+    oracle's weight mode 2 on the same file, with the Q8 bars."""
+    tok = ma.synthetic_tokens(24, seed=1000)
+    r, o = _q8_forced(ma, oracle, q4_model, tok, steps=40, speaker=1)
+    _check_hidden_q8(r.hidden[0, :41], o["hidden"])
+
+
+def test_q4_batch_equals_single(ma, q4_model):
+    toks = [ma.synthetic_tokens(8 + 3 * b, seed=3100 + b) for b in range(3)]
+    dev = ma.Device(q4_model, weights="q4")
+    rb = dev.synthesize(toks, speakers=[0, 1, 2], max_dec_steps=16, ignore_eos=True, trace=True)
+    for b in (0, 2):
+        rs = dev.synthesize([toks[b]], speakers=[b], max_dec_steps=16, ignore_eos=True, trace=True)
+        assert np.array_equal(rb.codes[b], rs.codes[0]) and np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b}"
+    dev.close()
 
 
 def test_q8_mode_needs_q8_file(ma, small_model):

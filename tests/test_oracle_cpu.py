@@ -266,6 +266,109 @@ def test_oracle_q8_mode(oracle, q8_model, small_model):
     m.close()
 
 
+# ---------------------------------------------------------------- Q4_0 (weight mode 2)
+def _q4_blocks_like_converter(W):
+    """convert_magpie_to_gguf.py:107-138 in numpy: fp16 d = amax/7, q = clip(round(x/d),
+    -8, 7) + 8, low nibbles = elements 0..15, high nibbles = 16..31."""
+    x = W.astype(np.float32).reshape(-1, 32)
+    amax = np.abs(x).max(axis=1)
+    d = np.where(amax != 0, amax / 7.0, 0.0).astype(np.float16)
+    ds = np.where(d != 0, d.astype(np.float32), 1.0)[:, None]
+    q = np.clip(np.round(x / ds).astype(np.int8), -8, 7)
+    q = np.where(d[:, None] != 0, q, 0)
+    u = (q + 8).astype(np.uint8)
+    packed = (u[:, :16] & 0x0F) | (u[:, 16:] << 4)
+    blk = np.empty(len(x), np.dtype([("d", "<f2"), ("q", "u1", 16)]))
+    blk["d"], blk["q"] = d, packed
+    return blk.tobytes(), q.astype(np.int64), d.astype(np.float64)
+
+
+def test_q4_file_blocks_match_converter(small_model, q4_model):
+    """The synthetic Q4_0 file holds exactly the converter's blocks of the same f32
+    weights (tensor set: the converter's default patterns; pos_ff stays F32)."""
+    from gguf_raw import GgufRaw
+    f32, q4 = GgufRaw(small_model), GgufRaw(q4_model)
+    for name in ("decoder.layers.1.self_attention.qkv_net.weight", "decoder.layers.0.cross_attention.o_net.weight",
+                 "local_transformer_out_projections.5.weight"):
+        typ, _, raw = q4.raw(name)
+        assert typ == 2, name
+        want, _, _ = _q4_blocks_like_converter(f32.f32(name))
+        assert raw == want, name
+    assert q4.raw("decoder.layers.0.pos_ff.proj.conv.weight")[0] == 0
+    assert q4.raw("audio_embeddings.0.weight")[0] == 0
+
+
+def test_q4_matvec_matches_numpy_restatement(oracle):
+    """ggml's vec_dot_q4_0_q8_0: integer dot of (q - 8) with the Q8_0-quantised
+    activation, times d_w * d_a: the oracle's weight mode 2 on Q4_0 blocks."""
+    rng = np.random.default_rng(9)
+    N, K = 64, 256
+    W = rng.normal(0, 0.02, (N, K)).astype(np.float32)
+    W[5, 32:64] = 0.0
+    _, q, d = _q4_blocks_like_converter(W)
+    # the same integers through the Q8_0 entry point: q8 blocks holding q (what the loader repacks to)
+    blk = np.empty(N * K // 32, np.dtype([("d", "<f2"), ("q", "i1", 32)]))
+    blk["d"], blk["q"] = d.astype(np.float16), q.astype(np.int8).reshape(-1, 32)
+    x = rng.normal(0, 1.0, K).astype(np.float32)
+    y = oracle.q8_matvec(blk.tobytes(), N, K, x)
+    ref = _ggml_q8_matvec_numpy(q, d, N, K, x)
+    np.testing.assert_allclose(y, ref.astype(np.float32), rtol=2e-6, atol=1e-9)
+
+
+def test_oracle_q4_mode(oracle, q4_model):
+    """Weight mode 2 on a Q4_0 file: deterministic, within Q4 quantisation noise of the
+    dequantised-f32 mode."""
+    import magpie_amd as ma
+    tok = ma.synthetic_tokens(12, seed=4)
+    m = oracle.Model(q4_model)
+    f = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.set_weight_mode(2)
+    a = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    b = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.close()
+    assert np.array_equal(a["hidden"], b["hidden"]) and np.array_equal(a["codes"], b["codes"])
+    d0 = np.abs(f["hidden"][0] - a["hidden"][0]).max()
+    assert 0 < d0 < 0.5, d0
+
+
+# ---------------------------------------------------------------- F16 (weight mode 3)
+def test_f16_file_tensor_set_matches_converter(small_model, f16_model):
+    """convert_magpie_to_gguf.py:155-176, 311-327 with --outtype f16: the projection
+    patterns (pos_ff convs included: F16 has no block constraint) become F16 (the
+    f32 values rounded to nearest even); embeddings, norms and biases stay F32."""
+    from gguf_raw import GgufRaw
+    f32, f16 = GgufRaw(small_model), GgufRaw(f16_model)
+    for name in ("decoder.layers.1.self_attention.qkv_net.weight", "decoder.layers.0.pos_ff.o_net.conv.weight",
+                 "encoder.layers.0.pos_ff.proj.conv.weight", "local_transformer.layers.0.pos_ff.proj.conv.weight",
+                 "local_transformer_in_projection.weight", "decoder.layers.0.cross_attention.kv_net.weight"):
+        typ, _, raw = f16.raw(name)
+        assert typ == 1, name
+        assert raw == f32.f32(name).astype(np.float16).tobytes(), name
+    for name in ("audio_embeddings.3.weight", "decoder.layers.0.norm_pos_ff.weight", "final_proj.bias",
+                 "local_transformer.position_embeddings.weight", "baked_context_embedding.weight"):
+        assert f16.raw(name)[0] == 0, name
+
+
+def test_oracle_f16_mode(oracle, f16_model, small_model):
+    """Weight mode 3 (ggml F16 mul_mat): deterministic, within f16 rounding noise of
+    the widened-f32 mode, and needs a file with F16 tensors."""
+    import magpie_amd as ma
+    tok = ma.synthetic_tokens(12, seed=4)
+    m = oracle.Model(f16_model)
+    f = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.set_weight_mode(3)
+    a = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    b = m.synthesize(tok, max_steps=3, ignore_eos=True)
+    m.close()
+    assert np.array_equal(a["hidden"], b["hidden"]) and np.array_equal(a["codes"], b["codes"])
+    d0 = np.abs(f["hidden"][0] - a["hidden"][0]).max()
+    assert 0 < d0 < 2e-2, d0
+    m = oracle.Model(small_model)
+    with pytest.raises(RuntimeError):
+        m.set_weight_mode(3)  # F32 file: nothing to run as F16
+    m.close()
+
+
 def test_teacher_forced_run_reproduces_free_run(oracle, small_model):
     """Forced along its own codes, the oracle reproduces its free run exactly (codes,
     margins, hidden); forced along other codes it follows them."""

@@ -1,11 +1,15 @@
-"""Workload for the PMC passes (tools_dev/pmc_traffic.sh): the bench's N=1
-configuration (Magpie-357M f32, batch 1, T=64, EOS masked) decoded with every
-kernel launched eagerly (MAGPIE_EAGER=1 is set by the caller) so rocprofv3 can
-attribute counters per dispatch. Writes the op -> kernel symbol order of one
-iteration to gpurun_out/pmc_ops.json."""
+"""Workloads for the PMC passes (tools_dev/pmc_collect.sh), every kernel launched
+eagerly (MAGPIE_EAGER=1 is set by the caller) so rocprofv3 attributes counters per
+dispatch:
+  decode WEIGHTS B : the bench's model (Magpie-357M, decisive LT heads), T=64, EOS
+                     masked, 64 frames; writes the op order of one iteration to
+                     gpurun_out/pmc_ops_<WEIGHTS>_<B>.json
+  codec            : the bench's codec shape, 8 chunks x 32 frames, 4 decodes"""
 import json
 import os
 import sys
+
+import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "magpie-tts.cpp_amd"))
@@ -13,11 +17,24 @@ import magpie_amd as ma  # noqa: E402
 
 cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
 os.makedirs(cache, exist_ok=True)
-path = ma.synth_gguf(os.path.join(cache, "magpie_357m_f32.gguf"))
-dev = ma.Device(path)
-tok = [ma.synthetic_tokens(64, seed=1000)]
-r = dev.synthesize(tok, speakers=[0], max_dec_steps=int(os.environ.get("PMC_FRAMES", "64")), ignore_eos=True)
 os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-json.dump({"ops": dev.ops(), "frames": int(r.n_frames[0])}, open(os.path.join(REPO, "gpurun_out", "pmc_ops.json"), "w"))
-dev.close()
-print("pmc workload done", r.n_frames[0], "frames")
+mode = sys.argv[1] if len(sys.argv) > 1 else "decode"
+if mode == "codec":
+    c = ma.Codec(ma.synth_gguf(os.path.join(cache, "nano_codec.gguf"), kind="codec"))
+    codes = np.random.default_rng(1).integers(0, 2016, (8, 8, 32)).astype(np.int32)
+    for _ in range(4):
+        c.decode_chunks(codes)
+    c.close()
+    print("pmc codec workload done")
+else:
+    weights = sys.argv[2] if len(sys.argv) > 2 else "f32"
+    B = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    path = ma.synth_gguf(os.path.join(cache, "magpie_357m_f32_k32.gguf"), lt_head_scale=ma.DECISIVE)
+    dev = ma.Device(path, weights=weights)
+    toks = [ma.synthetic_tokens(64, seed=1000 + b) for b in range(B)]
+    r = dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=int(os.environ.get("PMC_FRAMES", "64")),
+                       ignore_eos=True)
+    json.dump({"ops": dev.ops(), "frames": int(r.n_frames[0])},
+              open(os.path.join(REPO, "gpurun_out", f"pmc_ops_{weights}_{B}.json"), "w"))
+    dev.close()
+    print("pmc decode workload done", weights, B, r.n_frames[0], "frames")

@@ -41,7 +41,8 @@ CODEC_FLOP_PER_FRAME = 2.447e9  # 1.2234 G MAC per codec frame
 CODEC_CHUNK = 32  # the CLI decodes stateless 32-frame chunks (magpie-tts.cpp:181-206)
 FRAMES = 256
 TEXT_TOKENS = 64
-PMC_TRAFFIC = "r01v_pmc_traffic.json"  # per-op HBM bytes of the N=1 workload (tools_dev/pmc_parse.py)
+PMC_TRAFFIC = "r02ao_pmc_decode_f32_b1.json"  # per-op HBM bytes of the N=1 workload (tools_dev/pmc_report.py)
+PMC_CODEC = "r02ao_pmc_codec.json"  # codec MFMA busy cycles + bytes per kernel (tools_dev/pmc_report.py)
 
 
 def decoder_bytes_per_frame(B: int, L_mean: float, T: int, dec_layers: int = 12, weights: str = "f32") -> float:
@@ -78,6 +79,16 @@ def measure_extra(model_path: str, codec_path, args) -> dict:
         dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=args.frames, ignore_eos=True)
         out[f"bf16_batch{B}_fps"] = round(_decode_fps(dev, B, args.frames), 1)
     dev.close()
+    # the reference converter's other file types at batch 1: F16 (ggml F16 mul_mat
+    # semantics, f16 MFMA) and Q4_0 (on the Q8_0 kernels, int8 q - 8)
+    for dt, wm in (("f16", "f16"), ("q4_0", "q4")):
+        pth = os.path.join(os.path.dirname(model_path), f"magpie_357m_{dt}_k32.gguf")
+        ma.synth_gguf(pth, dtype=dt, lt_head_scale=ma.DECISIVE)
+        dev = ma.Device(pth, weights=wm)
+        dev.synthesize([ma.synthetic_tokens(args.tokens, seed=1000)], speakers=[0], max_dec_steps=args.frames,
+                       ignore_eos=True)
+        out[f"{wm}_batch1_fps"] = round(_decode_fps(dev, 1, args.frames), 1)
+        dev.close()
     # configs[4]: Q8_0 GGUF (the reference converter's default patterns), 60 s of
     # long-form audio streamed sentence by sentence with 4-frame codec chunks; the
     # sentences run as one device batch (magpie_synthesize_streaming's sentence
@@ -285,6 +296,13 @@ def main() -> None:
         codec = {"frames": cframes, "ms": round(codec_ms, 3), "fps": round(cframes / (codec_ms * 1e-3), 1),
                  "tflops": round(tfs, 1), "mfma_f16_peak_tflops": MFMA_F16_PEAK_TFS,
                  "frac": round(tfs / MFMA_F16_PEAK_TFS, 4), "audio_peak": round(float(np.abs(audio).max()), 4)}
+        pmc_codec = os.path.join(REPO, "profiles", PMC_CODEC)
+        if os.path.exists(pmc_codec):  # counters of the same codec shape (tools_dev/pmc_report.py)
+            sm = json.load(open(pmc_codec))["summary"]
+            codec["pmc"] = {"mfma_util": sm.get("mfma_util_traced"), "hbm_tbs": sm.get("hbm_tbs_traced"),
+                            "bytes_per_decode": sm.get("per_decode_bytes"),
+                            "source": f"profiles/{PMC_CODEC}: SQ_VALU_MFMA_BUSY_CYCLES / (traced duration x "
+                                      "2.4 GHz x 1024 SIMDs); FETCH_SIZE/WRITE_SIZE passes"}
 
     # ---- roofline of the dominant kernel, timed in situ: whole decode iterations
     # launched eagerly on the decode stream, each kernel through hipExtLaunchKernel
@@ -328,8 +346,9 @@ def main() -> None:
                     "timing": "dispatch begin/end stamped on the kernel's own start/stop events "
                               "(hipExtLaunchKernel; the rocprofv3 kernel-trace interval), whole eager "
                               "iterations at the mid-utterance state (mp_hip_profile_ops_kev)"}
-        # HBM bytes per launch from the committed PMC passes (tools_dev/pmc_traffic.sh +
-        # pmc_parse.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE correction)
+        # HBM bytes per launch from the committed PMC passes (tools_dev/pmc_collect.sh +
+        # pmc_report.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE
+        # correction for the 16 B/lane kernels)
         pmc_path = os.path.join(REPO, "profiles", PMC_TRAFFIC)
         if args.weights == "f32" and B == 1 and os.path.exists(pmc_path):
             pmc_ops = json.load(open(pmc_path))["ops"]

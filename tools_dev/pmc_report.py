@@ -11,7 +11,12 @@ kernels whose bulk loads are 16 B per lane (WIDE below); other kernels' fetch is
 reported raw and marked uncalibrated. WRITE_SIZE is exact for 16 B/lane stores.
 Infinity-Cache hits are counted: these are L2-miss (fabric) bytes, an upper bound
 on HBM bytes. MFMA utilisation = sum SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x
-1024 SIMDs) (rocprofv3's MfmaUtil expression); MFMA FLOPs = MOPS x 512."""
+1024 SIMDs) (rocprofv3's MfmaUtil expression); MFMA FLOPs = MOPS x 512. Under
+per-dispatch PMC collection GRBM_GUI_ACTIVE includes the profiler's own per-dispatch
+overhead, so with a kernel trace of the same workload (TRACE_CSV, e.g. the bench's
+rocprofv3 --kernel-trace run) the codec utilisation is also given against the traced
+duration: busy / (duration x 2.4 GHz x 1024).
+usage: pmc_report.py TAG [TRACE_CSV]"""
 import csv
 import json
 import os
@@ -23,6 +28,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 SIMDS = 256 * 4
+CLK = 2.4e9  # shader clock (MI355X_MICROARCH.md)
 # kernels whose bulk global loads are 16 B per lane (float4 / uint4 / half8)
 WIDE = ("gemv_kernel", "gemm_b16_kernel", "xa_part_kernel", "sa_attn_kernel", "lt_ffn2_kernel", "lt_ffn_kernel",
         "conv_mfma_kernel")
@@ -82,7 +88,18 @@ def decode_ops(tag, pre, ops_file, mfma):
     return out
 
 
-def codec(tag):
+def trace_durations(path):
+    """{(kernel, grid threads): mean duration us} from a rocprofv3 kernel trace"""
+    d = defaultdict(list)
+    if path:
+        for r in csv.DictReader(open(path)):
+            g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+            d[(r["Kernel_Name"], g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
+    return {k: float(np.mean(v)) for k, v in d.items()}
+
+
+def codec(tag, trace=None):
+    dur = trace_durations(trace)
     passes = {k: rows(tag, "codec_" + k) for k in ("fetch", "write", "mfma")}
     groups = {}
     for k, v in passes.items():
@@ -100,17 +117,32 @@ def codec(tag):
         flops = float(np.mean(g.get("SQ_INSTS_VALU_MFMA_MOPS_F16", [0.0]))) * 512
         n = len(g["FETCH_SIZE"])
         fb = 2 * f if wide(kern) else f
-        out.append({"kernel": kern, "grid": grid, "dispatches": n, "fetch_bytes": round(fb), "fetch_corrected": wide(kern),
-                    "write_bytes": round(w), "mfma_flops": round(flops), "mfma_busy_cycles": round(busy),
-                    "gui_active_cycles": round(gui), "mfma_util": round(busy / (gui * SIMDS), 4) if gui else None})
+        rec = {"kernel": kern, "grid": grid, "dispatches": n, "fetch_bytes": round(fb), "fetch_corrected": wide(kern),
+               "write_bytes": round(w), "mfma_flops": round(flops), "mfma_busy_cycles": round(busy),
+               "gui_active_cycles": round(gui), "mfma_util": round(busy / (gui * SIMDS), 4) if gui else None}
+        if flops:
+            rec["busy_cycles_per_mfma_16x16x32"] = round(busy / (flops / 16384), 2)
+        t = dur.get((kern, grid))
+        if t:
+            rec["traced_us"] = round(t, 2)
+            rec["mfma_util_traced"] = round(busy / (t * 1e-6 * CLK * SIMDS), 4)
+            rec["tflops_traced"] = round(flops / (t * 1e-6) / 1e12, 1)
+            rec["hbm_tbs_traced"] = round((fb + w) / (t * 1e-6) / 1e12, 2)
+            tot["t"] += n * t
         tot["bytes"] += n * (fb + w)
         tot["flops"] += n * flops
         tot["busy"] += n * busy
         tot["gui"] += n * gui
+        out.append(rec)
     out.sort(key=lambda r: -r["dispatches"] * r["gui_active_cycles"])
     decodes = 4
     summary = {"per_decode_bytes": round(tot["bytes"] / decodes), "per_decode_mfma_flops": round(tot["flops"] / decodes),
-               "mfma_util_time_weighted": round(tot["busy"] / (tot["gui"] * SIMDS), 4) if tot["gui"] else None}
+               "mfma_util_gui_active": round(tot["busy"] / (tot["gui"] * SIMDS), 4) if tot["gui"] else None}
+    if tot["t"]:
+        summary["per_decode_traced_us"] = round(tot["t"] / decodes, 1)
+        summary["mfma_util_traced"] = round(tot["busy"] / (tot["t"] * 1e-6 * CLK * SIMDS), 4)
+        summary["tflops_traced"] = round(tot["flops"] / (tot["t"] * 1e-6) / 1e12, 1)
+        summary["hbm_tbs_traced"] = round(tot["bytes"] / (tot["t"] * 1e-6) / 1e12, 2)
     return {"summary": summary, "kernels": out}
 
 
@@ -127,7 +159,7 @@ def main():
         for op, v in res["ops"].items():
             extra = f" mfma util {v['mfma_util']}" if "mfma_util" in v else ""
             print(f"  {op:10s} fetch {v['fetch_bytes'] / 1e6:8.3f} MB write {v['write_bytes'] / 1e6:7.3f} MB{extra}")
-    c = codec(tag)
+    c = codec(tag, sys.argv[2] if len(sys.argv) > 2 else None)
     c["source"] = src
     json.dump(c, open(os.path.join(REPO, "profiles", f"{tag}_pmc_codec.json"), "w"), indent=1)
     print("== codec", c["summary"])

@@ -365,6 +365,10 @@ int load_model(mp_dev *dev, const char *path) {
     m.text_vocab = (int)g.get_u32("magpie.text_vocab_size", 2380);
     m.audio_bos = (int)g.get_u32("magpie.audio_bos_id", 2016);
     m.audio_eos = (int)g.get_u32("magpie.audio_eos_id", 2017);
+    // the kernels' forbidden-token mask is the range [bos, bos + 7] minus eos, which is
+    // the reference's explicit list (magpie.cpp:1133-1145) only when eos == bos + 1
+    if (m.audio_eos != m.audio_bos + 1 || m.audio_bos < 0 || m.audio_bos + 8 > mp::VCB)
+        return fail(dev, MP_ERR_UNSUPPORTED, "audio_eos_id must be audio_bos_id + 1 (forbidden-token layout)");
     m.max_dec_steps = (int)g.get_u32("magpie.max_dec_steps", 500);
     m.eps = (float)g.get_f32("magpie.eps", 1e-5);
     if (m.enc_layers < 1 || m.dec_layers < 1 || m.enc_layers > 64 || m.dec_layers > 64)

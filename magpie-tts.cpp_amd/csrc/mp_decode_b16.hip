@@ -21,6 +21,7 @@
 #include "mp_device.hpp"
 #include "mp_fused.hpp"
 #include "mp_params.hpp"
+#include "mp_xa.hpp"
 
 namespace mp {
 
@@ -77,6 +78,13 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     __shared__ __attribute__((aligned(16))) floatx4 part[MP_NWAVES][64];
     __shared__ float red[8];
     __shared__ float sc[SC];
+    if constexpr (EPI == EPI_RESID_XA) {
+        // the launch's last XA_SPLITS x NB workgroups: cross-attention on this launch's x1 (mp_xa.hpp)
+        if ((int)blockIdx.x >= p.nrow_blocks) {
+            xa_tail(p, t_start);
+            return;
+        }
+    }
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = blockIdx.x;
 
     // weight fragments of this wave's K slice, issued before the prologue
@@ -169,7 +177,8 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const float v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
     const int n = rt * 16 + row;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
+    if constexpr (EPI == EPI_RESID_XA) publish_x1(p, v, n, col);
+    else epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
     ts_end(p.ts, t_start);
 }
 
@@ -195,13 +204,19 @@ static bool b16_args_ok(const GemvP &p) {
     if constexpr (EPI == EPI_LTX_ADD) ok &= p.out && p.ptab && p.lt_pos && p.cb >= 1;
     if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
+    if constexpr (EPI == EPI_RESID_XA)
+        ok &= p.resid && p.xh && p.iter && p.hx_err && p.N == D && p.xa.part && p.xa.lnw && p.xa.kp && p.xa.vp &&
+              p.xa.T && p.xa.Tmax >= 1 && p.xa.Tmax <= TMAX_LIMIT;
     return ok;
 }
 
 template <int NB, int K, int PRO, int EPI, bool F16 = false>
 static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     if (!b16_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
-    mp::launch((gemm_b16_kernel<NB, K, PRO, EPI, F16>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
+    GemvP q = p;
+    q.nrow_blocks = (p.N + 15) / 16;
+    const int grid = q.nrow_blocks + (EPI == EPI_RESID_XA ? XA_SPLITS * NB : 0);
+    mp::launch((gemm_b16_kernel<NB, K, PRO, EPI, F16>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();
 }
 
@@ -209,6 +224,9 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     hipError_t b16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }   \
+    hipError_t b16_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                      \
+        return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA>(p, s);                                                       \
+    }                                                                                                                   \
     hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_B16>(p, s); }     \
     hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE>(p, s); }  \
     hipError_t b16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
@@ -222,6 +240,9 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     hipError_t f16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV, true>(p, s); } \
     hipError_t f16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV, true>(p, s); }             \
     hipError_t f16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID, true>(p, s); }   \
+    hipError_t f16_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                      \
+        return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA, true>(p, s);                                                 \
+    }                                                                                                                   \
     hipError_t f16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_F16, true>(p, s); }     \
     hipError_t f16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE, true>(p, s); }  \
     hipError_t f16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV, true>(p, s); }    \

@@ -50,7 +50,7 @@ hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
     hipError_t b16_ff2_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_a_##NB(const GemvP &, hipStream_t);           \
     hipError_t b16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_b_##NB(const GemvP &, hipStream_t);         \
     hipError_t b16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_d_##NB(const GemvP &, hipStream_t);          \
-    hipError_t b16_lt_e_##NB(const GemvP &, hipStream_t);
+    hipError_t b16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t b16_oproj_xa_##NB(const GemvP &, hipStream_t);
 MP_DECL_B16(1)
 MP_DECL_B16(2)
 MP_DECL_B16(4)
@@ -62,7 +62,8 @@ MP_DECL_B16(16)
     hipError_t f16_ff2_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_a_##NB(const GemvP &, hipStream_t);           \
     hipError_t f16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_b_##NB(const GemvP &, hipStream_t);         \
     hipError_t f16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_d_##NB(const GemvP &, hipStream_t);          \
-    hipError_t f16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_in0_##NB(const GemvP &, hipStream_t);
+    hipError_t f16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_in0_##NB(const GemvP &, hipStream_t); \
+    hipError_t f16_oproj_xa_##NB(const GemvP &, hipStream_t);
 MP_DECL_F16(1)
 MP_DECL_F16(2)
 MP_DECL_F16(4)
@@ -107,7 +108,7 @@ hipError_t op_finalize(const FinP &, int, hipStream_t);
 namespace mp {
 
 // ff1: LN(x2) prologue (x2 materialised: Q8 unfused XA); ff1x: the fused XA's split states merged into x2 first
-// oproj_xa: O-projection + the fused XA in one launch (EPI_RESID_XA; f32 GEMV family only)
+// oproj_xa: O-projection + the fused XA in one launch (EPI_RESID_XA)
 struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e, oproj_xa; };
 #define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, \
@@ -116,13 +117,13 @@ static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TAB
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
 #define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, nullptr, b16_ff1_##NB, b16_ff2_##NB, \
                            op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_bg_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
-                           b16_lt_d_##NB, b16_lt_e_##NB, nullptr }
+                           b16_lt_d_##NB, b16_lt_e_##NB, b16_oproj_xa_##NB }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
 // F16 weight mode (an F16 GGUF): the same MFMA family on f16, the LT in_proj included
 #define MP_TABLE_F16(NB) { f16_qkv_embed_##NB, f16_qkv_##NB, f16_oproj_##NB, nullptr, f16_ff1_##NB, f16_ff2_##NB, \
                            f16_lt_in0_##NB, f16_lt_a_##NB, f16_lt_bg_##NB, f16_lt_b_##NB, f16_lt_c_##NB,  \
-                           f16_lt_d_##NB, f16_lt_e_##NB, nullptr }
+                           f16_lt_d_##NB, f16_lt_e_##NB, f16_oproj_xa_##NB }
 static const OpTable kTablesF16[5] = {MP_TABLE_F16(1), MP_TABLE_F16(2), MP_TABLE_F16(4), MP_TABLE_F16(8),
                                       MP_TABLE_F16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)

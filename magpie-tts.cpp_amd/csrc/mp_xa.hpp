@@ -1,0 +1,194 @@
+// The fused cross-attention (XA) body shared by xa_part_kernel and the
+// O-projection launches that carry it (EPI_RESID_XA: the f32 GEMV and the 16-bit
+// MFMA families), and the O-projection side of that hand-off.
+#pragma once
+#include "mp_device.hpp"
+#include "mp_fused.hpp"
+#include "mp_params.hpp"
+
+namespace mp {
+
+// XA reassociated: with K'_t = W_q^T K_t and V'_t = W_o V_t precomputed per
+// utterance and layer, x += sum_t softmax_t(K'_t . LN(x) / sqrt(128)) V'_t.
+// Split over text keys: grid (split, slot), 8 waves. Split s takes keys
+// [s*chunk, (s+1)*chunk) of T; wave w takes t = t0 + w, t0 + w + 8, ... with its
+// first keys' K' and V' rows issued before x is fetched (one round trip), every
+// wave normalises x itself (DPP statistics, no barrier), keeps an online softmax
+// (m, l, o[768] in 12 registers per lane); the 8 wave states merge in LDS and
+// the split's state (m, l, unnormalised O[768]) is stored. The next op (FFN up,
+// PRO_XA_LN) merges the XA_SPLITS states, adds x and normalises.
+#ifndef MP_XA_WAVES
+#define MP_XA_WAVES 4
+#define MP_XA_KPW 4
+#endif
+constexpr int XA_WAVES = MP_XA_WAVES, XA_THREADS = XA_WAVES * 64, XA_KPW = MP_XA_KPW;  // keys in flight per wave
+constexpr int XA_V = D / 256;  // float4 per lane per 768-row: lane owns elements 4 lane + 256 i + (0..3)
+static_assert(XA_THREADS == MP_BLOCK, "XA workgroups ride in the O-projection launch (EPI_RESID_XA)");
+// Hand-off bound: polls of the x1 granules before an XA workgroup gives up (with
+// s_sleep between polls this is far beyond any O-projection's duration)
+constexpr unsigned HX_SPIN_LIMIT = 1u << 20;
+using gu64 = __attribute__((address_space(1))) unsigned long long;
+using gi32 = __attribute__((address_space(1))) int;
+
+// Split sp of slot b. HANDOFF: x1 comes from the O-projection in the same launch,
+// as {tag, value} granules xh[b][768] (EPI_RESID_XA): every wave sweeps all 768
+// with relaxed agent-scope loads (write-through producer stores, so no fence is
+// needed) until every tag matches, after its K'/V' rows are already in flight.
+template <bool HANDOFF>
+__device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned long long *xh, unsigned tag, int *err,
+                                        int dep, unsigned long long *ts = nullptr, unsigned long long t_start = 0) {
+    __shared__ float wm[XA_WAVES], wl[XA_WAVES];
+    __shared__ __attribute__((aligned(16))) float wo[XA_WAVES][D];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int Tb = p.T[b];
+    const int chunk = (Tb + XA_SPLITS - 1) / XA_SPLITS;
+    const int t0 = sp * chunk, t1 = min(Tb, t0 + chunk);
+    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * D;
+    const float *Kp = p.kp + base + 4 * lane + dep, *Vp = p.vp + base + 4 * lane;
+    float4 k[XA_KPW][XA_V], vv[XA_KPW][XA_V];
+#pragma unroll
+    for (int u = 0; u < XA_KPW; ++u) {
+        const int t = t0 + w + XA_WAVES * u;
+        const size_t r = (size_t)(t < t1 ? t : 0) * D;
+#pragma unroll
+        for (int i = 0; i < XA_V; ++i) {
+            k[u][i] = *(const float4 *)(Kp + r + 256 * i);
+            vv[u][i] = *(const float4 *)(Vp + r + 256 * i);
+        }
+    }
+    float4 h[XA_V];
+    {   // LN(x) (magpie.cpp:3513), every wave for itself (DPP statistics, no barrier)
+        float4 x4[XA_V], g4[XA_V];
+#pragma unroll
+        for (int i = 0; i < XA_V; ++i) g4[i] = *(const float4 *)(p.lnw + 4 * lane + 256 * i);
+        if constexpr (HANDOFF) {
+            gu64 *g = (gu64 *)(xh + (size_t)b * D);
+            float xv[D / 64];
+            for (unsigned spins = 0;; ++spins) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < D / 64; ++j) {
+                    const unsigned long long u = __hip_atomic_load(g + lane + 64 * j, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    xv[j] = __uint_as_float((unsigned)u);
+                    ok &= (unsigned)(u >> 32) == tag;
+                }
+                if (__all(ok)) break;
+                if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+                    if (lane == 0) __hip_atomic_store((gi32 *)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                    for (int j = 0; j < D / 64; ++j) xv[j] = __builtin_nanf("");
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            ts_mark(ts, t_start);  // profiling: when this wave saw all of x1
+            // to the float4 layout through this wave's own LDS row (reused for o below)
+#pragma unroll
+            for (int j = 0; j < D / 64; ++j) wo[w][lane + 64 * j] = xv[j];
+            wave_lds_sync();
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)&wo[w][4 * lane + 256 * i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)(p.x + (size_t)b * D + 4 * lane + 256 * i);
+        }
+        float v[4 * XA_V];
+#pragma unroll
+        for (int i = 0; i < XA_V; ++i) { v[4 * i] = x4[i].x; v[4 * i + 1] = x4[i].y; v[4 * i + 2] = x4[i].z; v[4 * i + 3] = x4[i].w; }
+        float mean, var;
+        wave_meanvar<4 * XA_V>(v, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+        for (int i = 0; i < XA_V; ++i)
+            h[i] = make_float4(((x4[i].x - mean) * rstd) * g4[i].x, ((x4[i].y - mean) * rstd) * g4[i].y,
+                               ((x4[i].z - mean) * rstd) * g4[i].z, ((x4[i].w - mean) * rstd) * g4[i].w);
+        if (p.q_f16)  // h . K'_t = q . K_t with q = W_q f16(h): the rounding commutes through K'
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i)
+                h[i] = make_float4((float)(_Float16)h[i].x, (float)(_Float16)h[i].y, (float)(_Float16)h[i].z,
+                                   (float)(_Float16)h[i].w);
+    }
+    const float scale = 1.0f / sqrtf((float)DXA);
+    float m = -INFINITY, l = 0.f;
+    float4 o[XA_V];
+#pragma unroll
+    for (int i = 0; i < XA_V; ++i) o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int tb = t0 + w; tb < t1; tb += XA_WAVES * XA_KPW) {
+#pragma unroll
+        for (int u = 0; u < XA_KPW; ++u) {
+            const int t = tb + XA_WAVES * u;
+            if (t >= t1) break;  // wave-uniform
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i) acc += dotv(k[u][i], h[i]);
+            const float sv = wave_sum(acc) * scale;
+            const float mn = fmaxf(m, sv), c = expf(m - mn), e = expf(sv - mn);
+            l = l * c + e;
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i) {
+                o[i].x = o[i].x * c + e * vv[u][i].x; o[i].y = o[i].y * c + e * vv[u][i].y;
+                o[i].z = o[i].z * c + e * vv[u][i].z; o[i].w = o[i].w * c + e * vv[u][i].w;
+            }
+            m = mn;
+        }
+        const int tn = tb + XA_WAVES * XA_KPW;
+        if (tn >= t1) break;
+#pragma unroll
+        for (int u = 0; u < XA_KPW; ++u) {  // next keys (long texts)
+            const int t = tn + XA_WAVES * u;
+            const size_t r = (size_t)(t < t1 ? t : 0) * D;
+#pragma unroll
+            for (int i = 0; i < XA_V; ++i) {
+                k[u][i] = *(const float4 *)(Kp + r + 256 * i);
+                vv[u][i] = *(const float4 *)(Vp + r + 256 * i);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < XA_V; ++i) *(float4 *)&wo[w][4 * lane + 256 * i] = o[i];
+    if (lane == 0) { wm[w] = m; wl[w] = l; }
+    lds_sync();
+    float M = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < XA_WAVES; ++q) M = fmaxf(M, wm[q]);
+    float den = 0.f, e[XA_WAVES];
+#pragma unroll
+    for (int q = 0; q < XA_WAVES; ++q) {
+        e[q] = wm[q] == -INFINITY ? 0.f : expf(wm[q] - M);
+        den += e[q] * wl[q];
+    }
+    float *pp = p.part + ((size_t)b * XA_SPLITS + sp) * XA_PART;
+    if (tid < D / 4) {
+        float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < XA_WAVES; ++q) {
+            const float4 v4 = *(const float4 *)&wo[q][4 * tid];
+            num.x += e[q] * v4.x; num.y += e[q] * v4.y; num.z += e[q] * v4.z; num.w += e[q] * v4.w;
+        }
+        *(float4 *)(pp + 4 + 4 * tid) = num;
+    }
+    if (tid == 0) { pp[0] = M; pp[1] = den; }
+}
+
+
+// EPI_RESID_XA epilogue, output (row n, slot b): resid += v, and the new x1 value
+// published as a {tag, value} granule with a relaxed agent-scope (write-through) store
+__device__ __forceinline__ void publish_x1(const GemvP &p, float v, int n, int b) {
+    float *r = p.resid + (size_t)b * D + n;
+    const float x1 = v + *r;
+    *r = x1;
+    const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+    __hip_atomic_store((gu64 *)(p.xh + (size_t)b * D + n), ((unsigned long long)tag << 32) | __float_as_uint(x1),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the launch's XA workgroups (blockIdx.x >= nrow_blocks): split k % XA_SPLITS of slot k / XA_SPLITS
+__device__ __forceinline__ void xa_tail(const GemvP &p, unsigned long long t_start) {
+    const int k = blockIdx.x - p.nrow_blocks;
+    xa_part<true>(p.xa, k % XA_SPLITS, k / XA_SPLITS, p.xh, (unsigned)p.iter[0] * 64u + p.layer + 1u, p.hx_err,
+                  ts_dep(t_start), p.ts, t_start);
+    ts_end(p.ts, t_start);
+}
+
+}  // namespace mp

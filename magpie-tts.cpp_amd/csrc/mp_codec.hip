@@ -33,6 +33,7 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include <string>
 #include <vector>
@@ -61,11 +62,12 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 struct ConvP {
     // per-branch (grid.z) operands
     const _Float16 *W[3];    // [Coutp][ks][Cinp] f16
+    const _Float16 *Wf[3];   // the same in MFMA A-fragment order [Coutp/16][Cinp/32][ks][64 lanes][8] (conv2)
     const float *bias[3];    // [Coutp] (zero padded)
-    const _Float16 *x[3];    // input activation [chunk][T][Cinp] f16 (already HalfSnake'd)
+    const _Float16 *x[3];    // input activation, block-major [chunk][Cinp/32][T][32] f16 (already HalfSnake'd)
     float *out[3];           // optional f32 output [chunk][T][Coutp]
     const float *resid[3];   // optional residual [chunk][T][Coutp]
-    _Float16 *act[3];        // optional f16 HalfSnake(output) for the next conv [chunk][T][Coutp]
+    _Float16 *act[3];        // optional f16 HalfSnake(output) for the next conv, block-major [chunk][Coutp/32][T][32]
     const float *act_alpha[3];
     int ks[3];
     const int *codes;        // IN_FSQ: [chunk][8][T]
@@ -86,6 +88,15 @@ __device__ __forceinline__ float half_snake(float v, int c, int n_snake, int cin
     }
     if (c < cin_real) return v > 0.f ? v : 0.01f * v;
     return 0.f;
+}
+
+// half_snake with the channel's alpha already in a register, both forms computed
+// and selected (no divergent branch; same arithmetic as half_snake)
+__device__ __forceinline__ float half_snake_sel(float v, int c, int n_snake, int cin_real, float a) {
+    const float s = __sinf(v * a);
+    const float snake = v + __fdividef(s * s, a);
+    const float leaky = v > 0.f ? v : 0.01f * v;
+    return c < n_snake ? snake : (c < cin_real ? leaky : 0.f);
 }
 
 // fsq_dequantize_cpu (nano-codec.cpp:721-752): channel c = 4*cb + d
@@ -156,7 +167,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
                     const int r = e >> 2, q = e & 3;
                     const int t = t0 - pad + r;
                     uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                    if (t >= 0 && t < p.T) v = *(const uint4 *)(xin + (size_t)t * p.Cinp + i0 + 8 * q);
+                    if (t >= 0 && t < p.T) v = *(const uint4 *)(xin + ((size_t)(i0 >> 5) * p.T + t) * 32 + 8 * q);
                     *(uint4 *)(xs[0] + r * ROWB + 16 * q) = v;
                 }
             }
@@ -192,7 +203,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
                 const int e = tid + 256 * u;
                 const int t = t0 - pad + (e >> 2);
                 xv[u] = make_uint4(0u, 0u, 0u, 0u);
-                if (e < items && t >= 0 && t < p.T) xv[u] = *(const uint4 *)(xin + (size_t)t * p.Cinp + i0 + 8 * (e & 3));
+                if (e < items && t >= 0 && t < p.T) xv[u] = *(const uint4 *)(xin + ((size_t)(i0 >> 5) * p.T + t) * 32 + 8 * (e & 3));
             }
         };
         load_blk(0);
@@ -245,8 +256,174 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
             h[1] = (_Float16)half_snake(v.y, o + 1, p.act_nsnake, p.cout_real, aal);
             h[2] = (_Float16)half_snake(v.z, o + 2, p.act_nsnake, p.cout_real, aal);
             h[3] = (_Float16)half_snake(v.w, o + 3, p.act_nsnake, p.cout_real, aal);
-            *(half4 *)(p.act[br] + off) = h;
+            *(half4 *)(p.act[br] + (size_t)chunk * p.T * p.Coutp + ((size_t)(o >> 5) * p.T + t) * 32 + (o & 31)) = h;
         }
+    }
+}
+
+// Wide-tile implicit-GEMM causal conv for the ResLayer convs (f16 operands):
+// RWV x CWV waves, each wave owns 32 output channels (2 A fragments) x 64 time
+// steps (4 B fragments), so every B fragment read from LDS feeds 2 MFMAs and every
+// A fragment 4. The tap count is a compile-time constant per branch (grid.z picks
+// the instantiation), so the tap loop is straight-line code: the B fragments of
+// tap k+1 are read while tap k's MFMAs run, and the A fragment of (block b, tap k)
+// is re-loaded for block b+1 right after its last use (one register set, a whole
+// block of lead time). Channel blocks are software-pipelined: block b+1's input
+// rows go to registers during block b's MFMAs, two LDS buffers, one barrier per
+// block. Accumulation order (block, tap ascending) equals conv_mfma_kernel's, so
+// the two kernels give the same bits.
+constexpr int C2_WR = 2, C2_NT = 4;
+template <int KS, int RWV, int CWV, int NCB, int R>
+__device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
+    constexpr int NTH = 64 * RWV * CWV;
+    constexpr int BN = CWV * 16 * C2_NT;
+    constexpr int ROWB = 80;             // LDS bytes per time row: 32 halves + 16 B pad
+    constexpr int MAXHALO = 50;          // (11 - 1) * 5
+    constexpr int BUFB = (BN + MAXHALO) * ROWB;
+    constexpr int RPT = ((BN + MAXHALO) * 4 + NTH - 1) / NTH;  // 16-byte row pieces per thread
+    const int br = blockIdx.z;
+    const int dil = p.dil;
+    const int pad = (KS - 1) * dil;
+    const int m0 = blockIdx.x * (RWV * 32);
+    const int chunk = blockIdx.y / p.tiles_per_chunk;
+    const int t0 = (blockIdx.y % p.tiles_per_chunk) * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rw = w % RWV, cw = w / RWV;
+    const int kg = lane >> 4, l16 = lane & 15;
+    const _Float16 *xin = p.x[br] + (size_t)chunk * p.T * p.Cinp;
+    // A fragment (16-row tile mt, channel block cb, tap k) = 1 KiB contiguous (Wf layout)
+    const _Float16 *wrow0 = p.Wf[br] + (size_t)((m0 >> 4) + rw * 2) * NCB * KS * 512 + lane * 8;
+    const _Float16 *wrow1 = wrow0 + (size_t)NCB * KS * 512;
+    const int rows = BN + pad, items = rows * 4;
+
+    floatx4 acc[C2_WR][C2_NT];
+#pragma unroll
+    for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+        for (int j = 0; j < C2_NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // A stream: step s = cb * KS + k (channel block, tap) is the 1 KiB fragment at
+    // wrow + s * 512. The channel-block loop is unrolled (NCB is a template
+    // argument), so the ring of R A-slots is indexed at compile time: step s + R is
+    // loaded into slot s % R right after step s's MFMAs (R steps of lead; R >= KS
+    // keeps every A wait behind loads issued before the next block's input rows,
+    // vmcnt being in order), and the compiler counts vmcnt exactly.
+    constexpr int NS = NCB * KS;
+    half8 ring[R][C2_WR];
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+        if (q < NS) {
+            ring[q][0] = *(const half8 *)(wrow0 + (size_t)q * 512);
+            ring[q][1] = *(const half8 *)(wrow1 + (size_t)q * 512);
+        }
+    uint4 xv[RPT];
+    auto load_x = [&](int cb) {
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int e = tid + NTH * u;
+            const int t = t0 - pad + (e >> 2);
+            xv[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (e < items && t >= 0 && t < p.T) xv[u] = *(const uint4 *)(xin + ((size_t)cb * p.T + t) * 32 + 8 * (e & 3));
+        }
+    };
+    load_x(0);
+    const int colb = cw * (16 * C2_NT) + l16;
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+        char *xb = xs + (cb & 1) * BUFB;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int e = tid + NTH * u;
+            if (e < items) *(uint4 *)(xb + (e >> 2) * ROWB + 16 * (e & 3)) = xv[u];
+        }
+        if (cb + 1 < NCB) load_x(cb + 1);
+        __syncthreads();
+        const char *bbase = xb + colb * ROWB + 16 * kg;
+        half8 bc[C2_NT], bn[C2_NT];
+#pragma unroll
+        for (int j = 0; j < C2_NT; ++j) bc[j] = *(const half8 *)(bbase + j * 16 * ROWB);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const int st = cb * KS + k;
+            if (k + 1 < KS) {
+#pragma unroll
+                for (int j = 0; j < C2_NT; ++j) bn[j] = *(const half8 *)(bbase + (j * 16 + (k + 1) * dil) * ROWB);
+            }
+#pragma unroll
+            for (int j = 0; j < C2_NT; ++j) {
+                acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][0], bc[j], acc[0][j], 0, 0, 0);
+                acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][1], bc[j], acc[1][j], 0, 0, 0);
+            }
+            if (st + R < NS) {
+                ring[st % R][0] = *(const half8 *)(wrow0 + (size_t)(st + R) * 512);
+                ring[st % R][1] = *(const half8 *)(wrow1 + (size_t)(st + R) * 512);
+            }
+            if (k + 1 < KS) {
+#pragma unroll
+                for (int j = 0; j < C2_NT; ++j) bc[j] = bn[j];
+            }
+        }
+    }
+    // ---- epilogue through LDS: the accumulator tile (C[row = 4*kg + r][col = l16] per
+    // fragment) is written as [time][channel] f32, then every thread handles 4
+    // consecutive channels of one time step in linear order, so bias / residual /
+    // output / f16 operand accesses are contiguous rows (the whole [t0, t0 + BN) x
+    // Coutp range when the tile spans every channel)
+    constexpr int BM = RWV * 32, CST = BM + 4;  // +4 floats: row stride off the bank period
+    float *ct = (float *)xs;
+    __syncthreads();  // every wave is done with the input buffers
+#pragma unroll
+    for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+        for (int j = 0; j < C2_NT; ++j)
+            *(floatx4 *)(ct + (colb + j * 16) * CST + rw * 32 + a * 16 + 4 * kg) = acc[a][j];
+    __syncthreads();
+    const size_t chunk_out = (size_t)chunk * p.T * p.Coutp;
+    // NTH is a multiple of BM / 4: every thread keeps the same 4 channels for the
+    // whole loop, so bias and HalfSnake alphas are loaded once (alpha arrays are
+    // zero-padded to Coutp at load, the HalfSnake select is branch-free)
+    static_assert(NTH % (BM / 4) == 0, "fixed channels per thread");
+    const int cl = (tid % (BM / 4)) * 4, o = m0 + cl;
+    const float4 bb = *(const float4 *)(p.bias[br] + o);
+    float al[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.act[br]) {
+        const float4 a4 = *(const float4 *)(p.act_alpha[br] + o);
+        al[0] = a4.x; al[1] = a4.y; al[2] = a4.z; al[3] = a4.w;
+    }
+    for (int tl = tid / (BM / 4); tl < BN; tl += NTH / (BM / 4)) {
+        const int t = t0 + tl;
+        if (t >= p.T) break;
+        const float4 a4 = *(const float4 *)(ct + tl * CST + cl);
+        float4 v = make_float4(a4.x + bb.x, a4.y + bb.y, a4.z + bb.z, a4.w + bb.w);
+        const size_t off = chunk_out + (size_t)t * p.Coutp + o;
+        if (p.resid[br]) {
+            const float4 r = *(const float4 *)(p.resid[br] + off);
+            v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;  // input + h (568-599)
+        }
+        if (p.out[br]) *(float4 *)(p.out[br] + off) = v;
+        if (p.act[br]) {  // the next conv's operand: f16(HalfSnake(v)) (ggml F16 im2col), block-major
+            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+            half4 h;
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) h[u] = (_Float16)half_snake_sel(vv[u], o + u, p.act_nsnake, p.cout_real, al[u]);
+            *(half4 *)(p.act[br] + chunk_out + ((size_t)(o >> 5) * p.T + t) * 32 + (o & 31)) = h;
+        }
+    }
+}
+
+// NCB = Cinp / 32 channel blocks (unrolled); DEEP: an A ring of max(KS, 6) slots
+// (a block or more of lead, for grids of about one wave per SIMD whose weights come
+// from the Infinity Cache) instead of 3 (occupancy-hidden latency, <= 128 VGPRs).
+template <int RWV, int CWV, int NCB, bool DEEP>
+__global__ __launch_bounds__(64 * RWV * CWV, DEEP ? 1 : 2) void conv2_kernel(ConvP p) {
+    constexpr int BN = CWV * 16 * C2_NT;
+    constexpr int XSB = 2 * (BN + 50) * 80, CTB = BN * (RWV * 32 + 4) * 4;  // input buffers / epilogue tile
+    __shared__ __attribute__((aligned(16))) char xs[XSB > CTB ? XSB : CTB];
+    switch (p.ks[blockIdx.z]) {
+        case 3: conv2_body<3, RWV, CWV, NCB, DEEP ? 6 : 3>(p, xs); break;
+        case 7: conv2_body<7, RWV, CWV, NCB, DEEP ? 7 : 3>(p, xs); break;
+        default: conv2_body<11, RWV, CWV, NCB, DEEP ? 11 : 3>(p, xs); break;
     }
 }
 
@@ -306,9 +483,11 @@ __global__ __launch_bounds__(256) void conv_transpose_kernel(ConvTP p) {
             }
             const size_t oo = ((size_t)chunk * p.Tin * p.s + t) * p.Coutp + g;
             p.out[oo] = acc;
+            // the f16 operands block-major [chunk][Coutp/32][T][32]
+            const size_t ob = (size_t)chunk * p.Tin * p.s * p.Coutp + ((size_t)(g >> 5) * p.Tin * p.s + t) * 32 + (g & 31);
 #pragma unroll
             for (int j = 0; j < 3; ++j)
-                p.act[j][oo] = (_Float16)half_snake(acc, g, p.cout_real / 2, p.cout_real, p.act_alpha[j]);
+                p.act[j][ob] = (_Float16)half_snake(acc, g, p.cout_real / 2, p.cout_real, p.act_alpha[j]);
         }
     }
 }
@@ -362,7 +541,7 @@ struct mp_codec {
     std::string err;
     hipStream_t stream = nullptr;
     // weights
-    struct Conv { _Float16 *w = nullptr; float *b = nullptr; int ks = 0, cin = 0, cout = 0, cinp = 0, coutp = 0; };
+    struct Conv { _Float16 *w = nullptr, *wf = nullptr; float *b = nullptr; int ks = 0, cin = 0, cout = 0, cinp = 0, coutp = 0; };
     Conv pre, rb[5][3][3][2];  // [stage][kernel j][dilation k][in/skip]
     float *rb_alpha[5][3][3][2] = {};
     float *up_alpha[5] = {}, *up_w[5] = {}, *up_b[5] = {};
@@ -417,6 +596,17 @@ int load_conv(mp_codec *c, const mp::Gguf &g, const std::string &wname, const st
     for (int o = 0; o < cout; ++o)
         for (int i = 0; i < cin; ++i)
             for (int k = 0; k < ks; ++k) wi[((size_t)o * ks + k) * cinp + i] = (_Float16)w[((size_t)o * cin + i) * ks + k];
+    // MFMA A-fragment order for conv2: [coutp/16][cinp/32][ks][lane = 16*kg + l16][8]
+    std::vector<_Float16> wf(wi.size());
+    const int ncb = cinp / 32;
+    for (int mt = 0; mt < coutp / 16; ++mt)
+        for (int cb = 0; cb < ncb; ++cb)
+            for (int k = 0; k < ks; ++k)
+                for (int ln = 0; ln < 64; ++ln)
+                    for (int e = 0; e < 8; ++e)
+                        wf[((((size_t)mt * ncb + cb) * ks + k) * 64 + ln) * 8 + e] =
+                            wi[((size_t)(mt * 16 + (ln & 15)) * ks + k) * cinp + cb * 32 + 8 * (ln >> 4) + e];
+    if (int rc = upload(c, &cv.wf, wf)) return rc;
     b.resize(coutp, 0.f);
     cv.ks = ks; cv.cin = cin; cv.cout = cout; cv.cinp = cinp; cv.coutp = coutp;
     if (int rc = upload(c, &cv.w, wi)) return rc;
@@ -446,9 +636,12 @@ int load_codec(mp_codec *c, const char *path) {
         for (int j = 0; j < 3; ++j)
             for (int k = 0; k < 3; ++k) {
                 const std::string p = "dec.rl." + std::to_string(i) + ".rb." + std::to_string(j) + ".rb." + std::to_string(k) + ".";
+                // alphas zero-padded to the padded channel count (conv2's epilogue loads 4 at a time)
                 if (int rc = load_f32(c, g, p + "in_act.alpha", C / 2, v)) return rc;
+                v.resize(CP[i], 0.f);
                 if (int rc = upload(c, &c->rb_alpha[i][j][k][0], v)) return rc;
                 if (int rc = load_f32(c, g, p + "sk_act.alpha", C / 2, v)) return rc;
+                v.resize(CP[i], 0.f);
                 if (int rc = upload(c, &c->rb_alpha[i][j][k][1], v)) return rc;
                 if (int rc = load_conv(c, g, p + "in_conv.weight", p + "in_conv.bias", C, C, KS[j], CP[i], CP[i], c->rb[i][j][k][0])) return rc;
                 if (int rc = load_conv(c, g, p + "sk_conv.weight", p + "sk_conv.bias", C, C, KS[j], CP[i], CP[i], c->rb[i][j][k][1])) return rc;
@@ -505,8 +698,30 @@ hipError_t launch_conv(const mpc::ConvP &p, int nchunk, int nbranch, hipStream_t
     return hipGetLastError();
 }
 
+template <int RWV, int CWV, int NCB, bool DEEP>
+hipError_t launch_conv2(mpc::ConvP p, int nchunk, int nbranch, hipStream_t s) {
+    constexpr int BN = CWV * 16 * mpc::C2_NT;
+    if (p.Cinp != NCB * 32) return hipErrorInvalidValue;
+    p.tiles_per_chunk = (p.T + BN - 1) / BN;
+    dim3 grid(p.Coutp / (RWV * 32), nchunk * p.tiles_per_chunk, nbranch);
+    hipLaunchKernelGGL((mpc::conv2_kernel<RWV, CWV, NCB, DEEP>), grid, dim3(64 * RWV * CWV), 0, s, p);
+    return hipGetLastError();
+}
+
 hipError_t run_conv(const mpc::ConvP &p, int BM, int mode, int nchunk, int nbranch, hipStream_t s) {
     using namespace mpc;
+    // ResLayer convs: the wide-tile kernel once a chunk fills at least half a tile
+    // (per-chunk length decides, so a chunk decodes the same alone or batched)
+    static const bool v1 = getenv("MAGPIE_CODEC_V1") != nullptr;  // A/B switch: the narrow-tile kernel only
+    if (mode == IN_F16 && !v1) {
+        switch (p.Coutp) {
+            case 448: if (p.T >= 64) return launch_conv2<2, 2, 14, true>(p, nchunk, nbranch, s); break;
+            case 224: if (p.T >= 128) return launch_conv2<1, 4, 7, true>(p, nchunk, nbranch, s); break;
+            case 128: if (p.T >= 64) return launch_conv2<4, 2, 4, false>(p, nchunk, nbranch, s); break;
+            case 64: if (p.T >= 128) return launch_conv2<2, 4, 2, false>(p, nchunk, nbranch, s); break;
+            case 32: if (p.T >= 128) return launch_conv2<1, 4, 1, false>(p, nchunk, nbranch, s); break;
+        }
+    }
     if (BM == 64) {
         if (mode == IN_FSQ) return launch_conv<64, 64, IN_FSQ>(p, nchunk, nbranch, s);
         return launch_conv<64, 64, IN_F16>(p, nchunk, nbranch, s);
@@ -550,7 +765,7 @@ int codec_run(mp_codec *c, int nchunk, int F) {
             ConvP p{};
             for (int j = 0; j < 3; ++j) {
                 const mp_codec::Conv &cv = c->rb[i][j][k][0];
-                p.W[j] = cv.w; p.bias[j] = cv.b; p.x[j] = c->a16[j]; p.out[j] = nullptr; p.resid[j] = nullptr;
+                p.W[j] = cv.w; p.Wf[j] = cv.wf; p.bias[j] = cv.b; p.x[j] = c->a16[j]; p.out[j] = nullptr; p.resid[j] = nullptr;
                 p.act[j] = c->b16[j]; p.act_alpha[j] = c->rb_alpha[i][j][k][1]; p.ks[j] = KS[j];
             }
             p.act_nsnake = C / 2; p.cout_real = C; p.Cinp = Cp; p.Coutp = Cp; p.T = T; p.dil = DIL[k];
@@ -559,7 +774,7 @@ int codec_run(mp_codec *c, int nchunk, int F) {
             // x' = x + conv_{ks_j, 1}(HS_sk(h)); plus the next block's operand HS_in(x')
             for (int j = 0; j < 3; ++j) {
                 const mp_codec::Conv &cv = c->rb[i][j][k][1];
-                p.W[j] = cv.w; p.bias[j] = cv.b; p.x[j] = c->b16[j];
+                p.W[j] = cv.w; p.Wf[j] = cv.wf; p.bias[j] = cv.b; p.x[j] = c->b16[j];
                 p.out[j] = c->brb[j]; p.resid[j] = k == 0 ? c->x0 : c->brb[j];
                 p.act[j] = k < 2 ? c->a16[j] : nullptr;
                 p.act_alpha[j] = k < 2 ? c->rb_alpha[i][j][k + 1][0] : nullptr;

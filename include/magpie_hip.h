@@ -99,6 +99,16 @@ int mp_hip_load_model(mp_dev *dev, const char *gguf_path);
  * MP_ERR_UNSUPPORTED for a file whose projections are not F16. */
 #define MP_WEIGHTS_F16 3
 int mp_hip_load_model_ex(mp_dev *dev, const char *gguf_path, int weight_mode);
+/* SA (self-attention) cache element type, applied from the next mp_hip_begin_batch.
+ * F32 is the reference's graph-reuse cache (magpie.cpp:3313-3376, f32 K/V tensors).
+ * BF16 stores every K and V row rounded to bf16 (round to nearest even) when it is
+ * appended, in the 110-frame prefill and every decode step, and every attention
+ * (prefill and decode) reads the rounded rows: half the cache bytes per step, which
+ * at batch 16 are about as many as the bf16 weights. No reference counterpart; the
+ * oracle's kv_bf16 mode restates it. Any weight mode. */
+#define MP_KV_F32 0
+#define MP_KV_BF16 1
+int mp_hip_set_kv_mode(mp_dev *dev, int kv_mode);
 int mp_hip_weight_mode(mp_dev *dev);
 int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes);
 /* replaces magpie_free (magpie.cpp:882-910) */

@@ -492,6 +492,101 @@ __global__ __launch_bounds__(256) void conv_transpose_kernel(ConvTP p) {
     }
 }
 
+// The same grouped ConvTranspose1d with the shape compile-time per stage: one thread
+// per (chunk, run of R input steps, output channel pair). The channel pair's 4
+// input channels arrive as one float4 per branch and step (the previous step kept in
+// registers), its 4 x 2s weights and all alphas stay in registers, outputs go out as
+// float2 (f32) and half2 (block-major f16 operands). Same arithmetic and summation
+// order as conv_transpose_kernel.
+template <int CINP, int COUTP, int S, bool AVG, int R>
+__global__ __launch_bounds__(256) void conv_transpose2_kernel(ConvTP p) {
+    constexpr int NG = COUTP / 2, K = 2 * S;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    const int gp = e % NG, rest = e / NG;
+    const int tiles = (p.Tin + R - 1) / R;
+    const int tt = rest % tiles, chunk = rest / tiles;
+    if (chunk >= p.nchunk) return;
+    const int g = 2 * gp, c0 = 2 * g;  // outputs g, g + 1 <- inputs c0 .. c0 + 3
+    const bool live0 = g < p.cout_real, live1 = g + 1 < p.cout_real;
+    float w[4][K];
+    float ia[4], bias0 = 0.f, bias1 = 0.f, oa[3][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = c0 + i;
+        const bool lv = i < 2 ? live0 : live1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) w[i][k] = lv ? p.w[(size_t)c * K + k] : 0.f;
+        ia[i] = c < p.n_snake ? p.alpha[c] : 0.f;
+    }
+    if (live0) bias0 = p.bias[g];
+    if (live1) bias1 = p.bias[g + 1];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        oa[j][0] = g < p.cout_real / 2 ? p.act_alpha[j][g] : 0.f;
+        oa[j][1] = g + 1 < p.cout_real / 2 ? p.act_alpha[j][g + 1] : 0.f;
+    }
+    const int nsn = p.cout_real / 2;
+    const size_t cin_base = (size_t)chunk * p.Tin * CINP;
+    auto load_in = [&](int tau, float *v) {  // HalfSnake(mean of the branches) of inputs c0..c0+3 at step tau
+        if (c0 >= CINP) {  // padded output pairs past the padded input (stage 2: 2 x 128 > 224)
+            v[0] = v[1] = v[2] = v[3] = 0.f;
+            return;
+        }
+        const size_t xo = cin_base + (size_t)tau * CINP + c0;
+        float4 a = *(const float4 *)(p.x + xo);
+        if constexpr (AVG) {
+            const float4 b = *(const float4 *)(p.xa + xo), d = *(const float4 *)(p.xb + xo);
+            a.x = ((a.x + b.x) + d.x) * (1.0f / 3.0f);
+            a.y = ((a.y + b.y) + d.y) * (1.0f / 3.0f);
+            a.z = ((a.z + b.z) + d.z) * (1.0f / 3.0f);
+            a.w = ((a.w + b.w) + d.w) * (1.0f / 3.0f);
+        }
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = half_snake_sel(av[i], c0 + i, p.n_snake, p.cin_real, ia[i]);
+    };
+    const int tau0 = tt * R;
+    float prev[4] = {0.f, 0.f, 0.f, 0.f}, cur[4];
+    if (tau0 >= 1) load_in(tau0 - 1, prev);
+    const int Tout = p.Tin * S;
+    const size_t cout_base = (size_t)chunk * Tout * COUTP;
+    const size_t act_base = cout_base + (size_t)(g >> 5) * Tout * 32 + (g & 31);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int tau = tau0 + r;
+        if (tau >= p.Tin) break;
+        load_in(tau, cur);
+#pragma unroll
+        for (int u = 0; u < S; ++u) {
+            const int t = tau * S + u;
+            float a0 = 0.f, a1 = 0.f;
+            // ggml order: channel c outer, tau = t/s - 1 then t/s inner
+#pragma unroll
+            for (int ci = 0; ci < 2; ++ci) {
+                if (tau >= 1) {
+                    a0 += prev[ci] * w[ci][u + S];
+                    a1 += prev[2 + ci] * w[2 + ci][u + S];
+                }
+                a0 += cur[ci] * w[ci][u];
+                a1 += cur[2 + ci] * w[2 + ci][u];
+            }
+            if (live0) a0 += bias0;
+            if (live1) a1 += bias1;
+            *(float2 *)(p.out + cout_base + (size_t)t * COUTP + g) = make_float2(a0, a1);
+            typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                half2v h;
+                h[0] = (_Float16)half_snake_sel(a0, g, nsn, p.cout_real, oa[j][0]);
+                h[1] = (_Float16)half_snake_sel(a1, g + 1, nsn, p.cout_real, oa[j][1]);
+                *(half2v *)(p.act[j] + act_base + (size_t)t * 32) = h;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) prev[i] = cur[i];
+    }
+}
+
 // HalfSnake(post) -> causal conv 27->1 k3 (f16 operands, ggml_conv_1d) -> +b -> tanh
 // (nano-codec.cpp:702-712) on the 3-branch mean of the last ResLayer.
 struct PostP {
@@ -753,10 +848,16 @@ int codec_run(mp_codec *c, int nchunk, int F) {
         tp.w = c->up_w[i]; tp.bias = c->up_b[i]; tp.out = c->x0; tp.cout_real = C; tp.Coutp = Cp;
         for (int j = 0; j < 3; ++j) { tp.act[j] = c->a16[j]; tp.act_alpha[j] = c->rb_alpha[i][j][0][0]; }
         tp.Tin = T; tp.s = RATE[i]; tp.nchunk = nchunk;
-        const size_t total = (size_t)nchunk * T * Cp;
-        const int grid = (int)std::min<size_t>((total + 255) / 256, 65536);
-        if (i == 0) hipLaunchKernelGGL(conv_transpose_kernel<false>, dim3(grid), dim3(256), 0, s, tp);
-        else hipLaunchKernelGGL(conv_transpose_kernel<true>, dim3(grid), dim3(256), 0, s, tp);
+        // R input steps per thread: 1 on the short early stages (threads), 4 later (re-reads)
+        const int R = i == 0 ? 1 : i == 1 ? 2 : 4;
+        const dim3 g2((nchunk * ((T + R - 1) / R) * (Cp / 2) + 255) / 256);
+        switch (i) {
+            case 0: hipLaunchKernelGGL((conv_transpose2_kernel<896, 448, 8, false, 1>), g2, dim3(256), 0, s, tp); break;
+            case 1: hipLaunchKernelGGL((conv_transpose2_kernel<448, 224, 8, true, 2>), g2, dim3(256), 0, s, tp); break;
+            case 2: hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4>), g2, dim3(256), 0, s, tp); break;
+            case 3: hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, 4>), g2, dim3(256), 0, s, tp); break;
+            default: hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, 4>), g2, dim3(256), 0, s, tp); break;
+        }
         CHK(hipGetLastError());
         T *= RATE[i];
         const int BM = BMS[i], BN = BM == 64 ? 64 : 128;

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 // (softmax(K q / 8) V per head, 3457-3476). At batch 1 that is 48 workgroups of
 // ~L/4 keys each instead of one workgroup streaming a whole head.
 constexpr int SA_WAVES = 8, SA_THREADS = SA_WAVES * 64, SA_IF = 4;  // iterations in flight
+template <bool KV16>
 __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     const int h = blockIdx.x, sp = blockIdx.y, b = blockIdx.z;
@@ -127,8 +128,8 @@ __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
             // keys past the split re-read its last row (an L1/L2 hit, no extra HBM
             // traffic); rows < max_seq are valid memory: no load waits for the mask
             const int j = min(j0 + 4 * (w + SA_WAVES * (r0 + u)) + kk, max(j1 - 1, 0));
-            k4[u] = *(const float4 *)(p.kc + base + (size_t)j * D);
-            v4[u] = *(const float4 *)(p.vc + base + (size_t)j * D);
+            k4[u] = kv_load4<KV16>(p.kc, base + (size_t)j * D);
+            v4[u] = kv_load4<KV16>(p.vc, base + (size_t)j * D);
         }
         float sv[SA_IF];
         float mb = -INFINITY;
@@ -326,7 +327,8 @@ hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
     if (!p.q || !p.kc || !p.vc || !p.pos || !p.part || p.max_seq < 1 || p.max_seq > NCH_MAX * SA_CHUNK)
         return hipErrorInvalidValue;
-    mp::launch(sa_attn_kernel, dim3(NH, SA_SPLITS, B), dim3(SA_THREADS), 0, s, p);
+    if (p.kv16) mp::launch(sa_attn_kernel<true>, dim3(NH, SA_SPLITS, B), dim3(SA_THREADS), 0, s, p);
+    else mp::launch(sa_attn_kernel<false>, dim3(NH, SA_SPLITS, B), dim3(SA_THREADS), 0, s, p);
     return hipGetLastError();
 }
 

@@ -285,6 +285,27 @@ template <> struct vecf<4> { using T = float4; };
 template <> struct vecf<2> { using T = float2; };
 template <> struct vecf<1> { using T = float; };
 
+// SA cache element store / load (MP_KV_BF16: bf16, round to nearest even on the
+// f32 bits; K/V values are finite). The cache pointer is typed float in both modes.
+__device__ __forceinline__ unsigned short f32_to_bf16_rne(float v) {
+    const unsigned u = __float_as_uint(v);
+    return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ void kv_store(float *c, size_t i, float v, int kv16) {
+    if (kv16) ((unsigned short *)c)[i] = f32_to_bf16_rne(v);
+    else c[i] = v;
+}
+__device__ __forceinline__ float4 bf16x4_to_f32(uint2 u) {
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xFFFF0000u));
+}
+// 4 consecutive cache elements starting at element i (i a multiple of 4)
+template <bool KV16>
+__device__ __forceinline__ float4 kv_load4(const float *c, size_t i) {
+    if constexpr (KV16) return bf16x4_to_f32(*(const uint2 *)((const unsigned short *)c + i));
+    else return *(const float4 *)(c + i);
+}
+
 __device__ __forceinline__ float dotv(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
 __device__ __forceinline__ float dotv(float2 a, float2 b) { return a.x * b.x + a.y * b.y; }
 __device__ __forceinline__ float dotv(float a, float b) { return a * b; }

@@ -624,8 +624,7 @@ __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b,
     else if constexpr (EPI == EPI_QKV) {
         const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + p.pos[b]) * D;
         if (n < D) p.out[(size_t)b * D + n] = v;
-        else if (n < 2 * D) p.kc[slot + n - D] = v;
-        else p.vc[slot + n - 2 * D] = v;
+        else kv_store(n < 2 * D ? p.kc : p.vc, slot + (n < 2 * D ? n - D : n - 2 * D), v, p.kv16);
     } else if constexpr (EPI == EPI_LTKVO) {
         if (n < LTD) p.lk[(size_t)b * NCB * LTD + n] = v;
         else p.lv[(size_t)b * NCB * LTD + n - LTD] = v;

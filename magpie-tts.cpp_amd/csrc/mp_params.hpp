@@ -195,7 +195,8 @@ struct GemvP {
     unsigned short *out_b16;        // EPI_GELU_B16
     float *resid;
     const float *addsrc;
-    float *kc, *vc;
+    float *kc, *vc;      // SA cache; bf16 elements when kv16 (mp_hip_set_kv_mode)
+    int kv16;
     int max_seq;
     float *lq, *lk, *lv;
     // early exit once every slot is done (count >= nslots)
@@ -245,9 +246,10 @@ struct XaQ8P {
 
 struct AttnP {  // decode self-attention (one query per utterance)
     const float *q;
-    const float *kc, *vc;
+    const float *kc, *vc;    // bf16 elements when kv16
     int layer, nlayers, max_seq;
     const int *pos;
+    int kv16;
     float *part;         // [B][NH][SA_SPLITS][SA_PART] partial softmax states over key splits
                          // (merged in the O-projection's PRO_SA_MERGE prologue)
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks

@@ -30,8 +30,7 @@ __device__ __forceinline__ void gemm_store1(const GemmP &p, int m, int n, float 
     else if constexpr (EPI == GE_QKV_CACHE) {
         const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.max_seq + t) * D;
         if (n < D) p.C[(size_t)m * p.ldc + n] = v;
-        else if (n < 2 * D) p.kc[slot + n - D] = v;
-        else p.vc[slot + n - 2 * D] = v;
+        else kv_store(n < 2 * D ? p.kc : p.vc, slot + (n < 2 * D ? n - D : n - 2 * D), v, p.kv16);
     } else if constexpr (EPI == GE_XAKV) {
         const size_t slot = ((size_t)(b * p.nlayers + p.layer) * p.Tmax + t) * DXA;
         if (n < DXA) p.xak[slot + n] = v;
@@ -225,6 +224,7 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const float *X, int ldx, c
 // Keys for row (b, t) are rows j <= t of the same utterance, read through
 // (kbase, vbase) + b * utt_stride + j * row_stride + h * 64.
 
+template <bool KV16>
 __global__ __launch_bounds__(256) void row_attn_kernel(RowAttnP p) {
     __shared__ float pr[4][TMAX_LIMIT];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -234,13 +234,12 @@ __global__ __launch_bounds__(256) void row_attn_kernel(RowAttnP p) {
     const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
     const int nk = t + 1;
     const float *q = p.Q + (size_t)m * p.ldq + h * DH;
-    const float *Kb = p.Kb + b * p.utt_stride + h * DH;
-    const float *Vb = p.Vb + b * p.utt_stride + h * DH;
+    const size_t kb0 = b * p.utt_stride + h * DH;
     float mx = -INFINITY;
     for (int j = lane; j < nk; j += 64) {
-        const float *k = Kb + (size_t)j * p.row_stride;
+        const size_t k = kb0 + (size_t)j * p.row_stride;
         float s = 0.f;
-        for (int d = 0; d < DH; d += 4) s += dotv(*(const float4 *)(q + d), *(const float4 *)(k + d));
+        for (int d = 0; d < DH; d += 4) s += dotv(*(const float4 *)(q + d), kv_load4<KV16>(p.Kb, k + d));
         s *= 0.125f;
         pr[w][j] = s;
         mx = fmaxf(mx, s);
@@ -251,7 +250,10 @@ __global__ __launch_bounds__(256) void row_attn_kernel(RowAttnP p) {
     l = wave_sum(l);
     __builtin_amdgcn_wave_barrier();
     float o = 0.f;
-    for (int j = 0; j < nk; ++j) o += pr[w][j] * Vb[(size_t)j * p.row_stride + lane];
+    for (int j = 0; j < nk; ++j) {
+        const size_t vi = kb0 + (size_t)j * p.row_stride + lane;
+        o += pr[w][j] * (KV16 ? __uint_as_float((unsigned)((const unsigned short *)p.Vb)[vi] << 16) : p.Vb[vi]);
+    }
     p.O[(size_t)m * D + h * DH + lane] = o / l;
 }
 
@@ -408,7 +410,8 @@ hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s)
     return hipGetLastError();
 }
 hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s) {
-    hipLaunchKernelGGL(row_attn_kernel, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
+    if (p.kv16) hipLaunchKernelGGL(row_attn_kernel<true>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(row_attn_kernel<false>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 hipError_t pre_row_xa(const RowXaP &p, hipStream_t s) {

@@ -28,7 +28,8 @@ struct GemmP {
                        //    W re-laid out tap-major [N][k][Cin] at load
     int rows_per_utt;  // for (b, t) decomposition of a row
     const int *T;      // valid rows per utterance (conv zero padding / masking)
-    float *kc, *vc;
+    float *kc, *vc;    // bf16 elements when kv16
+    int kv16;
     int layer, nlayers, max_seq;
     float *xak, *xav;
     int Tmax;
@@ -60,6 +61,7 @@ struct RowAttnP {
     int M, rows_per_utt, heads;
     int key_limit_T;  // 1: also mask keys j >= T[b] (unused when causal suffices)
     const int *T;
+    int kv16;         // Kb / Vb hold bf16 elements (the SA cache in MP_KV_BF16 mode)
 };
 
 // Cross-attention for a block of rows (1 head x 128, no mask).

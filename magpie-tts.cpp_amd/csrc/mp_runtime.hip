@@ -226,6 +226,8 @@ struct mp_dev {
     // batch configuration
     int B = 0, NB = 0, Tmax = 0, max_steps = 0, max_seq = 0, nch = 0;
     mp_params params{};
+    int kv_mode = MP_KV_F32;  // mp_hip_set_kv_mode: applies from the next mp_hip_begin_batch
+    int kv16 = 0;             // the current batch's SA cache holds bf16
     // device state (one allocation per buffer, sized for the configuration)
     std::vector<void *> allocs;
     float *x = nullptr, *x2 = nullptr, *kp = nullptr, *vp = nullptr, *q = nullptr, *sa_out = nullptr,
@@ -702,7 +704,9 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
     A(xh, (size_t)NB * D);
-    A(kc, (size_t)NB * L * dev->max_seq * D); A(vc, (size_t)NB * L * dev->max_seq * D);
+    dev->kv16 = dev->kv_mode == MP_KV_BF16;
+    const size_t kvn = (size_t)NB * L * dev->max_seq * D;  // elements; bf16 mode: 2 per float slot
+    A(kc, dev->kv16 ? kvn / 2 : kvn); A(vc, dev->kv16 ? kvn / 2 : kvn);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
@@ -774,7 +778,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // LN + QKV (+ frame embedding on layer 0) + KV append   (3415-3442)
         g.W = W.qkv; g.Wb = b16 ? m.pk_qkv[l] : nullptr; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
         g.Wq = W.qkv8.q; g.Wd = W.qkv8.d;
-        g.kc = dev->kc; g.vc = dev->vc;
+        g.kc = dev->kc; g.vc = dev->vc; g.kv16 = dev->kv16;
         // layer 0 embeds the frame (2746-2787) in the prologue; batches of 8+ embed it once
         // in a separate launch instead of in every workgroup (the same arithmetic)
         const bool embed_in = l == 0 && NB < 8;
@@ -795,7 +799,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
                           (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
         }
         // self-attention over the cache, one workgroup per (head, slot) (3457-3476)
-        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->sa_part};
+        mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->kv16, dev->sa_part};
         if (record) {
             mp::OpRec r{};
             r.name = "sa_attn"; r.kind = mp::K_ATTN; r.a = a; r.B = NB;
@@ -1195,13 +1199,18 @@ int run_preamble(mp_dev *dev) {
         HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_self, dev->pH, 768, Mc, m.eps, s));
         GemmP gp{};
         gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.Wq = W.qkv8.q; gp.Wd = W.qkv8.d; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Mc; gp.N = 2304; gp.K = 768;
-        gp.rows_per_utt = CTX; gp.kc = dev->kc; gp.vc = dev->vc; gp.layer = l; gp.nlayers = L; gp.max_seq = dev->max_seq;
+        gp.rows_per_utt = CTX; gp.kc = dev->kc; gp.vc = dev->vc; gp.kv16 = dev->kv16; gp.layer = l; gp.nlayers = L;
+        gp.max_seq = dev->max_seq;
         HIPCHK(pre_gemm(gp, GE_QKV_CACHE, s));
         RowAttnP ra{};
         ra.Q = dev->pQKV; ra.ldq = 2304;
-        ra.Kb = dev->kc + (size_t)l * dev->max_seq * 768; ra.Vb = dev->vc + (size_t)l * dev->max_seq * 768;
+        {   // layer l's rows, offset in cache elements (bf16 elements in MP_KV_BF16 mode)
+            const size_t off = (size_t)l * dev->max_seq * 768;
+            ra.Kb = dev->kv16 ? (const float *)((const unsigned short *)dev->kc + off) : dev->kc + off;
+            ra.Vb = dev->kv16 ? (const float *)((const unsigned short *)dev->vc + off) : dev->vc + off;
+        }
         ra.utt_stride = (size_t)L * dev->max_seq * 768; ra.row_stride = 768; ra.O = dev->pATT; ra.M = Mc;
-        ra.rows_per_utt = CTX; ra.heads = 12; ra.T = dev->T;
+        ra.rows_per_utt = CTX; ra.heads = 12; ra.T = dev->T; ra.kv16 = dev->kv16;
         HIPCHK(pre_row_attn(ra, s));
         gp = GemmP{};
         gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.Wq = W.o8.q; gp.Wd = W.o8.d; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 768;
@@ -1316,6 +1325,12 @@ int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *wei
 
 int mp_hip_weight_mode(mp_dev *dev) { return dev && dev->loaded ? dev->m.weight_mode : MP_ERR_STATE; }
 
+int mp_hip_set_kv_mode(mp_dev *dev, int kv_mode) {
+    if (!dev || (kv_mode != MP_KV_F32 && kv_mode != MP_KV_BF16)) return MP_ERR_ARG;
+    dev->kv_mode = kv_mode;
+    return MP_OK;
+}
+
 void mp_hip_free(mp_dev *dev) {
     if (!dev) return;
     hipSetDevice(dev->device);
@@ -1369,7 +1384,8 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     const bool same = dev->NB > 0 && dev->B == B && dev->Tmax == Tmax && dev->max_steps == max_steps &&
                       (dev->trace != nullptr) == trace && dev->params.ignore_eos == params->ignore_eos &&
                       (dev->params.temperature >= 0.01f) == (params->temperature >= 0.01f) &&
-                      dev->params.emit_eos_frame == params->emit_eos_frame;
+                      dev->params.emit_eos_frame == params->emit_eos_frame &&
+                      dev->kv16 == (dev->kv_mode == MP_KV_BF16);
     dev->params = *params;
     if (!same) {
         if (int rc = alloc_batch(dev, B, Tmax, max_steps, trace)) return rc;
@@ -1708,8 +1724,8 @@ int64_t mp_hip_debug_buffer(mp_dev *dev, const char *name, void *host, int64_t b
     if (n == "enc_out") { src = dev->enc_out; sz = NB * T * 768 * 4; }
     else if (n == "xak") { src = dev->xak; sz = NB * L * T * 128 * 4; }
     else if (n == "xav") { src = dev->xav; sz = NB * L * T * 128 * 4; }
-    else if (n == "kc") { src = dev->kc; sz = NB * L * S * 768 * 4; }
-    else if (n == "vc") { src = dev->vc; sz = NB * L * S * 768 * 4; }
+    else if (n == "kc") { src = dev->kc; sz = NB * L * S * 768 * (dev->kv16 ? 2 : 4); }
+    else if (n == "vc") { src = dev->vc; sz = NB * L * S * 768 * (dev->kv16 ? 2 : 4); }
     else if (n == "x") { src = dev->x; sz = NB * 768 * 4; }
     else return fail(dev, MP_ERR_ARG, "unknown buffer " + n);
     if (host) {

@@ -64,6 +64,7 @@ SYMBOLS = [
     ("mp_hip_load_model", _I, [_P, ctypes.c_char_p]),
     ("mp_hip_load_model_ex", _I, [_P, ctypes.c_char_p, _I]),
     ("mp_hip_weight_mode", _I, [_P]),
+    ("mp_hip_set_kv_mode", _I, [_P, _I]),
     ("mp_hip_model_info", _I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_size_t)]),
     ("mp_hip_free", None, [_P]),
     ("mp_hip_error", ctypes.c_char_p, [_P]),
@@ -170,14 +171,20 @@ class Device:
 
     WEIGHT_MODES = {"f32": 0, "as_stored": 0, "bf16": 1, "q8": 2, "q4": 2, "f16": 3}
 
-    def __init__(self, model_path: str, device: int = 0, weights: str = "f32"):
+    KV_MODES = {"f32": 0, "bf16": 1}
+
+    def __init__(self, model_path: str, device: int = 0, weights: str = "f32", kv: str = "f32"):
         """weights: "f32" (as stored, widened to f32), "bf16" (decode projections
         on bf16 MFMA, activations rounded to bf16; batches up to 16) or "q8" / "q4"
         (the file's Q8_0 / Q4_0 tensors kept as int8 (Q4_0: q - 8, losslessly),
         multiplied with ggml's semantics: activations quantised to Q8_0 per
         32-block, integer dots scaled by d_w * d_a; batches up to 8) or "f16" (an
         F16 file with ggml's F16 mul_mat semantics: activations rounded to f16,
-        decode projections on f16 MFMA; batches up to 16)."""
+        decode projections on f16 MFMA; batches up to 16).
+        kv: SA cache element type, "f32" (the reference's) or "bf16" (rows rounded
+        to bf16 on append, mp_hip_set_kv_mode)."""
+        if kv not in self.KV_MODES:
+            raise ValueError(f"kv must be one of {sorted(self.KV_MODES)}")
         if weights not in self.WEIGHT_MODES:
             raise ValueError(f"weights must be one of {sorted(self.WEIGHT_MODES)}")
         self.lib = load_library()
@@ -188,6 +195,8 @@ class Device:
         self.h = h
         self.weights = weights
         self._check(self.lib.mp_hip_load_model_ex(self.h, model_path.encode(), self.WEIGHT_MODES[weights]))
+        self.kv = kv
+        self._check(self.lib.mp_hip_set_kv_mode(self.h, self.KV_MODES[kv]))
 
     def _check(self, rc: int) -> None:
         if rc != MP_OK:

@@ -424,6 +424,19 @@ static void free_half(orc_model *m) {
     m->half = 0;
 }
 
+// SA cache element type (this build's MP_KV_BF16, include/magpie_hip.h): every K and V
+// row rounded to bf16 (round to nearest even) as it is appended to the cache, in the
+// 110-frame prefill and every decode step; attention reads the rounded rows.
+static int g_kv_bf16 = 0;
+void orc_set_kv_bf16(int on) { g_kv_bf16 = on != 0; }
+static inline float round_bf16(float v) {
+    uint32_t u;
+    memcpy(&u, &v, 4);
+    u = (u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u;
+    memcpy(&v, &u, 4);
+    return v;
+}
+
 int orc_set_weight_mode(orc_model *m, int mode) {
     if (!m || mode < 0 || mode > 3) return -1;
     free_half(m);
@@ -590,6 +603,11 @@ static void decoder_layer(const orc_model *m, dstate *s, int l, float *x, int M,
     for (int r = 0; r < M; ++r) {
         memcpy(Kc + (size_t)(pos0 + r) * d, qkv + (size_t)r * 3 * d + d, sizeof(float) * d);
         memcpy(Vc + (size_t)(pos0 + r) * d, qkv + (size_t)r * 3 * d + 2 * d, sizeof(float) * d);
+        if (g_kv_bf16)
+            for (int i = 0; i < d; ++i) {
+                Kc[(size_t)(pos0 + r) * d + i] = round_bf16(Kc[(size_t)(pos0 + r) * d + i]);
+                Vc[(size_t)(pos0 + r) * d + i] = round_bf16(Vc[(size_t)(pos0 + r) * d + i]);
+            }
     }
     causal_mha(qkv, M, d, m->dec_heads, att, pos0, Kc, Vc);
     matmul_sel(m, L->o, hm ? L->o_h : NULL, NULL, att, o, M, d, d);

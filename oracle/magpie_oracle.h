@@ -44,6 +44,8 @@ orc_model *orc_load(const char *gguf_path);
 // prefill, decode steps, LT in_proj/layer/heads): src1 rounded to f16, products
 // exact, f32/f64 accumulation; -1 if the file has no F16 tensor.
 int orc_set_weight_mode(orc_model *m, int mode);
+/* SA cache rounded to bf16 on append (MP_KV_BF16); process-wide, default off. */
+void orc_set_kv_bf16(int on);
 void orc_free(orc_model *m);
 int orc_dec_layers(const orc_model *m);
 

@@ -39,6 +39,7 @@ def lib() -> ctypes.CDLL:
         L.orc_encode.argtypes = [P, P, I, P]
         L.orc_synthesize_forced.argtypes = [P, P, I, I, I, I, ctypes.c_float, I, ctypes.c_uint64, I, P, P, P, P]
         L.orc_set_weight_mode.argtypes = [P, I]
+        L.orc_set_kv_bf16.argtypes = [I]
         L.orc_lt_sample.argtypes = [P, P, ctypes.c_float, I, I, ctypes.c_uint64, I, I, P, P, P]
         L.orc_draw_u.restype = ctypes.c_float
         L.orc_draw_u.argtypes = [ctypes.c_uint64, I, I, I]
@@ -55,6 +56,11 @@ def lib() -> ctypes.CDLL:
 
 def set_mode(acc64: bool = True, gelu_f16: bool = False, threads: int = 0) -> None:
     lib().orc_set_mode(int(acc64), int(gelu_f16), int(threads))
+
+
+def set_kv_bf16(on: bool) -> None:
+    """SA cache rows rounded to bf16 on append (the GPU's MP_KV_BF16 mode)."""
+    lib().orc_set_kv_bf16(int(on))
 
 
 def draw_u(seed: int, stream: int, step: int, cb: int) -> float:

@@ -69,7 +69,7 @@ def measure_extra(model_path: str, codec_path, args) -> dict:
     """Throughput of the BASELINE configs' other shapes on this one GPU (fixed-length
     greedy decode, same synthetic prompts): bf16 projections at batch 1, 8
     (configs[3]'s per-GPU share of batch 64) and 16 (configs[2]); Q8_0 weights at
-    batch 1 and 60 s of long-form streaming (configs[4]); and the streaming path
+    batch 1 and 16 (int8 MFMA) and 60 s of long-form streaming (configs[4]); and the streaming path
     (sentence streaming, 4-frame codec chunks): time to first audio and real-time
     factor of one utterance."""
     out = {}
@@ -99,6 +99,9 @@ def measure_extra(model_path: str, codec_path, args) -> dict:
     tok1 = [ma.synthetic_tokens(args.tokens, seed=1000)]
     dev.synthesize(tok1, speakers=[0], max_dec_steps=args.frames, ignore_eos=True)
     out["q8_batch1_fps"] = round(_decode_fps(dev, 1, args.frames), 1)
+    toks16 = [ma.synthetic_tokens(args.tokens, seed=1000 + b) for b in range(16)]
+    dev.synthesize(toks16, speakers=[b % 5 for b in range(16)], max_dec_steps=args.frames, ignore_eos=True)
+    out["q8_batch16_fps"] = round(_decode_fps(dev, 16, args.frames), 1)
     if codec_path:
         cdc = ma.Codec(codec_path)
         sents = [ma.synthetic_tokens(40, seed=5000 + i) for i in range(6)]

@@ -110,6 +110,10 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *gguf_path, int weight_mode);
 #define MP_KV_BF16 1
 int mp_hip_set_kv_mode(mp_dev *dev, int kv_mode);
 int mp_hip_weight_mode(mp_dev *dev);
+/* the largest batch mp_hip_begin_batch accepts for the loaded model: 16 in the
+ * bf16 / F16 modes and for a Q8_0 / Q4_0 file whose decode projections are all
+ * quantised, else 8 (negative MP_ERR_* without a model) */
+int mp_hip_max_batch(mp_dev *dev);
 int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *weight_bytes);
 /* replaces magpie_free (magpie.cpp:882-910) */
 void mp_hip_free(mp_dev *dev);

@@ -323,7 +323,7 @@ int magpie_synthesize_streaming(magpie_context *ctx, magpie_codec *codec, const 
     ctx->temperature = params.temperature;
     ctx->top_k = params.top_k;
     ctx->speaker_id = params.speaker_id;
-    const int bmax = mp_hip_weight_mode(ctx->model.dev) == MP_WEIGHTS_BF16 ? 16 : 8;
+    const int bmax = std::max(1, mp_hip_max_batch(ctx->model.dev));
     const int P = std::max(1, std::min(params.max_parallel_sentences, bmax));
     long long total = 0;
     for (size_t s0 = 0; s0 < sents.size(); s0 += P) {

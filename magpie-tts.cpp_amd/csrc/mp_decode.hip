@@ -1,4 +1,5 @@
-// Per-frame decode kernels for gfx950 (f32 path, batch NB <= 8 utterances).
+// Per-frame decode kernels for gfx950 (f32 path, batch NB <= 8 utterances;
+// the F32 FFN convs of a Q8_0 file also at 16).
 //
 // One decode iteration = 12 decoder layers (magpie_build_decoder_layer_gpu_cached,
 // magpie.cpp:3484-3528) + the 8-codebook local transformer
@@ -43,8 +44,13 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     constexpr int VW = K >= 256 ? 4 : K / 64;
     constexpr int NV = K / (64 * VW);
     using VT = typename vecf<VW>::T;
-    constexpr int SC = pro_scratch<NB, PRO>();
-    __shared__ __attribute__((aligned(16))) float act[NB * K];
+    // rows too wide for LDS at 16 slots (PRO_PLAIN, K = 3072: 192 KB) are staged
+    // 8 slots at a time against the same weight registers; per (row, slot) the
+    // arithmetic is the same at every batch size
+    constexpr int NBS = (PRO == PRO_PLAIN && NB * K > 32768) ? NB / 2 : NB;
+    static_assert(NBS == NB || PRO == PRO_PLAIN, "only plain rows are staged in halves");
+    constexpr int SC = pro_scratch<NBS, PRO>();
+    __shared__ __attribute__((aligned(16))) float act[NBS * K];
     __shared__ float red[8];
     __shared__ float sc[SC];
 
@@ -60,19 +66,29 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) wv[r][i] = wr[lane + 64 * i];
     }
-    prologue<NB, K, PRO>(p, act, red, sc);
     float acc[RW][NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        VT av[NV];
+    for (int hh = 0; hh < NB / NBS; ++hh) {
+        if constexpr (NBS == NB) {
+            prologue<NB, K, PRO>(p, act, red, sc);
+        } else {
+            if (hh) lds_sync();  // every wave is done with the previous slots' rows
+            GemvP ph = p;
+            ph.src = p.src + (size_t)hh * NBS * p.src_ld;
+            prologue<NBS, K, PRO>(ph, act, red, sc);
+        }
 #pragma unroll
-        for (int i = 0; i < NV; ++i) av[i] = ((const VT *)(act + b * K))[lane + 64 * i];
+        for (int b = 0; b < NBS; ++b) {
+            VT av[NV];
 #pragma unroll
-        for (int r = 0; r < RW; ++r) {
-            float s = 0.f;
+            for (int i = 0; i < NV; ++i) av[i] = ((const VT *)(act + b * K))[lane + 64 * i];
 #pragma unroll
-            for (int i = 0; i < NV; ++i) s += dotv(wv[r][i], av[i]);
-            acc[r][b] = wave_sum(s);
+            for (int r = 0; r < RW; ++r) {
+                float s = 0.f;
+#pragma unroll
+                for (int i = 0; i < NV; ++i) s += dotv(wv[r][i], av[i]);
+                acc[r][hh * NBS + b] = wave_sum(s);
+            }
         }
     }
     // acc[][] is wave-uniform: lane r*NB + b owns output (row0 + r, slot b), so the
@@ -322,6 +338,9 @@ MP_DECODE_OPS(8)
 hipError_t op_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 1, D, PRO_PLAIN, EPI_BIAS>(p, s); }
 // bf16 weight mode at 16 slots: only the f32 LT in_proj runs on the GEMV family
 hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, D, PRO_LN, EPI_BIAS>(p, s); }
+// Q8_0 weight mode at 16 slots: the FFN convs (F32 in the reference's Q8 file)
+hipError_t op_ff1_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 2, D, PRO_LN, EPI_GELU>(p, s); }
+hipError_t op_ff2_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 
 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {
@@ -472,6 +491,7 @@ hipError_t op_lt_ffn(const LtFfnP &p, int NB, hipStream_t s) {
     case 2: mp::launch(lt_ffn_kernel<2>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
     case 4: mp::launch(lt_ffn_kernel<4>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
     case 8: mp::launch(lt_ffn_kernel<8>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
+    case 16: mp::launch(lt_ffn_kernel<16>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -483,6 +503,7 @@ hipError_t op_lt_merge(const LtFfnP &p, int NB, hipStream_t s) {
     case 2: mp::launch(lt_merge_kernel<2>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
     case 4: mp::launch(lt_merge_kernel<4>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
     case 8: mp::launch(lt_merge_kernel<8>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
+    case 16: mp::launch(lt_merge_kernel<16>, dim3(1), dim3(MP_BLOCK), 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

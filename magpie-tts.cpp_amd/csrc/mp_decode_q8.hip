@@ -1,4 +1,4 @@
-// Q8_0 weight mode of the decode projections (gfx950), batch NB <= 8.
+// Q8_0 weight mode of the decode projections (gfx950) on int8 MFMA, batch NB <= 16.
 //
 // The reference's Q8 GGUF stores the attention / cross-attention / LT
 // projections as Q8_0 blocks (scripts/convert_magpie_to_gguf.py:155-176: per 32
@@ -6,20 +6,27 @@
 // quantised mul_mat: the activation row is itself quantised to Q8_0
 // (quantize_row_q8_0_ref: d = amax/127, id = 1/d, q = roundf(x*id), d kept as
 // fp16) and every block contributes its exact integer dot times d_w * d_a
-// (ggml_vec_dot_q8_0_q8_0). This file computes exactly that, per
-// decode step, as a weight-streaming GEMV:
+// (ggml_vec_dot_q8_0_q8_0). This file computes exactly that per
+// decode step as a skinny GEMM on v_mfma_i32_16x16x32_i8:
 //
-//  * weights stay int8 in HBM (1 B/param + 2 B per 32: 34/32 B/param as in the
-//    file, 26 % of f32), repacked once at load into int8 [N][K] + fp16 scales
-//    [N][K/32] so each lane streams a 16-byte half block (one 1 KiB coalesced
-//    wave-instruction over rows that are contiguous in memory);
+//  * one MFMA = one Q8_0 block: A = 16 weight rows x 32 int8 (the block), B =
+//    32 int8 x 16 utterance columns (columns >= NB read a zero row), D = the 256
+//    exact int32 block dots; the block scales are applied in f32 as the
+//    accumulator is updated (acc += (float)sumi * (d_w * d_a)), so the int8 ->
+//    real dequantisation is fused into the MFMA loop and no weight is ever
+//    widened in memory;
+//  * weights stay int8 in HBM (34/32 B per param as in the file), repacked once
+//    at load into fragment order [N/16][K/64][64 lanes][16 B] (lane l: row l&15,
+//    8 bytes of block 2j and 8 of block 2j+1 at k-offset 8(l>>4)): every
+//    wave-instruction of the weight stream is one contiguous 1 KiB
+//    global_load_dwordx4; the scales likewise [N/16][K/64][4][2 blocks x 4 rows]
+//    fp16, one 16-byte load per lane per two blocks;
 //  * the prologue (LN / frame embedding / LT pick + gather / LT attention,
-//    shared with the f32 and bf16 families, mp_fused.hpp) builds the f32
-//    activation rows in LDS, then 32 lanes per block quantise them to Q8_0 in
-//    LDS (amax by DPP);
-//  * the two halves of a block (adjacent lanes) are dotted with v_dot4c_i32_i8
-//    and summed exactly by one DPP swap, scaled by d_w * d_a, and accumulated
-//    per output row; rows are then reduced across the wave by DPP.
+//    shared with the f32 and 16-bit families, mp_fused.hpp) builds the f32
+//    activation rows in LDS, then 4 lanes per block quantise them to Q8_0 in LDS;
+//  * a workgroup owns one 16-row tile, its 4 waves split K and reduce in LDS in a
+//    fixed order: every output's arithmetic is independent of NB, so a batch
+//    reproduces its utterances run alone bit for bit.
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -30,86 +37,130 @@
 
 namespace mp {
 
-// Rows [row0, row0 + R) of W are R*K contiguous bytes: 16-byte chunk c = lane +
-// 64 j of the wave belongs to row c / (K/16), half block (c % (K/16)) of it.
-template <int NB, int K, int R, int PRO, int EPI>
-__global__ __launch_bounds__(MP_BLOCK) void gemv_q8_kernel(GemvP p) {
-    constexpr int CPR = K / 16;    // 16-byte chunks per row
-    constexpr int NBLK = K / 32;   // Q8_0 blocks per row
-    constexpr int J = R * CPR / 64;
-    static_assert(R * CPR % 64 == 0, "a wave's rows must fill whole wave-instructions");
-    static_assert(R * NB <= 64, "one lane per output");
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef int intx4 __attribute__((ext_vector_type(4)));
+
+// max over the 4 lanes of a DPP quad
+__device__ __forceinline__ float quad_max(float v) {
+    v = fmaxf(v, dpp_mov<0xB1>(v));
+    return fmaxf(v, dpp_mov<0x4E>(v));
+}
+
+template <int NB, int K, int PRO, int EPI>
+__global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
+    const unsigned long long t_start = ts_begin(p.ts);
+    static_assert(NB >= 1 && NB <= 16, "one 16-column MFMA tile of utterances");
+    static_assert(K % 256 == 0, "K splits into 4 waves x 64-wide block pairs");
+    constexpr int KP = K / 64, KW = KP / MP_NWAVES, NBLK = K / 32;
+    constexpr int QS = K + 16;  // padded int8 row: the 16 column rows spread over the banks
     constexpr int SC = pro_scratch<NB, PRO>();
     __shared__ __attribute__((aligned(16))) float act[NB * K];
-    __shared__ __attribute__((aligned(16))) signed char actq[NB * K];
-    __shared__ float actd[NB * NBLK];
+    __shared__ __attribute__((aligned(16))) signed char actq[(NB + 1) * QS];
+    __shared__ float actd[(NB + 1) * NBLK];
+    __shared__ __attribute__((aligned(16))) floatx4 part[MP_NWAVES][64];
     __shared__ float red[8];
     __shared__ float sc[SC];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = blockIdx.x;
 
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int row0 = (blockIdx.x * MP_NWAVES + w) * R;
-    // the weight stream (and its scales) does not depend on the prologue: issue it first
-    uint4 wv[J];
-    float ws[J];
+    // this wave's weight fragments and their scales, issued before the prologue
+    const uint4 *wf = (const uint4 *)p.Wq + ((size_t)rt * KP + w * KW) * 64 + lane + ts_dep(t_start);
+    const uint4 *sf = (const uint4 *)p.Wd + ((size_t)rt * KP + w * KW) * 4 + (lane >> 4);
+    uint4 a[KW], sd[KW];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int c = lane + 64 * j;
-        const int n = min(row0 + c / CPR, p.N - 1);
-        wv[j] = *(const uint4 *)(p.Wq + (size_t)n * K + (c % CPR) * 16);
-        ws[j] = __half2float(__ushort_as_half(p.Wd[(size_t)n * NBLK + (c % CPR) / 2]));
-    }
+    for (int i = 0; i < KW; ++i) { a[i] = wf[(size_t)i * 64]; sd[i] = sf[(size_t)i * 4]; }
+
     prologue<NB, K, PRO>(p, act, red, sc);
 
-    // activation rows -> Q8_0 (quantize_row_q8_0_ref), 32 lanes per block
-    {
-        const int e = lane & 31;
-        for (int blk = 2 * w + (lane >> 5); blk < NB * NBLK; blk += 2 * MP_NWAVES) {
-            const float x = act[blk * 32 + e];
-            float a = row_max16(fabsf(x));
-            a = fmaxf(a, __shfl_xor(a, 16, 64));
-            const float dd = a / 127.0f;
-            const float id = dd != 0.f ? 1.0f / dd : 0.0f;
-            actq[blk * 32 + e] = (signed char)(int)roundf(x * id);
-            if (e == 0) actd[blk] = __half2float(__float2half(dd));
-        }
-        lds_sync();
+    // activation rows -> Q8_0 (quantize_row_q8_0_ref), 4 lanes x 8 elements per block;
+    // row NB is zero (q = 0, d = 0) and feeds MFMA columns NB..15
+    for (int e = tid; e < (QS + 4 * NBLK) / 4; e += MP_BLOCK) {
+        if (e < QS / 4) ((int *)(actq + NB * QS))[e] = 0;
+        else actd[NB * NBLK + (e - QS / 4)] = 0.f;
     }
+    for (int blk = (tid >> 2); blk < NB * NBLK; blk += MP_BLOCK / 4) {
+        const int b = blk / NBLK, kb = blk % NBLK, e8 = 8 * (lane & 3);
+        const float4 x0 = *(const float4 *)(act + b * K + kb * 32 + e8);
+        const float4 x1 = *(const float4 *)(act + b * K + kb * 32 + e8 + 4);
+        float am = fmaxf(fmaxf(fmaxf(fabsf(x0.x), fabsf(x0.y)), fmaxf(fabsf(x0.z), fabsf(x0.w))),
+                         fmaxf(fmaxf(fabsf(x1.x), fabsf(x1.y)), fmaxf(fabsf(x1.z), fabsf(x1.w))));
+        am = quad_max(am);
+        const float dd = am / 127.0f;
+        const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        unsigned qw[2] = {0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qw[j >> 2] |= ((unsigned)(int)roundf(xs[j] * id) & 0xFFu) << (8 * (j & 3));
+        *(uint2 *)(actq + b * QS + kb * 32 + e8) = make_uint2(qw[0], qw[1]);
+        if ((lane & 3) == 0) actd[blk] = __half2float(__float2half(dd));
+    }
+    lds_sync();
+    ts_mark(p.ts, t_start);  // profiling: activation tile quantised
 
-    float acc[R][NB];
+    const int c = min(lane & 15, NB);
+    const signed char *bq = actq + c * QS + 8 * (lane >> 4);
+    const float *bd = actd + c * NBLK;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int i = 0; i < KW; ++i) {
+        const int kp = w * KW + i;
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[r][b] = 0.f;
+        for (int h = 0; h < 2; ++h) {
+            const int kc = 2 * kp + h;
+            const long av = h ? (long)(((unsigned long)a[i].w << 32) | a[i].z)
+                              : (long)(((unsigned long)a[i].y << 32) | a[i].x);
+            const long bv = *(const long *)(bq + kc * 32);
+            const intx4 zero = {0, 0, 0, 0};
+            const intx4 s = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv, zero, 0, 0, 0);
+            const float da = bd[kc];
+            const unsigned dlo = h ? sd[i].z : sd[i].x, dhi = h ? sd[i].w : sd[i].y;  // rows 4g..4g+3
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int c = lane + 64 * j;
-        const int r = c / CPR, kc = c % CPR;
-        const int r_lo = (64 * j) / CPR, r_hi = (64 * j + 63) / CPR;  // rows this wave-instruction touches
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int4 a4 = *(const int4 *)(actq + b * K + kc * 16);
-            int s = __builtin_amdgcn_sdot4((int)wv[j].x, a4.x, 0, false);
-            s = __builtin_amdgcn_sdot4((int)wv[j].y, a4.y, s, false);
-            s = __builtin_amdgcn_sdot4((int)wv[j].z, a4.z, s, false);
-            s = __builtin_amdgcn_sdot4((int)wv[j].w, a4.w, s, false);
-            s += __builtin_amdgcn_update_dpp(0, s, 0xB1, 0xF, 0xF, false);  // + the other half of the block
-            const float f = (lane & 1) ? 0.f : (float)s * (ws[j] * actd[b * NBLK + (kc >> 1)]);
-#pragma unroll
-            for (int rr = r_lo; rr <= r_hi; ++rr) acc[rr][b] += (r == rr) ? f : 0.f;
+            for (int r = 0; r < 4; ++r) {
+                const unsigned wd = r < 2 ? dlo : dhi;
+                const float dw = __half2float(__ushort_as_half((unsigned short)((r & 1) ? wd >> 16 : wd & 0xFFFFu)));
+                acc[r] += (float)s[r] * (dw * da);
+            }
         }
     }
-    float v = 0.f;
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const float t = wave_sum(acc[r][b]);
-            if (lane == r * NB + b) v = t;
-        }
-    if (lane >= R * NB) return;
-    const int b = lane % NB, n = row0 + lane / NB;
+    part[w][lane] = acc;
+    lds_sync();
+    // thread t -> (row t/16, column t%16); D[row][col] sits in lane (row/4)*16 + col, register row%4
+    const int row = tid >> 4, col = tid & 15;
+    if (col >= NB) return;
+    const int ls = (row >> 2) * 16 + col, rg = row & 3;
+    const float v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
+    const int n = rt * 16 + row;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
+    epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
+    ts_end(p.ts, t_start);
+}
+
+// int8 [N][K] + fp16 scales [N][K/32] (the file's blocks) -> fragment order:
+// q [ceil(N/16)][K/64][64][16 B], d [ceil(N/16)][K/64][4][8 fp16]; rows >= N zero
+__global__ void pack_q8_kernel(const signed char *q, const unsigned short *d, int N, int K, unsigned char *oq,
+                               unsigned short *od) {
+    const int KP = K / 64;
+    const size_t total = (size_t)((N + 15) / 16) * KP * 64;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(e % 64), g = lane >> 4;
+        const size_t frag = e / 64;
+        const int kp = (int)(frag % KP), rt = (int)(frag / KP);
+        const int n = rt * 16 + (lane & 15);
+        for (int j = 0; j < 16; ++j) {
+            const int k = kp * 64 + (j >> 3) * 32 + 8 * g + (j & 7);
+            oq[e * 16 + j] = n < N ? (unsigned char)q[(size_t)n * K + k] : 0;
+        }
+        if ((lane & 15) == 0)
+            for (int j = 0; j < 8; ++j) {
+                const int r = rt * 16 + 4 * g + (j & 3), blk = 2 * kp + (j >> 2);
+                od[(frag * 4 + g) * 8 + j] = r < N ? d[(size_t)r * (K / 32) + blk] : 0;
+            }
+    }
+}
+hipError_t pack_q8(const signed char *q, const unsigned short *d, int N, int K, unsigned char *oq,
+                   unsigned short *od, hipStream_t s) {
+    if (!q || !d || !oq || !od || N <= 0 || K % 256) return hipErrorInvalidValue;
+    mp::launch(pack_q8_kernel, dim3(1024), dim3(256), 0, s, q, d, N, K, oq, od);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- fused Q8 XA tail
@@ -118,8 +169,8 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_q8_kernel(GemvP p) {
 // does attention + o_net + residual: grid (768/64, B), a workgroup owns 64 rows
 // of o_net and recomputes the slot's attention over the text (K, V: 2 x T x 128
 // f32, coalesced: half a wave per key row), quantises it to Q8_0 and finishes
-// x2 = x + Q8(o_net) a for its rows with gemv_q8<.., 128, 8, PRO_PLAIN,
-// EPI_ADD_STORE>'s arithmetic. The o_net rows are issued first.
+// x2 = x + Q8(o_net) a for its rows (v_dot4 per half block: the exact int32
+// block dots, times d_w * d_a). The o_net rows are issued first.
 constexpr int XQ8_ROWS = 64;  // o_net rows per workgroup
 __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
     constexpr int OR = 8, OCPR = DXA / 16;                 // o_net: groups of 8 rows
@@ -264,37 +315,38 @@ static bool q8_args_ok(const GemvP &p) {
     return ok;
 }
 
-template <int NB, int K, int R, int PRO, int EPI>
+template <int NB, int K, int PRO, int EPI>
 static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     if (!q8_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
-    const int rows = MP_NWAVES * R;
-    mp::launch((gemv_q8_kernel<NB, K, R, PRO, EPI>), dim3((p.N + rows - 1) / rows), dim3(MP_BLOCK), 0, s, p);
+    mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
 // Named entry points of the Q8_0 projections of one decode iteration (the
 // pos_ff conv weights stay F32 in the reference's Q8 file and run on the f32
-// GEMV family), instantiated for NB in {1, 2, 4, 8}.
+// GEMV family), instantiated for NB in {1, 2, 4, 8, 16}.
 #define MP_Q8_OPS(NB)                                                                                                  \
-    hipError_t q8_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_EMBED_LN, EPI_QKV>(p, s); } \
-    hipError_t q8_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_QKV>(p, s); }             \
-    hipError_t q8_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_SA_MERGE, EPI_RESID>(p, s); }      \
-    hipError_t q8_xq_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_STORE>(p, s); }            \
-    hipError_t q8_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, 4, PRO_LN, EPI_BIAS>(p, s); }         \
-    hipError_t q8_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
-    hipError_t q8_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LTARG_ATTN, EPI_LTX_ADD>(p, s); } \
-    hipError_t q8_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
-    hipError_t q8_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, 4, PRO_PLAIN, EPI_BIAS>(p, s); }
+    hipError_t q8_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
+    hipError_t q8_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
+    hipError_t q8_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }      \
+    hipError_t q8_xq_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_LN, EPI_STORE>(p, s); }            \
+    hipError_t q8_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_LN, EPI_BIAS>(p, s); }         \
+    hipError_t q8_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
+    hipError_t q8_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_LTARG_ATTN, EPI_LTX_ADD>(p, s); } \
+    hipError_t q8_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
+    hipError_t q8_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }
 
 MP_Q8_OPS(1)
 MP_Q8_OPS(2)
 MP_Q8_OPS(4)
 MP_Q8_OPS(8)
+MP_Q8_OPS(16)
 // LT in_proj of a caller-supplied normalised hidden (magpie_local_transformer_sample_all)
-hipError_t q8_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_q8<1, D, 4, PRO_PLAIN, EPI_BIAS>(p, s); }
+hipError_t q8_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_q8<1, D, PRO_PLAIN, EPI_BIAS>(p, s); }
 // o_net + residual after lt_pick_kernel (large batches)
-hipError_t q8_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_q8<8, LTD, 4, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
+hipError_t q8_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_q8<8, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
+hipError_t q8_lt_bo_16(const GemvP &p, hipStream_t s) { return launch_q8<16, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 // the LT head at batch 1 with the LT FFN merge as its prologue (lt_ffn_kernel)
-hipError_t q8_lt_em_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, 4, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
+hipError_t q8_lt_em_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 
 }  // namespace mp

@@ -83,6 +83,12 @@ MP_DECL_Q8(1)
 MP_DECL_Q8(2)
 MP_DECL_Q8(4)
 MP_DECL_Q8(8)
+MP_DECL_Q8(16)
+hipError_t q8_lt_bo_16(const GemvP &, hipStream_t);
+hipError_t op_ff1_16(const GemvP &, hipStream_t);
+hipError_t op_ff2_16(const GemvP &, hipStream_t);
+hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
+hipError_t pack_q8(const signed char *, const unsigned short *, int, int, unsigned char *, unsigned short *, hipStream_t);
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
 hipError_t q8_lt_em_1(const GemvP &, hipStream_t);
 hipError_t op_lt_pick(const GemvP &, int, hipStream_t);
@@ -113,7 +119,10 @@ struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_
 #define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, \
                        op_oproj_xa_##NB }
-static const OpTable kTables[4] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8)};
+// 16 slots in the f32 family only for a Q8_0 file's F32 tensors: its FFN convs and LT in_proj
+static const OpTable kTables[5] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8),
+                                   {nullptr, nullptr, nullptr, op_ff1_16, nullptr, op_ff2_16, op_lt_in0_16, nullptr,
+                                    nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}};
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
 #define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, nullptr, b16_ff1_##NB, b16_ff2_##NB, \
                            op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_bg_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
@@ -130,7 +139,8 @@ static const OpTable kTablesF16[5] = {MP_TABLE_F16(1), MP_TABLE_F16(2), MP_TABLE
 struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, lt_in0, lt_a, lt_bg, lt_b, lt_e; };
 #define MP_TABLE_Q8(NB) { q8_qkv_embed_##NB, q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_lt_in0_##NB, \
                           q8_lt_a_##NB, q8_lt_bg_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
-static const OpTableQ8 kTablesQ8[4] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8)};
+static const OpTableQ8 kTablesQ8[5] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8),
+                                        MP_TABLE_Q8(16)};
 static int nb_index(int NB) { return NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : NB == 8 ? 3 : 4; }
 // the 16-bit MFMA family serves the bf16 and F16 weight modes
 static bool h16_mode(int weight_mode) { return weight_mode == MP_WEIGHTS_BF16 || weight_mode == MP_WEIGHTS_F16; }
@@ -139,14 +149,21 @@ static const OpTable &table_for(int NB, int weight_mode) {
            : weight_mode == MP_WEIGHTS_BF16 ? kTablesB16[nb_index(NB)]
                                             : kTables[nb_index(NB)];
 }
-static const OpTableQ8 &table_q8(int NB) { return kTablesQ8[nb_index(NB) < 4 ? nb_index(NB) : 3]; }
+static const OpTableQ8 &table_q8(int NB) { return kTablesQ8[nb_index(NB)]; }
 
-// A Q8_0 tensor as stored (weight mode MP_WEIGHTS_Q8): int8 [N][K] + fp16 scales [N][K/32]
+// A Q8_0 tensor (weight mode MP_WEIGHTS_Q8): as stored, int8 [N][K] + fp16 scales
+// [N][K/32] (the preamble GEMMs), and for the decode projections also in int8 MFMA
+// fragment order (pq, pd: mp_decode_q8.hip)
 struct QW {
     const signed char *q = nullptr;
     const unsigned short *d = nullptr;
+    const signed char *pq = nullptr;
+    const unsigned short *pd = nullptr;
     explicit operator bool() const { return q != nullptr; }
 };
+// bytes of a packed Q8_0 tensor: fragments and scales
+static size_t q8p_qbytes(int N, int K) { return (size_t)((N + 15) / 16) * (K / 64) * 1024; }
+static size_t q8p_dbytes(int N, int K) { return (size_t)((N + 15) / 16) * (K / 64) * 64; }
 
 struct EncLayerW { const float *norm_self, *qkv, *o, *norm_ff, *ff1, *ff2; QW qkv8, o8; };
 struct DecLayerW {
@@ -178,8 +195,9 @@ struct Model {
                          *pk_lt_out = nullptr,  // lt_out: [8][127 tiles][8][64][8]
                          *pk_lt_in = nullptr;   // F16 mode only: the LT in_proj [256][768]
     // weight mode MP_WEIGHTS_Q8: the file's Q8_0 tensors as stored (ggml's quantised mul_mat)
-    void *q8_arena = nullptr;
+    void *q8_arena = nullptr, *q8p_arena = nullptr;
     size_t q8_bytes = 0;
+    bool q8_all = false;  // every decode projection is Q8_0 / Q4_0: batches up to 16
     QW lt_in8, lt_qkv8, lt_o8, lt_out8;  // lt_out8: [8][2024][256] (+ [8][2024][8] scales)
     float *arena = nullptr;
     size_t arena_bytes = 0;
@@ -681,8 +699,48 @@ int load_q8(mp_dev *dev, const char *path) {
         HIPCHK(hipMemcpy(dq, hq.data(), n, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(dd, hd.data(), n / 32 * 2, hipMemcpyHostToDevice));
     }
+    // the decode projections once more in int8 MFMA fragment order
+    struct Dec { mp::QW *w; int N, K, heads; };
+    std::vector<Dec> dec;
+    bool all = true;
+    auto add = [&](mp::QW &w, int N, int K, int heads) {
+        if (w) dec.push_back({&w, N, K, heads});
+        else all = false;
+    };
+    for (int l = 0; l < m.dec_layers; ++l) {
+        add(m.dec[l].qkv8, 2304, 768, 1);
+        add(m.dec[l].o8, 768, 768, 1);
+        add(m.dec[l].xq8, 128, 768, 1);
+        if (!m.dec[l].xo8) all = false;
+    }
+    add(m.lt_in8, 256, 768, 1);
+    add(m.lt_qkv8, 768, 256, 1);
+    add(m.lt_o8, 256, 256, 1);
+    add(m.lt_out8, 2024, 256, 8);
+    size_t ptotal = 0;
+    for (auto &d : dec) ptotal += d.heads * (align_up(mp::q8p_qbytes(d.N, d.K)) + align_up(mp::q8p_dbytes(d.N, d.K)));
+    if (m.q8p_arena) { hipFree(m.q8p_arena); m.q8p_arena = nullptr; }
+    if (ptotal) HIPCHK(hipMalloc(&m.q8p_arena, ptotal));
+    char *pc = (char *)m.q8p_arena;
+    for (auto &d : dec) {
+        const size_t qb = align_up(mp::q8p_qbytes(d.N, d.K)), db = align_up(mp::q8p_dbytes(d.N, d.K));
+        signed char *oq = (signed char *)pc;
+        pc += d.heads * qb;
+        unsigned short *od = (unsigned short *)pc;
+        pc += d.heads * db;
+        for (int h = 0; h < d.heads; ++h)
+            HIPCHK(mp::pack_q8(d.w->q + (size_t)h * d.N * d.K, d.w->d + (size_t)h * d.N * (d.K / 32), d.N, d.K,
+                               (unsigned char *)oq + h * qb, (unsigned short *)((char *)od + h * db), nullptr));
+        d.w->pq = oq;
+        d.w->pd = od;
+    }
+    HIPCHK(hipDeviceSynchronize());
+    m.q8_all = all;
     return MP_OK;
 }
+// stride between the 8 packed LT heads (fragments, scales), as laid out above
+static size_t q8p_head_q() { return (mp::q8p_qbytes(2024, 256) + 255) & ~(size_t)255; }
+static size_t q8p_head_d() { return (mp::q8p_dbytes(2024, 256) + 255) & ~(size_t)255; }
 
 // ------------------------------------------------------------------ batch state
 int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
@@ -767,6 +825,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             r.name = name; r.kind = mp::K_GEMV; r.fn = fn; r.g = g; r.B = NB; r.bytes = bytes;
             dev->ops.push_back(r);
         }
+        if (!fn) return fail(dev, MP_ERR_UNSUPPORTED, std::string(name) + ": no kernel for this batch size / weight mode");
         HIPCHK(fn(g, s));
         return MP_OK;
     };
@@ -777,7 +836,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.layer = l;
         // LN + QKV (+ frame embedding on layer 0) + KV append   (3415-3442)
         g.W = W.qkv; g.Wb = b16 ? m.pk_qkv[l] : nullptr; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
-        g.Wq = W.qkv8.q; g.Wd = W.qkv8.d;
+        g.Wq = W.qkv8.pq; g.Wd = W.qkv8.pd;
         g.kc = dev->kc; g.vc = dev->vc; g.kv16 = dev->kv16;
         // layer 0 embeds the frame (2746-2787) in the prologue; batches of 8+ embed it once
         // in a separate launch instead of in every workgroup (the same arithmetic)
@@ -810,7 +869,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.part = dev->sa_part;
-        g.Wq = W.o8.q; g.Wd = W.o8.d;
+        g.Wq = W.o8.pq; g.Wd = W.o8.pd;
         mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
         xp.q_f16 = m.weight_mode == MP_WEIGHTS_F16;
         const double xa_bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
@@ -828,7 +887,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             // cross-attention with Q8_0 q_net / o_net, as ggml computes it (1713-1767):
             // q = Q8(q_net) LN(x) (GEMV), then x2 = x + Q8(o_net) attn(q, K, V) (xa_q8_kernel)
             g = gemv_base(dev); g.layer = l;
-            g.W = W.xq; g.Wq = W.xq8.q; g.Wd = W.xq8.d; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
+            g.W = W.xq; g.Wq = W.xq8.pq; g.Wd = W.xq8.pd; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
             g.out = dev->xqb; g.out_ld = 128;
             if ((rc = run("xq", tq.xq, g, Fq * (128.0 * 768) + A * act * (768 + 128))) != MP_OK) return rc;
             mp::XaQ8P xq{dev->x, dev->x2, dev->xqb, W.xo8.q, W.xo8.d, dev->xak, dev->xav, dev->T, dev->Tmax, l, L};
@@ -919,6 +978,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             r.name = name; r.kind = mp::K_GEMV; r.fn = fn; r.g = g; r.B = NB; r.bytes = bytes;
             ops->push_back(r);
         }
+        if (!fn) return fail(dev, MP_ERR_UNSUPPORTED, std::string(name) + ": no kernel for this batch size / weight mode");
         HIPCHK(fn(g, s));
         dump_lt(io, s);
         return MP_OK;
@@ -939,7 +999,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     {
         mp::GemvP g = base();
         g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.out = io.lt_s; g.out_ld = 9 * 256;
-        g.Wq = m.lt_in8.q; g.Wd = m.lt_in8.d; g.Wb = m.pk_lt_in;  // pk_lt_in: F16 mode only
+        g.Wq = m.lt_in8.pq; g.Wd = m.lt_in8.pd; g.Wb = m.pk_lt_in;  // pk_lt_in: F16 mode only
         const double Fi = m.lt_in8 ? Fq : m.pk_lt_in ? 2.0 : A;
         if (io.lt_only) {
             // in_proj of the caller's (already normalised) hidden (1161-1163)
@@ -1014,14 +1074,14 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             // position 0 (the hidden's in_proj): LN + q|k|v GEMV, then attention + o_net
             g = base(); g.cb = 0;
             g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX;
-            g.Wq = m.lt_qkv8.q; g.Wd = m.lt_qkv8.d;
+            g.Wq = m.lt_qkv8.pq; g.Wd = m.lt_qkv8.pd;
             g.lnw = m.lt_norm_self; g.lq = io.ltq; g.lk = io.ltk; g.lv = io.ltv;
             if ((rc = run("lt_a", m.lt_qkv8 ? tq.lt_a : tb.lt_a, g,
                           (m.lt_qkv8 ? Fq : F) * (768.0 * 256) + A * act * (256 * 3 + 768 + 256))) != MP_OK)
                 return rc;
             g = base(); g.cb = 0;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = io.ltq; g.ltk = io.ltk; g.ltv = io.ltv; g.out = io.ltY;
-            g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
+            g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd;
             g.out_ld = 256; g.addsrc = io.ltX;
             if ((rc = run("lt_b", m.lt_o8 ? tq.lt_b : tb.lt_b, g,
                           (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * (256 * 5))) != MP_OK)
@@ -1043,9 +1103,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             dump_lt(io, s);
             g = base(); g.cb = cb;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.src = io.ltq; g.src_ld = 256; g.out = io.ltY; g.out_ld = 256;
-            g.addsrc = io.ltX; g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
+            g.addsrc = io.ltX; g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd;
             const bool f16 = m.weight_mode == MP_WEIGHTS_F16;
-            const mp::GemvFn bo = m.lt_o8 ? mp::q8_lt_bo_8
+            const mp::GemvFn bo = m.lt_o8 ? (NB == 16 ? mp::q8_lt_bo_16 : mp::q8_lt_bo_8)
                                   : f16   ? (NB == 16 ? mp::f16_lt_bo_16 : mp::f16_lt_bo_8)
                                   : b16   ? (NB == 16 ? mp::b16_lt_bo_16 : mp::b16_lt_bo_8)
                                           : mp::op_lt_bo_8;
@@ -1055,7 +1115,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             // table (no q|k|v GEMV), attention + o_net + residual, one launch
             g = base(); g.cb = cb;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.out = io.ltY; g.out_ld = 256;
-            g.Wq = m.lt_o8.q; g.Wd = m.lt_o8.d;
+            g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd;
             g.logits = io.logits; g.codes_cur = io.codes_cur; g.qkvtab = m.lt_qkvtab; g.ptab = m.lt_ptab;
             g.lt_pos = m.lt_pos; g.ltk = io.ltk; g.ltv = io.ltv; g.lk = io.ltk; g.lv = io.ltv;
             if ((rc = run("lt_bg", m.lt_o8 ? tq.lt_bg : tb.lt_bg, g,
@@ -1099,8 +1159,8 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         g.Wb = b16 ? m.pk_lt_out + (size_t)cb * pk_elems(2024, 256) : nullptr; g.bias = m.lt_out_b + (size_t)cb * 2024;
         g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
         if (m.lt_out8) {
-            g.Wq = m.lt_out8.q + (size_t)cb * 2024 * 256;
-            g.Wd = m.lt_out8.d + (size_t)cb * 2024 * 8;
+            g.Wq = m.lt_out8.pq + (size_t)cb * q8p_head_q();
+            g.Wd = (const unsigned short *)((const char *)m.lt_out8.pd + (size_t)cb * q8p_head_d());
         }
         mp::GemvFn efn = m.lt_out8 ? tq.lt_e : tb.lt_e;
         if (ffn1 && NB == 1) {  // the FFN merge is the head's prologue
@@ -1278,6 +1338,8 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     dev->m.weight_mode = MP_WEIGHTS_AS_STORED;
     // drop the Q8_0 views of a previous model
     if (dev->m.q8_arena) { hipFree(dev->m.q8_arena); dev->m.q8_arena = nullptr; dev->m.q8_bytes = 0; }
+    if (dev->m.q8p_arena) { hipFree(dev->m.q8p_arena); dev->m.q8p_arena = nullptr; }
+    dev->m.q8_all = false;
     dev->m.lt_in8 = dev->m.lt_qkv8 = dev->m.lt_o8 = dev->m.lt_out8 = mp::QW{};
     dev->m.pk_lt_in = nullptr;  // set again by an F16 load
     if (weight_mode == MP_WEIGHTS_Q8 || weight_mode == MP_WEIGHTS_F16) {  // cheap header check before any upload
@@ -1324,6 +1386,10 @@ int mp_hip_model_info(mp_dev *dev, int *dec_layers, int *enc_layers, size_t *wei
 }
 
 int mp_hip_weight_mode(mp_dev *dev) { return dev && dev->loaded ? dev->m.weight_mode : MP_ERR_STATE; }
+int mp_hip_max_batch(mp_dev *dev) {
+    if (!dev || !dev->loaded) return MP_ERR_STATE;
+    return mp::h16_mode(dev->m.weight_mode) || (dev->m.weight_mode == MP_WEIGHTS_Q8 && dev->m.q8_all) ? 16 : 8;
+}
 
 int mp_hip_set_kv_mode(mp_dev *dev, int kv_mode) {
     if (!dev || (kv_mode != MP_KV_F32 && kv_mode != MP_KV_BF16)) return MP_ERR_ARG;
@@ -1343,6 +1409,7 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.lt_kvo) hipFree(dev->m.lt_kvo);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
     if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
+    if (dev->m.q8p_arena) hipFree(dev->m.q8p_arena);
     for (void *p : dev->lt_allocs) hipFree(p);
     for (float *p : dev->m.xq_t) hipFree(p);
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
@@ -1359,7 +1426,7 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
                        int tmax, const mp_params *params) {
     if (!dev) return MP_ERR_ARG;
     if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
-    const int bmax = mp::h16_mode(dev->m.weight_mode) ? 16 : 8;
+    const int bmax = mp_hip_max_batch(dev);
     if (!tokens || !n_tokens || !speaker || B < 1 || B > bmax || tmax < 1 || !params)
         return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..8, 1..16 with bf16 weights)");
     if (params->temperature >= 0.01f && (params->top_k < 1 || params->top_k > mp::VCB))

@@ -64,6 +64,7 @@ SYMBOLS = [
     ("mp_hip_load_model", _I, [_P, ctypes.c_char_p]),
     ("mp_hip_load_model_ex", _I, [_P, ctypes.c_char_p, _I]),
     ("mp_hip_weight_mode", _I, [_P]),
+    ("mp_hip_max_batch", _I, [_P]),
     ("mp_hip_set_kv_mode", _I, [_P, _I]),
     ("mp_hip_model_info", _I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_size_t)]),
     ("mp_hip_free", None, [_P]),
@@ -218,6 +219,11 @@ class Device:
         dl, el, wb = ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
         self._check(self.lib.mp_hip_model_info(self.h, ctypes.byref(dl), ctypes.byref(el), ctypes.byref(wb)))
         return {"dec_layers": dl.value, "enc_layers": el.value, "weight_bytes": wb.value}
+
+    def max_batch(self) -> int:
+        n = self.lib.mp_hip_max_batch(self.h)
+        self._check(min(n, 0))
+        return n
 
     def begin(self, tokens: Sequence[Sequence[int]], speakers: Optional[Sequence[int]] = None,
               max_dec_steps: int = 500, temperature: float = 0.0, top_k: int = 80, ignore_eos: bool = False,

@@ -74,6 +74,31 @@ def test_bf16_full_model_sampled_batch8_equals_single(ma, full_model):
     dev.close()
 
 
+def test_q8_full_model_batch16_equals_single(ma, oracle, q8_full_model):
+    """Q8_0 Magpie-357M at 16 utterances (int8 MFMA projections, F32 FFN convs on the
+    f32 GEMV family in two 8-slot halves): each slot equals its single run bit for
+    bit, and slot 0's decisions match the oracle's Q8_0 mode teacher forced."""
+    B, steps = 16, 24
+    toks = [ma.synthetic_tokens(40 + 3 * b, seed=7300 + b) for b in range(B)]
+    spk = [b % 5 for b in range(B)]
+    dev = ma.Device(q8_full_model, weights="q8")
+    assert dev.max_batch() == 16
+    rb = dev.synthesize(toks, speakers=spk, max_dec_steps=steps, ignore_eos=True, trace=True)
+    assert (rb.n_frames == steps).all()
+    for b in (0, 9, 15):
+        rs = dev.synthesize([toks[b]], speakers=[spk[b]], max_dec_steps=steps, ignore_eos=True, trace=True)
+        assert np.array_equal(rb.codes[b], rs.codes[0]), f"slot {b} codes"
+        assert np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b} hidden"
+    dev.close()
+    om = oracle.Model(q8_full_model)
+    om.set_weight_mode(2)
+    o = om.synthesize_forced(toks[0], rb.codes[0], speaker=spk[0], ignore_eos=True)
+    om.close()
+    res = compare_forced(rb.codes[0], o, tie_eps=Q8_TIE_EPS, max_ties=10)  # 5 % of 192
+    assert res["decisions"] == steps * 8
+    _hidden_ok(rb.hidden[0, :steps + 1], o["hidden"])
+
+
 def test_q8_longform_60s_batched_equals_sentence_by_sentence(ma, oracle, q8_full_model, codec_model):
     """configs[4] as the bench runs it: 6 sentences x 216 frames (60.2 s of audio)
     streamed as one device batch with 4-frame codec chunks; every sentence's codes and

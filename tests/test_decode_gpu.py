@@ -108,7 +108,8 @@ def test_batch_equals_single(ma, small_model, B):
     dev.close()
 
 
-@pytest.mark.parametrize("weights,B", [("f32", 4), ("bf16", 4), ("q8", 4), ("f32", 8), ("bf16", 16), ("q8", 8)])
+@pytest.mark.parametrize("weights,B", [("f32", 4), ("bf16", 4), ("q8", 4), ("f32", 8), ("bf16", 16), ("q8", 8),
+                                       ("q8", 16)])
 def test_sampled_batch_equals_single(ma, small_model, q8_model, weights, B):
     """Sampling is what exposes ulp-level batch variance (a near-tie in the top-k
     order flips a draw), so a sampled batch over many frames must reproduce each
@@ -434,13 +435,16 @@ def test_q8_mode_differs_from_dequantised(ma, q8_model):
     assert 1e-5 < d < 0.2, d
 
 
-@pytest.mark.parametrize("B", [3, 8])
+@pytest.mark.parametrize("B", [3, 8, 16])
 def test_q8_batch_equals_single(ma, q8_model, B):
+    """The int8 MFMA projections serve every batch size (one 16-column tile, fixed
+    K split and merge order), so slot b of a batch is its single run bit for bit."""
     toks = [ma.synthetic_tokens(8 + 3 * b, seed=3000 + b) for b in range(B)]
     spk = [b % 5 for b in range(B)]
     dev = ma.Device(q8_model, weights="q8")
+    assert dev.max_batch() == 16
     rb = dev.synthesize(toks, speakers=spk, max_dec_steps=16, ignore_eos=True, trace=True)
-    for b in (0, B - 1):
+    for b in ((0, B - 1) if B < 16 else (0, 7, 8, 15)):
         rs = dev.synthesize([toks[b]], speakers=[spk[b]], max_dec_steps=16, ignore_eos=True, trace=True)
         assert np.array_equal(rb.codes[b], rs.codes[0]), f"slot {b}"
         assert np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b} hidden"
@@ -467,12 +471,13 @@ def test_q4_small_model_matches_oracle(ma, oracle, q4_model):
     _check_hidden_q8(r.hidden[0, :41], o["hidden"])
 
 
-def test_q4_batch_equals_single(ma, q4_model):
-    toks = [ma.synthetic_tokens(8 + 3 * b, seed=3100 + b) for b in range(3)]
+@pytest.mark.parametrize("B", [3, 16])
+def test_q4_batch_equals_single(ma, q4_model, B):
+    toks = [ma.synthetic_tokens(8 + 3 * b, seed=3100 + b) for b in range(B)]
     dev = ma.Device(q4_model, weights="q4")
-    rb = dev.synthesize(toks, speakers=[0, 1, 2], max_dec_steps=16, ignore_eos=True, trace=True)
-    for b in (0, 2):
-        rs = dev.synthesize([toks[b]], speakers=[b], max_dec_steps=16, ignore_eos=True, trace=True)
+    rb = dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=16, ignore_eos=True, trace=True)
+    for b in (0, B - 1):
+        rs = dev.synthesize([toks[b]], speakers=[b % 5], max_dec_steps=16, ignore_eos=True, trace=True)
         assert np.array_equal(rb.codes[b], rs.codes[0]) and np.array_equal(rb.hidden[b], rs.hidden[0]), f"slot {b}"
     dev.close()
 

@@ -109,6 +109,20 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *gguf_path, int weight_mode);
 #define MP_KV_F32 0
 #define MP_KV_BF16 1
 int mp_hip_set_kv_mode(mp_dev *dev, int kv_mode);
+/* Cross-attention form of the decode step, applied from the next mp_hip_begin_batch.
+ * REASSOC: x += sum_t softmax_t(K'_t . LN(x)) V'_t with K' = W_q^T K, V' = W_o V
+ * precomputed per utterance (reads 6 KB per text token and layer; fused into the
+ * O-projection launch). DIRECT: q = W_q LN(x), attention over K, V, W_o (reads 1 KB
+ * per text token and layer + q_net / o_net, 0.79 MB; two launches), the order
+ * magpie.cpp:1713-1767 computes. AUTO (default): DIRECT when the batch's longest text
+ * exceeds MP_XA_DIRECT_T tokens (where it reads fewer bytes), else REASSOC. The F16
+ * weight mode is always REASSOC; the Q8_0 mode always direct (its quantised q_net /
+ * o_net). A batch reproduces its utterances run alone when both use the same form. */
+#define MP_XA_AUTO 0
+#define MP_XA_REASSOC 1
+#define MP_XA_DIRECT 2
+#define MP_XA_DIRECT_T 160
+int mp_hip_set_xa_mode(mp_dev *dev, int xa_mode);
 int mp_hip_weight_mode(mp_dev *dev);
 /* the largest batch mp_hip_begin_batch accepts for the loaded model: 16 in the
  * bf16 / F16 modes and for a Q8_0 / Q4_0 file whose decode projections are all

@@ -19,6 +19,7 @@
 #include "mp_device.hpp"
 #include "mp_fused.hpp"
 #include "mp_params.hpp"
+#include "mp_sa.hpp"
 #include "mp_xa.hpp"
 
 namespace mp {
@@ -34,6 +35,13 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
         // the launch's last XA_SPLITS x NB workgroups: cross-attention on this launch's x1
         if ((int)blockIdx.x >= p.nrow_blocks) {
             xa_tail(p, t_start);
+            return;
+        }
+    }
+    if constexpr (EPI == EPI_QKV_SA) {
+        // the launch's last NH x SA_SPLITS x NB workgroups: self-attention on this launch's q|k|v
+        if ((int)blockIdx.x >= p.nrow_blocks) {
+            sa_tail(p, t_start);
             return;
         }
     }
@@ -105,6 +113,8 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     if (n >= p.N) return;
     if constexpr (EPI == EPI_RESID_XA) {
         publish_x1(p, v, n, b);
+    } else if constexpr (EPI == EPI_QKV_SA) {
+        publish_qkv(p, v, n, b);
     } else {
         epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
     }
@@ -112,87 +122,16 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 }
 
 // ---------------------------------------------------------------- SA decode attention
-// Split-K over the live cache: grid (head, split, slot), 8 waves per workgroup.
-// Split s of head h takes keys [s*chunk, (s+1)*chunk) of L = pos + 1
-// (magpie.cpp:3412); wave w takes keys 4(w + 8 r) + kk of it (16 lanes x float4
-// cover one 64-dim row, a wave does 4 keys per instruction) with four
-// iterations' K and V loads in flight, keeps an online softmax (m, l, o[64]),
-// the 8 wave states are merged in LDS, and the split's state (m, l, unnormalised
-// O) is stored; the O-projection's PRO_SA_MERGE prologue merges the splits
-// (softmax(K q / 8) V per head, 3457-3476). At batch 1 that is 48 workgroups of
-// ~L/4 keys each instead of one workgroup streaming a whole head.
-constexpr int SA_WAVES = 8, SA_THREADS = SA_WAVES * 64, SA_IF = 4;  // iterations in flight
+// Split-K over the live cache (sa_part, mp_sa.hpp): grid (head, split, slot), 4
+// waves per workgroup; at batch 1 that is 48 workgroups of ~L/4 keys each instead
+// of one workgroup streaming a whole head. Layers >= 1 of the f32 and 16-bit
+// families run the same body in their QKV launch (EPI_QKV_SA) below 16 slots;
+// this kernel serves layer 0, 16 slots and the Q8_0 mode.
+constexpr int SA_WAVES = MP_NWAVES, SA_THREADS = SA_WAVES * 64;
 template <bool KV16>
 __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     const unsigned long long t_start = ts_begin(p.ts);
-    const int h = blockIdx.x, sp = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int kk = lane >> 4, dc = lane & 15;
-    __shared__ float wm[SA_WAVES], wl[SA_WAVES];
-    __shared__ __attribute__((aligned(16))) float wo[SA_WAVES][DH];
-    const float4 q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
-    const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc + ts_dep(t_start);
-    const int L = p.pos[b] + 1;
-    const int chunk = (L + SA_SPLITS - 1) / SA_SPLITS;
-    const int j0 = sp * chunk, j1 = min(L, j0 + chunk);
-    float m = -INFINITY, l = 0.f;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r0 = 0; j0 + 4 * SA_WAVES * r0 < j1; r0 += SA_IF) {
-        float4 k4[SA_IF], v4[SA_IF];
-#pragma unroll
-        for (int u = 0; u < SA_IF; ++u) {
-            // keys past the split re-read its last row (an L1/L2 hit, no extra HBM
-            // traffic); rows < max_seq are valid memory: no load waits for the mask
-            const int j = min(j0 + 4 * (w + SA_WAVES * (r0 + u)) + kk, max(j1 - 1, 0));
-            k4[u] = kv_load4<KV16>(p.kc, base + (size_t)j * D);
-            v4[u] = kv_load4<KV16>(p.vc, base + (size_t)j * D);
-        }
-        float sv[SA_IF];
-        float mb = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < SA_IF; ++u) {
-            const int j = j0 + 4 * (w + SA_WAVES * (r0 + u)) + kk;
-            const float v = group_sum<16>(dotv(q4, k4[u])) * 0.125f;  // 1/sqrt(64)
-            sv[u] = j < j1 ? v : -INFINITY;
-            mb = fmaxf(mb, sv[u]);
-        }
-        mb = wave_max(mb);
-        if (mb == -INFINITY) continue;  // nothing live for this wave in this batch
-        const float mn = fmaxf(m, mb), c = expf(m - mn);
-        l *= c;
-        o.x *= c; o.y *= c; o.z *= c; o.w *= c;
-#pragma unroll
-        for (int u = 0; u < SA_IF; ++u) {
-            const float e = sv[u] == -INFINITY ? 0.f : expf(sv[u] - mn);
-            l += e;  // per lane: its key group's keys; summed over the wave below
-            o.x += e * v4[u].x; o.y += e * v4[u].y; o.z += e * v4[u].z; o.w += e * v4[u].w;
-        }
-        m = mn;
-    }
-    // merge the 4 key groups of the wave (lanes l, l^16, l^32, l^48 share dims)
-#pragma unroll
-    for (int msk = 16; msk <= 32; msk <<= 1) {
-        o.x += __shfl_xor(o.x, msk, 64); o.y += __shfl_xor(o.y, msk, 64);
-        o.z += __shfl_xor(o.z, msk, 64); o.w += __shfl_xor(o.w, msk, 64);
-        l += __shfl_xor(l, msk, 64);
-    }
-    if (lane < 16) *(float4 *)(&wo[w][4 * lane]) = o;
-    if (lane == 0) { wm[w] = m; wl[w] = l; }
-    lds_sync();
-    if (tid >= DH) return;
-    float M = -INFINITY;
-#pragma unroll
-    for (int q = 0; q < SA_WAVES; ++q) M = fmaxf(M, wm[q]);
-    float num = 0.f, den = 0.f;
-#pragma unroll
-    for (int q = 0; q < SA_WAVES; ++q) {
-        const float e = wm[q] == -INFINITY ? 0.f : expf(wm[q] - M);
-        den += e * wl[q];
-        num += e * wo[q][tid];
-    }
-    float *pp = p.part + ((size_t)(b * NH + h) * SA_SPLITS + sp) * SA_PART;
-    pp[4 + tid] = num;  // relative to M (an empty split stores M = -inf, l = 0, O = 0)
-    if (tid == 0) { pp[0] = M; pp[1] = den; }
+    sa_part<KV16, SA_WAVES, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, nullptr, 0u, nullptr, ts_dep(t_start));
     ts_end(p.ts, t_start);
 }
 
@@ -288,7 +227,8 @@ static bool gemv_args_ok(const GemvP &p) {
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
     if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
     if constexpr (EPI == EPI_LTX_ADD) ok &= p.out && p.ptab && p.lt_pos && p.cb >= 1;
-    if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_QKV || EPI == EPI_QKV_SA) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_QKV_SA) ok &= qkv_sa_args_ok(p);
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
     if constexpr (EPI == EPI_LTKVO) ok &= p.lk && p.lv && p.N == 2 * LTD;
     if constexpr (EPI == EPI_RESID_XA)
@@ -303,7 +243,7 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
     const int rows_per_block = MP_NWAVES * RW;
     GemvP q = p;
     q.nrow_blocks = (p.N + rows_per_block - 1) / rows_per_block;
-    const int grid = q.nrow_blocks + (EPI == EPI_RESID_XA ? XA_SPLITS * NB : 0);
+    const int grid = q.nrow_blocks + (EPI == EPI_RESID_XA ? XA_SPLITS * NB : EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : 0);
     mp::launch((gemv_kernel<NB, RW, K, PRO, EPI>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();
 }
@@ -313,6 +253,8 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
 #define MP_DECODE_OPS(NB)                                                                                        \
     hipError_t op_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
+    hipError_t op_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV_SA>(p, s); }       \
+    hipError_t op_xq_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_STORE>(p, s); }            \
     hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_SA_MERGE, EPI_RESID>(p, s); } \
     hipError_t op_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                   \
         return launch_gemv<NB, 1, D, PRO_SA_MERGE, EPI_RESID_XA>(p, s);                                            \
@@ -341,6 +283,8 @@ hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 
 // Q8_0 weight mode at 16 slots: the FFN convs (F32 in the reference's Q8 file)
 hipError_t op_ff1_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 2, D, PRO_LN, EPI_GELU>(p, s); }
 hipError_t op_ff2_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
+// the direct XA's f32 q_net at 16 slots (bf16 mode)
+hipError_t op_xq_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, D, PRO_LN, EPI_STORE>(p, s); }
 
 
 hipError_t op_sa_attn(const AttnP &p, int B, hipStream_t s) {

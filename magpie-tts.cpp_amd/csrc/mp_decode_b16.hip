@@ -21,6 +21,7 @@
 #include "mp_device.hpp"
 #include "mp_fused.hpp"
 #include "mp_params.hpp"
+#include "mp_sa.hpp"
 #include "mp_xa.hpp"
 
 namespace mp {
@@ -82,6 +83,13 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
         // the launch's last XA_SPLITS x NB workgroups: cross-attention on this launch's x1 (mp_xa.hpp)
         if ((int)blockIdx.x >= p.nrow_blocks) {
             xa_tail(p, t_start);
+            return;
+        }
+    }
+    if constexpr (EPI == EPI_QKV_SA) {
+        // the launch's last NH x SA_SPLITS x NB workgroups: self-attention on this launch's q|k|v
+        if ((int)blockIdx.x >= p.nrow_blocks) {
+            sa_tail(p, t_start);
             return;
         }
     }
@@ -178,6 +186,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const int n = rt * 16 + row;
     if (n >= p.N) return;
     if constexpr (EPI == EPI_RESID_XA) publish_x1(p, v, n, col);
+    else if constexpr (EPI == EPI_QKV_SA) publish_qkv(p, v, n, col);
     else epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
     ts_end(p.ts, t_start);
 }
@@ -202,7 +211,8 @@ static bool b16_args_ok(const GemvP &p) {
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
     if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
     if constexpr (EPI == EPI_LTX_ADD) ok &= p.out && p.ptab && p.lt_pos && p.cb >= 1;
-    if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_QKV || EPI == EPI_QKV_SA) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_QKV_SA) ok &= qkv_sa_args_ok(p);
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
     if constexpr (EPI == EPI_RESID_XA)
         ok &= p.resid && p.xh && p.iter && p.hx_err && p.N == D && p.xa.part && p.xa.lnw && p.xa.kp && p.xa.vp &&
@@ -215,7 +225,7 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     if (!b16_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
     GemvP q = p;
     q.nrow_blocks = (p.N + 15) / 16;
-    const int grid = q.nrow_blocks + (EPI == EPI_RESID_XA ? XA_SPLITS * NB : 0);
+    const int grid = q.nrow_blocks + (EPI == EPI_RESID_XA ? XA_SPLITS * NB : EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : 0);
     mp::launch((gemm_b16_kernel<NB, K, PRO, EPI, F16>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();
 }
@@ -223,11 +233,13 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
 #define MP_B16_OPS(NB)                                                                                                  \
     hipError_t b16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
+    hipError_t b16_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV_SA>(p, s); }       \
     hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }   \
     hipError_t b16_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                      \
         return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA>(p, s);                                                       \
     }                                                                                                                   \
     hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_B16>(p, s); }     \
+    hipError_t b16_ff1p_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_GELU_B16>(p, s); }       \
     hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE>(p, s); }  \
     hipError_t b16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
     hipError_t b16_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_ATTN, EPI_LTX_ADD>(p, s); } \
@@ -239,6 +251,7 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
 #define MP_F16_OPS(NB)                                                                                                  \
     hipError_t f16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV, true>(p, s); } \
     hipError_t f16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV, true>(p, s); }             \
+    hipError_t f16_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV_SA, true>(p, s); }       \
     hipError_t f16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID, true>(p, s); }   \
     hipError_t f16_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                      \
         return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA, true>(p, s);                                                 \

@@ -163,19 +163,81 @@ hipError_t pack_q8(const signed char *q, const unsigned short *d, int N, int K, 
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- fused Q8 XA tail
-// Cross-attention with Q8_0 q_net / o_net: q = Q8(q_net) LN(x) is one GEMV
-// launch (q8_xq, 8 workgroups: q_net's 98 KB spread over CUs); this kernel then
-// does attention + o_net + residual: grid (768/64, B), a workgroup owns 64 rows
-// of o_net and recomputes the slot's attention over the text (K, V: 2 x T x 128
-// f32, coalesced: half a wave per key row), quantises it to Q8_0 and finishes
-// x2 = x + Q8(o_net) a for its rows (v_dot4 per half block: the exact int32
-// block dots, times d_w * d_a). The o_net rows are issued first.
+// ---------------------------------------------------------------- XA, direct form
+// Cross-attention as ggml computes it (magpie.cpp:1713-1767): q = q_net LN(x) is
+// one GEMV launch (8 workgroups: q_net's 128 rows spread over CUs); xa_dir_kernel
+// then does attention + o_net + residual: grid (768/64, B), a workgroup owns 64 rows
+// of o_net, issues them first, recomputes the slot's attention over the text (K, V:
+// 2 x T x 128 f32, coalesced: half a wave per key row; xa_text_attention) and
+// finishes x2 = x + o_net a for its rows.
+//  * Q8_0 q_net / o_net (xa_q8_kernel): a is quantised to Q8_0 and dotted with
+//    v_dot4 per half block (the exact int32 block dots, times d_w * d_a);
+//  * f32 (xa_f32_kernel; long texts, where the reassociated K'/V' form of mp_xa.hpp
+//    would read 6 KB per text token and layer against 1 KB here).
 constexpr int XQ8_ROWS = 64;  // o_net rows per workgroup
+
+// a = softmax_t(q . K_t / sqrt(128)) V  of slot b into a_s[128] (every thread
+// returns after a barrier); pr: per-key scores [TMAX_LIMIT]
+__device__ __forceinline__ void xa_text_attention(const float *q, const float *Kb, const float *Vb, int Tb,
+                                                  float *pr, float *a_s) {
+    __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
+    __shared__ float wred[2 * MP_NWAVES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int h = lane >> 5, d4 = 4 * (lane & 31);
+    const float4 q4 = *(const float4 *)(q + d4);
+    const float scale = 1.0f / sqrtf((float)DXA);
+    float mx = -INFINITY;
+    for (int t0 = 2 * w; t0 < Tb; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
+        float4 k4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(t0 + 2 * MP_NWAVES * u + h, Tb - 1);
+            k4[u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + 2 * MP_NWAVES * u + h;
+            const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
+            if (t < Tb) {
+                if ((lane & 31) == 0) pr[t] = sv;
+                mx = fmaxf(mx, sv);
+            }
+        }
+    }
+    mx = wave_max(mx);
+    if (lane == 0) wred[w] = mx;
+    lds_sync();
+    const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
+    // o[d] = sum_t e_t V_t[d]: wave w takes keys t = w + 4 u, lane owns dims lane, 64 + lane
+    float l = 0.f, o0 = 0.f, o1 = 0.f;
+    for (int t0 = w; t0 < Tb; t0 += MP_NWAVES * 4) {
+        float v0[4], v1[4], e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(t0 + MP_NWAVES * u, Tb - 1);
+            v0[u] = Vb[(size_t)t * DXA + lane];
+            v1[u] = Vb[(size_t)t * DXA + 64 + lane];
+            e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { l += e[u]; o0 += e[u] * v0[u]; o1 += e[u] * v1[u]; }
+    }
+    pv[w][lane] = o0;
+    pv[w][64 + lane] = o1;
+    if (lane == 0) wred[MP_NWAVES + w] = l;
+    lds_sync();
+    if (tid < DXA) {
+        const float den = ((wred[4] + wred[5]) + wred[6]) + wred[7];
+        a_s[tid] = (((pv[0][tid] + pv[1][tid]) + pv[2][tid]) + pv[3][tid]) / den;
+    }
+    lds_sync();
+}
+
 __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
     constexpr int OR = 8, OCPR = DXA / 16;                 // o_net: groups of 8 rows
     constexpr int OG = XQ8_ROWS / MP_NWAVES / OR;          // 2 groups per wave
     __shared__ float pr[TMAX_LIMIT];
+    __shared__ __attribute__((aligned(16))) float a_s[DXA];
     __shared__ __attribute__((aligned(16))) signed char aq[DXA];
     __shared__ float ad[DXA / 32];
     const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -188,74 +250,18 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
         wo[g] = *(const uint4 *)(p.wo + (size_t)row * DXA + kc * 16);
         wos[g] = __half2float(__ushort_as_half(p.wod[(size_t)row * (DXA / 32) + kc / 2]));
     }
-    // ---- attention over the utterance's text, coalesced: a half-wave (32 lanes x
-    //      float4) covers one 128-dim key row; wave w scores keys t = w + 4 u
-    __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
-    __shared__ float wred[2 * MP_NWAVES];
-    {
-        const int Tb = p.T[b];
-        const int h = lane >> 5, d4 = 4 * (lane & 31);
-        const float4 q4 = *(const float4 *)(p.q + (size_t)b * DXA + d4);
-        const float *Kb = p.xak + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-        const float *Vb = p.xav + ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-        const float scale = 1.0f / sqrtf((float)DXA);
-        float mx = -INFINITY;
-        for (int t0 = 2 * w; t0 < Tb; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
-            float4 k4[4];
+    const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+    xa_text_attention(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
+    if (w == 0) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = min(t0 + 2 * MP_NWAVES * u + h, Tb - 1);
-                k4[u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = t0 + 2 * MP_NWAVES * u + h;
-                const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
-                if (t < Tb) {
-                    if ((lane & 31) == 0) pr[t] = sv;
-                    mx = fmaxf(mx, sv);
-                }
-            }
-        }
-        mx = wave_max(mx);
-        if (lane == 0) wred[w] = mx;
-        lds_sync();
-        const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
-        // o[d] = sum_t e_t V_t[d]: wave w takes keys t = w + 4 u, lane owns dims lane, 64 + lane
-        float l = 0.f, o0 = 0.f, o1 = 0.f;
-        for (int t0 = w; t0 < Tb; t0 += MP_NWAVES * 4) {
-            float v0[4], v1[4], e[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = min(t0 + MP_NWAVES * u, Tb - 1);
-                v0[u] = Vb[(size_t)t * DXA + lane];
-                v1[u] = Vb[(size_t)t * DXA + 64 + lane];
-                e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) { l += e[u]; o0 += e[u] * v0[u]; o1 += e[u] * v1[u]; }
-        }
-        pv[w][lane] = o0;
-        pv[w][64 + lane] = o1;
-        if (lane == 0) wred[MP_NWAVES + w] = l;
-        lds_sync();
-        if (w == 0) {
-            const float den = ((wred[4] + wred[5]) + wred[6]) + wred[7];
-            float av[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int d = lane + 64 * i;
-                av[i] = (((pv[0][d] + pv[1][d]) + pv[2][d]) + pv[3][d]) / den;
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {  // element lane + 64 i; its Q8_0 block = this half-wave
-                float a = row_max16(fabsf(av[i]));
-                a = fmaxf(a, __shfl_xor(a, 16, 64));
-                const float dd = a / 127.0f;
-                const float id = dd != 0.f ? 1.0f / dd : 0.0f;
-                aq[lane + 64 * i] = (signed char)(int)roundf(av[i] * id);
-                if ((lane & 31) == 0) ad[(lane + 64 * i) / 32] = __half2float(__float2half(dd));
-            }
+        for (int i = 0; i < 2; ++i) {  // element lane + 64 i; its Q8_0 block = this half-wave
+            const float av = a_s[lane + 64 * i];
+            float a = row_max16(fabsf(av));
+            a = fmaxf(a, __shfl_xor(a, 16, 64));
+            const float dd = a / 127.0f;
+            const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+            aq[lane + 64 * i] = (signed char)(int)roundf(av * id);
+            if ((lane & 31) == 0) ad[(lane + 64 * i) / 32] = __half2float(__float2half(dd));
         }
     }
     lds_sync();
@@ -283,11 +289,37 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
     }
 }
 
+// f32 o_net: lane l holds elements 4l..4l+3 of half a row, a wave covers 2 rows
+// per instruction; 64 rows = 4 waves x 8 pairs
+__global__ __launch_bounds__(MP_BLOCK) void xa_f32_kernel(XaQ8P p) {
+    constexpr int RP = XQ8_ROWS / MP_NWAVES / 2;  // row pairs per wave
+    __shared__ float pr[TMAX_LIMIT];
+    __shared__ __attribute__((aligned(16))) float a_s[DXA];
+    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r0 = blockIdx.x * XQ8_ROWS + w * 2 * RP, hr = lane >> 5, d4 = 4 * (lane & 31);
+    float4 wo[RP];
+#pragma unroll
+    for (int i = 0; i < RP; ++i) wo[i] = *(const float4 *)(p.wof + (size_t)(r0 + 2 * i + hr) * DXA + d4);
+    const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+    xa_text_attention(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
+    const float4 a4 = *(const float4 *)&a_s[d4];
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+        const float t = group_sum<32>(dotv(wo[i], a4));
+        if ((lane & 31) == i) v = t;  // row r0 + 2 i + hr lands in lane i (+32)
+    }
+    if ((lane & 31) < RP) {
+        const int row = r0 + 2 * (lane & 31) + hr;
+        p.x2[(size_t)b * D + row] = v + p.x[(size_t)b * D + row];
+    }
+}
+
 hipError_t op_xa_q8(const XaQ8P &p, int B, hipStream_t s) {
-    if (!p.x || !p.x2 || !p.q || !p.wo || !p.wod || !p.xak || !p.xav || !p.T || p.Tmax < 1 ||
-        p.Tmax > TMAX_LIMIT)
-        return hipErrorInvalidValue;
-    mp::launch(xa_q8_kernel, dim3(D / XQ8_ROWS, B), dim3(MP_BLOCK), 0, s, p);
+    if (!p.x || !p.x2 || !p.q || !p.xak || !p.xav || !p.T || p.Tmax < 1 || p.Tmax > TMAX_LIMIT) return hipErrorInvalidValue;
+    if (p.wof) mp::launch(xa_f32_kernel, dim3(D / XQ8_ROWS, B), dim3(MP_BLOCK), 0, s, p);
+    else if (p.wo && p.wod) mp::launch(xa_q8_kernel, dim3(D / XQ8_ROWS, B), dim3(MP_BLOCK), 0, s, p);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -60,6 +60,8 @@ enum Epi {
     EPI_GELU_F16 = 11,  // out_b16 = f16(gelu(v)): EPI_GELU_B16 for the F16 weight mode
     EPI_RESID_XA = 10,  // resid += v, each new x1 value also published as a tagged granule; the
                         // launch's last XA_SPLITS x NB workgroups run the fused XA on it (below)
+    EPI_QKV_SA = 12,    // EPI_QKV, each q|k|v value also published as a tagged granule qh[b][2304];
+                        // the launch's last NH x SA_SPLITS x NB workgroups run the SA on it
 };
 
 // Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
@@ -155,6 +157,17 @@ struct XaP {
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 
+struct AttnP {  // decode self-attention (one query per utterance)
+    const float *q;
+    const float *kc, *vc;    // bf16 elements when kv16
+    int layer, nlayers, max_seq;
+    const int *pos;
+    int kv16;
+    float *part;         // [B][NH][SA_SPLITS][SA_PART] partial softmax states over key splits
+                         // (merged in the O-projection's PRO_SA_MERGE prologue)
+    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
+};
+
 struct GemvP {
     const float *W;
     const unsigned short *Wb;  // bf16 weights in MFMA fragment order (mp_decode_b16.hip), or null
@@ -213,6 +226,13 @@ struct GemvP {
     // gives up after a bound and raises *hx_err.
     XaP xa;
     unsigned long long *xh;
+    // EPI_QKV_SA (QKV projection + self-attention in one launch): the QKV workgroups
+    // publish q|k|v as {tag, value} granules qh[B][2304] (tag as for xh); the last
+    // NH x SA_SPLITS x B workgroups prefetch their cached K/V rows (keys < pos), sweep
+    // their head's granules and run the split's attention (the new key from the
+    // granules, not from the cache row this launch writes)
+    AttnP sa;
+    unsigned long long *qh;
     const int *iter;
     int *hx_err;
     int nrow_blocks;     // set by the launcher: workgroups of the O-projection
@@ -239,20 +259,11 @@ struct XaQ8P {
     const float *q;                 // [B][128] = Q8(q_net) LN(x)
     const signed char *wo;          // o_net int8 [768][128]
     const unsigned short *wod;      //   fp16 block scales [768][4]
+    const float *wof;               // or f32 o_net [768][128] (direct f32 XA, long texts)
     const float *xak, *xav;         // XA K, V [B][L][Tmax][128]
     const int *T;
     int Tmax, layer, nlayers;
 };
 
-struct AttnP {  // decode self-attention (one query per utterance)
-    const float *q;
-    const float *kc, *vc;    // bf16 elements when kv16
-    int layer, nlayers, max_seq;
-    const int *pos;
-    int kv16;
-    float *part;         // [B][NH][SA_SPLITS][SA_PART] partial softmax states over key splits
-                         // (merged in the O-projection's PRO_SA_MERGE prologue)
-    unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
-};
 
 }  // namespace mp

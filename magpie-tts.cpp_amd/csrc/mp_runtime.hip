@@ -34,6 +34,7 @@ using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
     hipError_t op_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t op_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t op_oproj_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_ff1x_##NB(const GemvP &, hipStream_t); hipError_t op_oproj_xa_##NB(const GemvP &, hipStream_t);       \
+    hipError_t op_qkv_sa_##NB(const GemvP &, hipStream_t); hipError_t op_xq_##NB(const GemvP &, hipStream_t); \
     hipError_t op_ff2_##NB(const GemvP &, hipStream_t); hipError_t op_lt_in0_##NB(const GemvP &, hipStream_t);           \
     hipError_t op_lt_a_##NB(const GemvP &, hipStream_t); hipError_t op_lt_b_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_lt_bg_##NB(const GemvP &, hipStream_t);                                                              \
@@ -50,7 +51,8 @@ hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
     hipError_t b16_ff2_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_a_##NB(const GemvP &, hipStream_t);           \
     hipError_t b16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_b_##NB(const GemvP &, hipStream_t);         \
     hipError_t b16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_d_##NB(const GemvP &, hipStream_t);          \
-    hipError_t b16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t b16_oproj_xa_##NB(const GemvP &, hipStream_t);
+    hipError_t b16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t b16_oproj_xa_##NB(const GemvP &, hipStream_t); \
+    hipError_t b16_qkv_sa_##NB(const GemvP &, hipStream_t); hipError_t b16_ff1p_##NB(const GemvP &, hipStream_t);
 MP_DECL_B16(1)
 MP_DECL_B16(2)
 MP_DECL_B16(4)
@@ -63,7 +65,7 @@ MP_DECL_B16(16)
     hipError_t f16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_b_##NB(const GemvP &, hipStream_t);         \
     hipError_t f16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_d_##NB(const GemvP &, hipStream_t);          \
     hipError_t f16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_in0_##NB(const GemvP &, hipStream_t); \
-    hipError_t f16_oproj_xa_##NB(const GemvP &, hipStream_t);
+    hipError_t f16_oproj_xa_##NB(const GemvP &, hipStream_t); hipError_t f16_qkv_sa_##NB(const GemvP &, hipStream_t);
 MP_DECL_F16(1)
 MP_DECL_F16(2)
 MP_DECL_F16(4)
@@ -87,6 +89,7 @@ MP_DECL_Q8(16)
 hipError_t q8_lt_bo_16(const GemvP &, hipStream_t);
 hipError_t op_ff1_16(const GemvP &, hipStream_t);
 hipError_t op_ff2_16(const GemvP &, hipStream_t);
+hipError_t op_xq_16(const GemvP &, hipStream_t);
 hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
 hipError_t pack_q8(const signed char *, const unsigned short *, int, int, unsigned char *, unsigned short *, hipStream_t);
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
@@ -115,24 +118,27 @@ namespace mp {
 
 // ff1: LN(x2) prologue (x2 materialised: Q8 unfused XA); ff1x: the fused XA's split states merged into x2 first
 // oproj_xa: O-projection + the fused XA in one launch (EPI_RESID_XA)
-struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e, oproj_xa; };
+// qkv_sa: the QKV projection + the SA in one launch (EPI_QKV_SA)
+// xq: the direct XA's f32 q_net GEMV (f32 and bf16 modes); ff1: FFN up from a materialised x2
+struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e, oproj_xa,
+                 qkv_sa, xq; };
 #define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, \
-                       op_oproj_xa_##NB }
+                       op_oproj_xa_##NB, op_qkv_sa_##NB, op_xq_##NB }
 // 16 slots in the f32 family only for a Q8_0 file's F32 tensors: its FFN convs and LT in_proj
 static const OpTable kTables[5] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8),
                                    {nullptr, nullptr, nullptr, op_ff1_16, nullptr, op_ff2_16, op_lt_in0_16, nullptr,
-                                    nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}};
+                                    nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, op_xq_16}};
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
-#define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, nullptr, b16_ff1_##NB, b16_ff2_##NB, \
+#define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, b16_ff1p_##NB, b16_ff1_##NB, b16_ff2_##NB, \
                            op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_bg_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
-                           b16_lt_d_##NB, b16_lt_e_##NB, b16_oproj_xa_##NB }
+                           b16_lt_d_##NB, b16_lt_e_##NB, b16_oproj_xa_##NB, b16_qkv_sa_##NB, op_xq_##NB }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
 // F16 weight mode (an F16 GGUF): the same MFMA family on f16, the LT in_proj included
 #define MP_TABLE_F16(NB) { f16_qkv_embed_##NB, f16_qkv_##NB, f16_oproj_##NB, nullptr, f16_ff1_##NB, f16_ff2_##NB, \
                            f16_lt_in0_##NB, f16_lt_a_##NB, f16_lt_bg_##NB, f16_lt_b_##NB, f16_lt_c_##NB,  \
-                           f16_lt_d_##NB, f16_lt_e_##NB, f16_oproj_xa_##NB }
+                           f16_lt_d_##NB, f16_lt_e_##NB, f16_oproj_xa_##NB, f16_qkv_sa_##NB }
 static const OpTable kTablesF16[5] = {MP_TABLE_F16(1), MP_TABLE_F16(2), MP_TABLE_F16(4), MP_TABLE_F16(8),
                                       MP_TABLE_F16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
@@ -219,6 +225,7 @@ struct OpRec {
     EmbP e;
     int B;
     double bytes;
+    bool add_sa = false;  // the launch also runs the SA (EPI_QKV_SA): its live-cache bytes are added
 };
 
 // Buffers of the local-transformer + bookkeeping part of an iteration
@@ -245,6 +252,8 @@ struct mp_dev {
     int B = 0, NB = 0, Tmax = 0, max_steps = 0, max_seq = 0, nch = 0;
     mp_params params{};
     int kv_mode = MP_KV_F32;  // mp_hip_set_kv_mode: applies from the next mp_hip_begin_batch
+    int xa_mode = MP_XA_AUTO;  // mp_hip_set_xa_mode: likewise
+    bool xa_direct = false;    // this batch runs the direct XA form (f32 / bf16 modes)
     int kv16 = 0;             // the current batch's SA cache holds bf16
     // device state (one allocation per buffer, sized for the configuration)
     std::vector<void *> allocs;
@@ -258,6 +267,7 @@ struct mp_dev {
     size_t h_codes_n = 0;
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     unsigned long long *xh = nullptr;  // O-projection -> XA hand-off granules [NB][768] (EPI_RESID_XA)
+    unsigned long long *qh = nullptr;  // QKV -> SA hand-off granules [NB][2304] (EPI_QKV_SA)
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
@@ -743,6 +753,14 @@ static size_t q8p_head_q() { return (mp::q8p_qbytes(2024, 256) + 255) & ~(size_t
 static size_t q8p_head_d() { return (mp::q8p_dbytes(2024, 256) + 255) & ~(size_t)255; }
 
 // ------------------------------------------------------------------ batch state
+// the cross-attention form of a batch (mp_hip_set_xa_mode): direct where it reads fewer
+// bytes (Tmax > MP_XA_DIRECT_T); F16 keeps the reassociated form, Q8_0 has its own
+bool want_xa_direct(const mp_dev *dev, int Tmax) {
+    const int wm = dev->m.weight_mode;
+    if (wm != MP_WEIGHTS_AS_STORED && wm != MP_WEIGHTS_BF16) return false;
+    return dev->xa_mode == MP_XA_DIRECT || (dev->xa_mode == MP_XA_AUTO && Tmax > MP_XA_DIRECT_T);
+}
+
 int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     free_batch(dev);
     const int NB = B <= 1 ? 1 : B <= 2 ? 2 : B <= 4 ? 4 : B <= 8 ? 8 : 16;
@@ -758,11 +776,14 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     int rc = MP_OK;
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
-    A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); A(sa_out, NB * 768);
+    if (!dev->xa_direct) { A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); }
+    else dev->kp = dev->vp = nullptr;
+    A(sa_out, NB * 768);
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
-    A(xh, (size_t)NB * D);
+    A(xh, (size_t)NB * D); A(qh, (size_t)NB * 3 * D);
     dev->kv16 = dev->kv_mode == MP_KV_BF16;
+    dev->xa_direct = want_xa_direct(dev, Tmax);
     const size_t kvn = (size_t)NB * L * dev->max_seq * D;  // elements; bf16 mode: 2 per float slot
     A(kc, dev->kv16 ? kvn / 2 : kvn); A(vc, dev->kv16 ? kvn / 2 : kvn);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -852,13 +873,24 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             HIPCHK(mp::op_embed(ep, NB, s));
         }
         if (embed_in) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
-        {
-            const mp::GemvFn fn = W.qkv8 ? (embed_in ? tq.qkv_embed : tq.qkv) : (embed_in ? tb.qkv_embed : tb.qkv);
-            if ((rc = run(embed_in ? "qkv_embed" : "qkv", fn, g,
-                          (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
-        }
-        // self-attention over the cache, one workgroup per (head, slot) (3457-3476)
+        // self-attention over the cache, split over keys (3457-3476); the f32 family runs
+        // it in the QKV launch on a hand-off of q|k|v (EPI_QKV_SA), the others separately
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->kv16, dev->sa_part};
+        // (not in layer 0: behind its frame-embedding prologue the fused launch measured
+        // 30 us, 11.5 us back to back, against 6.3 + 4.0 us as two launches; not at 16
+        // slots: bf16 B=16 20.1k vs 21.5k frames/s. Both forms compute the same bits.)
+        const bool sa_in_qkv = !W.qkv8 && tb.qkv_sa && l > 0 && NB < 16;
+        {
+            mp::GemvFn fn = W.qkv8 ? (embed_in ? tq.qkv_embed : tq.qkv) : (embed_in ? tb.qkv_embed : tb.qkv);
+            if (sa_in_qkv) {
+                fn = tb.qkv_sa;
+                g.sa = a; g.qh = dev->qh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
+            }
+            if ((rc = run(sa_in_qkv ? "qkv_sa" : embed_in ? "qkv_embed" : "qkv", fn, g,
+                          (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
+            if (sa_in_qkv && record) dev->ops.back().add_sa = true;
+        }
+        if (!sa_in_qkv) {
         if (record) {
             mp::OpRec r{};
             r.name = "sa_attn"; r.kind = mp::K_ATTN; r.a = a; r.B = NB;
@@ -866,6 +898,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             dev->ops.push_back(r);
         }
         HIPCHK(mp::op_sa_attn(a, NB, s));
+        }
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.part = dev->sa_part;
@@ -873,7 +906,9 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
         xp.q_f16 = m.weight_mode == MP_WEIGHTS_F16;
         const double xa_bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
-        const bool xa_in_oproj = tb.oproj_xa && !W.o8 && !W.xq8;
+        // direct XA (Q8_0 q_net / o_net, or long texts: mp_hip_set_xa_mode): x2 materialised
+        const bool xa_dir = W.xq8 || dev->xa_direct;
+        const bool xa_in_oproj = tb.oproj_xa && !W.o8 && !xa_dir;
         if (xa_in_oproj) {
             // f32: the fused XA rides in the O-projection's launch on a hand-off of x1
             g.xa = xp; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
@@ -883,18 +918,24 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
                              (W.o8 ? Fq : F) * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) {
             return rc;
         }
-        if (W.xq8) {
-            // cross-attention with Q8_0 q_net / o_net, as ggml computes it (1713-1767):
-            // q = Q8(q_net) LN(x) (GEMV), then x2 = x + Q8(o_net) attn(q, K, V) (xa_q8_kernel)
+        if (xa_dir) {
+            // cross-attention as ggml computes it (1713-1767): q = q_net LN(x) (GEMV), then
+            // x2 = x + o_net attn(q, K, V) (xa_q8_kernel / xa_f32_kernel); Q8_0 q_net / o_net
+            // quantise their activations, else f32 (the bf16 mode keeps XA f32)
             g = gemv_base(dev); g.layer = l;
             g.W = W.xq; g.Wq = W.xq8.pq; g.Wd = W.xq8.pd; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
             g.out = dev->xqb; g.out_ld = 128;
-            if ((rc = run("xq", tq.xq, g, Fq * (128.0 * 768) + A * act * (768 + 128))) != MP_OK) return rc;
-            mp::XaQ8P xq{dev->x, dev->x2, dev->xqb, W.xo8.q, W.xo8.d, dev->xak, dev->xav, dev->T, dev->Tmax, l, L};
+            const double Fx = W.xq8 ? Fq : A;
+            if ((rc = run("xq", W.xq8 ? tq.xq : tb.xq, g, Fx * (128.0 * 768) + A * act * (768 + 128))) != MP_OK) return rc;
+            mp::XaQ8P xq{};
+            xq.x = dev->x; xq.x2 = dev->x2; xq.q = dev->xqb; xq.xak = dev->xak; xq.xav = dev->xav; xq.T = dev->T;
+            xq.Tmax = dev->Tmax; xq.layer = l; xq.nlayers = L;
+            if (W.xq8) { xq.wo = W.xo8.q; xq.wod = W.xo8.d; }
+            else xq.wof = W.xo;
             if (record) {
                 mp::OpRec r{};
-                r.name = "xa_q8"; r.kind = mp::K_XAQ8; r.xq = xq; r.B = NB;
-                r.bytes = Fq * (768.0 * 128) + A * act * (128.0 + 768 * 2 + 2.0 * 128 * dev->Tmax);
+                r.name = W.xq8 ? "xa_q8" : "xa_dir"; r.kind = mp::K_XAQ8; r.xq = xq; r.B = NB;
+                r.bytes = Fx * (768.0 * 128) + A * act * (128.0 + 768 * 2 + 2.0 * 128 * dev->Tmax);
                 dev->ops.push_back(r);
             }
             HIPCHK(mp::op_xa_q8(xq, NB, s));
@@ -911,8 +952,9 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // LN + FFN up + GELU (1796-1799)
         g = gemv_base(dev); g.layer = l;
         g.W = W.ff1; g.Wb = b16 ? m.pk_ff1[l] : nullptr; g.N = 3072; g.lnw = W.norm_ff; g.out = dev->h; g.out_ld = 3072;
-        if (W.xq8) {  // x2 materialised by the Q8 o_net
+        if (xa_dir) {  // x2 materialised by the direct XA
             g.src = dev->x2; g.src_ld = 768;
+            if (b16) g.out_b16 = dev->h_b16;
             if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
         } else {      // x2 = x + merged XA split states, stored by block 0 for the FFN residual
             g.src = dev->x; g.src_ld = 768; g.part = dev->xa_part; g.xres = dev->x2;
@@ -1241,7 +1283,7 @@ int run_preamble(mp_dev *dev) {
     //     not with Q8_0 q_net / o_net, whose activations ggml quantises: unfused XA there)
     for (int b = 0; b < NB; ++b)
         for (int l = 0; l < L; ++l) {
-            if (m.dec[l].xq8) continue;
+            if (m.dec[l].xq8 || dev->xa_direct) continue;
             const size_t xo = ((size_t)(b * L + l) * Tmax) * 128, po = ((size_t)(b * L + l) * Tmax) * 768;
             GemmP gp{};
             gp.A = dev->xak + xo; gp.lda = 128; gp.W = m.xq_t[l]; gp.C = dev->kp + po; gp.ldc = 768;
@@ -1391,6 +1433,12 @@ int mp_hip_max_batch(mp_dev *dev) {
     return mp::h16_mode(dev->m.weight_mode) || (dev->m.weight_mode == MP_WEIGHTS_Q8 && dev->m.q8_all) ? 16 : 8;
 }
 
+int mp_hip_set_xa_mode(mp_dev *dev, int xa_mode) {
+    if (!dev || xa_mode < MP_XA_AUTO || xa_mode > MP_XA_DIRECT) return MP_ERR_ARG;
+    dev->xa_mode = xa_mode;
+    return MP_OK;
+}
+
 int mp_hip_set_kv_mode(mp_dev *dev, int kv_mode) {
     if (!dev || (kv_mode != MP_KV_F32 && kv_mode != MP_KV_BF16)) return MP_ERR_ARG;
     dev->kv_mode = kv_mode;
@@ -1452,7 +1500,7 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
                       (dev->trace != nullptr) == trace && dev->params.ignore_eos == params->ignore_eos &&
                       (dev->params.temperature >= 0.01f) == (params->temperature >= 0.01f) &&
                       dev->params.emit_eos_frame == params->emit_eos_frame &&
-                      dev->kv16 == (dev->kv_mode == MP_KV_BF16);
+                      dev->kv16 == (dev->kv_mode == MP_KV_BF16) && dev->xa_direct == want_xa_direct(dev, Tmax);
     dev->params = *params;
     if (!same) {
         if (int rc = alloc_batch(dev, B, Tmax, max_steps, trace)) return rc;
@@ -1498,6 +1546,7 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->argeos, 0, NB * 4, dev->stream));
     // hand-off tags restart with the iteration counter (ndone[1]): no stale tag may match
     HIPCHK(hipMemsetAsync(dev->xh, 0, (size_t)NB * 768 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go
     HIPCHK(hipStreamSynchronize(dev->stream));
     return MP_OK;
@@ -1819,12 +1868,14 @@ const char *mp_hip_op_name(mp_dev *dev, int op) {
 double mp_hip_op_bytes(mp_dev *dev, int op) {
     if (!dev || op < 0 || op >= (int)dev->ops.size()) return -1.0;
     const mp::OpRec &r = dev->ops[op];
-    if (r.kind == mp::K_ATTN) {
+    if (r.kind == mp::K_ATTN || r.add_sa) {
         // live cache length of slot 0 after the run: keys 0..pos
         int pos = 0;
         hipMemcpy(&pos, dev->pos, 4, hipMemcpyDeviceToHost);
-        // K, V rows + q in + the split states out
-        return 4.0 * dev->NB * ((double)(pos + 1) * 768 * 2 + 768 + mp::NH * mp::SA_SPLITS * mp::SA_PART);
+        // K, V rows (+ q in, unless handed over in-launch) + the split states out
+        const double kvb = dev->kv16 ? 2.0 : 4.0;
+        return (r.add_sa ? r.bytes : 4.0 * dev->NB * 768) +
+               dev->NB * ((double)(pos + 1) * 768 * 2 * kvb + 4.0 * mp::NH * mp::SA_SPLITS * mp::SA_PART);
     }
     return r.bytes;
 }

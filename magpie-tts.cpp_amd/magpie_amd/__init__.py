@@ -66,6 +66,7 @@ SYMBOLS = [
     ("mp_hip_weight_mode", _I, [_P]),
     ("mp_hip_max_batch", _I, [_P]),
     ("mp_hip_set_kv_mode", _I, [_P, _I]),
+    ("mp_hip_set_xa_mode", _I, [_P, _I]),
     ("mp_hip_model_info", _I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_size_t)]),
     ("mp_hip_free", None, [_P]),
     ("mp_hip_error", ctypes.c_char_p, [_P]),
@@ -173,8 +174,9 @@ class Device:
     WEIGHT_MODES = {"f32": 0, "as_stored": 0, "bf16": 1, "q8": 2, "q4": 2, "f16": 3}
 
     KV_MODES = {"f32": 0, "bf16": 1}
+    XA_MODES = {"auto": 0, "reassoc": 1, "direct": 2}
 
-    def __init__(self, model_path: str, device: int = 0, weights: str = "f32", kv: str = "f32"):
+    def __init__(self, model_path: str, device: int = 0, weights: str = "f32", kv: str = "f32", xa: str = "auto"):
         """weights: "f32" (as stored, widened to f32), "bf16" (decode projections
         on bf16 MFMA, activations rounded to bf16; batches up to 16) or "q8" / "q4"
         (the file's Q8_0 / Q4_0 tensors kept as int8 (Q4_0: q - 8, losslessly),
@@ -183,7 +185,12 @@ class Device:
         F16 file with ggml's F16 mul_mat semantics: activations rounded to f16,
         decode projections on f16 MFMA; batches up to 16).
         kv: SA cache element type, "f32" (the reference's) or "bf16" (rows rounded
-        to bf16 on append, mp_hip_set_kv_mode)."""
+        to bf16 on append, mp_hip_set_kv_mode).
+        xa: cross-attention form (mp_hip_set_xa_mode): "auto" (direct above 160 text
+        tokens), "reassoc" (K'/V' precomputed, fused in the O-projection launch) or
+        "direct" (q_net, attention, o_net)."""
+        if xa not in self.XA_MODES:
+            raise ValueError(f"xa must be one of {sorted(self.XA_MODES)}")
         if kv not in self.KV_MODES:
             raise ValueError(f"kv must be one of {sorted(self.KV_MODES)}")
         if weights not in self.WEIGHT_MODES:
@@ -198,6 +205,8 @@ class Device:
         self._check(self.lib.mp_hip_load_model_ex(self.h, model_path.encode(), self.WEIGHT_MODES[weights]))
         self.kv = kv
         self._check(self.lib.mp_hip_set_kv_mode(self.h, self.KV_MODES[kv]))
+        self.xa = xa
+        self._check(self.lib.mp_hip_set_xa_mode(self.h, self.XA_MODES[xa]))
 
     def _check(self, rc: int) -> None:
         if rc != MP_OK:

@@ -257,11 +257,11 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
     if constexpr (PRO == PRO_SA_MERGE) {
         // self-attention output of every head: its SA_SPLITS key-split states merged
         static_assert(K == D, "SA output is d_model wide");
-        merge_weights<SA_SPLITS>(p.part, SA_PART, NB * NH, sc);
-        lds_sync();
         constexpr int ITEMS = NB * (K / 4);
-        for (int base = 0; base < ITEMS; base += MP_BLOCK * IB) {
-            float4 o[IB][SA_SPLITS];
+        float4 o[IB][SA_SPLITS];
+        // the first round's split outputs are loaded together with the split weights'
+        // (m, l): one memory round trip before the first combine, not two
+        auto load_o = [&](int base) {
 #pragma unroll
             for (int u = 0; u < IB; ++u) {
                 const int e = base + u * MP_BLOCK + tid;
@@ -271,6 +271,12 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 for (int s2 = 0; s2 < SA_SPLITS; ++s2)
                     o[u][s2] = *(const float4 *)(p.part + ((size_t)q * SA_SPLITS + s2) * SA_PART + 4 + k % DH);
             }
+        };
+        load_o(0);
+        merge_weights<SA_SPLITS>(p.part, SA_PART, NB * NH, sc);
+        lds_sync();
+        for (int base = 0; base < ITEMS; base += MP_BLOCK * IB) {
+            if (base) load_o(base);
 #pragma unroll
             for (int u = 0; u < IB; ++u) {
                 const int e = base + u * MP_BLOCK + tid;
@@ -292,11 +298,10 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         // stores x2 (the FFN's residual input); act = LN(x2) * lnw with the same one-wave
         // DPP statistics as PRO_LN, so batch 1 and batched prologues agree bit for bit
         static_assert(K == D, "XA output is d_model wide");
-        merge_weights<XA_SPLITS>(p.part, XA_PART, NB, sc);
-        lds_sync();
         constexpr int ITEMS = NB * (K / 4);
-        for (int base = 0; base < ITEMS; base += MP_BLOCK * IB) {
-            float4 o[IB][XA_SPLITS], xv[IB];
+        float4 o[IB][XA_SPLITS], xv[IB];
+        // the first round's inputs are loaded together with the split weights' (m, l)
+        auto load_o = [&](int base) {
 #pragma unroll
             for (int u = 0; u < IB; ++u) {
                 const int e = base + u * MP_BLOCK + tid;
@@ -307,6 +312,12 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 for (int s2 = 0; s2 < XA_SPLITS; ++s2)
                     o[u][s2] = *(const float4 *)(p.part + ((size_t)b * XA_SPLITS + s2) * XA_PART + 4 + k);
             }
+        };
+        load_o(0);
+        merge_weights<XA_SPLITS>(p.part, XA_PART, NB, sc);
+        lds_sync();
+        for (int base = 0; base < ITEMS; base += MP_BLOCK * IB) {
+            if (base) load_o(base);
 #pragma unroll
             for (int u = 0; u < IB; ++u) {
                 const int e = base + u * MP_BLOCK + tid;

@@ -3,7 +3,8 @@
 # pass per counter group, never combined with any trace domain. FETCH_SIZE needs 3
 # TCC counters and WRITE_SIZE 2, so they get separate passes; the MFMA pass holds 4
 # SQ counters + 1 GRBM. Workloads: f32 B=1 decode (the bench line), bf16 B=16
-# decode (configs[2]), the codec (8 x 32 frames). Then tools_dev/pmc_report.py TAG.
+# decode (configs[2]), Q8_0 B=16 decode (int8 MFMA), the codec (8 x 32 frames).
+# Then tools_dev/pmc_report.py TAG.
 # Usage: tools_dev/pmc_collect.sh TAG
 set -e -o pipefail
 TAG=${1:-r02}
@@ -22,6 +23,10 @@ run b16b16_fetch FETCH_SIZE tools_dev/pmc_workload.py decode bf16 16
 run b16b16_write WRITE_SIZE tools_dev/pmc_workload.py decode bf16 16
 run b16b16_mfma "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" \
   tools_dev/pmc_workload.py decode bf16 16
+run q8b16_fetch FETCH_SIZE tools_dev/pmc_workload.py decode q8 16
+run q8b16_write WRITE_SIZE tools_dev/pmc_workload.py decode q8 16
+run q8b16_mfma "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_I8 SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" \
+  tools_dev/pmc_workload.py decode q8 16
 run codec_fetch FETCH_SIZE tools_dev/pmc_workload.py codec
 run codec_write WRITE_SIZE tools_dev/pmc_workload.py codec
 run codec_mfma "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" \

@@ -31,9 +31,10 @@ SIMDS = 256 * 4
 CLK = 2.4e9  # shader clock (MI355X_MICROARCH.md)
 # kernels whose bulk global loads are 16 B per lane (float4 / uint4 / half8)
 WIDE = ("gemv_kernel", "gemm_b16_kernel", "xa_part_kernel", "sa_attn_kernel", "lt_ffn2_kernel", "lt_ffn_kernel",
-        "conv_mfma_kernel")
-DECODE = ("gemv_kernel", "sa_attn_kernel", "xa_part_kernel", "lt_finalize_kernel", "gemm_b16_kernel", "gemv_q8_kernel",
-          "lt_ffn_kernel", "lt_ffn2_kernel", "lt_merge_kernel", "lt_pick_kernel", "xa_q8_kernel", "embed_kernel")
+        "conv_mfma_kernel", "gemm_q8_kernel_dec")
+DECODE = ("gemv_kernel", "sa_attn_kernel", "xa_part_kernel", "lt_finalize_kernel", "gemm_b16_kernel", "gemm_q8_kernel_dec",
+          "lt_ffn_kernel", "lt_ffn2_kernel", "lt_merge_kernel", "lt_pick_kernel", "xa_q8_kernel", "xa_f32_kernel",
+          "embed_kernel")
 
 
 def rows(tag, name):
@@ -84,6 +85,9 @@ def decode_ops(tag, pre, ops_file, mfma):
             o["mfma_busy_cycles"] = round(busy)
             o["gui_active_cycles"] = round(gui)
             o["mfma_util"] = round(busy / (gui * SIMDS), 4) if gui else None
+            mops = [v for k, v in rec.items() if k.startswith("SQ_INSTS_VALU_MFMA_MOPS_")]
+            if mops:
+                o["mfma_ops"] = round(float(np.mean(mops[0])) * 512)  # MOPS x 512 = multiply-adds x 2
         out[op] = o
     return out
 
@@ -152,7 +156,8 @@ def main():
     src = ("rocprofv3 --pmc, separate passes per counter group (tools_dev/pmc_collect.sh), eager launches; "
            "bytes = FETCH_SIZE x 1024 (x2 for 16 B/lane kernels, gfx950) + WRITE_SIZE x 1024")
     for pre, ops_file, mfma, name in (("f32b1", "pmc_ops_f32_1.json", False, "decode_f32_b1"),
-                                      ("b16b16", "pmc_ops_bf16_16.json", True, "decode_bf16_b16")):
+                                      ("b16b16", "pmc_ops_bf16_16.json", True, "decode_bf16_b16"),
+                                      ("q8b16", "pmc_ops_q8_16.json", True, "decode_q8_b16")):
         res = {"source": src, "workload": name, "ops": decode_ops(tag, pre, ops_file, mfma)}
         json.dump(res, open(os.path.join(REPO, "profiles", f"{tag}_pmc_{name}.json"), "w"), indent=1)
         print(f"== {name}")

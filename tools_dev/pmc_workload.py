@@ -1,7 +1,8 @@
 """Workloads for the PMC passes (tools_dev/pmc_collect.sh), every kernel launched
 eagerly (MAGPIE_EAGER=1 is set by the caller) so rocprofv3 attributes counters per
 dispatch:
-  decode WEIGHTS B : the bench's model (Magpie-357M, decisive LT heads), T=64, EOS
+  decode WEIGHTS B : the bench's model (Magpie-357M, decisive LT heads; WEIGHTS q8:
+                     its Q8_0 twin), T=64, EOS
                      masked, 64 frames; writes the op order of one iteration to
                      gpurun_out/pmc_ops_<WEIGHTS>_<B>.json
   codec            : the bench's codec shape, 8 chunks x 32 frames, 4 decodes"""
@@ -29,7 +30,10 @@ if mode == "codec":
 else:
     weights = sys.argv[2] if len(sys.argv) > 2 else "f32"
     B = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-    path = ma.synth_gguf(os.path.join(cache, "magpie_357m_f32_k32.gguf"), lt_head_scale=ma.DECISIVE)
+    if weights == "q8":  # the reference converter's Q8_0 patterns (int8 MFMA decode projections)
+        path = ma.synth_gguf(os.path.join(cache, "magpie_357m_q8_k32.gguf"), dtype="q8_0", lt_head_scale=ma.DECISIVE)
+    else:
+        path = ma.synth_gguf(os.path.join(cache, "magpie_357m_f32_k32.gguf"), lt_head_scale=ma.DECISIVE)
     dev = ma.Device(path, weights=weights)
     toks = [ma.synthetic_tokens(64, seed=1000 + b) for b in range(B)]
     r = dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=int(os.environ.get("PMC_FRAMES", "64")),

@@ -67,9 +67,14 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmP p, int splits) {
     }
 }
 
+// K steps of 16 with PF steps' operand loads in flight per thread (register ring):
+// a step's loads are issued PF steps before its tile is staged, so the global latency
+// is paid once per PF steps, not per step (the preamble GEMMs have small grids: one
+// workgroup per CU or fewer). The arithmetic (k order, FMA order) is the plain
+// LDS-tiled GEMM's.
 template <int EPI, int TAPS>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
-    constexpr int BM = 64, BN = 64, BK = 16;
+    constexpr int BM = 64, BN = 64, BK = 16, PF = 4;
     __shared__ float As[BK][BM + 4];
     __shared__ float Ws[BK][BN + 4];
     const int tid = threadIdx.x;
@@ -78,50 +83,56 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
     float acc[4][4] = {};
     const int lr = tid >> 2, lk = (tid & 3) * 4;  // loader: row lr, k lk..lk+3
     const int ks = p.K / gridDim.z, kbeg = blockIdx.z * ks;  // split-K slice (gridDim.z == 1: all of K)
-    for (int k0 = kbeg; k0 < kbeg + ks; k0 += BK) {
-        {   // A tile
-            const int m = m0 + lr;
-            float a[4] = {0.f, 0.f, 0.f, 0.f};
-            if (m < p.M) {
-                if constexpr (TAPS == 0) {
-                    const float4 v = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + lk);
-                    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-                } else {
-                    // weights are tap-major [N][tap][Cin] (re-laid out at load), so a
-                    // 16-wide K step lies inside one tap: one float4 of input row t-2+tap
-                    const int t = m % p.rows_per_utt;
-                    const int tap = k0 / p.lda, i = k0 % p.lda + lk;
-                    const int st = t - (TAPS - 1) + tap;
-                    if (st >= 0) {
-                        const float4 v = *(const float4 *)(p.A + (size_t)(m - (TAPS - 1) + tap) * p.lda + i);
-                        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-                    }
-                }
+    const int nsteps = ks / BK;
+    const int m = m0 + lr, n = n0 + lr;
+    auto load_a = [&](int k0) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < p.M) {
+            if constexpr (TAPS == 0) {
+                v = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + lk);
+            } else {
+                // weights are tap-major [N][tap][Cin] (re-laid out at load), so a
+                // 16-wide K step lies inside one tap: one float4 of input row t-2+tap
+                const int t = m % p.rows_per_utt;
+                const int tap = k0 / p.lda, i = k0 % p.lda + lk;
+                if (t - (TAPS - 1) + tap >= 0) v = *(const float4 *)(p.A + (size_t)(m - (TAPS - 1) + tap) * p.lda + i);
             }
+        }
+        return v;
+    };
+    auto load_w = [&](int k0) {
+        return n < p.N ? *(const float4 *)(p.W + (size_t)n * p.K + k0 + lk) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    float4 ra[PF], rw[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (u < nsteps) { ra[u] = load_a(kbeg + u * BK); rw[u] = load_w(kbeg + u * BK); }
+    for (int base = 0; base < nsteps; base += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int step = base + u;
+            if (step >= nsteps) break;
+            float a[4] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w};
             if (p.xround)  // F16 weights: the operand ggml's F16 mul_mat multiplies (uniform branch)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) a[e] = (float)(_Float16)a[e];
 #pragma unroll
             for (int e = 0; e < 4; ++e) As[lk + e][lr] = a[e];
-        }
-        {   // W tile
-            const int n = n0 + lr;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (n < p.N) v = *(const float4 *)(p.W + (size_t)n * p.K + k0 + lk);
-            Ws[lk + 0][lr] = v.x; Ws[lk + 1][lr] = v.y; Ws[lk + 2][lr] = v.z; Ws[lk + 3][lr] = v.w;
-        }
-        __syncthreads();
+            Ws[lk + 0][lr] = rw[u].x; Ws[lk + 1][lr] = rw[u].y; Ws[lk + 2][lr] = rw[u].z; Ws[lk + 3][lr] = rw[u].w;
+            if (step + PF < nsteps) { ra[u] = load_a(kbeg + (step + PF) * BK); rw[u] = load_w(kbeg + (step + PF) * BK); }
+            __syncthreads();
 #pragma unroll
-        for (int kk = 0; kk < BK; ++kk) {
-            const float4 a4 = *(const float4 *)&As[kk][ty * 4];
-            const float4 w4 = *(const float4 *)&Ws[kk][tx * 4];
-            const float a[4] = {a4.x, a4.y, a4.z, a4.w}, w[4] = {w4.x, w4.y, w4.z, w4.w};
+            for (int kk = 0; kk < BK; ++kk) {
+                const float4 a4 = *(const float4 *)&As[kk][ty * 4];
+                const float4 w4 = *(const float4 *)&Ws[kk][tx * 4];
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w}, wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * w[j];
+                    for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * wv[j];
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
     gemm_store<EPI>(p, acc, m0 + ty * 4, n0 + tx * 4);
 }

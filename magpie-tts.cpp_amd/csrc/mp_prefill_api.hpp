@@ -44,7 +44,7 @@ struct GemmP {
 
 // Split count of a preamble GEMM over K (fixed per K: batch-invariant results).
 inline int gemm_splits(int K) {
-    int s = K / 384;
+    int s = K / 96;
     if (s < 1) s = 1;
     if (s > 16) s = 16;
     while (s > 1 && (K % (s * 32)) != 0) --s;  // whole 32-wide (Q8_0) blocks per split

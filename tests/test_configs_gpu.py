@@ -17,7 +17,7 @@ from parity import compare_forced
 
 pytestmark = pytest.mark.gpu
 
-TIE_EPS = 1e-2          # bf16 near-tie bar (test_decode_gpu.py)
+TIE_EPS = 3e-2          # bf16 near-tie bar (test_decode_gpu.py: the oracle's own f32/f64 spread)
 Q8_TIE_EPS = 1e-1       # Q8_0 near-tie bar (test_decode_gpu.py: the oracle's own f32/f64 spread)
 HIDDEN_TOL, HIDDEN_REL = 3e-2, 5e-3
 

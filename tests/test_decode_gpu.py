@@ -222,7 +222,10 @@ def test_sampling_eos_from_argmax(ma, oracle, eos_model):
 # over 24 frames (a mis-indexed fragment gives O(1)). The bar is therefore wider
 # than f32's: identical codes up to a decision whose oracle margin is < 1e-2
 # (logits / draw probability), hidden within 3e-2 max abs and 5e-3 relative L2.
-BF16_TIE_EPS = 1e-2
+# bf16 near-tie bar: the oracle's own bf16 mode with f32 instead of f64 accumulation
+# shifts margins by up to 0.026 and flips a decision of margin 0.0119
+# (test_oracle_cpu.py::test_bf16_mode_accumulation_spread)
+BF16_TIE_EPS = 3e-2
 BF16_HIDDEN_TOL = 3e-2
 BF16_HIDDEN_REL = 5e-3
 

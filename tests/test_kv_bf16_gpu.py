@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 CTX = 110
 TIE_EPS_F32 = 2e-4
-BF16_TIE_EPS = 1e-2
+BF16_TIE_EPS = 3e-2  # the oracle's own bf16 f32/f64 spread (test_decode_gpu.py)
 # bf16 weights AND bf16 cache: two bf16 roundings whose flips (GPU f32 vs oracle f64
 # arithmetic rounding a value to the other side of a bf16 half-ulp) both reach the
 # logits; the near-tie bar is doubled (measured: first flip at margin 0.015)

@@ -90,6 +90,27 @@ def test_oracle_modes_agree(oracle, small_model):
     np.testing.assert_array_equal(a["codes"], b["codes"])
 
 
+def test_bf16_mode_accumulation_spread(oracle, small_model):
+    """Basis of the bf16 tie bar (BF16_TIE_EPS, test_decode_gpu.py): the oracle's own bf16
+    mode (weight mode 1) with f32 instead of f64 accumulation, teacher forced along its
+    f64 run, moves the top-1/top-2 margins by up to ~0.026 and flips the decision whose
+    f64 margin is 0.0119, so a GPU difference below that spread is rounding, not error."""
+    import magpie_amd as ma
+    tok = ma.synthetic_tokens(24, seed=1000)
+    m = oracle.Model(small_model)
+    m.set_weight_mode(1)
+    a = m.synthesize(tok, speaker=1, max_steps=40, ignore_eos=True, trace=False)
+    oracle.set_mode(acc64=False, gelu_f16=False, threads=8)
+    f = m.synthesize_forced(tok, a["codes"], speaker=1, ignore_eos=True)
+    oracle.set_mode(acc64=True, gelu_f16=False, threads=8)
+    m.close()
+    shift = np.abs(np.asarray(f["margins"]) - np.asarray(a["margins"])).max()
+    diff = np.argwhere(np.asarray(f["codes"]) != np.asarray(a["codes"]))
+    flipped = [float(np.asarray(a["margins"])[i, j]) for i, j in diff]
+    assert 1e-2 < shift < 3e-2, shift
+    assert flipped and max(flipped) > 1e-2 and max(flipped) < 3e-2, flipped
+
+
 def test_eos_forbidden_for_first_four_frames(oracle, eos_model):
     """min_generated_frames = 4 (magpie.cpp:4267, 4325): the EOS-biased model stops
     at step 4 exactly; the EOS frame is not emitted (4349-4352)."""

@@ -15,7 +15,7 @@ from parity import compare_codes, compare_forced
 pytestmark = pytest.mark.gpu
 
 HIDDEN_TOL = 2e-3
-BF16_TIE_EPS, BF16_HIDDEN_TOL = 1e-2, 3e-2
+BF16_TIE_EPS, BF16_HIDDEN_TOL = 3e-2, 3e-2  # test_decode_gpu.py
 
 
 @pytest.fixture(scope="module")

@@ -161,16 +161,36 @@ __global__ __launch_bounds__(256) void gemm_q8_kernel(GemmP p) {
     const int nblk = p.K / 32;
     const int bs = nblk / gridDim.z, bbeg = blockIdx.z * bs;  // split-K slice in whole blocks
     float acc[4][4] = {};
-    for (int kb = bbeg; kb < bbeg + bs; ++kb) {
+    // PF blocks' operand loads in flight per thread (register ring), as gemm_f32_kernel
+    constexpr int PF = 4;
+    const int m = m0 + lr, n = n0 + lr;
+    float4 ra0[PF], ra1[PF];
+    uint2 rwv[PF];
+    float rwd[PF];
+    auto load = [&](int u, int kb) {
         const int k0 = kb * 32 + part * 8;
+        ra0[u] = ra1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < p.M) {
+            ra0[u] = *(const float4 *)(p.A + (size_t)m * p.lda + k0);
+            ra1[u] = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + 4);
+        }
+        rwv[u] = make_uint2(0u, 0u);
+        rwd[u] = 0.f;
+        if (n < p.N) {
+            rwv[u] = *(const uint2 *)(p.Wq + (size_t)n * p.K + k0);
+            rwd[u] = __half2float(__ushort_as_half(p.Wd[(size_t)n * nblk + kb]));
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (u < bs) load(u, bbeg + u);
+    for (int base = 0; base < bs; base += PF)
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+        const int step = base + u;
+        if (step >= bs) break;
         {   // A rows -> Q8_0
-            float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            const int m = m0 + lr;
-            if (m < p.M) {
-                const float4 v0 = *(const float4 *)(p.A + (size_t)m * p.lda + k0);
-                const float4 v1 = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + 4);
-                a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w; a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
-            }
+            float a[8] = {ra0[u].x, ra0[u].y, ra0[u].z, ra0[u].w, ra1[u].x, ra1[u].y, ra1[u].z, ra1[u].w};
             float amax = 0.f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(a[e]));
@@ -183,17 +203,11 @@ __global__ __launch_bounds__(256) void gemm_q8_kernel(GemmP p) {
             if (part == 0) Ad[lr] = __half2float(__float2half(dd));
         }
         {   // W rows: int8 + block scale
-            const int n = n0 + lr;
-            uint2 wv = make_uint2(0u, 0u);
-            float wd = 0.f;
-            if (n < p.N) {
-                wv = *(const uint2 *)(p.Wq + (size_t)n * p.K + k0);
-                wd = __half2float(__ushort_as_half(p.Wd[(size_t)n * nblk + kb]));
-            }
-            Wq[lr][2 * part] = (int)wv.x;
-            Wq[lr][2 * part + 1] = (int)wv.y;
-            if (part == 0) Wd[lr] = wd;
+            Wq[lr][2 * part] = (int)rwv[u].x;
+            Wq[lr][2 * part + 1] = (int)rwv[u].y;
+            if (part == 0) Wd[lr] = rwd[u];
         }
+        if (step + PF < bs) load(u, bbeg + step + PF);
         __syncthreads();
         int s[4][4] = {};
 #pragma unroll

@@ -166,41 +166,60 @@ __global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
         const int stp = p.step[b];
         i0 = wave_pick(p.logits + (size_t)b * VCB + ts_dep(t_start), p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp,
                        NCB - 1, scratch, amax);
-        if (tid != 0) return;
     }
-    int *ccp = p.codes_cur + b * NCB;
-    ccp[NCB - 1] = i0;
-    int cc[NCB];
+    // lane 0 keeps the books; the wave then embeds the next frame of a slot that advances
+    int adv = 0, np = 0;
+    int cc[NCB] = {};
+    if (tid == 0) {
+        int *ccp = p.codes_cur + b * NCB;
+        ccp[NCB - 1] = i0;
 #pragma unroll
-    for (int cb = 0; cb < NCB - 1; ++cb) cc[cb] = ccp[cb];
-    cc[NCB - 1] = i0;
-    if (p.smp.amax) p.smp.amax[b * NCB + NCB - 1] = amax;
-    // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
-    bool eos = amax == p.audio_eos;
-    eos |= p.smp.argeos[b] != 0;
-    p.smp.argeos[b] = 0;
-    if (p.lt_only) return;  // magpie_local_transformer_sample_all: codes only
-    for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
-    const int s = p.step[b];
-    if (eos) {
-        // graph_reuse drops the EOS frame (4349-4352); the streaming loop emits it (4800-4806)
-        if (p.emit_eos)
-            for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
-        p.done[b] = 1;
-        p.nframes[b] = p.emit_eos ? s + 1 : s;
-        atomicAdd(p.ndone, 1);
-        return;
+        for (int cb = 0; cb < NCB - 1; ++cb) cc[cb] = ccp[cb];
+        cc[NCB - 1] = i0;
+        if (p.smp.amax) p.smp.amax[b * NCB + NCB - 1] = amax;
+        // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
+        bool eos = amax == p.audio_eos;
+        eos |= p.smp.argeos[b] != 0;
+        p.smp.argeos[b] = 0;
+        if (!p.lt_only) {  // magpie_local_transformer_sample_all: codes only
+            for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
+            const int s = p.step[b];
+            if (eos) {
+                // graph_reuse drops the EOS frame (4349-4352); the streaming loop emits it (4800-4806)
+                if (p.emit_eos)
+                    for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
+                p.done[b] = 1;
+                p.nframes[b] = p.emit_eos ? s + 1 : s;
+                atomicAdd(p.ndone, 1);
+            } else {
+                for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
+                p.step[b] = s + 1;
+                if (s + 1 >= p.max_steps) {
+                    p.done[b] = 1;
+                    p.nframes[b] = s + 1;
+                    atomicAdd(p.ndone, 1);
+                } else {
+                    for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
+                    np = p.pos[b] + 1;
+                    p.pos[b] = np;
+                    adv = 1;
+                }
+            }
+        }
     }
-    for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
-    p.step[b] = s + 1;
-    if (s + 1 >= p.max_steps) {
-        p.done[b] = 1;
-        p.nframes[b] = s + 1;
-        atomicAdd(p.ndone, 1);
-        return;
+    adv = __shfl(adv, 0, 64);
+    if (adv && p.x) {
+        np = __shfl(np, 0, 64);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) cc[cb] = __shfl(cc[cb], 0, 64);
+        // embed_kernel's arithmetic: codebooks summed in order, / 8, + position
+        for (int k = tid; k < D; k += 64) {
+            float s = p.emb[((size_t)0 * VCB + cc[0]) * D + k];
+#pragma unroll
+            for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + cc[cb]) * D + k];
+            p.x[(size_t)b * D + k] = s * 0.125f + p.pos_emb[(size_t)np * D + k];
+        }
     }
-    for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
-    p.pos[b] += 1;
     ts_end(p.ts, t_start);
 }
 
@@ -217,7 +236,6 @@ static bool gemv_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_LTFFN_MERGE) ok &= p.part && p.addsrc;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
-    if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
     if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
     if constexpr (PRO == PRO_LTARG_ATTN)
@@ -251,7 +269,6 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
 // Named entry points (one per fused op of the decode iteration), instantiated
 // for NB in {1, 2, 4, 8}.
 #define MP_DECODE_OPS(NB)                                                                                        \
-    hipError_t op_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t op_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV_SA>(p, s); }       \
     hipError_t op_xq_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_STORE>(p, s); }            \
@@ -346,9 +363,8 @@ hipError_t op_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_gemv<8, 1, 
 
 // ---------------------------------------------------------------- frame embedding
 // One workgroup per slot; each element summed over the 8 codebooks in order, /8,
-// + position: PRO_EMBED_LN's arithmetic, whose LayerNorm then runs in the qkv
-// GEMV's PRO_LN prologue (batches of 8+, where every qkv workgroup re-gathering
-// 9 rows per slot would cost more than this launch).
+// + position: the first frame's decoder input (reset_decode_state); every later
+// frame's is written by lt_finalize_kernel with the same arithmetic.
 __global__ __launch_bounds__(MP_BLOCK) void embed_kernel(EmbP p) {
     const int b = blockIdx.x;
     int c[NCB];

@@ -200,7 +200,6 @@ static bool b16_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
-    if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
     if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
     if constexpr (PRO == PRO_LTARG_ATTN)
@@ -231,7 +230,6 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
 }
 
 #define MP_B16_OPS(NB)                                                                                                  \
-    hipError_t b16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t b16_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV_SA>(p, s); }       \
     hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }   \
@@ -249,7 +247,6 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     hipError_t b16_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }
 
 #define MP_F16_OPS(NB)                                                                                                  \
-    hipError_t f16_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_EMBED_LN, EPI_QKV, true>(p, s); } \
     hipError_t f16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV, true>(p, s); }             \
     hipError_t f16_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV_SA, true>(p, s); }       \
     hipError_t f16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID, true>(p, s); }   \

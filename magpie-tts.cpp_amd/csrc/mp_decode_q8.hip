@@ -332,7 +332,6 @@ static bool q8_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_LTFFN_MERGE) ok &= p.part && p.addsrc;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
-    if constexpr (PRO == PRO_EMBED_LN) ok &= p.emb && p.codes && p.pos_emb && p.pos && p.xres && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
     if constexpr (PRO == PRO_LT_ATTN) ok &= p.ltq && p.ltk && p.ltv;
     if constexpr (PRO == PRO_LTARG_ATTN)
@@ -358,7 +357,6 @@ static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
 // pos_ff conv weights stay F32 in the reference's Q8 file and run on the f32
 // GEMV family), instantiated for NB in {1, 2, 4, 8, 16}.
 #define MP_Q8_OPS(NB)                                                                                                  \
-    hipError_t q8_qkv_embed_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_EMBED_LN, EPI_QKV>(p, s); } \
     hipError_t q8_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t q8_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }      \
     hipError_t q8_xq_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_LN, EPI_STORE>(p, s); }            \

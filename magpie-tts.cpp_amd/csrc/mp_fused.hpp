@@ -447,68 +447,6 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[(size_t)s * K + k] = y;
         }
         lds_sync();
-    } else if constexpr (PRO == PRO_EMBED_LN && NB >= 2) {
-        static_assert(K == D, "embed prologue is d_model wide");
-        const int lane = tid & 63, w = tid >> 6;
-        float g[K / 64];
-        load_lnw<K / 64>(p.lnw, g);
-        for (int b = w; b < NB; b += MP_NWAVES) {
-            int c[NCB];
-#pragma unroll
-            for (int cb = 0; cb < NCB; ++cb) c[cb] = p.codes[b * NCB + cb];
-            const int ps = p.pos[b];
-            float x[K / 64];
-#pragma unroll
-            for (int i = 0; i < K / 64; ++i) {
-                const int k = lane + 64 * i;
-                float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
-#pragma unroll
-                for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
-                x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
-            }
-            if (blockIdx.x == 0)  // after every load of the row (a store would order the loads behind it)
-#pragma unroll
-                for (int i = 0; i < K / 64; ++i) p.xres[(size_t)b * D + lane + 64 * i] = x[i];
-            float mean, var;
-            wave_meanvar<K / 64>(x, mean, var);
-            const float rstd = 1.0f / sqrtf(var + p.eps);
-#pragma unroll
-            for (int i = 0; i < K / 64; ++i) {
-                const int k = lane + 64 * i;
-                act[b * K + k] = ((x[i] - mean) * rstd) * g[i];
-            }
-        }
-        lds_sync();
-    } else if constexpr (PRO == PRO_EMBED_LN) {
-        static_assert(K == D, "embed prologue is d_model wide");
-        const int lane = tid & 63, w = tid >> 6;
-        constexpr int PER = K / 64, Q = PER / MP_NWAVES;
-        float g[PER];
-        load_lnw<PER>(p.lnw, g);
-        int c[NCB];
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) c[cb] = p.codes[cb];
-        const int ps = p.pos[0];
-        float x[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int k = lane + 64 * i;
-            float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
-#pragma unroll
-            for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
-            x[i] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
-        }
-        float mean, var;
-        wave_meanvar<PER>(x, mean, var);
-        const float rstd = 1.0f / sqrtf(var + p.eps);
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            if (i / Q != w) continue;
-            const int k = lane + 64 * i;
-            if (blockIdx.x == 0) p.xres[k] = x[i];
-            act[k] = ((x[i] - mean) * rstd) * g[i];
-        }
-        lds_sync();
     } else if constexpr (PRO == PRO_LTX_LN) {
         // one wave per slot at every batch size (wave_block_meanvar), so a batch
         // reproduces its utterances run alone bit for bit

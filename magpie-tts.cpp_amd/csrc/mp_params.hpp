@@ -31,7 +31,7 @@ constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = par
 enum Pro {
     PRO_PLAIN = 0,      // act = src
     PRO_LN = 1,         // act = LN(src) * lnw                          (magpie.cpp:2237-2259)
-    PRO_EMBED_LN = 2,   // x = sum_cb emb[cb][code]/8 + pos; act = LN(x)*lnw (2746-2787, 4376-4379)
+    // 2: retired (the frame embedding is written by lt_finalize_kernel, FinP::x)
     PRO_LTX_LN = 5,     // X = s_cb + lt_pos[cb]; act = LN(X)*lnw       (1015-1034, 946-958)
     PRO_LT_ATTN = 6,    // act = causal 1x256 attention over LT positions 0..cb (965-966)
     PRO_LTARG_ATTN = 8, // cb >= 1: code_{cb-1} = top-k draw / masked argmax of the logits; q|k|v of
@@ -184,9 +184,6 @@ struct GemvP {
     float *hidden_out;   // PRO_LN: block 0 stores the normalised vector (decoder hidden)
     float *trace;        // optional [B][trace_steps][768] hidden trace
     int trace_steps;
-    const float *emb;    // audio embeddings [8][2024][768]
-    const int *codes;    // [B][8]
-    const float *pos_emb;
     const int *pos;      // [B] decoder position
     float *xres;         // [B][768] residual stream
     int layer, nlayers;
@@ -248,6 +245,10 @@ struct FinP {
     int lt_only;    // magpie_local_transformer_sample_all: pick codebook 7, no loop bookkeeping
     int *iter;      // decode iteration counter (tags of the in-launch hand-offs), +1 per iteration
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
+    // the next frame's decoder input (magpie.cpp:2746-2787): for a slot that advances,
+    // x[b] = (sum over codebooks of emb[cb][code]) / 8 + pos_emb[new pos] (null: not written)
+    const float *emb, *pos_emb;
+    float *x;
 };
 
 // Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the

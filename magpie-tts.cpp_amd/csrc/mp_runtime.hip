@@ -31,7 +31,7 @@ namespace mp {
 // ---- launchers (mp_decode.hip / mp_prefill.hip)
 using GemvFn = hipError_t (*)(const GemvP &, hipStream_t);
 #define MP_DECL_OPS(NB)                                                                                     \
-    hipError_t op_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t op_qkv_##NB(const GemvP &, hipStream_t);        \
+    hipError_t op_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t op_oproj_##NB(const GemvP &, hipStream_t); hipError_t op_ff1_##NB(const GemvP &, hipStream_t);            \
     hipError_t op_ff1x_##NB(const GemvP &, hipStream_t); hipError_t op_oproj_xa_##NB(const GemvP &, hipStream_t);       \
     hipError_t op_qkv_sa_##NB(const GemvP &, hipStream_t); hipError_t op_xq_##NB(const GemvP &, hipStream_t); \
@@ -46,7 +46,7 @@ MP_DECL_OPS(4)
 MP_DECL_OPS(8)
 hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
 #define MP_DECL_B16(NB)                                                                                      \
-    hipError_t b16_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t b16_qkv_##NB(const GemvP &, hipStream_t);      \
+    hipError_t b16_qkv_##NB(const GemvP &, hipStream_t);      \
     hipError_t b16_oproj_##NB(const GemvP &, hipStream_t); hipError_t b16_ff1_##NB(const GemvP &, hipStream_t);          \
     hipError_t b16_ff2_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_a_##NB(const GemvP &, hipStream_t);           \
     hipError_t b16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_b_##NB(const GemvP &, hipStream_t);         \
@@ -59,7 +59,7 @@ MP_DECL_B16(4)
 MP_DECL_B16(8)
 MP_DECL_B16(16)
 #define MP_DECL_F16(NB)                                                                                      \
-    hipError_t f16_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t f16_qkv_##NB(const GemvP &, hipStream_t);      \
+    hipError_t f16_qkv_##NB(const GemvP &, hipStream_t);      \
     hipError_t f16_oproj_##NB(const GemvP &, hipStream_t); hipError_t f16_ff1_##NB(const GemvP &, hipStream_t);          \
     hipError_t f16_ff2_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_a_##NB(const GemvP &, hipStream_t);           \
     hipError_t f16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t f16_lt_b_##NB(const GemvP &, hipStream_t);         \
@@ -76,7 +76,7 @@ hipError_t f16_lt_bo_8(const GemvP &, hipStream_t);
 hipError_t f16_lt_bo_16(const GemvP &, hipStream_t);
 hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t, bool f16);
 #define MP_DECL_Q8(NB)                                                                                       \
-    hipError_t q8_qkv_embed_##NB(const GemvP &, hipStream_t); hipError_t q8_qkv_##NB(const GemvP &, hipStream_t);        \
+    hipError_t q8_qkv_##NB(const GemvP &, hipStream_t);        \
     hipError_t q8_oproj_##NB(const GemvP &, hipStream_t); hipError_t q8_xq_##NB(const GemvP &, hipStream_t);             \
     hipError_t q8_lt_in0_##NB(const GemvP &, hipStream_t);                                                             \
     hipError_t q8_lt_a_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_bg_##NB(const GemvP &, hipStream_t);           \
@@ -120,30 +120,30 @@ namespace mp {
 // oproj_xa: O-projection + the fused XA in one launch (EPI_RESID_XA)
 // qkv_sa: the QKV projection + the SA in one launch (EPI_QKV_SA)
 // xq: the direct XA's f32 q_net GEMV (f32 and bf16 modes); ff1: FFN up from a materialised x2
-struct OpTable { GemvFn qkv_embed, qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e, oproj_xa,
+struct OpTable { GemvFn qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e, oproj_xa,
                  qkv_sa, xq; };
-#define MP_TABLE(NB) { op_qkv_embed_##NB, op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
+#define MP_TABLE(NB) { op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, \
                        op_oproj_xa_##NB, op_qkv_sa_##NB, op_xq_##NB }
 // 16 slots in the f32 family only for a Q8_0 file's F32 tensors: its FFN convs and LT in_proj
 static const OpTable kTables[5] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TABLE(8),
-                                   {nullptr, nullptr, nullptr, op_ff1_16, nullptr, op_ff2_16, op_lt_in0_16, nullptr,
+                                   {nullptr, nullptr, op_ff1_16, nullptr, op_ff2_16, op_lt_in0_16, nullptr,
                                     nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, op_xq_16}};
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
-#define MP_TABLE_B16(NB) { b16_qkv_embed_##NB, b16_qkv_##NB, b16_oproj_##NB, b16_ff1p_##NB, b16_ff1_##NB, b16_ff2_##NB, \
+#define MP_TABLE_B16(NB) { b16_qkv_##NB, b16_oproj_##NB, b16_ff1p_##NB, b16_ff1_##NB, b16_ff2_##NB, \
                            op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_bg_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
                            b16_lt_d_##NB, b16_lt_e_##NB, b16_oproj_xa_##NB, b16_qkv_sa_##NB, op_xq_##NB }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
 // F16 weight mode (an F16 GGUF): the same MFMA family on f16, the LT in_proj included
-#define MP_TABLE_F16(NB) { f16_qkv_embed_##NB, f16_qkv_##NB, f16_oproj_##NB, nullptr, f16_ff1_##NB, f16_ff2_##NB, \
+#define MP_TABLE_F16(NB) { f16_qkv_##NB, f16_oproj_##NB, nullptr, f16_ff1_##NB, f16_ff2_##NB, \
                            f16_lt_in0_##NB, f16_lt_a_##NB, f16_lt_bg_##NB, f16_lt_b_##NB, f16_lt_c_##NB,  \
                            f16_lt_d_##NB, f16_lt_e_##NB, f16_oproj_xa_##NB, f16_qkv_sa_##NB }
 static const OpTable kTablesF16[5] = {MP_TABLE_F16(1), MP_TABLE_F16(2), MP_TABLE_F16(4), MP_TABLE_F16(8),
                                       MP_TABLE_F16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
-struct OpTableQ8 { GemvFn qkv_embed, qkv, oproj, xq, lt_in0, lt_a, lt_bg, lt_b, lt_e; };
-#define MP_TABLE_Q8(NB) { q8_qkv_embed_##NB, q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_lt_in0_##NB, \
+struct OpTableQ8 { GemvFn qkv, oproj, xq, lt_in0, lt_a, lt_bg, lt_b, lt_e; };
+#define MP_TABLE_Q8(NB) { q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_lt_in0_##NB, \
                           q8_lt_a_##NB, q8_lt_bg_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
 static const OpTableQ8 kTablesQ8[5] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8),
                                         MP_TABLE_Q8(16)};
@@ -859,34 +859,21 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.W = W.qkv; g.Wb = b16 ? m.pk_qkv[l] : nullptr; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
         g.Wq = W.qkv8.pq; g.Wd = W.qkv8.pd;
         g.kc = dev->kc; g.vc = dev->vc; g.kv16 = dev->kv16;
-        // layer 0 embeds the frame (2746-2787) in the prologue; batches of 8+ embed it once
-        // in a separate launch instead of in every workgroup (the same arithmetic)
-        const bool embed_in = l == 0 && NB < 8;
-        if (l == 0 && !embed_in) {
-            mp::EmbP ep{m.audio_emb, dev->codes_prev, m.dec_pos, dev->pos, dev->x};
-            if (record) {
-                mp::OpRec r{};
-                r.name = "embed"; r.kind = mp::K_EMBED; r.e = ep; r.B = NB;
-                r.bytes = A * act * (9.0 * 768 + 768);
-                dev->ops.push_back(r);
-            }
-            HIPCHK(mp::op_embed(ep, NB, s));
-        }
-        if (embed_in) { g.emb = m.audio_emb; g.codes = dev->codes_prev; g.pos_emb = m.dec_pos; g.xres = dev->x; }
+        // the frame embedding (2746-2787) is in x already: written by the previous
+        // iteration's finalize (lt_finalize_kernel), for the first frame by reset_decode_state
         // self-attention over the cache, split over keys (3457-3476); the f32 family runs
         // it in the QKV launch on a hand-off of q|k|v (EPI_QKV_SA), the others separately
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->kv16, dev->sa_part};
-        // (not in layer 0: behind its frame-embedding prologue the fused launch measured
-        // 30 us, 11.5 us back to back, against 6.3 + 4.0 us as two launches; not at 16
-        // slots: bf16 B=16 20.1k vs 21.5k frames/s. Both forms compute the same bits.)
-        const bool sa_in_qkv = !W.qkv8 && tb.qkv_sa && l > 0 && NB < 16;
+        // (not at 16 slots: bf16 B=16 20.1k vs 21.5k frames/s; both forms compute the
+        // same bits)
+        const bool sa_in_qkv = !W.qkv8 && tb.qkv_sa && NB < 16;
         {
-            mp::GemvFn fn = W.qkv8 ? (embed_in ? tq.qkv_embed : tq.qkv) : (embed_in ? tb.qkv_embed : tb.qkv);
+            mp::GemvFn fn = W.qkv8 ? tq.qkv : tb.qkv;
             if (sa_in_qkv) {
                 fn = tb.qkv_sa;
                 g.sa = a; g.qh = dev->qh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
             }
-            if ((rc = run(sa_in_qkv ? "qkv_sa" : embed_in ? "qkv_embed" : "qkv", fn, g,
+            if ((rc = run(sa_in_qkv ? "qkv_sa" : "qkv", fn, g,
                           (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
             if (sa_in_qkv && record) dev->ops.back().add_sa = true;
         }
@@ -1217,6 +1204,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                io.max_steps, io.ignore_eos, m.audio_bos, m.audio_eos, NB,
                mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax}, io.emit_eos, io.lt_only,
                io.lt_only ? nullptr : io.ndone + 1};
+    if (!io.lt_only) { f.emb = m.audio_emb; f.pos_emb = m.dec_pos; f.x = io.x; }  // the next frame's input
     if (ops) {
         mp::OpRec r{};
         r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = A * act * 2024;
@@ -1547,6 +1535,8 @@ int reset_decode_state(mp_dev *dev) {
     // hand-off tags restart with the iteration counter (ndone[1]): no stale tag may match
     HIPCHK(hipMemsetAsync(dev->xh, 0, (size_t)NB * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
+    // the first frame's decoder input (the BOS codes); later frames' by lt_finalize_kernel
+    HIPCHK(mp::op_embed(mp::EmbP{dev->m.audio_emb, dev->codes_prev, dev->m.dec_pos, dev->pos, dev->x}, NB, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go
     HIPCHK(hipStreamSynchronize(dev->stream));
     return MP_OK;

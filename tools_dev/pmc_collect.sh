@@ -13,7 +13,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp MAGPIE_EAGER=1
 run() {  # name counters workload...
   local name=$1 ctr=$2; shift 2
-  timeout -s KILL 150 rocprofv3 --pmc $ctr -f csv -d "$OUT/${TAG}_pmc_${name}" -o pmc -- python3 -u "$@" \
+  timeout -s KILL 240 rocprofv3 --pmc $ctr -f csv -d "$OUT/${TAG}_pmc_${name}" -o pmc -- python3 -u "$@" \
     > "$OUT/${TAG}_pmc_${name}.log" 2>&1
   echo "pass $name ok"
 }

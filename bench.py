@@ -33,13 +33,21 @@ sys.path.insert(0, os.path.join(REPO, "magpie-tts.cpp_amd"))
 
 import numpy as np  # noqa: E402
 
-import magpie_amd as ma  # noqa: E402  (loads libmagpie_hip.so before torch can load another HIP runtime)
+import magpie_amd as ma  # noqa: E402
+
+# libmagpie_hip.so (hipcc 7.2, NEEDs libamdhip64.so.7) is loaded before anything can
+# import torch, whose wheel bundles its own libamdhip64.so.7 (ROCm 7.0): the first
+# object of that soname in the process is the one every later NEEDED entry binds to,
+# so every N runs the kernels on /opt/rocm's runtime (tests/test_dist_cpu.py checks
+# /proc/self/maps after this import sequence).
+ma.load_library()
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
 CODEC_FLOP_PER_FRAME = 2.447e9  # 1.2234 G MAC per codec frame
 CODEC_CHUNK = 32  # the CLI decodes stateless 32-frame chunks (magpie-tts.cpp:181-206)
 FRAMES = 256
+SCALE_BATCH = 8  # configs[3]: batch 64 split 8 per GPU
 TEXT_TOKENS = 64
 PMC_TRAFFIC = "r02bf_pmc_decode_f32_b1.json"  # per-op HBM bytes of the N=1 workload (tools_dev/pmc_report.py)
 PMC_CODEC = "r02bf_pmc_codec.json"  # codec MFMA busy cycles + bytes per kernel (tools_dev/pmc_report.py)
@@ -208,7 +216,11 @@ def main() -> None:
             seen = [rank]
         # one write(2) per line: the ranks share the launcher's stdout pipe
         os.write(1, (json.dumps({"rank": rank, "local_rank": local, "world": world, "ranks_seen": seen,
-                                 "weights": args.weights, "batch_per_gpu": args.batch}) + "\n").encode())
+                                 "weights": args.weights, "batch_per_gpu": args.batch,
+                                 "scaling_baseline": {"weights": "bf16", "batch_per_gpu": SCALE_BATCH,
+                                                      "measured": "rank 0 alone" if world > 1 else "after the headline"},
+                                 "efficiency": "value / (n_gpus x scaling_baseline.value)" if world > 1 else None})
+                     + "\n").encode())
         return
     # one rank per GPU; with fewer GPUs than ranks (a rehearsal) ranks share devices
     ndev = ma.device_count()
@@ -243,15 +255,28 @@ def main() -> None:
         if dist is not None:
             dist.barrier()
 
+    def timed_decodes():
+        t0 = time.perf_counter()
+        ms, fr = [], 0
+        for _ in range(args.steps):
+            res = dev.decode(B, args.frames)  # synchronises its stream before returning
+            ms.append(res.decode_ms)
+            fr += int(res.n_frames.sum())
+        return time.perf_counter() - t0, ms, fr, res
+
+    # N > 1: the like-for-like 1-GPU point of the weak-scaling curve, measured in this
+    # run on this node: rank 0 decodes its share alone (the other ranks wait at the
+    # barrier, their GPUs idle), then every rank decodes together
+    solo = None
+    if dist is not None:
+        barrier()
+        if rank == 0:
+            s_el, _, s_fr, _ = timed_decodes()
+            solo = s_fr / s_el
+        barrier()
+
     barrier()
-    t0 = time.perf_counter()
-    decode_ms = []
-    frames = 0
-    for _ in range(args.steps):
-        rr = dev.decode(B, args.frames)  # synchronises its stream before returning
-        decode_ms.append(rr.decode_ms)
-        frames += int(rr.n_frames.sum())
-    elapsed = time.perf_counter() - t0
+    elapsed, decode_ms, frames, rr = timed_decodes()
     barrier()
     assert frames == args.steps * B * args.frames, f"expected fixed-length output, got {frames} frames"
 
@@ -269,6 +294,33 @@ def main() -> None:
     total_frames = sum(r["frames"] for r in per_rank)
     value = total_frames / t_max
     ms_per_step = 1e3 * t_max / args.steps
+
+    # ---- weak-scaling baseline: configs[3]'s per-GPU share (bf16, 8 utterances per GPU)
+    # on ONE GPU. At N > 1 that is the workload itself, timed on rank 0 alone above;
+    # at N = 1 (configs[1], f32 batch 1) it is timed here, after the headline decode, so a
+    # SCALE series divides like by like: efficiency(N) = value(N) / (N x this value).
+    scaling = None
+    sb_desc = f"Magpie-357M bf16, batch={SCALE_BATCH}/GPU, {args.frames} frames/utterance, T={args.tokens} (configs[3] per-GPU share), one GPU"
+    if dist is not None:
+        scaling = {"workload": sb_desc if (args.weights, B) == ("bf16", SCALE_BATCH) else
+                   f"this line's workload on one GPU", "value": round(solo, 2) if solo else None,
+                   "unit": "frames/s", "measured": "rank 0 alone in this run (other ranks idle at a barrier)"}
+    elif rank == 0:
+        if (args.weights, B) == ("bf16", SCALE_BATCH):
+            sval = value
+        else:
+            sdev = ma.Device(model_path, device=device, weights="bf16")
+            stoks = [ma.synthetic_tokens(args.tokens, seed=1000 + b) for b in range(SCALE_BATCH)]
+            sdev.synthesize(stoks, speakers=[b % 5 for b in range(SCALE_BATCH)], max_dec_steps=args.frames,
+                            ignore_eos=True)
+            t0 = time.perf_counter()
+            sfr = 0
+            for _ in range(args.steps):
+                sfr += int(sdev.decode(SCALE_BATCH, args.frames).n_frames.sum())
+            sval = sfr / (time.perf_counter() - t0)
+            sdev.close()
+        scaling = {"workload": sb_desc, "value": round(sval, 2), "unit": "frames/s",
+                   "measured": "this run, after the headline decode, same steps"}
 
     # ---- nano-codec on the device: every utterance's 256 frames as 32-frame chunks
     codec = None
@@ -338,7 +390,12 @@ def main() -> None:
             if n != "finalize":
                 rec["bytes"] = dev.op_bytes(idxs[0])
                 # back to back (one event pair around 50 launches; weights warm in L2/MALL)
-                rec["b2b_us"] = round(dev.time_op(idxs[0], reps=50), 3)
+                # (not for ops carrying an in-launch hand-off: relaunched with the same
+                # iteration tag their consumers would not wait; the library refuses)
+                try:
+                    rec["b2b_us"] = round(dev.time_op(idxs[0], reps=50), 3)
+                except ma.MagpieError:
+                    rec["b2b_us"] = None
             op_table[n] = rec
         dom = max(((n, r) for n, r in op_table.items() if "bytes" in r), key=lambda kv: kv[1]["us_per_frame"])
         name, rec = dom
@@ -418,6 +475,9 @@ def main() -> None:
                                          ((ms_per_step + preamble_ms + (codec["ms"] if codec else 0)) * 1e-3), 1)),
             "decode_roofline": {"bytes_per_frame": round(bpf), "achieved_GBs": round(bpf * fps_per_gpu / 1e9, 1),
                                 "frac": round(bpf * fps_per_gpu / 1e9 / HBM_PEAK_GBS, 4)},
+            "scaling_baseline": scaling,
+            "efficiency": (round(value / (world * scaling["value"]), 4)
+                           if world > 1 and scaling and scaling["value"] else None),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "ops": op_table,

@@ -75,8 +75,14 @@ struct magpie_tokenizer {
     int32_t eos_id = -1;
     bool loaded = false;
 };
-// magpie_tokenizer_init (magpie.h:107) takes a ggml gguf_context there; here the
-// GGUF path (strings magpie.tokenizer.vocab / .dict, ids magpie.tokenizer.*).
+// magpie.h:107: magpie_tokenizer_init from an open GGUF's metadata (strings
+// magpie.tokenizer.vocab / .dict, ids magpie.tokenizer.*). gguf_context is this
+// library's own opaque, ggml-free GGUF handle: magpie_gguf_open / magpie_gguf_close.
+struct gguf_context;
+struct gguf_context *magpie_gguf_open(const char *gguf_path);  // nullptr + stderr on failure
+void magpie_gguf_close(struct gguf_context *gguf_ctx);
+bool magpie_tokenizer_init(magpie_tokenizer *tok, struct gguf_context *gguf_ctx);
+// the same from a GGUF path (open, init, close)
 bool magpie_tokenizer_load(magpie_tokenizer *tok, const char *gguf_path);
 // magpie.h:110: normalise, lower-case, dictionary/IPA or letter fallback, BOS..EOS
 std::vector<int32_t> magpie_tokenize(const magpie_tokenizer *tok, const std::string &text);
@@ -88,16 +94,43 @@ struct magpie_model {
     mp_dev *dev = nullptr;  // resident weights + device state (replaces ggml ctx/buffers)
 };
 
-// magpie.h:293-307 — public inference settings kept as plain fields.
+// magpie.h:265-287 — the per-call generation state, host side. The KV caches and
+// the graph allocator live on the device (mp_dev) and are not exposed; the
+// fields a caller can read are filled by the single-utterance synthesis calls:
+// the last call's frames (frame-major, as returned) and its encoder output
+// ([enc_seq_len][d_model], magpie_encode_text's copy, magpie.cpp:2364-2367).
+struct magpie_state {
+    std::vector<int32_t> generated_codes;
+    int32_t n_generated_frames = 0;
+    std::vector<float> encoder_output;
+    int32_t enc_seq_len = 0;
+    void reset() {
+        generated_codes.clear();
+        n_generated_frames = 0;
+        encoder_output.clear();
+        enc_seq_len = 0;
+    }
+};
+
+// magpie.h:293-307 — same members, names and defaults; public inference settings
+// kept as plain fields.
 struct magpie_context {
     magpie_model model;
+    magpie_state state;
     int n_threads;  // accepted, unused (the reference never applies it either, magpie.h:298)
     float temperature;
     int top_k;
     int speaker_id;
     struct magpie_codec *codec;
-    uint64_t seed;  // added: the reference's sampler is an unseeded static mt19937 (magpie.cpp:1129)
-    magpie_context() : n_threads(4), temperature(0.7f), top_k(80), speaker_id(0), codec(nullptr), seed(0) {}
+    // added: the reference's sampler is an unseeded static mt19937 (magpie.cpp:1129);
+    // here every draw is u(seed, stream, step, codebook)
+    uint64_t seed;
+    // added: magpie_synthesize_streaming runs up to this many sentences as one device
+    // batch (audio still delivered in sentence order, identical samples); 1 = one by one
+    int max_parallel_sentences;
+    magpie_context()
+        : n_threads(4), temperature(0.7f), top_k(80), speaker_id(0), codec(nullptr), seed(0),
+          max_parallel_sentences(8) {}
 };
 
 // magpie.h:310-313
@@ -161,7 +194,7 @@ std::vector<float> magpie_codec_decode(magpie_codec *codec, const int32_t *codes
 magpie_sample_result magpie_local_transformer_sample_all(magpie_context *ctx, const float *decoder_hidden,
                                                         float temperature, int top_k, bool forbid_eos = false);
 
-// ---- streaming (magpie.h:596-648, same types and defaults)
+// ---- streaming (magpie.h:596-648, same types, fields and defaults)
 typedef bool (*magpie_audio_callback)(const float *samples, int n_samples, void *user_data);
 typedef void (*magpie_progress_callback)(int frames_generated, int sentence_index, int total_sentences,
                                          void *user_data);
@@ -174,9 +207,6 @@ struct magpie_stream_params {
     magpie_audio_callback on_audio = nullptr;
     magpie_progress_callback on_progress = nullptr;
     void *user_data = nullptr;
-    // added: sentences synthesised concurrently as one device batch (audio still
-    // delivered in sentence order; identical samples). 1 = the reference's order.
-    int max_parallel_sentences = 8;
 };
 std::vector<std::string> magpie_split_sentences(const char *text);
 // total samples, or -1 on error

@@ -63,6 +63,11 @@ typedef struct mp_timing {
 
 /* --- device + weights ---------------------------------------------------- */
 int mp_hip_device_count(int *n);
+/* the file of the HIP runtime this library's calls are bound to (dladdr of
+ * hipGetDeviceCount as resolved from here): a process that also loads torch's
+ * bundled copy must still run the kernels on /opt/rocm's (bench.py loads this
+ * library first; tests/test_dist_cpu.py) */
+const char *mp_hip_runtime_path(void);
 /* replaces init_backend / ggml_backend_cuda_init (magpie.cpp:14-67) */
 int mp_hip_init(int device, mp_dev **out);
 /* replaces gguf_init_from_file + read_hparams + create_tensors + load_tensor_data
@@ -84,7 +89,8 @@ int mp_hip_load_model(mp_dev *dev, const char *gguf_path);
  * every activation row is quantised to Q8_0 (quantize_row_q8_0_ref) and each
  * 32-block contributes its exact integer dot times d_w*d_a — in the encoder, the
  * XA K/V precompute, the prefill, every decode step and the LT. F32 tensors (the
- * pos_ff convs) keep the f32 path. Batches up to 8. MP_ERR_UNSUPPORTED for a file
+ * pos_ff convs) keep the f32 path. Batches up to 16 when every decode projection is
+ * quantised (the reference converter's files), else 8 (mp_hip_max_batch). MP_ERR_UNSUPPORTED for a file
  * without Q8_0 tensors (BASELINE config 5). A Q4_0 file (convert_magpie_to_gguf.py:
  * 107-138) runs in this mode too: its blocks are repacked losslessly to int8 q - 8
  * with the same fp16 scale, so the same kernels compute ggml's vec_dot_q4_0_q8_0. */
@@ -134,8 +140,8 @@ void mp_hip_free(mp_dev *dev);
 const char *mp_hip_error(mp_dev *dev);
 
 /* --- synthesis ------------------------------------------------------------ */
-/* Per-utterance preamble for B independent utterances (B <= 8; <= 16 in the
- * BF16 weight mode): text encoder
+/* Per-utterance preamble for B independent utterances (1 <= B <= mp_hip_max_batch:
+ * 16 in the bf16 / F16 modes and for a fully quantised Q8_0 / Q4_0 file, else 8): text encoder
  * (magpie_encode_text, magpie.cpp:2284-2374), cross-attention K/V
  * (magpie.cpp:4098-4136), baked speaker context + 110-frame prefill
  * (magpie.cpp:4138-4238). tokens: [B][tmax] row-major (padding ignored),

@@ -117,7 +117,20 @@ std::vector<int32_t> magpie_synthesize_codes_graph_reuse(magpie_context *ctx, co
     std::vector<int32_t> out;
     const int32_t *tp[1] = {tokens};
     const int nt[1] = {n_tokens};
+    ctx->state.reset();
     if (!magpie_synthesize_codes_batch(ctx, tp, nt, 1, &out)) return {};
+    // ctx->state as the reference leaves it: the encoder output of this utterance
+    // (magpie.cpp:2364-2367) and the generated frames
+    const long long eb = mp_hip_debug_buffer(ctx->model.dev, "enc_out", nullptr, 0);
+    if (eb >= (long long)n_tokens * 768 * 4) {
+        std::vector<float> enc((size_t)eb / 4);
+        if (mp_hip_debug_buffer(ctx->model.dev, "enc_out", enc.data(), eb) == eb) {
+            ctx->state.encoder_output.assign(enc.begin(), enc.begin() + (size_t)n_tokens * 768);
+            ctx->state.enc_seq_len = n_tokens;
+        }
+    }
+    ctx->state.generated_codes = out;
+    ctx->state.n_generated_frames = (int32_t)(out.size() / 8);
     mp_timing t{};
     mp_hip_get_timing(ctx->model.dev, &t);
     const int n_frames = (int)out.size() / 8;
@@ -302,7 +315,7 @@ int magpie_synthesize_sentence_streaming(magpie_context *ctx, magpie_codec *code
 }
 
 // magpie_synthesize_streaming (magpie.cpp:4843-4863). Sentences of the text run
-// as device batches of up to max_parallel_sentences; the audio reaches on_audio
+// as device batches of up to ctx->max_parallel_sentences; the audio reaches on_audio
 // in sentence order, sample for sample what the sentence-by-sentence loop gives.
 int magpie_synthesize_streaming(magpie_context *ctx, magpie_codec *codec, const char *text,
                                 const magpie_stream_params &params) {
@@ -324,7 +337,7 @@ int magpie_synthesize_streaming(magpie_context *ctx, magpie_codec *codec, const 
     ctx->top_k = params.top_k;
     ctx->speaker_id = params.speaker_id;
     const int bmax = std::max(1, mp_hip_max_batch(ctx->model.dev));
-    const int P = std::max(1, std::min(params.max_parallel_sentences, bmax));
+    const int P = std::max(1, std::min(ctx->max_parallel_sentences, bmax));
     long long total = 0;
     for (size_t s0 = 0; s0 < sents.size(); s0 += P) {
         const size_t s1 = std::min(sents.size(), s0 + P);

@@ -153,13 +153,35 @@ hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
 // (magpie.cpp:4340-4358): stop on EOS in any codebook (frame not emitted), else
 // append the frame; stop at max_dec_steps; otherwise the frame becomes the next
 // decoder input and the position advances.
+// slot b's decoder input from the frame codes cc at position ps, one wave:
+// embed_kernel's arithmetic (codebooks summed in order, / 8, + position)
+template <typename C>
+__device__ __forceinline__ void embed_row(const FinP &p, int b, const C &cc, int ps) {
+    int c[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) c[cb] = cc[cb];
+    for (int k = threadIdx.x; k < D; k += 64) {
+        float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
+#pragma unroll
+        for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
+        p.x[(size_t)b * D + k] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
+    }
+}
+
 __global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     // one wave per slot: codebook 7's pick with the same wave_pick as every other
     // codebook (masked first-max argmax; top-k draw when sampling)
     const int b = blockIdx.x, tid = threadIdx.x;
     if (p.iter && b == 0 && tid == 0) p.iter[0] += 1;  // the next iteration's hand-off tags
-    if (p.done[b]) return;
+    if (p.done[b]) {
+        // a finished slot keeps running with the batch: give it its frozen input again
+        // (codes_prev / pos no longer advance), so every later iteration recomputes the
+        // values of the one that ended it (the hidden-state trace row at the frozen
+        // step included) instead of running on the last output residual
+        if (p.x && !p.lt_only) embed_row(p, b, p.codes_prev + b * NCB, p.pos[b]);
+        return;
+    }
     __shared__ float scratch[2 * VCB];
     int i0, amax;
     {
@@ -212,13 +234,7 @@ __global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
         np = __shfl(np, 0, 64);
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) cc[cb] = __shfl(cc[cb], 0, 64);
-        // embed_kernel's arithmetic: codebooks summed in order, / 8, + position
-        for (int k = tid; k < D; k += 64) {
-            float s = p.emb[((size_t)0 * VCB + cc[0]) * D + k];
-#pragma unroll
-            for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + cc[cb]) * D + k];
-            p.x[(size_t)b * D + k] = s * 0.125f + p.pos_emb[(size_t)np * D + k];
-        }
+        embed_row(p, b, cc, np);
     }
     ts_end(p.ts, t_start);
 }

@@ -235,6 +235,9 @@ struct GemvP {
     int nrow_blocks;     // set by the launcher: workgroups of the O-projection
 };
 
+// error bits raised in *hx_err (ndone[2]) by an in-launch hand-off that gave up
+constexpr int HX_ERR_XA = 1, HX_ERR_SA = 2;
+
 struct FinP {
     const float *logits;
     int *codes_cur, *codes_prev, *codes_out;

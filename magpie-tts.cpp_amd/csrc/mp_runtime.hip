@@ -9,6 +9,7 @@
 // (12 decoder layers + 8-codebook local transformer + EOS bookkeeping, 133
 // kernels at NB=1) is captured once as a hipGraph and replayed per frame with
 // no host round trip; the host only polls the done counter every few frames.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -326,6 +327,8 @@ void free_batch(mp_dev *dev) {
     dev->ops.clear();
     dev->batch_ready = false;
     dev->B = dev->NB = dev->Tmax = dev->max_steps = 0;
+    dev->xa_direct = false;
+    dev->kp = dev->vp = nullptr;
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -775,6 +778,10 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     const size_t D = 768;
     int rc = MP_OK;
 #define A(ptr, n) if ((rc = dalloc(dev, &dev->ptr, (size_t)(n))) != MP_OK) return rc
+    // this batch's KV width and XA form first: the allocations below depend on them
+    // (a batch must never inherit the previous batch's form)
+    dev->kv16 = dev->kv_mode == MP_KV_BF16;
+    dev->xa_direct = want_xa_direct(dev, Tmax);
     A(x, NB * D); A(x2, NB * D); A(q, NB * D);
     if (!dev->xa_direct) { A(kp, (size_t)NB * L * Tmax * D); A(vp, (size_t)NB * L * Tmax * D); }
     else dev->kp = dev->vp = nullptr;
@@ -782,8 +789,6 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
     A(xh, (size_t)NB * D); A(qh, (size_t)NB * 3 * D);
-    dev->kv16 = dev->kv_mode == MP_KV_BF16;
-    dev->xa_direct = want_xa_direct(dev, Tmax);
     const size_t kvn = (size_t)NB * L * dev->max_seq * D;  // elements; bf16 mode: 2 per float slot
     A(kc, dev->kv16 ? kvn / 2 : kvn); A(vc, dev->kv16 ? kvn / 2 : kvn);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -1341,6 +1346,12 @@ int mp_hip_device_count(int *n) {
     return MP_OK;
 }
 
+const char *mp_hip_runtime_path(void) {
+    Dl_info info;
+    if (dladdr((void *)&hipGetDeviceCount, &info) && info.dli_fname) return info.dli_fname;
+    return "";
+}
+
 int mp_hip_init(int device, mp_dev **out) {
     if (!out) return MP_ERR_ARG;
     *out = nullptr;
@@ -1575,7 +1586,12 @@ int launch_iteration(mp_dev *dev) {
 static int check_handoff(mp_dev *dev) {
     int nd[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpy(nd, dev->ndone, sizeof nd, hipMemcpyDeviceToHost));
-    if (nd[2]) return fail(dev, MP_ERR_HIP, "in-launch hand-off (O-projection -> cross-attention) timed out");
+    if (nd[2]) {
+        std::string what;
+        if (nd[2] & mp::HX_ERR_XA) what += " O-projection -> cross-attention";
+        if (nd[2] & mp::HX_ERR_SA) what += std::string(what.empty() ? "" : ",") + " QKV -> self-attention";
+        return fail(dev, MP_ERR_HIP, "in-launch hand-off timed out:" + what);
+    }
     return MP_OK;
 }
 
@@ -2020,6 +2036,11 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     // XA rewrites this layer's split states only; XA-Q8 rewrites x2 with the same values
     auto launch = [&]() -> hipError_t { return launch_rec(r, dev->stream); };
     if (r.kind == mp::K_FIN) return fail(dev, MP_ERR_ARG, "op cannot be timed standalone");
+    // an op carrying an in-launch hand-off (QKV -> SA, O-projection -> XA) tags it with the
+    // iteration counter: relaunched with the same tag, its consumers would find the previous
+    // launch's granules and not wait for their producers (a different, shorter critical path)
+    if (r.kind == mp::K_GEMV && r.g.iter)
+        return fail(dev, MP_ERR_ARG, "op carries an in-launch hand-off: back-to-back timing would not wait for it");
     HIPCHK(launch());  // warm
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));

@@ -70,7 +70,7 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
             }
             if (__all(ok)) break;
             if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
-                if (lane == 0) __hip_atomic_store((gi32 *)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_SA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 qv = kv = vv = __builtin_nanf("");
                 break;
             }

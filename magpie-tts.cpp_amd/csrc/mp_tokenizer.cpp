@@ -5,6 +5,7 @@
 // words, BOS/EOS. Host C++ (string work, no device involvement); vocabulary and
 // dictionary come from the GGUF strings magpie.tokenizer.vocab / .dict.
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -131,12 +132,31 @@ std::vector<std::string> split_on(const std::string &s, char sep) {
 
 }  // namespace
 
-// magpie_tokenizer_init (magpie.cpp:353-398) from a GGUF path
-bool magpie_tokenizer_load(magpie_tokenizer *tok, const char *gguf_path) {
-    if (!tok || !gguf_path) return false;
+// the opaque GGUF handle of magpie.h (ggml-free: mp::Gguf, a read-only mapping)
+struct gguf_context {
     mp::Gguf g;
-    std::string err, vocab, dict;
-    if (!g.open(gguf_path, err) || !g.get_str("magpie.tokenizer.vocab", vocab)) return false;
+};
+
+struct gguf_context *magpie_gguf_open(const char *gguf_path) {
+    if (!gguf_path) return nullptr;
+    gguf_context *c = new gguf_context();
+    std::string err;
+    if (!c->g.open(gguf_path, err)) {
+        fprintf(stderr, "magpie_gguf_open: %s\n", err.c_str());
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void magpie_gguf_close(struct gguf_context *gguf_ctx) { delete gguf_ctx; }
+
+// magpie_tokenizer_init (magpie.cpp:353-398): false when the GGUF carries no tokenizer
+bool magpie_tokenizer_init(magpie_tokenizer *tok, struct gguf_context *gguf_ctx) {
+    if (!tok || !gguf_ctx) return false;
+    mp::Gguf &g = gguf_ctx->g;
+    std::string vocab, dict;
+    if (!g.get_str("magpie.tokenizer.vocab", vocab)) return false;
     tok->vocab = split_on(vocab, '\n');
     tok->token_to_id.clear();
     for (size_t i = 0; i < tok->vocab.size(); ++i) tok->token_to_id[tok->vocab[i]] = (int32_t)i;
@@ -153,6 +173,15 @@ bool magpie_tokenizer_load(magpie_tokenizer *tok, const char *gguf_path) {
     tok->eos_id = (int32_t)g.get_u32("magpie.text_eos_id", 2379);
     tok->loaded = true;
     return true;
+}
+
+bool magpie_tokenizer_load(magpie_tokenizer *tok, const char *gguf_path) {
+    if (!tok || !gguf_path) return false;
+    gguf_context *c = magpie_gguf_open(gguf_path);
+    if (!c) return false;
+    const bool ok = magpie_tokenizer_init(tok, c);
+    magpie_gguf_close(c);
+    return ok;
 }
 
 // magpie_tokenize (magpie.cpp:400-492)

@@ -75,7 +75,7 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
                 }
                 if (__all(ok)) break;
                 if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
-                    if (lane == 0) __hip_atomic_store((gi32 *)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
                     for (int j = 0; j < D / 64; ++j) xv[j] = __builtin_nanf("");
                     break;

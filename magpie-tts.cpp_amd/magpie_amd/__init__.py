@@ -60,6 +60,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 SYMBOLS = [
     ("mp_hip_device_count", _I, [ctypes.POINTER(_I)]),
+    ("mp_hip_runtime_path", ctypes.c_char_p, []),
     ("mp_hip_init", _I, [_I, ctypes.POINTER(_P)]),
     ("mp_hip_load_model", _I, [_P, ctypes.c_char_p]),
     ("mp_hip_load_model_ex", _I, [_P, ctypes.c_char_p, _I]),
@@ -181,7 +182,8 @@ class Device:
         on bf16 MFMA, activations rounded to bf16; batches up to 16) or "q8" / "q4"
         (the file's Q8_0 / Q4_0 tensors kept as int8 (Q4_0: q - 8, losslessly),
         multiplied with ggml's semantics: activations quantised to Q8_0 per
-        32-block, integer dots scaled by d_w * d_a; batches up to 8) or "f16" (an
+        32-block, integer dots scaled by d_w * d_a; batches up to 16 when every
+        decode projection is quantised, else 8, Device.max_batch()) or "f16" (an
         F16 file with ggml's F16 mul_mat semantics: activations rounded to f16,
         decode projections on f16 MFMA; batches up to 16).
         kv: SA cache element type, "f32" (the reference's) or "bf16" (rows rounded

@@ -74,6 +74,52 @@ def test_bench_gpus_2_spawns_two_ranks():
     for x in lines:
         assert x["world"] == 2 and x["ranks_seen"] == [0, 1]
         assert x["weights"] == "bf16" and x["batch_per_gpu"] == 8
+        # the like-for-like 1-GPU point (configs[3]'s per-GPU share, rank 0 alone) and
+        # the efficiency against it ride on every N > 1 line
+        assert x["scaling_baseline"] == {"weights": "bf16", "batch_per_gpu": 8, "measured": "rank 0 alone"}
+        assert x["efficiency"] == "value / (n_gpus x scaling_baseline.value)"
+
+
+def test_bench_n1_dry_run_names_the_scaling_baseline():
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    x = json.loads(out.stdout.strip().splitlines()[-1])
+    assert x["weights"] == "f32" and x["batch_per_gpu"] == 1  # configs[1]
+    assert x["scaling_baseline"]["weights"] == "bf16" and x["scaling_baseline"]["batch_per_gpu"] == 8
+
+
+MAPS_PROBE = r'''
+import importlib.util, json, os, sys
+spec = importlib.util.spec_from_file_location("bench", sys.argv[1])
+bench = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(bench)          # bench.py's imports: loads libmagpie_hip.so
+import torch.distributed                 # what an N > 1 rank imports next (gloo)
+import torch
+bound = bench.ma.load_library().mp_hip_runtime_path().decode()
+print(json.dumps({"bound": bound, "torch": torch.__file__}))
+'''
+
+
+def test_bench_binds_kernels_to_one_hip_runtime():
+    """torch's wheel bundles its own libamdhip64 (soname libamdhip64.so.7, ROCm 7.0).
+    bench.py loads libmagpie_hip.so before torch, so the library's HIP calls stay bound
+    to /opt/rocm's runtime after the ranks import torch.distributed: every N runs the
+    kernels on the same runtime (torch's copy is mapped but never initialised)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", MAPS_PROBE, os.path.join(repo, "bench.py")], capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert os.path.realpath(r["bound"]).startswith(os.path.realpath("/opt/rocm")), r
 
 
 def test_bench_rejects_mismatched_world():

@@ -236,3 +236,88 @@ def test_bench_bytes_per_frame_matches_survey():
     spec.loader.exec_module(bench)
     # ~388.4 MB/frame at B=1, L=238.5, T=64 (f32)
     assert abs(bench.decoder_bytes_per_frame(1, 238.5, 64) / 1e6 - 388.4) < 0.5
+
+
+def _gfx950_code_objects(so_path, tmp_path):
+    """Every gfx950 code object in a HIP shared library: the .hip_fatbin section is a
+    run of clang offload bundles (one per translation unit), each '__CLANG_OFFLOAD_
+    BUNDLE__' + entry count + (offset, size, triple) records, offsets from its start."""
+    sec = tmp_path / "fatbin.bin"
+    subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objcopy", f"--dump-section=.hip_fatbin={sec}", so_path,
+                    str(tmp_path / "discard.so")], check=True)
+    data = sec.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out, pos = [], data.find(magic)
+    while pos >= 0:
+        n, = struct.unpack_from("<Q", data, pos + 24)
+        p = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            triple = data[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" in triple and size:
+                co = tmp_path / f"co{len(out)}.elf"
+                co.write_bytes(data[pos + off:pos + off + size])
+                out.append(co)
+        pos = data.find(magic, pos + 1)
+    return out
+
+
+def test_library_has_no_packed_fp32_instructions(tmp_path):
+    """v_pk_fma/mul/add_f32 returned wrong values on gfx950 while
+    MFMA work ran on the GPU; the library is built with -packed-fp32-ops
+    (magpie-tts.cpp_amd/Makefile, NOPK, appended in the rules). A rebuild that loses
+    the flag must fail here, not corrupt a decode beside the codec."""
+    import magpie_amd as ma
+    cos = _gfx950_code_objects(ma.LIB_PATH, tmp_path)
+    assert len(cos) >= 6, f"expected one gfx950 code object per HIP source, found {len(cos)}"
+    n_mfma = 0
+    for co in cos:
+        dis = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", "--mcpu=gfx950", str(co)],
+                             capture_output=True, text=True, check=True).stdout
+        bad = re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", dis)
+        assert not bad, f"{co.name}: {len(bad)} packed-FP32 instructions ({bad[0]})"
+        n_mfma += len(re.findall(r"\bv_mfma_", dis))
+    assert n_mfma > 1000  # the disassembly is real: the MFMA kernels are in it
+
+
+CALLER = r'''
+// a caller written against the reference header (src/magpie.h:107,265-307,604-648)
+#include "magpie.h"
+static bool on_audio(const float *, int, void *) { return true; }
+static void on_progress(int, int, int, void *) {}
+int use(magpie_context *ctx, magpie_codec *codec) {
+    ctx->temperature = 0.0f; ctx->top_k = 80; ctx->speaker_id = 1; ctx->n_threads = 8; ctx->codec = codec;
+    ctx->model.hparams.max_dec_steps = 500;
+    ctx->state.reset();
+    size_t n = ctx->state.generated_codes.size() + ctx->state.encoder_output.size();
+    n += (size_t)ctx->state.n_generated_frames + (size_t)ctx->state.enc_seq_len;
+    magpie_tokenizer tok;
+    struct gguf_context *g = magpie_gguf_open("x.gguf");
+    bool ok = magpie_tokenizer_init(&tok, g) && tok.loaded;
+    magpie_gguf_close(g);
+    magpie_stream_params p{0.7f, 80, 0, 4, true, on_audio, on_progress, nullptr};  // the reference's 8 fields, in order
+    p.temperature = 0.5f; p.top_k = 40; p.speaker_id = 2; p.frames_per_chunk = 8; p.sentence_chunking = false;
+    p.on_audio = on_audio; p.on_progress = on_progress; p.user_data = nullptr;
+    int s = magpie_synthesize_streaming(ctx, codec, "Hello, world!", p);
+    std::vector<int32_t> ids = magpie_tokenize(&ctx->model.tokenizer, "Hello");
+    std::vector<int32_t> codes = magpie_synthesize_codes_graph_reuse(ctx, ids.data(), (int)ids.size());
+    magpie_sample_result r = magpie_local_transformer_sample_all(ctx, nullptr, 0.7f, 80, false);
+    return (int)n + s + (ok ? 1 : 0) + (int)codes.size() + (int)r.argmax_codes.size();
+}
+'''
+
+
+def test_reference_caller_compiles_and_links(tmp_path):
+    """include/magpie.h keeps the reference's field names (magpie_context incl. state,
+    magpie_stream_params' exact 8 fields, magpie_tokenizer_init): a reference-side
+    caller compiles unchanged and links against libmagpie_hip.so."""
+    import magpie_amd as ma
+    src = tmp_path / "caller.cpp"
+    src.write_text(CALLER + "int main() { return 0; }\n")
+    exe = tmp_path / "caller"
+    r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"),
+                        "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", str(src), "-o", str(exe),
+                        ma.LIB_PATH, f"-Wl,-rpath,{os.path.dirname(ma.LIB_PATH)}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]

@@ -1,0 +1,241 @@
+// Probe: does a two-stream "ladder" of dependent GEMV launches (link j on stream
+// j % 2, NO graph edge between consecutive links; the data edge carried by
+// {tag, value} granules) beat a plain one-stream graph chain?
+//
+// Links alternate FFN-up (768 -> 3072) and FFN-down (3072 -> 768) f32 GEMVs with
+// distinct weights (48 links x 9.4 MB > the 256 MiB Infinity Cache: HBM
+// streaming, as in the batch-1 decode). Each link issues its weight rows first,
+// then takes its input vector (plain loads, or a bounded granule poll), dots,
+// and stores its output (plain, or granules). Every spin is bounded.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include <algorithm>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("ERR %s at %d: %s\n", #x, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
+
+constexpr int D = 768, F = 3072, NLINK = 48;
+using gu64 = __attribute__((address_space(1))) unsigned long long;
+using gi32 = __attribute__((address_space(1))) int;
+
+__device__ __forceinline__ float wave_sum(float v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+struct LinkP {
+    const float *W;
+    int N;
+    const float *in;             // plain input
+    unsigned long long *gin;     // granule input
+    float *out;                  // plain output
+    unsigned long long *gout;    // granule output
+    const unsigned *epoch;
+    int link;
+    int *err;
+};
+
+template <int K, int RW, bool GIN, bool GOUT>
+__global__ __launch_bounds__(256) void link_kernel(LinkP p) {
+    constexpr int NV = K / 256;
+    __shared__ __attribute__((aligned(16))) float act[K];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int row0 = (blockIdx.x * 4 + w) * RW;
+    float4 wv[RW][NV];
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) wv[r][i] = ((const float4 *)(p.W + (size_t)(row0 + r) * K))[lane + 64 * i];
+    const unsigned ep = p.epoch[0];
+    if constexpr (GIN) {
+        const unsigned tag = ep * 64u + (unsigned)p.link;
+        gu64 *g = (gu64 *)p.gin;
+        float xv[K / 256];
+        for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < K / 256; ++j) {
+                const unsigned long long u = __hip_atomic_load(g + tid + 256 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                xv[j] = __uint_as_float((unsigned)u);
+                ok &= (unsigned)(u >> 32) == tag;
+            }
+            if (__all(ok)) break;
+            if (spins >= (1u << 18)) {
+                if (lane == 0) __hip_atomic_store((gi32 *)p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int j = 0; j < K / 256; ++j) act[tid + 256 * j] = xv[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < K / 256; ++j) act[tid + 256 * j] = p.in[tid + 256 * j];
+    }
+    lds_sync();
+    float acc[RW];
+    float4 av[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) av[i] = ((const float4 *)act)[lane + 64 * i];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) s += wv[r][i].x * av[i].x + wv[r][i].y * av[i].y + wv[r][i].z * av[i].z + wv[r][i].w * av[i].w;
+        acc[r] = wave_sum(s);
+    }
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < RW; ++r) if (lane == r) v = acc[r];
+    if (lane >= RW) return;
+    const int n = row0 + lane;
+    v = tanhf(v);
+    if constexpr (GOUT) {
+        const unsigned tag = ep * 64u + (unsigned)p.link + 1u;
+        __hip_atomic_store((gu64 *)(p.gout + n), ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        p.out[n] = v;
+    }
+}
+
+// start of a replay: epoch += 1, x0 published as plain values and as granules of tag epoch*64
+__global__ void epoch_kernel(unsigned *epoch, const float *x0, float *xplain, unsigned long long *gx) {
+    __shared__ unsigned ep;
+    if (threadIdx.x == 0) { ep = epoch[0] + 1; epoch[0] = ep; }
+    __syncthreads();
+    for (int k = threadIdx.x; k < D; k += blockDim.x) {
+        xplain[k] = x0[k];
+        __hip_atomic_store((gu64 *)(gx + k), ((unsigned long long)(ep * 64u) << 32) | __float_as_uint(x0[k]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+static float *g_W[NLINK];
+static float *g_act[NLINK + 1];
+static unsigned long long *g_gact[NLINK + 1];
+static unsigned *g_epoch;
+static int *g_err;
+static float *g_x0;
+
+template <bool GIN, bool GOUT>
+static void launch_link(int j, hipStream_t s) {
+    LinkP p{};
+    p.W = g_W[j];
+    p.in = g_act[j];
+    p.gin = g_gact[j];
+    p.out = g_act[j + 1];
+    p.gout = g_gact[j + 1];
+    p.epoch = g_epoch;
+    p.link = j;
+    p.err = g_err;
+    if (j % 2 == 0) {  // up: K = 768, N = 3072, RW 2 -> 384 workgroups
+        p.N = F;
+        hipLaunchKernelGGL((link_kernel<D, 2, GIN, GOUT>), dim3(F / 8), dim3(256), 0, s, p);
+    } else {  // down: K = 3072, N = 768, RW 1 -> 192 workgroups
+        p.N = D;
+        hipLaunchKernelGGL((link_kernel<F, 1, GIN, GOUT>), dim3(D / 4), dim3(256), 0, s, p);
+    }
+}
+
+// mode 0: one stream, plain; 1: one stream, granules; 2: two-stream ladder, granules; 3: three-stream ladder
+static double run_mode(int mode, std::vector<float> &final_out, int reps) {
+    hipStream_t st[3];
+    for (auto &s : st) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t ef, ej[3];
+    CK(hipEventCreateWithFlags(&ef, hipEventDisableTiming));
+    for (auto &ev : ej) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const int ns = mode == 2 ? 2 : mode == 3 ? 3 : 1;
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(st[0], hipStreamCaptureModeGlobal));
+    hipLaunchKernelGGL(epoch_kernel, dim3(1), dim3(256), 0, st[0], g_epoch, g_x0, g_act[0], g_gact[0]);
+    if (ns > 1) {
+        CK(hipEventRecord(ef, st[0]));
+        for (int i = 1; i < ns; ++i) CK(hipStreamWaitEvent(st[i], ef, 0));
+    }
+    for (int j = 0; j < NLINK; ++j) {
+        hipStream_t s = st[j % ns];
+        const bool last = j == NLINK - 1;
+        if (mode == 0) launch_link<false, false>(j, s);
+        else if (last) launch_link<true, false>(j, s);  // the last link stores plain for the check
+        else launch_link<true, true>(j, s);
+    }
+    if (ns > 1) {
+        for (int i = 1; i < ns; ++i) { CK(hipEventRecord(ej[i], st[i])); CK(hipStreamWaitEvent(st[0], ej[i], 0)); }
+    }
+    CK(hipStreamEndCapture(st[0], &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, st[0]));
+        CK(hipGraphLaunch(ge, st[0]));
+        CK(hipEventRecord(e1, st[0]));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 3) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    final_out.resize(D);
+    CK(hipMemcpy(final_out.data(), g_act[NLINK], D * sizeof(float), hipMemcpyDeviceToHost));
+    int err = 0;
+    CK(hipMemcpy(&err, g_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) printf("  mode %d: HAND-OFF TIMEOUT flagged\n", mode);
+    hipGraphExecDestroy(ge);
+    hipGraphDestroy(g);
+    for (auto &s : st) hipStreamDestroy(s);
+    return t[t.size() / 2] * 1e3;
+}
+
+__global__ void init_kernel(float *w, size_t n, unsigned seed, float a) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u ^ seed;
+        x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+        w[i] = a * (((x & 0xFFFFFF) / 16777216.0f) * 2.f - 1.f);
+    }
+}
+
+int main() {
+    for (int j = 0; j < NLINK; ++j) {
+        CK(hipMalloc(&g_W[j], (size_t)D * F * sizeof(float)));
+        const int K = j % 2 == 0 ? D : F;
+        hipLaunchKernelGGL(init_kernel, dim3(1024), dim3(256), 0, 0, g_W[j], (size_t)D * F, 1234u + j, 2.0f * sqrtf(3.0f / K));
+    }
+    for (int j = 0; j <= NLINK; ++j) {
+        CK(hipMalloc(&g_act[j], F * sizeof(float)));
+        CK(hipMalloc(&g_gact[j], F * sizeof(unsigned long long)));
+        CK(hipMemset(g_gact[j], 0, F * sizeof(unsigned long long)));
+    }
+    CK(hipMalloc(&g_epoch, 256));
+    CK(hipMemset(g_epoch, 0, 256));
+    CK(hipMalloc(&g_err, 256));
+    CK(hipMemset(g_err, 0, 256));
+    CK(hipMalloc(&g_x0, D * sizeof(float)));
+    hipLaunchKernelGGL(init_kernel, dim3(4), dim3(256), 0, 0, g_x0, (size_t)D, 99u, 1.0f);
+    CK(hipDeviceSynchronize());
+    const char *names[4] = {"1 stream, plain loads/stores", "1 stream, granules", "2-stream ladder, granules",
+                            "3-stream ladder, granules"};
+    std::vector<float> ref, o;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int m = 0; m < 4; ++m) {
+            const double us = run_mode(m, o, 30);
+            if (m == 0 && pass == 0) ref = o;
+            const bool same = memcmp(ref.data(), o.data(), D * sizeof(float)) == 0;
+            printf("%-34s %8.2f us per replay, %6.2f us per link, output %s\n", names[m], us, us / NLINK,
+                   same ? "bit-identical" : "DIFFERS");
+        }
+    }
+    printf("done\n");
+    return 0;
+}

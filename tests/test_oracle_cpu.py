@@ -406,3 +406,40 @@ def test_teacher_forced_run_reproduces_free_run(oracle, small_model):
     np.testing.assert_array_equal(g["hidden"][0], r["hidden"][0])   # BOS step precedes any code
     assert np.abs(g["hidden"][2] - r["hidden"][2]).max() > 1e-3     # the frame embedding follows the forced codes
     m.close()
+
+
+def test_ggml_cpu_gelu_table_vs_plain_f32_on_full_model(oracle, full_model):
+    """configs[0] is the reference binary on the ggml CPU backend, whose GELU is an fp16
+    lookup table (ggml_gelu at magpie.cpp:1799,1869; assumed, ggml absent).
+    The GPU f32 path computes GELU in f32 and is bit-identical in codes to the oracle's
+    plain mode over 500 frames (tests/test_long_range_gpu.py). This quantifies how far
+    the ggml-CPU arithmetic sits from that: the oracle in fp16-table mode, teacher forced
+    along the plain run's codes on Magpie-357M (configs[0]'s model shape), every
+    decision and hidden state compared. Bar: >= 95 % of the
+    decisions agree, every differing one at an oracle margin < 0.1, hidden-state
+    relative L2 < 5e-3."""
+    import magpie_amd as ma
+    tok = ma.synthetic_tokens(64, seed=1000)
+    steps = 32
+    m = oracle.Model(full_model)
+    try:
+        oracle.set_mode(acc64=True, gelu_f16=False, threads=min(8, os.cpu_count() or 1))
+        plain = m.synthesize(tok, speaker=0, max_steps=steps, ignore_eos=True, trace=True)
+        oracle.set_mode(acc64=True, gelu_f16=True, threads=min(8, os.cpu_count() or 1))
+        tab = m.synthesize_forced(tok, plain["codes"], speaker=0, ignore_eos=True)
+    finally:
+        oracle.set_mode(acc64=True, gelu_f16=False, threads=min(16, os.cpu_count() or 1))
+        m.close()
+    pc, tc = np.asarray(plain["codes"]), np.asarray(tab["codes"])
+    agree = float((pc == tc).mean())
+    diff = np.argwhere(pc != tc)
+    margins = [float(np.asarray(tab["margins"])[i, j]) for i, j in diff]
+    h, ht = plain["hidden"][:steps], tab["hidden"][:steps]
+    abs_err = float(np.abs(h - ht).max())
+    rel = float((np.linalg.norm(h - ht, axis=-1) / np.linalg.norm(h, axis=-1)).max())
+    print(f"gelu fp16 table vs f32: {agree * 100:.2f} % of {pc.size} decisions agree "
+          f"(differing at margins {[round(x, 4) for x in margins[:8]]}); hidden max abs {abs_err:.3g}, "
+          f"max rel L2 {rel:.3g}")
+    assert agree >= 0.95
+    assert all(x < 0.1 for x in margins), margins
+    assert rel < 5e-3, rel

@@ -31,9 +31,13 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "mp_device.hpp"
 #include "mp_fused.hpp"
 #include "mp_params.hpp"
+#include "mp_sa.hpp"
+#include "mp_xa.hpp"
 
 namespace mp {
 
@@ -46,7 +50,9 @@ __device__ __forceinline__ float quad_max(float v) {
     return fmaxf(v, dpp_mov<0x4E>(v));
 }
 
-template <int NB, int K, int PRO, int EPI>
+__device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char *actq, float *actd, unsigned long long t_start);
+
+template <int NB, int K, int PRO, int EPI, bool Q4>
 __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     static_assert(NB >= 1 && NB <= 16, "one 16-column MFMA tile of utterances");
@@ -57,15 +63,33 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     __shared__ __attribute__((aligned(16))) float act[NB * K];
     __shared__ __attribute__((aligned(16))) signed char actq[(NB + 1) * QS];
     __shared__ float actd[(NB + 1) * NBLK];
+    __shared__ int actsum[Q4 ? (NB + 1) * NBLK : 1];  // Q4: each activation block's integer sum
     __shared__ __attribute__((aligned(16))) floatx4 part[MP_NWAVES][64];
     __shared__ float red[8];
     __shared__ float sc[SC];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = blockIdx.x;
+    if constexpr (EPI == EPI_QKV_SA) {
+        // the launch's last NH x SA_SPLITS x NB workgroups: self-attention on this launch's q|k|v
+        if (rt >= p.nrow_blocks) {
+            sa_tail(p, t_start);
+            return;
+        }
+    }
+    if constexpr (EPI == EPI_RESID_XQ8) {
+        // the launch's last XQG x NB workgroups: the XA's q_net on this launch's x1
+        if (rt >= p.nrow_blocks) {
+            xq8_tail(p, act, actq, actd, t_start);
+            return;
+        }
+    }
 
     // this wave's weight fragments and their scales, issued before the prologue
-    const uint4 *wf = (const uint4 *)p.Wq + ((size_t)rt * KP + w * KW) * 64 + lane + ts_dep(t_start);
+    // (Q4: 8 nibbles per block and lane, half the bytes: the Q4_0 file's 18 per 32)
+    using AT = typename std::conditional<Q4, uint2, uint4>::type;
+    const AT *wf = (const AT *)p.Wq + ((size_t)rt * KP + w * KW) * 64 + lane + ts_dep(t_start);
     const uint4 *sf = (const uint4 *)p.Wd + ((size_t)rt * KP + w * KW) * 4 + (lane >> 4);
-    uint4 a[KW], sd[KW];
+    AT a[KW];
+    uint4 sd[KW];
 #pragma unroll
     for (int i = 0; i < KW; ++i) { a[i] = wf[(size_t)i * 64]; sd[i] = sf[(size_t)i * 4]; }
 
@@ -77,6 +101,8 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
         if (e < QS / 4) ((int *)(actq + NB * QS))[e] = 0;
         else actd[NB * NBLK + (e - QS / 4)] = 0.f;
     }
+    if constexpr (Q4)
+        for (int e = tid; e < NBLK; e += MP_BLOCK) actsum[NB * NBLK + e] = 0;
     for (int blk = (tid >> 2); blk < NB * NBLK; blk += MP_BLOCK / 4) {
         const int b = blk / NBLK, kb = blk % NBLK, e8 = 8 * (lane & 3);
         const float4 x0 = *(const float4 *)(act + b * K + kb * 32 + e8);
@@ -88,10 +114,20 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
         const float id = dd != 0.f ? 1.0f / dd : 0.0f;
         const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         unsigned qw[2] = {0u, 0u};
+        int qs = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qw[j >> 2] |= ((unsigned)(int)roundf(xs[j] * id) & 0xFFu) << (8 * (j & 3));
+        for (int j = 0; j < 8; ++j) {
+            const int qj = (int)roundf(xs[j] * id);
+            qs += qj;
+            qw[j >> 2] |= ((unsigned)qj & 0xFFu) << (8 * (j & 3));
+        }
         *(uint2 *)(actq + b * QS + kb * 32 + e8) = make_uint2(qw[0], qw[1]);
         if ((lane & 3) == 0) actd[blk] = __half2float(__float2half(dd));
+        if constexpr (Q4) {  // the block's sum over its 4 lanes (a DPP quad)
+            qs += __builtin_amdgcn_update_dpp(0, qs, 0xB1, 0xF, 0xF, false);
+            qs += __builtin_amdgcn_update_dpp(0, qs, 0x4E, 0xF, 0xF, false);
+            if ((lane & 3) == 0) actsum[blk] = qs;
+        }
     }
     lds_sync();
     ts_mark(p.ts, t_start);  // profiling: activation tile quantised
@@ -99,6 +135,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     const int c = min(lane & 15, NB);
     const signed char *bq = actq + c * QS + 8 * (lane >> 4);
     const float *bd = actd + c * NBLK;
+    const int *bs = actsum + (Q4 ? c * NBLK : 0);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < KW; ++i) {
@@ -106,18 +143,28 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int kc = 2 * kp + h;
-            const long av = h ? (long)(((unsigned long)a[i].w << 32) | a[i].z)
-                              : (long)(((unsigned long)a[i].y << 32) | a[i].x);
+            long av;
+            if constexpr (Q4) {
+                // nibbles u = q + 8 (byte i of the word: u_i | u_{i+4} << 4) as int8 0..15
+                const unsigned wn = h ? a[i].y : a[i].x;
+                av = (long)(((unsigned long)((wn >> 4) & 0x0F0F0F0Fu) << 32) | (wn & 0x0F0F0F0Fu));
+            } else {
+                av = h ? (long)(((unsigned long)a[i].w << 32) | a[i].z) : (long)(((unsigned long)a[i].y << 32) | a[i].x);
+            }
             const long bv = *(const long *)(bq + kc * 32);
             const intx4 zero = {0, 0, 0, 0};
-            const intx4 s = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv, zero, 0, 0, 0);
+            intx4 s = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv, zero, 0, 0, 0);
+            if constexpr (Q4) {  // sum (u - 8) a = sum u a - 8 sum a: the exact integer dot of ggml's q - 8
+                const int corr = 8 * bs[kc];
+                s[0] -= corr; s[1] -= corr; s[2] -= corr; s[3] -= corr;
+            }
             const float da = bd[kc];
             const unsigned dlo = h ? sd[i].z : sd[i].x, dhi = h ? sd[i].w : sd[i].y;  // rows 4g..4g+3
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const unsigned wd = r < 2 ? dlo : dhi;
                 const float dw = __half2float(__ushort_as_half((unsigned short)((r & 1) ? wd >> 16 : wd & 0xFFFFu)));
-                acc[r] += (float)s[r] * (dw * da);
+                acc[r] = fmaf((float)s[r], dw * da, acc[r]);  // ggml's per-block update (the fused XA repeats it)
             }
         }
     }
@@ -130,7 +177,9 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     const float v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
     const int n = rt * 16 + row;
     if (n >= p.N) return;
-    epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
+    if constexpr (EPI == EPI_QKV_SA) publish_qkv(p, v, n, col);
+    else if constexpr (EPI == EPI_RESID_XQ8) publish_x1(p, v, n, col);
+    else epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
     ts_end(p.ts, t_start);
 }
 
@@ -145,10 +194,11 @@ __global__ void pack_q8_kernel(const signed char *q, const unsigned short *d, in
         const size_t frag = e / 64;
         const int kp = (int)(frag % KP), rt = (int)(frag / KP);
         const int n = rt * 16 + (lane & 15);
-        for (int j = 0; j < 16; ++j) {
-            const int k = kp * 64 + (j >> 3) * 32 + 8 * g + (j & 7);
-            oq[e * 16 + j] = n < N ? (unsigned char)q[(size_t)n * K + k] : 0;
-        }
+        if (oq)  // (null: the scales only, a Q4_0 tensor's nibbles come from pack_q4)
+            for (int j = 0; j < 16; ++j) {
+                const int k = kp * 64 + (j >> 3) * 32 + 8 * g + (j & 7);
+                oq[e * 16 + j] = n < N ? (unsigned char)q[(size_t)n * K + k] : 0;
+            }
         if ((lane & 15) == 0)
             for (int j = 0; j < 8; ++j) {
                 const int r = rt * 16 + 4 * g + (j & 3), blk = 2 * kp + (j >> 2);
@@ -158,8 +208,37 @@ __global__ void pack_q8_kernel(const signed char *q, const unsigned short *d, in
 }
 hipError_t pack_q8(const signed char *q, const unsigned short *d, int N, int K, unsigned char *oq,
                    unsigned short *od, hipStream_t s) {
-    if (!q || !d || !oq || !od || N <= 0 || K % 256) return hipErrorInvalidValue;
+    if (!q || !d || !od || N <= 0 || K % 256) return hipErrorInvalidValue;
     mp::launch(pack_q8_kernel, dim3(1024), dim3(256), 0, s, q, d, N, K, oq, od);
+    return hipGetLastError();
+}
+
+// Q4_0 decode fragments from the int8 q - 8 values: [ceil(N/16)][K/64][64 lanes][2 x u32],
+// word h of lane l = the 8 values of block 2j+h at k-offset 8(l>>4) as nibbles u = q + 8,
+// byte i holding u_i | u_{i+4} << 4 (two masks give the MFMA operand's 8 int8 bytes);
+// the scales as pack_q8 lays them out (pass od = null to keep those of a pack_q8 call)
+__global__ void pack_q4_kernel(const signed char *q, int N, int K, unsigned *oq) {
+    const int KP = K / 64;
+    const size_t total = (size_t)((N + 15) / 16) * KP * 64;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(e % 64), g = lane >> 4;
+        const size_t frag = e / 64;
+        const int kp = (int)(frag % KP), rt = (int)(frag / KP);
+        const int n = rt * 16 + (lane & 15);
+        for (int h = 0; h < 2; ++h) {
+            unsigned wd = 0u;
+            for (int i = 0; i < 8; ++i) {
+                const int k = kp * 64 + h * 32 + 8 * g + i;
+                const unsigned u = (unsigned)((n < N ? (int)q[(size_t)n * K + k] : 0) + 8) & 15u;
+                wd |= u << (i < 4 ? 8 * i : 8 * (i - 4) + 4);
+            }
+            oq[e * 2 + h] = wd;
+        }
+    }
+}
+hipError_t pack_q4(const signed char *q, int N, int K, unsigned char *oq, hipStream_t s) {
+    if (!q || !oq || N <= 0 || K % 256) return hipErrorInvalidValue;
+    mp::launch(pack_q4_kernel, dim3(1024), dim3(256), 0, s, q, N, K, (unsigned *)oq);
     return hipGetLastError();
 }
 
@@ -177,30 +256,64 @@ hipError_t pack_q8(const signed char *q, const unsigned short *d, int N, int K, 
 constexpr int XQ8_ROWS = 64;  // o_net rows per workgroup
 
 // a = softmax_t(q . K_t / sqrt(128)) V  of slot b into a_s[128] (every thread
-// returns after a barrier); pr: per-key scores [TMAX_LIMIT]
+// returns after a barrier); pr: per-key scores [TMAX_LIMIT]. STAGED: the key and
+// value rows pass through LDS in chunks of XS_ROWS (Ks, Vs [XS_ROWS][128]; chunk 0
+// already there when `pre`), read in the same order with the same arithmetic, so both
+// forms compute the same bits: a key's score is one half-wave dot, the maximum is
+// order-free, and wave w accumulates its keys w, w + 4, ... in ascending order either
+// way (chunks are whole multiples of 16 keys).
+constexpr int XS_ROWS = 64;
+// rows [c0, c0 + n) of a [T][128] f32 matrix into LDS stage[XS_ROWS][128]
+__device__ __forceinline__ void xa_stage_rows(const float *src, int c0, int n, float *stage) {
+    constexpr int PER = XS_ROWS * DXA / 4 / MP_BLOCK;  // float4 per thread
+    float4 r[PER];  // every load issued (rows past n re-read row n - 1), then stored
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int e = threadIdx.x + MP_BLOCK * j, row = min(e / (DXA / 4), n - 1);
+        r[j] = *(const float4 *)(src + (size_t)(c0 + row) * DXA + 4 * (e % (DXA / 4)));
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int e = threadIdx.x + MP_BLOCK * j, row = e / (DXA / 4);
+        if (row < n) *(float4 *)(stage + 4 * e) = r[j];
+    }
+}
+template <bool STAGED>
 __device__ __forceinline__ void xa_text_attention(const float *q, const float *Kb, const float *Vb, int Tb,
-                                                  float *pr, float *a_s) {
+                                                  float *pr, float *a_s, float *Ks = nullptr, float *Vs = nullptr,
+                                                  bool pre = false) {
+#pragma clang fp contract(off)
     __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
     __shared__ float wred[2 * MP_NWAVES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int h = lane >> 5, d4 = 4 * (lane & 31);
     const float4 q4 = *(const float4 *)(q + d4);
     const float scale = 1.0f / sqrtf((float)DXA);
+    const int CH = STAGED ? XS_ROWS : Tb;  // keys per chunk
     float mx = -INFINITY;
-    for (int t0 = 2 * w; t0 < Tb; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
-        float4 k4[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = min(t0 + 2 * MP_NWAVES * u + h, Tb - 1);
-            k4[u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
+    for (int c0 = 0; c0 < Tb; c0 += CH) {
+        const int c1 = min(Tb, c0 + CH);
+        if (STAGED && !(pre && c0 == 0)) {
+            lds_sync();
+            xa_stage_rows(Kb, c0, c1 - c0, Ks);
+            lds_sync();
         }
+        for (int t0 = c0 + 2 * w; t0 < c1; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
+            float4 k4[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = t0 + 2 * MP_NWAVES * u + h;
-            const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
-            if (t < Tb) {
-                if ((lane & 31) == 0) pr[t] = sv;
-                mx = fmaxf(mx, sv);
+            for (int u = 0; u < 4; ++u) {
+                const int t = min(t0 + 2 * MP_NWAVES * u + h, c1 - 1);
+                k4[u] = STAGED ? *(const float4 *)(Ks + (size_t)(t - c0) * DXA + d4)
+                               : *(const float4 *)(Kb + (size_t)t * DXA + d4);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 2 * MP_NWAVES * u + h;
+                const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
+                if (t < c1) {
+                    if ((lane & 31) == 0) pr[t] = sv;
+                    mx = fmaxf(mx, sv);
+                }
             }
         }
     }
@@ -210,17 +323,25 @@ __device__ __forceinline__ void xa_text_attention(const float *q, const float *K
     const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
     // o[d] = sum_t e_t V_t[d]: wave w takes keys t = w + 4 u, lane owns dims lane, 64 + lane
     float l = 0.f, o0 = 0.f, o1 = 0.f;
-    for (int t0 = w; t0 < Tb; t0 += MP_NWAVES * 4) {
-        float v0[4], v1[4], e[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = min(t0 + MP_NWAVES * u, Tb - 1);
-            v0[u] = Vb[(size_t)t * DXA + lane];
-            v1[u] = Vb[(size_t)t * DXA + 64 + lane];
-            e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
+    for (int c0 = 0; c0 < Tb; c0 += CH) {
+        const int c1 = min(Tb, c0 + CH);
+        if (STAGED && !(pre && c0 == 0)) {
+            lds_sync();
+            xa_stage_rows(Vb, c0, c1 - c0, Vs);
+            lds_sync();
         }
+        for (int t0 = c0 + w; t0 < c1; t0 += MP_NWAVES * 4) {
+            float v0[4], v1[4], e[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) { l += e[u]; o0 += e[u] * v0[u]; o1 += e[u] * v1[u]; }
+            for (int u = 0; u < 4; ++u) {
+                const int t = min(t0 + MP_NWAVES * u, Tb - 1);
+                v0[u] = STAGED ? Vs[(size_t)(t - c0) * DXA + lane] : Vb[(size_t)t * DXA + lane];
+                v1[u] = STAGED ? Vs[(size_t)(t - c0) * DXA + 64 + lane] : Vb[(size_t)t * DXA + 64 + lane];
+                e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { l += e[u]; o0 = fmaf(e[u], v0[u], o0); o1 = fmaf(e[u], v1[u], o1); }
+        }
     }
     pv[w][lane] = o0;
     pv[w][64 + lane] = o1;
@@ -233,26 +354,10 @@ __device__ __forceinline__ void xa_text_attention(const float *q, const float *K
     lds_sync();
 }
 
-__global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
-    constexpr int OR = 8, OCPR = DXA / 16;                 // o_net: groups of 8 rows
-    constexpr int OG = XQ8_ROWS / MP_NWAVES / OR;          // 2 groups per wave
-    __shared__ float pr[TMAX_LIMIT];
-    __shared__ __attribute__((aligned(16))) float a_s[DXA];
-    __shared__ __attribute__((aligned(16))) signed char aq[DXA];
-    __shared__ float ad[DXA / 32];
-    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r0 = blockIdx.x * XQ8_ROWS;
-    uint4 wo[OG];
-    float wos[OG];
-#pragma unroll
-    for (int g = 0; g < OG; ++g) {
-        const int row = r0 + (w * OG + g) * OR + lane / OCPR, kc = lane % OCPR;
-        wo[g] = *(const uint4 *)(p.wo + (size_t)row * DXA + kc * 16);
-        wos[g] = __half2float(__ushort_as_half(p.wod[(size_t)row * (DXA / 32) + kc / 2]));
-    }
-    const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-    xa_text_attention(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
-    if (w == 0) {
+// a (LDS, [128]) -> Q8_0 blocks aq / ad (ggml quantises the o_net operand), wave 0
+__device__ __forceinline__ void xa_quantize_a(const float *a_s, signed char *aq, float *ad) {
+    const int lane = threadIdx.x & 63;
+    if ((threadIdx.x >> 6) == 0) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {  // element lane + 64 i; its Q8_0 block = this half-wave
             const float av = a_s[lane + 64 * i];
@@ -265,10 +370,19 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
         }
     }
     lds_sync();
-    // ---- x2 = x + Q8(o_net) a for this workgroup's 64 rows (8 per group)
+}
+
+// o_net rows of one wave: G groups of 8 rows (8 lanes x 16 B per row), the Q8_0 block
+// dots on v_dot4 times d_w * d_a, summed over the row's 4 blocks; x2 = v + x1
+constexpr int XQ8_OR = 8, XQ8_OCPR = DXA / 16;
+template <int G>
+__device__ __forceinline__ void xa_q8_onet(const uint4 (&wo)[G], const float (&wos)[G], int row0, const signed char *aq,
+                                           const float *ad, const float *x1, float *x2) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int g = 0; g < OG; ++g) {
-        const int r = lane / OCPR, kc = lane % OCPR;
+    for (int g = 0; g < G; ++g) {
+        const int r = lane / XQ8_OCPR, kc = lane % XQ8_OCPR;
         const int4 a4 = *(const int4 *)(aq + kc * 16);
         int s = __builtin_amdgcn_sdot4((int)wo[g].x, a4.x, 0, false);
         s = __builtin_amdgcn_sdot4((int)wo[g].y, a4.y, s, false);
@@ -278,15 +392,158 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
         const float f = (lane & 1) ? 0.f : (float)s * (wos[g] * ad[kc >> 1]);
         float v = 0.f;
 #pragma unroll
-        for (int rr = 0; rr < OR; ++rr) {
+        for (int rr = 0; rr < XQ8_OR; ++rr) {
             const float t = wave_sum((r == rr) ? f : 0.f);
             if (lane == rr) v = t;
         }
-        if (lane < OR) {
-            const int row = r0 + (w * OG + g) * OR + lane;
-            p.x2[(size_t)b * D + row] = v + p.x[(size_t)b * D + row];
+        if (lane < XQ8_OR) {
+            const int row = row0 + g * XQ8_OR + lane;
+            x2[row] = v + x1[row];
         }
     }
+}
+
+__global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
+    constexpr int OG = XQ8_ROWS / MP_NWAVES / XQ8_OR;  // 2 groups of 8 rows per wave
+    __shared__ float pr[TMAX_LIMIT];
+    __shared__ __attribute__((aligned(16))) float a_s[DXA];
+    __shared__ __attribute__((aligned(16))) signed char aq[DXA];
+    __shared__ float ad[DXA / 32];
+    const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = blockIdx.x * XQ8_ROWS + w * OG * XQ8_OR;
+    uint4 wo[OG];
+    float wos[OG];
+#pragma unroll
+    for (int g = 0; g < OG; ++g) {
+        const int row = r0 + g * XQ8_OR + lane / XQ8_OCPR, kc = lane % XQ8_OCPR;
+        wo[g] = *(const uint4 *)(p.wo + (size_t)row * DXA + kc * 16);
+        wos[g] = __half2float(__ushort_as_half(p.wod[(size_t)row * (DXA / 32) + kc / 2]));
+    }
+    // the slot's first XS_ROWS text keys and values into LDS, every load in flight at
+    // once (they do not depend on q), then the same attention on the staged rows
+    __shared__ __attribute__((aligned(16))) float Ks[XS_ROWS * DXA];
+    __shared__ __attribute__((aligned(16))) float Vs[XS_ROWS * DXA];
+    const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+    const int Tb = p.T[b];
+    xa_stage_rows(p.xak + kv, 0, min(Tb, XS_ROWS), Ks);
+    xa_stage_rows(p.xav + kv, 0, min(Tb, XS_ROWS), Vs);
+    lds_sync();
+    xa_text_attention<true>(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, Tb, pr, a_s, Ks, Vs, true);
+    xa_quantize_a(a_s, aq, ad);
+    // ---- x2 = x + Q8(o_net) a for this workgroup's 64 rows (8 per group)
+    xa_q8_onet<OG>(wo, wos, r0, aq, ad, p.x + (size_t)b * D, p.x2 + (size_t)b * D);
+}
+
+// ---------------------------------------------------------------- XA q_net, fused (EPI_RESID_XQ8)
+// The cross-attention's Q8_0 q_net riding in the Q8_0 O-projection's launch: the
+// launch's last XQG x NB workgroups, XQ_ROWS rows of q each. A workgroup issues its
+// q_net rows (wave 0, lane = (row, quarter): 6 blocks of int8 + their scales, the
+// MFMA kernel's K split) before x1 exists, sweeps the x1 granules (publish_x1), and
+// computes exactly what the separate q GEMV does: LN(x1) * lnw (PRO_LN's wave
+// statistics), the Q8_0 activation blocks (gemm_q8_kernel_dec's quantiser), each
+// quarter's block dots accumulated in block order and the quarters summed in order,
+// stored to q. xa_q8_kernel (the next launch) does the attention and o_net. Same bits
+// as the q GEMV (tests/test_q8_fused_gpu.py).
+constexpr int XQG = 8, XQ_ROWS = DXA / XQG, XQ_QB = D / 32 / 4;  // 8 workgroups x 16 rows; 6 blocks per quarter
+__device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char *actq, float *actd,
+                                         unsigned long long t_start) {
+#pragma clang fp contract(off)
+    const XaQ8P &x = p.xq8;
+    const int k = blockIdx.x - p.nrow_blocks, b = k / XQG, r0 = (k % XQG) * XQ_ROWS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int qr = r0 + (lane >> 2), qa = lane & 3;  // wave 0: (row, quarter) per lane
+    uint4 wq[2 * XQ_QB];
+    unsigned short wqs[XQ_QB];
+    if (w == 0) {
+        const uint4 *src = (const uint4 *)(x.wq + (size_t)qr * D + qa * XQ_QB * 32 + ts_dep(t_start));
+#pragma unroll
+        for (int i = 0; i < 2 * XQ_QB; ++i) wq[i] = src[i];
+#pragma unroll
+        for (int j = 0; j < XQ_QB; ++j) wqs[j] = x.wqd[(size_t)qr * (D / 32) + qa * XQ_QB + j];
+    }
+    constexpr int PER = D / 64;
+    float g[PER];
+    load_lnw<PER>(x.lnw, g);
+    // x1 from the O-projection workgroups of this launch (every wave sweeps the row)
+    float v[PER];
+    {
+        const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+        gu64 *gr = (gu64 *)(p.xh + (size_t)b * D);
+        for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const unsigned long long u = __hip_atomic_load(gr + lane + 64 * j, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                v[j] = __uint_as_float((unsigned)u);
+                ok &= (unsigned)(u >> 32) == tag;
+            }
+            if (__all(ok)) break;
+            if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+                if (lane == 0)
+                    __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int j = 0; j < PER; ++j) v[j] = __builtin_nanf("");
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    ts_mark(p.ts, t_start);  // profiling: x1 seen
+    {   // LN(x1) * lnw (PRO_LN at batch 1: every wave the whole row, wave w stores its quarter)
+        constexpr int Q = PER / MP_NWAVES;
+        float mean, var;
+        wave_meanvar<PER>(v, mean, var);
+        const float rstd = 1.0f / sqrtf(var + x.eps);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (i / Q != w) continue;
+            act[lane + 64 * i] = ((v[i] - mean) * rstd) * g[i];
+        }
+    }
+    lds_sync();
+    // Q8_0 blocks of the row (gemm_q8_kernel_dec's quantiser)
+    constexpr int NBLK = D / 32;
+    if (tid < 4 * NBLK) {
+        const int kb = tid >> 2, e8 = 8 * (lane & 3);
+        const float4 x0 = *(const float4 *)(act + kb * 32 + e8);
+        const float4 xx = *(const float4 *)(act + kb * 32 + e8 + 4);
+        float am = fmaxf(fmaxf(fmaxf(fabsf(x0.x), fabsf(x0.y)), fmaxf(fabsf(x0.z), fabsf(x0.w))),
+                         fmaxf(fmaxf(fabsf(xx.x), fabsf(xx.y)), fmaxf(fabsf(xx.z), fabsf(xx.w))));
+        am = quad_max(am);
+        const float dd = am / 127.0f;
+        const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, xx.x, xx.y, xx.z, xx.w};
+        unsigned qw[2] = {0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qw[j >> 2] |= ((unsigned)(int)roundf(xs[j] * id) & 0xFFu) << (8 * (j & 3));
+        *(uint2 *)(actq + kb * 32 + e8) = make_uint2(qw[0], qw[1]);
+        if ((lane & 3) == 0) actd[kb] = __half2float(__float2half(dd));
+    }
+    lds_sync();
+    if (w != 0) return;
+    // this lane's quarter: its blocks in order (fmaf, as gemm_q8_kernel_dec), then the
+    // row's 4 quarters summed in order by its quarter-0 lane
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < XQ_QB; ++j) {
+        const int blk = qa * XQ_QB + j;
+        const int4 x0 = *(const int4 *)(actq + blk * 32), xx = *(const int4 *)(actq + blk * 32 + 16);
+        const uint4 w0 = wq[2 * j], w1 = wq[2 * j + 1];
+        int sd = __builtin_amdgcn_sdot4((int)w0.x, x0.x, 0, false);
+        sd = __builtin_amdgcn_sdot4((int)w0.y, x0.y, sd, false);
+        sd = __builtin_amdgcn_sdot4((int)w0.z, x0.z, sd, false);
+        sd = __builtin_amdgcn_sdot4((int)w0.w, x0.w, sd, false);
+        sd = __builtin_amdgcn_sdot4((int)w1.x, xx.x, sd, false);
+        sd = __builtin_amdgcn_sdot4((int)w1.y, xx.y, sd, false);
+        sd = __builtin_amdgcn_sdot4((int)w1.z, xx.z, sd, false);
+        sd = __builtin_amdgcn_sdot4((int)w1.w, xx.w, sd, false);
+        const float dw = __half2float(__ushort_as_half(wqs[j]));
+        acc = fmaf((float)sd, dw * actd[blk], acc);
+    }
+    const float p1 = __shfl_down(acc, 1, 64), p2 = __shfl_down(acc, 2, 64), p3 = __shfl_down(acc, 3, 64);
+    if (qa == 0) const_cast<float *>(x.q)[(size_t)b * DXA + qr] = ((acc + p1) + p2) + p3;  // q: this tail's output
+    ts_end(p.ts, t_start);
 }
 
 // f32 o_net: lane l holds elements 4l..4l+3 of half a row, a wave covers 2 rows
@@ -301,7 +558,7 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_f32_kernel(XaQ8P p) {
 #pragma unroll
     for (int i = 0; i < RP; ++i) wo[i] = *(const float4 *)(p.wof + (size_t)(r0 + 2 * i + hr) * DXA + d4);
     const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-    xa_text_attention(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
+    xa_text_attention<false>(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
     const float4 a4 = *(const float4 *)&a_s[d4];
     float v = 0.f;
 #pragma unroll
@@ -341,15 +598,24 @@ static bool q8_args_ok(const GemvP &p) {
     if constexpr (EPI == EPI_RESID) ok &= p.resid != nullptr;
     if constexpr (EPI == EPI_ADD_STORE) ok &= p.out && p.addsrc;
     if constexpr (EPI == EPI_LTX_ADD) ok &= p.out && p.ptab && p.lt_pos && p.cb >= 1;
-    if constexpr (EPI == EPI_QKV) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_QKV || EPI == EPI_QKV_SA) ok &= p.out && p.kc && p.vc && p.pos;
+    if constexpr (EPI == EPI_QKV_SA) ok &= qkv_sa_args_ok(p);
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
+    if constexpr (EPI == EPI_RESID_XQ8) {
+        const XaQ8P &x = p.xq8;
+        ok &= p.resid && p.xh && p.iter && p.hx_err && p.N == D && x.q && x.wq && x.wqd && x.lnw;
+    }
     return ok;
 }
 
 template <int NB, int K, int PRO, int EPI>
 static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     if (!q8_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
-    mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI>), dim3((p.N + 15) / 16), dim3(MP_BLOCK), 0, s, p);
+    GemvP q = p;
+    q.nrow_blocks = (p.N + 15) / 16;
+    const int grid = q.nrow_blocks + (EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : EPI == EPI_RESID_XQ8 ? XQG * NB : 0);
+    if (p.q4) mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI, true>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
+    else mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI, false>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();
 }
 
@@ -364,7 +630,11 @@ static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     hipError_t q8_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
     hipError_t q8_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_LTARG_ATTN, EPI_LTX_ADD>(p, s); } \
     hipError_t q8_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
-    hipError_t q8_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }
+    hipError_t q8_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); } \
+    hipError_t q8_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_q8<NB, D, PRO_LN, EPI_QKV_SA>(p, s); }   \
+    hipError_t q8_oproj_xq_##NB(const GemvP &p, hipStream_t s) {                                                    \
+        return launch_q8<NB, D, PRO_SA_MERGE, EPI_RESID_XQ8>(p, s);                                                  \
+    }
 
 MP_Q8_OPS(1)
 MP_Q8_OPS(2)

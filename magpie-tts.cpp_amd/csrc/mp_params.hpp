@@ -62,6 +62,9 @@ enum Epi {
                         // launch's last XA_SPLITS x NB workgroups run the fused XA on it (below)
     EPI_QKV_SA = 12,    // EPI_QKV, each q|k|v value also published as a tagged granule qh[b][2304];
                         // the launch's last NH x SA_SPLITS x NB workgroups run the SA on it
+    EPI_RESID_XQ8 = 13, // Q8_0 O-projection: EPI_RESID_XA's stores and granules; the launch's last
+                        // XQG x NB workgroups compute the cross-attention's q = Q8(q_net) LN(x1) on
+                        // them (xa_q8_kernel, the next launch, does the attention and o_net)
 };
 
 // Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
@@ -157,6 +160,27 @@ struct XaP {
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
 };
 
+// Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the
+// q GEMV: x2 = x + Q8(o_net) attn(q, K, V), the attention output quantised where
+// ggml quantises it (magpie.cpp:1713-1767, 3513-3519).
+struct XaQ8P {
+    const float *x;                 // [B][768]
+    float *x2;                      // [B][768]
+    const float *q;                 // [B][128] = Q8(q_net) LN(x)
+    const signed char *wo;          // o_net int8 [768][128]
+    const unsigned short *wod;      //   fp16 block scales [768][4]
+    const float *wof;               // or f32 o_net [768][128] (direct f32 XA, long texts)
+    const float *xak, *xav;         // XA K, V [B][L][Tmax][128]
+    const int *T;
+    int Tmax, layer, nlayers;
+    // EPI_RESID_XQ8 (q_net in the Q8_0 O-projection's launch): q = Q8(q_net) Q8(LN(x1) * lnw)
+    // from the handed-off x1, stored to q
+    const signed char *wq;          // q_net int8 [128][768] as stored
+    const unsigned short *wqd;      //   fp16 block scales [128][24]
+    const float *lnw;               // norm_xattn_query
+    float eps;
+};
+
 struct AttnP {  // decode self-attention (one query per utterance)
     const float *q;
     const float *kc, *vc;    // bf16 elements when kv16
@@ -173,6 +197,7 @@ struct GemvP {
     const unsigned short *Wb;  // bf16 weights in MFMA fragment order (mp_decode_b16.hip), or null
     const signed char *Wq;     // Q8_0 weights as stored: int8 [N][K] (mp_decode_q8.hip), or null
     const unsigned short *Wd;  //   and their fp16 block scales [N][K/32]
+    int q4;                    // Wq holds Q4_0 nibble fragments (pack_q4), not int8 ones
     int N;
     const float *bias;
     // prologue inputs
@@ -229,6 +254,7 @@ struct GemvP {
     // their head's granules and run the split's attention (the new key from the
     // granules, not from the cache row this launch writes)
     AttnP sa;
+    XaQ8P xq8;           // EPI_RESID_XQ8: the q_net of the launch's tail
     unsigned long long *qh;
     const int *iter;
     int *hx_err;
@@ -254,20 +280,6 @@ struct FinP {
     float *x;
 };
 
-// Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the
-// q GEMV: x2 = x + Q8(o_net) attn(q, K, V), the attention output quantised where
-// ggml quantises it (magpie.cpp:1713-1767, 3513-3519).
-struct XaQ8P {
-    const float *x;                 // [B][768]
-    float *x2;                      // [B][768]
-    const float *q;                 // [B][128] = Q8(q_net) LN(x)
-    const signed char *wo;          // o_net int8 [768][128]
-    const unsigned short *wod;      //   fp16 block scales [768][4]
-    const float *wof;               // or f32 o_net [768][128] (direct f32 XA, long texts)
-    const float *xak, *xav;         // XA K, V [B][L][Tmax][128]
-    const int *T;
-    int Tmax, layer, nlayers;
-};
 
 
 }  // namespace mp

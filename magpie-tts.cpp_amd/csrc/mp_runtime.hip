@@ -81,7 +81,8 @@ hipError_t pack_b16(const float *, int, int, unsigned short *, hipStream_t, bool
     hipError_t q8_oproj_##NB(const GemvP &, hipStream_t); hipError_t q8_xq_##NB(const GemvP &, hipStream_t);             \
     hipError_t q8_lt_in0_##NB(const GemvP &, hipStream_t);                                                             \
     hipError_t q8_lt_a_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_bg_##NB(const GemvP &, hipStream_t);           \
-    hipError_t q8_lt_b_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_e_##NB(const GemvP &, hipStream_t);
+    hipError_t q8_lt_b_##NB(const GemvP &, hipStream_t); hipError_t q8_lt_e_##NB(const GemvP &, hipStream_t);           \
+    hipError_t q8_qkv_sa_##NB(const GemvP &, hipStream_t); hipError_t q8_oproj_xq_##NB(const GemvP &, hipStream_t);
 MP_DECL_Q8(1)
 MP_DECL_Q8(2)
 MP_DECL_Q8(4)
@@ -93,6 +94,7 @@ hipError_t op_ff2_16(const GemvP &, hipStream_t);
 hipError_t op_xq_16(const GemvP &, hipStream_t);
 hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
 hipError_t pack_q8(const signed char *, const unsigned short *, int, int, unsigned char *, unsigned short *, hipStream_t);
+hipError_t pack_q4(const signed char *, int, int, unsigned char *, hipStream_t);
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
 hipError_t q8_lt_em_1(const GemvP &, hipStream_t);
 hipError_t op_lt_pick(const GemvP &, int, hipStream_t);
@@ -143,9 +145,9 @@ static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE
 static const OpTable kTablesF16[5] = {MP_TABLE_F16(1), MP_TABLE_F16(2), MP_TABLE_F16(4), MP_TABLE_F16(8),
                                       MP_TABLE_F16(16)};
 // Q8_0 weight mode: the projections whose tensors are Q8_0 in the file (mp_decode_q8.hip)
-struct OpTableQ8 { GemvFn qkv, oproj, xq, lt_in0, lt_a, lt_bg, lt_b, lt_e; };
+struct OpTableQ8 { GemvFn qkv, oproj, xq, lt_in0, lt_a, lt_bg, lt_b, lt_e, qkv_sa, oproj_xq; };
 #define MP_TABLE_Q8(NB) { q8_qkv_##NB, q8_oproj_##NB, q8_xq_##NB, q8_lt_in0_##NB, \
-                          q8_lt_a_##NB, q8_lt_bg_##NB, q8_lt_b_##NB, q8_lt_e_##NB }
+                          q8_lt_a_##NB, q8_lt_bg_##NB, q8_lt_b_##NB, q8_lt_e_##NB, q8_qkv_sa_##NB, q8_oproj_xq_##NB }
 static const OpTableQ8 kTablesQ8[5] = {MP_TABLE_Q8(1), MP_TABLE_Q8(2), MP_TABLE_Q8(4), MP_TABLE_Q8(8),
                                         MP_TABLE_Q8(16)};
 static int nb_index(int NB) { return NB == 1 ? 0 : NB == 2 ? 1 : NB == 4 ? 2 : NB == 8 ? 3 : 4; }
@@ -166,10 +168,13 @@ struct QW {
     const unsigned short *d = nullptr;
     const signed char *pq = nullptr;
     const unsigned short *pd = nullptr;
+    int nib = 0;        // a Q4_0 tensor: pq holds nibble fragments (pack_q4, 18 B per 32 weights)
+    size_t head_q = 0;  // bytes between consecutive heads' fragments (the 8 LT output heads)
     explicit operator bool() const { return q != nullptr; }
 };
-// bytes of a packed Q8_0 tensor: fragments and scales
+// bytes of a packed Q8_0 tensor: fragments and scales (Q4_0: half the fragment bytes)
 static size_t q8p_qbytes(int N, int K) { return (size_t)((N + 15) / 16) * (K / 64) * 1024; }
+static size_t q4p_qbytes(int N, int K) { return (size_t)((N + 15) / 16) * (K / 64) * 512; }
 static size_t q8p_dbytes(int N, int K) { return (size_t)((N + 15) / 16) * (K / 64) * 64; }
 
 struct EncLayerW { const float *norm_self, *qkv, *o, *norm_ff, *ff1, *ff2; QW qkv8, o8; };
@@ -627,6 +632,10 @@ int load_q8(mp_dev *dev, const char *path) {
     if (!g.open(path, err)) return fail(dev, MP_ERR_IO, err);
     mp::Model &m = dev->m;
     struct Item { const mp::GgufTensor *t; mp::QW *dst; int group; };
+    // a Q4_0 tensor's decode fragments stream its nibbles (MAGPIE_Q4_AS_Q8=1: as int8 q - 8,
+    // the same integers at 34 B per 32 weights; both compute the same bits)
+    const char *q4e = getenv("MAGPIE_Q4_AS_Q8");
+    const bool q4_nib = !(q4e && atoi(q4e) != 0);
     std::vector<Item> items;
     auto want = [&](const std::string &name, mp::QW *dst) {
         const mp::GgufTensor *t = g.find(name);
@@ -699,6 +708,7 @@ int load_q8(mp_dev *dev, const char *path) {
             dq = (signed char *)cur; cur += align_up(n);
             dd = (unsigned short *)cur; cur += align_up(n / 32 * 2);
             it.dst->q = dq; it.dst->d = dd;
+            it.dst->nib = q4_nib && it.t->type == 2;
         } else {  // the 8 LT heads as one [8][2024][256] array (indexed by a device codebook)
             if (n != out_n) return fail(dev, MP_ERR_FORMAT, "unexpected LT output projection shape");
             if (!out_q) {
@@ -708,6 +718,9 @@ int load_q8(mp_dev *dev, const char *path) {
             dq = out_q + (size_t)it.group * n;
             dd = out_d + (size_t)it.group * (n / 32);
             it.dst->q = out_q; it.dst->d = out_d;
+            if (it.group == 0) it.dst->nib = q4_nib && it.t->type == 2;
+            else if (it.dst->nib != (int)(q4_nib && it.t->type == 2))
+                return fail(dev, MP_ERR_UNSUPPORTED, "mixed Q4_0 / Q8_0 LT output projections");
         }
         HIPCHK(hipMemcpy(dq, hq.data(), n, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(dd, hd.data(), n / 32 * 2, hipMemcpyHostToDevice));
@@ -731,28 +744,36 @@ int load_q8(mp_dev *dev, const char *path) {
     add(m.lt_o8, 256, 256, 1);
     add(m.lt_out8, 2024, 256, 8);
     size_t ptotal = 0;
-    for (auto &d : dec) ptotal += d.heads * (align_up(mp::q8p_qbytes(d.N, d.K)) + align_up(mp::q8p_dbytes(d.N, d.K)));
+    auto frag_bytes = [&](const Dec &d) {
+        return align_up(d.w->nib ? mp::q4p_qbytes(d.N, d.K) : mp::q8p_qbytes(d.N, d.K));
+    };
+    for (auto &d : dec) ptotal += d.heads * (frag_bytes(d) + align_up(mp::q8p_dbytes(d.N, d.K)));
     if (m.q8p_arena) { hipFree(m.q8p_arena); m.q8p_arena = nullptr; }
     if (ptotal) HIPCHK(hipMalloc(&m.q8p_arena, ptotal));
     char *pc = (char *)m.q8p_arena;
     for (auto &d : dec) {
-        const size_t qb = align_up(mp::q8p_qbytes(d.N, d.K)), db = align_up(mp::q8p_dbytes(d.N, d.K));
+        const size_t qb = frag_bytes(d), db = align_up(mp::q8p_dbytes(d.N, d.K));
         signed char *oq = (signed char *)pc;
         pc += d.heads * qb;
         unsigned short *od = (unsigned short *)pc;
         pc += d.heads * db;
-        for (int h = 0; h < d.heads; ++h)
-            HIPCHK(mp::pack_q8(d.w->q + (size_t)h * d.N * d.K, d.w->d + (size_t)h * d.N * (d.K / 32), d.N, d.K,
-                               (unsigned char *)oq + h * qb, (unsigned short *)((char *)od + h * db), nullptr));
+        for (int h = 0; h < d.heads; ++h) {
+            const signed char *hq = d.w->q + (size_t)h * d.N * d.K;
+            // the scales (and, for Q8_0, the int8 fragments) in fragment order
+            HIPCHK(mp::pack_q8(hq, d.w->d + (size_t)h * d.N * (d.K / 32), d.N, d.K,
+                               d.w->nib ? nullptr : (unsigned char *)oq + h * qb,
+                               (unsigned short *)((char *)od + h * db), nullptr));
+            if (d.w->nib) HIPCHK(mp::pack_q4(hq, d.N, d.K, (unsigned char *)oq + h * qb, nullptr));
+        }
         d.w->pq = oq;
         d.w->pd = od;
+        d.w->head_q = qb;
     }
     HIPCHK(hipDeviceSynchronize());
     m.q8_all = all;
     return MP_OK;
 }
-// stride between the 8 packed LT heads (fragments, scales), as laid out above
-static size_t q8p_head_q() { return (mp::q8p_qbytes(2024, 256) + 255) & ~(size_t)255; }
+// stride between the 8 packed LT heads' scales, as laid out above (fragments: QW::head_q)
 static size_t q8p_head_d() { return (mp::q8p_dbytes(2024, 256) + 255) & ~(size_t)255; }
 
 // ------------------------------------------------------------------ batch state
@@ -832,6 +853,7 @@ mp::GemvP gemv_base(mp_dev *dev) {
 }
 
 int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vector<mp::OpRec> *ops);
+bool q8_unfused();
 
 // Enqueue one decode iteration: decoder step at pos (embedding codes_prev), LT
 // over 8 codebooks, finalize. When `record` is set, the op list is rebuilt for
@@ -843,7 +865,9 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     const mp::OpTable &tb = mp::table_for(NB, m.weight_mode);
     const mp::OpTableQ8 &tq = mp::table_q8(NB);
     // algorithmic bytes: weights at their stored width (Q8_0: 34 B per 32), activations f32
-    const double F = b16 ? 2.0 : 4.0, Fq = 34.0 / 32.0, A = 4.0, act = (double)NB;
+    const double F = b16 ? 2.0 : 4.0, A = 4.0, act = (double)NB;
+    // a quantised tensor's decode bytes per weight: Q8_0 34/32, Q4_0 nibble fragments 18/32
+    auto Fq = [](const mp::QW &w) { return w.nib ? 18.0 / 32.0 : 34.0 / 32.0; };
     if (record) dev->ops.clear();
     auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
         if (record) {
@@ -862,7 +886,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g.layer = l;
         // LN + QKV (+ frame embedding on layer 0) + KV append   (3415-3442)
         g.W = W.qkv; g.Wb = b16 ? m.pk_qkv[l] : nullptr; g.N = 2304; g.lnw = W.norm_self; g.src = dev->x; g.src_ld = 768; g.out = dev->q;
-        g.Wq = W.qkv8.pq; g.Wd = W.qkv8.pd;
+        g.Wq = W.qkv8.pq; g.Wd = W.qkv8.pd; g.q4 = W.qkv8.nib;
         g.kc = dev->kc; g.vc = dev->vc; g.kv16 = dev->kv16;
         // the frame embedding (2746-2787) is in x already: written by the previous
         // iteration's finalize (lt_finalize_kernel), for the first frame by reset_decode_state
@@ -871,15 +895,18 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->kv16, dev->sa_part};
         // (not at 16 slots: bf16 B=16 20.1k vs 21.5k frames/s; both forms compute the
         // same bits)
-        const bool sa_in_qkv = !W.qkv8 && tb.qkv_sa && NB < 16;
+        // (Q8_0: the same hand-off in the int8 MFMA launch, mp_decode_q8.hip; MAGPIE_Q8_UNFUSED=1
+        // keeps the separate launches, which compute the same bits)
+        const bool q8_fuse = !q8_unfused();
+        const bool sa_in_qkv = (W.qkv8 ? q8_fuse && tq.qkv_sa : tb.qkv_sa != nullptr) && NB < 16;
         {
             mp::GemvFn fn = W.qkv8 ? tq.qkv : tb.qkv;
             if (sa_in_qkv) {
-                fn = tb.qkv_sa;
+                fn = W.qkv8 ? tq.qkv_sa : tb.qkv_sa;
                 g.sa = a; g.qh = dev->qh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
             }
             if ((rc = run(sa_in_qkv ? "qkv_sa" : "qkv", fn, g,
-                          (W.qkv8 ? Fq : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
+                          (W.qkv8 ? Fq(W.qkv8) : F) * (2304.0 * 768) + A * act * ((768 + 2304)))) != MP_OK) return rc;
             if (sa_in_qkv && record) dev->ops.back().add_sa = true;
         }
         if (!sa_in_qkv) {
@@ -894,20 +921,31 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // O-proj + residual (3479, 3509)
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.part = dev->sa_part;
-        g.Wq = W.o8.pq; g.Wd = W.o8.pd;
+        g.Wq = W.o8.pq; g.Wd = W.o8.pd; g.q4 = W.o8.nib;
         mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
         xp.q_f16 = m.weight_mode == MP_WEIGHTS_F16;
         const double xa_bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
         // direct XA (Q8_0 q_net / o_net, or long texts: mp_hip_set_xa_mode): x2 materialised
         const bool xa_dir = W.xq8 || dev->xa_direct;
         const bool xa_in_oproj = tb.oproj_xa && !W.o8 && !xa_dir;
-        if (xa_in_oproj) {
+        // Q8_0 file: the cross-attention's q_net rides in the Q8_0 O-projection's launch on a
+        // hand-off of x1 (EPI_RESID_XQ8); xa_q8_kernel then does the attention and o_net
+        const bool xq8_in_oproj = q8_fuse && W.o8 && W.xq8 && W.xo8 && tq.oproj_xq;
+        if (xq8_in_oproj) {
+            mp::XaQ8P xq{};
+            xq.q = dev->xqb; xq.wq = W.xq8.q; xq.wqd = W.xq8.d; xq.lnw = W.norm_xq; xq.eps = m.eps;
+            g.xq8 = xq; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
+            if ((rc = run("oproj_xq", tq.oproj_xq, g,
+                          Fq(W.o8) * (768.0 * 768) + A * act * (768 * 3) + (34.0 / 32.0) * (128.0 * 768) +
+                              A * act * 128)) != MP_OK)
+                return rc;
+        } else if (xa_in_oproj) {
             // f32: the fused XA rides in the O-projection's launch on a hand-off of x1
             g.xa = xp; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
             if ((rc = run("oproj_xa", tb.oproj_xa, g, F * (768.0 * 768) + A * act * (768 * 3) + xa_bytes)) != MP_OK)
                 return rc;
         } else if ((rc = run("oproj", W.o8 ? tq.oproj : tb.oproj, g,
-                             (W.o8 ? Fq : F) * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) {
+                             (W.o8 ? Fq(W.o8) : F) * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) {
             return rc;
         }
         if (xa_dir) {
@@ -915,10 +953,12 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             // x2 = x + o_net attn(q, K, V) (xa_q8_kernel / xa_f32_kernel); Q8_0 q_net / o_net
             // quantise their activations, else f32 (the bf16 mode keeps XA f32)
             g = gemv_base(dev); g.layer = l;
-            g.W = W.xq; g.Wq = W.xq8.pq; g.Wd = W.xq8.pd; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
+            g.W = W.xq; g.Wq = W.xq8.pq; g.Wd = W.xq8.pd; g.q4 = W.xq8.nib; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
             g.out = dev->xqb; g.out_ld = 128;
-            const double Fx = W.xq8 ? Fq : A;
-            if ((rc = run("xq", W.xq8 ? tq.xq : tb.xq, g, Fx * (128.0 * 768) + A * act * (768 + 128))) != MP_OK) return rc;
+            const double Fx = W.xq8 ? Fq(W.xq8) : A;
+            if (!xq8_in_oproj &&
+                (rc = run("xq", W.xq8 ? tq.xq : tb.xq, g, Fx * (128.0 * 768) + A * act * (768 + 128))) != MP_OK)
+                return rc;
             mp::XaQ8P xq{};
             xq.x = dev->x; xq.x2 = dev->x2; xq.q = dev->xqb; xq.xak = dev->xak; xq.xav = dev->xav; xq.T = dev->T;
             xq.Tmax = dev->Tmax; xq.layer = l; xq.nlayers = L;
@@ -983,6 +1023,12 @@ bool eager_mode() {
     const char *e = getenv("MAGPIE_EAGER");
     return e && atoi(e) != 0;
 }
+// MAGPIE_Q8_UNFUSED=1: the Q8_0 mode's SA and XA as separate launches (the fused forms
+// compute the same bits; tests/test_q8_fused_gpu.py compares them)
+bool q8_unfused() {
+    const char *e = getenv("MAGPIE_Q8_UNFUSED");
+    return e && atoi(e) != 0;
+}
 
 // Diagnostics (MAGPIE_EAGER=1 and MAGPIE_DUMP_LT=file): after every launch of
 // the local transformer, slot 0's LT state is appended to the file as f32
@@ -1005,7 +1051,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     const bool b16 = mp::h16_mode(m.weight_mode);
     const mp::OpTable &tb = mp::table_for(NB, m.weight_mode);
     const mp::OpTableQ8 &tq = mp::table_q8(NB);
-    const double F = b16 ? 2.0 : 4.0, Fq = 34.0 / 32.0, A = 4.0, act = (double)NB;
+    const double F = b16 ? 2.0 : 4.0, A = 4.0, act = (double)NB;
+    // a quantised tensor's decode bytes per weight: Q8_0 34/32, Q4_0 nibble fragments 18/32
+    auto Fq = [](const mp::QW &w) { return w.nib ? 18.0 / 32.0 : 34.0 / 32.0; };
     auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
         if (ops) {
             mp::OpRec r{};
@@ -1033,8 +1081,8 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     {
         mp::GemvP g = base();
         g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.out = io.lt_s; g.out_ld = 9 * 256;
-        g.Wq = m.lt_in8.pq; g.Wd = m.lt_in8.pd; g.Wb = m.pk_lt_in;  // pk_lt_in: F16 mode only
-        const double Fi = m.lt_in8 ? Fq : m.pk_lt_in ? 2.0 : A;
+        g.Wq = m.lt_in8.pq; g.Wd = m.lt_in8.pd; g.q4 = m.lt_in8.nib; g.Wb = m.pk_lt_in;  // pk_lt_in: F16 mode only
+        const double Fi = m.lt_in8 ? Fq(m.lt_in8) : m.pk_lt_in ? 2.0 : A;
         if (io.lt_only) {
             // in_proj of the caller's (already normalised) hidden (1161-1163)
             g.src = io.hidden; g.src_ld = 768;
@@ -1108,17 +1156,17 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             // position 0 (the hidden's in_proj): LN + q|k|v GEMV, then attention + o_net
             g = base(); g.cb = 0;
             g.W = m.lt_qkv; g.Wb = m.pk_lt_qkv; g.N = 768; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX;
-            g.Wq = m.lt_qkv8.pq; g.Wd = m.lt_qkv8.pd;
+            g.Wq = m.lt_qkv8.pq; g.Wd = m.lt_qkv8.pd; g.q4 = m.lt_qkv8.nib;
             g.lnw = m.lt_norm_self; g.lq = io.ltq; g.lk = io.ltk; g.lv = io.ltv;
             if ((rc = run("lt_a", m.lt_qkv8 ? tq.lt_a : tb.lt_a, g,
-                          (m.lt_qkv8 ? Fq : F) * (768.0 * 256) + A * act * (256 * 3 + 768 + 256))) != MP_OK)
+                          (m.lt_qkv8 ? Fq(m.lt_qkv8) : F) * (768.0 * 256) + A * act * (256 * 3 + 768 + 256))) != MP_OK)
                 return rc;
             g = base(); g.cb = 0;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.ltq = io.ltq; g.ltk = io.ltk; g.ltv = io.ltv; g.out = io.ltY;
-            g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd;
+            g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd; g.q4 = m.lt_o8.nib;
             g.out_ld = 256; g.addsrc = io.ltX;
             if ((rc = run("lt_b", m.lt_o8 ? tq.lt_b : tb.lt_b, g,
-                          (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * (256 * 5))) != MP_OK)
+                          (m.lt_o8 ? Fq(m.lt_o8) : F) * (256.0 * 256) + A * act * (256 * 5))) != MP_OK)
                 return rc;
         } else if (NB >= 8) {
             // large batches: the per-slot pick + gathers + attention as one wave per slot
@@ -1137,23 +1185,23 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             dump_lt(io, s);
             g = base(); g.cb = cb;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.src = io.ltq; g.src_ld = 256; g.out = io.ltY; g.out_ld = 256;
-            g.addsrc = io.ltX; g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd;
+            g.addsrc = io.ltX; g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd; g.q4 = m.lt_o8.nib;
             const bool f16 = m.weight_mode == MP_WEIGHTS_F16;
             const mp::GemvFn bo = m.lt_o8 ? (NB == 16 ? mp::q8_lt_bo_16 : mp::q8_lt_bo_8)
                                   : f16   ? (NB == 16 ? mp::f16_lt_bo_16 : mp::f16_lt_bo_8)
                                   : b16   ? (NB == 16 ? mp::b16_lt_bo_16 : mp::b16_lt_bo_8)
                                           : mp::op_lt_bo_8;
-            if ((rc = run("lt_bo", bo, g, (m.lt_o8 ? Fq : F) * (256.0 * 256) + A * act * (256 * 3))) != MP_OK) return rc;
+            if ((rc = run("lt_bo", bo, g, (m.lt_o8 ? Fq(m.lt_o8) : F) * (256.0 * 256) + A * act * (256 * 3))) != MP_OK) return rc;
         } else {
             // position cb: codebook cb-1's pick, its q|k|v row gathered from the load-time
             // table (no q|k|v GEMV), attention + o_net + residual, one launch
             g = base(); g.cb = cb;
             g.W = m.lt_o; g.Wb = m.pk_lt_o; g.N = 256; g.out = io.ltY; g.out_ld = 256;
-            g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd;
+            g.Wq = m.lt_o8.pq; g.Wd = m.lt_o8.pd; g.q4 = m.lt_o8.nib;
             g.logits = io.logits; g.codes_cur = io.codes_cur; g.qkvtab = m.lt_qkvtab; g.ptab = m.lt_ptab;
             g.lt_pos = m.lt_pos; g.ltk = io.ltk; g.ltv = io.ltv; g.lk = io.ltk; g.lv = io.ltv;
             if ((rc = run("lt_bg", m.lt_o8 ? tq.lt_bg : tb.lt_bg, g,
-                          (m.lt_o8 ? Fq : F) * (256.0 * 256) +
+                          (m.lt_o8 ? Fq(m.lt_o8) : F) * (256.0 * 256) +
                               A * act * (2024 + 3 * 256 + 2 * 256 * cb + 2 * 256 + 256))) != MP_OK)
                 return rc;
         }
@@ -1193,7 +1241,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         g.Wb = b16 ? m.pk_lt_out + (size_t)cb * pk_elems(2024, 256) : nullptr; g.bias = m.lt_out_b + (size_t)cb * 2024;
         g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
         if (m.lt_out8) {
-            g.Wq = m.lt_out8.pq + (size_t)cb * q8p_head_q();
+            g.Wq = m.lt_out8.pq + (size_t)cb * m.lt_out8.head_q; g.q4 = m.lt_out8.nib;
             g.Wd = (const unsigned short *)((const char *)m.lt_out8.pd + (size_t)cb * q8p_head_d());
         }
         mp::GemvFn efn = m.lt_out8 ? tq.lt_e : tb.lt_e;
@@ -1202,7 +1250,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             efn = m.lt_out8 ? mp::q8_lt_em_1 : mp::op_lt_em_1;
         }
         if ((rc = run("lt_e", efn, g,
-                      (m.lt_out8 ? Fq : F) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
+                      (m.lt_out8 ? Fq(m.lt_out8) : F) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
             return rc;
     }
     mp::FinP f{io.logits, io.codes_cur, io.codes_prev, io.codes_out, io.step, io.pos, io.done, io.nframes, io.ndone,

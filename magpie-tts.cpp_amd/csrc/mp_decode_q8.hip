@@ -256,66 +256,63 @@ hipError_t pack_q4(const signed char *q, int N, int K, unsigned char *oq, hipStr
 constexpr int XQ8_ROWS = 64;  // o_net rows per workgroup
 
 // a = softmax_t(q . K_t / sqrt(128)) V  of slot b into a_s[128] (every thread
-// returns after a barrier); pr: per-key scores [TMAX_LIMIT]. STAGED: the key and
-// value rows pass through LDS in chunks of XS_ROWS (Ks, Vs [XS_ROWS][128]; chunk 0
-// already there when `pre`), read in the same order with the same arithmetic, so both
-// forms compute the same bits: a key's score is one half-wave dot, the maximum is
-// order-free, and wave w accumulates its keys w, w + 4, ... in ascending order either
-// way (chunks are whole multiples of 16 keys).
-constexpr int XS_ROWS = 64;
-// rows [c0, c0 + n) of a [T][128] f32 matrix into LDS stage[XS_ROWS][128]
-__device__ __forceinline__ void xa_stage_rows(const float *src, int c0, int n, float *stage) {
-    constexpr int PER = XS_ROWS * DXA / 4 / MP_BLOCK;  // float4 per thread
-    float4 r[PER];  // every load issued (rows past n re-read row n - 1), then stored
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int e = threadIdx.x + MP_BLOCK * j, row = min(e / (DXA / 4), n - 1);
-        r[j] = *(const float4 *)(src + (size_t)(c0 + row) * DXA + 4 * (e % (DXA / 4)));
-    }
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int e = threadIdx.x + MP_BLOCK * j, row = e / (DXA / 4);
-        if (row < n) *(float4 *)(stage + 4 * e) = r[j];
-    }
-}
-template <bool STAGED>
+// returns after a barrier); pr: per-key scores [TMAX_LIMIT]. The first XA_PF_K
+// rounds of key rows and XA_PF_V rounds of value rows (the first 64 keys) are issued
+// at entry, before q is read: one memory round trip for a text of up to 64 tokens
+// instead of one per round; longer texts load the later rounds in the loops. Each
+// key's score is one half-wave dot and wave w accumulates its keys w, w + 4, ... in
+// ascending order, however the rows arrive.
+constexpr int XA_PF_K = 2, XA_PF_V = 4;  // rounds of 32 / 16 keys
 __device__ __forceinline__ void xa_text_attention(const float *q, const float *Kb, const float *Vb, int Tb,
-                                                  float *pr, float *a_s, float *Ks = nullptr, float *Vs = nullptr,
-                                                  bool pre = false) {
+                                                  float *pr, float *a_s) {
 #pragma clang fp contract(off)
     __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
     __shared__ float wred[2 * MP_NWAVES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int h = lane >> 5, d4 = 4 * (lane & 31);
+    // pass-1 rounds: keys t0 + 8 u + h, t0 = 2 w + 32 r; pass-2 rounds: keys t0 + 4 u, t0 = w + 16 r
+    float4 kpf[XA_PF_K][4];
+    float v0pf[XA_PF_V][4], v1pf[XA_PF_V][4];
+#pragma unroll
+    for (int r = 0; r < XA_PF_K; ++r)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(2 * w + 32 * r + 2 * MP_NWAVES * u + h, Tb - 1);
+            kpf[r][u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
+        }
+#pragma unroll
+    for (int r = 0; r < XA_PF_V; ++r)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(w + 16 * r + MP_NWAVES * u, Tb - 1);
+            v0pf[r][u] = Vb[(size_t)t * DXA + lane];
+            v1pf[r][u] = Vb[(size_t)t * DXA + 64 + lane];
+        }
     const float4 q4 = *(const float4 *)(q + d4);
     const float scale = 1.0f / sqrtf((float)DXA);
-    const int CH = STAGED ? XS_ROWS : Tb;  // keys per chunk
     float mx = -INFINITY;
-    for (int c0 = 0; c0 < Tb; c0 += CH) {
-        const int c1 = min(Tb, c0 + CH);
-        if (STAGED && !(pre && c0 == 0)) {
-            lds_sync();
-            xa_stage_rows(Kb, c0, c1 - c0, Ks);
-            lds_sync();
-        }
-        for (int t0 = c0 + 2 * w; t0 < c1; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
-            float4 k4[4];
+    auto scores = [&](int t0, const float4 (&k4)[4]) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = min(t0 + 2 * MP_NWAVES * u + h, c1 - 1);
-                k4[u] = STAGED ? *(const float4 *)(Ks + (size_t)(t - c0) * DXA + d4)
-                               : *(const float4 *)(Kb + (size_t)t * DXA + d4);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = t0 + 2 * MP_NWAVES * u + h;
-                const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
-                if (t < c1) {
-                    if ((lane & 31) == 0) pr[t] = sv;
-                    mx = fmaxf(mx, sv);
-                }
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + 2 * MP_NWAVES * u + h;
+            const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
+            if (t < Tb) {
+                if ((lane & 31) == 0) pr[t] = sv;
+                mx = fmaxf(mx, sv);
             }
         }
+    };
+#pragma unroll
+    for (int r = 0; r < XA_PF_K; ++r)
+        if (2 * w + 32 * r < Tb) scores(2 * w + 32 * r, kpf[r]);
+    for (int t0 = 2 * w + 32 * XA_PF_K; t0 < Tb; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
+        float4 k4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(t0 + 2 * MP_NWAVES * u + h, Tb - 1);
+            k4[u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
+        }
+        scores(t0, k4);
     }
     mx = wave_max(mx);
     if (lane == 0) wred[w] = mx;
@@ -323,25 +320,28 @@ __device__ __forceinline__ void xa_text_attention(const float *q, const float *K
     const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
     // o[d] = sum_t e_t V_t[d]: wave w takes keys t = w + 4 u, lane owns dims lane, 64 + lane
     float l = 0.f, o0 = 0.f, o1 = 0.f;
-    for (int c0 = 0; c0 < Tb; c0 += CH) {
-        const int c1 = min(Tb, c0 + CH);
-        if (STAGED && !(pre && c0 == 0)) {
-            lds_sync();
-            xa_stage_rows(Vb, c0, c1 - c0, Vs);
-            lds_sync();
-        }
-        for (int t0 = c0 + w; t0 < c1; t0 += MP_NWAVES * 4) {
-            float v0[4], v1[4], e[4];
+    auto accum = [&](int t0, const float (&v0)[4], const float (&v1)[4]) {
+        float e[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = min(t0 + MP_NWAVES * u, Tb - 1);
-                v0[u] = STAGED ? Vs[(size_t)(t - c0) * DXA + lane] : Vb[(size_t)t * DXA + lane];
-                v1[u] = STAGED ? Vs[(size_t)(t - c0) * DXA + 64 + lane] : Vb[(size_t)t * DXA + 64 + lane];
-                e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) { l += e[u]; o0 = fmaf(e[u], v0[u], o0); o1 = fmaf(e[u], v1[u], o1); }
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(t0 + MP_NWAVES * u, Tb - 1);
+            e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { l += e[u]; o0 = fmaf(e[u], v0[u], o0); o1 = fmaf(e[u], v1[u], o1); }
+    };
+#pragma unroll
+    for (int r = 0; r < XA_PF_V; ++r)
+        if (w + 16 * r < Tb) accum(w + 16 * r, v0pf[r], v1pf[r]);
+    for (int t0 = w + 16 * XA_PF_V; t0 < Tb; t0 += MP_NWAVES * 4) {
+        float v0[4], v1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(t0 + MP_NWAVES * u, Tb - 1);
+            v0[u] = Vb[(size_t)t * DXA + lane];
+            v1[u] = Vb[(size_t)t * DXA + 64 + lane];
+        }
+        accum(t0, v0, v1);
     }
     pv[w][lane] = o0;
     pv[w][64 + lane] = o1;
@@ -419,16 +419,8 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
         wo[g] = *(const uint4 *)(p.wo + (size_t)row * DXA + kc * 16);
         wos[g] = __half2float(__ushort_as_half(p.wod[(size_t)row * (DXA / 32) + kc / 2]));
     }
-    // the slot's first XS_ROWS text keys and values into LDS, every load in flight at
-    // once (they do not depend on q), then the same attention on the staged rows
-    __shared__ __attribute__((aligned(16))) float Ks[XS_ROWS * DXA];
-    __shared__ __attribute__((aligned(16))) float Vs[XS_ROWS * DXA];
     const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-    const int Tb = p.T[b];
-    xa_stage_rows(p.xak + kv, 0, min(Tb, XS_ROWS), Ks);
-    xa_stage_rows(p.xav + kv, 0, min(Tb, XS_ROWS), Vs);
-    lds_sync();
-    xa_text_attention<true>(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, Tb, pr, a_s, Ks, Vs, true);
+    xa_text_attention(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
     xa_quantize_a(a_s, aq, ad);
     // ---- x2 = x + Q8(o_net) a for this workgroup's 64 rows (8 per group)
     xa_q8_onet<OG>(wo, wos, r0, aq, ad, p.x + (size_t)b * D, p.x2 + (size_t)b * D);
@@ -558,7 +550,7 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_f32_kernel(XaQ8P p) {
 #pragma unroll
     for (int i = 0; i < RP; ++i) wo[i] = *(const float4 *)(p.wof + (size_t)(r0 + 2 * i + hr) * DXA + d4);
     const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
-    xa_text_attention<false>(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
+    xa_text_attention(p.q + (size_t)b * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
     const float4 a4 = *(const float4 *)&a_s[d4];
     float v = 0.f;
 #pragma unroll

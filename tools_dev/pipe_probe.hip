@@ -43,11 +43,11 @@ struct LinkP {
 };
 
 template <int K, int RW, bool GIN, bool GOUT>
-__global__ __launch_bounds__(256) void link_kernel(LinkP p) {
+__device__ __forceinline__ void link_body(const LinkP &p, int blk) {
     constexpr int NV = K / 256;
     __shared__ __attribute__((aligned(16))) float act[K];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int row0 = (blockIdx.x * 4 + w) * RW;
+    const int row0 = (blk * 4 + w) * RW;
     float4 wv[RW][NV];
 #pragma unroll
     for (int r = 0; r < RW; ++r)
@@ -105,6 +105,14 @@ __global__ __launch_bounds__(256) void link_kernel(LinkP p) {
         p.out[n] = v;
     }
 }
+template <int K, int RW, bool GIN, bool GOUT>
+__global__ __launch_bounds__(256) void link_kernel(LinkP p) { link_body<K, RW, GIN, GOUT>(p, blockIdx.x); }
+// a down link (3072 -> 768, plain input, granule output) and the next up link
+// (768 -> 3072, granule input from it, plain output) in ONE launch
+__global__ __launch_bounds__(256) void pair_kernel(LinkP pd, LinkP pu, int nd) {
+    if ((int)blockIdx.x < nd) link_body<F, 1, false, true>(pd, blockIdx.x);
+    else link_body<D, 2, true, false>(pu, blockIdx.x - nd);
+}
 
 // start of a replay: epoch += 1, x0 published as plain values and as granules of tag epoch*64
 __global__ void epoch_kernel(unsigned *epoch, const float *x0, float *xplain, unsigned long long *gx) {
@@ -161,6 +169,18 @@ static double run_mode(int mode, std::vector<float> &final_out, int reps) {
         CK(hipEventRecord(ef, st[0]));
         for (int i = 1; i < ns; ++i) CK(hipStreamWaitEvent(st[i], ef, 0));
     }
+    if (mode == 4) {
+        // up0 alone; then (down_j, up_j+1) pairs in one launch each; the last down alone
+        launch_link<false, false>(0, st[0]);
+        for (int j = 1; j < NLINK; j += 2) {
+            if (j + 1 >= NLINK) { launch_link<false, false>(j, st[0]); break; }
+            LinkP pd{}, pu{};
+            pd.W = g_W[j]; pd.N = D; pd.in = g_act[j]; pd.gout = g_gact[j + 1]; pd.epoch = g_epoch; pd.link = j; pd.err = g_err;
+            pu.W = g_W[j + 1]; pu.N = F; pu.gin = g_gact[j + 1]; pu.out = g_act[j + 2]; pu.epoch = g_epoch; pu.link = j + 1;
+            pu.err = g_err;
+            hipLaunchKernelGGL(pair_kernel, dim3(D / 4 + F / 8), dim3(256), 0, st[0], pd, pu, D / 4);
+        }
+    } else
     for (int j = 0; j < NLINK; ++j) {
         hipStream_t s = st[j % ns];
         const bool last = j == NLINK - 1;
@@ -224,11 +244,11 @@ int main() {
     CK(hipMalloc(&g_x0, D * sizeof(float)));
     hipLaunchKernelGGL(init_kernel, dim3(4), dim3(256), 0, 0, g_x0, (size_t)D, 99u, 1.0f);
     CK(hipDeviceSynchronize());
-    const char *names[4] = {"1 stream, plain loads/stores", "1 stream, granules", "2-stream ladder, granules",
-                            "3-stream ladder, granules"};
+    const char *names[5] = {"1 stream, plain loads/stores", "1 stream, granules", "2-stream ladder, granules",
+                            "3-stream ladder, granules", "down+up pairs in one launch"};
     std::vector<float> ref, o;
     for (int pass = 0; pass < 2; ++pass) {
-        for (int m = 0; m < 4; ++m) {
+        for (int m : {0, 4, 1}) {
             const double us = run_mode(m, o, 30);
             if (m == 0 && pass == 0) ref = o;
             const bool same = memcmp(ref.data(), o.data(), D * sizeof(float)) == 0;

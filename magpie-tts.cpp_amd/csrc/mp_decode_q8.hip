@@ -51,6 +51,8 @@ __device__ __forceinline__ float quad_max(float v) {
 }
 
 __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char *actq, float *actd, unsigned long long t_start);
+__device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_start);
+constexpr int XQG = 8;  // q_net workgroups per slot in EPI_RESID_XQ8 (16 rows each)
 
 template <int NB, int K, int PRO, int EPI, bool Q4>
 __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
@@ -76,7 +78,12 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
         }
     }
     if constexpr (EPI == EPI_RESID_XQ8) {
-        // the launch's last XQG x NB workgroups: the XA's q_net on this launch's x1
+        // then XQG x NB workgroups: the XA's q_net on this launch's x1; then XQ8A x NB:
+        // the XA's attention + o_net on that q
+        if (rt >= p.nrow_blocks + XQG * NB) {
+            xq8a_tail(p, t_start);
+            return;
+        }
         if (rt >= p.nrow_blocks) {
             xq8_tail(p, act, actq, actd, t_start);
             return;
@@ -263,8 +270,9 @@ constexpr int XQ8_ROWS = 64;  // o_net rows per workgroup
 // key's score is one half-wave dot and wave w accumulates its keys w, w + 4, ... in
 // ascending order, however the rows arrive.
 constexpr int XA_PF_K = 2, XA_PF_V = 4;  // rounds of 32 / 16 keys
-__device__ __forceinline__ void xa_text_attention(const float *q, const float *Kb, const float *Vb, int Tb,
-                                                  float *pr, float *a_s) {
+template <typename QF>
+__device__ __forceinline__ void xa_text_attention_q(QF getq, const float *Kb, const float *Vb, int Tb, float *pr,
+                                                    float *a_s) {
 #pragma clang fp contract(off)
     __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
     __shared__ float wred[2 * MP_NWAVES];
@@ -288,7 +296,7 @@ __device__ __forceinline__ void xa_text_attention(const float *q, const float *K
             v0pf[r][u] = Vb[(size_t)t * DXA + lane];
             v1pf[r][u] = Vb[(size_t)t * DXA + 64 + lane];
         }
-    const float4 q4 = *(const float4 *)(q + d4);
+    const float4 q4 = getq(d4);  // this lane's q[d4 .. d4 + 3]
     const float scale = 1.0f / sqrtf((float)DXA);
     float mx = -INFINITY;
     auto scores = [&](int t0, const float4 (&k4)[4]) {
@@ -352,6 +360,11 @@ __device__ __forceinline__ void xa_text_attention(const float *q, const float *K
         a_s[tid] = (((pv[0][tid] + pv[1][tid]) + pv[2][tid]) + pv[3][tid]) / den;
     }
     lds_sync();
+}
+
+__device__ __forceinline__ void xa_text_attention(const float *q, const float *Kb, const float *Vb, int Tb,
+                                                  float *pr, float *a_s) {
+    xa_text_attention_q([&](int d4) { return *(const float4 *)(q + d4); }, Kb, Vb, Tb, pr, a_s);
 }
 
 // a (LDS, [128]) -> Q8_0 blocks aq / ad (ggml quantises the o_net operand), wave 0
@@ -436,7 +449,7 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
 // quarter's block dots accumulated in block order and the quarters summed in order,
 // stored to q. xa_q8_kernel (the next launch) does the attention and o_net. Same bits
 // as the q GEMV (tests/test_q8_fused_gpu.py).
-constexpr int XQG = 8, XQ_ROWS = DXA / XQG, XQ_QB = D / 32 / 4;  // 8 workgroups x 16 rows; 6 blocks per quarter
+constexpr int XQ_ROWS = DXA / XQG, XQ_QB = D / 32 / 4;  // 8 workgroups x 16 rows; 6 blocks per quarter
 __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char *actq, float *actd,
                                          unsigned long long t_start) {
 #pragma clang fp contract(off)
@@ -534,7 +547,80 @@ __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char
         acc = fmaf((float)sd, dw * actd[blk], acc);
     }
     const float p1 = __shfl_down(acc, 1, 64), p2 = __shfl_down(acc, 2, 64), p3 = __shfl_down(acc, 3, 64);
-    if (qa == 0) const_cast<float *>(x.q)[(size_t)b * DXA + qr] = ((acc + p1) + p2) + p3;  // q: this tail's output
+    if (qa == 0) {  // q to the launch's attention workgroups as a {tag, value} granule
+        const float qv = ((acc + p1) + p2) + p3;
+        const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+        __hip_atomic_store((gu64 *)(x.qg + (size_t)b * DXA + qr), ((unsigned long long)tag << 32) | __float_as_uint(qv),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    ts_end(p.ts, t_start);
+}
+
+// The attention + o_net stage of the same launch (the launch's last XQ8A x NB
+// workgroups, XQ8_ROWS o_net rows each): o_net rows and the first 64 text keys and
+// values issued at entry, q swept from the q_net tail's granules (each wave the 128,
+// through its own LDS row into the float4 layout), then xa_q8_kernel's arithmetic:
+// the attention, a quantised to Q8_0, x2 = x1 + o_net a for its rows (x1 from the
+// O-projection's granules).
+constexpr int XQ8A = D / XQ8_ROWS;
+__device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_start) {
+    constexpr int OG = XQ8_ROWS / MP_NWAVES / XQ8_OR;
+    const XaQ8P &x = p.xq8;
+    __shared__ float pr[TMAX_LIMIT];
+    __shared__ __attribute__((aligned(16))) float a_s[DXA];
+    __shared__ __attribute__((aligned(16))) signed char aq[DXA];
+    __shared__ float ad[DXA / 32];
+    __shared__ __attribute__((aligned(16))) float qrow[MP_NWAVES][DXA];
+    __shared__ float x1s[XQ8_ROWS];
+    const int k = blockIdx.x - p.nrow_blocks - XQG * p.nslots, b = k / XQ8A, rb = k % XQ8A;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rb * XQ8_ROWS + w * OG * XQ8_OR;
+    uint4 wo[OG];
+    float wos[OG];
+#pragma unroll
+    for (int g = 0; g < OG; ++g) {
+        const int row = r0 + g * XQ8_OR + lane / XQ8_OCPR, kc = lane % XQ8_OCPR;
+        wo[g] = *(const uint4 *)(x.wo + (size_t)row * DXA + kc * 16 + ts_dep(t_start));
+        wos[g] = __half2float(__ushort_as_half(x.wod[(size_t)row * (DXA / 32) + kc / 2]));
+    }
+    const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+    auto sweep = [&](gu64 *gr, float *dst, int n) {  // n = 64 or 128 granules, every lane its share
+        float v[2];
+        for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (lane + 64 * j >= n) continue;
+                const unsigned long long u = __hip_atomic_load(gr + lane + 64 * j, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                v[j] = __uint_as_float((unsigned)u);
+                ok &= (unsigned)(u >> 32) == tag;
+            }
+            if (__all(ok)) break;
+            if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+                if (lane == 0)
+                    __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v[0] = v[1] = __builtin_nanf("");
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (lane + 64 * j < n) dst[lane + 64 * j] = v[j];
+    };
+    const size_t kv = ((size_t)(b * x.nlayers + x.layer) * x.Tmax) * DXA;
+    xa_text_attention_q(
+        [&](int d4) {
+            sweep((gu64 *)(x.qg + (size_t)b * DXA), qrow[w], DXA);
+            wave_lds_sync();
+            return *(const float4 *)&qrow[w][d4];
+        },
+        x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
+    ts_mark(p.ts, t_start);  // profiling: attention done
+    if (w == 0) sweep((gu64 *)(p.xh + (size_t)b * D + rb * XQ8_ROWS), x1s, XQ8_ROWS);
+    xa_quantize_a(a_s, aq, ad);  // (its barrier also publishes x1s)
+    xa_q8_onet<OG>(wo, wos, r0, aq, ad, x1s - rb * XQ8_ROWS, x.x2 + (size_t)b * D);
     ts_end(p.ts, t_start);
 }
 
@@ -595,7 +681,8 @@ static bool q8_args_ok(const GemvP &p) {
     if constexpr (EPI == EPI_LTQKV) ok &= p.lq && p.lk && p.lv;
     if constexpr (EPI == EPI_RESID_XQ8) {
         const XaQ8P &x = p.xq8;
-        ok &= p.resid && p.xh && p.iter && p.hx_err && p.N == D && x.q && x.wq && x.wqd && x.lnw;
+        ok &= p.resid && p.xh && p.iter && p.hx_err && p.N == D && x.qg && x.wq && x.wqd && x.lnw && x.x2 && x.wo &&
+              x.wod && x.xak && x.xav && x.T && x.Tmax >= 1 && x.Tmax <= TMAX_LIMIT && x.layer == p.layer;
     }
     return ok;
 }
@@ -605,7 +692,7 @@ static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     if (!q8_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
     GemvP q = p;
     q.nrow_blocks = (p.N + 15) / 16;
-    const int grid = q.nrow_blocks + (EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : EPI == EPI_RESID_XQ8 ? XQG * NB : 0);
+    const int grid = q.nrow_blocks + (EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : EPI == EPI_RESID_XQ8 ? (XQG + XQ8A) * NB : 0);
     if (p.q4) mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI, true>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     else mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI, false>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();

@@ -62,9 +62,10 @@ enum Epi {
                         // launch's last XA_SPLITS x NB workgroups run the fused XA on it (below)
     EPI_QKV_SA = 12,    // EPI_QKV, each q|k|v value also published as a tagged granule qh[b][2304];
                         // the launch's last NH x SA_SPLITS x NB workgroups run the SA on it
-    EPI_RESID_XQ8 = 13, // Q8_0 O-projection: EPI_RESID_XA's stores and granules; the launch's last
-                        // XQG x NB workgroups compute the cross-attention's q = Q8(q_net) LN(x1) on
-                        // them (xa_q8_kernel, the next launch, does the attention and o_net)
+    EPI_RESID_XQ8 = 13, // Q8_0 O-projection: EPI_RESID_XA's stores and granules; then XQG x NB
+                        // workgroups compute the cross-attention's q = Q8(q_net) LN(x1) and hand it on
+                        // as granules, and XQ8A x NB workgroups the attention + o_net: x2 (direct
+                        // Q8_0 XA, xa_q8_kernel's arithmetic)
 };
 
 // Temperature / top-k sampling (sample_top_k, magpie.cpp:1072-1109). Off when
@@ -173,12 +174,13 @@ struct XaQ8P {
     const float *xak, *xav;         // XA K, V [B][L][Tmax][128]
     const int *T;
     int Tmax, layer, nlayers;
-    // EPI_RESID_XQ8 (q_net in the Q8_0 O-projection's launch): q = Q8(q_net) Q8(LN(x1) * lnw)
-    // from the handed-off x1, stored to q
+    // EPI_RESID_XQ8 (the XA in the Q8_0 O-projection's launch): q = Q8(q_net) Q8(LN(x1) * lnw)
+    // from the handed-off x1, handed to the attention workgroups as granules qg[B][128]
     const signed char *wq;          // q_net int8 [128][768] as stored
     const unsigned short *wqd;      //   fp16 block scales [128][24]
     const float *lnw;               // norm_xattn_query
     float eps;
+    unsigned long long *qg;         // [B][128] {tag, value} granules of q
 };
 
 struct AttnP {  // decode self-attention (one query per utterance)

@@ -274,6 +274,7 @@ struct mp_dev {
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     unsigned long long *xh = nullptr;  // O-projection -> XA hand-off granules [NB][768] (EPI_RESID_XA)
     unsigned long long *qh = nullptr;  // QKV -> SA hand-off granules [NB][2304] (EPI_QKV_SA)
+    unsigned long long *xqh = nullptr; // Q8_0 XA q_net -> attention hand-off granules [NB][128] (EPI_RESID_XQ8)
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
@@ -809,7 +810,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(sa_out, NB * 768);
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
-    A(xh, (size_t)NB * D); A(qh, (size_t)NB * 3 * D);
+    A(xh, (size_t)NB * D); A(qh, (size_t)NB * 3 * D); A(xqh, (size_t)NB * 128);
     const size_t kvn = (size_t)NB * L * dev->max_seq * D;  // elements; bf16 mode: 2 per float slot
     A(kc, dev->kv16 ? kvn / 2 : kvn); A(vc, dev->kv16 ? kvn / 2 : kvn);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
@@ -928,16 +929,21 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // direct XA (Q8_0 q_net / o_net, or long texts: mp_hip_set_xa_mode): x2 materialised
         const bool xa_dir = W.xq8 || dev->xa_direct;
         const bool xa_in_oproj = tb.oproj_xa && !W.o8 && !xa_dir;
-        // Q8_0 file: the cross-attention's q_net rides in the Q8_0 O-projection's launch on a
-        // hand-off of x1 (EPI_RESID_XQ8); xa_q8_kernel then does the attention and o_net
-        const bool xq8_in_oproj = q8_fuse && W.o8 && W.xq8 && W.xo8 && tq.oproj_xq;
+        // Q8_0 file: the whole direct Q8_0 cross-attention rides in the Q8_0 O-projection's
+        // launch (EPI_RESID_XQ8): q_net workgroups on a hand-off of x1, then attention +
+        // o_net workgroups on a hand-off of q; x2 materialised
+        // (up to 8 slots: its 48 + 20 NB workgroups are then co-resident even at one per CU,
+        // so no hand-off waits on a workgroup that has not been dispatched)
+        const bool xq8_in_oproj = q8_fuse && W.o8 && W.xq8 && W.xo8 && tq.oproj_xq && NB <= 8;
         if (xq8_in_oproj) {
             mp::XaQ8P xq{};
-            xq.q = dev->xqb; xq.wq = W.xq8.q; xq.wqd = W.xq8.d; xq.lnw = W.norm_xq; xq.eps = m.eps;
+            xq.x2 = dev->x2; xq.xak = dev->xak; xq.xav = dev->xav; xq.T = dev->T; xq.Tmax = dev->Tmax;
+            xq.layer = l; xq.nlayers = L; xq.wo = W.xo8.q; xq.wod = W.xo8.d;
+            xq.wq = W.xq8.q; xq.wqd = W.xq8.d; xq.lnw = W.norm_xq; xq.eps = m.eps; xq.qg = dev->xqh;
             g.xq8 = xq; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
-            if ((rc = run("oproj_xq", tq.oproj_xq, g,
-                          Fq(W.o8) * (768.0 * 768) + A * act * (768 * 3) + (34.0 / 32.0) * (128.0 * 768) +
-                              A * act * 128)) != MP_OK)
+            if ((rc = run("oproj_xa_q8", tq.oproj_xq, g,
+                          Fq(W.o8) * (768.0 * 768) + A * act * (768 * 3) + (34.0 / 32.0) * (2.0 * 128 * 768) +
+                              A * act * (768 + 2.0 * 128 * dev->Tmax))) != MP_OK)
                 return rc;
         } else if (xa_in_oproj) {
             // f32: the fused XA rides in the O-projection's launch on a hand-off of x1
@@ -948,7 +954,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
                              (W.o8 ? Fq(W.o8) : F) * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) {
             return rc;
         }
-        if (xa_dir) {
+        if (xa_dir && !xq8_in_oproj) {
             // cross-attention as ggml computes it (1713-1767): q = q_net LN(x) (GEMV), then
             // x2 = x + o_net attn(q, K, V) (xa_q8_kernel / xa_f32_kernel); Q8_0 q_net / o_net
             // quantise their activations, else f32 (the bf16 mode keeps XA f32)
@@ -956,8 +962,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             g.W = W.xq; g.Wq = W.xq8.pq; g.Wd = W.xq8.pd; g.q4 = W.xq8.nib; g.N = 128; g.lnw = W.norm_xq; g.src = dev->x; g.src_ld = 768;
             g.out = dev->xqb; g.out_ld = 128;
             const double Fx = W.xq8 ? Fq(W.xq8) : A;
-            if (!xq8_in_oproj &&
-                (rc = run("xq", W.xq8 ? tq.xq : tb.xq, g, Fx * (128.0 * 768) + A * act * (768 + 128))) != MP_OK)
+            if ((rc = run("xq", W.xq8 ? tq.xq : tb.xq, g, Fx * (128.0 * 768) + A * act * (768 + 128))) != MP_OK)
                 return rc;
             mp::XaQ8P xq{};
             xq.x = dev->x; xq.x2 = dev->x2; xq.q = dev->xqb; xq.xak = dev->xak; xq.xav = dev->xav; xq.T = dev->T;
@@ -971,7 +976,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
                 dev->ops.push_back(r);
             }
             HIPCHK(mp::op_xa_q8(xq, NB, s));
-        } else if (!xa_in_oproj) {
+        } else if (!xa_in_oproj && !xq8_in_oproj) {
             // cross-attention, fused (1713-1767, 3513-3519): x2 = x + o_net(attn(q_net(LN(x))))
             if (record) {
                 mp::OpRec r{};
@@ -1594,6 +1599,7 @@ int reset_decode_state(mp_dev *dev) {
     // hand-off tags restart with the iteration counter (ndone[1]): no stale tag may match
     HIPCHK(hipMemsetAsync(dev->xh, 0, (size_t)NB * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->xqh, 0, (size_t)NB * 128 * 8, dev->stream));
     // the first frame's decoder input (the BOS codes); later frames' by lt_finalize_kernel
     HIPCHK(mp::op_embed(mp::EmbP{dev->m.audio_emb, dev->codes_prev, dev->m.dec_pos, dev->pos, dev->x}, NB, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go
@@ -1653,14 +1659,17 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, dev->stream));
-    const int poll = 8;
+    // one graph replay per frame: capturing 4 to 64 iterations per graph measured the same
+    // frames/s (2619 vs 2617-2626, tools_dev/graph_iters_ab.py), replay boundaries cost nothing
+    const int poll = 8;  // the host checks the done counter every `poll` iterations
     int it = 0;
-    for (; it < dev->max_steps; ++it) {
+    while (it < dev->max_steps) {
         if (int rc = launch_iteration(dev)) return rc;
-        if (!dev->params.ignore_eos && (it + 1) % poll == 0 && it + 1 < dev->max_steps) {
+        ++it;
+        if (!dev->params.ignore_eos && it % poll == 0 && it < dev->max_steps) {
             HIPCHK(hipMemcpyAsync(dev->h_ndone, dev->ndone, 4, hipMemcpyDeviceToHost, dev->stream));
             HIPCHK(hipStreamSynchronize(dev->stream));
-            if (*dev->h_ndone >= NB) { ++it; break; }
+            if (*dev->h_ndone >= NB) break;
         }
     }
     HIPCHK(hipEventRecord(e1, dev->stream));

@@ -1,14 +1,15 @@
 """The Q8_0 weight mode's fused launches against its separate ones.
 
-A Q8_0 (or Q4_0) file runs the decoder layer in five launches: the int8 MFMA QKV
-projection with the self-attention riding in it (EPI_QKV_SA, the hand-off the f32
-and 16-bit families use), the int8 O-projection with the cross-attention's q_net
-riding in it (EPI_RESID_XQ8), xa_q8_kernel (attention over the text keys staged in
-LDS, o_net, x2), then the two F32 FFN convs. MAGPIE_Q8_UNFUSED=1 runs the same
-arithmetic as seven separate launches (QKV, sa_attn, O-projection, the q_net GEMV,
-xa_q8_kernel, FFN); the fused forms must reproduce them bit for bit: codes and every
-hidden state, greedy and sampled, at every batch size, for texts inside one staged
-key chunk (T <= 64) and across several (T > 64). Agreement with the oracle's Q8_0
+A Q8_0 (or Q4_0) file runs the decoder layer in four launches (up to 8 slots): the
+int8 MFMA QKV projection with the self-attention riding in it (EPI_QKV_SA, the
+hand-off the f32 and 16-bit families use), the int8 O-projection with the whole
+direct Q8_0 cross-attention riding in it (EPI_RESID_XQ8: q_net workgroups on a
+hand-off of x1, attention + o_net workgroups on a hand-off of q), then the two F32
+FFN convs. MAGPIE_Q8_UNFUSED=1 runs the same arithmetic as seven separate launches
+(QKV, sa_attn, O-projection, the q_net GEMV, xa_q8_kernel, FFN); the fused forms must
+reproduce them bit for bit: codes and every hidden state, greedy and sampled, at
+every batch size, for texts inside the prefetched first 64 keys and beyond them
+(T > 64). Agreement with the oracle's Q8_0
 mode is checked by tests/test_decode_gpu.py and tests/test_configs_gpu.py on the
 default (fused) path.
 """
@@ -47,9 +48,10 @@ def test_q8_fused_equals_unfused(ma, q8_model, B, T):
     kw = dict(max_dec_steps=24, ignore_eos=True)
     rf, ops_f = _run(ma, q8_model, toks, False, **kw)
     ru, ops_u = _run(ma, q8_model, toks, True, **kw)
-    assert "oproj_xq" in ops_f and "xq" not in ops_f and "oproj" not in ops_f, sorted(set(ops_f))
-    assert "xq" in ops_u and "oproj" in ops_u and "oproj_xq" not in ops_u, sorted(set(ops_u))
-    if B < 16:
+    assert "xq" in ops_u and "oproj" in ops_u and "xa_q8" in ops_u and "oproj_xa_q8" not in ops_u, sorted(set(ops_u))
+    assert "xa" not in ops_f and "xa" not in ops_u  # no reassociated-XA launch in the Q8_0 mode
+    if B < 16:  # (16 slots keep the separate launches)
+        assert "oproj_xa_q8" in ops_f and "xq" not in ops_f and "xa_q8" not in ops_f, sorted(set(ops_f))
         assert "qkv_sa" in ops_f and "sa_attn" not in ops_f
     print(f"B={B} T={T}: {len(ops_f)} launches per iteration fused, {len(ops_u)} unfused")
     for b in range(B):

@@ -153,88 +153,104 @@ hipError_t op_xa(const XaP &p, int B, hipStream_t s) {
 // (magpie.cpp:4340-4358): stop on EOS in any codebook (frame not emitted), else
 // append the frame; stop at max_dec_steps; otherwise the frame becomes the next
 // decoder input and the position advances.
-// slot b's decoder input from the frame codes cc at position ps, one wave:
-// embed_kernel's arithmetic (codebooks summed in order, / 8, + position)
-template <typename C>
-__device__ __forceinline__ void embed_row(const FinP &p, int b, const C &cc, int ps) {
-    int c[NCB];
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) c[cb] = cc[cb];
-    for (int k = threadIdx.x; k < D; k += 64) {
-        float s = p.emb[((size_t)0 * VCB + c[0]) * D + k];
-#pragma unroll
-        for (int cb = 1; cb < NCB; ++cb) s = s + p.emb[((size_t)cb * VCB + c[cb]) * D + k];
-        p.x[(size_t)b * D + k] = s * 0.125f + p.pos_emb[(size_t)ps * D + k];
-    }
-}
-
-__global__ __launch_bounds__(64) void lt_finalize_kernel(FinP p) {
+// Launched with FIN_THREADS = 4 waves per slot. Wave 0 runs codebook 7's pick
+// and the books; waves 1-3 (192 lanes, one float4 of the 768 each) meanwhile
+// gather the next decoder input's codebook 0-6 rows and its position row, which do
+// not depend on the pick, so only codebook 7's row is loaded after it. The sum
+// keeps embed_kernel's order (codebooks 0..7 in sequence, / 8, + position): the
+// same bits.
+constexpr int FIN_THREADS = 256;
+__global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
     const unsigned long long t_start = ts_begin(p.ts);
-    // one wave per slot: codebook 7's pick with the same wave_pick as every other
-    // codebook (masked first-max argmax; top-k draw when sampling)
-    const int b = blockIdx.x, tid = threadIdx.x;
+    const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
     if (p.iter && b == 0 && tid == 0) p.iter[0] += 1;  // the next iteration's hand-off tags
-    if (p.done[b]) {
-        // a finished slot keeps running with the batch: give it its frozen input again
-        // (codes_prev / pos no longer advance), so every later iteration recomputes the
-        // values of the one that ended it (the hidden-state trace row at the frozen
-        // step included) instead of running on the last output residual
-        if (p.x && !p.lt_only) embed_row(p, b, p.codes_prev + b * NCB, p.pos[b]);
+    // a finished slot keeps running with the batch: it gets its frozen input again
+    // (codes_prev / pos no longer advance), so every later iteration recomputes the
+    // values of the one that ended it (the hidden-state trace row at the frozen step
+    // included) instead of running on the last output residual
+    const bool done = p.done[b] != 0;
+    const bool embed = p.x != nullptr && !p.lt_only;
+    const int e = tid - 64;  // waves 1-3: float4 e of the row
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), pe = s;
+    if (embed && w >= 1) {
+        const int *cs = (done ? p.codes_prev : p.codes_cur) + b * NCB;
+        int ps = done ? p.pos[b] : p.pos[b] + 1;
+        ps = ps < p.pos_rows ? ps : p.pos_rows - 1;  // a slot that stops this frame reads a row it never uses
+        const int ncb = done ? NCB : NCB - 1;
+        s = *(const float4 *)(p.emb + (size_t)cs[0] * D + 4 * e);
+#pragma unroll
+        for (int cb = 1; cb < NCB; ++cb) {
+            if (cb >= ncb) break;
+            const float4 r = *(const float4 *)(p.emb + ((size_t)cb * VCB + cs[cb]) * D + 4 * e);
+            s.x = s.x + r.x; s.y = s.y + r.y; s.z = s.z + r.z; s.w = s.w + r.w;
+        }
+        pe = *(const float4 *)(p.pos_emb + (size_t)ps * D + 4 * e);
+    }
+    __shared__ int sh_adv, sh_code;
+    __syncthreads();  // every read of pos / codes above precedes wave 0's updates
+    if (done) {
+        if (embed && w >= 1)
+            *(float4 *)(p.x + (size_t)b * D + 4 * e) = make_float4(s.x * 0.125f + pe.x, s.y * 0.125f + pe.y,
+                                                                   s.z * 0.125f + pe.z, s.w * 0.125f + pe.w);
         return;
     }
-    __shared__ float scratch[2 * VCB];
-    int i0, amax;
-    {
-        const int stp = p.step[b];
-        i0 = wave_pick(p.logits + (size_t)b * VCB + ts_dep(t_start), p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp,
-                       NCB - 1, scratch, amax);
-    }
-    // lane 0 keeps the books; the wave then embeds the next frame of a slot that advances
-    int adv = 0, np = 0;
-    int cc[NCB] = {};
-    if (tid == 0) {
-        int *ccp = p.codes_cur + b * NCB;
-        ccp[NCB - 1] = i0;
+    if (w == 0) {
+        // codebook 7's pick with the same wave_pick as every other codebook (masked
+        // first-max argmax; top-k draw when sampling); lane 0 keeps the books
+        __shared__ float scratch[2 * VCB];
+        int i0, amax;
+        {
+            const int stp = p.step[b];
+            i0 = wave_pick(p.logits + (size_t)b * VCB + ts_dep(t_start), p.ignore_eos || stp < 4, p.audio_bos,
+                           p.audio_eos, p.smp, b, stp, NCB - 1, scratch, amax);
+        }
+        if (tid == 0) {
+            int adv = 0;
+            int cc[NCB];
+            int *ccp = p.codes_cur + b * NCB;
+            ccp[NCB - 1] = i0;
 #pragma unroll
-        for (int cb = 0; cb < NCB - 1; ++cb) cc[cb] = ccp[cb];
-        cc[NCB - 1] = i0;
-        if (p.smp.amax) p.smp.amax[b * NCB + NCB - 1] = amax;
-        // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
-        bool eos = amax == p.audio_eos;
-        eos |= p.smp.argeos[b] != 0;
-        p.smp.argeos[b] = 0;
-        if (!p.lt_only) {  // magpie_local_transformer_sample_all: codes only
-            for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
-            const int s = p.step[b];
-            if (eos) {
-                // graph_reuse drops the EOS frame (4349-4352); the streaming loop emits it (4800-4806)
-                if (p.emit_eos)
-                    for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
-                p.done[b] = 1;
-                p.nframes[b] = p.emit_eos ? s + 1 : s;
-                atomicAdd(p.ndone, 1);
-            } else {
-                for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + s) * NCB + cb] = cc[cb];
-                p.step[b] = s + 1;
-                if (s + 1 >= p.max_steps) {
+            for (int cb = 0; cb < NCB - 1; ++cb) cc[cb] = ccp[cb];
+            cc[NCB - 1] = i0;
+            if (p.smp.amax) p.smp.amax[b * NCB + NCB - 1] = amax;
+            // EOS if any codebook's sampled code or argmax is EOS (magpie.cpp:4340-4348)
+            bool eos = amax == p.audio_eos;
+            eos |= p.smp.argeos[b] != 0;
+            p.smp.argeos[b] = 0;
+            if (!p.lt_only) {  // magpie_local_transformer_sample_all: codes only
+                for (int cb = 0; cb < NCB; ++cb) eos |= cc[cb] == p.audio_eos;
+                const int st = p.step[b];
+                if (eos) {
+                    // graph_reuse drops the EOS frame (4349-4352); the streaming loop emits it (4800-4806)
+                    if (p.emit_eos)
+                        for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + st) * NCB + cb] = cc[cb];
                     p.done[b] = 1;
-                    p.nframes[b] = s + 1;
+                    p.nframes[b] = p.emit_eos ? st + 1 : st;
                     atomicAdd(p.ndone, 1);
                 } else {
-                    for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
-                    np = p.pos[b] + 1;
-                    p.pos[b] = np;
-                    adv = 1;
+                    for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + st) * NCB + cb] = cc[cb];
+                    p.step[b] = st + 1;
+                    if (st + 1 >= p.max_steps) {
+                        p.done[b] = 1;
+                        p.nframes[b] = st + 1;
+                        atomicAdd(p.ndone, 1);
+                    } else {
+                        for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
+                        p.pos[b] = p.pos[b] + 1;
+                        adv = 1;
+                    }
                 }
             }
+            sh_adv = adv;
+            sh_code = i0;
         }
     }
-    adv = __shfl(adv, 0, 64);
-    if (adv && p.x) {
-        np = __shfl(np, 0, 64);
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) cc[cb] = __shfl(cc[cb], 0, 64);
-        embed_row(p, b, cc, np);
+    __syncthreads();
+    if (sh_adv && embed && w >= 1) {
+        const float4 r = *(const float4 *)(p.emb + ((size_t)(NCB - 1) * VCB + sh_code) * D + 4 * e);
+        s.x = s.x + r.x; s.y = s.y + r.y; s.z = s.z + r.z; s.w = s.w + r.w;
+        *(float4 *)(p.x + (size_t)b * D + 4 * e) = make_float4(s.x * 0.125f + pe.x, s.y * 0.125f + pe.y,
+                                                               s.z * 0.125f + pe.z, s.w * 0.125f + pe.w);
     }
     ts_end(p.ts, t_start);
 }
@@ -404,7 +420,7 @@ hipError_t op_embed(const EmbP &p, int NB, hipStream_t s) {
 // FFN up + GELU + FFN down of the local transformer in one launch
 // (magpie.cpp:983-992): workgroup p owns hidden units j in [16p, 16p+16). Its
 // weights (16 rows of W1, the 16-column slice of W2 that row n = thread n
-// reads) are issued first; every slot's LN(y) row is built by one wave (DPP
+// reads, one contiguous 16 KiB block of the slice-major copy) are issued first; every slot's LN(y) row is built by one wave (DPP
 // statistics, the same code at every batch size), a wave computes 4 units per
 // slot (float4 lanes, DPP sum, GELU) into LDS, then thread n adds its 16 units'
 // contributions to output n in ascending order. The LT_FFN_P partial sums are
@@ -420,7 +436,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_ffn_kernel(LtFfnP p) {
 #pragma unroll
     for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
 #pragma unroll
-    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.w2 + (size_t)tid * LTF + j0 + 4 * i);
+    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.w2 + (size_t)j0 * LTD + tid * U + 4 * i);
     for (int b = w; b < NB; b += MP_NWAVES) {
         float x[LTD / 64];
 #pragma unroll
@@ -563,7 +579,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
 #pragma unroll
     for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
 #pragma unroll
-    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.f.w2 + (size_t)tid * LTF + j0 + 4 * i);
+    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i);
     for (int b = w; b < NB; b += MP_NWAVES) {
         const float4 y = lt_y_slot(p, b, blockIdx.x == 0, wsc_all[w]);
         if (blockIdx.x == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
@@ -631,7 +647,8 @@ hipError_t op_lt_kvo(const GemvP &p, int NB, hipStream_t s) {
 
 hipError_t op_finalize(const FinP &p, int B, hipStream_t s) {
     if (!p.smp.cfg || !p.smp.argeos) return hipErrorInvalidValue;
-    mp::launch(lt_finalize_kernel, dim3(B), dim3(64), 0, s, p);
+    if (p.x && (!p.emb || !p.pos_emb || p.pos_rows < 1)) return hipErrorInvalidValue;
+    mp::launch(lt_finalize_kernel, dim3(B), dim3(FIN_THREADS), 0, s, p);
     return hipGetLastError();
 }
 

@@ -91,7 +91,7 @@ struct LtFfnP {
     const float *y;      // [B][256] LT residual stream after attention (ltY)
     const float *lnw;    // norm_pos_ff weight
     const float *w1;     // [1024][256] FFN up
-    const float *w2;     // [256][1024] FFN down
+    const float *w2;     // FFN down [256][1024] re-laid slice-major [LT_FFN_P][256][1024 / LT_FFN_P]
     float eps;
     float *part;         // [B][LT_FFN_P][256]
     float *out;          // lt_merge_kernel: [B][256] = ltY + merged FFN down
@@ -280,6 +280,7 @@ struct FinP {
     // x[b] = (sum over codebooks of emb[cb][code]) / 8 + pos_emb[new pos] (null: not written)
     const float *emb, *pos_emb;
     float *x;
+    int pos_rows;   // rows of pos_emb (the speculative read of the next position is clamped to it)
 };
 
 

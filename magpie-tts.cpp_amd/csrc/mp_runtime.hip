@@ -198,6 +198,11 @@ struct Model {
     // f32 weight mode (lt_ffn2_kernel): [7][2024][256] = o_net(v third of lt_qkvtab), and
     // [512][256] = [W_k ; W_o W_v] for position 0 (W_o W_v formed in double on the host)
     float *lt_votab = nullptr, *lt_kvo = nullptr;
+    // the LT FFN-down weights [256][1024] re-laid slice-major [LT_FFN_P][256][16]: the FFN
+    // workgroup that owns hidden units [16p, 16p+16) reads one contiguous 16 KiB block
+    // instead of 256 half cache lines (whose other halves sit with workgroup p +- 1 on
+    // another XCD: every line was fetched twice)
+    float *lt_ff2s = nullptr;
     std::vector<float *> xq_t;  // per layer W_q^T [768][128] (for K' = K W_q)
     // weight mode MP_WEIGHTS_BF16: decode projections repacked as bf16 MFMA fragments
     int weight_mode = 0;
@@ -616,6 +621,16 @@ int build_ptab(mp_dev *dev, int weight_mode) {
     if (wq) hipFree(wq);
     HIPCHK(ge);
     HIPCHK(se);
+    if (!m.lt_ff2s) {
+        constexpr int U = 1024 / mp::LT_FFN_P;
+        std::vector<float> w2((size_t)256 * 1024), w2s(w2.size());
+        HIPCHK(hipMemcpy(w2.data(), m.lt_ff2, w2.size() * 4, hipMemcpyDeviceToHost));
+        for (int p = 0; p < mp::LT_FFN_P; ++p)
+            for (int n = 0; n < 256; ++n)
+                memcpy(&w2s[((size_t)p * 256 + n) * U], &w2[(size_t)n * 1024 + p * U], U * 4);
+        HIPCHK(hipMalloc(&m.lt_ff2s, w2s.size() * 4));
+        HIPCHK(hipMemcpy(m.lt_ff2s, w2s.data(), w2s.size() * 4, hipMemcpyHostToDevice));
+    }
     return f32_lt_mode(m) ? build_vo_tables(dev) : MP_OK;
 }
 
@@ -1119,7 +1134,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         dump_lt(io, s);
         for (int cb = 0; cb < 8; ++cb) {
             mp::LtFfn2P l2{};
-            l2.f = mp::LtFfnP{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2, m.eps, io.ltp, io.lty2};
+            l2.f = mp::LtFfnP{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2s, m.eps, io.ltp, io.lty2};
             l2.cb = cb; l2.ltX = io.ltX; l2.ltk = io.ltk; l2.ltv = io.ltv; l2.qkvtab = m.lt_qkvtab;
             l2.votab = m.lt_votab; l2.ptab = m.lt_ptab; l2.lt_pos = m.lt_pos; l2.logits = io.logits;
             l2.codes_cur = io.codes_cur; l2.step = io.step; l2.ignore_eos = io.ignore_eos;
@@ -1214,7 +1229,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         // the head's prologue at batch 1 or by a one-workgroup merge; bf16 mode: two GEMVs
         const bool ffn1 = !b16;
         if (ffn1) {
-            mp::LtFfnP lf{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2, m.eps, io.ltp, io.lty2};
+            mp::LtFfnP lf{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2s, m.eps, io.ltp, io.lty2};
             if (ops) {
                 mp::OpRec r{};
                 r.name = "lt_ffn"; r.kind = mp::K_LTFFN; r.lf = lf; r.B = NB;
@@ -1262,7 +1277,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                io.max_steps, io.ignore_eos, m.audio_bos, m.audio_eos, NB,
                mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax}, io.emit_eos, io.lt_only,
                io.lt_only ? nullptr : io.ndone + 1};
-    if (!io.lt_only) { f.emb = m.audio_emb; f.pos_emb = m.dec_pos; f.x = io.x; }  // the next frame's input
+    if (!io.lt_only) { f.emb = m.audio_emb; f.pos_emb = m.dec_pos; f.x = io.x; f.pos_rows = m.dec_pos_rows; }  // the next frame's input
     if (ops) {
         mp::OpRec r{};
         r.name = "finalize"; r.kind = mp::K_FIN; r.f = f; r.B = NB; r.bytes = A * act * 2024;
@@ -1507,6 +1522,7 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.lt_qkvtab) hipFree(dev->m.lt_qkvtab);
     if (dev->m.lt_votab) hipFree(dev->m.lt_votab);
     if (dev->m.lt_kvo) hipFree(dev->m.lt_kvo);
+    if (dev->m.lt_ff2s) hipFree(dev->m.lt_ff2s);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
     if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
     if (dev->m.q8p_arena) hipFree(dev->m.q8p_arena);

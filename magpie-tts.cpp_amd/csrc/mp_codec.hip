@@ -427,6 +427,199 @@ __global__ __launch_bounds__(64 * RWV * CWV, DEEP ? 1 : 2) void conv2_kernel(Con
     }
 }
 
+// ---------------------------------------------------------------- fused residual block
+// One HiFiGAN residual block of one branch (nano-codec.cpp:568-599) in one launch,
+// for the small-channel stages (128 / 64 / 32 padded channels, where the f32 residual
+// stream and the f16 operands between the two convs were the traffic):
+//   x' = x + conv_{KS,1}(HS_sk(conv_{KS,d}(HS_in(x)))).
+// A workgroup owns output steps [t0, t0 + BN) of one chunk and every channel:
+//  A. the x rows [t0 - 16 - (KS-1)d, t0 - 16 + 64 CWV) are read once (f32), HalfSnake'd
+//     with the in_act alphas and rounded to f16 (ggml's F16 im2col) into LDS
+//     [channel block][row][32 halves + 16 B pad];
+//  B. conv_d over the 64 CWV columns [t0 - 16, t0 - 16 + 64 CWV): each wave owns 32
+//     channels x 64 steps (conv2's wave tile, A fragments through a register ring);
+//  C. bias + sk HalfSnake + f16 into LDS over the dead x rows (steps < 0 are zero:
+//     conv_1's causal padding);
+//  D. conv_1 (dilation 1) over [t0, t0 + BN), BN = 64 CWV - 16, then bias + x -> x'.
+// The intermediate never leaves the CU; x is read once per block (not as an f32
+// residual plus an f16 operand) and no f16 operand is written. Operand values,
+// fragments and accumulation order (channel block, tap ascending) are conv2's: the
+// same bits.
+struct RbP {
+    const float *x[3];              // residual stream in, [chunk][T][CP] f32 (block 0: the convT output)
+    float *out[3];                  // residual stream out: another buffer (the next tile reads x's halo)
+    const _Float16 *Wd[3], *W1[3];  // conv_d / conv_1 weights in A-fragment order (Conv::wf)
+    const float *bd[3], *b1[3];     // biases, zero padded to CP
+    const float *al_in[3], *al_sk[3];  // HalfSnake alphas, zero padded to CP
+    int ks[3];
+    int nsnake, creal, T, dil, tiles_per_chunk;
+};
+constexpr int RB_ROWB = 80;   // LDS bytes per time row of a 32-channel block
+constexpr int RB_MAXHALO = 50;  // (11 - 1) * 5
+
+template <int RWV, int CWV>
+constexpr int rb_lds_bytes() { return RWV * (64 * CWV + RB_MAXHALO) * RB_ROWB; }
+
+template <int KS, int RWV, int CWV, int R>
+__device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
+    constexpr int NCB = RWV, CPD = NCB * 32;  // one wave row per 32-channel block
+    constexpr int NTH = 64 * RWV * CWV;
+    constexpr int NCD = 64 * CWV;             // conv_d columns
+    constexpr int BN = NCD - 16;              // outputs per workgroup
+    constexpr int XR = NCD + RB_MAXHALO;      // LDS rows per channel block
+    constexpr int NS = NCB * KS;              // A-stream steps (channel block, tap)
+    const int br = blockIdx.y;
+    const int d = p.dil, halo = (KS - 1) * d;
+    const int chunk = blockIdx.x / p.tiles_per_chunk;
+    const int t0 = (blockIdx.x % p.tiles_per_chunk) * BN;
+    const int tx0 = t0 - 16 - halo;           // time of x row 0 (conv_d column 0 is t0 - 16)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rw = w % RWV, cw = w / RWV;
+    const int kg = lane >> 4, l16 = lane & 15;
+    const size_t cbase = (size_t)chunk * p.T * CPD;
+
+    // ---- A: x rows -> HS_in -> f16 -> LDS (each thread keeps one 8-channel piece)
+    {
+        constexpr int PPR = NCB * 4, RSTEP = NTH / PPR, NU = (XR + RSTEP - 1) / RSTEP;
+        static_assert(NTH % PPR == 0, "fixed piece per thread");
+        const int pc = tid % PPR, c0 = pc * 8, r0 = tid / PPR;
+        float al[8];
+        {
+            const float4 a0 = *(const float4 *)(p.al_in[br] + c0), a1 = *(const float4 *)(p.al_in[br] + c0 + 4);
+            al[0] = a0.x; al[1] = a0.y; al[2] = a0.z; al[3] = a0.w;
+            al[4] = a1.x; al[5] = a1.y; al[6] = a1.z; al[7] = a1.w;
+        }
+        const int rows = NCD + halo;
+        const float *src = p.x[br] + cbase + c0;
+        float4 v[NU][2];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int r = r0 + u * RSTEP, t = tx0 + r;
+            v[u][0] = v[u][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < rows && t >= 0 && t < p.T) {
+                v[u][0] = *(const float4 *)(src + (size_t)t * CPD);
+                v[u][1] = *(const float4 *)(src + (size_t)t * CPD + 4);
+            }
+        }
+        char *dst = xs + (pc >> 2) * XR * RB_ROWB + 16 * (pc & 3);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int r = r0 + u * RSTEP, t = tx0 + r;
+            if (r >= rows) break;
+            const float vv[8] = {v[u][0].x, v[u][0].y, v[u][0].z, v[u][0].w, v[u][1].x, v[u][1].y, v[u][1].z, v[u][1].w};
+            half8 h;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) h[i] = (_Float16)half_snake_sel(vv[i], c0 + i, p.nsnake, p.creal, al[i]);
+            if (t < 0 || t >= p.T) h = half8{0, 0, 0, 0, 0, 0, 0, 0};  // causal zero padding / past the chunk
+            *(half8 *)(dst + r * RB_ROWB) = h;
+        }
+    }
+    __syncthreads();
+
+    // ---- B / D: one causal conv from the LDS operand (rows: column c, tap k -> row
+    // c * 1 + rowoff + k * dk), A stream from `wf` (conv2's ring), NT column tiles
+    floatx4 acc[C2_WR][C2_NT];
+    half8 ring[R][C2_WR];
+    const int colb = cw * 64 + l16;
+    auto conv = [&](const _Float16 *wf, int rowoff, int dk, int nt) {
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+            for (int j = 0; j < C2_NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        const _Float16 *wrow0 = wf + (size_t)(rw * 2) * NS * 512 + lane * 8, *wrow1 = wrow0 + (size_t)NS * 512;
+#pragma unroll
+        for (int q = 0; q < R; ++q)
+            if (q < NS) {
+                ring[q][0] = *(const half8 *)(wrow0 + (size_t)q * 512);
+                ring[q][1] = *(const half8 *)(wrow1 + (size_t)q * 512);
+            }
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+            const char *bbase = xs + cb * XR * RB_ROWB + (colb + rowoff) * RB_ROWB + 16 * kg;
+            half8 bc[C2_NT], bn[C2_NT];
+#pragma unroll
+            for (int j = 0; j < C2_NT; ++j) bc[j] = *(const half8 *)(bbase + j * 16 * RB_ROWB);
+#pragma unroll
+            for (int k = 0; k < KS; ++k) {
+                const int st = cb * KS + k;
+                if (k + 1 < KS) {
+#pragma unroll
+                    for (int j = 0; j < C2_NT; ++j) bn[j] = *(const half8 *)(bbase + (j * 16 + (k + 1) * dk) * RB_ROWB);
+                }
+#pragma unroll
+                for (int j = 0; j < C2_NT; ++j) {
+                    if (j < nt) {
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][0], bc[j], acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][1], bc[j], acc[1][j], 0, 0, 0);
+                    }
+                }
+                if (st + R < NS) {
+                    ring[st % R][0] = *(const half8 *)(wrow0 + (size_t)(st + R) * 512);
+                    ring[st % R][1] = *(const half8 *)(wrow1 + (size_t)(st + R) * 512);
+                }
+                if (k + 1 < KS) {
+#pragma unroll
+                    for (int j = 0; j < C2_NT; ++j) bc[j] = bn[j];
+                }
+            }
+        }
+    };
+    // B: conv_d, column c = time t0 - 16 + c, x row c + k d
+    conv(p.Wd[br], 0, d, C2_NT);
+    // each lane's 8 channels: rw * 32 + a * 16 + 4 kg + r
+    const int chl = rw * 32 + 4 * kg;
+    __syncthreads();  // every wave is done reading x rows
+    // ---- C: h = f16(HS_sk(conv_d + b)) into LDS rows 0 .. NCD-1 (row c = time t0 - 16 + c)
+    {
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a) {
+            const int ch = chl + a * 16;
+            const float4 bb = *(const float4 *)(p.bd[br] + ch), al = *(const float4 *)(p.al_sk[br] + ch);
+            const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, av[4] = {al.x, al.y, al.z, al.w};
+#pragma unroll
+            for (int j = 0; j < C2_NT; ++j) {
+                const int c = cw * 64 + j * 16 + l16, t = t0 - 16 + c;
+                half4 h;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) h[r] = (_Float16)half_snake_sel(acc[a][j][r] + bv[r], ch + r, p.nsnake, p.creal, av[r]);
+                if (t < 0) h = half4{0, 0, 0, 0};
+                *(half4 *)(xs + rw * XR * RB_ROWB + c * RB_ROWB + (a * 16 + 4 * kg) * 2) = h;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- D: conv_1, output column o = time t0 + o, h row o + 16 - (KS - 1) + k
+    const int nt = cw == CWV - 1 ? C2_NT - 1 : C2_NT;  // BN = 64 CWV - 16 outputs
+    conv(p.W1[br], 16 - (KS - 1), 1, nt);
+    // ---- E: + bias + x -> x'
+#pragma unroll
+    for (int a = 0; a < C2_WR; ++a) {
+        const int ch = chl + a * 16;
+        const float4 bb = *(const float4 *)(p.b1[br] + ch);
+#pragma unroll
+        for (int j = 0; j < C2_NT; ++j) {
+            const int t = t0 + cw * 64 + j * 16 + l16;
+            if (j >= nt || t >= p.T) continue;
+            const size_t off = cbase + (size_t)t * CPD + ch;
+            const float4 r = *(const float4 *)(p.x[br] + off);
+            const floatx4 y = acc[a][j];
+            const float4 v = make_float4(y[0] + bb.x, y[1] + bb.y, y[2] + bb.z, y[3] + bb.w);
+            *(float4 *)(p.out[br] + off) = make_float4(r.x + v.x, r.y + v.y, r.z + v.z, r.w + v.w);  // input + h
+        }
+    }
+}
+
+template <int RWV, int CWV>
+__global__ __launch_bounds__(64 * RWV * CWV, 2) void rb_kernel(RbP p) {
+    __shared__ __attribute__((aligned(16))) char xs[rb_lds_bytes<RWV, CWV>()];
+    switch (p.ks[blockIdx.y]) {
+        case 3: rb_body<3, RWV, CWV, 3>(p, xs); break;
+        case 7: rb_body<7, RWV, CWV, 3>(p, xs); break;
+        default: rb_body<11, RWV, CWV, 3>(p, xs); break;
+    }
+}
+
 // Grouped ConvTranspose1d (nano-codec.cpp:481-565), HalfSnake on its input,
 // optional 3-branch mean before it: out[t][g] = b[g] + sum_{c in {2g,2g+1}}
 // sum_{tau: 0 <= t - tau*s < 2s} x[tau][c] * w[c][t - tau*s]; kept length T*s.
@@ -498,7 +691,9 @@ __global__ __launch_bounds__(256) void conv_transpose_kernel(ConvTP p) {
 // registers), its 4 x 2s weights and all alphas stay in registers, outputs go out as
 // float2 (f32) and half2 (block-major f16 operands). Same arithmetic and summation
 // order as conv_transpose_kernel.
-template <int CINP, int COUTP, int S, bool AVG, int R>
+// ACT: also emit the 3 branches' k=0 in_conv operands (the stages whose residual
+// blocks are fused compute them from the f32 output instead).
+template <int CINP, int COUTP, int S, bool AVG, int R, bool ACT = true>
 __global__ __launch_bounds__(256) void conv_transpose2_kernel(ConvTP p) {
     constexpr int NG = COUTP / 2, K = 2 * S;
     const int e = blockIdx.x * 256 + threadIdx.x;
@@ -573,6 +768,7 @@ __global__ __launch_bounds__(256) void conv_transpose2_kernel(ConvTP p) {
             if (live0) a0 += bias0;
             if (live1) a1 += bias1;
             *(float2 *)(p.out + cout_base + (size_t)t * COUTP + g) = make_float2(a0, a1);
+            if constexpr (!ACT) continue;
             typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -645,6 +841,7 @@ struct mp_codec {
     // activations (grown on demand)
     size_t cap_elems = 0;
     float *x_pre = nullptr, *x0 = nullptr, *brb[3] = {}, *audio = nullptr;
+    float *rbt[3] = {};  // fused residual blocks: block 1's output (block 2 reads its halo)
     _Float16 *a16[3] = {}, *b16[3] = {};  // f16 conv operands: in_conv (HS_in x), sk_conv (HS_sk h)
     int *codes = nullptr;
     size_t codes_cap = 0, audio_cap = 0;
@@ -760,7 +957,7 @@ int ensure_buffers(mp_codec *c, int nchunk, int F) {
     }
     need = std::max(need, (size_t)nchunk * F * CP_PRE);
     if (need > c->cap_elems) {
-        float **bufs[5] = {&c->x_pre, &c->x0, &c->brb[0], &c->brb[1], &c->brb[2]};
+        float **bufs[8] = {&c->x_pre, &c->x0, &c->brb[0], &c->brb[1], &c->brb[2], &c->rbt[0], &c->rbt[1], &c->rbt[2]};
         for (auto b : bufs) if (*b) { hipFree(*b); *b = nullptr; }
         for (auto b : bufs) CHK(hipMalloc((void **)b, need * 4 + 256));
         _Float16 **hb[6] = {&c->a16[0], &c->a16[1], &c->a16[2], &c->b16[0], &c->b16[1], &c->b16[2]};
@@ -801,6 +998,27 @@ hipError_t launch_conv2(mpc::ConvP p, int nchunk, int nbranch, hipStream_t s) {
     dim3 grid(p.Coutp / (RWV * 32), nchunk * p.tiles_per_chunk, nbranch);
     hipLaunchKernelGGL((mpc::conv2_kernel<RWV, CWV, NCB, DEEP>), grid, dim3(64 * RWV * CWV), 0, s, p);
     return hipGetLastError();
+}
+
+template <int RWV, int CWV>
+hipError_t launch_rb(mpc::RbP p, int nchunk, hipStream_t s) {
+    constexpr int BN = 64 * CWV - 16;
+    p.tiles_per_chunk = (p.T + BN - 1) / BN;
+    hipLaunchKernelGGL((mpc::rb_kernel<RWV, CWV>), dim3(nchunk * p.tiles_per_chunk, 3), dim3(64 * RWV * CWV), 0, s, p);
+    return hipGetLastError();
+}
+// the fused residual block for a stage's padded channel count (0: not fused)
+bool rb_fused(int Cp) {
+    const bool off = getenv("MAGPIE_CODEC_UNFUSED") != nullptr;  // A/B switch (read per decode): the two-launch blocks
+    return !off && (Cp == 128 || Cp == 64 || Cp == 32);
+}
+hipError_t run_rb(const mpc::RbP &p, int Cp, int nchunk, hipStream_t s) {
+    switch (Cp) {
+        case 128: return launch_rb<4, 2>(p, nchunk, s);
+        case 64: return launch_rb<2, 4>(p, nchunk, s);
+        case 32: return launch_rb<1, 8>(p, nchunk, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t run_conv(const mpc::ConvP &p, int BM, int mode, int nchunk, int nbranch, hipStream_t s) {
@@ -851,15 +1069,43 @@ int codec_run(mp_codec *c, int nchunk, int F) {
         // R input steps per thread: 1 on the short early stages (threads), 4 later (re-reads)
         const int R = i == 0 ? 1 : i == 1 ? 2 : 4;
         const dim3 g2((nchunk * ((T + R - 1) / R) * (Cp / 2) + 255) / 256);
+        const bool fused = rb_fused(Cp);
         switch (i) {
             case 0: hipLaunchKernelGGL((conv_transpose2_kernel<896, 448, 8, false, 1>), g2, dim3(256), 0, s, tp); break;
             case 1: hipLaunchKernelGGL((conv_transpose2_kernel<448, 224, 8, true, 2>), g2, dim3(256), 0, s, tp); break;
-            case 2: hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4>), g2, dim3(256), 0, s, tp); break;
-            case 3: hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, 4>), g2, dim3(256), 0, s, tp); break;
-            default: hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, 4>), g2, dim3(256), 0, s, tp); break;
+            case 2:
+                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4, false>), g2, dim3(256), 0, s, tp);
+                else hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4>), g2, dim3(256), 0, s, tp);
+                break;
+            case 3:
+                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, 4, false>), g2, dim3(256), 0, s, tp);
+                else hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, 4>), g2, dim3(256), 0, s, tp);
+                break;
+            default:
+                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, 4, false>), g2, dim3(256), 0, s, tp);
+                else hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, 4>), g2, dim3(256), 0, s, tp);
+                break;
         }
         CHK(hipGetLastError());
         T *= RATE[i];
+        if (fused) {
+            // x0 -> brb (block 0) -> rbt (block 1) -> brb (block 2): out of place, since a
+            // tile reads its left neighbour's rows as halo
+            for (int k = 0; k < 3; ++k) {
+                RbP rp{};
+                for (int j = 0; j < 3; ++j) {
+                    const mp_codec::Conv &cd = c->rb[i][j][k][0], &c1 = c->rb[i][j][k][1];
+                    rp.x[j] = k == 0 ? c->x0 : k == 1 ? c->brb[j] : c->rbt[j];
+                    rp.out[j] = k == 1 ? c->rbt[j] : c->brb[j];
+                    rp.Wd[j] = cd.wf; rp.W1[j] = c1.wf; rp.bd[j] = cd.b; rp.b1[j] = c1.b;
+                    rp.al_in[j] = c->rb_alpha[i][j][k][0]; rp.al_sk[j] = c->rb_alpha[i][j][k][1];
+                    rp.ks[j] = KS[j];
+                }
+                rp.nsnake = C / 2; rp.creal = C; rp.T = T; rp.dil = DIL[k];
+                CHK(run_rb(rp, Cp, nchunk, s));
+            }
+            continue;
+        }
         const int BM = BMS[i], BN = BM == 64 ? 64 : 128;
         for (int k = 0; k < 3; ++k) {
             // h = conv_{ks_j, d_k}(HS_in(x)) for the 3 branches j; only HS_sk(h) (f16) is kept

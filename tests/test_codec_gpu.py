@@ -68,3 +68,15 @@ def test_chunked_equals_independent(gpu_codec, n, F):
 def test_codec_deterministic(gpu_codec):
     codes = np.random.default_rng(11).integers(0, 2016, (8, 12)).astype(np.int32)
     np.testing.assert_array_equal(gpu_codec.decode(codes), gpu_codec.decode(codes))
+
+
+@pytest.mark.parametrize("F", [1, 4, 32])
+def test_fused_blocks_equal_two_launch_blocks(gpu_codec, monkeypatch, F):
+    """The fused residual block (rb_kernel: conv_d -> HS_sk -> conv_1 + residual in one
+    launch, 128/64/32-channel stages) computes the same bits as the two-launch form
+    (MAGPIE_CODEC_UNFUSED=1): same f16 operands, fragments and accumulation order."""
+    codes = np.random.default_rng(40 + F).integers(0, 2016, (2, 8, F)).astype(np.int32)
+    fused = gpu_codec.decode_chunks(codes)
+    monkeypatch.setenv("MAGPIE_CODEC_UNFUSED", "1")
+    unfused = gpu_codec.decode_chunks(codes)
+    np.testing.assert_array_equal(fused, unfused)

@@ -4,7 +4,8 @@ batch to mid-utterance, then time whole eager iterations op by op
 wave spans (mp_hip_profile_ops_ts), plus the graph-replayed frames/s.
 
 usage: python tools_dev/mode_ops.py WEIGHTS B [model] [ENV=VAL ...]
-  WEIGHTS: f32 | bf16 | q8 | q4 | f16;  model: f32 (default) | q8 | q4 | f16 file"""
+  WEIGHTS: f32 | bf16 | q8 | q4 | f16;  model: f32 (default) | q8 | q4 | f16 file
+  MODE_XA=auto|reassoc|direct, MODE_KV=f32|bf16: the Device's cross-attention form / SA cache type"""
 import os
 import sys
 
@@ -26,7 +27,7 @@ files = {"f32": ("magpie_357m_f32_k32.gguf", "f32"), "q8": ("magpie_357m_q8_k32.
          "q4": ("magpie_357m_q4_k32.gguf", "q4_0"), "f16": ("magpie_357m_f16_k32.gguf", "f16")}
 fn, dt = files[kind]
 path = ma.synth_gguf(os.path.join(C, fn), dtype=dt, lt_head_scale=ma.DECISIVE)
-dev = ma.Device(path, weights=weights)
+dev = ma.Device(path, weights=weights, xa=os.environ.get("MODE_XA", "auto"), kv=os.environ.get("MODE_KV", "f32"))
 toks = [ma.synthetic_tokens(64, seed=1000 + b) for b in range(B)]
 frames = 256
 dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=frames, ignore_eos=True)

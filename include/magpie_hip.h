@@ -76,10 +76,12 @@ int mp_hip_init(int device, mp_dev **out);
 int mp_hip_load_model(mp_dev *dev, const char *gguf_path);
 /* Weight modes of mp_hip_load_model_ex. AS_STORED streams the GGUF's weights
  * as f32 (F16/BF16/Q8_0 tensors are widened at load). BF16 additionally repacks
- * the decode-step projections (decoder qkv/o/ff1/ff2, LT layer, LT heads) into
- * bf16 MFMA fragments: half the bytes per frame, activations rounded to bf16
- * like ggml's BF16 mul_mat; batches up to 16 (BASELINE configs 3-4). The
- * preamble and cross-attention stay f32. No reference counterpart (the
+ * the decode-step projections (decoder qkv/o/ff1/ff2, LT FFN, LT heads) into
+ * bf16 (MFMA fragments for the decoder and heads): half the bytes per frame,
+ * activations rounded to bf16 like ggml's BF16 mul_mat; batches up to 16
+ * (BASELINE configs 3-4). The preamble, cross-attention, LT in_proj and the LT
+ * layer's attention (through load-time f32 tables, as AS_STORED computes it)
+ * stay f32. No reference counterpart (the
  * reference converter writes F32/F16/Q8_0/Q4_0, convert_magpie_to_gguf.py:197-206). */
 #define MP_WEIGHTS_AS_STORED 0
 #define MP_WEIGHTS_BF16 1

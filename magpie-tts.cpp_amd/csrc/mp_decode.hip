@@ -132,6 +132,7 @@ template <bool KV16>
 __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     sa_part<KV16, SA_WAVES, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, nullptr, 0u, nullptr, ts_dep(t_start));
+    if (p.merged) sa_merge_last(p, blockIdx.x, blockIdx.z);
     ts_end(p.ts, t_start);
 }
 
@@ -632,6 +633,105 @@ hipError_t op_lt_ffn2(const LtFfn2P &p, int NB, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- LT step, bf16 weight mode
+// The bf16 mode's LT step of codebook cb, workgroup (q, b): slot b's y through
+// lt_y_slot (wave 0; the attention in f32 through the load-time q|k|vo tables, as
+// the f32 mode computes it), LN(y) rounded to bf16, then the FFN for hidden units
+// [32q, 32q + 32): up (bf16 W1 rows, f32 sums, GELU, rounded to bf16) and its share
+// of FFN down (bf16 W2 slice) as partial sums. The partials are published with
+// write-through stores; the slot's last workgroup to count in (cnt[b], monotonic:
+// the last of every LTS_P arrivals) merges them in q order, so the result does not
+// depend on who arrives last, and writes y2 = y + FFN(y) for the bf16 head.
+// LTS_P workgroups per slot at every batch size (16 KiB of W1 and of W2 each): no
+// slot's pick waits behind another's, and a batch reproduces its utterances run
+// alone. The weights are issued before the pick.
+constexpr int LTS_U = LTF / LTS_P, LTS_UPW = LTS_U / MP_NWAVES;
+__device__ __forceinline__ float bf16_round(float v) { return __uint_as_float((unsigned)f32_to_bf16_rne(v) << 16); }
+__device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+__global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
+    using gf32 = __attribute__((address_space(1))) float;
+    using gu32 = __attribute__((address_space(1))) unsigned;
+    const unsigned long long t_start = ts_begin(p.f.ts);
+    static_assert(LTD == MP_BLOCK && LTS_U % 8 == 0 && LTS_U % MP_NWAVES == 0, "unit split");
+    __shared__ __attribute__((aligned(16))) float xs[LTD];
+    __shared__ __attribute__((aligned(16))) float ys[LTD];
+    __shared__ __attribute__((aligned(16))) float hs[LTS_U];
+    __shared__ __attribute__((aligned(16))) float wsc[2 * VCB];
+    __shared__ int last;
+    const int q = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int u0 = q * LTS_U + ts_dep(t_start);
+    uint2 a1[LTS_UPW];  // W1 rows u0 + LTS_UPW w + r, elements 4 lane .. 4 lane + 3
+#pragma unroll
+    for (int r = 0; r < LTS_UPW; ++r) a1[r] = *(const uint2 *)(p.w1h + (size_t)(u0 + w * LTS_UPW + r) * LTD + 4 * lane);
+    uint4 a2[LTS_U / 8];  // W2 row tid, units u0 .. u0 + LTS_U - 1
+#pragma unroll
+    for (int i = 0; i < LTS_U / 8; ++i) a2[i] = *(const uint4 *)(p.w2h + ((size_t)q * LTD + tid) * LTS_U + 8 * i);
+    if (w == 0) {
+        const float4 y = lt_y_slot(p, b, q == 0, wsc);
+        if (q == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
+        *(float4 *)&ys[4 * lane] = y;
+        const float x[4] = {y.x, y.y, y.z, y.w};
+        float mean, var;
+        wave_meanvar<4>(x, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.f.eps);
+        const float4 g = *(const float4 *)(p.f.lnw + 4 * lane);
+        *(float4 *)&xs[4 * lane] =
+            make_float4(bf16_round(((x[0] - mean) * rstd) * g.x), bf16_round(((x[1] - mean) * rstd) * g.y),
+                        bf16_round(((x[2] - mean) * rstd) * g.z), bf16_round(((x[3] - mean) * rstd) * g.w));
+    }
+    lds_sync();
+    const float4 xv = *(const float4 *)&xs[4 * lane];
+#pragma unroll
+    for (int r = 0; r < LTS_UPW; ++r) {
+        const float4 wv = make_float4(bf16_lo(a1[r].x), bf16_hi(a1[r].x), bf16_lo(a1[r].y), bf16_hi(a1[r].y));
+        const float v = wave_sum(dotv(wv, xv));
+        if (lane == 0) hs[w * LTS_UPW + r] = bf16_round(gelu_tanh(v));
+    }
+    lds_sync();
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < LTS_U / 8; ++i) {
+        const float4 h0 = *(const float4 *)&hs[8 * i], h1 = *(const float4 *)&hs[8 * i + 4];
+        acc = fmaf(bf16_lo(a2[i].x), h0.x, acc);
+        acc = fmaf(bf16_hi(a2[i].x), h0.y, acc);
+        acc = fmaf(bf16_lo(a2[i].y), h0.z, acc);
+        acc = fmaf(bf16_hi(a2[i].y), h0.w, acc);
+        acc = fmaf(bf16_lo(a2[i].z), h1.x, acc);
+        acc = fmaf(bf16_hi(a2[i].z), h1.y, acc);
+        acc = fmaf(bf16_lo(a2[i].w), h1.z, acc);
+        acc = fmaf(bf16_hi(a2[i].w), h1.w, acc);
+    }
+    if (!p.cnt) {  // small batches: the head's prologue merges (PRO_LTS_MERGE)
+        p.f.part[((size_t)b * LTS_P + q) * LTD + tid] = acc;
+        ts_end(p.f.ts, t_start);
+        return;
+    }
+    gf32 *part = (gf32 *)p.f.part + (size_t)b * LTS_P * LTD;
+    __hip_atomic_store(part + (size_t)q * LTD + tid, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's partial has landed before the workgroup counts in
+    __syncthreads();
+    if (tid == 0)
+        last = __hip_atomic_fetch_add((gu32 *)p.cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % LTS_P ==
+               LTS_P - 1;
+    __syncthreads();
+    if (last) {
+        float s = __hip_atomic_load(part + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll 8
+        for (int k = 1; k < LTS_P; ++k) s += __hip_atomic_load(part + (size_t)k * LTD + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        p.f.out[(size_t)b * LTD + tid] = s + ys[tid];
+    }
+    ts_end(p.f.ts, t_start);
+}
+hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
+    if (!p.f.y || !p.f.lnw || !p.w1h || !p.w2h || !p.f.part || (p.cnt && !p.f.out) || !p.ltX || !p.ltk || !p.ltv ||
+        !p.qkvtab || !p.votab || !p.ptab || !p.lt_pos || !p.logits || !p.codes_cur || !p.step || !p.smp.cfg ||
+        !p.smp.argeos || p.cb < 0 || p.cb >= NCB || NB < 1 || NB > 16)
+        return hipErrorInvalidValue;
+    mp::launch(lt_slot_kernel, dim3(LTS_P, NB), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
 // the LT head at batch 1 with the FFN merge as its prologue
 hipError_t op_lt_em_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 2, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 // f32 LT position 0: LN(X_0) -> [k_0 | vo_0] (W = [W_k ; W_o W_v], 512 x 256)
@@ -641,6 +741,7 @@ hipError_t op_lt_kvo(const GemvP &p, int NB, hipStream_t s) {
     case 2: return launch_gemv<2, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
     case 4: return launch_gemv<4, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
     case 8: return launch_gemv<8, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
+    case 16: return launch_gemv<16, 1, LTD, PRO_LTX_LN, EPI_LTKVO>(p, s);
     }
     return hipErrorInvalidValue;
 }

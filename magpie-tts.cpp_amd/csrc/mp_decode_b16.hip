@@ -198,6 +198,7 @@ static bool b16_args_ok(const GemvP &p) {
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
     if constexpr (PRO == PRO_PLAIN_B16) ok &= p.src_b16 != nullptr;
     if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
+    if constexpr (PRO == PRO_LTS_MERGE) ok &= p.part && p.addsrc;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
@@ -244,7 +245,9 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     hipError_t b16_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
     hipError_t b16_lt_c_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LN, EPI_GELU>(p, s); }         \
     hipError_t b16_lt_d_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTF, PRO_PLAIN, EPI_ADD_STORE>(p, s); } \
-    hipError_t b16_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }
+    hipError_t b16_lt_e_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }      \
+    hipError_t b16_lt_es_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_PLAIN, EPI_BIAS>(p, s); }      \
+    hipError_t b16_lt_em_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTS_MERGE, EPI_BIAS>(p, s); }
 
 #define MP_F16_OPS(NB)                                                                                                  \
     hipError_t f16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV, true>(p, s); }             \
@@ -272,6 +275,9 @@ MP_F16_OPS(2)
 MP_F16_OPS(4)
 MP_F16_OPS(8)
 MP_F16_OPS(16)
+// bf16 mode at 16 slots: the O-projection + XA launch reads the SA output the SA
+// kernel's last-arriver merge wrote (plain rows), and its XA workgroups merge x2
+hipError_t b16_oproj_xa_pm_16(const GemvP &p, hipStream_t s) { return launch_b16<16, D, PRO_PLAIN, EPI_RESID_XA>(p, s); }
 // the LT in_proj of an F16 file is F16 too (the bf16 mode keeps it f32)
 hipError_t f16_lt_in0_1(const GemvP &p, hipStream_t s) { return launch_b16<1, D, PRO_LN, EPI_BIAS, true>(p, s); }
 hipError_t f16_lt_in0_2(const GemvP &p, hipStream_t s) { return launch_b16<2, D, PRO_LN, EPI_BIAS, true>(p, s); }

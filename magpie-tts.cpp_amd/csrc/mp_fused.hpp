@@ -202,6 +202,16 @@ __device__ __forceinline__ float lt_ffn_merge(const float *part, const float *y,
     return s + y[(size_t)b * LTD + k];
 }
 
+// The same for the LTS_P partial sums of lt_slot_kernel (bf16 weight mode); the slot's
+// last workgroup merges them with this arithmetic when the head does not
+__device__ __forceinline__ float lts_merge(const float *part, const float *y, int b, int k) {
+    const float *pp = part + (size_t)b * LTS_P * LTD + k;
+    float s = pp[0];
+#pragma unroll 8
+    for (int q = 1; q < LTS_P; ++q) s += pp[(size_t)q * LTD];
+    return s + y[(size_t)b * LTD + k];
+}
+
 // LayerNorm weights of this lane's elements lane + 64 i, loaded before the
 // prologue's first global store (a load behind a store that may alias it waits
 // for the store: one memory round trip per element otherwise)
@@ -227,26 +237,59 @@ constexpr int pro_scratch() {
 // M = max_s m_s, den = sum_s e_s l_s (an empty split has m = -inf, l = 0, O = 0);
 // sc[q*(NS+1) + s] = e_s, sc[q*(NS+1) + NS] = 1/den. The merged output is
 // (sum_s e_s O_s) * (1/den). Computed once per group, not per element.
+// x2 = merged XA output + x, unfused (shared by PRO_XA_LN and the XA tail's merge)
+__device__ __forceinline__ float4 xa_x2(float4 a, float4 x) {
+#pragma clang fp contract(off)
+    return make_float4(a.x + x.x, a.y + x.y, a.z + x.z, a.w + x.w);
+}
+
+// The arithmetic is spelled out (contraction off, explicit fmaf) and shared by the
+// merging prologues and the attention kernels' own last-arriver merges (16 slots),
+// so a state merged by either computes the same bits.
+template <int NS>
+__device__ __forceinline__ void split_weights(const float (&ms)[NS], const float (&ls)[NS], float (&e)[NS], float &rd) {
+#pragma clang fp contract(off)
+    float M = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) M = fmaxf(M, ms[s]);
+    float den = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        e[s] = ms[s] == -INFINITY ? 0.f : expf(ms[s] - M);
+        den = fmaf(e[s], ls[s], den);
+    }
+    rd = 1.0f / den;
+}
+// one merged output element: (sum_s e_s O_s) * rd
+template <int NS>
+__device__ __forceinline__ float split_merge(const float *e, const float (&o)[NS], float rd) {
+#pragma clang fp contract(off)
+    float num = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) num = fmaf(e[s], o[s], num);
+    return num * rd;
+}
+template <int NS>
+__device__ __forceinline__ float4 split_merge4(const float *e, const float4 (&o)[NS], float rd) {
+    float ox[NS], oy[NS], oz[NS], ow[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) { ox[s] = o[s].x; oy[s] = o[s].y; oz[s] = o[s].z; ow[s] = o[s].w; }
+    return make_float4(split_merge<NS>(e, ox, rd), split_merge<NS>(e, oy, rd), split_merge<NS>(e, oz, rd),
+                       split_merge<NS>(e, ow, rd));
+}
 template <int NS>
 __device__ __forceinline__ void merge_weights(const float *pp, int stride, int nq, float *sc) {
     for (int q = threadIdx.x; q < nq; q += MP_BLOCK) {
-        float ms[NS], ls[NS];
+        float ms[NS], ls[NS], e[NS], rd;
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             ms[s] = pp[((size_t)q * NS + s) * stride];
             ls[s] = pp[((size_t)q * NS + s) * stride + 1];
         }
-        float M = -INFINITY;
+        split_weights<NS>(ms, ls, e, rd);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) M = fmaxf(M, ms[s]);
-        float den = 0.f;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const float e = ms[s] == -INFINITY ? 0.f : expf(ms[s] - M);
-            sc[q * (NS + 1) + s] = e;
-            den += e * ls[s];
-        }
-        sc[q * (NS + 1) + NS] = 1.0f / den;
+        for (int s = 0; s < NS; ++s) sc[q * (NS + 1) + s] = e[s];
+        sc[q * (NS + 1) + NS] = rd;
     }
 }
 
@@ -282,14 +325,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 const int e = base + u * MP_BLOCK + tid;
                 if (e >= ITEMS) break;
                 const int b = e / (K / 4), k = (e % (K / 4)) * 4, q = b * NH + k / DH;
-                float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int s2 = 0; s2 < SA_SPLITS; ++s2) {
-                    const float w = sc[q * (SA_SPLITS + 1) + s2];
-                    num.x += w * o[u][s2].x; num.y += w * o[u][s2].y; num.z += w * o[u][s2].z; num.w += w * o[u][s2].w;
-                }
-                const float rd = sc[q * (SA_SPLITS + 1) + SA_SPLITS];
-                *(float4 *)(act + b * K + k) = make_float4(num.x * rd, num.y * rd, num.z * rd, num.w * rd);
+                *(float4 *)(act + b * K + k) =
+                    split_merge4<SA_SPLITS>(sc + q * (SA_SPLITS + 1), o[u], sc[q * (SA_SPLITS + 1) + SA_SPLITS]);
             }
         }
         lds_sync();
@@ -323,16 +360,8 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 const int e = base + u * MP_BLOCK + tid;
                 if (e >= ITEMS) break;
                 const int b = e / (K / 4), k = (e % (K / 4)) * 4;
-                float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int s2 = 0; s2 < XA_SPLITS; ++s2) {
-                    const float w = sc[b * (XA_SPLITS + 1) + s2];
-                    num.x += w * o[u][s2].x; num.y += w * o[u][s2].y; num.z += w * o[u][s2].z; num.w += w * o[u][s2].w;
-                }
-                const float rd = sc[b * (XA_SPLITS + 1) + XA_SPLITS];
-                const float4 x2 = make_float4(num.x * rd + xv[u].x, num.y * rd + xv[u].y, num.z * rd + xv[u].z,
-                                              num.w * rd + xv[u].w);
-                *(float4 *)(act + b * K + k) = x2;
+                const float4 a = split_merge4<XA_SPLITS>(sc + b * (XA_SPLITS + 1), o[u], sc[b * (XA_SPLITS + 1) + XA_SPLITS]);
+                *(float4 *)(act + b * K + k) = xa_x2(a, xv[u]);
             }
         }
         lds_sync();
@@ -383,6 +412,11 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         static_assert(K == LTD, "LT is 256 wide");
         for (int e = tid; e < NB * K; e += MP_BLOCK) act[e] = lt_ffn_merge(p.part, p.addsrc, e / K, e % K);
         lds_sync();
+    } else if constexpr (PRO == PRO_LTS_MERGE) {
+        static_assert(K == LTD, "LT is 256 wide");
+        for (int e = tid; e < NB * K; e += MP_BLOCK) act[e] = lts_merge(p.part, p.addsrc, e / K, e % K);
+        lds_sync();
+
     } else if constexpr (PRO == PRO_PLAIN) {
         for (int b = 0; b < NB; ++b)
             for (int k = tid * 4; k < K; k += MP_BLOCK * 4)

@@ -26,6 +26,7 @@ constexpr int SA_PART = 4 + DH;     // per (slot, head, split): m, l, -, -, O[64
 constexpr int XA_SPLITS = 4;        // text-key splits of the fused cross-attention (xa_part_kernel)
 constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
 constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
+constexpr int LTS_P = 32;           // bf16 mode LT step (lt_slot_kernel): workgroups per slot = partial FFN-down sums
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
 enum Pro {
@@ -45,6 +46,7 @@ enum Pro {
     PRO_PLAIN_B16 = 11, // bf16 kernels only: act = src_b16 (rows already bf16, EPI_GELU_B16 output)
     PRO_LTFFN_MERGE = 12, // act = (sum over p of the LT_FFN_P partial FFN-down sums, p ascending)
                           //       + addsrc: the LT FFN output (lt_ffn_kernel, 983-992)
+    PRO_LTS_MERGE = 13,   // the same over the LTS_P partial sums of lt_slot_kernel (bf16 mode, small batches)
 };
 enum Epi {
     EPI_STORE = 0,      // out = v
@@ -118,6 +120,12 @@ struct LtFfn2P {
     const int *step;
     int ignore_eos, audio_bos, audio_eos;
     Sampling smp;
+    // bf16 weight mode (lt_slot_kernel): the FFN weights rounded to bf16, W1 row-major
+    // [1024][256], W2 slice-major [LTS_P][256][1024 / LTS_P]; partials f.part [B][LTS_P][256],
+    // merged by the slot's last workgroup (arrival counter cnt[b]) into f.out = y2, or (cnt
+    // null: small batches) by the head's prologue (PRO_LTS_MERGE)
+    const unsigned short *w1h, *w2h;
+    unsigned *cnt;
 };
 
 // Frame embedding of every slot (layer 0's residual input, magpie.cpp:2746-2787,
@@ -159,6 +167,11 @@ struct XaP {
     int Tmax, layer, nlayers;
     int q_f16;             // F16 weight mode: LN(x) rounded to f16, the q_net operand ggml multiplies
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
+    // x2 (nullable; the O-projection's XA tail at 16 slots): the split states published
+    // write-through and merged with x1 by each slot's last split workgroup (arrival
+    // counter cnt[b]) into x2[b][768] (FFN up then normalises plain rows)
+    float *x2;
+    unsigned *cnt;
 };
 
 // Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the
@@ -192,6 +205,11 @@ struct AttnP {  // decode self-attention (one query per utterance)
     float *part;         // [B][NH][SA_SPLITS][SA_PART] partial softmax states over key splits
                          // (merged in the O-projection's PRO_SA_MERGE prologue)
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
+    // merged (nullable; sa_attn_kernel at 16 slots): the split states published write-through
+    // and merged by each head's last split workgroup (arrival counter cnt[b][h]) into
+    // merged[b][768] (the O-projection then reads plain rows)
+    float *merged;
+    unsigned *cnt;
 };
 
 struct GemvP {

@@ -53,7 +53,8 @@ hipError_t op_lt_in0_16(const GemvP &, hipStream_t);
     hipError_t b16_lt_bg_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_b_##NB(const GemvP &, hipStream_t);         \
     hipError_t b16_lt_c_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_d_##NB(const GemvP &, hipStream_t);          \
     hipError_t b16_lt_e_##NB(const GemvP &, hipStream_t); hipError_t b16_oproj_xa_##NB(const GemvP &, hipStream_t); \
-    hipError_t b16_qkv_sa_##NB(const GemvP &, hipStream_t); hipError_t b16_ff1p_##NB(const GemvP &, hipStream_t);
+    hipError_t b16_qkv_sa_##NB(const GemvP &, hipStream_t); hipError_t b16_ff1p_##NB(const GemvP &, hipStream_t); \
+    hipError_t b16_lt_es_##NB(const GemvP &, hipStream_t); hipError_t b16_lt_em_##NB(const GemvP &, hipStream_t);
 MP_DECL_B16(1)
 MP_DECL_B16(2)
 MP_DECL_B16(4)
@@ -107,8 +108,10 @@ hipError_t op_lt_em_1(const GemvP &, hipStream_t);
 hipError_t op_lt_ffn(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_ffn2(const LtFfn2P &, int, hipStream_t);
+hipError_t op_lt_slot(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_kvo(const GemvP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
+hipError_t b16_oproj_xa_pm_16(const GemvP &, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_xa_q8(const XaQ8P &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
@@ -124,7 +127,7 @@ namespace mp {
 // qkv_sa: the QKV projection + the SA in one launch (EPI_QKV_SA)
 // xq: the direct XA's f32 q_net GEMV (f32 and bf16 modes); ff1: FFN up from a materialised x2
 struct OpTable { GemvFn qkv, oproj, ff1, ff1x, ff2, lt_in0, lt_a, lt_bg, lt_b, lt_c, lt_d, lt_e, oproj_xa,
-                 qkv_sa, xq; };
+                 qkv_sa, xq, lt_es, lt_em; };
 #define MP_TABLE(NB) { op_qkv_##NB, op_oproj_##NB, op_ff1_##NB, op_ff1x_##NB, op_ff2_##NB, \
                        op_lt_in0_##NB, op_lt_a_##NB, op_lt_bg_##NB, op_lt_b_##NB, op_lt_c_##NB, op_lt_d_##NB, op_lt_e_##NB, \
                        op_oproj_xa_##NB, op_qkv_sa_##NB, op_xq_##NB }
@@ -135,7 +138,7 @@ static const OpTable kTables[5] = {MP_TABLE(1), MP_TABLE(2), MP_TABLE(4), MP_TAB
 // bf16 weight mode: every projection on MFMA except the f32 LT in_proj
 #define MP_TABLE_B16(NB) { b16_qkv_##NB, b16_oproj_##NB, b16_ff1p_##NB, b16_ff1_##NB, b16_ff2_##NB, \
                            op_lt_in0_##NB, b16_lt_a_##NB, b16_lt_bg_##NB, b16_lt_b_##NB, b16_lt_c_##NB,  \
-                           b16_lt_d_##NB, b16_lt_e_##NB, b16_oproj_xa_##NB, b16_qkv_sa_##NB, op_xq_##NB }
+                           b16_lt_d_##NB, b16_lt_e_##NB, b16_oproj_xa_##NB, b16_qkv_sa_##NB, op_xq_##NB, b16_lt_es_##NB, b16_lt_em_##NB }
 static const OpTable kTablesB16[5] = {MP_TABLE_B16(1), MP_TABLE_B16(2), MP_TABLE_B16(4), MP_TABLE_B16(8),
                                       MP_TABLE_B16(16)};
 // F16 weight mode (an F16 GGUF): the same MFMA family on f16, the LT in_proj included
@@ -203,6 +206,9 @@ struct Model {
     // instead of 256 half cache lines (whose other halves sit with workgroup p +- 1 on
     // another XCD: every line was fetched twice)
     float *lt_ff2s = nullptr;
+    // bf16 weight mode (lt_slot_kernel): the LT FFN weights rounded to bf16, W1 row-major
+    // [1024][256] and W2 slice-major [LTS_P][256][1024 / LTS_P]
+    unsigned short *lt_ff1h = nullptr, *lt_ff2h = nullptr;
     std::vector<float *> xq_t;  // per layer W_q^T [768][128] (for K' = K W_q)
     // weight mode MP_WEIGHTS_BF16: decode projections repacked as bf16 MFMA fragments
     int weight_mode = 0;
@@ -221,7 +227,7 @@ struct Model {
 };
 
 enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9,
-              K_LTFFN2 = 10, K_LTKVO = 11 };
+              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12 };
 struct OpRec {
     std::string name;
     int kind;
@@ -244,7 +250,8 @@ struct LtIo {
     float *x, *hidden, *trace;
     int trace_steps;
     float *lt_s, *ltX, *ltY, *lty2, *ltq, *ltk, *ltv, *ltf, *logits;
-    float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel)
+    float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel; lt_slot_kernel: [NB][LTS_P][256])
+    unsigned *ltcnt;  // [NB] lt_slot_kernel's arrival counters (monotonic)
     int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
     SmpCfg *cfg;
     int sampling, ignore_eos, emit_eos, max_steps, lt_only;
@@ -277,12 +284,14 @@ struct mp_dev {
     int32_t *h_codes = nullptr;              // streaming: pinned host mirror of codes_out [NB][S][8] + snapshots
     size_t h_codes_n = 0;
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
+    unsigned *sacnt = nullptr, *xacnt = nullptr;   // 16-slot last-arriver merges: [NB][12], [NB]
     unsigned long long *xh = nullptr;  // O-projection -> XA hand-off granules [NB][768] (EPI_RESID_XA)
     unsigned long long *qh = nullptr;  // QKV -> SA hand-off granules [NB][2304] (EPI_QKV_SA)
     unsigned long long *xqh = nullptr; // Q8_0 XA q_net -> attention hand-off granules [NB][128] (EPI_RESID_XQ8)
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
+    unsigned *ltcnt = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
         *argeos = nullptr, *amax = nullptr;
@@ -554,9 +563,20 @@ int load_model(mp_dev *dev, const char *path) {
     return MP_OK;
 }
 
+// f32 -> bf16 bits, round to nearest even (ggml_compute_fp32_to_bf16; finite weights)
+static unsigned short bf16_bits(float x) {
+    unsigned u;
+    memcpy(&u, &x, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 64);
+    return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
 // f32 mode's LT (lt_ffn2_kernel) needs o_net applied to v rows ahead of time:
 // VO[c][v] = W_o V[c][v] for every table row, and [W_k ; W_o W_v] for position 0.
 bool f32_lt_mode(const mp::Model &m) { return m.weight_mode == MP_WEIGHTS_AS_STORED; }
+// the LT attention through the load-time q|k|vo tables in f32: the f32 mode, and the bf16
+// mode (whose LT FFN and heads are bf16: lt_slot_kernel + the bf16 head)
+bool lt_table_attn(const mp::Model &m) { return m.weight_mode == MP_WEIGHTS_AS_STORED || m.weight_mode == MP_WEIGHTS_BF16; }
 
 int build_vo_tables(mp_dev *dev) {
     mp::Model &m = dev->m;
@@ -605,9 +625,10 @@ int build_ptab(mp_dev *dev, int weight_mode) {
     HIPCHK(hipMalloc(&m.lt_qkvtab, R * 768 * 4));
     float *rows = nullptr, *wq = nullptr;
     HIPCHK(hipMalloc(&rows, R * 256 * 4));
-    const bool b16 = weight_mode == MP_WEIGHTS_BF16;  // F16: the file's weights are already f16 values
+    // the bf16 mode's LT attention is f32 (lt_table_attn); F16: the file's weights are already f16 values
+    const bool b16 = false;
     HIPCHK(mp::pre_lt_tab_rows(m.lt_ptab, m.lt_pos, m.lt_norm_self, m.eps, rows,
-                               b16 ? 1 : weight_mode == MP_WEIGHTS_F16 ? 2 : 0, dev->stream));
+                               weight_mode == MP_WEIGHTS_F16 ? 2 : 0, dev->stream));
     if (b16) {
         HIPCHK(hipMalloc(&wq, (size_t)768 * 256 * 4));
         HIPCHK(mp::pre_round_bf16(m.lt_qkv, wq, (size_t)768 * 256, dev->stream));
@@ -631,7 +652,22 @@ int build_ptab(mp_dev *dev, int weight_mode) {
         HIPCHK(hipMalloc(&m.lt_ff2s, w2s.size() * 4));
         HIPCHK(hipMemcpy(m.lt_ff2s, w2s.data(), w2s.size() * 4, hipMemcpyHostToDevice));
     }
-    return f32_lt_mode(m) ? build_vo_tables(dev) : MP_OK;
+    if (weight_mode == MP_WEIGHTS_BF16 && !m.lt_ff1h) {
+        std::vector<float> w1((size_t)1024 * 256), w2((size_t)256 * 1024);
+        HIPCHK(hipMemcpy(w1.data(), m.lt_ff1, w1.size() * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(w2.data(), m.lt_ff2, w2.size() * 4, hipMemcpyDeviceToHost));
+        constexpr int U = 1024 / mp::LTS_P;
+        std::vector<unsigned short> h1(w1.size()), h2(w2.size());
+        for (size_t i = 0; i < w1.size(); ++i) h1[i] = bf16_bits(w1[i]);
+        for (int q = 0; q < mp::LTS_P; ++q)
+            for (int n = 0; n < 256; ++n)
+                for (int u = 0; u < U; ++u) h2[((size_t)q * 256 + n) * U + u] = bf16_bits(w2[(size_t)n * 1024 + q * U + u]);
+        HIPCHK(hipMalloc(&m.lt_ff1h, h1.size() * 2));
+        HIPCHK(hipMemcpy(m.lt_ff1h, h1.data(), h1.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&m.lt_ff2h, h2.size() * 2));
+        HIPCHK(hipMemcpy(m.lt_ff2h, h2.data(), h2.size() * 2, hipMemcpyHostToDevice));
+    }
+    return lt_table_attn(m) ? build_vo_tables(dev) : MP_OK;
 }
 
 // Weight mode MP_WEIGHTS_Q8: upload every block-quantised tensor the decode path
@@ -825,13 +861,14 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(sa_out, NB * 768);
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
+    A(sacnt, (size_t)NB * mp::NH); A(xacnt, NB);
     A(xh, (size_t)NB * D); A(qh, (size_t)NB * 3 * D); A(xqh, (size_t)NB * 128);
     const size_t kvn = (size_t)NB * L * dev->max_seq * D;  // elements; bf16 mode: 2 per float slot
     A(kc, dev->kv16 ? kvn / 2 : kvn); A(vc, dev->kv16 ? kvn / 2 : kvn);
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
-    A(ltp, (size_t)NB * mp::LT_FFN_P * 256);
+    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltcnt, NB);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -909,6 +946,12 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // self-attention over the cache, split over keys (3457-3476); the f32 family runs
         // it in the QKV launch on a hand-off of q|k|v (EPI_QKV_SA), the others separately
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->kv16, dev->sa_part};
+        // bf16 mode at 16 slots: the SA and XA split states are merged once, by the last
+        // split workgroup of each head / slot (sa_merge_last, xa_merge_last), not by every
+        // O-projection / FFN-up workgroup's prologue (196 / 245 KiB each at 16 slots); the
+        // same arithmetic, so batches still reproduce single runs
+        const bool merge16 = NB == 16 && m.weight_mode == MP_WEIGHTS_BF16 && !dev->xa_direct;
+        if (merge16) { a.merged = dev->sa_out; a.cnt = dev->sacnt; }
         // (not at 16 slots: bf16 B=16 20.1k vs 21.5k frames/s; both forms compute the
         // same bits)
         // (Q8_0: the same hand-off in the int8 MFMA launch, mp_decode_q8.hip; MAGPIE_Q8_UNFUSED=1
@@ -962,8 +1005,14 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
                 return rc;
         } else if (xa_in_oproj) {
             // f32: the fused XA rides in the O-projection's launch on a hand-off of x1
+            mp::GemvFn fn = tb.oproj_xa;
+            if (merge16) {
+                g.part = nullptr; g.src = dev->sa_out; g.src_ld = 768;
+                xp.x2 = dev->x2; xp.cnt = dev->xacnt;
+                fn = mp::b16_oproj_xa_pm_16;
+            }
             g.xa = xp; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
-            if ((rc = run("oproj_xa", tb.oproj_xa, g, F * (768.0 * 768) + A * act * (768 * 3) + xa_bytes)) != MP_OK)
+            if ((rc = run("oproj_xa", fn, g, F * (768.0 * 768) + A * act * (768 * 3) + xa_bytes)) != MP_OK)
                 return rc;
         } else if ((rc = run("oproj", W.o8 ? tq.oproj : tb.oproj, g,
                              (W.o8 ? Fq(W.o8) : F) * (768.0 * 768) + A * act * (768 * 3))) != MP_OK) {
@@ -1004,7 +1053,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // LN + FFN up + GELU (1796-1799)
         g = gemv_base(dev); g.layer = l;
         g.W = W.ff1; g.Wb = b16 ? m.pk_ff1[l] : nullptr; g.N = 3072; g.lnw = W.norm_ff; g.out = dev->h; g.out_ld = 3072;
-        if (xa_dir) {  // x2 materialised by the direct XA
+        if (xa_dir || merge16) {  // x2 materialised by the direct XA / the XA tail's merge
             g.src = dev->x2; g.src_ld = 768;
             if (b16) g.out_b16 = dev->h_b16;
             if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
@@ -1025,6 +1074,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     io.x = dev->x; io.hidden = dev->hidden; io.trace = dev->trace; io.trace_steps = dev->max_steps + 1;
     io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
     io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits; io.ltp = dev->ltp;
+    io.ltcnt = dev->ltcnt;
     io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
     io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
     io.amax = dev->amax; io.cfg = dev->smpcfg;
@@ -1118,7 +1168,54 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                 return rc;
         }
     }
-    if (f32_lt_mode(m)) {
+    if (m.weight_mode == MP_WEIGHTS_BF16) {
+        // bf16 mode: the f32 mode's position 0 (LN + [k_0 | vo_0]), then per codebook the
+        // LT step as LTS_P workgroups per slot (lt_slot_kernel: pick, f32 attention
+        // through the tables, bf16 FFN, partial sums merged by the slot's last
+        // workgroup) and the bf16 head: 2 launches per codebook at every batch size
+        mp::GemvP g = base(); g.cb = 0;
+        g.W = m.lt_kvo; g.N = 512; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX; g.lnw = m.lt_norm_self;
+        g.lk = io.ltk; g.lv = io.ltv;
+        if (ops) {
+            mp::OpRec r{};
+            r.name = "lt_kvo"; r.kind = mp::K_LTKVO; r.g = g; r.B = NB;
+            r.bytes = A * (512.0 * 256) + A * act * (256 * 4);
+            ops->push_back(r);
+        }
+        HIPCHK(mp::op_lt_kvo(g, NB, s));
+        dump_lt(io, s);
+        for (int cb = 0; cb < 8; ++cb) {
+            mp::LtFfn2P l2{};
+            l2.f = mp::LtFfnP{io.ltY, m.lt_norm_ff, nullptr, nullptr, m.eps, io.ltp, io.lty2};
+            // the partial sums merged by the head's prologue at batch 1 (32 KiB per head
+            // workgroup; 4 slots' 128 KiB took 11.5 us), by the slot's last LT-step workgroup
+            // above
+            const bool head_merge = NB == 1;
+            l2.w1h = m.lt_ff1h; l2.w2h = m.lt_ff2h; l2.cnt = head_merge ? nullptr : io.ltcnt;
+            l2.cb = cb; l2.ltX = io.ltX; l2.ltk = io.ltk; l2.ltv = io.ltv; l2.qkvtab = m.lt_qkvtab;
+            l2.votab = m.lt_votab; l2.ptab = m.lt_ptab; l2.lt_pos = m.lt_pos; l2.logits = io.logits;
+            l2.codes_cur = io.codes_cur; l2.step = io.step; l2.ignore_eos = io.ignore_eos;
+            l2.audio_bos = m.audio_bos; l2.audio_eos = m.audio_eos;
+            l2.smp = mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax};
+            if (ops) {
+                mp::OpRec r{};
+                r.name = "lt_slot"; r.kind = mp::K_LTSLOT; r.l2 = l2; r.B = NB;
+                r.bytes = F * (1024.0 * 256 * 2) + A * act * (cb ? 2024 + 4 * 256 + 2 * 256 * cb : 512) +
+                          A * act * (mp::LTS_P * 256 + 256);
+                ops->push_back(r);
+            }
+            HIPCHK(mp::op_lt_slot(l2, NB, s));
+            dump_lt(io, s);
+            g = base(); g.cb = cb;
+            g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024; g.bias = m.lt_out_b + (size_t)cb * 2024;
+            g.Wb = m.pk_lt_out + (size_t)cb * pk_elems(2024, 256);
+            g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
+            if (head_merge) { g.part = io.ltp; g.addsrc = io.ltY; }
+            if ((rc = run("lt_e", head_merge ? tb.lt_em : tb.lt_es, g,
+                          F * (2024.0 * 256) + A * 2024 + A * act * ((head_merge ? mp::LTS_P * 256 : 256) + 2024))) != MP_OK)
+                return rc;
+        }
+    } else if (f32_lt_mode(m)) {
         // f32 mode: LN + [k_0 | vo_0] for position 0, then per codebook ONE launch for
         // pick + attention + o_net + residual + FFN (lt_ffn2_kernel) and the head
         mp::GemvP g = base(); g.cb = 0;
@@ -1451,6 +1548,9 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     dev->m.q8_all = false;
     dev->m.lt_in8 = dev->m.lt_qkv8 = dev->m.lt_o8 = dev->m.lt_out8 = mp::QW{};
     dev->m.pk_lt_in = nullptr;  // set again by an F16 load
+    // derived LT weight layouts of a previous model (rebuilt by build_ptab)
+    for (void **pp : {(void **)&dev->m.lt_ff2s, (void **)&dev->m.lt_ff1h, (void **)&dev->m.lt_ff2h})
+        if (*pp) { hipFree(*pp); *pp = nullptr; }
     if (weight_mode == MP_WEIGHTS_Q8 || weight_mode == MP_WEIGHTS_F16) {  // cheap header check before any upload
         mp::Gguf g;
         std::string err;
@@ -1478,8 +1578,8 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     } else if (weight_mode == MP_WEIGHTS_Q8) {
         if (int rc = load_q8(dev, path)) return rc;
     }
+    dev->m.weight_mode = weight_mode;  // the load-time LT tables depend on it
     if (int rc = build_ptab(dev, weight_mode)) return rc;
-    dev->m.weight_mode = weight_mode;
     dev->loaded = true;
     return MP_OK;
 }
@@ -1523,6 +1623,8 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.lt_votab) hipFree(dev->m.lt_votab);
     if (dev->m.lt_kvo) hipFree(dev->m.lt_kvo);
     if (dev->m.lt_ff2s) hipFree(dev->m.lt_ff2s);
+    if (dev->m.lt_ff1h) hipFree(dev->m.lt_ff1h);
+    if (dev->m.lt_ff2h) hipFree(dev->m.lt_ff2h);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
     if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
     if (dev->m.q8p_arena) hipFree(dev->m.q8p_arena);
@@ -1879,7 +1981,8 @@ int mp_hip_lt_sample(mp_dev *dev, const float *hidden, float temperature, int to
         int rc = MP_OK;
         if ((rc = al(&io.hidden, 768)) || (rc = al(&io.lt_s, 9 * 256)) || (rc = al(&io.ltX, 256)) ||
             (rc = al(&io.ltY, 256)) || (rc = al(&io.lty2, 256)) || (rc = al(&io.ltq, 256)) ||
-            (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) || (rc = al(&io.ltp, mp::LT_FFN_P * 256)) ||
+            (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) || (rc = al(&io.ltp, std::max(mp::LT_FFN_P, mp::LTS_P) * 256)) ||
+            (rc = al(&io.ltcnt, 16)) ||
             (rc = al(&io.logits, 2024)) || (rc = al(&io.codes_cur, 8)) || (rc = al(&io.step, 1)) ||
             (rc = al(&io.done, 1)) || (rc = al(&io.argeos, 1)) || (rc = al(&io.amax, 8)) || (rc = al(&io.cfg, 8)))
             return rc;
@@ -1970,6 +2073,7 @@ static hipError_t launch_rec(const mp::OpRec &r, hipStream_t s) {
     case mp::K_LTMERGE: return mp::op_lt_merge(r.lf, r.B, s);
     case mp::K_LTPICK: return mp::op_lt_pick(r.g, r.B, s);
     case mp::K_LTFFN2: return mp::op_lt_ffn2(r.l2, r.B, s);
+    case mp::K_LTSLOT: return mp::op_lt_slot(r.l2, r.B, s);
     case mp::K_LTKVO: return mp::op_lt_kvo(r.g, r.B, s);
     case mp::K_EMBED: return mp::op_embed(r.e, r.B, s);
     case mp::K_FIN: return mp::op_finalize(r.f, r.B, s);

@@ -148,8 +148,43 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
         num = fmaf(e, wo[q][tid], num);
     }
     float *pp = p.part + ((size_t)(b * NH + h) * SA_SPLITS + sp) * SA_PART;
+    if (p.merged) {  // write-through: the head's last split workgroup merges (sa_merge_last)
+        gf32 *gp = (gf32 *)pp;
+        __hip_atomic_store(gp + 4 + tid, num, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            __hip_atomic_store(gp, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     pp[4 + tid] = num;  // relative to M (an empty split stores M = -inf, l = 0, O = 0)
     if (tid == 0) { pp[0] = M; pp[1] = den; }
+}
+
+// AttnP::merged: every thread of the workgroup after sa_part. The split's stores are
+// drained, the workgroup counts in on its head's counter (monotonic: the last of every
+// SA_SPLITS arrivals), and the last one merges the head's SA_SPLITS states with
+// PRO_SA_MERGE's arithmetic (split_weights, split_merge), whoever it is.
+__device__ __forceinline__ void sa_merge_last(const AttnP &p, int h, int b) {
+    __shared__ int last;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add((gu32 *)p.cnt + b * NH + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) %
+                   SA_SPLITS == SA_SPLITS - 1;
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (!last || tid >= DH) return;
+    const gf32 *pp = (const gf32 *)p.part + (size_t)(b * NH + h) * SA_SPLITS * SA_PART;
+    float ms[SA_SPLITS], ls[SA_SPLITS], o[SA_SPLITS], e[SA_SPLITS], rd;
+#pragma unroll
+    for (int s = 0; s < SA_SPLITS; ++s) {
+        ms[s] = __hip_atomic_load(pp + s * SA_PART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ls[s] = __hip_atomic_load(pp + s * SA_PART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        o[s] = __hip_atomic_load(pp + s * SA_PART + 4 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    split_weights<SA_SPLITS>(ms, ls, e, rd);
+    p.merged[(size_t)b * D + h * DH + tid] = split_merge<SA_SPLITS>(e, o, rd);
 }
 
 // EPI_QKV_SA epilogue, output (row n, slot b): EPI_QKV's stores, and the value

@@ -29,6 +29,8 @@ static_assert(XA_THREADS == MP_BLOCK, "XA workgroups ride in the O-projection la
 constexpr unsigned HX_SPIN_LIMIT = 1u << 20;
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 using gi32 = __attribute__((address_space(1))) int;
+using gu32 = __attribute__((address_space(1))) unsigned;
+using gf32 = __attribute__((address_space(1))) float;
 
 // Split sp of slot b. HANDOFF: x1 comes from the O-projection in the same launch,
 // as {tag, value} granules xh[b][768] (EPI_RESID_XA): every wave sweeps all 768
@@ -166,9 +168,62 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
             const float4 v4 = *(const float4 *)&wo[q][4 * tid];
             num.x += e[q] * v4.x; num.y += e[q] * v4.y; num.z += e[q] * v4.z; num.w += e[q] * v4.w;
         }
-        *(float4 *)(pp + 4 + 4 * tid) = num;
+        if (p.x2) {  // write-through: the slot's last split workgroup merges (xa_merge_last)
+            gf32 *gp = (gf32 *)pp + 4 + 4 * tid;
+            __hip_atomic_store(gp, num.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp + 1, num.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp + 2, num.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp + 3, num.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            *(float4 *)(pp + 4 + 4 * tid) = num;
+        }
     }
-    if (tid == 0) { pp[0] = M; pp[1] = den; }
+    if (tid == 0) {
+        if (p.x2) {
+            __hip_atomic_store((gf32 *)pp, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gf32 *)pp + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            pp[0] = M; pp[1] = den;
+        }
+    }
+}
+
+// XaP::x2 (16 slots): every thread of an XA workgroup after xa_part. The split's
+// stores are drained, the workgroup counts in on its slot's counter (monotonic: the
+// last of every XA_SPLITS arrivals), and the last one writes x2 = x1 + the merged XA
+// output with PRO_XA_LN's arithmetic (split_weights, split_merge4, xa_x2), x1 from
+// the granules this workgroup has already seen complete.
+__device__ __forceinline__ void xa_merge_last(const XaP &p, int b, const unsigned long long *xh) {
+    __shared__ int last;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add((gu32 *)p.cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % XA_SPLITS ==
+               XA_SPLITS - 1;
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (!last || tid >= D / 4) return;
+    const gf32 *pp = (const gf32 *)p.part + (size_t)b * XA_SPLITS * XA_PART;
+    float ms[XA_SPLITS], ls[XA_SPLITS], e[XA_SPLITS], rd;
+    float4 o[XA_SPLITS];
+#pragma unroll
+    for (int s = 0; s < XA_SPLITS; ++s) {
+        const gf32 *q = pp + s * XA_PART;
+        ms[s] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ls[s] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        o[s] = make_float4(__hip_atomic_load(q + 4 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __hip_atomic_load(q + 5 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __hip_atomic_load(q + 6 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __hip_atomic_load(q + 7 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    const gu64 *g = (const gu64 *)xh + (size_t)b * D + 4 * tid;
+    float x1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        x1[i] = __uint_as_float((unsigned)__hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    split_weights<XA_SPLITS>(ms, ls, e, rd);
+    const float4 a = split_merge4<XA_SPLITS>(e, o, rd);
+    *(float4 *)(p.x2 + (size_t)b * D + 4 * tid) = xa_x2(a, make_float4(x1[0], x1[1], x1[2], x1[3]));
 }
 
 
@@ -188,6 +243,7 @@ __device__ __forceinline__ void xa_tail(const GemvP &p, unsigned long long t_sta
     const int k = blockIdx.x - p.nrow_blocks;
     xa_part<true>(p.xa, k % XA_SPLITS, k / XA_SPLITS, p.xh, (unsigned)p.iter[0] * 64u + p.layer + 1u, p.hx_err,
                   ts_dep(t_start), p.ts, t_start);
+    if (p.xa.x2) xa_merge_last(p.xa, k / XA_SPLITS, p.xh);
     ts_end(p.ts, t_start);
 }
 

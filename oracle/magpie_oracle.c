@@ -461,8 +461,8 @@ int orc_set_weight_mode(orc_model *m, int mode) {
         L->ff1_h = bf16_copy(L->ff1, (size_t)dff * d);
         L->ff2_h = bf16_copy(L->ff2, (size_t)d * dff);
     }
-    m->lt_qkv_h = bf16_copy(m->lt_qkv, (size_t)3 * D * D);
-    m->lt_o_h = bf16_copy(m->lt_o, (size_t)D * D);
+    // the LT attention (q|k|v, o_net) stays f32 in this mode: the build computes it through
+    // load-time f32 tables (lt_slot_kernel); its FFN and output heads are bf16
     m->lt_ff1_h = bf16_copy(m->lt_ff1, (size_t)F * D);
     m->lt_ff2_h = bf16_copy(m->lt_ff2, (size_t)D * F);
     for (int c = 0; c < 8; ++c) m->lt_out_w_h[c] = bf16_copy(m->lt_out_w[c], (size_t)m->vocab_cb * D);

@@ -30,10 +30,12 @@ void orc_set_mode(int acc64, int gelu_f16, int n_threads);
 orc_model *orc_load(const char *gguf_path);
 // Weight mode 1 = this build's bf16 decode path (no reference file format: the
 // reference converter writes F32/F16/Q8_0/Q4_0): in decode steps (BOS included)
-// the projections qkv/o/ff1/ff2 of every decoder layer and of the LT layer, and
-// the 8 LT output projections, use bf16-rounded weights and bf16-rounded input
-// activations (ggml's BF16 mul_mat semantics), f32/f64 accumulation. Encoder,
-// prefill, cross-attention and LT in_proj stay f32. 0 = as stored (Q8_0/F16
+// the projections qkv/o/ff1/ff2 of every decoder layer, the LT layer's FFN
+// (ff1/ff2) and the 8 LT output projections use bf16-rounded weights and
+// bf16-rounded input activations (ggml's BF16 mul_mat semantics), f32/f64
+// accumulation. Encoder, prefill, cross-attention, LT in_proj and the LT layer's
+// attention (q|k|v, o_net: the build computes it through load-time f32 tables)
+// stay f32. 0 = as stored (Q8_0/F16
 // tensors dequantised to f32, f32 activations). Weight mode 2 = ggml's Q8_0
 // mul_mat for every Q8_0 tensor of the file, everywhere it is used (encoder,
 // XA K/V, prefill, decode steps, LT): the activation row is quantised to Q8_0

@@ -21,6 +21,10 @@ pytestmark = pytest.mark.gpu
 
 HIDDEN_TOL = 2e-3  # reference's own full-decoder tolerance 2.66e-3 (docs/STATUS.md:108-116)
 TIE_EPS = 3e-2     # bf16 near-tie bar (tests/test_decode_gpu.py, the oracle's own f32/f64 spread)
+# over configs[2]'s whole 256-frame utterance on 12 layers the oracle's own bf16-mode f32/f64
+# spread is ~0.09 (margins shift up to 0.0915, a decision of margin 0.060 flips:
+# tests/test_oracle_cpu.py::test_bf16_mode_spread_full_model_256, tools_dev/bf16_spread.py)
+BF16_LONG_TIE_EPS = 0.1
 HIDDEN_TOL16, HIDDEN_REL16 = 3e-2, 5e-3
 
 
@@ -97,7 +101,8 @@ def test_bf16_batch16_teacher_forced_256(ma, oracle, full_model):
     om.set_weight_mode(1)
     o = om.synthesize_forced(toks[0], rb.codes[0], speaker=spk[0], ignore_eos=True)
     om.close()
-    res = compare_forced(rb.codes[0], o, tie_eps=TIE_EPS, max_ties=steps * 8 // 40)
+    res = compare_forced(rb.codes[0], o, tie_eps=BF16_LONG_TIE_EPS, max_ties=steps * 8 // 40)
+    print(f"bf16 slot 0: {res}")
     assert res["decisions"] == steps * 8
     h, ho = rb.hidden[0, :steps + 1], o["hidden"]
     live = np.linalg.norm(ho, axis=-1) > 0  # rows the forced run computed (BOS .. last input frame)

@@ -1,17 +1,16 @@
 """Per-dispatch counters of the last codec decode from tools_dev/codec_pmc.sh passes."""
 import csv, glob, os, sys
 out = sys.argv[1]
-names = ["pre"]
-for s in range(5):
-    names.append(f"s{s} convT")
-    for k in range(3):
-        names += [f"s{s} k{k} in", f"s{s} k{k} sk"]
-names.append("post")
 table = {}
+names = []
 for f in sorted(glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True)):
     rows = [r for r in csv.DictReader(open(f)) if "mpc::" in r["Kernel_Name"]]
     ids = sorted({int(r["Dispatch_Id"]) for r in rows})
-    last = ids[-len(names):]
+    per = len(ids) // 3  # tools_dev/codec_prof.py: the last of its 3 decodes
+    last = ids[-per:]
+    if not names:
+        kn = {int(r["Dispatch_Id"]): r["Kernel_Name"].split("(")[0].replace("void mpc::", "") for r in rows}
+        names = [kn[d][:22] for d in last]
     for r in rows:
         d = int(r["Dispatch_Id"])
         if d in last:
@@ -23,4 +22,4 @@ cols = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_
 print("op " + " ".join(c.replace("SQ_", "").replace("_sum", "")[:14] for c in cols))
 for i, n in enumerate(names):
     t = table.get(i, {})
-    print(f"{n:11s} " + " ".join(f"{t.get(c, float('nan')):.3g}" for c in cols))
+    print(f"{n:22s} " + " ".join(f"{t.get(c, float('nan')):.3g}" for c in cols))

@@ -429,7 +429,7 @@ __global__ __launch_bounds__(64 * RWV * CWV, DEEP ? 1 : 2) void conv2_kernel(Con
 
 // ---------------------------------------------------------------- fused residual block
 // One HiFiGAN residual block of one branch (nano-codec.cpp:568-599) in one launch,
-// for the small-channel stages (128 / 64 / 32 padded channels, where the f32 residual
+// for the stages of 224 / 128 / 64 / 32 padded channels (where the f32 residual
 // stream and the f16 operands between the two convs were the traffic):
 //   x' = x + conv_{KS,1}(HS_sk(conv_{KS,d}(HS_in(x)))).
 // A workgroup owns output steps [t0, t0 + BN) of one chunk and every channel:
@@ -457,14 +457,15 @@ struct RbP {
 constexpr int RB_ROWB = 80;   // LDS bytes per time row of a 32-channel block
 constexpr int RB_MAXHALO = 50;  // (11 - 1) * 5
 
-template <int RWV, int CWV>
-constexpr int rb_lds_bytes() { return RWV * (64 * CWV + RB_MAXHALO) * RB_ROWB; }
+template <int RWV, int CWV, int NT>
+constexpr int rb_lds_bytes() { return RWV * (16 * NT * CWV + RB_MAXHALO) * RB_ROWB; }
 
-template <int KS, int RWV, int CWV, int R>
+// NT: 16-step column tiles per wave (each A fragment feeds 2 NT MFMAs)
+template <int KS, int RWV, int CWV, int NT, int R>
 __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
     constexpr int NCB = RWV, CPD = NCB * 32;  // one wave row per 32-channel block
     constexpr int NTH = 64 * RWV * CWV;
-    constexpr int NCD = 64 * CWV;             // conv_d columns
+    constexpr int NCD = 16 * NT * CWV;        // conv_d columns
     constexpr int BN = NCD - 16;              // outputs per workgroup
     constexpr int XR = NCD + RB_MAXHALO;      // LDS rows per channel block
     constexpr int NS = NCB * KS;              // A-stream steps (channel block, tap)
@@ -518,14 +519,14 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
 
     // ---- B / D: one causal conv from the LDS operand (rows: column c, tap k -> row
     // c * 1 + rowoff + k * dk), A stream from `wf` (conv2's ring), NT column tiles
-    floatx4 acc[C2_WR][C2_NT];
+    floatx4 acc[C2_WR][NT];
     half8 ring[R][C2_WR];
-    const int colb = cw * 64 + l16;
+    const int colb = cw * 16 * NT + l16;
     auto conv = [&](const _Float16 *wf, int rowoff, int dk, int nt) {
 #pragma unroll
         for (int a = 0; a < C2_WR; ++a)
 #pragma unroll
-            for (int j = 0; j < C2_NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
         const _Float16 *wrow0 = wf + (size_t)(rw * 2) * NS * 512 + lane * 8, *wrow1 = wrow0 + (size_t)NS * 512;
 #pragma unroll
         for (int q = 0; q < R; ++q)
@@ -536,18 +537,18 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
             const char *bbase = xs + cb * XR * RB_ROWB + (colb + rowoff) * RB_ROWB + 16 * kg;
-            half8 bc[C2_NT], bn[C2_NT];
+            half8 bc[NT], bn[NT];
 #pragma unroll
-            for (int j = 0; j < C2_NT; ++j) bc[j] = *(const half8 *)(bbase + j * 16 * RB_ROWB);
+            for (int j = 0; j < NT; ++j) bc[j] = *(const half8 *)(bbase + j * 16 * RB_ROWB);
 #pragma unroll
             for (int k = 0; k < KS; ++k) {
                 const int st = cb * KS + k;
                 if (k + 1 < KS) {
 #pragma unroll
-                    for (int j = 0; j < C2_NT; ++j) bn[j] = *(const half8 *)(bbase + (j * 16 + (k + 1) * dk) * RB_ROWB);
+                    for (int j = 0; j < NT; ++j) bn[j] = *(const half8 *)(bbase + (j * 16 + (k + 1) * dk) * RB_ROWB);
                 }
 #pragma unroll
-                for (int j = 0; j < C2_NT; ++j) {
+                for (int j = 0; j < NT; ++j) {
                     if (j < nt) {
                         acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][0], bc[j], acc[0][j], 0, 0, 0);
                         acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][1], bc[j], acc[1][j], 0, 0, 0);
@@ -559,13 +560,13 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
                 }
                 if (k + 1 < KS) {
 #pragma unroll
-                    for (int j = 0; j < C2_NT; ++j) bc[j] = bn[j];
+                    for (int j = 0; j < NT; ++j) bc[j] = bn[j];
                 }
             }
         }
     };
     // B: conv_d, column c = time t0 - 16 + c, x row c + k d
-    conv(p.Wd[br], 0, d, C2_NT);
+    conv(p.Wd[br], 0, d, NT);
     // each lane's 8 channels: rw * 32 + a * 16 + 4 kg + r
     const int chl = rw * 32 + 4 * kg;
     __syncthreads();  // every wave is done reading x rows
@@ -578,8 +579,8 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
             const float4 bb = *(const float4 *)(p.bd[br] + ch), al = *(const float4 *)(p.al_sk[br] + ch);
             const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, av[4] = {al.x, al.y, al.z, al.w};
 #pragma unroll
-            for (int j = 0; j < C2_NT; ++j) {
-                const int c = cw * 64 + j * 16 + l16, t = t0 - 16 + c;
+            for (int j = 0; j < NT; ++j) {
+                const int c = cw * 16 * NT + j * 16 + l16, t = t0 - 16 + c;
                 half4 h;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) h[r] = (_Float16)half_snake_sel(acc[a][j][r] + bv[r], ch + r, p.nsnake, p.creal, av[r]);
@@ -590,7 +591,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
     }
     __syncthreads();
     // ---- D: conv_1, output column o = time t0 + o, h row o + 16 - (KS - 1) + k
-    const int nt = cw == CWV - 1 ? C2_NT - 1 : C2_NT;  // BN = 64 CWV - 16 outputs
+    const int nt = cw == CWV - 1 ? NT - 1 : NT;  // BN = 16 NT CWV - 16 outputs
     conv(p.W1[br], 16 - (KS - 1), 1, nt);
     // ---- E: + bias + x -> x'
 #pragma unroll
@@ -598,8 +599,8 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
         const int ch = chl + a * 16;
         const float4 bb = *(const float4 *)(p.b1[br] + ch);
 #pragma unroll
-        for (int j = 0; j < C2_NT; ++j) {
-            const int t = t0 + cw * 64 + j * 16 + l16;
+        for (int j = 0; j < NT; ++j) {
+            const int t = t0 + cw * 16 * NT + j * 16 + l16;
             if (j >= nt || t >= p.T) continue;
             const size_t off = cbase + (size_t)t * CPD + ch;
             const float4 r = *(const float4 *)(p.x[br] + off);
@@ -610,13 +611,13 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
     }
 }
 
-template <int RWV, int CWV>
-__global__ __launch_bounds__(64 * RWV * CWV, 2) void rb_kernel(RbP p) {
-    __shared__ __attribute__((aligned(16))) char xs[rb_lds_bytes<RWV, CWV>()];
+template <int RWV, int CWV, int NT>
+__global__ __launch_bounds__(64 * RWV * CWV, RWV * CWV > 8 || NT > 4 ? 1 : 2) void rb_kernel(RbP p) {
+    __shared__ __attribute__((aligned(16))) char xs[rb_lds_bytes<RWV, CWV, NT>()];
     switch (p.ks[blockIdx.y]) {
-        case 3: rb_body<3, RWV, CWV, 3>(p, xs); break;
-        case 7: rb_body<7, RWV, CWV, 3>(p, xs); break;
-        default: rb_body<11, RWV, CWV, 3>(p, xs); break;
+        case 3: rb_body<3, RWV, CWV, NT, 3>(p, xs); break;
+        case 7: rb_body<7, RWV, CWV, NT, 3>(p, xs); break;
+        default: rb_body<11, RWV, CWV, NT, 3>(p, xs); break;
     }
 }
 
@@ -1000,23 +1001,27 @@ hipError_t launch_conv2(mpc::ConvP p, int nchunk, int nbranch, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int RWV, int CWV>
+template <int RWV, int CWV, int NT = 4>
 hipError_t launch_rb(mpc::RbP p, int nchunk, hipStream_t s) {
-    constexpr int BN = 64 * CWV - 16;
+    constexpr int BN = 16 * NT * CWV - 16;
     p.tiles_per_chunk = (p.T + BN - 1) / BN;
-    hipLaunchKernelGGL((mpc::rb_kernel<RWV, CWV>), dim3(nchunk * p.tiles_per_chunk, 3), dim3(64 * RWV * CWV), 0, s, p);
+    hipLaunchKernelGGL((mpc::rb_kernel<RWV, CWV, NT>), dim3(nchunk * p.tiles_per_chunk, 3), dim3(64 * RWV * CWV), 0, s, p);
     return hipGetLastError();
 }
 // the fused residual block for a stage's padded channel count (0: not fused)
 bool rb_fused(int Cp) {
     const bool off = getenv("MAGPIE_CODEC_UNFUSED") != nullptr;  // A/B switch (read per decode): the two-launch blocks
-    return !off && (Cp == 128 || Cp == 64 || Cp == 32);
+    return !off && (Cp == 224 || Cp == 128 || Cp == 64 || Cp == 32);
 }
 hipError_t run_rb(const mpc::RbP &p, int Cp, int nchunk, hipStream_t s) {
+    // waves x steps per wave, measured per stage (8 x 32-frame chunks, same box): 64 steps
+    // per wave everywhere but the 32-channel stage (32: 240 vs 273 us); 128 per wave took
+    // 1.2-1.5x longer (one workgroup per CU), 32 per wave 1.3x on 128 / 64 channels
     switch (Cp) {
+        case 224: return launch_rb<7, 2>(p, nchunk, s);
         case 128: return launch_rb<4, 2>(p, nchunk, s);
         case 64: return launch_rb<2, 4>(p, nchunk, s);
-        case 32: return launch_rb<1, 8>(p, nchunk, s);
+        case 32: return launch_rb<1, 8, 2>(p, nchunk, s);
     }
     return hipErrorInvalidValue;
 }
@@ -1072,7 +1077,10 @@ int codec_run(mp_codec *c, int nchunk, int F) {
         const bool fused = rb_fused(Cp);
         switch (i) {
             case 0: hipLaunchKernelGGL((conv_transpose2_kernel<896, 448, 8, false, 1>), g2, dim3(256), 0, s, tp); break;
-            case 1: hipLaunchKernelGGL((conv_transpose2_kernel<448, 224, 8, true, 2>), g2, dim3(256), 0, s, tp); break;
+            case 1:
+                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<448, 224, 8, true, 2, false>), g2, dim3(256), 0, s, tp);
+                else hipLaunchKernelGGL((conv_transpose2_kernel<448, 224, 8, true, 2>), g2, dim3(256), 0, s, tp);
+                break;
             case 2:
                 if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4, false>), g2, dim3(256), 0, s, tp);
                 else hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4>), g2, dim3(256), 0, s, tp);

@@ -33,7 +33,8 @@ CLK = 2.4e9  # shader clock (MI355X_MICROARCH.md)
 WIDE = ("gemv_kernel", "gemm_b16_kernel", "xa_part_kernel", "sa_attn_kernel", "lt_ffn2_kernel", "lt_ffn_kernel",
         "conv_mfma_kernel", "gemm_q8_kernel_dec")
 DECODE = ("gemv_kernel", "sa_attn_kernel", "xa_part_kernel", "lt_finalize_kernel", "gemm_b16_kernel", "gemm_q8_kernel_dec",
-          "lt_ffn_kernel", "lt_ffn2_kernel", "lt_merge_kernel", "lt_pick_kernel", "xa_q8_kernel", "xa_f32_kernel")
+          "lt_ffn_kernel", "lt_ffn2_kernel", "lt_merge_kernel", "lt_pick_kernel", "xa_q8_kernel", "xa_f32_kernel",
+          "lt_slot_kernel")
 # (embed_kernel runs once per decode, for the BOS frame, outside the iteration)
 
 

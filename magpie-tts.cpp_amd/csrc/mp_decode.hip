@@ -638,10 +638,11 @@ hipError_t op_lt_ffn2(const LtFfn2P &p, int NB, hipStream_t s) {
 // lt_y_slot (wave 0; the attention in f32 through the load-time q|k|vo tables, as
 // the f32 mode computes it), LN(y) rounded to bf16, then the FFN for hidden units
 // [32q, 32q + 32): up (bf16 W1 rows, f32 sums, GELU, rounded to bf16) and its share
-// of FFN down (bf16 W2 slice) as partial sums. The partials are published with
-// write-through stores; the slot's last workgroup to count in (cnt[b], monotonic:
-// the last of every LTS_P arrivals) merges them in q order, so the result does not
-// depend on who arrives last, and writes y2 = y + FFN(y) for the bf16 head.
+// of FFN down (bf16 W2 slice) as partial sums. From 2 slots up the partials are
+// published as {tag, value} granules and every workgroup of the slot merges 8 of the
+// 256 outputs (all-to-all over 32 workgroups, 2 KiB swept each, in q order whoever
+// publishes last) into y2 = y + FFN(y) for the bf16 head; at batch 1 the head's
+// prologue merges (the same operations in the same order).
 // LTS_P workgroups per slot at every batch size (16 KiB of W1 and of W2 each): no
 // slot's pick waits behind another's, and a batch reproduces its utterances run
 // alone. The weights are issued before the pick.
@@ -658,7 +659,6 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
     __shared__ __attribute__((aligned(16))) float ys[LTD];
     __shared__ __attribute__((aligned(16))) float hs[LTS_U];
     __shared__ __attribute__((aligned(16))) float wsc[2 * VCB];
-    __shared__ int last;
     const int q = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int u0 = q * LTS_U + ts_dep(t_start);
     uint2 a1[LTS_UPW];  // W1 rows u0 + LTS_UPW w + r, elements 4 lane .. 4 lane + 3
@@ -702,29 +702,48 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
         acc = fmaf(bf16_lo(a2[i].w), h1.z, acc);
         acc = fmaf(bf16_hi(a2[i].w), h1.w, acc);
     }
-    if (!p.cnt) {  // small batches: the head's prologue merges (PRO_LTS_MERGE)
+    if (!p.gh) {  // batch 1: the head's prologue merges (PRO_LTS_MERGE)
         p.f.part[((size_t)b * LTS_P + q) * LTD + tid] = acc;
         ts_end(p.f.ts, t_start);
         return;
     }
-    gf32 *part = (gf32 *)p.f.part + (size_t)b * LTS_P * LTD;
-    __hip_atomic_store(part + (size_t)q * LTD + tid, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's partial has landed before the workgroup counts in
-    __syncthreads();
-    if (tid == 0)
-        last = __hip_atomic_fetch_add((gu32 *)p.cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % LTS_P ==
-               LTS_P - 1;
-    __syncthreads();
-    if (last) {
-        float s = __hip_atomic_load(part + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the partial sums as {tag, value} granules; workgroup q then merges outputs
+    // [ME q, ME q + ME) of its slot: thread t sweeps partial t / ME's granule of output
+    // ME q + t % ME, and ME threads add the LTS_P values in q order (lts_merge's order)
+    constexpr int ME = LTD / LTS_P;
+    static_assert(ME * LTS_P == LTD && ME * LTS_P == MP_BLOCK, "one granule per thread");
+    __shared__ float mv[LTS_P][ME];
+    const unsigned tag = (unsigned)p.iter[0] * 64u + 32u + (unsigned)p.cb;
+    gu64 *gh = (gu64 *)p.gh + (size_t)b * LTS_P * LTD;
+    __hip_atomic_store(gh + (size_t)q * LTD + tid, ((unsigned long long)tag << 32) | __float_as_uint(acc),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    {
+        const gu64 *g = gh + (size_t)(tid / ME) * LTD + ME * q + tid % ME;
+        float v;
+        for (unsigned spins = 0;; ++spins) {
+            const unsigned long long u = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = __uint_as_float((unsigned)u);
+            if (__all((unsigned)(u >> 32) == tag)) break;
+            if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+                if (lane == 0) __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = __builtin_nanf("");
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        mv[tid / ME][tid % ME] = v;
+    }
+    lds_sync();
+    if (tid < ME) {
+        float s = mv[0][tid];
 #pragma unroll 8
-        for (int k = 1; k < LTS_P; ++k) s += __hip_atomic_load(part + (size_t)k * LTD + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        p.f.out[(size_t)b * LTD + tid] = s + ys[tid];
+        for (int k = 1; k < LTS_P; ++k) s += mv[k][tid];
+        p.f.out[(size_t)b * LTD + ME * q + tid] = s + ys[ME * q + tid];
     }
     ts_end(p.f.ts, t_start);
 }
 hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
-    if (!p.f.y || !p.f.lnw || !p.w1h || !p.w2h || !p.f.part || (p.cnt && !p.f.out) || !p.ltX || !p.ltk || !p.ltv ||
+    if (!p.f.y || !p.f.lnw || !p.w1h || !p.w2h || !p.f.part || (p.gh && (!p.f.out || !p.iter || !p.hx_err)) || !p.ltX || !p.ltk || !p.ltv ||
         !p.qkvtab || !p.votab || !p.ptab || !p.lt_pos || !p.logits || !p.codes_cur || !p.step || !p.smp.cfg ||
         !p.smp.argeos || p.cb < 0 || p.cb >= NCB || NB < 1 || NB > 16)
         return hipErrorInvalidValue;

@@ -121,11 +121,14 @@ struct LtFfn2P {
     int ignore_eos, audio_bos, audio_eos;
     Sampling smp;
     // bf16 weight mode (lt_slot_kernel): the FFN weights rounded to bf16, W1 row-major
-    // [1024][256], W2 slice-major [LTS_P][256][1024 / LTS_P]; partials f.part [B][LTS_P][256],
-    // merged by the slot's last workgroup (arrival counter cnt[b]) into f.out = y2, or (cnt
-    // null: small batches) by the head's prologue (PRO_LTS_MERGE)
+    // [1024][256], W2 slice-major [LTS_P][256][1024 / LTS_P]. The LTS_P partial sums per slot
+    // go to f.part, merged by the head's prologue (PRO_LTS_MERGE; gh null, batch 1), or as
+    // {tag, value} granules gh[B][LTS_P][256] of which every workgroup merges its 256 / LTS_P
+    // outputs into f.out = y2 (tags iter[0] * 64 + 32 + cb; hx_err: hand-off timeout)
     const unsigned short *w1h, *w2h;
-    unsigned *cnt;
+    unsigned long long *gh;
+    const int *iter;
+    int *hx_err;
 };
 
 // Frame embedding of every slot (layer 0's residual input, magpie.cpp:2746-2787,
@@ -282,7 +285,7 @@ struct GemvP {
 };
 
 // error bits raised in *hx_err (ndone[2]) by an in-launch hand-off that gave up
-constexpr int HX_ERR_XA = 1, HX_ERR_SA = 2;
+constexpr int HX_ERR_XA = 1, HX_ERR_SA = 2, HX_ERR_LT = 4;
 
 struct FinP {
     const float *logits;

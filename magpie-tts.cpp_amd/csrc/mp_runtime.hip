@@ -251,7 +251,8 @@ struct LtIo {
     int trace_steps;
     float *lt_s, *ltX, *ltY, *lty2, *ltq, *ltk, *ltv, *ltf, *logits;
     float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel; lt_slot_kernel: [NB][LTS_P][256])
-    unsigned *ltcnt;  // [NB] lt_slot_kernel's arrival counters (monotonic)
+    unsigned long long *ltgh;  // [NB][LTS_P][256] lt_slot_kernel's partial-sum granules
+    int *iter, *hx_err;        // decode iteration counter (hand-off tags), hand-off error bits
     int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
     SmpCfg *cfg;
     int sampling, ignore_eos, emit_eos, max_steps, lt_only;
@@ -291,7 +292,7 @@ struct mp_dev {
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
-    unsigned *ltcnt = nullptr;
+    unsigned long long *ltgh = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
         *argeos = nullptr, *amax = nullptr;
@@ -868,7 +869,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
-    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltcnt, NB);
+    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * mp::LTS_P * 256);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -1074,7 +1075,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     io.x = dev->x; io.hidden = dev->hidden; io.trace = dev->trace; io.trace_steps = dev->max_steps + 1;
     io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
     io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits; io.ltp = dev->ltp;
-    io.ltcnt = dev->ltcnt;
+    io.ltgh = dev->ltgh; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
     io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
     io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
     io.amax = dev->amax; io.cfg = dev->smpcfg;
@@ -1188,10 +1189,11 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             mp::LtFfn2P l2{};
             l2.f = mp::LtFfnP{io.ltY, m.lt_norm_ff, nullptr, nullptr, m.eps, io.ltp, io.lty2};
             // the partial sums merged by the head's prologue at batch 1 (32 KiB per head
-            // workgroup; 4 slots' 128 KiB took 11.5 us), by the slot's last LT-step workgroup
-            // above
+            // workgroup; 4 slots' 128 KiB took 11.5 us), through granules by the LT step
+            // itself above (the standalone LT API is batch 1: no iteration counter needed)
             const bool head_merge = NB == 1;
-            l2.w1h = m.lt_ff1h; l2.w2h = m.lt_ff2h; l2.cnt = head_merge ? nullptr : io.ltcnt;
+            l2.w1h = m.lt_ff1h; l2.w2h = m.lt_ff2h;
+            if (!head_merge) { l2.gh = io.ltgh; l2.iter = io.iter; l2.hx_err = io.hx_err; }
             l2.cb = cb; l2.ltX = io.ltX; l2.ltk = io.ltk; l2.ltv = io.ltv; l2.qkvtab = m.lt_qkvtab;
             l2.votab = m.lt_votab; l2.ptab = m.lt_ptab; l2.lt_pos = m.lt_pos; l2.logits = io.logits;
             l2.codes_cur = io.codes_cur; l2.step = io.step; l2.ignore_eos = io.ignore_eos;
@@ -1718,6 +1720,7 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->xh, 0, (size_t)NB * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xqh, 0, (size_t)NB * 128 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->ltgh, 0, (size_t)NB * mp::LTS_P * 256 * 8, dev->stream));
     // the first frame's decoder input (the BOS codes); later frames' by lt_finalize_kernel
     HIPCHK(mp::op_embed(mp::EmbP{dev->m.audio_emb, dev->codes_prev, dev->m.dec_pos, dev->pos, dev->x}, NB, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go
@@ -1762,6 +1765,7 @@ static int check_handoff(mp_dev *dev) {
         std::string what;
         if (nd[2] & mp::HX_ERR_XA) what += " O-projection -> cross-attention";
         if (nd[2] & mp::HX_ERR_SA) what += std::string(what.empty() ? "" : ",") + " QKV -> self-attention";
+        if (nd[2] & mp::HX_ERR_LT) what += std::string(what.empty() ? "" : ",") + " LT FFN partial sums";
         return fail(dev, MP_ERR_HIP, "in-launch hand-off timed out:" + what);
     }
     return MP_OK;
@@ -1982,7 +1986,7 @@ int mp_hip_lt_sample(mp_dev *dev, const float *hidden, float temperature, int to
         if ((rc = al(&io.hidden, 768)) || (rc = al(&io.lt_s, 9 * 256)) || (rc = al(&io.ltX, 256)) ||
             (rc = al(&io.ltY, 256)) || (rc = al(&io.lty2, 256)) || (rc = al(&io.ltq, 256)) ||
             (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) || (rc = al(&io.ltp, std::max(mp::LT_FFN_P, mp::LTS_P) * 256)) ||
-            (rc = al(&io.ltcnt, 16)) ||
+
             (rc = al(&io.logits, 2024)) || (rc = al(&io.codes_cur, 8)) || (rc = al(&io.step, 1)) ||
             (rc = al(&io.done, 1)) || (rc = al(&io.argeos, 1)) || (rc = al(&io.amax, 8)) || (rc = al(&io.cfg, 8)))
             return rc;

@@ -132,7 +132,7 @@ template <bool KV16>
 __global__ __launch_bounds__(SA_THREADS) void sa_attn_kernel(AttnP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     sa_part<KV16, SA_WAVES, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, nullptr, 0u, nullptr, ts_dep(t_start));
-    if (p.merged) sa_merge_last(p, blockIdx.x, blockIdx.z);
+    if (p.merged) sa_merge_split(p, blockIdx.x, blockIdx.y, blockIdx.z);
     ts_end(p.ts, t_start);
 }
 
@@ -651,8 +651,6 @@ __device__ __forceinline__ float bf16_round(float v) { return __uint_as_float((u
 __device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
-    using gf32 = __attribute__((address_space(1))) float;
-    using gu32 = __attribute__((address_space(1))) unsigned;
     const unsigned long long t_start = ts_begin(p.f.ts);
     static_assert(LTD == MP_BLOCK && LTS_U % 8 == 0 && LTS_U % MP_NWAVES == 0, "unit split");
     __shared__ __attribute__((aligned(16))) float xs[LTD];

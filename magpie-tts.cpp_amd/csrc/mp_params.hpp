@@ -170,11 +170,12 @@ struct XaP {
     int Tmax, layer, nlayers;
     int q_f16;             // F16 weight mode: LN(x) rounded to f16, the q_net operand ggml multiplies
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
-    // x2 (nullable; the O-projection's XA tail at 16 slots): the split states published
-    // write-through and merged with x1 by each slot's last split workgroup (arrival
-    // counter cnt[b]) into x2[b][768] (FFN up then normalises plain rows)
+    // x2 (nullable; the O-projection's XA tail at 16 slots): the split states published as
+    // {tag, value} granules gh[b][split][XA_PART]; each of a slot's XA_SPLITS workgroups
+    // merges 768 / XA_SPLITS outputs with x1 into x2[b][768] (FFN up then normalises
+    // plain rows)
     float *x2;
-    unsigned *cnt;
+    unsigned long long *gh;
 };
 
 // Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the
@@ -208,11 +209,14 @@ struct AttnP {  // decode self-attention (one query per utterance)
     float *part;         // [B][NH][SA_SPLITS][SA_PART] partial softmax states over key splits
                          // (merged in the O-projection's PRO_SA_MERGE prologue)
     unsigned long long *ts;  // profiling (nullable): [first wave start, last wave end], s_memrealtime ticks
-    // merged (nullable; sa_attn_kernel at 16 slots): the split states published write-through
-    // and merged by each head's last split workgroup (arrival counter cnt[b][h]) into
-    // merged[b][768] (the O-projection then reads plain rows)
+    // merged (nullable; sa_attn_kernel at 16 slots): the split states published as {tag,
+    // value} granules gh[b][h][split][SA_PART] (tag iter[0] * 64 + layer + 1); each of a
+    // head's SA_SPLITS workgroups merges 64 / SA_SPLITS of its dims into merged[b][768]
+    // (the O-projection then reads plain rows)
     float *merged;
-    unsigned *cnt;
+    unsigned long long *gh;
+    const int *iter;
+    int *hx_err;
 };
 
 struct GemvP {

@@ -285,7 +285,7 @@ struct mp_dev {
     int32_t *h_codes = nullptr;              // streaming: pinned host mirror of codes_out [NB][S][8] + snapshots
     size_t h_codes_n = 0;
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
-    unsigned *sacnt = nullptr, *xacnt = nullptr;   // 16-slot last-arriver merges: [NB][12], [NB]
+    unsigned long long *sagh = nullptr, *xagh = nullptr;  // 16-slot merges: split-state granules
     unsigned long long *xh = nullptr;  // O-projection -> XA hand-off granules [NB][768] (EPI_RESID_XA)
     unsigned long long *qh = nullptr;  // QKV -> SA hand-off granules [NB][2304] (EPI_QKV_SA)
     unsigned long long *xqh = nullptr; // Q8_0 XA q_net -> attention hand-off granules [NB][128] (EPI_RESID_XQ8)
@@ -862,7 +862,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(sa_out, NB * 768);
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
-    A(sacnt, (size_t)NB * mp::NH); A(xacnt, NB);
+    A(sagh, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xagh, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
     A(xh, (size_t)NB * D); A(qh, (size_t)NB * 3 * D); A(xqh, (size_t)NB * 128);
     const size_t kvn = (size_t)NB * L * dev->max_seq * D;  // elements; bf16 mode: 2 per float slot
     A(kc, dev->kv16 ? kvn / 2 : kvn); A(vc, dev->kv16 ? kvn / 2 : kvn);
@@ -947,12 +947,13 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // self-attention over the cache, split over keys (3457-3476); the f32 family runs
         // it in the QKV launch on a hand-off of q|k|v (EPI_QKV_SA), the others separately
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->kv16, dev->sa_part};
-        // bf16 mode at 16 slots: the SA and XA split states are merged once, by the last
-        // split workgroup of each head / slot (sa_merge_last, xa_merge_last), not by every
-        // O-projection / FFN-up workgroup's prologue (196 / 245 KiB each at 16 slots); the
-        // same arithmetic, so batches still reproduce single runs
+        // bf16 mode at 16 slots: the SA and XA split states are merged once, by the split
+        // workgroups themselves through granules (sa_merge_split, xa_merge_split: each merges
+        // 1 / SPLITS of its head's / slot's outputs), not by every O-projection / FFN-up
+        // workgroup's prologue (196 / 245 KiB each at 16 slots); the same arithmetic, so
+        // batches still reproduce single runs
         const bool merge16 = NB == 16 && m.weight_mode == MP_WEIGHTS_BF16 && !dev->xa_direct;
-        if (merge16) { a.merged = dev->sa_out; a.cnt = dev->sacnt; }
+        if (merge16) { a.merged = dev->sa_out; a.gh = dev->sagh; a.iter = dev->ndone + 1; a.hx_err = dev->ndone + 2; }
         // (not at 16 slots: bf16 B=16 20.1k vs 21.5k frames/s; both forms compute the
         // same bits)
         // (Q8_0: the same hand-off in the int8 MFMA launch, mp_decode_q8.hip; MAGPIE_Q8_UNFUSED=1
@@ -1009,7 +1010,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             mp::GemvFn fn = tb.oproj_xa;
             if (merge16) {
                 g.part = nullptr; g.src = dev->sa_out; g.src_ld = 768;
-                xp.x2 = dev->x2; xp.cnt = dev->xacnt;
+                xp.x2 = dev->x2; xp.gh = dev->xagh;
                 fn = mp::b16_oproj_xa_pm_16;
             }
             g.xa = xp; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
@@ -1721,6 +1722,8 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xqh, 0, (size_t)NB * 128 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->ltgh, 0, (size_t)NB * mp::LTS_P * 256 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->sagh, 0, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->xagh, 0, (size_t)NB * mp::XA_SPLITS * mp::XA_PART * 8, dev->stream));
     // the first frame's decoder input (the BOS codes); later frames' by lt_finalize_kernel
     HIPCHK(mp::op_embed(mp::EmbP{dev->m.audio_emb, dev->codes_prev, dev->m.dec_pos, dev->pos, dev->x}, NB, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go

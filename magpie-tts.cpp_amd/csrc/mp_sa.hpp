@@ -148,12 +148,13 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
         num = fmaf(e, wo[q][tid], num);
     }
     float *pp = p.part + ((size_t)(b * NH + h) * SA_SPLITS + sp) * SA_PART;
-    if (p.merged) {  // write-through: the head's last split workgroup merges (sa_merge_last)
-        gf32 *gp = (gf32 *)pp;
-        __hip_atomic_store(gp + 4 + tid, num, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p.merged) {  // granules: the head's split workgroups merge them (sa_merge_split)
+        const unsigned long long tag = (unsigned long long)((unsigned)p.iter[0] * 64u + p.layer + 1u) << 32;
+        gu64 *g = (gu64 *)p.gh + ((size_t)(b * NH + h) * SA_SPLITS + sp) * SA_PART;
+        __hip_atomic_store(g + 4 + tid, tag | __float_as_uint(num), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (tid == 0) {
-            __hip_atomic_store(gp, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gp + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(g, tag | __float_as_uint(M), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(g + 1, tag | __float_as_uint(den), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
     }
@@ -161,30 +162,40 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
     if (tid == 0) { pp[0] = M; pp[1] = den; }
 }
 
-// AttnP::merged: every thread of the workgroup after sa_part. The split's stores are
-// drained, the workgroup counts in on its head's counter (monotonic: the last of every
-// SA_SPLITS arrivals), and the last one merges the head's SA_SPLITS states with
-// PRO_SA_MERGE's arithmetic (split_weights, split_merge), whoever it is.
-__device__ __forceinline__ void sa_merge_last(const AttnP &p, int h, int b) {
-    __shared__ int last;
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add((gu32 *)p.cnt + b * NH + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) %
-                   SA_SPLITS == SA_SPLITS - 1;
-    __syncthreads();
+// AttnP::merged (16 slots), after sa_part: split sp of head h merges dims
+// [16 sp, 16 sp + 16) of the head from the SA_SPLITS states' granules (one lane per dim,
+// a bounded sweep), with PRO_SA_MERGE's arithmetic (split_weights, split_merge)
+__device__ __forceinline__ void sa_merge_split(const AttnP &p, int h, int sp, int b) {
+    constexpr int MD = DH / SA_SPLITS;
     const int tid = threadIdx.x;
-    if (!last || tid >= DH) return;
-    const gf32 *pp = (const gf32 *)p.part + (size_t)(b * NH + h) * SA_SPLITS * SA_PART;
+    if (tid >= MD) return;  // one partial wave: no barrier follows
+    const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+    const gu64 *g = (const gu64 *)p.gh + (size_t)(b * NH + h) * SA_SPLITS * SA_PART;
+    const int d = MD * sp + tid;
     float ms[SA_SPLITS], ls[SA_SPLITS], o[SA_SPLITS], e[SA_SPLITS], rd;
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
 #pragma unroll
-    for (int s = 0; s < SA_SPLITS; ++s) {
-        ms[s] = __hip_atomic_load(pp + s * SA_PART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ls[s] = __hip_atomic_load(pp + s * SA_PART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        o[s] = __hip_atomic_load(pp + s * SA_PART + 4 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int s = 0; s < SA_SPLITS; ++s) {
+            const unsigned long long um = __hip_atomic_load(g + s * SA_PART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long ul = __hip_atomic_load(g + s * SA_PART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long uo = __hip_atomic_load(g + s * SA_PART + 4 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok &= (unsigned)(um >> 32) == tag && (unsigned)(ul >> 32) == tag && (unsigned)(uo >> 32) == tag;
+            ms[s] = __uint_as_float((unsigned)um);
+            ls[s] = __uint_as_float((unsigned)ul);
+            o[s] = __uint_as_float((unsigned)uo);
+        }
+        if (__all(ok)) break;
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+            if (tid == 0) __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_SA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int s = 0; s < SA_SPLITS; ++s) o[s] = __builtin_nanf("");
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
     split_weights<SA_SPLITS>(ms, ls, e, rd);
-    p.merged[(size_t)b * D + h * DH + tid] = split_merge<SA_SPLITS>(e, o, rd);
+    p.merged[(size_t)b * D + h * DH + d] = split_merge<SA_SPLITS>(e, o, rd);
 }
 
 // EPI_QKV_SA epilogue, output (row n, slot b): EPI_QKV's stores, and the value

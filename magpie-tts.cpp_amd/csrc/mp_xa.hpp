@@ -29,8 +29,6 @@ static_assert(XA_THREADS == MP_BLOCK, "XA workgroups ride in the O-projection la
 constexpr unsigned HX_SPIN_LIMIT = 1u << 20;
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 using gi32 = __attribute__((address_space(1))) int;
-using gu32 = __attribute__((address_space(1))) unsigned;
-using gf32 = __attribute__((address_space(1))) float;
 
 // Split sp of slot b. HANDOFF: x1 comes from the O-projection in the same launch,
 // as {tag, value} granules xh[b][768] (EPI_RESID_XA): every wave sweeps all 768
@@ -161,6 +159,7 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
         den += e[q] * wl[q];
     }
     float *pp = p.part + ((size_t)b * XA_SPLITS + sp) * XA_PART;
+    const unsigned long long tagx = (unsigned long long)tag << 32;  // XaP::x2: the granules' tag
     if (tid < D / 4) {
         float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -168,64 +167,66 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
             const float4 v4 = *(const float4 *)&wo[q][4 * tid];
             num.x += e[q] * v4.x; num.y += e[q] * v4.y; num.z += e[q] * v4.z; num.w += e[q] * v4.w;
         }
-        if (p.x2) {  // write-through: the slot's last split workgroup merges (xa_merge_last)
-            gf32 *gp = (gf32 *)pp + 4 + 4 * tid;
-            __hip_atomic_store(gp, num.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gp + 1, num.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gp + 2, num.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gp + 3, num.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p.x2) {  // granules: the slot's split workgroups merge them (xa_merge_split)
+            gu64 *g = (gu64 *)p.gh + ((size_t)b * XA_SPLITS + sp) * XA_PART + 4 + 4 * tid;
+            __hip_atomic_store(g, tagx | __float_as_uint(num.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(g + 1, tagx | __float_as_uint(num.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(g + 2, tagx | __float_as_uint(num.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(g + 3, tagx | __float_as_uint(num.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             *(float4 *)(pp + 4 + 4 * tid) = num;
         }
     }
     if (tid == 0) {
         if (p.x2) {
-            __hip_atomic_store((gf32 *)pp, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((gf32 *)pp + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gu64 *g = (gu64 *)p.gh + ((size_t)b * XA_SPLITS + sp) * XA_PART;
+            __hip_atomic_store(g, tagx | __float_as_uint(M), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(g + 1, tagx | __float_as_uint(den), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             pp[0] = M; pp[1] = den;
         }
     }
 }
 
-// XaP::x2 (16 slots): every thread of an XA workgroup after xa_part. The split's
-// stores are drained, the workgroup counts in on its slot's counter (monotonic: the
-// last of every XA_SPLITS arrivals), and the last one writes x2 = x1 + the merged XA
-// output with PRO_XA_LN's arithmetic (split_weights, split_merge4, xa_x2), x1 from
-// the granules this workgroup has already seen complete.
-__device__ __forceinline__ void xa_merge_last(const XaP &p, int b, const unsigned long long *xh) {
-    __shared__ int last;
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add((gu32 *)p.cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % XA_SPLITS ==
-               XA_SPLITS - 1;
-    __syncthreads();
+// XaP::x2 (16 slots), after xa_part: split sp of slot b merges outputs
+// [192 sp, 192 sp + 192) from the XA_SPLITS states' granules (one thread per output, a
+// bounded sweep) and writes x2 = x1 + merged XA with PRO_XA_LN's arithmetic
+// (split_weights, split_merge, xa_x2), x1 from the granules this workgroup saw complete.
+__device__ __forceinline__ void xa_merge_split(const XaP &p, int sp, int b, const unsigned long long *xh, unsigned tag,
+                                               int *err) {
+    constexpr int MO = D / XA_SPLITS;
     const int tid = threadIdx.x;
-    if (!last || tid >= D / 4) return;
-    const gf32 *pp = (const gf32 *)p.part + (size_t)b * XA_SPLITS * XA_PART;
-    float ms[XA_SPLITS], ls[XA_SPLITS], e[XA_SPLITS], rd;
-    float4 o[XA_SPLITS];
+    if (tid >= MO) return;  // no barrier follows
+    const gu64 *g = (const gu64 *)p.gh + (size_t)b * XA_SPLITS * XA_PART;
+    const int k = MO * sp + tid;
+    float ms[XA_SPLITS], ls[XA_SPLITS], o[XA_SPLITS], e[XA_SPLITS], rd;
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
 #pragma unroll
-    for (int s = 0; s < XA_SPLITS; ++s) {
-        const gf32 *q = pp + s * XA_PART;
-        ms[s] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ls[s] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        o[s] = make_float4(__hip_atomic_load(q + 4 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __hip_atomic_load(q + 5 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __hip_atomic_load(q + 6 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __hip_atomic_load(q + 7 + 4 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        for (int s = 0; s < XA_SPLITS; ++s) {
+            const unsigned long long um = __hip_atomic_load(g + s * XA_PART, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long ul = __hip_atomic_load(g + s * XA_PART + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long uo = __hip_atomic_load(g + s * XA_PART + 4 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok &= (unsigned)(um >> 32) == tag && (unsigned)(ul >> 32) == tag && (unsigned)(uo >> 32) == tag;
+            ms[s] = __uint_as_float((unsigned)um);
+            ls[s] = __uint_as_float((unsigned)ul);
+            o[s] = __uint_as_float((unsigned)uo);
+        }
+        if (__all(ok)) break;
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+            if ((tid & 63) == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int s = 0; s < XA_SPLITS; ++s) o[s] = __builtin_nanf("");
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
-    const gu64 *g = (const gu64 *)xh + (size_t)b * D + 4 * tid;
-    float x1[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        x1[i] = __uint_as_float((unsigned)__hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const float x1 = __uint_as_float((unsigned)__hip_atomic_load((const gu64 *)xh + (size_t)b * D + k, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT));
     split_weights<XA_SPLITS>(ms, ls, e, rd);
-    const float4 a = split_merge4<XA_SPLITS>(e, o, rd);
-    *(float4 *)(p.x2 + (size_t)b * D + 4 * tid) = xa_x2(a, make_float4(x1[0], x1[1], x1[2], x1[3]));
+    const float a = split_merge<XA_SPLITS>(e, o, rd);
+    p.x2[(size_t)b * D + k] = xa_x2(make_float4(a, 0.f, 0.f, 0.f), make_float4(x1, 0.f, 0.f, 0.f)).x;
 }
-
 
 // EPI_RESID_XA epilogue, output (row n, slot b): resid += v, and the new x1 value
 // published as a {tag, value} granule with a relaxed agent-scope (write-through) store
@@ -243,7 +244,7 @@ __device__ __forceinline__ void xa_tail(const GemvP &p, unsigned long long t_sta
     const int k = blockIdx.x - p.nrow_blocks;
     xa_part<true>(p.xa, k % XA_SPLITS, k / XA_SPLITS, p.xh, (unsigned)p.iter[0] * 64u + p.layer + 1u, p.hx_err,
                   ts_dep(t_start), p.ts, t_start);
-    if (p.xa.x2) xa_merge_last(p.xa, k / XA_SPLITS, p.xh);
+    if (p.xa.x2) xa_merge_split(p.xa, k % XA_SPLITS, k / XA_SPLITS, p.xh, (unsigned)p.iter[0] * 64u + p.layer + 1u, p.hx_err);
     ts_end(p.ts, t_start);
 }
 

@@ -275,9 +275,10 @@ MP_F16_OPS(2)
 MP_F16_OPS(4)
 MP_F16_OPS(8)
 MP_F16_OPS(16)
-// bf16 mode at 16 slots: the O-projection + XA launch reads the SA output the SA
-// kernel's last-arriver merge wrote (plain rows), and its XA workgroups merge x2
+// bf16 mode at 8 and 16 slots: the O-projection + XA launch reads the SA output its
+// split workgroups merged (plain rows), and its XA workgroups merge x2
 hipError_t b16_oproj_xa_pm_16(const GemvP &p, hipStream_t s) { return launch_b16<16, D, PRO_PLAIN, EPI_RESID_XA>(p, s); }
+hipError_t b16_oproj_xa_pm_8(const GemvP &p, hipStream_t s) { return launch_b16<8, D, PRO_PLAIN, EPI_RESID_XA>(p, s); }
 // the LT in_proj of an F16 file is F16 too (the bf16 mode keeps it f32)
 hipError_t f16_lt_in0_1(const GemvP &p, hipStream_t s) { return launch_b16<1, D, PRO_LN, EPI_BIAS, true>(p, s); }
 hipError_t f16_lt_in0_2(const GemvP &p, hipStream_t s) { return launch_b16<2, D, PRO_LN, EPI_BIAS, true>(p, s); }

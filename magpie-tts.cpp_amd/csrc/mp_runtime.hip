@@ -112,6 +112,7 @@ hipError_t op_lt_slot(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_kvo(const GemvP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t b16_oproj_xa_pm_16(const GemvP &, hipStream_t);
+hipError_t b16_oproj_xa_pm_8(const GemvP &, hipStream_t);
 hipError_t op_xa(const XaP &, int, hipStream_t);
 hipError_t op_xa_q8(const XaQ8P &, int, hipStream_t);
 hipError_t op_finalize(const FinP &, int, hipStream_t);
@@ -947,12 +948,12 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // self-attention over the cache, split over keys (3457-3476); the f32 family runs
         // it in the QKV launch on a hand-off of q|k|v (EPI_QKV_SA), the others separately
         mp::AttnP a{dev->q, dev->kc, dev->vc, l, L, dev->max_seq, dev->pos, dev->kv16, dev->sa_part};
-        // bf16 mode at 16 slots: the SA and XA split states are merged once, by the split
+        // bf16 mode at 8 and 16 slots: the SA and XA split states are merged once, by the split
         // workgroups themselves through granules (sa_merge_split, xa_merge_split: each merges
         // 1 / SPLITS of its head's / slot's outputs), not by every O-projection / FFN-up
         // workgroup's prologue (196 / 245 KiB each at 16 slots); the same arithmetic, so
-        // batches still reproduce single runs
-        const bool merge16 = NB == 16 && m.weight_mode == MP_WEIGHTS_BF16 && !dev->xa_direct;
+        // batches still reproduce single runs (at 8 slots the SA merge runs in the QKV launch)
+        const bool merge16 = NB >= 8 && m.weight_mode == MP_WEIGHTS_BF16 && !dev->xa_direct;
         if (merge16) { a.merged = dev->sa_out; a.gh = dev->sagh; a.iter = dev->ndone + 1; a.hx_err = dev->ndone + 2; }
         // (not at 16 slots: bf16 B=16 20.1k vs 21.5k frames/s; both forms compute the
         // same bits)
@@ -1011,7 +1012,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             if (merge16) {
                 g.part = nullptr; g.src = dev->sa_out; g.src_ld = 768;
                 xp.x2 = dev->x2; xp.gh = dev->xagh;
-                fn = mp::b16_oproj_xa_pm_16;
+                fn = NB == 16 ? mp::b16_oproj_xa_pm_16 : mp::b16_oproj_xa_pm_8;
             }
             g.xa = xp; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
             if ((rc = run("oproj_xa", fn, g, F * (768.0 * 768) + A * act * (768 * 3) + xa_bytes)) != MP_OK)

@@ -222,6 +222,7 @@ __device__ __forceinline__ void sa_tail(const GemvP &p, unsigned long long t_sta
     const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
     if (p.sa.kv16) sa_part<true, MP_NWAVES, true>(p.sa, h, sp, b, p.qh, tag, p.hx_err, ts_dep(t_start));
     else sa_part<false, MP_NWAVES, true>(p.sa, h, sp, b, p.qh, tag, p.hx_err, ts_dep(t_start));
+    if (p.sa.merged) sa_merge_split(p.sa, h, sp, b);
     ts_end(p.ts, t_start);
 }
 

@@ -749,6 +749,165 @@ hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- LT front, f32 batch 1
+// LtFrontP (mp_params.hpp). Workgroup p, wave w: in_proj row 4p + w exactly as
+// gemv_kernel<1, 1, 768, PRO_LN, EPI_BIAS> computes it, rows 4p + w and 256 + 4p + w of
+// [W_k ; W_o W_v] as gemv_kernel<1, 1, 256, PRO_LTX_LN, EPI_LTKVO> does, then the FFN
+// step of lt_ffn2_kernel<1> for codebook 0 (y = X_0 + vo_0). The two all-to-all edges
+// (in_proj output -> LN(X_0); vo_0 -> y) are 256-value granule sweeps (2 KiB) by the
+// 64 workgroups of the launch, all co-resident.
+__device__ __forceinline__ float gh_wait(const unsigned long long *g, unsigned tag, int *err) {
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned long long u = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((unsigned)(u >> 32) == tag)) return __uint_as_float((unsigned)u);
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison and say so
+            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return __builtin_nanf("");
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+__global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
+    const unsigned long long t_start = ts_begin(p.l.f.ts);
+    constexpr int U = LTF / LT_FFN_P, UPW = U / MP_NWAVES, PER = D / 64, Q = PER / MP_NWAVES;
+    static_assert(U % MP_NWAVES == 0 && LTD == MP_BLOCK && LT_FFN_P * MP_NWAVES == LTD, "unit split");
+    __shared__ __attribute__((aligned(16))) float act[D];
+    __shared__ __attribute__((aligned(16))) float act2[LTD];
+    __shared__ __attribute__((aligned(16))) float xs[LTD];
+    __shared__ __attribute__((aligned(16))) float fs[U];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, pb = blockIdx.x;
+    const int n_in = pb * MP_NWAVES + w + ts_dep(t_start);  // this wave's in_proj / k / vo row
+    // every weight of the launch first: in_proj row, k and vo rows, the FFN slice
+    float4 wi[3], wk, wv;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) wi[i] = *(const float4 *)(p.w_in + (size_t)n_in * D + 4 * (lane + 64 * i));
+    wk = *(const float4 *)(p.w_kvo + (size_t)n_in * LTD + 4 * lane);
+    wv = *(const float4 *)(p.w_kvo + (size_t)(LTD + n_in) * LTD + 4 * lane);
+    const int j0 = pb * U;
+    float4 a1[UPW], a2[U / 4];
+#pragma unroll
+    for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.l.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
+#pragma unroll
+    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.l.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i);
+    const unsigned tag_s = (unsigned)p.iter[0] * 64u + 40u, tag_v = tag_s + 1u;
+    // ---- LN(x) (PRO_LN, batch 1: every wave the whole row, writes its quarter)
+    {
+        float v[PER], g[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) v[i] = p.x[lane + 64 * i];
+        load_lnw<PER>(p.norm_out, g);
+        float mean, var;
+        wave_meanvar<PER>(v, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.l.f.eps);
+        const bool st = p.hidden_out && pb == 0;
+        const int s = (p.trace && pb == 0) ? p.l.step[0] : 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (i / Q != w) continue;
+            const int k = lane + 64 * i;
+            const float y = ((v[i] - mean) * rstd) * g[i];
+            act[k] = y;
+            if (st) p.hidden_out[k] = y;
+            if (p.trace && pb == 0 && s < p.trace_steps) p.trace[(size_t)s * D + k] = y;
+        }
+    }
+    lds_sync();
+    // ---- in_proj row n_in (+ bias), published
+    {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) s += dotv(wi[i], ((const float4 *)act)[lane + 64 * i]);
+        const float v = wave_sum(s) + p.b_in[n_in];
+        if (lane == 0) {
+            p.lt_s[n_in] = v;
+            __hip_atomic_store((gu64 *)p.gh + n_in, ((unsigned long long)tag_s << 32) | __float_as_uint(v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // ---- X_0 = s + lt_pos[0], LN(X_0) (PRO_LTX_LN's one-wave statistics): wave 0
+    if (w == 0) {
+        float g[4], X[4];
+        load_lnw<4>(p.norm_self, g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = lane + 64 * i;
+            X[i] = gh_wait(p.gh + k, tag_s, p.hx_err) + p.lt_pos[k];
+        }
+        if (pb == 0)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) const_cast<float *>(p.l.ltX)[lane + 64 * i] = X[i];  // lt_kvo wrote it
+        float mean, var;
+        wave_block_meanvar<1>(X, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.l.f.eps);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) act2[lane + 64 * i] = ((X[i] - mean) * rstd) * g[i];
+    }
+    lds_sync();
+    // ---- k_0 row and vo_0 row n_in (EPI_LTKVO); vo_0 published
+    {
+        const float4 av = *(const float4 *)&act2[4 * lane];
+        float sk = 0.f, sv = 0.f;  // gemv_kernel's accumulation, term for term
+        sk += dotv(wk, av);
+        sv += dotv(wv, av);
+        const float k0 = wave_sum(sk), vo0 = wave_sum(sv);
+        if (lane == 0) {
+            p.l.ltk[n_in] = k0;
+            p.l.ltv[n_in] = vo0;
+            __hip_atomic_store((gu64 *)p.gh + LTD + n_in, ((unsigned long long)tag_v << 32) | __float_as_uint(vo0),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // ---- codebook 0's FFN step (lt_ffn2_kernel<1>: y = X_0 + vo_0, wave 0)
+    if (w == 0) {
+        float xv[4], vv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int k = 4 * lane + c;
+            xv[c] = gh_wait(p.gh + k, tag_s, p.hx_err) + p.lt_pos[k];
+            vv[c] = gh_wait(p.gh + LTD + k, tag_v, p.hx_err);
+        }
+        const float4 y = make_float4(xv[0] + vv[0], xv[1] + vv[1], xv[2] + vv[2], xv[3] + vv[3]);
+        if (pb == 0) *(float4 *)((float *)p.l.f.y + 4 * lane) = y;
+        const float x[4] = {y.x, y.y, y.z, y.w};
+        float mean, var;
+        wave_meanvar<4>(x, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.l.f.eps);
+        const float4 g = *(const float4 *)(p.l.f.lnw + 4 * lane);
+        *(float4 *)&xs[4 * lane] = make_float4(((x[0] - mean) * rstd) * g.x, ((x[1] - mean) * rstd) * g.y,
+                                               ((x[2] - mean) * rstd) * g.z, ((x[3] - mean) * rstd) * g.w);
+    }
+    lds_sync();
+    {
+        const float4 xv = *(const float4 *)&xs[4 * lane];
+#pragma unroll
+        for (int r = 0; r < UPW; ++r) {
+            const float v = wave_sum(dotv(a1[r], xv));
+            if (lane == 0) fs[w * UPW + r] = gelu_tanh(v);
+        }
+    }
+    lds_sync();
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < U / 4; ++i) {
+        const float4 f4 = *(const float4 *)&fs[4 * i];
+        acc = fmaf(a2[i].x, f4.x, acc);
+        acc = fmaf(a2[i].y, f4.y, acc);
+        acc = fmaf(a2[i].z, f4.z, acc);
+        acc = fmaf(a2[i].w, f4.w, acc);
+    }
+    p.l.f.part[(size_t)pb * LTD + tid] = acc;
+    ts_end(p.l.f.ts, t_start);
+}
+hipError_t op_lt_front(const LtFrontP &p, hipStream_t s) {
+    static_assert(sizeof(LtFrontP) < 4096, "kernel argument size");
+    if (!p.x || !p.norm_out || !p.w_in || !p.b_in || !p.lt_s || !p.lt_pos || !p.norm_self || !p.w_kvo || !p.gh ||
+        !p.iter || !p.hx_err || !p.l.f.y || !p.l.f.lnw || !p.l.f.w1 || !p.l.f.w2 || !p.l.f.part || !p.l.ltX ||
+        !p.l.ltk || !p.l.ltv || !p.l.step || p.l.cb != 0)
+        return hipErrorInvalidValue;
+    mp::launch(lt_front_kernel, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
 // the LT head at batch 1 with the FFN merge as its prologue
 hipError_t op_lt_em_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 2, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 // f32 LT position 0: LN(X_0) -> [k_0 | vo_0] (W = [W_k ; W_o W_v], 512 x 256)

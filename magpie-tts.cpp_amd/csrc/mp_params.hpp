@@ -131,6 +131,28 @@ struct LtFfn2P {
     int *hx_err;
 };
 
+// f32 mode at batch 1: the LT's front in ONE launch (lt_front_kernel) instead of three
+// (lt_in0, lt_kvo, lt_ffn2 of codebook 0): in_proj of LN(x) (rows 4p + w of workgroup p)
+// and the rows of [W_k ; W_o W_v] LN(X_0) are handed between the 64 workgroups as
+// {tag, value} granules gh[2][256] (tags iter[0] * 64 + 40, + 41), then codebook 0's FFN
+// step as lt_ffn2_kernel computes it. Every row is computed with the same arithmetic as
+// the three separate launches, so batch 1 equals the batched path bit for bit.
+struct LtFrontP {
+    LtFfn2P l;                 // the codebook-0 FFN step (cb = 0): FFN weights, partials, y, ltX, ltk, ltv
+    const float *x;            // [768] decoder output (final LN input)
+    const float *norm_out;     // final decoder LayerNorm weight
+    const float *w_in, *b_in;  // LT in_proj [256][768] + bias
+    float *lt_s;               // [9][256] in_proj output (row 0 written)
+    float *hidden_out;         // [768] LN(x) (magpie_synthesize's hidden), nullable
+    float *trace;              // [trace_steps][768] per-step LN(x) (nullable)
+    int trace_steps;
+    const float *lt_pos, *norm_self;
+    const float *w_kvo;        // [512][256] = [W_k ; W_o W_v]
+    unsigned long long *gh;    // [2][256] granules: in_proj output, vo_0
+    const int *iter;
+    int *hx_err;
+};
+
 // Frame embedding of every slot (layer 0's residual input, magpie.cpp:2746-2787,
 // 4376-4379): x[b] = (sum_cb emb[cb][code_cb]) / 8 + pos_emb[pos[b]]
 struct EmbP {

@@ -109,6 +109,7 @@ hipError_t op_lt_ffn(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_ffn2(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_slot(const LtFfn2P &, int, hipStream_t);
+hipError_t op_lt_front(const LtFrontP &, hipStream_t);
 hipError_t op_lt_kvo(const GemvP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t b16_oproj_xa_pm_16(const GemvP &, hipStream_t);
@@ -228,7 +229,7 @@ struct Model {
 };
 
 enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9,
-              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12 };
+              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12, K_LTFRONT = 13 };
 struct OpRec {
     std::string name;
     int kind;
@@ -240,6 +241,7 @@ struct OpRec {
     XaQ8P xq;
     LtFfnP lf;
     LtFfn2P l2;
+    LtFrontP lf3;
     EmbP e;
     int B;
     double bytes;
@@ -253,6 +255,7 @@ struct LtIo {
     float *lt_s, *ltX, *ltY, *lty2, *ltq, *ltk, *ltv, *ltf, *logits;
     float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel; lt_slot_kernel: [NB][LTS_P][256])
     unsigned long long *ltgh;  // [NB][LTS_P][256] lt_slot_kernel's partial-sum granules
+    unsigned long long *ltfg;  // [2][256] lt_front_kernel's hand-off granules (f32, batch 1)
     int *iter, *hx_err;        // decode iteration counter (hand-off tags), hand-off error bits
     int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
     SmpCfg *cfg;
@@ -293,7 +296,7 @@ struct mp_dev {
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
-    unsigned long long *ltgh = nullptr;
+    unsigned long long *ltgh = nullptr, *ltfg = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
         *argeos = nullptr, *amax = nullptr;
@@ -870,7 +873,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
-    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * mp::LTS_P * 256);
+    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * mp::LTS_P * 256); A(ltfg, 2 * 256);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -1077,7 +1080,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     io.x = dev->x; io.hidden = dev->hidden; io.trace = dev->trace; io.trace_steps = dev->max_steps + 1;
     io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
     io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits; io.ltp = dev->ltp;
-    io.ltgh = dev->ltgh; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
+    io.ltgh = dev->ltgh; io.ltfg = dev->ltfg; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
     io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
     io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
     io.amax = dev->amax; io.cfg = dev->smpcfg;
@@ -1151,6 +1154,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         return g;
     };
     int rc;
+    // f32 mode at batch 1: final LN + in_proj + position 0 + codebook 0's FFN step in one
+    // launch (lt_front_kernel: the same rows, the same arithmetic; 2 in-launch granule edges)
+    const bool front = f32_lt_mode(m) && NB == 1 && !io.lt_only && io.ltfg && io.iter;
     {
         mp::GemvP g = base();
         g.W = m.lt_in_w; g.N = 256; g.bias = m.lt_in_b; g.out = io.lt_s; g.out_ld = 9 * 256;
@@ -1162,6 +1168,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             if ((rc = run("lt_inh", m.lt_in8 ? mp::q8_lt_inh_1 : m.pk_lt_in ? mp::f16_lt_inh_1 : mp::op_lt_inh_1, g,
                           Fi * 256.0 * 768 + A * 256 + A * (768 + 256))) != MP_OK)
                 return rc;
+        } else if (front) {
+            // f32, batch 1: lt_front_kernel below runs the final LN, in_proj, position 0 and
+            // codebook 0's FFN step in one launch
         } else {
             // final LN -> hidden (4394) fused into LT in_proj (1162-1163)
             g.lnw = m.dec_norm_out; g.src = io.x; g.src_ld = 768; g.hidden_out = io.hidden;
@@ -1225,14 +1234,16 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
         mp::GemvP g = base(); g.cb = 0;
         g.W = m.lt_kvo; g.N = 512; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX; g.lnw = m.lt_norm_self;
         g.lk = io.ltk; g.lv = io.ltv;
-        if (ops) {
-            mp::OpRec r{};
-            r.name = "lt_kvo"; r.kind = mp::K_LTKVO; r.g = g; r.B = NB;
-            r.bytes = A * (512.0 * 256) + A * act * (256 * 4);
-            ops->push_back(r);
+        if (!front) {
+            if (ops) {
+                mp::OpRec r{};
+                r.name = "lt_kvo"; r.kind = mp::K_LTKVO; r.g = g; r.B = NB;
+                r.bytes = A * (512.0 * 256) + A * act * (256 * 4);
+                ops->push_back(r);
+            }
+            HIPCHK(mp::op_lt_kvo(g, NB, s));
+            dump_lt(io, s);
         }
-        HIPCHK(mp::op_lt_kvo(g, NB, s));
-        dump_lt(io, s);
         for (int cb = 0; cb < 8; ++cb) {
             mp::LtFfn2P l2{};
             l2.f = mp::LtFfnP{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2s, m.eps, io.ltp, io.lty2};
@@ -1241,15 +1252,32 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             l2.codes_cur = io.codes_cur; l2.step = io.step; l2.ignore_eos = io.ignore_eos;
             l2.audio_bos = m.audio_bos; l2.audio_eos = m.audio_eos;
             l2.smp = mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax};
-            if (ops) {
-                mp::OpRec r{};
-                r.name = "lt_ffn2"; r.kind = mp::K_LTFFN2; r.l2 = l2; r.B = NB;
-                r.bytes = A * (1024.0 * 256 * 2) + A * act * (cb ? 2024 + 4 * 256 + 2 * 256 * cb : 512) +
-                          A * act * (mp::LT_FFN_P * 256 + 256);
-                ops->push_back(r);
+            if (front && cb == 0) {
+                mp::LtFrontP fp{};
+                fp.l = l2; fp.x = io.x; fp.norm_out = m.dec_norm_out; fp.w_in = m.lt_in_w; fp.b_in = m.lt_in_b;
+                fp.lt_s = io.lt_s; fp.hidden_out = io.hidden; fp.lt_pos = m.lt_pos; fp.norm_self = m.lt_norm_self;
+                fp.w_kvo = m.lt_kvo; fp.gh = io.ltfg; fp.iter = io.iter; fp.hx_err = io.hx_err;
+                if (io.trace) { fp.trace = io.trace; fp.trace_steps = io.trace_steps; }
+                if (ops) {
+                    mp::OpRec r{};
+                    r.name = "lt_front"; r.kind = mp::K_LTFRONT; r.lf3 = fp; r.B = NB;
+                    r.bytes = A * (256.0 * 768 + 512.0 * 256 + 1024.0 * 256 * 2) + A * (768 * 2 + 256 * 4) +
+                              A * (mp::LT_FFN_P * 256);
+                    ops->push_back(r);
+                }
+                HIPCHK(mp::op_lt_front(fp, s));
+                dump_lt(io, s);
+            } else {
+                if (ops) {
+                    mp::OpRec r{};
+                    r.name = "lt_ffn2"; r.kind = mp::K_LTFFN2; r.l2 = l2; r.B = NB;
+                    r.bytes = A * (1024.0 * 256 * 2) + A * act * (cb ? 2024 + 4 * 256 + 2 * 256 * cb : 512) +
+                              A * act * (mp::LT_FFN_P * 256 + 256);
+                    ops->push_back(r);
+                }
+                HIPCHK(mp::op_lt_ffn2(l2, NB, s));
+                dump_lt(io, s);
             }
-            HIPCHK(mp::op_lt_ffn2(l2, NB, s));
-            dump_lt(io, s);
             if (NB > 1) {
                 if (ops) {
                     mp::OpRec r{};
@@ -1723,6 +1751,7 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xqh, 0, (size_t)NB * 128 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->ltgh, 0, (size_t)NB * mp::LTS_P * 256 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->ltfg, 0, 2 * 256 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->sagh, 0, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xagh, 0, (size_t)NB * mp::XA_SPLITS * mp::XA_PART * 8, dev->stream));
     // the first frame's decoder input (the BOS codes); later frames' by lt_finalize_kernel
@@ -2082,6 +2111,7 @@ static hipError_t launch_rec(const mp::OpRec &r, hipStream_t s) {
     case mp::K_LTPICK: return mp::op_lt_pick(r.g, r.B, s);
     case mp::K_LTFFN2: return mp::op_lt_ffn2(r.l2, r.B, s);
     case mp::K_LTSLOT: return mp::op_lt_slot(r.l2, r.B, s);
+    case mp::K_LTFRONT: return mp::op_lt_front(r.lf3, s);
     case mp::K_LTKVO: return mp::op_lt_kvo(r.g, r.B, s);
     case mp::K_EMBED: return mp::op_embed(r.e, r.B, s);
     case mp::K_FIN: return mp::op_finalize(r.f, r.B, s);
@@ -2146,7 +2176,7 @@ int mp_hip_profile_ops_ts(mp_dev *dev, int iters, float *avg_us) {
         for (int i = 0; i < n; ++i) {
             mp::OpRec r = dev->ops[i];
             unsigned long long *t = ts + (size_t)i * per;
-            r.g.ts = t; r.a.ts = t; r.x.ts = t; r.f.ts = t; r.lf.ts = t; r.l2.f.ts = t;
+            r.g.ts = t; r.a.ts = t; r.x.ts = t; r.f.ts = t; r.lf.ts = t; r.l2.f.ts = t; r.lf3.l.f.ts = t;
             const hipError_t e = launch_rec(r, dev->stream);
             if (e != hipSuccess) { rc = fail(dev, MP_ERR_HIP, std::string("profile launch: ") + hipGetErrorString(e)); break; }
         }

@@ -563,27 +563,40 @@ __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, f
                        x4.w + pos4.w + a.w / l);
 }
 
-// The LT step of codebook cb in f32 mode, one launch: y (lt_y_slot, every workgroup
-// for itself; workgroup 0 stores it as the head's residual), then LN + FFN up +
-// GELU + FFN down partial sums exactly as lt_ffn_kernel (workgroup p owns hidden
-// units [16p, 16p+16)).
+// a {tag, value} granule's value once the wave sees the tag on every lane (bounded)
+__device__ __forceinline__ float gh_wait(const unsigned long long *g, unsigned tag, int *err) {
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned long long u = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((unsigned)(u >> 32) == tag)) return __uint_as_float((unsigned)u);
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison and say so
+            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return __builtin_nanf("");
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+// The LT step of codebook cb in f32 mode: y (lt_y_slot, every workgroup for itself;
+// workgroup 0 stores it as the head's residual), then LN + FFN up + GELU + FFN down
+// partial sums exactly as lt_ffn_kernel (workgroup pb owns hidden units [16pb,
+// 16pb+16)). acc[b]: this thread's (output tid) partial sum of slot b; ys (nullable):
+// slot 0's y for the caller.
 template <int NB>
-__global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
-    const unsigned long long t_start = ts_begin(p.f.ts);
+__device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, float (&accs)[NB], float *ys) {
     constexpr int U = LTF / LT_FFN_P, UPW = U / MP_NWAVES;
     static_assert(U % MP_NWAVES == 0 && U % 4 == 0 && LTD == MP_BLOCK, "unit split");
     __shared__ __attribute__((aligned(16))) float xs[NB][LTD];
     __shared__ __attribute__((aligned(16))) float fs[NB][U];
     __shared__ __attribute__((aligned(16))) float wsc_all[MP_NWAVES][2 * VCB];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = blockIdx.x * U + ts_dep(t_start);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = pb * U + dep;
     float4 a1[UPW], a2[U / 4];
 #pragma unroll
     for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
 #pragma unroll
     for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i);
     for (int b = w; b < NB; b += MP_NWAVES) {
-        const float4 y = lt_y_slot(p, b, blockIdx.x == 0, wsc_all[w]);
-        if (blockIdx.x == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
+        const float4 y = lt_y_slot(p, b, pb == 0, wsc_all[w]);
+        if (pb == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
+        if (ys && b == 0) *(float4 *)&ys[4 * lane] = y;
         const float x[4] = {y.x, y.y, y.z, y.w};
         float mean, var;
         wave_meanvar<4>(x, mean, var);
@@ -614,10 +627,19 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
             acc = fmaf(a2[i].z, f4.z, acc);
             acc = fmaf(a2[i].w, f4.w, acc);
         }
-        p.f.part[((size_t)b * LT_FFN_P + blockIdx.x) * LTD + tid] = acc;
+        accs[b] = acc;
     }
+}
+template <int NB>
+__global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
+    const unsigned long long t_start = ts_begin(p.f.ts);
+    float accs[NB];
+    lt_step_body<NB>(p, blockIdx.x, ts_dep(t_start), accs, nullptr);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) p.f.part[((size_t)b * LT_FFN_P + blockIdx.x) * LTD + threadIdx.x] = accs[b];
     ts_end(p.f.ts, t_start);
 }
+
 hipError_t op_lt_ffn2(const LtFfn2P &p, int NB, hipStream_t s) {
     if (!p.f.y || !p.f.lnw || !p.f.w1 || !p.f.w2 || !p.f.part || !p.ltX || !p.ltk || !p.ltv || !p.qkvtab ||
         !p.votab || !p.ptab || !p.lt_pos || !p.logits || !p.codes_cur || !p.step || !p.smp.cfg || !p.smp.argeos ||
@@ -756,17 +778,6 @@ hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
 // step of lt_ffn2_kernel<1> for codebook 0 (y = X_0 + vo_0). The two all-to-all edges
 // (in_proj output -> LN(X_0); vo_0 -> y) are 256-value granule sweeps (2 KiB) by the
 // 64 workgroups of the launch, all co-resident.
-__device__ __forceinline__ float gh_wait(const unsigned long long *g, unsigned tag, int *err) {
-    for (unsigned spins = 0;; ++spins) {
-        const unsigned long long u = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__all((unsigned)(u >> 32) == tag)) return __uint_as_float((unsigned)u);
-        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison and say so
-            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return __builtin_nanf("");
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
 __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     const unsigned long long t_start = ts_begin(p.l.f.ts);
     constexpr int U = LTF / LT_FFN_P, UPW = U / MP_NWAVES, PER = D / 64, Q = PER / MP_NWAVES;

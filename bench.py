@@ -76,7 +76,8 @@ def _decode_fps(dev, B, frames, steps=2):
 def measure_extra(model_path: str, codec_path, args) -> dict:
     """Throughput of the BASELINE configs' other shapes on this one GPU (fixed-length
     greedy decode, same synthetic prompts): bf16 projections at batch 1, 8
-    (configs[3]'s per-GPU share of batch 64) and 16 (configs[2]); Q8_0 weights at
+    (configs[3]'s per-GPU share of batch 64) and 16 (configs[2]), and at 8 / 16 with a
+    bf16 SA cache as well; Q8_0 weights at
     batch 1 and 16 (int8 MFMA) and 60 s of long-form streaming (configs[4]); and the streaming path
     (sentence streaming, 4-frame codec chunks): time to first audio and real-time
     factor of one utterance."""
@@ -86,6 +87,14 @@ def measure_extra(model_path: str, codec_path, args) -> dict:
         toks = [ma.synthetic_tokens(args.tokens, seed=1000 + b) for b in range(B)]
         dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=args.frames, ignore_eos=True)
         out[f"bf16_batch{B}_fps"] = round(_decode_fps(dev, B, args.frames), 1)
+    dev.close()
+    # the same bf16 batches with the SA cache in bf16 too (mp_hip_set_kv_mode MP_KV_BF16: rows
+    # rounded on append; half the attention bytes, which dominate from 8 slots up)
+    dev = ma.Device(model_path, weights="bf16", kv="bf16")
+    for B in (8, 16):
+        toks = [ma.synthetic_tokens(args.tokens, seed=1000 + b) for b in range(B)]
+        dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=args.frames, ignore_eos=True)
+        out[f"bf16_kv16_batch{B}_fps"] = round(_decode_fps(dev, B, args.frames), 1)
     dev.close()
     # the reference converter's other file types at batch 1: F16 (ggml F16 mul_mat
     # semantics, f16 MFMA) and Q4_0 (on the Q8_0 kernels, int8 q - 8)

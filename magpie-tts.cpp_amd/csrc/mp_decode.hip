@@ -563,18 +563,6 @@ __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, f
                        x4.w + pos4.w + a.w / l);
 }
 
-// a {tag, value} granule's value once the wave sees the tag on every lane (bounded)
-__device__ __forceinline__ float gh_wait(const unsigned long long *g, unsigned tag, int *err) {
-    for (unsigned spins = 0;; ++spins) {
-        const unsigned long long u = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__all((unsigned)(u >> 32) == tag)) return __uint_as_float((unsigned)u);
-        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison and say so
-            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return __builtin_nanf("");
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
 // The LT step of codebook cb in f32 mode: y (lt_y_slot, every workgroup for itself;
 // workgroup 0 stores it as the head's residual), then LN + FFN up + GELU + FFN down
 // partial sums exactly as lt_ffn_kernel (workgroup pb owns hidden units [16pb,

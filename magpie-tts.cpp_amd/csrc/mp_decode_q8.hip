@@ -52,6 +52,8 @@ __device__ __forceinline__ float quad_max(float v) {
 
 __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char *actq, float *actd, unsigned long long t_start);
 __device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_start);
+__device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed char *actq, float *actd,
+                                           unsigned long long t_start);
 constexpr int XQG = 8;  // q_net workgroups per slot in EPI_RESID_XQ8 (16 rows each)
 
 template <int NB, int K, int PRO, int EPI, bool Q4>
@@ -80,6 +82,10 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     if constexpr (EPI == EPI_RESID_XQ8) {
         // then XQG x NB workgroups: the XA's q_net on this launch's x1; then XQ8A x NB:
         // the XA's attention + o_net on that q
+        if (NB <= XQ8_QIN_NB && rt >= p.nrow_blocks && p.xq8.qin) {
+            xq8qa_tail(p, act, actq, actd, t_start);
+            return;
+        }
         if (rt >= p.nrow_blocks + XQG * NB) {
             xq8a_tail(p, t_start);
             return;
@@ -188,6 +194,181 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     else if constexpr (EPI == EPI_RESID_XQ8) publish_x1(p, v, n, col);
     else epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
     ts_end(p.ts, t_start);
+}
+
+// ---------------------------------------------------------------- LT step, Q8_0 mode
+// LtSlotQ8P (mp_params.hpp). Workgroup (q, b), LTQ_P per slot at every batch size.
+// (Every workgroup computing all 256 o_net rows itself, so that y needs no hand-off,
+// measured no faster at batch 1: 12.47 vs 12.41 us per step.)
+constexpr int LTQ_U = LTF / LTQ_P, LTQ_UPW = LTQ_U / MP_NWAVES, LTQ_R = LTD / LTQ_P, LTQ_RW = LTQ_R / MP_NWAVES;
+__global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
+#pragma clang fp contract(off)
+    const unsigned long long t_start = ts_begin(p.ts);
+    static_assert(LTD == MP_BLOCK && LTQ_RW >= 1 && LTQ_RW * MP_NWAVES * LTQ_P == LTD && LTQ_U % 4 == 0, "split");
+    __shared__ __attribute__((aligned(16))) float xs[LTD];   // X (the attention residual), then LN(y)
+    __shared__ __attribute__((aligned(16))) float ys[LTD];
+    __shared__ __attribute__((aligned(16))) int aq[LTD / 4];  // the attention output as Q8_0 (4 int8 per lane)
+    __shared__ float ad[LTD / 32];
+    __shared__ __attribute__((aligned(16))) float fs[LTQ_U];
+    __shared__ float mv[LTQ_P][LTQ_R];
+    __shared__ __attribute__((aligned(16))) float wsc[2 * VCB];
+    const GemvP &g = p.g;
+    const int q = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, cb = g.cb;
+    const int dep = ts_dep(t_start);
+    // wave 0 first issues what its pick waits on (the logits, earlier positions' k / v;
+    // position 0's v and X), then every wave its weights: o_net rows (4 int8 per lane,
+    // the lane's block scale), FFN rows / slice
+    const size_t rowb = (size_t)b * NCB * LTD + 4 * lane;
+    float4 kr[NCB], vr[NCB], pos4, a4, x4;
+    float lv[PICK_R];
+    if (w == 0) {
+        if (cb > 0) {
+            load_logits(g.logits + (size_t)b * VCB, lv);
+#pragma unroll
+            for (int j = 0; j < NCB - 1; ++j)
+                if (j < cb) { kr[j] = *(const float4 *)(g.ltk + rowb + j * LTD); vr[j] = *(const float4 *)(g.ltv + rowb + j * LTD); }
+            pos4 = *(const float4 *)(g.lt_pos + (size_t)cb * LTD + 4 * lane);
+        } else {  // one position: softmax weight 1, a = v_0 (lt_attend computes exactly that)
+            a4 = *(const float4 *)(g.ltv + rowb);
+            x4 = *(const float4 *)(g.ltX + (size_t)b * LTD + 4 * lane);
+        }
+    }
+    const int r0 = q * LTQ_R + LTQ_RW * w + dep;
+    int wq[LTQ_RW];
+    float wd[LTQ_RW];
+#pragma unroll
+    for (int r = 0; r < LTQ_RW; ++r) {
+        wq[r] = *(const int *)(p.woq + (size_t)(r0 + r) * LTD + 4 * lane);
+        wd[r] = __half2float(__ushort_as_half(p.wod[(size_t)(r0 + r) * (LTD / 32) + (lane >> 3)]));
+    }
+    const int u0 = q * LTQ_U;
+    float4 a1[LTQ_UPW], a2[LTQ_U / 4];
+#pragma unroll
+    for (int r = 0; r < LTQ_UPW; ++r) a1[r] = *(const float4 *)(p.w1 + (size_t)(u0 + w * LTQ_UPW + r) * LTD + 4 * lane);
+#pragma unroll
+    for (int i = 0; i < LTQ_U / 4; ++i) a2[i] = *(const float4 *)(p.w2s + ((size_t)q * LTD + tid) * LTQ_U + 4 * i);
+    // per codebook step its own tags (8 steps share the buffers within one frame)
+    const unsigned tag_y = (unsigned)p.iter[0] * 64u + 32u + (unsigned)cb, tag_p = tag_y + 16u;
+    if (w == 0) {
+        // the attention output a of position cb and its residual X (lt_pick_kernel's steps)
+        if (cb > 0) {
+            const int stp = g.step[b];
+            int amax;
+            const int code = wave_pick_v(lv, g.ignore_eos || stp < 4, g.audio_bos, g.audio_eos, g.smp, b, stp, cb - 1, wsc,
+                                         amax);
+            const size_t rr = (size_t)(cb - 1) * VCB + code;
+            const float *row = g.qkvtab + rr * (3 * LTD) + 4 * lane;
+            const float4 q4 = *(const float4 *)row, k4 = *(const float4 *)(row + LTD), v4 = *(const float4 *)(row + 2 * LTD);
+            const float4 xp = *(const float4 *)(g.ptab + rr * LTD + 4 * lane);
+            if (q == 0) {
+                if (lane == 0) {
+                    g.codes_cur[b * NCB + cb - 1] = code;
+                    if (amax == g.audio_eos) g.smp.argeos[b] = 1;
+                    if (g.smp.amax) g.smp.amax[b * NCB + cb - 1] = amax;
+                }
+                *(float4 *)(g.lk + ((size_t)b * NCB + cb) * LTD + 4 * lane) = k4;
+                *(float4 *)(g.lv + ((size_t)b * NCB + cb) * LTD + 4 * lane) = v4;
+            }
+            x4 = make_float4(xp.x + pos4.x, xp.y + pos4.y, xp.z + pos4.z, xp.w + pos4.w);
+            a4 = lt_attend<true, true>(g, b, q4, k4, v4, kr, vr);
+        }
+        *(float4 *)&xs[4 * lane] = x4;
+        // a -> Q8_0 (quantize_row_q8_0_ref): block = 8 lanes x 4 elements
+        float am = fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w)));
+        am = fmaxf(am, __shfl_xor(am, 1, 64));
+        am = fmaxf(am, __shfl_xor(am, 2, 64));
+        am = fmaxf(am, __shfl_xor(am, 4, 64));
+        const float dd = am / 127.0f;
+        const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+        unsigned qw = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qw |= ((unsigned)(int)roundf(av[j] * id) & 0xFFu) << (8 * j);
+        aq[lane] = (int)qw;
+        if ((lane & 7) == 0) ad[lane >> 3] = __half2float(__float2half(dd));
+    }
+    lds_sync();
+    // o_net: per block the exact integer dot, then sum_blocks isum * (d_w d_a) in block order
+    {
+        const int av = aq[lane];
+        float o[LTQ_RW];
+#pragma unroll
+        for (int r = 0; r < LTQ_RW; ++r) {
+            int is = __builtin_amdgcn_sdot4(wq[r], av, 0, false);
+            is += __shfl_xor(is, 1, 64);
+            is += __shfl_xor(is, 2, 64);
+            is += __shfl_xor(is, 4, 64);
+            const float fb = (float)is * (wd[r] * ad[lane >> 3]);  // lanes 8kb .. 8kb+7: block kb's term
+            float acc = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < LTD / 32; ++kb) acc += __shfl(fb, 8 * kb, 64);
+            o[r] = acc;
+        }
+        if (lane < LTQ_RW) {
+            const int n = r0 + lane;
+            const float yv = (lane == 0 ? o[0] : o[LTQ_RW - 1]) + xs[n];
+            __hip_atomic_store((gu64 *)p.gy + (size_t)b * LTD + n, ((unsigned long long)tag_y << 32) | __float_as_uint(yv),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            p.y[(size_t)b * LTD + n] = yv;
+        }
+    }
+    // y (all 256) from the slot's granules, LN -> xs (wave 0; the other waves wait)
+    if (w == 0) {
+        float yv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) yv[c] = gh_wait(p.gy + (size_t)b * LTD + 4 * lane + c, tag_y, p.hx_err);
+        *(float4 *)&ys[4 * lane] = make_float4(yv[0], yv[1], yv[2], yv[3]);
+        ts_mark(p.ts, t_start);  // profiling: y seen
+        float mean, var;
+        wave_meanvar<4>(yv, mean, var);
+        const float rstd = 1.0f / sqrtf(var + p.eps);
+        const float4 gl = *(const float4 *)(p.lnw + 4 * lane);
+        *(float4 *)&xs[4 * lane] = make_float4(((yv[0] - mean) * rstd) * gl.x, ((yv[1] - mean) * rstd) * gl.y,
+                                               ((yv[2] - mean) * rstd) * gl.z, ((yv[3] - mean) * rstd) * gl.w);
+    }
+    lds_sync();
+    {
+        const float4 xv = *(const float4 *)&xs[4 * lane];
+#pragma unroll
+        for (int r = 0; r < LTQ_UPW; ++r) {
+            const float v = wave_sum(dotv(a1[r], xv));
+            if (lane == 0) fs[w * LTQ_UPW + r] = gelu_tanh(v);
+        }
+    }
+    lds_sync();
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < LTQ_U / 4; ++i) {
+        const float4 f4 = *(const float4 *)&fs[4 * i];
+        acc = fmaf(a2[i].x, f4.x, acc);
+        acc = fmaf(a2[i].y, f4.y, acc);
+        acc = fmaf(a2[i].z, f4.z, acc);
+        acc = fmaf(a2[i].w, f4.w, acc);
+    }
+    // partial sums through granules; this workgroup merges its LTQ_R outputs in q order
+    gu64 *gp = (gu64 *)p.gp + (size_t)b * LTQ_P * LTD;
+    __hip_atomic_store(gp + (size_t)q * LTD + tid, ((unsigned long long)tag_p << 32) | __float_as_uint(acc),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mv[tid / LTQ_R][tid % LTQ_R] = gh_wait(p.gp + (size_t)b * LTQ_P * LTD + (size_t)(tid / LTQ_R) * LTD + LTQ_R * q + tid % LTQ_R,
+                                           tag_p, p.hx_err);
+    lds_sync();
+    if (tid < LTQ_R) {
+        float s = mv[0][tid];
+#pragma unroll 8
+        for (int k = 1; k < LTQ_P; ++k) s += mv[k][tid];
+        p.y2[(size_t)b * LTD + LTQ_R * q + tid] = s + ys[LTQ_R * q + tid];
+    }
+    ts_end(p.ts, t_start);
+}
+hipError_t op_lt_slot_q8(const LtSlotQ8P &p, int NB, hipStream_t s) {
+    const GemvP &g = p.g;
+    if (!p.woq || !p.wod || !p.lnw || !p.w1 || !p.w2s || !p.y || !p.y2 || !p.gy || !p.gp || !p.iter || !p.hx_err ||
+        !g.ltX || !g.ltk || !g.ltv || !g.lk || !g.lv || g.cb < 0 || g.cb >= NCB || NB < 1 || NB > 16 ||
+        (g.cb > 0 && (!g.logits || !g.codes_cur || !g.qkvtab || !g.ptab || !g.lt_pos || !g.step || !g.smp.cfg ||
+                      !g.smp.argeos)))
+        return hipErrorInvalidValue;
+    mp::launch(lt_slot_q8_kernel, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
 }
 
 // int8 [N][K] + fp16 scales [N][K/32] (the file's blocks) -> fragment order:
@@ -440,63 +621,48 @@ __global__ __launch_bounds__(MP_BLOCK) void xa_q8_kernel(XaQ8P p) {
 }
 
 // ---------------------------------------------------------------- XA q_net, fused (EPI_RESID_XQ8)
-// The cross-attention's Q8_0 q_net riding in the Q8_0 O-projection's launch: the
-// launch's last XQG x NB workgroups, XQ_ROWS rows of q each. A workgroup issues its
-// q_net rows (wave 0, lane = (row, quarter): 6 blocks of int8 + their scales, the
-// MFMA kernel's K split) before x1 exists, sweeps the x1 granules (publish_x1), and
-// computes exactly what the separate q GEMV does: LN(x1) * lnw (PRO_LN's wave
-// statistics), the Q8_0 activation blocks (gemm_q8_kernel_dec's quantiser), each
-// quarter's block dots accumulated in block order and the quarters summed in order,
-// stored to q. xa_q8_kernel (the next launch) does the attention and o_net. Same bits
-// as the q GEMV (tests/test_q8_fused_gpu.py).
 constexpr int XQ_ROWS = DXA / XQG, XQ_QB = D / 32 / 4;  // 8 workgroups x 16 rows; 6 blocks per quarter
-__device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char *actq, float *actd,
-                                         unsigned long long t_start) {
-#pragma clang fp contract(off)
-    const XaQ8P &x = p.xq8;
-    const int k = blockIdx.x - p.nrow_blocks, b = k / XQG, r0 = (k % XQG) * XQ_ROWS;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int qr = r0 + (lane >> 2), qa = lane & 3;  // wave 0: (row, quarter) per lane
-    uint4 wq[2 * XQ_QB];
-    unsigned short wqs[XQ_QB];
-    if (w == 0) {
-        const uint4 *src = (const uint4 *)(x.wq + (size_t)qr * D + qa * XQ_QB * 32 + ts_dep(t_start));
+// q_net row qr, quarter qa (6 blocks of int8 + their scales): issued before x1 exists
+__device__ __forceinline__ void xq8_load_rows(const XaQ8P &x, int qr, int qa, int dep, uint4 (&wq)[2 * XQ_QB],
+                                              unsigned short (&wqs)[XQ_QB]) {
+    const uint4 *src = (const uint4 *)(x.wq + (size_t)qr * D + qa * XQ_QB * 32 + dep);
 #pragma unroll
-        for (int i = 0; i < 2 * XQ_QB; ++i) wq[i] = src[i];
+    for (int i = 0; i < 2 * XQ_QB; ++i) wq[i] = src[i];
 #pragma unroll
-        for (int j = 0; j < XQ_QB; ++j) wqs[j] = x.wqd[(size_t)qr * (D / 32) + qa * XQ_QB + j];
-    }
+    for (int j = 0; j < XQ_QB; ++j) wqs[j] = x.wqd[(size_t)qr * (D / 32) + qa * XQ_QB + j];
+}
+// x1 of slot b from the O-projection workgroups' granules (every wave sweeps the row)
+__device__ __forceinline__ void xq8_sweep_x1(const GemvP &p, int b, float (&v)[D / 64]) {
     constexpr int PER = D / 64;
-    float g[PER];
-    load_lnw<PER>(x.lnw, g);
-    // x1 from the O-projection workgroups of this launch (every wave sweeps the row)
-    float v[PER];
-    {
-        const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
-        gu64 *gr = (gu64 *)(p.xh + (size_t)b * D);
-        for (unsigned spins = 0;; ++spins) {
-            bool ok = true;
+    const int lane = threadIdx.x & 63;
+    const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+    gu64 *gr = (gu64 *)(p.xh + (size_t)b * D);
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
 #pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const unsigned long long u = __hip_atomic_load(gr + lane + 64 * j, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                v[j] = __uint_as_float((unsigned)u);
-                ok &= (unsigned)(u >> 32) == tag;
-            }
-            if (__all(ok)) break;
-            if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
-                if (lane == 0)
-                    __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                for (int j = 0; j < PER; ++j) v[j] = __builtin_nanf("");
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+        for (int j = 0; j < PER; ++j) {
+            const unsigned long long u = __hip_atomic_load(gr + lane + 64 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[j] = __uint_as_float((unsigned)u);
+            ok &= (unsigned)(u >> 32) == tag;
         }
+        if (__all(ok)) break;
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+            if (lane == 0) __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int j = 0; j < PER; ++j) v[j] = __builtin_nanf("");
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
-    ts_mark(p.ts, t_start);  // profiling: x1 seen
-    {   // LN(x1) * lnw (PRO_LN at batch 1: every wave the whole row, wave w stores its quarter)
-        constexpr int Q = PER / MP_NWAVES;
+}
+// LN(x1) * lnw (PRO_LN at batch 1: every wave the whole row, wave w stores its quarter),
+// then the row's Q8_0 blocks (gemm_q8_kernel_dec's quantiser) into actq / actd
+__device__ __forceinline__ void xq8_ln_quant(const XaQ8P &x, const float (&v)[D / 64], const float (&g)[D / 64],
+                                             float *act, signed char *actq, float *actd) {
+#pragma clang fp contract(off)
+    constexpr int PER = D / 64, Q = PER / MP_NWAVES, NBLK = D / 32;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    {
         float mean, var;
         wave_meanvar<PER>(v, mean, var);
         const float rstd = 1.0f / sqrtf(var + x.eps);
@@ -507,8 +673,6 @@ __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char
         }
     }
     lds_sync();
-    // Q8_0 blocks of the row (gemm_q8_kernel_dec's quantiser)
-    constexpr int NBLK = D / 32;
     if (tid < 4 * NBLK) {
         const int kb = tid >> 2, e8 = 8 * (lane & 3);
         const float4 x0 = *(const float4 *)(act + kb * 32 + e8);
@@ -526,9 +690,12 @@ __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char
         if ((lane & 3) == 0) actd[kb] = __half2float(__float2half(dd));
     }
     lds_sync();
-    if (w != 0) return;
-    // this lane's quarter: its blocks in order (fmaf, as gemm_q8_kernel_dec), then the
-    // row's 4 quarters summed in order by its quarter-0 lane
+}
+// this lane's quarter: its blocks in order (fmaf, as gemm_q8_kernel_dec), then the row's
+// 4 quarters summed in order (valid in the quarter-0 lane)
+__device__ __forceinline__ float xq8_dot(const uint4 (&wq)[2 * XQ_QB], const unsigned short (&wqs)[XQ_QB], int qa,
+                                         const signed char *actq, const float *actd) {
+#pragma clang fp contract(off)
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < XQ_QB; ++j) {
@@ -547,8 +714,37 @@ __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char
         acc = fmaf((float)sd, dw * actd[blk], acc);
     }
     const float p1 = __shfl_down(acc, 1, 64), p2 = __shfl_down(acc, 2, 64), p3 = __shfl_down(acc, 3, 64);
+    return ((acc + p1) + p2) + p3;
+}
+
+// The cross-attention's Q8_0 q_net riding in the Q8_0 O-projection's launch: the
+// launch's last XQG x NB workgroups, XQ_ROWS rows of q each. A workgroup issues its
+// q_net rows (wave 0, lane = (row, quarter): 6 blocks of int8 + their scales, the
+// MFMA kernel's K split) before x1 exists, sweeps the x1 granules (publish_x1), and
+// computes exactly what the separate q GEMV does: LN(x1) * lnw (PRO_LN's wave
+// statistics), the Q8_0 activation blocks (gemm_q8_kernel_dec's quantiser), each
+// quarter's block dots accumulated in block order and the quarters summed in order,
+// stored to q. xa_q8_kernel (the next launch) does the attention and o_net. Same bits
+// as the q GEMV (tests/test_q8_fused_gpu.py).
+__device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char *actq, float *actd,
+                                         unsigned long long t_start) {
+    const XaQ8P &x = p.xq8;
+    const int k = blockIdx.x - p.nrow_blocks, b = k / XQG, r0 = (k % XQG) * XQ_ROWS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int qr = r0 + (lane >> 2), qa = lane & 3;  // wave 0: (row, quarter) per lane
+    uint4 wq[2 * XQ_QB];
+    unsigned short wqs[XQ_QB];
+    if (w == 0) xq8_load_rows(x, qr, qa, ts_dep(t_start), wq, wqs);
+    constexpr int PER = D / 64;
+    float g[PER];
+    load_lnw<PER>(x.lnw, g);
+    float v[PER];
+    xq8_sweep_x1(p, b, v);
+    ts_mark(p.ts, t_start);  // profiling: x1 seen
+    xq8_ln_quant(x, v, g, act, actq, actd);
+    if (w != 0) return;
+    const float qv = xq8_dot(wq, wqs, qa, actq, actd);
     if (qa == 0) {  // q to the launch's attention workgroups as a {tag, value} granule
-        const float qv = ((acc + p1) + p2) + p3;
         const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
         __hip_atomic_store((gu64 *)(x.qg + (size_t)b * DXA + qr), ((unsigned long long)tag << 32) | __float_as_uint(qv),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -624,6 +820,67 @@ __device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_s
     ts_end(p.ts, t_start);
 }
 
+// Small batches (XaQ8P::qin): the attention + o_net workgroups (XQ8A x NB, no q_net
+// workgroups) compute q themselves, so the launch has one hand-off (x1) instead of two.
+// A workgroup issues its o_net rows, all 128 q_net rows (lane = (row, quarter) as
+// xq8_tail, 2 rows per lane) and the first text keys / values at entry, sweeps x1,
+// and computes q with xq8_tail's arithmetic (same bits: LN, quantiser, block order,
+// quarter order) into LDS, then xq8a_tail's attention and o_net.
+__device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed char *actq, float *actd,
+                                           unsigned long long t_start) {
+    constexpr int OG = XQ8_ROWS / MP_NWAVES / XQ8_OR, PER = D / 64, QR = DXA / 64;  // q rows per lane
+    const XaQ8P &x = p.xq8;
+    __shared__ float pr[TMAX_LIMIT];
+    __shared__ __attribute__((aligned(16))) float a_s[DXA];
+    __shared__ __attribute__((aligned(16))) signed char aq[DXA];
+    __shared__ float ad[DXA / 32];
+    __shared__ __attribute__((aligned(16))) float qs[DXA];
+    __shared__ float x1s[XQ8_ROWS];
+    const int k = blockIdx.x - p.nrow_blocks, b = k / XQ8A, rb = k % XQ8A;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rb * XQ8_ROWS + w * OG * XQ8_OR, dep = ts_dep(t_start);
+    uint4 wo[OG];
+    float wos[OG];
+#pragma unroll
+    for (int g = 0; g < OG; ++g) {
+        const int row = r0 + g * XQ8_OR + lane / XQ8_OCPR, kc = lane % XQ8_OCPR;
+        wo[g] = *(const uint4 *)(x.wo + (size_t)row * DXA + kc * 16 + dep);
+        wos[g] = __half2float(__ushort_as_half(x.wod[(size_t)row * (DXA / 32) + kc / 2]));
+    }
+    const int qa = lane & 3;
+    uint4 wq[QR][2 * XQ_QB];
+    unsigned short wqs[QR][XQ_QB];
+#pragma unroll
+    for (int j = 0; j < QR; ++j) xq8_load_rows(x, 16 * w + 64 * j + (lane >> 2), qa, dep, wq[j], wqs[j]);
+    float g[PER];
+    load_lnw<PER>(x.lnw, g);
+    const size_t kv = ((size_t)(b * x.nlayers + x.layer) * x.Tmax) * DXA;
+    xa_text_attention_q(
+        [&](int d4) {
+            float v[PER];
+            xq8_sweep_x1(p, b, v);
+            ts_mark(p.ts, t_start);  // profiling: x1 seen
+            if (w == 0) {  // the residual rows of this workgroup's o_net
+                float xr = v[0];
+#pragma unroll
+                for (int j = 1; j < PER; ++j) xr = j == rb ? v[j] : xr;
+                x1s[lane] = xr;
+            }
+            xq8_ln_quant(x, v, g, act, actq, actd);
+#pragma unroll
+            for (int j = 0; j < QR; ++j) {
+                const float qv = xq8_dot(wq[j], wqs[j], qa, actq, actd);
+                if (qa == 0) qs[16 * w + 64 * j + (lane >> 2)] = qv;
+            }
+            lds_sync();
+            return *(const float4 *)&qs[d4];
+        },
+        x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
+    xa_quantize_a(a_s, aq, ad);
+    xa_q8_onet<OG>(wo, wos, r0, aq, ad, x1s - rb * XQ8_ROWS, x.x2 + (size_t)b * D);
+    ts_end(p.ts, t_start);
+}
+
 // f32 o_net: lane l holds elements 4l..4l+3 of half a row, a wave covers 2 rows
 // per instruction; 64 rows = 4 waves x 8 pairs
 __global__ __launch_bounds__(MP_BLOCK) void xa_f32_kernel(XaQ8P p) {
@@ -692,7 +949,7 @@ static hipError_t launch_q8(const GemvP &p, hipStream_t s) {
     if (!q8_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
     GemvP q = p;
     q.nrow_blocks = (p.N + 15) / 16;
-    const int grid = q.nrow_blocks + (EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : EPI == EPI_RESID_XQ8 ? (XQG + XQ8A) * NB : 0);
+    const int grid = q.nrow_blocks + (EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : EPI == EPI_RESID_XQ8 ? (NB <= XQ8_QIN_NB && p.xq8.qin ? XQ8A : XQG + XQ8A) * NB : 0);
     if (p.q4) mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI, true>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     else mp::launch((gemm_q8_kernel_dec<NB, K, PRO, EPI, false>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();

@@ -27,6 +27,7 @@ constexpr int XA_SPLITS = 4;        // text-key splits of the fused cross-attent
 constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
 constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
 constexpr int LTS_P = 32;           // bf16 mode LT step (lt_slot_kernel): workgroups per slot = partial FFN-down sums
+constexpr int LTQ_P = 32;           // Q8_0 mode LT step (lt_slot_q8_kernel): workgroups per slot = partial FFN-down sums
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
 enum Pro {
@@ -203,6 +204,7 @@ struct XaP {
 // Cross-attention with Q8_0 q_net / o_net (weight mode MP_WEIGHTS_Q8) after the
 // q GEMV: x2 = x + Q8(o_net) attn(q, K, V), the attention output quantised where
 // ggml quantises it (magpie.cpp:1713-1767, 3513-3519).
+constexpr int XQ8_QIN_NB = 2;      // Q8_0 XA in the O-projection launch: q in the attention workgroups up to this batch
 struct XaQ8P {
     const float *x;                 // [B][768]
     float *x2;                      // [B][768]
@@ -220,6 +222,7 @@ struct XaQ8P {
     const float *lnw;               // norm_xattn_query
     float eps;
     unsigned long long *qg;         // [B][128] {tag, value} granules of q
+    int qin;                        // 1: q computed in the attention workgroups (no q granules)
 };
 
 struct AttnP {  // decode self-attention (one query per utterance)
@@ -308,6 +311,27 @@ struct GemvP {
     const int *iter;
     int *hx_err;
     int nrow_blocks;     // set by the launcher: workgroups of the O-projection
+};
+
+// Q8_0 weight mode: the LT step of codebook cb as LTQ_P workgroups per slot
+// (lt_slot_q8_kernel): pick, gathers and attention as lt_pick_kernel (g), the Q8_0 o_net
+// of 256 / LTQ_P rows per workgroup (ggml's Q8_0 x Q8_0 dot: the attention output quantised per
+// 32-block, per-block integer dots times d_w d_a, blocks in order) published as y
+// granules, the F32 FFN (the Q8 file's FFN convs) for 1024 / LTQ_P hidden units per workgroup,
+// partial sums merged through granules into y2 for the Q8_0 head.
+struct LtSlotQ8P {
+    GemvP g;                       // pick / gathers / attention fields (lt_pick_kernel's), cb
+    const signed char *woq;        // o_net int8 [256][256] (Q4_0 blocks as q - 8)
+    const unsigned short *wod;     // o_net fp16 block scales [256][8]
+    const float *lnw;              // norm_pos_ff
+    float eps;
+    const float *w1;               // FFN up f32 [1024][256]
+    const float *w2s;              // FFN down f32 slice-major [LTQ_P][256][1024 / LTQ_P]
+    float *y, *y2;                 // [B][256] attention residual (ltY) and FFN output (the head's input)
+    unsigned long long *gy, *gp;   // granules: y [B][256] (tag iter * 64 + 32 + cb), partials [B][LTQ_P][256] (+ 48 + cb)
+    const int *iter;
+    int *hx_err;
+    unsigned long long *ts;
 };
 
 // error bits raised in *hx_err (ndone[2]) by an in-launch hand-off that gave up

@@ -110,6 +110,7 @@ hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_ffn2(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_slot(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_front(const LtFrontP &, hipStream_t);
+hipError_t op_lt_slot_q8(const LtSlotQ8P &, int, hipStream_t);
 hipError_t op_lt_kvo(const GemvP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
 hipError_t b16_oproj_xa_pm_16(const GemvP &, hipStream_t);
@@ -211,6 +212,8 @@ struct Model {
     // bf16 weight mode (lt_slot_kernel): the LT FFN weights rounded to bf16, W1 row-major
     // [1024][256] and W2 slice-major [LTS_P][256][1024 / LTS_P]
     unsigned short *lt_ff1h = nullptr, *lt_ff2h = nullptr;
+    // Q8_0 weight mode (lt_slot_q8_kernel): the F32 FFN-down weights slice-major [LTQ_P][256][1024 / LTQ_P]
+    float *lt_ff2q = nullptr;
     std::vector<float *> xq_t;  // per layer W_q^T [768][128] (for K' = K W_q)
     // weight mode MP_WEIGHTS_BF16: decode projections repacked as bf16 MFMA fragments
     int weight_mode = 0;
@@ -229,7 +232,7 @@ struct Model {
 };
 
 enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9,
-              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12, K_LTFRONT = 13 };
+              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12, K_LTFRONT = 13, K_LTSLOTQ8 = 14 };
 struct OpRec {
     std::string name;
     int kind;
@@ -242,6 +245,7 @@ struct OpRec {
     LtFfnP lf;
     LtFfn2P l2;
     LtFrontP lf3;
+    LtSlotQ8P lq8;
     EmbP e;
     int B;
     double bytes;
@@ -254,8 +258,9 @@ struct LtIo {
     int trace_steps;
     float *lt_s, *ltX, *ltY, *lty2, *ltq, *ltk, *ltv, *ltf, *logits;
     float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel; lt_slot_kernel: [NB][LTS_P][256])
-    unsigned long long *ltgh;  // [NB][LTS_P][256] lt_slot_kernel's partial-sum granules
+    unsigned long long *ltgh;  // [NB][LTS_P or LTQ_P][256] lt_slot(_q8)_kernel's partial-sum granules
     unsigned long long *ltfg;  // [2][256] lt_front_kernel's hand-off granules (f32, batch 1)
+    unsigned long long *ltyg;  // [NB][256] lt_slot_q8_kernel's y granules (Q8_0 mode)
     int *iter, *hx_err;        // decode iteration counter (hand-off tags), hand-off error bits
     int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
     SmpCfg *cfg;
@@ -296,7 +301,7 @@ struct mp_dev {
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
-    unsigned long long *ltgh = nullptr, *ltfg = nullptr;
+    unsigned long long *ltgh = nullptr, *ltfg = nullptr, *ltyg = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
         *argeos = nullptr, *amax = nullptr;
@@ -672,6 +677,16 @@ int build_ptab(mp_dev *dev, int weight_mode) {
         HIPCHK(hipMalloc(&m.lt_ff2h, h2.size() * 2));
         HIPCHK(hipMemcpy(m.lt_ff2h, h2.data(), h2.size() * 2, hipMemcpyHostToDevice));
     }
+    if (weight_mode == MP_WEIGHTS_Q8 && !m.lt_ff2q) {
+        constexpr int U = 1024 / mp::LTQ_P;
+        std::vector<float> w2((size_t)256 * 1024), w2q(w2.size());
+        HIPCHK(hipMemcpy(w2.data(), m.lt_ff2, w2.size() * 4, hipMemcpyDeviceToHost));
+        for (int q = 0; q < mp::LTQ_P; ++q)
+            for (int n = 0; n < 256; ++n)
+                memcpy(&w2q[((size_t)q * 256 + n) * U], &w2[(size_t)n * 1024 + q * U], U * 4);
+        HIPCHK(hipMalloc(&m.lt_ff2q, w2q.size() * 4));
+        HIPCHK(hipMemcpy(m.lt_ff2q, w2q.data(), w2q.size() * 4, hipMemcpyHostToDevice));
+    }
     return lt_table_attn(m) ? build_vo_tables(dev) : MP_OK;
 }
 
@@ -873,7 +888,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
-    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * mp::LTS_P * 256); A(ltfg, 2 * 256);
+    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, 2 * 256); A(ltyg, (size_t)NB * 256);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -995,7 +1010,8 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         const bool xa_in_oproj = tb.oproj_xa && !W.o8 && !xa_dir;
         // Q8_0 file: the whole direct Q8_0 cross-attention rides in the Q8_0 O-projection's
         // launch (EPI_RESID_XQ8): q_net workgroups on a hand-off of x1, then attention +
-        // o_net workgroups on a hand-off of q; x2 materialised
+        // o_net workgroups on a hand-off of q (up to XQ8_QIN_NB slots: the attention
+        // workgroups compute q on the hand-off of x1 themselves); x2 materialised
         // (up to 8 slots: its 48 + 20 NB workgroups are then co-resident even at one per CU,
         // so no hand-off waits on a workgroup that has not been dispatched)
         const bool xq8_in_oproj = q8_fuse && W.o8 && W.xq8 && W.xo8 && tq.oproj_xq && NB <= 8;
@@ -1004,6 +1020,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
             xq.x2 = dev->x2; xq.xak = dev->xak; xq.xav = dev->xav; xq.T = dev->T; xq.Tmax = dev->Tmax;
             xq.layer = l; xq.nlayers = L; xq.wo = W.xo8.q; xq.wod = W.xo8.d;
             xq.wq = W.xq8.q; xq.wqd = W.xq8.d; xq.lnw = W.norm_xq; xq.eps = m.eps; xq.qg = dev->xqh;
+            xq.qin = NB <= mp::XQ8_QIN_NB;  // small batches: q in the attention workgroups (one hand-off)
             g.xq8 = xq; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
             if ((rc = run("oproj_xa_q8", tq.oproj_xq, g,
                           Fq(W.o8) * (768.0 * 768) + A * act * (768 * 3) + (34.0 / 32.0) * (2.0 * 128 * 768) +
@@ -1080,7 +1097,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     io.x = dev->x; io.hidden = dev->hidden; io.trace = dev->trace; io.trace_steps = dev->max_steps + 1;
     io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
     io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits; io.ltp = dev->ltp;
-    io.ltgh = dev->ltgh; io.ltfg = dev->ltfg; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
+    io.ltgh = dev->ltgh; io.ltfg = dev->ltfg; io.ltyg = dev->ltyg; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
     io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
     io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
     io.amax = dev->amax; io.cfg = dev->smpcfg;
@@ -1296,6 +1313,42 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                 efn = mp::op_lt_em_1;
             }
             if ((rc = run("lt_e", efn, g, A * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
+                return rc;
+        }
+    } else if (m.weight_mode == MP_WEIGHTS_Q8 && m.lt_o8 && m.lt_out8 && m.lt_ff2q && !io.lt_only && io.ltyg) {
+        // Q8_0 mode: position 0's q|k|v (the Q8_0 GEMV), then per codebook the LT step as
+        // LTQ_P workgroups per slot (lt_slot_q8_kernel: pick, attention, Q8_0 o_net, F32
+        // FFN, partial sums merged through granules) and the Q8_0 head on its output
+        mp::GemvP g = base(); g.cb = 0;
+        g.W = m.lt_qkv; g.N = 768; g.lt_s = io.lt_s; g.lt_pos = m.lt_pos; g.ltX = io.ltX;
+        g.Wq = m.lt_qkv8.pq; g.Wd = m.lt_qkv8.pd; g.q4 = m.lt_qkv8.nib;
+        g.lnw = m.lt_norm_self; g.lq = io.ltq; g.lk = io.ltk; g.lv = io.ltv;
+        if ((rc = run("lt_a", tq.lt_a, g, Fq(m.lt_qkv8) * (768.0 * 256) + A * act * (256 * 3 + 768 + 256))) != MP_OK)
+            return rc;
+        for (int cb = 0; cb < 8; ++cb) {
+            mp::LtSlotQ8P sp{};
+            sp.g = base(); sp.g.cb = cb;
+            sp.g.logits = io.logits; sp.g.codes_cur = io.codes_cur; sp.g.qkvtab = m.lt_qkvtab; sp.g.ptab = m.lt_ptab;
+            sp.g.lt_pos = m.lt_pos; sp.g.ltk = io.ltk; sp.g.ltv = io.ltv; sp.g.lk = io.ltk; sp.g.lv = io.ltv;
+            sp.g.ltX = io.ltX;
+            sp.woq = m.lt_o8.q; sp.wod = m.lt_o8.d; sp.lnw = m.lt_norm_ff; sp.eps = m.eps; sp.w1 = m.lt_ff1;
+            sp.w2s = m.lt_ff2q; sp.y = io.ltY; sp.y2 = io.lty2; sp.gy = io.ltyg; sp.gp = io.ltgh;
+            sp.iter = io.iter; sp.hx_err = io.hx_err;
+            if (ops) {
+                mp::OpRec r{};
+                r.name = "lt_slot_q8"; r.kind = mp::K_LTSLOTQ8; r.lq8 = sp; r.B = NB;
+                r.bytes = (34.0 / 32.0) * (256.0 * 256) + A * (1024.0 * 256 * 2) +
+                          A * act * (cb ? 2024 + 4 * 256 + 2 * 256 * cb : 512) + A * act * (mp::LTQ_P * 256 + 512);
+                ops->push_back(r);
+            }
+            HIPCHK(mp::op_lt_slot_q8(sp, NB, s));
+            dump_lt(io, s);
+            g = base(); g.cb = cb;
+            g.W = m.lt_out_w + (size_t)cb * 2024 * 256; g.N = 2024; g.bias = m.lt_out_b + (size_t)cb * 2024;
+            g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
+            g.Wq = m.lt_out8.pq + (size_t)cb * m.lt_out8.head_q; g.q4 = m.lt_out8.nib;
+            g.Wd = (const unsigned short *)((const char *)m.lt_out8.pd + (size_t)cb * q8p_head_d());
+            if ((rc = run("lt_e", tq.lt_e, g, Fq(m.lt_out8) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
                 return rc;
         }
     } else
@@ -1581,7 +1634,7 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     dev->m.lt_in8 = dev->m.lt_qkv8 = dev->m.lt_o8 = dev->m.lt_out8 = mp::QW{};
     dev->m.pk_lt_in = nullptr;  // set again by an F16 load
     // derived LT weight layouts of a previous model (rebuilt by build_ptab)
-    for (void **pp : {(void **)&dev->m.lt_ff2s, (void **)&dev->m.lt_ff1h, (void **)&dev->m.lt_ff2h})
+    for (void **pp : {(void **)&dev->m.lt_ff2s, (void **)&dev->m.lt_ff1h, (void **)&dev->m.lt_ff2h, (void **)&dev->m.lt_ff2q})
         if (*pp) { hipFree(*pp); *pp = nullptr; }
     if (weight_mode == MP_WEIGHTS_Q8 || weight_mode == MP_WEIGHTS_F16) {  // cheap header check before any upload
         mp::Gguf g;
@@ -1657,6 +1710,7 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.lt_ff2s) hipFree(dev->m.lt_ff2s);
     if (dev->m.lt_ff1h) hipFree(dev->m.lt_ff1h);
     if (dev->m.lt_ff2h) hipFree(dev->m.lt_ff2h);
+    if (dev->m.lt_ff2q) hipFree(dev->m.lt_ff2q);
     if (dev->m.pk_arena) hipFree(dev->m.pk_arena);
     if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
     if (dev->m.q8p_arena) hipFree(dev->m.q8p_arena);
@@ -1750,8 +1804,9 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->xh, 0, (size_t)NB * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xqh, 0, (size_t)NB * 128 * 8, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->ltgh, 0, (size_t)NB * mp::LTS_P * 256 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->ltgh, 0, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->ltfg, 0, 2 * 256 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->ltyg, 0, (size_t)NB * 256 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->sagh, 0, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xagh, 0, (size_t)NB * mp::XA_SPLITS * mp::XA_PART * 8, dev->stream));
     // the first frame's decoder input (the BOS codes); later frames' by lt_finalize_kernel
@@ -2112,6 +2167,7 @@ static hipError_t launch_rec(const mp::OpRec &r, hipStream_t s) {
     case mp::K_LTFFN2: return mp::op_lt_ffn2(r.l2, r.B, s);
     case mp::K_LTSLOT: return mp::op_lt_slot(r.l2, r.B, s);
     case mp::K_LTFRONT: return mp::op_lt_front(r.lf3, s);
+    case mp::K_LTSLOTQ8: return mp::op_lt_slot_q8(r.lq8, r.B, s);
     case mp::K_LTKVO: return mp::op_lt_kvo(r.g, r.B, s);
     case mp::K_EMBED: return mp::op_embed(r.e, r.B, s);
     case mp::K_FIN: return mp::op_finalize(r.f, r.B, s);
@@ -2176,7 +2232,7 @@ int mp_hip_profile_ops_ts(mp_dev *dev, int iters, float *avg_us) {
         for (int i = 0; i < n; ++i) {
             mp::OpRec r = dev->ops[i];
             unsigned long long *t = ts + (size_t)i * per;
-            r.g.ts = t; r.a.ts = t; r.x.ts = t; r.f.ts = t; r.lf.ts = t; r.l2.f.ts = t; r.lf3.l.f.ts = t;
+            r.g.ts = t; r.a.ts = t; r.x.ts = t; r.f.ts = t; r.lf.ts = t; r.l2.f.ts = t; r.lf3.l.f.ts = t; r.lq8.ts = t;
             const hipError_t e = launch_rec(r, dev->stream);
             if (e != hipSuccess) { rc = fail(dev, MP_ERR_HIP, std::string("profile launch: ") + hipGetErrorString(e)); break; }
         }

@@ -30,6 +30,18 @@ constexpr unsigned HX_SPIN_LIMIT = 1u << 20;
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 using gi32 = __attribute__((address_space(1))) int;
 
+// a {tag, value} granule's value once the wave sees the tag on every lane (bounded)
+__device__ __forceinline__ float gh_wait(const unsigned long long *g, unsigned tag, int *err) {
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned long long u = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((unsigned)(u >> 32) == tag)) return __uint_as_float((unsigned)u);
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison and say so (HX_ERR_LT: the LT's edges use it)
+            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return __builtin_nanf("");
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
 // Split sp of slot b. HANDOFF: x1 comes from the O-projection in the same launch,
 // as {tag, value} granules xh[b][768] (EPI_RESID_XA): every wave sweeps all 768
 // with relaxed agent-scope loads (write-through producer stores, so no fence is

@@ -23,7 +23,10 @@ constexpr int TMAX_LIMIT = 1024;  // text tokens per utterance (LDS score buffer
 // split-K decode attention: partial softmax states, merged in the next op's prologue
 constexpr int SA_SPLITS = 4;        // key splits of each SA head (sa_attn_kernel)
 constexpr int SA_PART = 4 + DH;     // per (slot, head, split): m, l, -, -, O[64] (unnormalised)
-constexpr int XA_SPLITS = 4;        // text-key splits of the fused cross-attention (xa_part_kernel)
+#ifndef MP_XA_SPLITS
+#define MP_XA_SPLITS 4
+#endif
+constexpr int XA_SPLITS = MP_XA_SPLITS;  // text-key splits of the fused cross-attention (xa_part_kernel)
 constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
 constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
 constexpr int LTS_P = 32;           // bf16 mode LT step (lt_slot_kernel): workgroups per slot = partial FFN-down sums

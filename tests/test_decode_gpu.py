@@ -469,9 +469,11 @@ def test_q8_sampling_matches_oracle(ma, oracle, q8_model):
     69 of 192 sampled decisions (the draw lands within ~4e-3 of an interval boundary
     at the median). Bar: each differing decision has an oracle margin < Q8_TIE_EPS and
     no more differ than that spread (50 %); the exact checks of Q8 sampling are the
-    batch-invariance tests (test_sampled_batch_equals_single[q8-*])."""
+    batch-invariance tests (test_sampled_batch_equals_single[q8-*]). The arithmetic
+    under the draws is held to the Q8 hidden-state bars at every forced step."""
     tok = ma.synthetic_tokens(12, seed=41)
-    _q8_forced(ma, oracle, q8_model, tok, steps=24, tie_frac=0.5, temperature=0.7, top_k=80, seed=77)
+    r, o = _q8_forced(ma, oracle, q8_model, tok, steps=24, tie_frac=0.5, temperature=0.7, top_k=80, seed=77)
+    _check_hidden_q8(r.hidden[0, :25], o["hidden"])
 
 
 def test_q4_small_model_matches_oracle(ma, oracle, q4_model):

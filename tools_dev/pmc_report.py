@@ -34,7 +34,7 @@ WIDE = ("gemv_kernel", "gemm_b16_kernel", "xa_part_kernel", "sa_attn_kernel", "l
         "conv_mfma_kernel", "gemm_q8_kernel_dec")
 DECODE = ("gemv_kernel", "sa_attn_kernel", "xa_part_kernel", "lt_finalize_kernel", "gemm_b16_kernel", "gemm_q8_kernel_dec",
           "lt_ffn_kernel", "lt_ffn2_kernel", "lt_merge_kernel", "lt_pick_kernel", "xa_q8_kernel", "xa_f32_kernel",
-          "lt_slot_kernel")
+          "lt_slot_kernel", "lt_slot_q8_kernel", "lt_front_kernel")
 # (embed_kernel runs once per decode, for the BOS frame, outside the iteration)
 
 

@@ -127,31 +127,20 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
 #pragma unroll
     for (int i = 0; i < XA_V; ++i) o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int tb = t0 + w; tb < t1; tb += XA_WAVES * XA_KPW) {
-        {   // the round's XA_KPW scores first (independent reductions the compiler
-            // interleaves), then one online-softmax update for the set (keys past t1
-            // weigh 0): oproj_xa 6.3 -> 6.0 us at f32 batch 1 (was one key at a time)
-            float sv[XA_KPW], mn = m;
 #pragma unroll
-            for (int u = 0; u < XA_KPW; ++u) {
-                float acc = 0.f;
+        for (int u = 0; u < XA_KPW; ++u) {
+            const int t = tb + XA_WAVES * u;
+            if (t >= t1) break;  // wave-uniform
+            float acc = 0.f;
 #pragma unroll
-                for (int i = 0; i < XA_V; ++i) acc += dotv(k[u][i], h[i]);
-                sv[u] = tb + XA_WAVES * u < t1 ? wave_sum(acc) * scale : -INFINITY;
-                mn = fmaxf(mn, sv[u]);
-            }
-            const float c = expf(m - mn);
-            l *= c;
+            for (int i = 0; i < XA_V; ++i) acc += dotv(k[u][i], h[i]);
+            const float sv = wave_sum(acc) * scale;
+            const float mn = fmaxf(m, sv), c = expf(m - mn), e = expf(sv - mn);
+            l = l * c + e;
 #pragma unroll
-            for (int i = 0; i < XA_V; ++i) { o[i].x *= c; o[i].y *= c; o[i].z *= c; o[i].w *= c; }
-#pragma unroll
-            for (int u = 0; u < XA_KPW; ++u) {
-                const float e = expf(sv[u] - mn);
-                l += e;
-#pragma unroll
-                for (int i = 0; i < XA_V; ++i) {
-                    o[i].x += e * vv[u][i].x; o[i].y += e * vv[u][i].y;
-                    o[i].z += e * vv[u][i].z; o[i].w += e * vv[u][i].w;
-                }
+            for (int i = 0; i < XA_V; ++i) {
+                o[i].x = o[i].x * c + e * vv[u][i].x; o[i].y = o[i].y * c + e * vv[u][i].y;
+                o[i].z = o[i].z * c + e * vv[u][i].z; o[i].w = o[i].w * c + e * vv[u][i].w;
             }
             m = mn;
         }

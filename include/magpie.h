@@ -168,6 +168,16 @@ magpie_context *magpie_init(const char *model_path);
 magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_type backend);
 void magpie_free(magpie_context *ctx);
 const char *magpie_get_backend_name(magpie_context *ctx);
+// magpie.h:332: load a GGUF's weights into `model` (its device state is created on
+// first use, on the device MAGPIE_DEVICE names; a model already loaded is replaced).
+// The weight mode is picked from the file as magpie_init does. false + stderr on failure.
+bool magpie_model_load(const std::string &path, magpie_model &model, magpie_backend_type backend = MAGPIE_BACKEND_AUTO);
+
+// magpie.h:555-558: run the text encoder for one utterance; ctx->state.encoder_output
+// ([n_tokens][d_model]) and enc_seq_len receive its output, as in the reference
+// (magpie.cpp:2284-2374). On the device this is the per-utterance preamble (encoder,
+// cross-attention K/V, context prefill) of a batch of one.
+bool magpie_encode_text(magpie_context *ctx, const int32_t *tokens, int n_tokens);
 
 // ---- synthesis (magpie.h:571-595): frame-major codes [n_frames * 8], BOS
 // excluded; empty vector on failure. All four names run the same device loop
@@ -186,6 +196,8 @@ bool magpie_synthesize_codes_batch(magpie_context *ctx, const int32_t *const *to
 magpie_codec *magpie_codec_init(const char *codec_path);
 magpie_codec *magpie_codec_init_with_backend(const char *codec_path, magpie_backend_type backend);
 void magpie_codec_free(magpie_codec *codec);
+// magpie.h:753: load codec weights from a GGUF into `codec` (replacing any loaded ones)
+bool magpie_codec_load(const std::string &path, magpie_codec &codec, magpie_backend_type backend = MAGPIE_BACKEND_AUTO);
 // codes: [num_codebooks][n_frames] codebook-major; returns n_frames * 1024 samples
 std::vector<float> magpie_codec_decode(magpie_codec *codec, const int32_t *codes, int n_frames);
 

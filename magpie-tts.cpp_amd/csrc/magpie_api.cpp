@@ -16,15 +16,13 @@ static int env_device() {
 
 magpie_context *magpie_init(const char *model_path) { return magpie_init_with_backend(model_path, MAGPIE_BACKEND_AUTO); }
 
-// magpie_init_with_backend (magpie.cpp:781-880): nullptr + stderr on failure.
-magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_type backend) {
+// magpie_model_load (magpie.cpp:572-718 behind magpie.h:332): false + stderr on failure.
+bool magpie_model_load(const std::string &path, magpie_model &model, magpie_backend_type backend) {
     (void)backend;  // single HIP device path
-    if (!model_path) return nullptr;
-    magpie_context *ctx = new magpie_context();
-    if (mp_hip_init(env_device(), &ctx->model.dev) != MP_OK) {
+    if (!model.dev && mp_hip_init(env_device(), &model.dev) != MP_OK) {
         fprintf(stderr, "magpie: no usable HIP device\n");
-        delete ctx;
-        return nullptr;
+        model.dev = nullptr;
+        return false;
     }
     // Weight mode (magpie_hip.h): a GGUF with Q8_0 / Q4_0 tensors runs them as ggml does
     // (MP_WEIGHTS_Q8), an F16 file with ggml's F16 semantics (MP_WEIGHTS_F16), any other
@@ -39,24 +37,35 @@ magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_
                : !strcmp(wm, "f16") ? MP_WEIGHTS_F16
                                     : MP_WEIGHTS_AS_STORED;
     }
-    int rc = mp_hip_load_model_ex(ctx->model.dev, model_path, mode);
+    int rc = mp_hip_load_model_ex(model.dev, path.c_str(), mode);
     if (rc == MP_ERR_UNSUPPORTED && !forced)  // no block-quantised tensors: an F16 file?
-        rc = mp_hip_load_model_ex(ctx->model.dev, model_path, MP_WEIGHTS_F16);
+        rc = mp_hip_load_model_ex(model.dev, path.c_str(), MP_WEIGHTS_F16);
     if (rc == MP_ERR_UNSUPPORTED && !forced)  // neither: as stored
-        rc = mp_hip_load_model_ex(ctx->model.dev, model_path, MP_WEIGHTS_AS_STORED);
+        rc = mp_hip_load_model_ex(model.dev, path.c_str(), MP_WEIGHTS_AS_STORED);
     if (rc != MP_OK) {
-        fprintf(stderr, "magpie: failed to load '%s': %s\n", model_path, mp_hip_error(ctx->model.dev));
-        mp_hip_free(ctx->model.dev);
+        fprintf(stderr, "magpie: failed to load '%s': %s\n", path.c_str(), mp_hip_error(model.dev));
+        return false;
+    }
+    int dec = 12, enc = 6;
+    mp_hip_model_info(model.dev, &dec, &enc, nullptr);
+    // the text front end rides in the same GGUF (magpie.cpp:853-858); optional
+    model.tokenizer = magpie_tokenizer();
+    if (!magpie_tokenizer_load(&model.tokenizer, path.c_str()))
+        fprintf(stderr, "magpie: no tokenizer in '%s' (token-id entry points only)\n", path.c_str());
+    model.hparams.dec_layers = dec;
+    model.hparams.enc_layers = enc;
+    return true;
+}
+
+// magpie_init_with_backend (magpie.cpp:781-880): nullptr + stderr on failure.
+magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_type backend) {
+    if (!model_path) return nullptr;
+    magpie_context *ctx = new magpie_context();
+    if (!magpie_model_load(model_path, ctx->model, backend)) {
+        if (ctx->model.dev) mp_hip_free(ctx->model.dev);
         delete ctx;
         return nullptr;
     }
-    int dec = 12, enc = 6;
-    mp_hip_model_info(ctx->model.dev, &dec, &enc, nullptr);
-    // the text front end rides in the same GGUF (magpie.cpp:853-858); optional
-    if (!magpie_tokenizer_load(&ctx->model.tokenizer, model_path))
-        fprintf(stderr, "magpie: no tokenizer in '%s' (token-id entry points only)\n", model_path);
-    ctx->model.hparams.dec_layers = dec;
-    ctx->model.hparams.enc_layers = enc;
     return ctx;
 }
 
@@ -148,6 +157,34 @@ std::vector<int32_t> magpie_synthesize_codes_optimized(magpie_context *ctx, cons
     return magpie_synthesize_codes_graph_reuse(ctx, tokens, n_tokens);
 }
 
+// magpie_encode_text (magpie.cpp:2284-2374): the encoder output lands in ctx->state.
+bool magpie_encode_text(magpie_context *ctx, const int32_t *tokens, int n_tokens) {
+    if (!ctx || !ctx->model.dev || !tokens || n_tokens <= 0) {
+        fprintf(stderr, "magpie_encode_text: invalid args\n");
+        return false;
+    }
+    const mp_params p = params_of(ctx);
+    const int32_t spk = ctx->speaker_id;
+    if (mp_hip_begin_batch(ctx->model.dev, tokens, &n_tokens, &spk, 1, n_tokens, &p) != MP_OK) {
+        fprintf(stderr, "magpie_encode_text: %s\n", mp_hip_error(ctx->model.dev));
+        return false;
+    }
+    const long long want = (long long)n_tokens * 768 * 4;
+    const long long eb = mp_hip_debug_buffer(ctx->model.dev, "enc_out", nullptr, 0);
+    if (eb < want) {
+        fprintf(stderr, "magpie_encode_text: encoder output unavailable\n");
+        return false;
+    }
+    std::vector<float> enc((size_t)eb / 4);
+    if (mp_hip_debug_buffer(ctx->model.dev, "enc_out", enc.data(), eb) != eb) {
+        fprintf(stderr, "magpie_encode_text: %s\n", mp_hip_error(ctx->model.dev));
+        return false;
+    }
+    ctx->state.encoder_output.assign(enc.begin(), enc.begin() + (size_t)n_tokens * 768);
+    ctx->state.enc_seq_len = n_tokens;
+    return true;
+}
+
 magpie_codec *magpie_codec_init(const char *codec_path) {
     return magpie_codec_init_with_backend(codec_path, MAGPIE_BACKEND_AUTO);
 }
@@ -155,12 +192,25 @@ magpie_codec *magpie_codec_init_with_backend(const char *codec_path, magpie_back
     (void)backend;
     if (!codec_path) return nullptr;
     magpie_codec *c = new magpie_codec();
-    if (mp_hip_codec_init(env_device(), codec_path, &c->dev) != MP_OK) {
-        fprintf(stderr, "magpie_codec: failed to load %s\n", codec_path);
+    if (!magpie_codec_load(codec_path, *c, backend)) {
         delete c;
         return nullptr;
     }
     return c;
+}
+// magpie_codec_load (nano-codec.cpp:205-352 behind magpie.h:753)
+bool magpie_codec_load(const std::string &path, magpie_codec &codec, magpie_backend_type backend) {
+    (void)backend;
+    if (codec.dev) {
+        mp_hip_codec_free(codec.dev);
+        codec.dev = nullptr;
+    }
+    if (mp_hip_codec_init(env_device(), path.c_str(), &codec.dev) != MP_OK) {
+        fprintf(stderr, "magpie_codec: failed to load %s\n", path.c_str());
+        codec.dev = nullptr;
+        return false;
+    }
+    return true;
 }
 void magpie_codec_free(magpie_codec *codec) {
     if (!codec) return;

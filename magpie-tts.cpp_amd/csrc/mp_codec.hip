@@ -1010,7 +1010,8 @@ hipError_t launch_rb(mpc::RbP p, int nchunk, hipStream_t s) {
 }
 // the fused residual block for a stage's padded channel count (0: not fused)
 bool rb_fused(int Cp) {
-    const bool off = getenv("MAGPIE_CODEC_UNFUSED") != nullptr;  // A/B switch (read per decode): the two-launch blocks
+    const char *unf = getenv("MAGPIE_CODEC_UNFUSED");
+    const bool off = unf && atoi(unf) != 0;  // A/B switch (read per decode): the two-launch blocks
     return !off && (Cp == 224 || Cp == 128 || Cp == 64 || Cp == 32);
 }
 hipError_t run_rb(const mpc::RbP &p, int Cp, int nchunk, hipStream_t s) {

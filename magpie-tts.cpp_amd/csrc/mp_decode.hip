@@ -1,5 +1,5 @@
 // Per-frame decode kernels for gfx950 (f32 path, batch NB <= 8 utterances;
-// the F32 FFN convs of a Q8_0 file also at 16).
+// the F32 FFN convs of a Q8_0 / Q4_0 file also at 16).
 //
 // One decode iteration = 12 decoder layers (magpie_build_decoder_layer_gpu_cached,
 // magpie.cpp:3484-3528) + the 8-codebook local transformer
@@ -172,12 +172,9 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
     const bool done = p.done[b] != 0;
     const bool embed = p.x != nullptr && !p.lt_only;
     const int e = tid - 64;  // waves 1-3: float4 e of the row
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), pe = s;
-    if (embed && w >= 1) {
-        const int *cs = (done ? p.codes_prev : p.codes_cur) + b * NCB;
-        int ps = done ? p.pos[b] : p.pos[b] + 1;
+    // Σ_cb emb[cb][cs[cb]] over codebooks 0..ncb-1 in sequence, and position row ps
+    auto gather = [&](const int *cs, int ps, int ncb, float4 &s, float4 &pe) {
         ps = ps < p.pos_rows ? ps : p.pos_rows - 1;  // a slot that stops this frame reads a row it never uses
-        const int ncb = done ? NCB : NCB - 1;
         s = *(const float4 *)(p.emb + (size_t)cs[0] * D + 4 * e);
 #pragma unroll
         for (int cb = 1; cb < NCB; ++cb) {
@@ -186,13 +183,20 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
             s.x = s.x + r.x; s.y = s.y + r.y; s.z = s.z + r.z; s.w = s.w + r.w;
         }
         pe = *(const float4 *)(p.pos_emb + (size_t)ps * D + 4 * e);
+    };
+    auto store_x = [&](float4 s, float4 pe) {
+        *(float4 *)(p.x + (size_t)b * D + 4 * e) = make_float4(s.x * 0.125f + pe.x, s.y * 0.125f + pe.y,
+                                                               s.z * 0.125f + pe.z, s.w * 0.125f + pe.w);
+    };
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), pe = s;
+    if (embed && w >= 1) {
+        if (done) gather(p.codes_prev + b * NCB, p.pos[b], NCB, s, pe);
+        else gather(p.codes_cur + b * NCB, p.pos[b] + 1, NCB - 1, s, pe);
     }
-    __shared__ int sh_adv, sh_code;
+    __shared__ int sh_adv, sh_code, sh_stop;
     __syncthreads();  // every read of pos / codes above precedes wave 0's updates
     if (done) {
-        if (embed && w >= 1)
-            *(float4 *)(p.x + (size_t)b * D + 4 * e) = make_float4(s.x * 0.125f + pe.x, s.y * 0.125f + pe.y,
-                                                                   s.z * 0.125f + pe.z, s.w * 0.125f + pe.w);
+        if (embed && w >= 1) store_x(s, pe);
         return;
     }
     if (w == 0) {
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
                            p.audio_eos, p.smp, b, stp, NCB - 1, scratch, amax);
         }
         if (tid == 0) {
-            int adv = 0;
+            int adv = 0, stop = 0;
             int cc[NCB];
             int *ccp = p.codes_cur + b * NCB;
             ccp[NCB - 1] = i0;
@@ -228,6 +232,7 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
                     p.done[b] = 1;
                     p.nframes[b] = p.emit_eos ? st + 1 : st;
                     atomicAdd(p.ndone, 1);
+                    stop = 1;
                 } else {
                     for (int cb = 0; cb < NCB; ++cb) p.codes_out[((size_t)b * p.max_steps + st) * NCB + cb] = cc[cb];
                     p.step[b] = st + 1;
@@ -235,6 +240,7 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
                         p.done[b] = 1;
                         p.nframes[b] = st + 1;
                         atomicAdd(p.ndone, 1);
+                        stop = 1;
                     } else {
                         for (int cb = 0; cb < NCB; ++cb) p.codes_prev[b * NCB + cb] = cc[cb];
                         p.pos[b] = p.pos[b] + 1;
@@ -243,6 +249,7 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
                 }
             }
             sh_adv = adv;
+            sh_stop = stop;
             sh_code = i0;
         }
     }
@@ -250,8 +257,13 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
     if (sh_adv && embed && w >= 1) {
         const float4 r = *(const float4 *)(p.emb + ((size_t)(NCB - 1) * VCB + sh_code) * D + 4 * e);
         s.x = s.x + r.x; s.y = s.y + r.y; s.z = s.z + r.z; s.w = s.w + r.w;
-        *(float4 *)(p.x + (size_t)b * D + 4 * e) = make_float4(s.x * 0.125f + pe.x, s.y * 0.125f + pe.y,
-                                                               s.z * 0.125f + pe.z, s.w * 0.125f + pe.w);
+        store_x(s, pe);
+    } else if (sh_stop && embed && w >= 1) {
+        // the slot stopped this frame: from the next iteration on it gets its frozen
+        // input (the done branch's gather), so the iterations the batch still runs
+        // recompute this frame's values instead of running on the last FFN output
+        gather(p.codes_prev + b * NCB, p.pos[b], NCB, s, pe);
+        store_x(s, pe);
     }
     ts_end(p.ts, t_start);
 }

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     constexpr int KC = K / 32, KW = KC / MP_NWAVES;
     constexpr int KP = K + 8;  // padded bf16 row: rows land 16 B apart in the banks
     constexpr int NR = NB + 1;  // NB activation rows + one zero row for the unused MFMA columns
-    constexpr bool STAGE = PRO != PRO_PLAIN && PRO != PRO_PLAIN_B16;
+    constexpr bool STAGE = PRO != PRO_PLAIN && PRO != PRO_PLAIN_B16 && !(PRO == PRO_LN && NB >= 2);
     constexpr int SC = pro_scratch<NB, PRO>();
     __shared__ __attribute__((aligned(16))) float actf[STAGE ? NB * K : 4];
     __shared__ __attribute__((aligned(16))) unsigned short actb[NR * KP];
@@ -102,7 +102,19 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     for (int i = 0; i < KW; ++i) a[i] = wf[(size_t)i * 64];
 
     // activation rows -> bf16 in LDS; row NB is zero and feeds MFMA columns NB..15
-    if constexpr (STAGE) {
+    if constexpr (PRO == PRO_LN && NB >= 2) {
+        // LN rows rounded straight into the 16-bit tile (no f32 staging pass): the same
+        // y values the f32 rows held, rounded by the same RNE conversion
+        ln_slots<NB, K>(p, [&](int b, int k, float y) {
+            // y materialised as an f32 register first: the compiler would otherwise fuse the
+            // LN's last multiply into the f16 conversion (v_fma_mixlo_f16, one rounding
+            // instead of the batch-1 path's two: f32 row, then f16)
+            asm volatile("" : "+v"(y));
+            if constexpr (F16) actb[b * KP + k] = __builtin_bit_cast(unsigned short, (_Float16)y);
+            else actb[b * KP + k] = __builtin_bit_cast(unsigned short, (__bf16)y);
+        });
+        for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
+    } else if constexpr (STAGE) {
         prologue<NB, K, PRO>(p, actf, red, sc);
         for (int e = tid; e < NR * (K / 8); e += MP_BLOCK) {
             const int b = e / (K / 8), k = (e % (K / 8)) * 8;
@@ -166,7 +178,9 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
         for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     }
     lds_sync();
+#ifndef MP_TS_PROBE
     ts_mark(p.ts, t_start);  // profiling: activation tile staged
+#endif
 
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     const unsigned short *brow = actb + min(lane & 15, NB) * KP + 8 * (lane >> 4);

@@ -261,6 +261,52 @@ __device__ __forceinline__ void wave_meanvar(const float (&v)[PER], float &mean,
     var = bcast_lane63(M2) * (1.0f / (64.f * PER));
 }
 
+// wave_meanvar of S rows at once (row j: v[j]), the S chains advanced in lockstep so
+// their dependent DPP steps overlap; each row's arithmetic is wave_meanvar's exactly.
+template <int PER, int S>
+__device__ __forceinline__ void wave_meanvar_n(const float (&v)[S][PER], float (&mean)[S], float (&var)[S]) {
+    float m[S], M2[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        m[j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) m[j] += v[j][i];
+        m[j] *= 1.0f / PER;
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        M2[j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) { const float d = v[j][i] - m[j]; M2[j] += d * d; }
+    }
+    float n = (float)PER;
+    auto comb = [&](const float (&mb)[S], const float (&M2b)[S]) {
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const float d = mb[j] - m[j];
+            m[j] = m[j] + 0.5f * d;
+            M2[j] = M2[j] + M2b[j] + d * d * (0.5f * n);
+        }
+        n *= 2.f;
+    };
+    float mb[S], qb[S];
+#define MP_COMB_STEP(...)                                                            \
+    _Pragma("unroll") for (int j = 0; j < S; ++j) { mb[j] = __VA_ARGS__(m[j]); qb[j] = __VA_ARGS__(M2[j]); } \
+    comb(mb, qb);
+    MP_COMB_STEP(dpp_mov<0xB1>)
+    MP_COMB_STEP(dpp_mov<0x4E>)
+    MP_COMB_STEP(dpp_mov<0x141>)
+    MP_COMB_STEP(dpp_mov<0x140>)
+    MP_COMB_STEP(dpp_mov<0x142, 0xA>)
+    MP_COMB_STEP(dpp_mov<0x143, 0xC>)
+#undef MP_COMB_STEP
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        mean[j] = bcast_lane63(m[j]);
+        var[j] = bcast_lane63(M2[j]) * (1.0f / (64.f * PER));
+    }
+}
+
 // (value, index) argmax with the reference's tie rule: the FIRST maximal index
 // wins (strict '>' scan from index 0, magpie.cpp:1250-1258).
 __device__ __forceinline__ void argmax_merge(float &v, int &i, float v2, int i2) {

@@ -293,6 +293,81 @@ __device__ __forceinline__ void merge_weights(const float *pp, int stride, int n
     }
 }
 
+// Batched LayerNorm rows: wave w owns slots w, w+4, ...; the statistics are one
+// wave's DPP tree over the row (wave_meanvar), exactly as every wave computes them
+// at batch 1, so a batch reproduces its slots run alone. Every slot's row is loaded,
+// then every slot's statistics computed (independent DPP chains the scheduler can
+// interleave), then y = ((x - mean) * rstd) * lnw handed to put(b, k, y) for every
+// element (k = lane + 64 i). Block 0 stores the decoder hidden / trace rows after
+// that: a store in the middle would order the later loads and waits behind it.
+template <int NB, int K, typename Put>
+__device__ __forceinline__ void ln_slots(const GemvP &p, Put put) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int PER = K / 64, SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
+    float g[PER];
+    load_lnw<PER>(p.lnw, g);
+    float vs[SPW][PER];
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+        const int b = w + MP_NWAVES * j;
+        if (b < NB)
+#pragma unroll
+            for (int i = 0; i < PER; ++i) vs[j][i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
+    }
+#ifdef MP_TS_PROBE  // diagnostics build: (loads landed, stats done) / (stats done, rows put)
+    unsigned long long tA = 0, tB = 0;
+    if (p.ts) { __builtin_amdgcn_s_waitcnt(0); tA = __builtin_amdgcn_s_memrealtime(); }
+#endif
+    float mean[SPW], var[SPW], rstd[SPW];
+    if constexpr (SPW * MP_NWAVES == NB) {  // every wave owns SPW rows: one interleaved pass
+        wave_meanvar_n<PER, SPW>(vs, mean, var);
+    } else {
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            mean[j] = var[j] = 0.f;
+            if (w + MP_NWAVES * j < NB) wave_meanvar<PER>(vs[j], mean[j], var[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) rstd[j] = 1.0f / sqrtf(var[j] + p.eps);
+#ifdef MP_TS_PROBE
+    if (p.ts) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tB) : "v"(rstd[SPW - 1]), "v"(rstd[0]));
+#endif
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+        const int b = w + MP_NWAVES * j;
+        if (b >= NB) break;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            vs[j][i] = ((vs[j][i] - mean[j]) * rstd[j]) * g[i];
+            put(b, lane + 64 * i, vs[j][i]);
+        }
+    }
+#ifdef MP_TS_PROBE
+    if (p.ts) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tC = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && blockIdx.x < TS_BLOCKS)
+            *(ulonglong2 *)(p.ts + 2 * ((size_t)blockIdx.x * TS_WAVES + TS_WAVES / 2 + w)) =
+                w < 2 ? make_ulonglong2(tA, tB) : make_ulonglong2(tB, tC);
+    }
+#endif
+    if (blockIdx.x == 0 && (p.hidden_out || p.trace)) {
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b >= NB) break;
+            const int s = p.trace ? p.step[b] : 0;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int k = lane + 64 * i;
+                if (p.hidden_out) p.hidden_out[(size_t)b * K + k] = vs[j][i];
+                if (p.trace && s < p.trace_steps) p.trace[((size_t)b * p.trace_steps + s) * K + k] = vs[j][i];
+            }
+        }
+    }
+}
+
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red, float *sc) {
     const int tid = threadIdx.x;
@@ -423,39 +498,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
                 *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
         lds_sync();
     } else if constexpr (PRO == PRO_LN && NB >= 2) {
-        // batched: wave w owns slots w, w+4, ...; the statistics are one wave's DPP
-        // tree over the row, exactly as every wave computes them at batch 1
-        const int lane = tid & 63, w = tid >> 6;
-        constexpr int PER = K / 64, SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
-        float g[PER];  // in registers before any store: a load after a possibly aliasing
-        load_lnw<PER>(p.lnw, g);  // store would wait for it, one round trip per element
-        float vs[SPW][PER];  // every slot of this wave is loaded before any is reduced
-#pragma unroll
-        for (int j = 0; j < SPW; ++j) {
-            const int b = w + MP_NWAVES * j;
-            if (b < NB)
-#pragma unroll
-                for (int i = 0; i < PER; ++i) vs[j][i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
-        }
-#pragma unroll
-        for (int j = 0; j < SPW; ++j) {
-            const int b = w + MP_NWAVES * j;
-            if (b >= NB) break;
-            const float(&v)[PER] = vs[j];
-            float mean, var;
-            wave_meanvar<PER>(v, mean, var);
-            const float rstd = 1.0f / sqrtf(var + p.eps);
-            const bool st = p.hidden_out && blockIdx.x == 0;
-            const int s = (p.trace && blockIdx.x == 0) ? p.step[b] : 0;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int k = lane + 64 * i;
-                const float y = ((v[i] - mean) * rstd) * g[i];
-                act[b * K + k] = y;
-                if (st) p.hidden_out[(size_t)b * K + k] = y;
-                if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[((size_t)b * p.trace_steps + s) * K + k] = y;
-            }
-        }
+        ln_slots<NB, K>(p, [&](int b, int k, float y) { act[b * K + k] = y; });
         lds_sync();
     } else if constexpr (PRO == PRO_LN) {
         // batch 1: every wave loads the whole row and runs the same DPP statistics

@@ -3,11 +3,12 @@
 // Exposes the C-ABI declared in include/magpie_hip.h.
 //
 // Design: one mp_dev per GPU. Weights are uploaded once (f32, one
-// arena). A batch of B <= 8 utterances occupies NB = next_pow2(B) slots; every
+// arena). A batch of B utterances (1..8 with f32 weights, 1..16 in the bf16 / F16 /
+// Q8_0 / Q4_0 modes: mp_hip_max_batch) occupies NB = next_pow2(B) slots; every
 // per-utterance quantity (residual stream, KV cache, XA K/V, codes, position,
 // done flag) lives in HBM and is addressed by slot, so one decode iteration
-// (12 decoder layers + 8-codebook local transformer + EOS bookkeeping, 133
-// kernels at NB=1) is captured once as a hipGraph and replayed per frame with
+// (12 decoder layers + 8-codebook local transformer + EOS bookkeeping, 65
+// kernels at NB=1 in the f32 mode) is captured once as a hipGraph and replayed per frame with
 // no host round trip; the host only polls the done counter every few frames.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -1732,7 +1733,7 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
     const int bmax = mp_hip_max_batch(dev);
     if (!tokens || !n_tokens || !speaker || B < 1 || B > bmax || tmax < 1 || !params)
-        return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..8, 1..16 with bf16 weights)");
+        return fail(dev, MP_ERR_ARG, "invalid arguments (B must be 1..mp_hip_max_batch: 8 with f32 weights, 16 in the bf16 / F16 / Q8_0 / Q4_0 modes)");
     if (params->temperature >= 0.01f && (params->top_k < 1 || params->top_k > mp::VCB))
         return fail(dev, MP_ERR_ARG, "top_k must be in 1..2024 when sampling");
     int Tmax = 0;
@@ -2310,7 +2311,9 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     // an op carrying an in-launch hand-off (QKV -> SA, O-projection -> XA) tags it with the
     // iteration counter: relaunched with the same tag, its consumers would find the previous
     // launch's granules and not wait for their producers (a different, shorter critical path)
-    if (r.kind == mp::K_GEMV && r.g.iter)
+    const bool handoff = (r.kind == mp::K_GEMV && r.g.iter) || (r.kind == mp::K_LTSLOT && r.l2.gh) ||
+                         r.kind == mp::K_LTFRONT || r.kind == mp::K_LTSLOTQ8 || (r.kind == mp::K_ATTN && r.a.gh);
+    if (handoff)
         return fail(dev, MP_ERR_ARG, "op carries an in-launch hand-off: back-to-back timing would not wait for it");
     HIPCHK(launch());  // warm
     hipEvent_t e0, e1;

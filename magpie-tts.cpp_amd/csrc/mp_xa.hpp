@@ -42,6 +42,46 @@ __device__ __forceinline__ float gh_wait(const unsigned long long *g, unsigned t
         __builtin_amdgcn_s_sleep(1);
     }
 }
+// One round of the XA online softmax: keys tb + XA_WAVES u (u < XA_KPW; those >= t1
+// are masked), K' rows k[u], V' rows vv[u], query h (this lane's elements).
+// score_u = wave_sum(fmaf chain of k . h over the lane's elements) * scale; one
+// rescale c = exp(m - mn) for the round, then the keys' e_u = exp(score_u - mn) added
+// in key order: l = l c + Σ e_u, o = o c + Σ e_u v_u (each term an explicit fmaf).
+__device__ __forceinline__ void xa_round(const float4 (&k)[XA_KPW][XA_V], const float4 (&vv)[XA_KPW][XA_V],
+                                         const float4 (&h)[XA_V], float scale, int tb, int t1, float &m, float &l,
+                                         float4 (&o)[XA_V]) {
+#pragma clang fp contract(off)
+    float sv[XA_KPW], mn = m;
+#pragma unroll
+    for (int u = 0; u < XA_KPW; ++u) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < XA_V; ++i) {
+            acc = fmaf(k[u][i].x, h[i].x, acc);
+            acc = fmaf(k[u][i].y, h[i].y, acc);
+            acc = fmaf(k[u][i].z, h[i].z, acc);
+            acc = fmaf(k[u][i].w, h[i].w, acc);
+        }
+        sv[u] = tb + XA_WAVES * u < t1 ? wave_sum(acc) * scale : -INFINITY;
+        mn = fmaxf(mn, sv[u]);
+    }
+    const float c = expf(m - mn);
+    l = l * c;
+#pragma unroll
+    for (int i = 0; i < XA_V; ++i) { o[i].x = o[i].x * c; o[i].y = o[i].y * c; o[i].z = o[i].z * c; o[i].w = o[i].w * c; }
+#pragma unroll
+    for (int u = 0; u < XA_KPW; ++u) {
+        const float e = expf(sv[u] - mn);
+        l = l + e;
+#pragma unroll
+        for (int i = 0; i < XA_V; ++i) {
+            o[i].x = fmaf(e, vv[u][i].x, o[i].x); o[i].y = fmaf(e, vv[u][i].y, o[i].y);
+            o[i].z = fmaf(e, vv[u][i].z, o[i].z); o[i].w = fmaf(e, vv[u][i].w, o[i].w);
+        }
+    }
+    m = mn;
+}
+
 // Split sp of slot b. HANDOFF: x1 comes from the O-projection in the same launch,
 // as {tag, value} granules xh[b][768] (EPI_RESID_XA): every wave sweeps all 768
 // with relaxed agent-scope loads (write-through producer stores, so no fence is
@@ -127,23 +167,12 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
 #pragma unroll
     for (int i = 0; i < XA_V; ++i) o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int tb = t0 + w; tb < t1; tb += XA_WAVES * XA_KPW) {
-#pragma unroll
-        for (int u = 0; u < XA_KPW; ++u) {
-            const int t = tb + XA_WAVES * u;
-            if (t >= t1) break;  // wave-uniform
-            float acc = 0.f;
-#pragma unroll
-            for (int i = 0; i < XA_V; ++i) acc += dotv(k[u][i], h[i]);
-            const float sv = wave_sum(acc) * scale;
-            const float mn = fmaxf(m, sv), c = expf(m - mn), e = expf(sv - mn);
-            l = l * c + e;
-#pragma unroll
-            for (int i = 0; i < XA_V; ++i) {
-                o[i].x = o[i].x * c + e * vv[u][i].x; o[i].y = o[i].y * c + e * vv[u][i].y;
-                o[i].z = o[i].z * c + e * vv[u][i].z; o[i].w = o[i].w * c + e * vv[u][i].w;
-            }
-            m = mn;
-        }
+        // A round's XA_KPW scores first (independent wave reductions the scheduler
+        // interleaves), then one online-softmax update for the set (keys past t1 weigh
+        // 0). Every rounding is spelled out (contraction off, explicit fmaf in a fixed
+        // order), so each instantiation of this body (batch 1 / batched, handed-off /
+        // standalone, f32 / 16-bit families) computes the same bits.
+        xa_round(k, vv, h, scale, tb, t1, m, l, o);
         const int tn = tb + XA_WAVES * XA_KPW;
         if (tn >= t1) break;
 #pragma unroll
@@ -168,7 +197,7 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
 #pragma unroll
     for (int q = 0; q < XA_WAVES; ++q) {
         e[q] = wm[q] == -INFINITY ? 0.f : expf(wm[q] - M);
-        den += e[q] * wl[q];
+        den = fmaf(e[q], wl[q], den);
     }
     float *pp = p.part + ((size_t)b * XA_SPLITS + sp) * XA_PART;
     const unsigned long long tagx = (unsigned long long)tag << 32;  // XaP::x2: the granules' tag
@@ -177,7 +206,8 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
 #pragma unroll
         for (int q = 0; q < XA_WAVES; ++q) {
             const float4 v4 = *(const float4 *)&wo[q][4 * tid];
-            num.x += e[q] * v4.x; num.y += e[q] * v4.y; num.z += e[q] * v4.z; num.w += e[q] * v4.w;
+            num.x = fmaf(e[q], v4.x, num.x); num.y = fmaf(e[q], v4.y, num.y);
+            num.z = fmaf(e[q], v4.z, num.z); num.w = fmaf(e[q], v4.w, num.w);
         }
         if (p.x2) {  // granules: the slot's split workgroups merge them (xa_merge_split)
             gu64 *g = (gu64 *)p.gh + ((size_t)b * XA_SPLITS + sp) * XA_PART + 4 + 4 * tid;

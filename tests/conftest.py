@@ -44,6 +44,13 @@ def full_model():
 
 
 @pytest.fixture(scope="session")
+def full_model_default_heads():
+    """Magpie-357M shapes with the survey's default LT head distribution (scale 1.0):
+    near-flat logits, so most decisions are close calls (the margin rule's hard case)."""
+    return _gguf("magpie_357m_f32.gguf")
+
+
+@pytest.fixture(scope="session")
 def eos_model():
     import magpie_amd as ma
     os.makedirs(CACHE, exist_ok=True)

@@ -303,7 +303,13 @@ int use(magpie_context *ctx, magpie_codec *codec) {
     std::vector<int32_t> ids = magpie_tokenize(&ctx->model.tokenizer, "Hello");
     std::vector<int32_t> codes = magpie_synthesize_codes_graph_reuse(ctx, ids.data(), (int)ids.size());
     magpie_sample_result r = magpie_local_transformer_sample_all(ctx, nullptr, 0.7f, 80, false);
-    return (int)n + s + (ok ? 1 : 0) + (int)codes.size() + (int)r.argmax_codes.size();
+    // src/magpie.h:332, 555-558, 753
+    bool enc = magpie_encode_text(ctx, ids.data(), (int)ids.size()) && ctx->state.enc_seq_len > 0;
+    magpie_model m;
+    bool ld = magpie_model_load(std::string("model.gguf"), m) && magpie_model_load("model.gguf", m, MAGPIE_BACKEND_CPU);
+    magpie_codec c;
+    bool cl = magpie_codec_load(std::string("codec.gguf"), c, MAGPIE_BACKEND_AUTO);
+    return (int)n + s + (ok ? 1 : 0) + (int)codes.size() + (int)r.argmax_codes.size() + enc + ld + cl;
 }
 '''
 

@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.join(REPO, "magpie-tts.cpp_amd"))
 import magpie_amd as ma  # noqa: E402
 
 TS_WAVES, TS_BLOCKS = 8, 1024
+ROLE_SPLIT = {}  # op name -> row workgroups (set per batch in main)
 
 
 def main():
@@ -29,6 +30,7 @@ def main():
     toks = [ma.synthetic_tokens(64, seed=1000 + b) for b in range(B)]
     dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=128, ignore_eos=True)
     names = dev.ops()
+    ROLE_SPLIT.update({"oproj_xa": 48, "qkv_sa": 144})
     dev.profile_ops_ts(iters=2)
     raw = np.fromfile(dump, dtype=np.uint64).reshape(len(names), TS_BLOCKS, TS_WAVES, 2).astype(np.int64)
     seen = set()
@@ -45,11 +47,23 @@ def main():
         nb = int(ok[:, :4].any(axis=1).sum())
         st, en = rel[:nb, :4, 0], rel[:nb, :4, 1]
         mk = rel[:nb, 4:, 1][ok[:nb, 4:]]
+        mk0 = rel[:nb, 4:, 0][ok[:nb, 4:]]
         line = (f"{n:10s} wgs {nb:4d} start p50 {np.median(st):5.2f} max {st.max():5.2f} | "
                 f"end p50 {np.median(en):5.2f} max {en.max():5.2f}")
         if mk.size:
-            line += f" | mark p50 {np.median(mk):5.2f} max {mk.max():5.2f}"
+            line += f" | mark p50 {np.median(mk):5.2f} max {mk.max():5.2f} (first stamp p50 {np.median(mk0):5.2f})"
         print(line)
+        # launches with two roles (row workgroups, then the attention tail): each apart
+        nrow = ROLE_SPLIT.get(n)
+        if nrow and nb > nrow:
+            for lo, hi, role in ((0, nrow, "rows"), (nrow, nb, "tail")):
+                okr = ok[lo:hi, :4]
+                e2 = rel[lo:hi, :4, 1][okr]
+                m2 = rel[lo:hi, 4:, 1][ok[lo:hi, 4:]]
+                txt = f"   {role:5s} wgs {hi - lo:4d} end p50 {np.median(e2):5.2f} max {e2.max():5.2f}"
+                if m2.size:
+                    txt += f" | mark p50 {np.median(m2):5.2f} min {m2.min():5.2f} max {m2.max():5.2f}"
+                print(txt)
     dev.close()
 
 

@@ -227,8 +227,7 @@ def main() -> None:
         os.write(1, (json.dumps({"rank": rank, "local_rank": local, "world": world, "ranks_seen": seen,
                                  "weights": args.weights, "batch_per_gpu": args.batch,
                                  "scaling_baseline": {"weights": "bf16", "batch_per_gpu": SCALE_BATCH,
-                                                      "measured": "rank 0 alone" if world > 1 else "after the headline"},
-                                 "efficiency": "value / (n_gpus x scaling_baseline.value)" if world > 1 else None})
+                                                      "measured": "rank 0 alone" if world > 1 else "after the headline"}})
                      + "\n").encode())
         return
     # one rank per GPU; with fewer GPUs than ranks (a rehearsal) ranks share devices
@@ -438,7 +437,8 @@ def main() -> None:
         cpu = {"value": round(res["frames"] / res["decode_s"], 2), "unit": "frames/s", "cores": args.cpu_threads,
                "kind": "port",
                "sample": f"1 utterance x {res['frames']} frames (T={args.tokens}), decode loop only "
-                         f"(preamble {res['preamble_s']:.2f}s excluded), oracle f32-accumulate mode"}
+                         f"(preamble {res['preamble_s']:.2f}s excluded), oracle f32-accumulate mode",
+               "cpu_model": cpu_model_name()}
         # also at every core this process may use (the box's CPU share)
         nall = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
         if nall != args.cpu_threads:
@@ -485,8 +485,6 @@ def main() -> None:
             "decode_roofline": {"bytes_per_frame": round(bpf), "achieved_GBs": round(bpf * fps_per_gpu / 1e9, 1),
                                 "frac": round(bpf * fps_per_gpu / 1e9 / HBM_PEAK_GBS, 4)},
             "scaling_baseline": scaling,
-            "efficiency": (round(value / (world * scaling["value"]), 4)
-                           if world > 1 and scaling and scaling["value"] else None),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "ops": op_table,
@@ -496,6 +494,18 @@ def main() -> None:
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def cpu_model_name() -> str:
+    """The host CPU the cpu_baseline ran on (/proc/cpuinfo 'model name')."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 if __name__ == "__main__":

@@ -66,18 +66,28 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     // so the HBM latency overlaps the prologue's own dependent loads/reductions.
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int row0 = (blockIdx.x * MP_NWAVES + w) * RW + ts_dep(t_start);
+    // PRO_LN: the rows are loaded ahead of the weights (pre_load), the rest as before
+    PreRows<NB, K, PRO> pre;
+    constexpr bool PRE = PreRows<NB, K, PRO>::ON;
+    if constexpr (PRE) {
+        pre_load<NB, K, PRO>(p, pre);
+        __builtin_amdgcn_sched_barrier(0);  // issue order: rows, weights, then arithmetic
+    }
     VT wv[RW][NV];
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
         const int n = row0 + r < p.N ? row0 + r : p.N - 1;
         const VT *wr = (const VT *)(p.W + (size_t)n * K);
 #pragma unroll
-        for (int i = 0; i < NV; ++i) wv[r][i] = wr[lane + 64 * i];
+        for (int i = 0; i < NV; ++i) wv[r][i] = ld_weight(wr + lane + 64 * i);
     }
+    if constexpr (PRE) __builtin_amdgcn_sched_barrier(0);
     float acc[RW][NB];
 #pragma unroll
     for (int hh = 0; hh < NB / NBS; ++hh) {
-        if constexpr (NBS == NB) {
+        if constexpr (PRE) {
+            pre_finish<NB, K, PRO>(p, pre, act);
+        } else if constexpr (NBS == NB) {
             prologue<NB, K, PRO>(p, act, red, sc);
         } else {
             if (hh) lds_sync();  // every wave is done with the previous slots' rows

@@ -64,13 +64,22 @@ __device__ __forceinline__ floatx4 mfma16(uint4 a, uint4 b, floatx4 c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-template <int NB, int K, int PRO, int EPI, bool F16 = false>
+// KS > 1: split-K. A row tile's K is cut into KS slices, one workgroup each (blocks
+// tile * KS + ks, consecutive, so a tile's workgroups are dispatched together); each
+// stages only its slice of the activations, publishes its 16 x 16 partial tile as
+// {tag, value} granules and merges 16 / KS of the tile's rows from the KS partials,
+// added in slice order, then runs the epilogue. KS is a function of the op (K) only,
+// never of NB, so every batch size computes the same bits.
+template <int NB, int K, int PRO, int EPI, bool F16 = false, int KS = 1>
 __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     static_assert(NB >= 1 && NB <= 16, "one 16-column MFMA tile of utterances");
-    static_assert(K % 128 == 0, "K splits into 4 waves x 32-wide chunks");
-    constexpr int KC = K / 32, KW = KC / MP_NWAVES;
-    constexpr int KP = K + 8;  // padded bf16 row: rows land 16 B apart in the banks
+    static_assert(K % (128 * KS) == 0, "K splits into KS slices of 4 waves x 32-wide chunks");
+    static_assert(KS == 1 || PRO == PRO_PLAIN || PRO == PRO_PLAIN_B16, "split-K stages plain rows only");
+    static_assert(16 % KS == 0, "a split workgroup merges 16 / KS rows");
+    constexpr int KL = K / KS;  // this workgroup's K slice
+    constexpr int KC = K / 32, KCS = KL / 32, KW = KCS / MP_NWAVES;
+    constexpr int KP = KL + 8;  // padded bf16 row: rows land 16 B apart in the banks
     constexpr int NR = NB + 1;  // NB activation rows + one zero row for the unused MFMA columns
     constexpr bool STAGE = PRO != PRO_PLAIN && PRO != PRO_PLAIN_B16 && !(PRO == PRO_LN && NB >= 2);
     constexpr int SC = pro_scratch<NB, PRO>();
@@ -93,19 +102,30 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
             return;
         }
     }
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rt = KS == 1 ? (int)blockIdx.x : (int)blockIdx.x / KS, ks = KS == 1 ? 0 : (int)blockIdx.x % KS;
+
+    // batched LN rows: loaded ahead of the weight stream (vector loads complete in
+    // issue order, so rows loaded behind the weights would wait for all of them)
+    constexpr bool LNB = PRO == PRO_LN && NB >= 2;
+    PreRows<NB, K, PRO> pre;
+    if constexpr (PreRows<NB, K, PRO>::ON) {
+        pre_load<NB, K, PRO>(p, pre);
+        __builtin_amdgcn_sched_barrier(0);  // keep the issue order: rows, then weights, then arithmetic
+    }
 
     // weight fragments of this wave's K slice, issued before the prologue
-    const uint4 *wf = (const uint4 *)p.Wb + ((size_t)rt * KC + w * KW) * 64 + lane + ts_dep(t_start);
+    const uint4 *wf = (const uint4 *)p.Wb + ((size_t)rt * KC + ks * KCS + w * KW) * 64 + lane + ts_dep(t_start);
     uint4 a[KW];
 #pragma unroll
-    for (int i = 0; i < KW; ++i) a[i] = wf[(size_t)i * 64];
+    for (int i = 0; i < KW; ++i) a[i] = ld_weight(wf + (size_t)i * 64);
+    if constexpr (PreRows<NB, K, PRO>::ON) __builtin_amdgcn_sched_barrier(0);
 
     // activation rows -> bf16 in LDS; row NB is zero and feeds MFMA columns NB..15
-    if constexpr (PRO == PRO_LN && NB >= 2) {
+    if constexpr (LNB) {
         // LN rows rounded straight into the 16-bit tile (no f32 staging pass): the same
         // y values the f32 rows held, rounded by the same RNE conversion
-        ln_slots<NB, K>(p, [&](int b, int k, float y) {
+        ln_finish<NB, K>(p, pre.r, [&](int b, int k, float y) {
             // y materialised as an f32 register first: the compiler would otherwise fuse the
             // LN's last multiply into the f16 conversion (v_fma_mixlo_f16, one rounding
             // instead of the batch-1 path's two: f32 row, then f16)
@@ -115,7 +135,8 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
         });
         for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     } else if constexpr (STAGE) {
-        prologue<NB, K, PRO>(p, actf, red, sc);
+        if constexpr (PreRows<NB, K, PRO>::ON) pre_finish<NB, K, PRO>(p, pre, actf);  // batch 1
+        else prologue<NB, K, PRO>(p, actf, red, sc);
         for (int e = tid; e < NR * (K / 8); e += MP_BLOCK) {
             const int b = e / (K / 8), k = (e % (K / 8)) * 8;
             uint4 o = make_uint4(0, 0, 0, 0);
@@ -131,33 +152,34 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     } else if constexpr (PRO == PRO_PLAIN_B16) {
         // bf16 rows (written by the FFN-up epilogue): copied as they are, 12 uint4
         // per thread in flight
-        constexpr int ITEMS = NB * (K / 8), BATCH = 12;
+        constexpr int ITEMS = NB * (KL / 8), BATCH = 12;
+        const unsigned short *src = p.src_b16 + ks * KL;
         for (int base = 0; base < ITEMS; base += BATCH * MP_BLOCK) {
             uint4 v[BATCH];
 #pragma unroll
             for (int u = 0; u < BATCH; ++u) {
                 const int e = base + u * MP_BLOCK + tid;
-                v[u] = e < ITEMS ? *(const uint4 *)(p.src_b16 + (size_t)(e / (K / 8)) * p.src_ld + (e % (K / 8)) * 8)
+                v[u] = e < ITEMS ? *(const uint4 *)(src + (size_t)(e / (KL / 8)) * p.src_ld + (e % (KL / 8)) * 8)
                                  : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
             for (int u = 0; u < BATCH; ++u) {
                 const int e = base + u * MP_BLOCK + tid;
-                if (e < ITEMS) *(uint4 *)(actb + (e / (K / 8)) * KP + (e % (K / 8)) * 8) = v[u];
+                if (e < ITEMS) *(uint4 *)(actb + (e / (KL / 8)) * KP + (e % (KL / 8)) * 8) = v[u];
             }
         }
-        for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
+        for (int e = tid; e < KL / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     } else {
         // NB rows straight from HBM/L2, in batches of 8 items per thread with all
         // 16 loads issued before the first conversion (one latency per batch)
-        constexpr int ITEMS = NB * (K / 8), BATCH = 8;
+        constexpr int ITEMS = NB * (KL / 8), BATCH = 8;
         for (int base = 0; base < ITEMS; base += BATCH * MP_BLOCK) {
             float4 x0[BATCH], x1[BATCH];
 #pragma unroll
             for (int u = 0; u < BATCH; ++u) {
                 const int e = base + u * MP_BLOCK + tid;
                 if (e < ITEMS) {
-                    const float *src = p.src + (size_t)(e / (K / 8)) * p.src_ld + (e % (K / 8)) * 8;
+                    const float *src = p.src + ks * KL + (size_t)(e / (KL / 8)) * p.src_ld + (e % (KL / 8)) * 8;
                     x0[u] = *(const float4 *)src;
                     x1[u] = *(const float4 *)(src + 4);
                 }
@@ -171,11 +193,11 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
                     o.y = pk16<F16>(x0[u].z, x0[u].w);
                     o.z = pk16<F16>(x1[u].x, x1[u].y);
                     o.w = pk16<F16>(x1[u].z, x1[u].w);
-                    *(uint4 *)(actb + (e / (K / 8)) * KP + (e % (K / 8)) * 8) = o;
+                    *(uint4 *)(actb + (e / (KL / 8)) * KP + (e % (KL / 8)) * 8) = o;
                 }
             }
         }
-        for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
+        for (int e = tid; e < KL / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     }
     lds_sync();
 #ifndef MP_TS_PROBE
@@ -193,10 +215,51 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     part[w][lane] = acc;
     lds_sync();
     // thread t -> (row t/16, column t%16); D[row][col] sits in lane (row/4)*16 + col, register row%4
-    const int row = tid >> 4, col = tid & 15;
+    int row = tid >> 4;
+    const int col = tid & 15;
+    float v;
+    {
+        const int ls = (row >> 2) * 16 + col, rg = row & 3;
+        v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
+    }
+    if constexpr (KS > 1) {
+        // publish this slice's partial (row, col) ...
+        using gu64 = __attribute__((address_space(1))) unsigned long long;
+        const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+        gu64 *gt = (gu64 *)p.kgh + (size_t)rt * KS * 256;
+        __hip_atomic_store(gt + ks * 256 + tid, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        // ... and merge rows [ks * 16 / KS, (ks + 1) * 16 / KS) of the tile: the KS partials
+        // of (row, col), added in slice order (a bounded sweep; poisoned + HX_ERR_KS if a
+        // sibling never publishes)
+        constexpr int MR = 16 / KS;
+        if (tid >= MR * 16) return;
+        row = ks * MR + (tid >> 4);
+        const int gi = row * 16 + col;
+        float pv[KS];
+        for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                const unsigned long long u = __hip_atomic_load(gt + s2 * 256 + gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok &= (unsigned)(u >> 32) == tag;
+                pv[s2] = __uint_as_float((unsigned)u);
+            }
+            if (__all(ok)) break;
+            if (spins >= (1u << 20)) {
+                if ((tid & 63) == 0) __hip_atomic_fetch_or((__attribute__((address_space(1))) int *)p.hx_err, HX_ERR_KS,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int s2 = 0; s2 < KS; ++s2) pv[s2] = __builtin_nanf("");
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        v = pv[0];
+#pragma unroll
+        for (int s2 = 1; s2 < KS; ++s2) v = v + pv[s2];
+    }
     if (col >= NB) return;
-    const int ls = (row >> 2) * 16 + col, rg = row & 3;
-    const float v = ((part[0][ls][rg] + part[1][ls][rg]) + part[2][ls][rg]) + part[3][ls][rg];
     const int n = rt * 16 + row;
     if (n >= p.N) return;
     if constexpr (EPI == EPI_RESID_XA) publish_x1(p, v, n, col);
@@ -234,15 +297,21 @@ static bool b16_args_ok(const GemvP &p) {
     return ok;
 }
 
-template <int NB, int K, int PRO, int EPI, bool F16 = false>
+template <int NB, int K, int PRO, int EPI, bool F16 = false, int KS = 1>
 static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     if (!b16_args_ok<PRO, EPI>(p)) return hipErrorInvalidValue;
+    if (KS > 1 && (!p.kgh || !p.iter || !p.hx_err)) return hipErrorInvalidValue;
     GemvP q = p;
-    q.nrow_blocks = (p.N + 15) / 16;
+    q.nrow_blocks = (p.N + 15) / 16 * KS;  // row workgroups (KS per 16-row tile)
     const int grid = q.nrow_blocks + (EPI == EPI_RESID_XA ? XA_SPLITS * NB : EPI == EPI_QKV_SA ? NH * SA_SPLITS * NB : 0);
-    mp::launch((gemm_b16_kernel<NB, K, PRO, EPI, F16>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
+    mp::launch((gemm_b16_kernel<NB, K, PRO, EPI, F16, KS>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();
 }
+// split-K of the FFN-down projection (K = 3072, 48 row tiles): a function of the op only
+#ifndef MP_FF2_KS
+#define MP_FF2_KS 1
+#endif
+constexpr int FF2_KS = MP_FF2_KS;
 
 #define MP_B16_OPS(NB)                                                                                                  \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
@@ -253,7 +322,7 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     }                                                                                                                   \
     hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_B16>(p, s); }     \
     hipError_t b16_ff1p_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_GELU_B16>(p, s); }       \
-    hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE>(p, s); }  \
+    hipError_t b16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE, false, FF2_KS>(p, s); }  \
     hipError_t b16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
     hipError_t b16_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_ATTN, EPI_LTX_ADD>(p, s); } \
     hipError_t b16_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE>(p, s); } \
@@ -271,7 +340,7 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
         return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA, true>(p, s);                                                 \
     }                                                                                                                   \
     hipError_t f16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_F16, true>(p, s); }     \
-    hipError_t f16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE, true>(p, s); }  \
+    hipError_t f16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE, true, FF2_KS>(p, s); }  \
     hipError_t f16_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTX_LN, EPI_LTQKV, true>(p, s); }    \
     hipError_t f16_lt_bg_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LTARG_ATTN, EPI_LTX_ADD, true>(p, s); } \
     hipError_t f16_lt_b_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, LTD, PRO_LT_ATTN, EPI_ADD_STORE, true>(p, s); } \

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     AT a[KW];
     uint4 sd[KW];
 #pragma unroll
-    for (int i = 0; i < KW; ++i) { a[i] = wf[(size_t)i * 64]; sd[i] = sf[(size_t)i * 4]; }
+    for (int i = 0; i < KW; ++i) { a[i] = ld_weight(wf + (size_t)i * 64); sd[i] = ld_weight(sf + (size_t)i * 4); }
 
     prologue<NB, K, PRO>(p, act, red, sc);
 

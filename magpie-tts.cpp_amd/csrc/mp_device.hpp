@@ -352,6 +352,27 @@ __device__ __forceinline__ float4 kv_load4(const float *c, size_t i) {
     else return *(const float4 *)(c + i);
 }
 
+// Weight-stream loads (read once per launch by one CU). MP_NT_WEIGHTS builds issue
+// them non-temporal (global_load ... nt): the guide's nt-weights row; default off
+// until measured on this path.
+template <typename T>
+__device__ __forceinline__ T ld_weight(const T *p) {
+#ifdef MP_NT_WEIGHTS
+    if constexpr (sizeof(T) == 16) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        return __builtin_bit_cast(T, __builtin_nontemporal_load((const u4 *)p));
+    } else if constexpr (sizeof(T) == 8) {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        return __builtin_bit_cast(T, __builtin_nontemporal_load((const u2 *)p));
+    } else {
+        static_assert(sizeof(T) == 4, "4, 8 or 16 B");
+        return __builtin_bit_cast(T, __builtin_nontemporal_load((const unsigned *)p));
+    }
+#else
+    return *p;
+#endif
+}
+
 __device__ __forceinline__ float dotv(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
 __device__ __forceinline__ float dotv(float2 a, float2 b) { return a.x * b.x + a.y * b.y; }
 __device__ __forceinline__ float dotv(float a, float b) { return a * b; }

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "mp_device.hpp"
 #include "mp_params.hpp"
 
@@ -300,20 +302,35 @@ __device__ __forceinline__ void merge_weights(const float *pp, int stride, int n
 // interleave), then y = ((x - mean) * rstd) * lnw handed to put(b, k, y) for every
 // element (k = lane + 64 i). Block 0 stores the decoder hidden / trace rows after
 // that: a store in the middle would order the later loads and waits behind it.
-template <int NB, int K, typename Put>
-__device__ __forceinline__ void ln_slots(const GemvP &p, Put put) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    constexpr int PER = K / 64, SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
+template <int NB, int K>
+struct LnRows {
+    static constexpr int PER = K / 64, SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
     float g[PER];
-    load_lnw<PER>(p.lnw, g);
     float vs[SPW][PER];
+};
+// the loads of ln_slots (LN weights, this wave's rows): issued apart from the
+// arithmetic so a caller can put them ahead of its weight stream (vector-memory
+// loads complete in issue order: a row load issued behind the weights is only
+// usable once every weight load before it has landed)
+template <int NB, int K>
+__device__ __forceinline__ void ln_load(const GemvP &p, LnRows<NB, K> &r) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int PER = LnRows<NB, K>::PER, SPW = LnRows<NB, K>::SPW;
 #pragma unroll
     for (int j = 0; j < SPW; ++j) {
         const int b = w + MP_NWAVES * j;
         if (b < NB)
 #pragma unroll
-            for (int i = 0; i < PER; ++i) vs[j][i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
+            for (int i = 0; i < PER; ++i) r.vs[j][i] = p.src[(size_t)b * p.src_ld + lane + 64 * i];
     }
+    load_lnw<PER>(p.lnw, r.g);
+}
+template <int NB, int K, typename Put>
+__device__ __forceinline__ void ln_finish(const GemvP &p, LnRows<NB, K> &r, Put put) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int PER = LnRows<NB, K>::PER, SPW = LnRows<NB, K>::SPW;
+    float(&g)[PER] = r.g;
+    float(&vs)[SPW][PER] = r.vs;
 #ifdef MP_TS_PROBE  // diagnostics build: (loads landed, stats done) / (stats done, rows put)
     unsigned long long tA = 0, tB = 0;
     if (p.ts) { __builtin_amdgcn_s_waitcnt(0); tA = __builtin_amdgcn_s_memrealtime(); }
@@ -364,6 +381,83 @@ __device__ __forceinline__ void ln_slots(const GemvP &p, Put put) {
                 if (p.hidden_out) p.hidden_out[(size_t)b * K + k] = vs[j][i];
                 if (p.trace && s < p.trace_steps) p.trace[((size_t)b * p.trace_steps + s) * K + k] = vs[j][i];
             }
+        }
+    }
+}
+template <int NB, int K, typename Put>
+__device__ __forceinline__ void ln_slots(const GemvP &p, Put put) {
+    LnRows<NB, K> r;
+    ln_load<NB, K>(p, r);
+    ln_finish<NB, K>(p, r, put);
+}
+
+// Batch-1 LayerNorm row (PRO_LN, NB = 1): every wave loads the whole row and runs
+// the same DPP statistics (identical results, no barrier), then writes its quarter
+// of act. Loads and arithmetic apart, as ln_load / ln_finish.
+template <int K>
+struct Ln1Row {
+    static constexpr int PER = K / 64;
+    float v[PER], g[PER];
+    int s;  // trace row (block 0 with a trace only)
+};
+template <int K>
+__device__ __forceinline__ void ln1_load(const GemvP &p, Ln1Row<K> &r) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < Ln1Row<K>::PER; ++i) r.v[i] = p.src[lane + 64 * i];
+    load_lnw<Ln1Row<K>::PER>(p.lnw, r.g);
+    r.s = (p.trace && blockIdx.x == 0) ? p.step[0] : 0;
+}
+template <int K>
+__device__ __forceinline__ void ln1_finish(const GemvP &p, Ln1Row<K> &r, float *act) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int PER = K / 64, Q = PER / MP_NWAVES;
+    float mean, var;
+    wave_meanvar<PER>(r.v, mean, var);
+    const float rstd = 1.0f / sqrtf(var + p.eps);
+    const bool st = p.hidden_out && blockIdx.x == 0;
+    const int s = r.s;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        if (i / Q != w) continue;
+        const int k = lane + 64 * i;
+        const float y = ((r.v[i] - mean) * rstd) * r.g[i];
+        act[k] = y;
+        if (st) p.hidden_out[k] = y;
+        if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[(size_t)s * K + k] = y;
+    }
+    lds_sync();
+}
+
+// A prologue whose global loads a kernel issues AHEAD of its weight stream
+// (vector-memory loads complete in issue order: rows loaded behind the weights are
+// only usable once every weight has landed). PRO_LN only: its loads are the rows and
+// the LN weights, all independent of the launch's other work.
+template <int NB, int K, int PRO>
+struct PreRows {
+    static constexpr bool ON = false;
+};
+template <int NB, int K>
+struct PreRows<NB, K, PRO_LN> {
+    static constexpr bool ON = true;
+    typename std::conditional<NB == 1, Ln1Row<K>, LnRows<NB, K>>::type r;
+};
+template <int NB, int K, int PRO>
+__device__ __forceinline__ void pre_load(const GemvP &p, PreRows<NB, K, PRO> &pr) {
+    if constexpr (PreRows<NB, K, PRO>::ON) {
+        if constexpr (NB == 1) ln1_load<K>(p, pr.r);
+        else ln_load<NB, K>(p, pr.r);
+    }
+}
+// the prologue's arithmetic on preloaded rows: act[NB][K] f32, as prologue<NB, K, PRO>
+template <int NB, int K, int PRO>
+__device__ __forceinline__ void pre_finish(const GemvP &p, PreRows<NB, K, PRO> &pr, float *act) {
+    if constexpr (PreRows<NB, K, PRO>::ON) {
+        if constexpr (NB == 1) {
+            ln1_finish<K>(p, pr.r, act);
+        } else {
+            ln_finish<NB, K>(p, pr.r, [&](int b, int k, float y) { act[b * K + k] = y; });
+            lds_sync();
         }
     }
 }
@@ -501,29 +595,9 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         ln_slots<NB, K>(p, [&](int b, int k, float y) { act[b * K + k] = y; });
         lds_sync();
     } else if constexpr (PRO == PRO_LN) {
-        // batch 1: every wave loads the whole row and runs the same DPP statistics
-        // (identical results, no barrier), then writes its quarter
-        const int lane = tid & 63, w = tid >> 6;
-        constexpr int PER = K / 64, Q = PER / MP_NWAVES;
-        float v[PER], g[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) v[i] = p.src[lane + 64 * i];
-        load_lnw<PER>(p.lnw, g);
-        float mean, var;
-        wave_meanvar<PER>(v, mean, var);
-        const float rstd = 1.0f / sqrtf(var + p.eps);
-        const bool st = p.hidden_out && blockIdx.x == 0;
-        const int s = (p.trace && blockIdx.x == 0) ? p.step[0] : 0;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            if (i / Q != w) continue;
-            const int k = lane + 64 * i;
-            const float y = ((v[i] - mean) * rstd) * g[i];
-            act[k] = y;
-            if (st) p.hidden_out[k] = y;
-            if (p.trace && blockIdx.x == 0 && s < p.trace_steps) p.trace[(size_t)s * K + k] = y;
-        }
-        lds_sync();
+        Ln1Row<K> r;
+        ln1_load<K>(p, r);
+        ln1_finish<K>(p, r, act);
     } else if constexpr (PRO == PRO_LTX_LN) {
         // one wave per slot at every batch size (wave_block_meanvar), so a batch
         // reproduces its utterances run alone bit for bit

@@ -311,6 +311,10 @@ struct GemvP {
     AttnP sa;
     XaQ8P xq8;           // EPI_RESID_XQ8: the q_net of the launch's tail
     unsigned long long *qh;
+    // split-K 16-bit GEMMs (gemm_b16_kernel KS > 1): each of a row tile's KS workgroups
+    // publishes its 16 x 16 partial tile as {tag, value} granules kgh[tile][KS][256] (tag
+    // as for xh) and merges 16 / KS of the tile's rows from the KS partials in split order
+    unsigned long long *kgh;
     const int *iter;
     int *hx_err;
     int nrow_blocks;     // set by the launcher: workgroups of the O-projection
@@ -338,7 +342,8 @@ struct LtSlotQ8P {
 };
 
 // error bits raised in *hx_err (ndone[2]) by an in-launch hand-off that gave up
-constexpr int HX_ERR_XA = 1, HX_ERR_SA = 2, HX_ERR_LT = 4;
+constexpr int HX_ERR_XA = 1, HX_ERR_SA = 2, HX_ERR_LT = 4, HX_ERR_KS = 8;
+constexpr int KGH_MAX_KS = 8;  // split-K granule buffers hold up to this many slices per tile
 
 struct FinP {
     const float *logits;

@@ -296,6 +296,7 @@ struct mp_dev {
     size_t h_codes_n = 0;
     float *sa_part = nullptr, *xa_part = nullptr;  // split-K attention states [NB][12][4][68], [NB][4][772]
     unsigned long long *sagh = nullptr, *xagh = nullptr;  // 16-slot merges: split-state granules
+    unsigned long long *kgh = nullptr;  // split-K FFN-down partial tiles (16-bit modes): [48][KS][256]
     unsigned long long *xh = nullptr;  // O-projection -> XA hand-off granules [NB][768] (EPI_RESID_XA)
     unsigned long long *qh = nullptr;  // QKV -> SA hand-off granules [NB][2304] (EPI_QKV_SA)
     unsigned long long *xqh = nullptr; // Q8_0 XA q_net -> attention hand-off granules [NB][128] (EPI_RESID_XQ8)
@@ -883,6 +884,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(h, NB * 3072); A(hidden, NB * D); A(xqb, NB * 128); A(h_b16, NB * 3072);
     A(sa_part, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xa_part, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
     A(sagh, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART); A(xagh, (size_t)NB * mp::XA_SPLITS * mp::XA_PART);
+    A(kgh, (size_t)(768 / 16) * mp::KGH_MAX_KS * 256);
     A(xh, (size_t)NB * D); A(qh, (size_t)NB * 3 * D); A(xqh, (size_t)NB * 128);
     const size_t kvn = (size_t)NB * L * dev->max_seq * D;  // elements; bf16 mode: 2 per float slot
     A(kc, dev->kv16 ? kvn / 2 : kvn); A(vc, dev->kv16 ? kvn / 2 : kvn);
@@ -1091,7 +1093,10 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         // FFN down + residual (1805, 3525): x = x2 + W2 h
         g = gemv_base(dev); g.layer = l;
         g.W = W.ff2; g.Wb = b16 ? m.pk_ff2[l] : nullptr; g.N = 768; g.src = dev->h; g.src_ld = 3072; g.out = dev->x; g.out_ld = 768; g.addsrc = dev->x2;
-        if (b16) { g.src = nullptr; g.src_b16 = dev->h_b16; }
+        if (b16) {
+            g.src = nullptr; g.src_b16 = dev->h_b16;
+            g.kgh = dev->kgh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;  // split-K partial tiles
+        }
         if ((rc = run("ff2", tb.ff2, g, F * (768.0 * 3072) + A * act * ((3072 + 2 * 768)))) != MP_OK) return rc;
     }
     mp::LtIo io{};
@@ -1810,6 +1815,7 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->ltyg, 0, (size_t)NB * 256 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->sagh, 0, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xagh, 0, (size_t)NB * mp::XA_SPLITS * mp::XA_PART * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->kgh, 0, (size_t)(768 / 16) * mp::KGH_MAX_KS * 256 * 8, dev->stream));
     // the first frame's decoder input (the BOS codes); later frames' by lt_finalize_kernel
     HIPCHK(mp::op_embed(mp::EmbP{dev->m.audio_emb, dev->codes_prev, dev->m.dec_pos, dev->pos, dev->x}, NB, dev->stream));
     // the host copies are stack/heap temporaries: finish the uploads before they go
@@ -1855,6 +1861,7 @@ static int check_handoff(mp_dev *dev) {
         if (nd[2] & mp::HX_ERR_XA) what += " O-projection -> cross-attention";
         if (nd[2] & mp::HX_ERR_SA) what += std::string(what.empty() ? "" : ",") + " QKV -> self-attention";
         if (nd[2] & mp::HX_ERR_LT) what += std::string(what.empty() ? "" : ",") + " LT FFN partial sums";
+        if (nd[2] & mp::HX_ERR_KS) what += std::string(what.empty() ? "" : ",") + " split-K partial tiles";
         return fail(dev, MP_ERR_HIP, "in-launch hand-off timed out:" + what);
     }
     return MP_OK;

@@ -75,13 +75,14 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const unsigned long long t_start = ts_begin(p.ts);
     static_assert(NB >= 1 && NB <= 16, "one 16-column MFMA tile of utterances");
     static_assert(K % (128 * KS) == 0, "K splits into KS slices of 4 waves x 32-wide chunks");
-    static_assert(KS == 1 || PRO == PRO_PLAIN || PRO == PRO_PLAIN_B16, "split-K stages plain rows only");
+    static_assert(KS == 1 || PRO == PRO_PLAIN || PRO == PRO_PLAIN_B16 || PRO == PRO_SA_MERGE,
+                  "split-K stages plain rows or the SA merge of its slice's heads");
     static_assert(16 % KS == 0, "a split workgroup merges 16 / KS rows");
     constexpr int KL = K / KS;  // this workgroup's K slice
     constexpr int KC = K / 32, KCS = KL / 32, KW = KCS / MP_NWAVES;
     constexpr int KP = KL + 8;  // padded bf16 row: rows land 16 B apart in the banks
     constexpr int NR = NB + 1;  // NB activation rows + one zero row for the unused MFMA columns
-    constexpr bool STAGE = PRO != PRO_PLAIN && PRO != PRO_PLAIN_B16 && !(PRO == PRO_LN && NB >= 2);
+    constexpr bool STAGE = PRO != PRO_PLAIN && PRO != PRO_PLAIN_B16 && !(PRO == PRO_LN && NB >= 2) && KS == 1;
     constexpr int SC = pro_scratch<NB, PRO>();
     __shared__ __attribute__((aligned(16))) float actf[STAGE ? NB * K : 4];
     __shared__ __attribute__((aligned(16))) unsigned short actb[NR * KP];
@@ -134,6 +135,56 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
             else actb[b * KP + k] = __builtin_bit_cast(unsigned short, (__bf16)y);
         });
         for (int e = tid; e < K / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
+    } else if constexpr (PRO == PRO_SA_MERGE && KS > 1) {
+        // the SA output of this slice's heads only: their SA_SPLITS key-split states merged
+        // with PRO_SA_MERGE's arithmetic (split_weights, split_merge4), rounded to 16 bits
+        static_assert(K == D && KL % DH == 0, "whole heads per slice");
+        constexpr int HS = KL / DH;
+        const int h0 = ks * HS;
+        for (int q = tid; q < NB * HS; q += MP_BLOCK) {
+            const float *pp = p.part + (size_t)((q / HS) * NH + h0 + q % HS) * SA_SPLITS * SA_PART;
+            float ms[SA_SPLITS], ls[SA_SPLITS], e[SA_SPLITS], rd;
+#pragma unroll
+            for (int s2 = 0; s2 < SA_SPLITS; ++s2) { ms[s2] = pp[s2 * SA_PART]; ls[s2] = pp[s2 * SA_PART + 1]; }
+            split_weights<SA_SPLITS>(ms, ls, e, rd);
+#pragma unroll
+            for (int s2 = 0; s2 < SA_SPLITS; ++s2) sc[q * (SA_SPLITS + 1) + s2] = e[s2];
+            sc[q * (SA_SPLITS + 1) + SA_SPLITS] = rd;
+        }
+        constexpr int ITEMS = NB * (KL / 8);
+        constexpr int PT = (ITEMS + MP_BLOCK - 1) / MP_BLOCK;
+        float4 o0[PT][SA_SPLITS], o1[PT][SA_SPLITS];
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            if (e < ITEMS) {
+                const int b = e / (KL / 8), k = ks * KL + (e % (KL / 8)) * 8;
+                const float *pp = p.part + (size_t)(b * NH + k / DH) * SA_SPLITS * SA_PART + 4 + k % DH;
+#pragma unroll
+                for (int s2 = 0; s2 < SA_SPLITS; ++s2) {
+                    o0[u][s2] = *(const float4 *)(pp + s2 * SA_PART);
+                    o1[u][s2] = *(const float4 *)(pp + s2 * SA_PART + 4);
+                }
+            }
+        }
+        lds_sync();  // the merge weights
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            if (e < ITEMS) {
+                const int b = e / (KL / 8), kk = (e % (KL / 8)) * 8, q = b * HS + (ks * KL + kk) / DH - h0;
+                const float *eq = sc + q * (SA_SPLITS + 1);
+                const float4 x0 = split_merge4<SA_SPLITS>(eq, o0[u], eq[SA_SPLITS]);
+                const float4 x1 = split_merge4<SA_SPLITS>(eq, o1[u], eq[SA_SPLITS]);
+                uint4 o;
+                o.x = pk16<F16>(x0.x, x0.y);
+                o.y = pk16<F16>(x0.z, x0.w);
+                o.z = pk16<F16>(x1.x, x1.y);
+                o.w = pk16<F16>(x1.z, x1.w);
+                *(uint4 *)(actb + b * KP + kk) = o;
+            }
+        }
+        for (int e = tid; e < KL / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     } else if constexpr (STAGE) {
         if constexpr (PreRows<NB, K, PRO>::ON) pre_finish<NB, K, PRO>(p, pre, actf);  // batch 1
         else prologue<NB, K, PRO>(p, actf, red, sc);
@@ -312,13 +363,18 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
 #define MP_FF2_KS 1
 #endif
 constexpr int FF2_KS = MP_FF2_KS;
+// split-K of the O-projection (K = 768, 48 row tiles): whole SA heads per slice
+#ifndef MP_OPROJ_KS
+#define MP_OPROJ_KS 1
+#endif
+constexpr int OPROJ_KS = MP_OPROJ_KS;
 
 #define MP_B16_OPS(NB)                                                                                                  \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \
     hipError_t b16_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV_SA>(p, s); }       \
-    hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID>(p, s); }   \
+    hipError_t b16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID, false, OPROJ_KS>(p, s); }   \
     hipError_t b16_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                      \
-        return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA>(p, s);                                                       \
+        return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA, false, OPROJ_KS>(p, s);                                   \
     }                                                                                                                   \
     hipError_t b16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_B16>(p, s); }     \
     hipError_t b16_ff1p_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_GELU_B16>(p, s); }       \
@@ -335,9 +391,9 @@ constexpr int FF2_KS = MP_FF2_KS;
 #define MP_F16_OPS(NB)                                                                                                  \
     hipError_t f16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV, true>(p, s); }             \
     hipError_t f16_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV_SA, true>(p, s); }       \
-    hipError_t f16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID, true>(p, s); }   \
+    hipError_t f16_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID, true, OPROJ_KS>(p, s); }   \
     hipError_t f16_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                      \
-        return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA, true>(p, s);                                                 \
+        return launch_b16<NB, D, PRO_SA_MERGE, EPI_RESID_XA, true, OPROJ_KS>(p, s);                                   \
     }                                                                                                                   \
     hipError_t f16_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_XA_LN, EPI_GELU_F16, true>(p, s); }     \
     hipError_t f16_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, DFF, PRO_PLAIN_B16, EPI_ADD_STORE, true, FF2_KS>(p, s); }  \
@@ -360,8 +416,12 @@ MP_F16_OPS(8)
 MP_F16_OPS(16)
 // bf16 mode at 8 and 16 slots: the O-projection + XA launch reads the SA output its
 // split workgroups merged (plain rows), and its XA workgroups merge x2
-hipError_t b16_oproj_xa_pm_16(const GemvP &p, hipStream_t s) { return launch_b16<16, D, PRO_PLAIN, EPI_RESID_XA>(p, s); }
-hipError_t b16_oproj_xa_pm_8(const GemvP &p, hipStream_t s) { return launch_b16<8, D, PRO_PLAIN, EPI_RESID_XA>(p, s); }
+hipError_t b16_oproj_xa_pm_16(const GemvP &p, hipStream_t s) {
+    return launch_b16<16, D, PRO_PLAIN, EPI_RESID_XA, false, OPROJ_KS>(p, s);
+}
+hipError_t b16_oproj_xa_pm_8(const GemvP &p, hipStream_t s) {
+    return launch_b16<8, D, PRO_PLAIN, EPI_RESID_XA, false, OPROJ_KS>(p, s);
+}
 // the LT in_proj of an F16 file is F16 too (the bf16 mode keeps it f32)
 hipError_t f16_lt_in0_1(const GemvP &p, hipStream_t s) { return launch_b16<1, D, PRO_LN, EPI_BIAS, true>(p, s); }
 hipError_t f16_lt_in0_2(const GemvP &p, hipStream_t s) { return launch_b16<2, D, PRO_LN, EPI_BIAS, true>(p, s); }

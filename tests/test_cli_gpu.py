@@ -80,3 +80,27 @@ def test_cli_stream_matches_sentence_streams(ma, small_model, codec_model, tmp_p
     dev.close()
     cdc.close()
     assert np.array_equal(wav, _pcm(np.concatenate(parts)))
+
+
+def test_model_load_encode_text_codec_load(ma, oracle, small_model, codec_model, tmp_path):
+    """magpie_model_load, magpie_encode_text and magpie_codec_load (src/magpie.h:332,
+    555-558, 753) through bin/magpie-api-probe: the model loads, the encoder output that
+    magpie_encode_text leaves in ctx->state equals the oracle's encoder within 1e-4, and
+    the codec loads and decodes."""
+    import json
+    exe = os.path.join(os.path.dirname(ma.LIB_PATH), "..", "bin", "magpie-api-probe")
+    out = tmp_path / "enc.bin"
+    r = subprocess.run([exe, small_model, codec_model, str(out), "Hello, world!"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["model_load"] and info["encode_text"] and info["codec_load"], info
+    assert info["dec_layers"] == 2 and info["enc_seq_len"] == info["n_tokens"] > 2, info
+    assert info["codec_samples"] == 4 * 1024
+    enc = np.fromfile(out, np.float32).reshape(info["n_tokens"], 768)
+    om = oracle.Model(small_model)
+    ref = om.encode(np.asarray(info["tokens"], np.int32))
+    om.close()
+    err = float(np.abs(enc - ref).max())
+    print(f"encoder output (T = {info['n_tokens']}): max abs err {err:.3g}")
+    assert err < 1e-4, err

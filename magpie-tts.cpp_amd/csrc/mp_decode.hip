@@ -323,16 +323,25 @@ static hipError_t launch_gemv(const GemvP &p, hipStream_t s) {
 
 // Named entry points (one per fused op of the decode iteration), instantiated
 // for NB in {1, 2, 4, 8}.
+// rows per wave of the QKV and FFN-up GEMVs (2: 288 / 384 workgroups at 2304 / 3072 rows);
+// any value computes the same bits (each wave's rows are independent)
+#ifndef MP_RW_QKV
+#define MP_RW_QKV 2
+#endif
+#ifndef MP_RW_FF1
+#define MP_RW_FF1 2
+#endif
+constexpr int RW_QKV = MP_RW_QKV, RW_FF1 = MP_RW_FF1;
 #define MP_DECODE_OPS(NB)                                                                                        \
-    hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV>(p, s); }             \
-    hipError_t op_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_QKV_SA>(p, s); }       \
+    hipError_t op_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, RW_QKV, D, PRO_LN, EPI_QKV>(p, s); }        \
+    hipError_t op_qkv_sa_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, RW_QKV, D, PRO_LN, EPI_QKV_SA>(p, s); }  \
     hipError_t op_xq_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_STORE>(p, s); }            \
     hipError_t op_oproj_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_SA_MERGE, EPI_RESID>(p, s); } \
     hipError_t op_oproj_xa_##NB(const GemvP &p, hipStream_t s) {                                                   \
         return launch_gemv<NB, 1, D, PRO_SA_MERGE, EPI_RESID_XA>(p, s);                                            \
     }                                                                                                              \
-    hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_LN, EPI_GELU>(p, s); }            \
-    hipError_t op_ff1x_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 2, D, PRO_XA_LN, EPI_GELU>(p, s); }        \
+    hipError_t op_ff1_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, RW_FF1, D, PRO_LN, EPI_GELU>(p, s); }       \
+    hipError_t op_ff1x_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, RW_FF1, D, PRO_XA_LN, EPI_GELU>(p, s); }   \
     hipError_t op_ff2_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }  \
     hipError_t op_lt_in0_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, D, PRO_LN, EPI_BIAS>(p, s); }         \
     hipError_t op_lt_a_##NB(const GemvP &p, hipStream_t s) { return launch_gemv<NB, 1, LTD, PRO_LTX_LN, EPI_LTQKV>(p, s); }    \
@@ -789,18 +798,16 @@ hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
 // (in_proj output -> LN(X_0); vo_0 -> y) are 256-value granule sweeps (2 KiB) by the
 // 64 workgroups of the launch, all co-resident.
 // The front's work after its weight loads: LN(x) -> in_proj row n_in (published) ->
-// X_0, LN(X_0) -> k_0 / vo_0 row n_in (published; PUBK: k_0 too, for lt_chain_kernel's
-// later positions) -> y = X_0 + vo_0 (wave 0; *y4 and the lane's vo_0 elements *v4)
-// -> LN(y) -> this workgroup's 16 FFN units -> returns this thread's FFN-down partial
-// sum (output tid) of codebook 0.
+// X_0, LN(X_0) -> k_0 / vo_0 row n_in (vo_0 published) -> y = X_0 + vo_0 (wave 0; *y4
+// and the lane's vo_0 elements *v4 when non-null) -> LN(y) -> this workgroup's 16 FFN
+// units -> returns this thread's FFN-down partial sum (output tid) of codebook 0.
 constexpr int LTF_U = LTF / LT_FFN_P, LTF_UPW = LTF_U / MP_NWAVES;
-template <bool PUBK>
 __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_in, const float4 (&wi)[3], float4 wk,
                                                float4 wv, const float4 (&a1)[LTF_UPW], const float4 (&a2)[LTF_U / 4],
                                                float *act, float *act2, float *xs, float *fs, float4 *y4, float4 *v4) {
     constexpr int U = LTF_U, UPW = LTF_UPW, PER = D / 64, Q = PER / MP_NWAVES;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const unsigned tag_s = (unsigned)p.iter[0] * 64u + 40u, tag_v = tag_s + 1u, tag_k = tag_s + 2u;
+    const unsigned tag_s = (unsigned)p.iter[0] * 64u + 40u, tag_v = tag_s + 1u;
     // ---- LN(x) (PRO_LN, batch 1: every wave the whole row, writes its quarter)
     {
         float v[PER], g[PER];
@@ -854,7 +861,7 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
         for (int i = 0; i < 4; ++i) act2[lane + 64 * i] = ((X[i] - mean) * rstd) * g[i];
     }
     lds_sync();
-    // ---- k_0 row and vo_0 row n_in (EPI_LTKVO); vo_0 published (PUBK: k_0 too)
+    // ---- k_0 row and vo_0 row n_in (EPI_LTKVO); vo_0 published
     {
         const float4 av = *(const float4 *)&act2[4 * lane];
         float sk = 0.f, sv = 0.f;  // gemv_kernel's accumulation, term for term
@@ -866,9 +873,6 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
             p.l.ltv[n_in] = vo0;
             __hip_atomic_store((gu64 *)p.gh + LTD + n_in, ((unsigned long long)tag_v << 32) | __float_as_uint(vo0),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (PUBK)
-                __hip_atomic_store((gu64 *)p.gh + 2 * LTD + n_in, ((unsigned long long)tag_k << 32) | __float_as_uint(k0),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // ---- codebook 0's FFN step (lt_ffn2_kernel<1>: y = X_0 + vo_0, wave 0)
@@ -938,7 +942,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     const int n_in = pb * MP_NWAVES + w + ts_dep(t_start);  // this wave's in_proj / k / vo row
     float4 wi[3], wk, wv, a1[LTF_UPW], a2[LTF_U / 4];
     lt_front_weights(p, pb, n_in, wi, wk, wv, a1, a2);
-    const float acc = lt_front_core<false>(p, pb, n_in, wi, wk, wv, a1, a2, act, act2, xs, fs, nullptr, nullptr);
+    const float acc = lt_front_core(p, pb, n_in, wi, wk, wv, a1, a2, act, act2, xs, fs, nullptr, nullptr);
     p.l.f.part[(size_t)pb * LTD + tid] = acc;
     ts_end(p.l.f.ts, t_start);
 }
@@ -949,302 +953,6 @@ hipError_t op_lt_front(const LtFrontP &p, hipStream_t s) {
         !p.l.ltk || !p.l.ltv || !p.l.step || p.l.cb != 0)
         return hipErrorInvalidValue;
     mp::launch(lt_front_kernel, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------- LT chain, f32 batch 1
-// LtChainP (mp_params.hpp): heads 0..7 and the FFN steps of codebooks 1..7 in one
-// launch of LT_FFN_P workgroups (all co-resident: every hand-off is a granule sweep
-// across the grid). Per codebook three hand-offs (partial sums -> y2 slice, y2 -> every
-// workgroup, per-wave best -> every workgroup) and one table gather replace the two
-// launches of lt_ffn2_kernel + the head.
-constexpr int LTC_HR = 8;  // head rows per wave: 8 x 4 waves x 64 workgroups >= 2024
-__device__ __forceinline__ unsigned long long ltc_wait64(const unsigned long long *g, unsigned tag, int *err, bool &ok) {
-    for (unsigned spins = 0;; ++spins) {
-        const unsigned long long u = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((unsigned)(u >> 32) == tag) return u;
-        if (spins >= HX_SPIN_LIMIT) {
-            __hip_atomic_fetch_or((gi32 *)err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = false;
-            return 0x7fc00000ull;  // NaN value
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-template <bool FRONT>
-__global__ __launch_bounds__(MP_BLOCK) void lt_chain_kernel(LtChainP p) {
-    const unsigned long long t_start = ts_begin(p.fr.l.f.ts);
-    constexpr int U = LTF / LT_FFN_P, UPW = U / MP_NWAVES;
-    static_assert(U % MP_NWAVES == 0 && LTD == MP_BLOCK && LT_FFN_P * MP_NWAVES * LTC_HR >= VCB, "split");
-    __shared__ __attribute__((aligned(16))) float y2s[LTD];
-    __shared__ __attribute__((aligned(16))) float ys[LTD];
-    __shared__ __attribute__((aligned(16))) float xs[LTD];
-    __shared__ __attribute__((aligned(16))) float fs[U];
-    __shared__ __attribute__((aligned(16))) float kk[NCB][LTD], vv[NCB][LTD];  // positions' k / vo rows
-    __shared__ __attribute__((aligned(16))) float wsc[2 * VCB];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, pb = blockIdx.x;
-    const int gw = pb * MP_NWAVES + w, r0 = gw * LTC_HR + ts_dep(t_start);  // this wave's head rows
-    const LtFfn2P &l = p.fr.l;
-    const unsigned tag0 = (unsigned)p.iter[0] * 64u + 48u;
-    // the FFN slice (the same every codebook) and codebook 0's head rows
-    const int j0 = pb * U;
-    float4 a1[UPW], a2[U / 4], hw[LTC_HR];
-    if constexpr (FRONT) {
-        // lt_front_kernel's work first (its weights, then codebook 0's head rows)
-        const int n_in = pb * MP_NWAVES + w;
-        float4 wi[3], wk, wv;
-        lt_front_weights(p.fr, pb, n_in, wi, wk, wv, a1, a2);
-#pragma unroll
-        for (int i = 0; i < LTC_HR; ++i) {
-            const int r = min(r0 + i, VCB - 1);
-            hw[i] = *(const float4 *)(p.w_out + (size_t)r * LTD + 4 * lane);
-        }
-        float4 y4, v4;
-        const float acc = lt_front_core<true>(p.fr, pb, n_in, wi, wk, wv, a1, a2, wsc, wsc + D, xs, fs, &y4, &v4);
-        // codebook 0's partial sums published like every later step's; y and vo_0 into LDS
-        __hip_atomic_store((gu64 *)p.gpart + pb * LTD + tid, ((unsigned long long)tag0 << 32) | __float_as_uint(acc),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w == 0) {
-            *(float4 *)&ys[4 * lane] = y4;
-            *(float4 *)&vv[0][4 * lane] = v4;
-            const unsigned tag_k = (unsigned)p.iter[0] * 64u + 42u;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) kk[0][4 * lane + c] = gh_wait(p.fr.gh + 2 * LTD + 4 * lane + c, tag_k, p.hx_err);
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(l.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
-#pragma unroll
-        for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(l.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i);
-#pragma unroll
-        for (int i = 0; i < LTC_HR; ++i) {
-            const int r = min(r0 + i, VCB - 1);
-            hw[i] = *(const float4 *)(p.w_out + (size_t)r * LTD + 4 * lane);
-        }
-        // position 0's k / vo (lt_front), this launch's starting y (codebook 0's step)
-        if (w == 0) {
-            *(float4 *)&kk[0][4 * lane] = *(const float4 *)(l.ltk + 4 * lane);
-            *(float4 *)&vv[0][4 * lane] = *(const float4 *)(l.ltv + 4 * lane);
-        }
-        ys[tid] = l.f.y[tid];
-    }
-    lds_sync();  // ys is read by the y2 slice's threads
-    const int stp = l.step[0];
-    const bool forbid = l.ignore_eos || stp < 4;
-    bool ok = true;
-    for (int c = 0;; ++c) {
-        const unsigned tag = tag0 + (unsigned)c;
-        // ---- y2 slice: outputs [4 pb, 4 pb + 4) = (sum over q of part[q][k], q ascending) + y[k]
-        if (tid < 4) {
-            const int k = 4 * pb + tid;
-            float s;
-            if (c == 0 && !FRONT) {
-                s = l.f.part[k];
-#pragma unroll 8
-                for (int q = 1; q < LT_FFN_P; ++q) s += l.f.part[(size_t)q * LTD + k];
-            } else {
-                float pv[LT_FFN_P];
-                for (unsigned spins = 0;; ++spins) {
-                    bool all = true;
-#pragma unroll
-                    for (int q = 0; q < LT_FFN_P; ++q) {
-                        const unsigned long long u =
-                            __hip_atomic_load((const gu64 *)p.gpart + q * LTD + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        all &= (unsigned)(u >> 32) == tag;
-                        pv[q] = __uint_as_float((unsigned)u);
-                    }
-                    if (all) break;
-                    if (spins >= HX_SPIN_LIMIT) {
-                        __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        pv[0] = __builtin_nanf("");
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                s = pv[0];
-#pragma unroll
-                for (int q = 1; q < LT_FFN_P; ++q) s += pv[q];
-            }
-            const float v = s + ys[k];
-            l.f.out[k] = v;  // lty2 (diagnostics)
-            __hip_atomic_store((gu64 *)p.gy2 + k, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // ---- y2 to every workgroup
-        y2s[tid] = __uint_as_float((unsigned)ltc_wait64(p.gy2 + tid, tag, p.hx_err, ok));
-        lds_sync();
-        // ---- head rows of codebook c (gemv_kernel<1, 2, 256, ..., EPI_BIAS> arithmetic)
-        float bv = -INFINITY;
-        int bi = VCB;
-        {
-            const float4 av = *(const float4 *)&y2s[4 * lane];
-            const float *bias = p.b_out + (size_t)c * VCB;
-#pragma unroll
-            for (int i = 0; i < LTC_HR; ++i) {
-                const int r = r0 + i;
-                float s = 0.f;
-                s += dotv(hw[i], av);
-                const float v = wave_sum(s) + bias[min(r, VCB - 1)];
-                if (r < VCB) {
-                    if (lane == i) {
-                        const_cast<float *>(l.logits)[r] = v;
-                        if (l.smp.on)
-                            __hip_atomic_store((gu64 *)p.glog + r, ((unsigned long long)tag << 32) | __float_as_uint(v),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    const bool masked = r >= l.audio_bos && r <= l.audio_bos + 7 && (r != l.audio_eos || forbid);
-                    const float vm = masked ? -INFINITY : v;
-                    if (vm > bv) { bv = vm; bi = r; }
-                }
-            }
-        }
-        if (c + 1 < NCB) {  // the next codebook's head rows, in flight during the pick and the step
-#pragma unroll
-            for (int i = 0; i < LTC_HR; ++i) {
-                const int r = min(r0 + i, VCB - 1);
-                hw[i] = *(const float4 *)(p.w_out + ((size_t)(c + 1) * VCB + r) * LTD + 4 * lane);
-            }
-        }
-        if (!l.smp.on && lane == 0)
-            __hip_atomic_store((gu64 *)p.gbest + gw, ((unsigned long long)(((tag & 0x1FFFFFu) << 11) | (unsigned)bi) << 32) |
-                                                          __float_as_uint(bv),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c + 1 >= NCB) break;  // codebook 7 is the finalize's (lt_finalize_kernel)
-        // ---- codebook c's code (wave 0), then codebook c+1's step
-        if (w == 0) {
-            int code, amax;
-            if (!l.smp.on) {
-                // masked first-max argmax over the 256 wave results: max value, then the
-                // smallest index holding it (= wave_pick_v's greedy result)
-                float v4[4];
-                int i4[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const gu64 *g = (const gu64 *)p.gbest + lane + 64 * j;
-                    for (unsigned spins = 0;; ++spins) {
-                        const unsigned long long u = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((unsigned)(u >> 43) == (tag & 0x1FFFFFu)) {
-                            v4[j] = __uint_as_float((unsigned)u);
-                            i4[j] = (int)((u >> 32) & 0x7FFu);
-                            break;
-                        }
-                        if (spins >= HX_SPIN_LIMIT) {
-                            __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            v4[j] = -INFINITY;
-                            i4[j] = VCB;
-                            ok = false;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                float m = fmaxf(fmaxf(v4[0], v4[1]), fmaxf(v4[2], v4[3]));
-                m = wave_max(m);
-                int bidx = VCB;
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (v4[j] == m) bidx = min(bidx, i4[j]);
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) bidx = min(bidx, __shfl_xor(bidx, o, 64));
-                if (bidx < 0 || bidx >= VCB) bidx = 0;
-                code = amax = bidx;
-            } else {
-                float lv[PICK_R];
-#pragma unroll
-                for (int r = 0; r < PICK_R; ++r) {
-                    const int i = lane + 64 * r;
-                    lv[r] = i < VCB ? __uint_as_float((unsigned)ltc_wait64(p.glog + i, tag, p.hx_err, ok)) : -INFINITY;
-                }
-                code = wave_pick_v(lv, forbid, l.audio_bos, l.audio_eos, l.smp, 0, stp, c, wsc, amax);
-            }
-            // codebook c+1's LT residual y (lt_y_slot's arithmetic; earlier positions from LDS)
-            const int cb = c + 1;
-            const size_t r = (size_t)c * VCB + code;
-            const float *qkv = l.qkvtab + r * (3 * LTD) + 4 * lane;
-            const float4 q4 = *(const float4 *)qkv, k4 = *(const float4 *)(qkv + LTD);
-            const float4 vo4 = *(const float4 *)(l.votab + r * LTD + 4 * lane);
-            const float4 x4 = *(const float4 *)(l.ptab + r * LTD + 4 * lane);
-            const float4 pos4 = *(const float4 *)(l.lt_pos + (size_t)cb * LTD + 4 * lane);
-            if (pb == 0) {
-                if (lane == 0) {
-                    l.codes_cur[c] = code;
-                    if (amax == l.audio_eos) l.smp.argeos[0] = 1;
-                    if (l.smp.amax) l.smp.amax[c] = amax;
-                }
-                *(float4 *)(l.ltk + cb * LTD + 4 * lane) = k4;
-                *(float4 *)(l.ltv + cb * LTD + 4 * lane) = vo4;
-            }
-            *(float4 *)&kk[cb][4 * lane] = k4;
-            *(float4 *)&vv[cb][4 * lane] = vo4;
-            float sj[NCB];
-#pragma unroll
-            for (int j = 0; j < NCB; ++j)
-                sj[j] = j < cb ? wave_sum(dotv(q4, *(const float4 *)&kk[j][4 * lane])) * (1.0f / 16.0f)
-                               : j == cb ? wave_sum(dotv(q4, k4)) * (1.0f / 16.0f) : -INFINITY;
-            float m = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < NCB; ++j) m = fmaxf(m, sj[j]);
-            float lsum = 0.f;
-            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int j = 0; j < NCB; ++j) {
-                if (j > cb) break;
-                const float e = expf(sj[j] - m);
-                lsum += e;
-                const float4 v4 = j == cb ? vo4 : *(const float4 *)&vv[j][4 * lane];
-                a.x = fmaf(e, v4.x, a.x); a.y = fmaf(e, v4.y, a.y); a.z = fmaf(e, v4.z, a.z); a.w = fmaf(e, v4.w, a.w);
-            }
-            const float4 y = make_float4(x4.x + pos4.x + a.x / lsum, x4.y + pos4.y + a.y / lsum,
-                                         x4.z + pos4.z + a.z / lsum, x4.w + pos4.w + a.w / lsum);
-            if (pb == 0) *(float4 *)((float *)l.f.y + 4 * lane) = y;
-            *(float4 *)&ys[4 * lane] = y;
-            // LN(y) (lt_step_body's one-wave statistics)
-            const float x[4] = {y.x, y.y, y.z, y.w};
-            float mean, var;
-            wave_meanvar<4>(x, mean, var);
-            const float rstd = 1.0f / sqrtf(var + l.f.eps);
-            const float4 g = *(const float4 *)(l.f.lnw + 4 * lane);
-            *(float4 *)&xs[4 * lane] = make_float4(((x[0] - mean) * rstd) * g.x, ((x[1] - mean) * rstd) * g.y,
-                                                   ((x[2] - mean) * rstd) * g.z, ((x[3] - mean) * rstd) * g.w);
-        }
-        lds_sync();
-        // ---- FFN up (this workgroup's 16 units), GELU, FFN down partial sums, published
-        {
-            const float4 xv = *(const float4 *)&xs[4 * lane];
-#pragma unroll
-            for (int r = 0; r < UPW; ++r) {
-                const float v = wave_sum(dotv(a1[r], xv));
-                if (lane == 0) fs[w * UPW + r] = gelu_tanh(v);
-            }
-        }
-        lds_sync();
-        float acc = 0.f;
-#pragma unroll
-        for (int i = 0; i < U / 4; ++i) {
-            const float4 f4 = *(const float4 *)&fs[4 * i];
-            acc = fmaf(a2[i].x, f4.x, acc);
-            acc = fmaf(a2[i].y, f4.y, acc);
-            acc = fmaf(a2[i].z, f4.z, acc);
-            acc = fmaf(a2[i].w, f4.w, acc);
-        }
-        __hip_atomic_store((gu64 *)p.gpart + pb * LTD + tid, ((unsigned long long)(tag + 1u) << 32) | __float_as_uint(acc),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    (void)ok;
-    ts_end(p.fr.l.f.ts, t_start);
-}
-hipError_t op_lt_chain(const LtChainP &p, hipStream_t s) {
-    static_assert(sizeof(LtChainP) < 4096, "kernel argument size");
-    const LtFfn2P &l = p.fr.l;
-    if (p.front && (!p.fr.x || !p.fr.norm_out || !p.fr.w_in || !p.fr.b_in || !p.fr.lt_s || !p.fr.lt_pos ||
-                    !p.fr.norm_self || !p.fr.w_kvo || !p.fr.gh || !p.fr.iter || !p.fr.hx_err || !l.ltX))
-        return hipErrorInvalidValue;
-    if (!p.w_out || !p.b_out || !p.gpart || !p.gy2 || !p.gbest || !p.glog || !p.iter || !p.hx_err || !l.f.y ||
-        !l.f.lnw || !l.f.w1 || !l.f.w2 || !l.f.part || !l.f.out || !l.ltk || !l.ltv || !l.qkvtab || !l.votab || !l.ptab ||
-        !l.lt_pos || !l.logits || !l.codes_cur || !l.step || !l.smp.cfg || !l.smp.argeos)
-        return hipErrorInvalidValue;
-    if (p.front) mp::launch(lt_chain_kernel<true>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p);
-    else mp::launch(lt_chain_kernel<false>, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 

@@ -358,12 +358,16 @@ static hipError_t launch_b16(const GemvP &p, hipStream_t s) {
     mp::launch((gemm_b16_kernel<NB, K, PRO, EPI, F16, KS>), dim3(grid), dim3(MP_BLOCK), 0, s, q);
     return hipGetLastError();
 }
-// split-K of the FFN-down projection (K = 3072, 48 row tiles): a function of the op only
+// split-K of the FFN-down projection (K = 3072, 48 row tiles): a function of the op only.
+// 4 slices = 192 workgroups of 24 KiB weights + the slice's activations each: bf16 B=16
+// ff2 5.21 -> 4.37 us, 28.5k -> 29.3k frames/s, B=8 17.4k -> 17.6k, B=1 within 1 %
+// (gpurun_out/r04h_ab.txt, r04h_ops16_ks.txt)
 #ifndef MP_FF2_KS
-#define MP_FF2_KS 1
+#define MP_FF2_KS 4
 #endif
 constexpr int FF2_KS = MP_FF2_KS;
-// split-K of the O-projection (K = 768, 48 row tiles): whole SA heads per slice
+// split-K of the O-projection (K = 768, 48 row tiles): whole SA heads per slice. Measured
+// and left off: 2 slices moved bf16 B=16 by +0.5 % and B=8 / B=1 by -1.5 .. -3 %
 #ifndef MP_OPROJ_KS
 #define MP_OPROJ_KS 1
 #endif

@@ -341,30 +341,6 @@ struct LtSlotQ8P {
     unsigned long long *ts;
 };
 
-// f32 mode at batch 1: the local transformer's 8 heads and the FFN steps of codebooks
-// 1..7 as ONE launch of LT_FFN_P workgroups (lt_chain_kernel) after lt_front: per
-// codebook c, workgroup p merges outputs [4p, 4p + 4) of the FFN-down partial sums
-// (granules gpart[p'][256]) and publishes y2; every workgroup sweeps the 256 y2
-// granules, computes head rows [8 (4p + w), +8) per wave and publishes the wave's
-// masked first-max (value, index) (greedy) or its logits (sampling); every workgroup
-// reduces those into codebook c's code and runs codebook c+1's step (gathers,
-// attention over the positions it keeps in LDS, LN, its 16 FFN units) and publishes
-// its partial sums. Tags iter * 64 + 48 + c. Same arithmetic as lt_ffn2_kernel /
-// lt_em (PRO_LTFFN_MERGE) / wave_pick_v, so a batch-1 run still equals the batched path.
-struct LtChainP {
-    LtFrontP fr;                    // fr.l: tables, FFN weights, ltX / ltk / ltv, logits, codes, sampling;
-                                    // the rest: lt_front's inputs when the launch runs it too (front)
-    int front;                      // 1: lt_front_kernel's work first (granules fr.gh [3][256])
-    const float *w_out, *b_out;     // heads [8][2024][256], [8][2024]
-    unsigned long long *gpart;      // [LT_FFN_P][256] FFN-down partial sums
-    unsigned long long *gy2;        // [256] y2
-    unsigned long long *gbest;      // [LT_FFN_P * 4] per-wave (index | tag, value) of the greedy pick
-    unsigned long long *glog;       // [2048] logits (sampling)
-    const int *iter;
-    int *hx_err;
-};
-constexpr int LTC_GRANULES = LT_FFN_P * 256 + 256 + LT_FFN_P * 4 + 2048;
-
 // error bits raised in *hx_err (ndone[2]) by an in-launch hand-off that gave up
 constexpr int HX_ERR_XA = 1, HX_ERR_SA = 2, HX_ERR_LT = 4, HX_ERR_KS = 8;
 constexpr int KGH_MAX_KS = 8;  // split-K granule buffers hold up to this many slices per tile

@@ -111,7 +111,6 @@ hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_ffn2(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_slot(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_front(const LtFrontP &, hipStream_t);
-hipError_t op_lt_chain(const LtChainP &, hipStream_t);
 hipError_t op_lt_slot_q8(const LtSlotQ8P &, int, hipStream_t);
 hipError_t op_lt_kvo(const GemvP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
@@ -234,7 +233,7 @@ struct Model {
 };
 
 enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9,
-              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12, K_LTFRONT = 13, K_LTSLOTQ8 = 14, K_LTCHAIN = 15 };
+              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12, K_LTFRONT = 13, K_LTSLOTQ8 = 14 };
 struct OpRec {
     std::string name;
     int kind;
@@ -248,7 +247,6 @@ struct OpRec {
     LtFfn2P l2;
     LtFrontP lf3;
     LtSlotQ8P lq8;
-    LtChainP lc;
     EmbP e;
     int B;
     double bytes;
@@ -263,7 +261,6 @@ struct LtIo {
     float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel; lt_slot_kernel: [NB][LTS_P][256])
     unsigned long long *ltgh;  // [NB][LTS_P or LTQ_P][256] lt_slot(_q8)_kernel's partial-sum granules
     unsigned long long *ltfg;  // [2][256] lt_front_kernel's hand-off granules (f32, batch 1)
-    unsigned long long *ltcg;  // lt_chain_kernel's granules (f32, batch 1)
     unsigned long long *ltyg;  // [NB][256] lt_slot_q8_kernel's y granules (Q8_0 mode)
     int *iter, *hx_err;        // decode iteration counter (hand-off tags), hand-off error bits
     int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
@@ -307,7 +304,6 @@ struct mp_dev {
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
     unsigned long long *ltgh = nullptr, *ltfg = nullptr, *ltyg = nullptr;
-    unsigned long long *ltcg = nullptr;  // lt_chain_kernel's granules (f32, batch 1): LTC_GRANULES
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
         *argeos = nullptr, *amax = nullptr;
@@ -895,8 +891,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
-    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, 3 * 256); A(ltyg, (size_t)NB * 256);
-    A(ltcg, (size_t)mp::LTC_GRANULES);
+    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, 2 * 256); A(ltyg, (size_t)NB * 256);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -1110,7 +1105,7 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     io.x = dev->x; io.hidden = dev->hidden; io.trace = dev->trace; io.trace_steps = dev->max_steps + 1;
     io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
     io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits; io.ltp = dev->ltp;
-    io.ltgh = dev->ltgh; io.ltfg = dev->ltfg; io.ltyg = dev->ltyg; io.ltcg = dev->ltcg; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
+    io.ltgh = dev->ltgh; io.ltfg = dev->ltfg; io.ltyg = dev->ltyg; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
     io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
     io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
     io.amax = dev->amax; io.cfg = dev->smpcfg;
@@ -1274,12 +1269,6 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             HIPCHK(mp::op_lt_kvo(g, NB, s));
             dump_lt(io, s);
         }
-        // batch 1: the rest of the LT as one launch after lt_front (MAGPIE_LT_CHAIN=1; unset
-        // or 0: the per-codebook launches, the same bits)
-        const char *lce = getenv("MAGPIE_LT_CHAIN");
-        const bool chain = front && io.ltcg && lce && atoi(lce) != 0;
-        // MAGPIE_LT_CHAIN=2: lt_front's work inside the same launch too
-        const bool chain_front = chain && lce && atoi(lce) == 2;
         for (int cb = 0; cb < 8; ++cb) {
             mp::LtFfn2P l2{};
             l2.f = mp::LtFfnP{io.ltY, m.lt_norm_ff, m.lt_ff1, m.lt_ff2s, m.eps, io.ltp, io.lty2};
@@ -1294,39 +1283,15 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                 fp.lt_s = io.lt_s; fp.hidden_out = io.hidden; fp.lt_pos = m.lt_pos; fp.norm_self = m.lt_norm_self;
                 fp.w_kvo = m.lt_kvo; fp.gh = io.ltfg; fp.iter = io.iter; fp.hx_err = io.hx_err;
                 if (io.trace) { fp.trace = io.trace; fp.trace_steps = io.trace_steps; }
-                if (ops && !chain_front) {
+                if (ops) {
                     mp::OpRec r{};
                     r.name = "lt_front"; r.kind = mp::K_LTFRONT; r.lf3 = fp; r.B = NB;
                     r.bytes = A * (256.0 * 768 + 512.0 * 256 + 1024.0 * 256 * 2) + A * (768 * 2 + 256 * 4) +
                               A * (mp::LT_FFN_P * 256);
                     ops->push_back(r);
                 }
-                if (!chain_front) {
-                    HIPCHK(mp::op_lt_front(fp, s));
-                    dump_lt(io, s);
-                }
-                if (chain) {
-                    // heads 0..7 and the steps of codebooks 1..7: one launch (lt_chain_kernel),
-                    // with lt_front's work first when chain_front
-                    mp::LtChainP cp{};
-                    cp.fr = fp;
-                    cp.front = chain_front;
-                    cp.w_out = m.lt_out_w; cp.b_out = m.lt_out_b;
-                    cp.gpart = io.ltcg; cp.gy2 = cp.gpart + mp::LT_FFN_P * 256; cp.gbest = cp.gy2 + 256;
-                    cp.glog = cp.gbest + mp::LT_FFN_P * 4;
-                    cp.iter = io.iter; cp.hx_err = io.hx_err;
-                    if (ops) {
-                        mp::OpRec r{};
-                        r.name = chain_front ? "lt_chain_f" : "lt_chain"; r.kind = mp::K_LTCHAIN; r.lc = cp; r.B = NB;
-                        r.bytes = A * (8.0 * 2024 * 256 + 8 * 2024 + 1024.0 * 256 * 2) +
-                                  (chain_front ? A * (256.0 * 768 + 512.0 * 256) : 0.0) +
-                                  A * 7.0 * (2 * 3 * 256 + 2 * 256) + 8.0 * 8 * (64 * 256 + 256 + 256);
-                        ops->push_back(r);
-                    }
-                    HIPCHK(mp::op_lt_chain(cp, s));
-                    dump_lt(io, s);
-                    break;
-                }
+                HIPCHK(mp::op_lt_front(fp, s));
+                dump_lt(io, s);
             } else {
                 if (ops) {
                     mp::OpRec r{};
@@ -1848,8 +1813,7 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xqh, 0, (size_t)NB * 128 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->ltgh, 0, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256 * 8, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->ltfg, 0, 3 * 256 * 8, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->ltcg, 0, (size_t)mp::LTC_GRANULES * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->ltfg, 0, 2 * 256 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->ltyg, 0, (size_t)NB * 256 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->sagh, 0, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xagh, 0, (size_t)NB * mp::XA_SPLITS * mp::XA_PART * 8, dev->stream));
@@ -2213,7 +2177,6 @@ static hipError_t launch_rec(const mp::OpRec &r, hipStream_t s) {
     case mp::K_LTFFN2: return mp::op_lt_ffn2(r.l2, r.B, s);
     case mp::K_LTSLOT: return mp::op_lt_slot(r.l2, r.B, s);
     case mp::K_LTFRONT: return mp::op_lt_front(r.lf3, s);
-    case mp::K_LTCHAIN: return mp::op_lt_chain(r.lc, s);
     case mp::K_LTSLOTQ8: return mp::op_lt_slot_q8(r.lq8, r.B, s);
     case mp::K_LTKVO: return mp::op_lt_kvo(r.g, r.B, s);
     case mp::K_EMBED: return mp::op_embed(r.e, r.B, s);
@@ -2280,7 +2243,6 @@ int mp_hip_profile_ops_ts(mp_dev *dev, int iters, float *avg_us) {
             mp::OpRec r = dev->ops[i];
             unsigned long long *t = ts + (size_t)i * per;
             r.g.ts = t; r.a.ts = t; r.x.ts = t; r.f.ts = t; r.lf.ts = t; r.l2.f.ts = t; r.lf3.l.f.ts = t; r.lq8.ts = t;
-            r.lc.fr.l.f.ts = t;
             const hipError_t e = launch_rec(r, dev->stream);
             if (e != hipSuccess) { rc = fail(dev, MP_ERR_HIP, std::string("profile launch: ") + hipGetErrorString(e)); break; }
         }
@@ -2359,8 +2321,7 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     // iteration counter: relaunched with the same tag, its consumers would find the previous
     // launch's granules and not wait for their producers (a different, shorter critical path)
     const bool handoff = (r.kind == mp::K_GEMV && r.g.iter) || (r.kind == mp::K_LTSLOT && r.l2.gh) ||
-                         r.kind == mp::K_LTFRONT || r.kind == mp::K_LTSLOTQ8 || r.kind == mp::K_LTCHAIN ||
-                         (r.kind == mp::K_ATTN && r.a.gh);
+                         r.kind == mp::K_LTFRONT || r.kind == mp::K_LTSLOTQ8 || (r.kind == mp::K_ATTN && r.a.gh);
     if (handoff)
         return fail(dev, MP_ERR_ARG, "op carries an in-launch hand-off: back-to-back timing would not wait for it");
     HIPCHK(launch());  // warm

@@ -609,9 +609,9 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = pb * U + dep;
     float4 a1[UPW], a2[U / 4];
 #pragma unroll
-    for (int r = 0; r < UPW; ++r) a1[r] = *(const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane);
+    for (int r = 0; r < UPW; ++r) a1[r] = ld_weight((const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane));
 #pragma unroll
-    for (int i = 0; i < U / 4; ++i) a2[i] = *(const float4 *)(p.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i);
+    for (int i = 0; i < U / 4; ++i) a2[i] = ld_weight((const float4 *)(p.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i));
     for (int b = w; b < NB; b += MP_NWAVES) {
         const float4 y = lt_y_slot(p, b, pb == 0, wsc_all[w]);
         if (pb == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
@@ -702,10 +702,10 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
     const int u0 = q * LTS_U + ts_dep(t_start);
     uint2 a1[LTS_UPW];  // W1 rows u0 + LTS_UPW w + r, elements 4 lane .. 4 lane + 3
 #pragma unroll
-    for (int r = 0; r < LTS_UPW; ++r) a1[r] = *(const uint2 *)(p.w1h + (size_t)(u0 + w * LTS_UPW + r) * LTD + 4 * lane);
+    for (int r = 0; r < LTS_UPW; ++r) a1[r] = ld_weight((const uint2 *)(p.w1h + (size_t)(u0 + w * LTS_UPW + r) * LTD + 4 * lane));
     uint4 a2[LTS_U / 8];  // W2 row tid, units u0 .. u0 + LTS_U - 1
 #pragma unroll
-    for (int i = 0; i < LTS_U / 8; ++i) a2[i] = *(const uint4 *)(p.w2h + ((size_t)q * LTD + tid) * LTS_U + 8 * i);
+    for (int i = 0; i < LTS_U / 8; ++i) a2[i] = ld_weight((const uint4 *)(p.w2h + ((size_t)q * LTD + tid) * LTS_U + 8 * i));
     if (w == 0) {
         const float4 y = lt_y_slot(p, b, q == 0, wsc);
         if (q == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
@@ -922,14 +922,15 @@ __device__ __forceinline__ void lt_front_weights(const LtFrontP &p, int pb, int 
                                                  float4 &wv, float4 (&a1)[LTF_UPW], float4 (&a2)[LTF_U / 4]) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) wi[i] = *(const float4 *)(p.w_in + (size_t)n_in * D + 4 * (lane + 64 * i));
-    wk = *(const float4 *)(p.w_kvo + (size_t)n_in * LTD + 4 * lane);
-    wv = *(const float4 *)(p.w_kvo + (size_t)(LTD + n_in) * LTD + 4 * lane);
+    for (int i = 0; i < 3; ++i) wi[i] = ld_weight((const float4 *)(p.w_in + (size_t)n_in * D + 4 * (lane + 64 * i)));
+    wk = ld_weight((const float4 *)(p.w_kvo + (size_t)n_in * LTD + 4 * lane));
+    wv = ld_weight((const float4 *)(p.w_kvo + (size_t)(LTD + n_in) * LTD + 4 * lane));
     const int j0 = pb * LTF_U;
 #pragma unroll
-    for (int r = 0; r < LTF_UPW; ++r) a1[r] = *(const float4 *)(p.l.f.w1 + (size_t)(j0 + w * LTF_UPW + r) * LTD + 4 * lane);
+    for (int r = 0; r < LTF_UPW; ++r)
+        a1[r] = ld_weight((const float4 *)(p.l.f.w1 + (size_t)(j0 + w * LTF_UPW + r) * LTD + 4 * lane));
 #pragma unroll
-    for (int i = 0; i < LTF_U / 4; ++i) a2[i] = *(const float4 *)(p.l.f.w2 + (size_t)j0 * LTD + tid * LTF_U + 4 * i);
+    for (int i = 0; i < LTF_U / 4; ++i) a2[i] = ld_weight((const float4 *)(p.l.f.w2 + (size_t)j0 * LTD + tid * LTF_U + 4 * i));
 }
 __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     const unsigned long long t_start = ts_begin(p.l.f.ts);

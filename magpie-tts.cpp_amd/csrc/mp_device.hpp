@@ -352,12 +352,14 @@ __device__ __forceinline__ float4 kv_load4(const float *c, size_t i) {
     else return *(const float4 *)(c + i);
 }
 
-// Weight-stream loads (read once per launch by one CU). MP_NT_WEIGHTS builds issue
-// them non-temporal (global_load ... nt): the guide's nt-weights row; default off
-// until measured on this path.
+// Weight-stream loads (read once per launch by one CU), issued non-temporal
+// (global_load ... nt: the guide's nt-weights row). Measured on this path, two
+// alternating rounds on one box (gpurun_out/r04j_ab.txt): f32 B=1 2,677 / 2,596 ->
+// 2,724 / 2,725 frames/s, bf16 B=8 +2.7 %, B=16 +2 %, bf16 B=1 and Q8_0 B=1 within noise.
+// MP_NO_NT_WEIGHTS builds use the default policy.
 template <typename T>
 __device__ __forceinline__ T ld_weight(const T *p) {
-#ifdef MP_NT_WEIGHTS
+#ifndef MP_NO_NT_WEIGHTS
     if constexpr (sizeof(T) == 16) {
         typedef unsigned u4 __attribute__((ext_vector_type(4)));
         return __builtin_bit_cast(T, __builtin_nontemporal_load((const u4 *)p));

@@ -66,7 +66,8 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     // so the HBM latency overlaps the prologue's own dependent loads/reductions.
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int row0 = (blockIdx.x * MP_NWAVES + w) * RW + ts_dep(t_start);
-    // PRO_LN: the rows are loaded ahead of the weights (pre_load), the rest as before
+    // PreRows prologues (LN rows, plain rows, split merges): their loads go ahead of the
+    // weights (pre_load), the arithmetic after them is unchanged
     PreRows<NB, K, PRO> pre;
     constexpr bool PRE = PreRows<NB, K, PRO>::ON;
     if constexpr (PRE) {
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 #pragma unroll
     for (int hh = 0; hh < NB / NBS; ++hh) {
         if constexpr (PRE) {
-            pre_finish<NB, K, PRO>(p, pre, act);
+            pre_finish<NB, K, PRO>(p, pre, act, sc);
         } else if constexpr (NBS == NB) {
             prologue<NB, K, PRO>(p, act, red, sc);
         } else {

@@ -106,21 +106,48 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int rt = KS == 1 ? (int)blockIdx.x : (int)blockIdx.x / KS, ks = KS == 1 ? 0 : (int)blockIdx.x % KS;
 
-    // batched LN rows: loaded ahead of the weight stream (vector loads complete in
-    // issue order, so rows loaded behind the weights would wait for all of them)
+    // The activation loads go ahead of the weight stream (vector loads complete in
+    // issue order, so rows loaded behind the weights would wait for all of them): the
+    // PreRows prologues (LN rows, split merges), and plain 16-bit / f32 rows of up to 8
+    // items per thread. The arithmetic after them is unchanged.
     constexpr bool LNB = PRO == PRO_LN && NB >= 2;
+    constexpr bool PRE = PreRows<NB, K, PRO>::ON && (LNB || STAGE);
+    constexpr int ITEMS8 = NB * (KL / 8), PT8 = (ITEMS8 + MP_BLOCK - 1) / MP_BLOCK;
+    constexpr bool PLB = PRO == PRO_PLAIN_B16 && PT8 <= 8, PLF = PRO == PRO_PLAIN && PT8 <= 8;
     PreRows<NB, K, PRO> pre;
-    if constexpr (PreRows<NB, K, PRO>::ON) {
-        pre_load<NB, K, PRO>(p, pre);
-        __builtin_amdgcn_sched_barrier(0);  // keep the issue order: rows, then weights, then arithmetic
+    // native vector types, every element assigned: an array of HIP's uint4 / float4 structs
+    // assigned under a condition was kept in scratch memory
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 vb[PLB ? PT8 : 1];
+    f32x4 x0p[PLF ? PT8 : 1], x1p[PLF ? PT8 : 1];
+    if constexpr (PRE) pre_load<NB, K, PRO>(p, pre);
+    if constexpr (PLB) {
+        const unsigned short *src = p.src_b16 + ks * KL;
+#pragma unroll
+        for (int u = 0; u < PT8; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            vb[u] = e < ITEMS8 ? *(const u32x4 *)(src + (size_t)(e / (KL / 8)) * p.src_ld + (e % (KL / 8)) * 8)
+                               : u32x4{0u, 0u, 0u, 0u};
+        }
     }
+    if constexpr (PLF) {
+#pragma unroll
+        for (int u = 0; u < PT8; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            const float *src = p.src + ks * KL + (size_t)(min(e, ITEMS8 - 1) / (KL / 8)) * p.src_ld +
+                               (min(e, ITEMS8 - 1) % (KL / 8)) * 8;
+            x0p[u] = *(const f32x4 *)src;
+            x1p[u] = *(const f32x4 *)(src + 4);
+        }
+    }
+    if constexpr (PRE || PLB || PLF) __builtin_amdgcn_sched_barrier(0);  // issue order: rows, weights, arithmetic
 
     // weight fragments of this wave's K slice, issued before the prologue
     const uint4 *wf = (const uint4 *)p.Wb + ((size_t)rt * KC + ks * KCS + w * KW) * 64 + lane + ts_dep(t_start);
     uint4 a[KW];
 #pragma unroll
     for (int i = 0; i < KW; ++i) a[i] = ld_weight(wf + (size_t)i * 64);
-    if constexpr (PreRows<NB, K, PRO>::ON) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRE || PLB || PLF) __builtin_amdgcn_sched_barrier(0);
 
     // activation rows -> bf16 in LDS; row NB is zero and feeds MFMA columns NB..15
     if constexpr (LNB) {
@@ -186,7 +213,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
         }
         for (int e = tid; e < KL / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     } else if constexpr (STAGE) {
-        if constexpr (PreRows<NB, K, PRO>::ON) pre_finish<NB, K, PRO>(p, pre, actf);  // batch 1
+        if constexpr (PRE) pre_finish<NB, K, PRO>(p, pre, actf, sc);  // loads issued first
         else prologue<NB, K, PRO>(p, actf, red, sc);
         for (int e = tid; e < NR * (K / 8); e += MP_BLOCK) {
             const int b = e / (K / 8), k = (e % (K / 8)) * 8;
@@ -200,6 +227,27 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
             }
             *(uint4 *)(actb + b * KP + k) = o;
         }
+    } else if constexpr (PLB) {
+#pragma unroll
+        for (int u = 0; u < PT8; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            if (e < ITEMS8) *(u32x4 *)(actb + (e / (KL / 8)) * KP + (e % (KL / 8)) * 8) = vb[u];
+        }
+        for (int e = tid; e < KL / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
+    } else if constexpr (PLF) {
+#pragma unroll
+        for (int u = 0; u < PT8; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            if (e < ITEMS8) {
+                uint4 o;
+                o.x = pk16<F16>(x0p[u].x, x0p[u].y);
+                o.y = pk16<F16>(x0p[u].z, x0p[u].w);
+                o.z = pk16<F16>(x1p[u].x, x1p[u].y);
+                o.w = pk16<F16>(x1p[u].z, x1p[u].w);
+                *(uint4 *)(actb + (e / (KL / 8)) * KP + (e % (KL / 8)) * 8) = o;
+            }
+        }
+        for (int e = tid; e < KL / 8; e += MP_BLOCK) *(uint4 *)(actb + NB * KP + e * 8) = make_uint4(0, 0, 0, 0);
     } else if constexpr (PRO == PRO_PLAIN_B16) {
         // bf16 rows (written by the FFN-up epilogue): copied as they are, 12 uint4
         // per thread in flight

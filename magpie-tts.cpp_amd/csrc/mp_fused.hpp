@@ -391,6 +391,55 @@ __device__ __forceinline__ void ln_slots(const GemvP &p, Put put) {
     ln_finish<NB, K>(p, r, put);
 }
 
+// PRO_XA_LN's LayerNorm of the x2 rows in act (LN weights g already in registers):
+// block 0 stores x2 (the FFN residual input); act = LN(x2) * lnw with the same
+// one-wave DPP statistics as PRO_LN, so batch 1 and batched prologues agree bit for bit
+template <int NB, int K>
+__device__ __forceinline__ void xa_ln_rows(const GemvP &p, float *act, const float (&g)[K / 64]) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int PER = K / 64;
+    if constexpr (NB == 1) {
+            constexpr int Q = PER / MP_NWAVES;
+            float v[PER];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) v[i] = act[lane + 64 * i];
+            // x2 to HBM (block 0) after every global load of the prologue: a store
+            // earlier would order the later loads behind it
+            if (blockIdx.x == 0 && w == 0)
+#pragma unroll
+                for (int i = 0; i < PER; ++i) p.xres[lane + 64 * i] = v[i];
+            float mean, var;
+            wave_meanvar<PER>(v, mean, var);
+            const float rstd = 1.0f / sqrtf(var + p.eps);
+            lds_sync();  // every wave has read the row before any overwrites its quarter
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                if (i / Q != w) continue;
+                const int k = lane + 64 * i;
+                act[k] = ((v[i] - mean) * rstd) * g[i];
+            }
+        } else {
+            for (int b = w; b < NB; b += MP_NWAVES) {  // a wave owns its slots' rows
+                float v[PER];
+#pragma unroll
+                for (int i = 0; i < PER; ++i) v[i] = act[b * K + lane + 64 * i];
+                if (blockIdx.x == 0)
+#pragma unroll
+                    for (int i = 0; i < PER; ++i) p.xres[(size_t)b * D + lane + 64 * i] = v[i];
+                float mean, var;
+                wave_meanvar<PER>(v, mean, var);
+                const float rstd = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int k = lane + 64 * i;
+                    act[b * K + k] = ((v[i] - mean) * rstd) * g[i];
+                }
+            }
+        }
+        lds_sync();
+
+}
+
 // Batch-1 LayerNorm row (PRO_LN, NB = 1): every wave loads the whole row and runs
 // the same DPP statistics (identical results, no barrier), then writes its quarter
 // of act. Loads and arithmetic apart, as ln_load / ln_finish.
@@ -431,8 +480,9 @@ __device__ __forceinline__ void ln1_finish(const GemvP &p, Ln1Row<K> &r, float *
 
 // A prologue whose global loads a kernel issues AHEAD of its weight stream
 // (vector-memory loads complete in issue order: rows loaded behind the weights are
-// only usable once every weight has landed). PRO_LN only: its loads are the rows and
-// the LN weights, all independent of the launch's other work.
+// only usable once every weight has landed). PRO_LN, plain rows, the SA / XA split
+// merges (up to 4 slots) and the LT head's FFN merge at batch 1: their loads are
+// independent of the launch's other work; the arithmetic after them is unchanged.
 template <int NB, int K, int PRO>
 struct PreRows {
     static constexpr bool ON = false;
@@ -442,23 +492,135 @@ struct PreRows<NB, K, PRO_LN> {
     static constexpr bool ON = true;
     typename std::conditional<NB == 1, Ln1Row<K>, LnRows<NB, K>>::type r;
 };
+// register arrays of these structs hold native 4-float vectors (an array of HIP's
+// float4 struct in a struct member was kept in scratch memory)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 to_v4(float4 a) { return f32x4{a.x, a.y, a.z, a.w}; }
+__device__ __forceinline__ float4 to_f4(f32x4 a) { return make_float4(a.x, a.y, a.z, a.w); }
+// Plain rows (PRO_PLAIN) while they fit in 12 float4 per thread
+template <int NB, int K>
+struct PreRows<NB, K, PRO_PLAIN> {
+    static constexpr int PT = (NB * K / 4 + MP_BLOCK - 1) / MP_BLOCK;
+    static constexpr bool ON = NB * K <= 12288;
+    f32x4 v[ON ? PT : 1];
+};
+// The SA / XA split merges while every item fits in one round of the prologue's
+// (batches up to 4): the split outputs, the split (m, l) pairs and, for XA, x and the
+// LN weights
+template <int NB, int K, int NS, int NQ, int PART>
+struct PreMerge {
+    static constexpr int PT = (NB * (K / 4) + MP_BLOCK - 1) / MP_BLOCK;
+    static constexpr bool ON = PT <= 4 && NQ <= MP_BLOCK;
+    f32x4 o[ON ? PT : 1][NS], xv[ON ? PT : 1];
+    float ms[NS], ls[NS];
+    float g[K / 64];
+};
+template <int NB, int K>
+struct PreRows<NB, K, PRO_SA_MERGE> : PreMerge<NB, K, SA_SPLITS, NB * NH, SA_PART> {};
+template <int NB, int K>
+struct PreRows<NB, K, PRO_XA_LN> : PreMerge<NB, K, XA_SPLITS, NB, XA_PART> {};
+// the LT head's FFN merge at batch 1: the 64 partial sums and y of output tid
+template <int NB, int K>
+struct PreRows<NB, K, PRO_LTFFN_MERGE> {
+    static constexpr bool ON = NB == 1 && K == MP_BLOCK;
+    float pp[LT_FFN_P], y;
+};
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void pre_load(const GemvP &p, PreRows<NB, K, PRO> &pr) {
-    if constexpr (PreRows<NB, K, PRO>::ON) {
+    const int tid = threadIdx.x;
+    if constexpr (!PreRows<NB, K, PRO>::ON) {
+        return;
+    } else if constexpr (PRO == PRO_LN) {
         if constexpr (NB == 1) ln1_load<K>(p, pr.r);
         else ln_load<NB, K>(p, pr.r);
+    } else if constexpr (PRO == PRO_PLAIN) {
+#pragma unroll
+        for (int u = 0; u < PreRows<NB, K, PRO>::PT; ++u) {
+            const int e = min(u * MP_BLOCK + tid, NB * (K / 4) - 1);  // every element assigned (no scratch)
+            pr.v[u] = *(const f32x4 *)(p.src + (size_t)(e / (K / 4)) * p.src_ld + (e % (K / 4)) * 4);
+        }
+    } else if constexpr (PRO == PRO_SA_MERGE || PRO == PRO_XA_LN) {
+        constexpr bool SA = PRO == PRO_SA_MERGE;
+        constexpr int NS = SA ? SA_SPLITS : XA_SPLITS, PART = SA ? SA_PART : XA_PART, NQ = SA ? NB * NH : NB;
+        static_assert(K == D, "d_model wide");
+#pragma unroll
+        for (int u = 0; u < PreRows<NB, K, PRO>::PT; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            if (e >= NB * (K / 4)) break;
+            const int b = e / (K / 4), k = (e % (K / 4)) * 4, q = SA ? b * NH + k / DH : b;
+            if constexpr (!SA) pr.xv[u] = *(const f32x4 *)(p.src + (size_t)b * p.src_ld + k);
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2)
+                pr.o[u][s2] = *(const f32x4 *)(p.part + ((size_t)q * NS + s2) * PART + 4 + (SA ? k % DH : k));
+        }
+        if (tid < NQ) {
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2) {
+                pr.ms[s2] = p.part[((size_t)tid * NS + s2) * PART];
+                pr.ls[s2] = p.part[((size_t)tid * NS + s2) * PART + 1];
+            }
+        }
+        if constexpr (!SA) load_lnw<K / 64>(p.lnw, pr.g);
+    } else if constexpr (PRO == PRO_LTFFN_MERGE) {
+        const float *pp = p.part + tid;
+#pragma unroll
+        for (int q = 0; q < LT_FFN_P; ++q) pr.pp[q] = pp[(size_t)q * LTD];
+        pr.y = p.addsrc[tid];
     }
 }
 // the prologue's arithmetic on preloaded rows: act[NB][K] f32, as prologue<NB, K, PRO>
 template <int NB, int K, int PRO>
-__device__ __forceinline__ void pre_finish(const GemvP &p, PreRows<NB, K, PRO> &pr, float *act) {
-    if constexpr (PreRows<NB, K, PRO>::ON) {
+__device__ __forceinline__ void pre_finish(const GemvP &p, PreRows<NB, K, PRO> &pr, float *act, float *sc) {
+    const int tid = threadIdx.x;
+    if constexpr (!PreRows<NB, K, PRO>::ON) {
+        return;
+    } else if constexpr (PRO == PRO_LN) {
         if constexpr (NB == 1) {
             ln1_finish<K>(p, pr.r, act);
         } else {
             ln_finish<NB, K>(p, pr.r, [&](int b, int k, float y) { act[b * K + k] = y; });
             lds_sync();
         }
+    } else if constexpr (PRO == PRO_PLAIN) {
+#pragma unroll
+        for (int u = 0; u < PreRows<NB, K, PRO>::PT; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            if (e < NB * (K / 4)) *(f32x4 *)(act + (e / (K / 4)) * K + (e % (K / 4)) * 4) = pr.v[u];
+        }
+        lds_sync();
+    } else if constexpr (PRO == PRO_SA_MERGE || PRO == PRO_XA_LN) {
+        // merge_weights' and the merge loop's arithmetic (split_weights, split_merge4, xa_x2)
+        constexpr bool SA = PRO == PRO_SA_MERGE;
+        constexpr int NS = SA ? SA_SPLITS : XA_SPLITS, NQ = SA ? NB * NH : NB;
+        if (tid < NQ) {
+            float e[NS], rd;
+            split_weights<NS>(pr.ms, pr.ls, e, rd);
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2) sc[tid * (NS + 1) + s2] = e[s2];
+            sc[tid * (NS + 1) + NS] = rd;
+        }
+        lds_sync();
+#pragma unroll
+        for (int u = 0; u < PreRows<NB, K, PRO>::PT; ++u) {
+            const int e = u * MP_BLOCK + tid;
+            if (e >= NB * (K / 4)) break;
+            const int b = e / (K / 4), k = (e % (K / 4)) * 4, q = SA ? b * NH + k / DH : b;
+            float4 ou[NS];
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2) ou[s2] = to_f4(pr.o[u][s2]);
+            const float4 a = split_merge4<NS>(sc + q * (NS + 1), ou, sc[q * (NS + 1) + NS]);
+            if constexpr (SA) *(float4 *)(act + b * K + k) = a;
+            else *(float4 *)(act + b * K + k) = xa_x2(a, to_f4(pr.xv[u]));
+        }
+        lds_sync();
+        if constexpr (!SA) xa_ln_rows<NB, K>(p, act, pr.g);
+    } else if constexpr (PRO == PRO_LTFFN_MERGE) {
+        // lt_ffn_merge's arithmetic: partial sums in ascending order, then the residual
+        float s2 = pr.pp[0];
+#pragma unroll
+        for (int q = 1; q < LT_FFN_P; ++q) s2 += pr.pp[q];
+        act[tid] = s2 + pr.y;
+        lds_sync();
     }
 }
 
@@ -534,49 +696,10 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
             }
         }
         lds_sync();
-        const int lane = tid & 63, w = tid >> 6;
         constexpr int PER = K / 64;
         float g[PER];
         load_lnw<PER>(p.lnw, g);
-        if constexpr (NB == 1) {
-            constexpr int Q = PER / MP_NWAVES;
-            float v[PER];
-#pragma unroll
-            for (int i = 0; i < PER; ++i) v[i] = act[lane + 64 * i];
-            // x2 to HBM (block 0) after every global load of the prologue: a store
-            // earlier would order the later loads behind it
-            if (blockIdx.x == 0 && w == 0)
-#pragma unroll
-                for (int i = 0; i < PER; ++i) p.xres[lane + 64 * i] = v[i];
-            float mean, var;
-            wave_meanvar<PER>(v, mean, var);
-            const float rstd = 1.0f / sqrtf(var + p.eps);
-            lds_sync();  // every wave has read the row before any overwrites its quarter
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                if (i / Q != w) continue;
-                const int k = lane + 64 * i;
-                act[k] = ((v[i] - mean) * rstd) * g[i];
-            }
-        } else {
-            for (int b = w; b < NB; b += MP_NWAVES) {  // a wave owns its slots' rows
-                float v[PER];
-#pragma unroll
-                for (int i = 0; i < PER; ++i) v[i] = act[b * K + lane + 64 * i];
-                if (blockIdx.x == 0)
-#pragma unroll
-                    for (int i = 0; i < PER; ++i) p.xres[(size_t)b * D + lane + 64 * i] = v[i];
-                float mean, var;
-                wave_meanvar<PER>(v, mean, var);
-                const float rstd = 1.0f / sqrtf(var + p.eps);
-#pragma unroll
-                for (int i = 0; i < PER; ++i) {
-                    const int k = lane + 64 * i;
-                    act[b * K + k] = ((v[i] - mean) * rstd) * g[i];
-                }
-            }
-        }
-        lds_sync();
+        xa_ln_rows<NB, K>(p, act, g);
     } else if constexpr (PRO == PRO_LTFFN_MERGE) {
         static_assert(K == LTD, "LT is 256 wide");
         for (int e = tid; e < NB * K; e += MP_BLOCK) act[e] = lt_ffn_merge(p.part, p.addsrc, e / K, e % K);

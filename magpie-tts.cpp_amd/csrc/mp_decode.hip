@@ -541,28 +541,48 @@ hipError_t op_lt_merge(const LtFfnP &p, int NB, hipStream_t s) {
 // elements 4l..4l+3. `wb0`: this is workgroup 0, which publishes the code and the
 // position's k / vo rows for the later codebooks. One body for every batch size
 // (one wave per slot), so a batch reproduces its utterances run alone.
-__device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, float *wsc) {
+// lt_y_slot's global loads (earlier positions' k / vo, the logits, the step; cb = 0:
+// X_0 and vo_0), apart from its arithmetic so a kernel can issue them ahead of its
+// weight stream (vector loads complete in issue order). Native vectors, every element
+// assigned (an array of HIP's float4 struct in a struct member went to scratch).
+struct LtYPre {
+    f32x4 kr[NCB - 1], vr[NCB - 1];
+    float lv[PICK_R];
+    int stp;
+};
+__device__ __forceinline__ void lt_y_load(const LtFfn2P &p, int b, LtYPre &r) {
     const int lane = threadIdx.x & 63, cb = p.cb;
     const size_t row = (size_t)b * NCB * LTD + 4 * lane;
     if (cb == 0) {
-        const float4 x = *(const float4 *)(p.ltX + (size_t)b * LTD + 4 * lane), v = *(const float4 *)(p.ltv + row);
+        r.kr[0] = *(const f32x4 *)(p.ltX + (size_t)b * LTD + 4 * lane);
+        r.vr[0] = *(const f32x4 *)(p.ltv + row);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < NCB - 1; ++j) {
+        const int jj = j < cb ? j : 0;  // every element assigned; positions >= cb unused
+        r.kr[j] = *(const f32x4 *)(p.ltk + row + jj * LTD);
+        r.vr[j] = *(const f32x4 *)(p.ltv + row + jj * LTD);
+    }
+    load_logits(p.logits + (size_t)b * VCB, r.lv);
+    r.stp = p.step[b];
+}
+__device__ __forceinline__ float4 lt_y_finish(const LtFfn2P &p, int b, bool wb0, float *wsc, LtYPre &r) {
+    const int lane = threadIdx.x & 63, cb = p.cb;
+    const size_t row = (size_t)b * NCB * LTD + 4 * lane;
+    if (cb == 0) {
+        const float4 x = to_f4(r.kr[0]), v = to_f4(r.vr[0]);
         return make_float4(x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w);
     }
-    float4 kr[NCB - 1], vr[NCB - 1];  // earlier positions' k / vo, in flight during the pick
-#pragma unroll
-    for (int j = 0; j < NCB - 1; ++j)
-        if (j < cb) { kr[j] = *(const float4 *)(p.ltk + row + j * LTD); vr[j] = *(const float4 *)(p.ltv + row + j * LTD); }
-    float lv[PICK_R];
-    load_logits(p.logits + (size_t)b * VCB, lv);
-    const int stp = p.step[b];
+    const int stp = r.stp;
     int amax;
-    const int code = wave_pick_v(lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, cb - 1, wsc,
+    const int code = wave_pick_v(r.lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, cb - 1, wsc,
                                  amax);
-    const size_t r = (size_t)(cb - 1) * VCB + code;
-    const float *qkv = p.qkvtab + r * (3 * LTD) + 4 * lane;
+    const size_t rr = (size_t)(cb - 1) * VCB + code;
+    const float *qkv = p.qkvtab + rr * (3 * LTD) + 4 * lane;
     const float4 q4 = *(const float4 *)qkv, k4 = *(const float4 *)(qkv + LTD);
-    const float4 vo4 = *(const float4 *)(p.votab + r * LTD + 4 * lane);
-    const float4 x4 = *(const float4 *)(p.ptab + r * LTD + 4 * lane);
+    const float4 vo4 = *(const float4 *)(p.votab + rr * LTD + 4 * lane);
+    const float4 x4 = *(const float4 *)(p.ptab + rr * LTD + 4 * lane);
     const float4 pos4 = *(const float4 *)(p.lt_pos + (size_t)cb * LTD + 4 * lane);
     if (wb0) {
         if (lane == 0) {
@@ -576,7 +596,7 @@ __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, f
     float sj[NCB];
 #pragma unroll
     for (int j = 0; j < NCB; ++j)
-        sj[j] = j < cb ? wave_sum(dotv(q4, kr[j < NCB - 1 ? j : 0])) * (1.0f / 16.0f)
+        sj[j] = j < cb ? wave_sum(dotv(q4, to_f4(r.kr[j < NCB - 1 ? j : 0]))) * (1.0f / 16.0f)
                        : j == cb ? wave_sum(dotv(q4, k4)) * (1.0f / 16.0f) : -INFINITY;
     float m = -INFINITY;
 #pragma unroll
@@ -588,11 +608,16 @@ __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, f
         if (j > cb) break;
         const float e = expf(sj[j] - m);
         l += e;
-        const float4 v4 = j == cb ? vo4 : vr[j < NCB - 1 ? j : 0];
+        const float4 v4 = j == cb ? vo4 : to_f4(r.vr[j < NCB - 1 ? j : 0]);
         a.x = fmaf(e, v4.x, a.x); a.y = fmaf(e, v4.y, a.y); a.z = fmaf(e, v4.z, a.z); a.w = fmaf(e, v4.w, a.w);
     }
     return make_float4(x4.x + pos4.x + a.x / l, x4.y + pos4.y + a.y / l, x4.z + pos4.z + a.z / l,
                        x4.w + pos4.w + a.w / l);
+}
+__device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, float *wsc) {
+    LtYPre r;
+    lt_y_load(p, b, r);
+    return lt_y_finish(p, b, wb0, wsc, r);
 }
 
 // The LT step of codebook cb in f32 mode: y (lt_y_slot, every workgroup for itself;
@@ -608,13 +633,18 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     __shared__ __attribute__((aligned(16))) float fs[NB][U];
     __shared__ __attribute__((aligned(16))) float wsc_all[MP_NWAVES][2 * VCB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = pb * U + dep;
+    // the wave's first slot's loads (logits, earlier positions) ahead of the weights
+    LtYPre yp;
+    if (w < NB) lt_y_load(p, w, yp);
+    __builtin_amdgcn_sched_barrier(0);
     float4 a1[UPW], a2[U / 4];
 #pragma unroll
     for (int r = 0; r < UPW; ++r) a1[r] = ld_weight((const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane));
 #pragma unroll
     for (int i = 0; i < U / 4; ++i) a2[i] = ld_weight((const float4 *)(p.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i));
+    __builtin_amdgcn_sched_barrier(0);
     for (int b = w; b < NB; b += MP_NWAVES) {
-        const float4 y = lt_y_slot(p, b, pb == 0, wsc_all[w]);
+        const float4 y = b == w ? lt_y_finish(p, b, pb == 0, wsc_all[w], yp) : lt_y_slot(p, b, pb == 0, wsc_all[w]);
         if (pb == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
         if (ys && b == 0) *(float4 *)&ys[4 * lane] = y;
         const float x[4] = {y.x, y.y, y.z, y.w};
@@ -701,14 +731,19 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
     __shared__ __attribute__((aligned(16))) float wsc[2 * VCB];
     const int q = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int u0 = q * LTS_U + ts_dep(t_start);
+    // wave 0's logits / earlier positions first, then the weights (in-order completion)
+    LtYPre yp;
+    if (w == 0) lt_y_load(p, b, yp);
+    __builtin_amdgcn_sched_barrier(0);
     uint2 a1[LTS_UPW];  // W1 rows u0 + LTS_UPW w + r, elements 4 lane .. 4 lane + 3
 #pragma unroll
     for (int r = 0; r < LTS_UPW; ++r) a1[r] = ld_weight((const uint2 *)(p.w1h + (size_t)(u0 + w * LTS_UPW + r) * LTD + 4 * lane));
     uint4 a2[LTS_U / 8];  // W2 row tid, units u0 .. u0 + LTS_U - 1
 #pragma unroll
     for (int i = 0; i < LTS_U / 8; ++i) a2[i] = ld_weight((const uint4 *)(p.w2h + ((size_t)q * LTD + tid) * LTS_U + 8 * i));
+    __builtin_amdgcn_sched_barrier(0);
     if (w == 0) {
-        const float4 y = lt_y_slot(p, b, q == 0, wsc);
+        const float4 y = lt_y_finish(p, b, q == 0, wsc, yp);
         if (q == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
         *(float4 *)&ys[4 * lane] = y;
         const float x[4] = {y.x, y.y, y.z, y.w};
@@ -805,16 +840,14 @@ hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
 constexpr int LTF_U = LTF / LT_FFN_P, LTF_UPW = LTF_U / MP_NWAVES;
 __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_in, const float4 (&wi)[3], float4 wk,
                                                float4 wv, const float4 (&a1)[LTF_UPW], const float4 (&a2)[LTF_U / 4],
-                                               float *act, float *act2, float *xs, float *fs, float4 *y4, float4 *v4) {
+                                               const float (&v)[D / 64], const float (&g)[D / 64], float *act, float *act2,
+                                               float *xs, float *fs, float4 *y4, float4 *v4) {
     constexpr int U = LTF_U, UPW = LTF_UPW, PER = D / 64, Q = PER / MP_NWAVES;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const unsigned tag_s = (unsigned)p.iter[0] * 64u + 40u, tag_v = tag_s + 1u;
-    // ---- LN(x) (PRO_LN, batch 1: every wave the whole row, writes its quarter)
+    // ---- LN(x) (PRO_LN, batch 1: every wave the whole row, writes its quarter); the row
+    // and the LN weights v, g were loaded by the caller ahead of the weight stream
     {
-        float v[PER], g[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) v[i] = p.x[lane + 64 * i];
-        load_lnw<PER>(p.norm_out, g);
         float mean, var;
         wave_meanvar<PER>(v, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.l.f.eps);
@@ -942,9 +975,19 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     __shared__ __attribute__((aligned(16))) float fs[LTF_U];
     const int tid = threadIdx.x, w = tid >> 6, pb = blockIdx.x;
     const int n_in = pb * MP_NWAVES + w + ts_dep(t_start);  // this wave's in_proj / k / vo row
+    // the decoder output row and the final LN's weights first (vector loads complete in
+    // issue order: behind the weights they would wait for all of them), then the weights
+    constexpr int PER = D / 64;
+    float v[PER], g[PER];
+    const int lane = tid & 63;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = p.x[lane + 64 * i];
+    load_lnw<PER>(p.norm_out, g);
+    __builtin_amdgcn_sched_barrier(0);
     float4 wi[3], wk, wv, a1[LTF_UPW], a2[LTF_U / 4];
     lt_front_weights(p, pb, n_in, wi, wk, wv, a1, a2);
-    const float acc = lt_front_core(p, pb, n_in, wi, wk, wv, a1, a2, act, act2, xs, fs, nullptr, nullptr);
+    __builtin_amdgcn_sched_barrier(0);
+    const float acc = lt_front_core(p, pb, n_in, wi, wk, wv, a1, a2, v, g, act, act2, xs, fs, nullptr, nullptr);
     p.l.f.part[(size_t)pb * LTD + tid] = acc;
     ts_end(p.l.f.ts, t_start);
 }

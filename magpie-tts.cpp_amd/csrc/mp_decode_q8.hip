@@ -98,6 +98,13 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
 
     // this wave's weight fragments and their scales, issued before the prologue
     // (Q4: 8 nibbles per block and lane, half the bytes: the Q4_0 file's 18 per 32)
+    // (the PreRows prologues' loads go first: vector loads complete in issue order)
+    constexpr bool PRE = PreRows<NB, K, PRO>::ON;
+    PreRows<NB, K, PRO> pre;
+    if constexpr (PRE) {
+        pre_load<NB, K, PRO>(p, pre);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     using AT = typename std::conditional<Q4, uint2, uint4>::type;
     const AT *wf = (const AT *)p.Wq + ((size_t)rt * KP + w * KW) * 64 + lane + ts_dep(t_start);
     const uint4 *sf = (const uint4 *)p.Wd + ((size_t)rt * KP + w * KW) * 4 + (lane >> 4);
@@ -105,8 +112,12 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     uint4 sd[KW];
 #pragma unroll
     for (int i = 0; i < KW; ++i) { a[i] = ld_weight(wf + (size_t)i * 64); sd[i] = ld_weight(sf + (size_t)i * 4); }
-
-    prologue<NB, K, PRO>(p, act, red, sc);
+    if constexpr (PRE) {
+        __builtin_amdgcn_sched_barrier(0);
+        pre_finish<NB, K, PRO>(p, pre, act, sc);
+    } else {
+        prologue<NB, K, PRO>(p, act, red, sc);
+    }
 
     // activation rows -> Q8_0 (quantize_row_q8_0_ref), 4 lanes x 8 elements per block;
     // row NB is zero (q = 0, d = 0) and feeds MFMA columns NB..15

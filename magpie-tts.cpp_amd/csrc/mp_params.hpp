@@ -29,7 +29,10 @@ constexpr int SA_PART = 4 + DH;     // per (slot, head, split): m, l, -, -, O[64
 constexpr int XA_SPLITS = MP_XA_SPLITS;  // text-key splits of the fused cross-attention (xa_part_kernel)
 constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
 constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
-constexpr int LTS_P = 32;           // bf16 mode LT step (lt_slot_kernel): workgroups per slot = partial FFN-down sums
+#ifndef MP_LTS_P
+#define MP_LTS_P 32
+#endif
+constexpr int LTS_P = MP_LTS_P;           // bf16 mode LT step (lt_slot_kernel): workgroups per slot = partial FFN-down sums
 constexpr int LTQ_P = 32;           // Q8_0 mode LT step (lt_slot_q8_kernel): workgroups per slot = partial FFN-down sums
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)

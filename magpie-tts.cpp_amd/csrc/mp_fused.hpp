@@ -160,9 +160,16 @@ constexpr int ltc_off() { return NB * LTD; }
 // (gathered this launch) when CUR, else row cb of ltk/ltv; earlier positions come
 // from kr/vr when PRE (loaded ahead by the caller), else from ltk/ltv. The
 // arithmetic is the same either way, at every batch size.
+// Inlined (a __noinline__ copy took its arrays through scratch memory); the rounding is
+// pinned instead (contraction off, explicit fmaf), so every caller computes the same bits.
+__device__ __forceinline__ float dot4_pinned(float4 a, float4 b) {
+#pragma clang fp contract(off)
+    return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
 template <bool CUR, bool PRE>
-__device__ __noinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4,
+__device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4,
                                             const float4 (&kr)[NCB], const float4 (&vr)[NCB]) {
+#pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     const int nk = p.cb + 1;
     const float *kb = p.ltk + (size_t)b * NCB * LTD + 4 * lane, *vb = p.ltv + (size_t)b * NCB * LTD + 4 * lane;
@@ -171,7 +178,7 @@ __device__ __noinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float
     for (int j = 0; j < NCB; ++j) {
         if (j < nk) {
             const float4 k4 = (CUR && j == p.cb) ? kc4 : PRE ? kr[j] : *(const float4 *)(kb + j * LTD);
-            sj[j] = wave_sum(dotv(q4, k4)) * (1.0f / 16.0f);
+            sj[j] = wave_sum(dot4_pinned(q4, k4)) * (1.0f / 16.0f);
         } else {
             sj[j] = -INFINITY;
         }

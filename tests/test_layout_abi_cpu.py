@@ -277,6 +277,11 @@ def test_library_has_no_packed_fp32_instructions(tmp_path):
                              capture_output=True, text=True, check=True).stdout
         bad = re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", dis)
         assert not bad, f"{co.name}: {len(bad)} packed-FP32 instructions ({bad[0]})"
+        # no kernel keeps registers in scratch memory (round 4: arrays of HIP's float4 /
+        # uint4 structs assigned under a condition, and arrays passed to a __noinline__
+        # function, went to scratch: a dependent memory round trip per element)
+        spill = re.findall(r"\bscratch_(?:load|store)_\w+", dis)
+        assert not spill, f"{co.name}: {len(spill)} scratch instructions ({spill[0]})"
         n_mfma += len(re.findall(r"\bv_mfma_", dis))
     assert n_mfma > 1000  # the disassembly is real: the MFMA kernels are in it
 

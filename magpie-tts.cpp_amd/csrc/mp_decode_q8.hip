@@ -209,13 +209,21 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
 
 // ---------------------------------------------------------------- LT step, Q8_0 mode
 // LtSlotQ8P (mp_params.hpp). Workgroup (q, b), LTQ_P per slot at every batch size.
-// (Every workgroup computing all 256 o_net rows itself, so that y needs no hand-off,
-// measured no faster at batch 1: 12.47 vs 12.41 us per step.)
+// RED (p.wot set): every workgroup computes all 256 o_net rows itself (thread t row t,
+// from the transposed copy: 16 coalesced 16-byte loads, L2-resident after the first
+// workgroup), so y needs no hand-off. DEFER (p.part set, batch 1): the partial FFN-down
+// sums are plain stores and the Q8_0 head's prologue merges them (PRO_LTFFN_MERGE: the
+// same p-ascending sum, then + y), so the launch has no hand-off at all. Every variant
+// computes the same bits: the o_net row is the block-ordered sum of (int dot) x (d_w d_a)
+// from 0, the merge sums the LTQ_P partials in ascending p, then adds y.
 constexpr int LTQ_U = LTF / LTQ_P, LTQ_UPW = LTQ_U / MP_NWAVES, LTQ_R = LTD / LTQ_P, LTQ_RW = LTQ_R / MP_NWAVES;
+static_assert(LTQ_P == LT_FFN_P, "the deferred merge is the head's PRO_LTFFN_MERGE prologue");
+template <bool RED, bool DEFER>
 __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
 #pragma clang fp contract(off)
     const unsigned long long t_start = ts_begin(p.ts);
     static_assert(LTD == MP_BLOCK && LTQ_RW >= 1 && LTQ_RW * MP_NWAVES * LTQ_P == LTD && LTQ_U % 4 == 0, "split");
+    static_assert(RED || !DEFER, "the deferred merge needs y in every workgroup");
     __shared__ __attribute__((aligned(16))) float xs[LTD];   // X (the attention residual), then LN(y)
     __shared__ __attribute__((aligned(16))) float ys[LTD];
     __shared__ __attribute__((aligned(16))) int aq[LTD / 4];  // the attention output as Q8_0 (4 int8 per lane)
@@ -247,10 +255,18 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
     const int r0 = q * LTQ_R + LTQ_RW * w + dep;
     int wq[LTQ_RW];
     float wd[LTQ_RW];
+    intx4 wr[RED ? LTD / 16 : 1];  // RED: row tid's 256 int8 (16 B per load, wot[i][tid])
+    intx4 wrd;                     // RED: row tid's 8 fp16 block scales
+    if constexpr (RED) {
 #pragma unroll
-    for (int r = 0; r < LTQ_RW; ++r) {
-        wq[r] = *(const int *)(p.woq + (size_t)(r0 + r) * LTD + 4 * lane);
-        wd[r] = __half2float(__ushort_as_half(p.wod[(size_t)(r0 + r) * (LTD / 32) + (lane >> 3)]));
+        for (int i = 0; i < LTD / 16; ++i) wr[i] = *(const intx4 *)(p.wot + ((size_t)i * LTD + tid + dep) * 16);
+        wrd = *(const intx4 *)(p.wod + (size_t)tid * (LTD / 32));
+    } else {
+#pragma unroll
+        for (int r = 0; r < LTQ_RW; ++r) {
+            wq[r] = *(const int *)(p.woq + (size_t)(r0 + r) * LTD + 4 * lane);
+            wd[r] = __half2float(__ushort_as_half(p.wod[(size_t)(r0 + r) * (LTD / 32) + (lane >> 3)]));
+        }
     }
     const int u0 = q * LTQ_U;
     float4 a1[LTQ_UPW], a2[LTQ_U / 4];
@@ -300,7 +316,30 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
     }
     lds_sync();
     // o_net: per block the exact integer dot, then sum_blocks isum * (d_w d_a) in block order
-    {
+    if constexpr (RED) {
+        float acc = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < LTD / 32; ++kb) {
+            const intx4 x0 = *(const intx4 *)&aq[8 * kb], x1 = *(const intx4 *)&aq[8 * kb + 4];
+            const intx4 w0 = wr[2 * kb], w1 = wr[2 * kb + 1];
+            int is = __builtin_amdgcn_sdot4(w0.x, x0.x, 0, false);
+            is = __builtin_amdgcn_sdot4(w0.y, x0.y, is, false);
+            is = __builtin_amdgcn_sdot4(w0.z, x0.z, is, false);
+            is = __builtin_amdgcn_sdot4(w0.w, x0.w, is, false);
+            is = __builtin_amdgcn_sdot4(w1.x, x1.x, is, false);
+            is = __builtin_amdgcn_sdot4(w1.y, x1.y, is, false);
+            is = __builtin_amdgcn_sdot4(w1.z, x1.z, is, false);
+            is = __builtin_amdgcn_sdot4(w1.w, x1.w, is, false);
+            const unsigned dw2 = (unsigned)wrd[kb >> 1];
+            const float dwk = __half2float(__ushort_as_half((unsigned short)((kb & 1) ? dw2 >> 16 : dw2 & 0xFFFFu)));
+            const float fb = (float)is * (dwk * ad[kb]);
+            acc += fb;
+        }
+        const float yv = acc + xs[tid];
+        ys[tid] = yv;
+        if (q == 0) p.y[(size_t)b * LTD + tid] = yv;
+        lds_sync();
+    } else {
         const int av = aq[lane];
         float o[LTQ_RW];
 #pragma unroll
@@ -326,9 +365,14 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
     // y (all 256) from the slot's granules, LN -> xs (wave 0; the other waves wait)
     if (w == 0) {
         float yv[4];
+        if constexpr (RED) {
+            const float4 y4 = *(const float4 *)&ys[4 * lane];
+            yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+        } else {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) yv[c] = gh_wait(p.gy + (size_t)b * LTD + 4 * lane + c, tag_y, p.hx_err);
-        *(float4 *)&ys[4 * lane] = make_float4(yv[0], yv[1], yv[2], yv[3]);
+            for (int c = 0; c < 4; ++c) yv[c] = gh_wait(p.gy + (size_t)b * LTD + 4 * lane + c, tag_y, p.hx_err);
+            *(float4 *)&ys[4 * lane] = make_float4(yv[0], yv[1], yv[2], yv[3]);
+        }
         ts_mark(p.ts, t_start);  // profiling: y seen
         float mean, var;
         wave_meanvar<4>(yv, mean, var);
@@ -356,6 +400,11 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
         acc = fmaf(a2[i].z, f4.z, acc);
         acc = fmaf(a2[i].w, f4.w, acc);
     }
+    if constexpr (DEFER) {  // the head's prologue merges (PRO_LTFFN_MERGE)
+        p.part[((size_t)b * LTQ_P + q) * LTD + tid] = acc;
+        ts_end(p.ts, t_start);
+        return;
+    }
     // partial sums through granules; this workgroup merges its LTQ_R outputs in q order
     gu64 *gp = (gu64 *)p.gp + (size_t)b * LTQ_P * LTD;
     __hip_atomic_store(gp + (size_t)q * LTD + tid, ((unsigned long long)tag_p << 32) | __float_as_uint(acc),
@@ -373,12 +422,15 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
 }
 hipError_t op_lt_slot_q8(const LtSlotQ8P &p, int NB, hipStream_t s) {
     const GemvP &g = p.g;
-    if (!p.woq || !p.wod || !p.lnw || !p.w1 || !p.w2s || !p.y || !p.y2 || !p.gy || !p.gp || !p.iter || !p.hx_err ||
+    if (!(p.woq || p.wot) || !p.wod || !p.lnw || !p.w1 || !p.w2s || !p.y || (!p.part && (!p.y2 || !p.gp)) ||
+        (!p.wot && !p.gy) || (p.part && (!p.wot || NB != 1)) || !p.iter || !p.hx_err ||
         !g.ltX || !g.ltk || !g.ltv || !g.lk || !g.lv || g.cb < 0 || g.cb >= NCB || NB < 1 || NB > 16 ||
         (g.cb > 0 && (!g.logits || !g.codes_cur || !g.qkvtab || !g.ptab || !g.lt_pos || !g.step || !g.smp.cfg ||
                       !g.smp.argeos)))
         return hipErrorInvalidValue;
-    mp::launch(lt_slot_q8_kernel, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
+    if (p.part) mp::launch(lt_slot_q8_kernel<true, true>, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
+    else if (p.wot) mp::launch(lt_slot_q8_kernel<true, false>, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
+    else mp::launch(lt_slot_q8_kernel<false, false>, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
@@ -595,14 +647,15 @@ __device__ __forceinline__ void xa_q8_onet(const uint4 (&wo)[G], const float (&w
         s = __builtin_amdgcn_sdot4((int)wo[g].w, a4.w, s, false);
         s += __builtin_amdgcn_update_dpp(0, s, 0xB1, 0xF, 0xF, false);
         const float f = (lane & 1) ? 0.f : (float)s * (wos[g] * ad[kc >> 1]);
-        float v = 0.f;
-#pragma unroll
-        for (int rr = 0; rr < XQ8_OR; ++rr) {
-            const float t = wave_sum((r == rr) ? f : 0.f);
-            if (lane == rr) v = t;
-        }
-        if (lane < XQ8_OR) {
-            const int row = row0 + g * XQ8_OR + lane;
+        // the row's 4 block terms (lanes 8r + 0, 2, 4, 6) as (f0 + f2) + (f4 + f6) in all 8 of
+        // its lanes, every row at once: the same bits as a full-wave tree sum of the row's
+        // lanes alone (whose remaining steps add +0, hence the final + 0)
+        float v = f + dpp_mov<0xB1>(f);
+        v += dpp_mov<0x4E>(v);
+        v += dpp_mov<0x141>(v);
+        v += 0.f;
+        if ((lane & 7) == 0) {
+            const int row = row0 + g * XQ8_OR + r;
             x2[row] = v + x1[row];
         }
     }
@@ -870,7 +923,7 @@ __device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed ch
         [&](int d4) {
             float v[PER];
             xq8_sweep_x1(p, b, v);
-            ts_mark(p.ts, t_start);  // profiling: x1 seen
+            ts_phase<0>(p.ts, t_start);  // profiling: x1 seen
             if (w == 0) {  // the residual rows of this workgroup's o_net
                 float xr = v[0];
 #pragma unroll
@@ -884,10 +937,13 @@ __device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed ch
                 if (qa == 0) qs[16 * w + 64 * j + (lane >> 2)] = qv;
             }
             lds_sync();
+            ts_phase<1>(p.ts, t_start);  // profiling: q done
             return *(const float4 *)&qs[d4];
         },
         x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
+    ts_phase<2>(p.ts, t_start);  // profiling: attention done
     xa_quantize_a(a_s, aq, ad);
+    ts_phase<3>(p.ts, t_start);  // profiling: a quantised
     xa_q8_onet<OG>(wo, wos, r0, aq, ad, x1s - rb * XQ8_ROWS, x.x2 + (size_t)b * D);
     ts_end(p.ts, t_start);
 }

@@ -117,6 +117,18 @@ __device__ __forceinline__ void ts_mark(unsigned long long *ts, unsigned long lo
                 make_ulonglong2(t0, t1);
     }
 }
+// stamp K (0 .. TS_WAVES/2 - 1) of a workgroup's phases, from wave 0, into slot TS_WAVES/2 + K
+// (diagnostics of kernels whose phases are workgroup-wide: use instead of ts_mark)
+template <int K>
+__device__ __forceinline__ void ts_phase(unsigned long long *ts, unsigned long long t0) {
+    static_assert(K >= 0 && K < TS_WAVES / 2, "phase slot");
+    if (ts) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const int blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if (threadIdx.x == 0 && blk < TS_BLOCKS)
+            *(ulonglong2 *)(ts + 2 * ((size_t)blk * TS_WAVES + TS_WAVES / 2 + K)) = make_ulonglong2(t0, t1);
+    }
+}
 __device__ __forceinline__ void ts_end(unsigned long long *ts, unsigned long long t0) {
     if (ts) {
         __builtin_amdgcn_s_waitcnt(0);

@@ -33,7 +33,7 @@ constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = par
 #define MP_LTS_P 32
 #endif
 constexpr int LTS_P = MP_LTS_P;           // bf16 mode LT step (lt_slot_kernel): workgroups per slot = partial FFN-down sums
-constexpr int LTQ_P = 32;           // Q8_0 mode LT step (lt_slot_q8_kernel): workgroups per slot = partial FFN-down sums
+constexpr int LTQ_P = 64;           // Q8_0 mode LT step (lt_slot_q8_kernel): workgroups per slot = partial FFN-down sums
 
 // prologue / epilogue selectors of the fused GEMV family (mp_decode.hip)
 enum Pro {
@@ -332,6 +332,8 @@ struct GemvP {
 struct LtSlotQ8P {
     GemvP g;                       // pick / gathers / attention fields (lt_pick_kernel's), cb
     const signed char *woq;        // o_net int8 [256][256] (Q4_0 blocks as q - 8)
+    const signed char *wot;        // the same transposed by 16-byte chunks [16][256][16] (RED: every workgroup all rows)
+    float *part;                   // DEFER (batch 1): plain partial sums [LTQ_P][256], merged by the head's prologue
     const unsigned short *wod;     // o_net fp16 block scales [256][8]
     const float *lnw;              // norm_pos_ff
     float eps;

@@ -228,6 +228,7 @@ struct Model {
     size_t q8_bytes = 0;
     bool q8_all = false;  // every decode projection is Q8_0 / Q4_0: batches up to 16
     QW lt_in8, lt_qkv8, lt_o8, lt_out8;  // lt_out8: [8][2024][256] (+ [8][2024][8] scales)
+    const signed char *lt_o8t = nullptr;  // lt_o8's int8 transposed by 16-byte chunks [16][256][16] (lt_slot_q8_kernel)
     float *arena = nullptr;
     size_t arena_bytes = 0;
 };
@@ -748,6 +749,7 @@ int load_q8(mp_dev *dev, const char *path) {
     for (auto &it : items) {
         const size_t n = (size_t)it.t->nelements();
         total += align_up(n) + align_up(n / 32 * 2);
+        if (it.dst == &m.lt_o8) total += align_up(n);  // the transposed copy
     }
     if (m.q8_arena) { hipFree(m.q8_arena); m.q8_arena = nullptr; }
     HIPCHK(hipMalloc(&m.q8_arena, total));
@@ -798,6 +800,16 @@ int load_q8(mp_dev *dev, const char *path) {
         }
         HIPCHK(hipMemcpy(dq, hq.data(), n, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(dd, hd.data(), n / 32 * 2, hipMemcpyHostToDevice));
+        if (it.dst == &m.lt_o8) {  // chunk i of row r at [i][r]: thread r's 16 loads coalesce across the wave
+            if (n != (size_t)256 * 256) return fail(dev, MP_ERR_FORMAT, "unexpected LT o_net shape");
+            std::vector<signed char> ht(n);
+            for (int r = 0; r < 256; ++r)
+                for (int i = 0; i < 16; ++i) memcpy(&ht[((size_t)i * 256 + r) * 16], &hq[(size_t)r * 256 + i * 16], 16);
+            signed char *dt = (signed char *)cur;
+            cur += align_up(n);
+            HIPCHK(hipMemcpy(dt, ht.data(), n, hipMemcpyHostToDevice));
+            m.lt_o8t = dt;
+        }
     }
     // the decode projections once more in int8 MFMA fragment order
     struct Dec { mp::QW *w; int N, K, heads; };
@@ -1130,6 +1142,14 @@ bool q8_unfused() {
     const char *e = getenv("MAGPIE_Q8_UNFUSED");
     return e && atoi(e) != 0;
 }
+// MAGPIE_LTQ8 (Q8_0 LT step, lt_slot_q8_kernel): 0 = o_net rows split over the workgroups
+// (y hand-off) and the FFN merge in the launch; 1 = every workgroup all o_net rows (no y
+// hand-off); 2 (default) = that up to 4 slots, and at batch 1 the FFN merge deferred to
+// the head's prologue. Every setting computes the same bits (tests/test_q8_fused_gpu.py).
+int ltq8_mode() {
+    const char *e = getenv("MAGPIE_LTQ8");
+    return e ? atoi(e) : 2;
+}
 
 // Diagnostics (MAGPIE_EAGER=1 and MAGPIE_DUMP_LT=file): after every launch of
 // the local transformer, slot 0's LT state is appended to the file as f32
@@ -1342,6 +1362,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             sp.woq = m.lt_o8.q; sp.wod = m.lt_o8.d; sp.lnw = m.lt_norm_ff; sp.eps = m.eps; sp.w1 = m.lt_ff1;
             sp.w2s = m.lt_ff2q; sp.y = io.ltY; sp.y2 = io.lty2; sp.gy = io.ltyg; sp.gp = io.ltgh;
             sp.iter = io.iter; sp.hx_err = io.hx_err;
+            const int lm = ltq8_mode();
+            if (lm == 1 || (lm >= 2 && NB <= 4)) sp.wot = m.lt_o8t;  // (8+ slots: 512+ workgroups, the split rows)
+            if (lm >= 2 && NB == 1 && sp.wot) sp.part = io.ltp;
             if (ops) {
                 mp::OpRec r{};
                 r.name = "lt_slot_q8"; r.kind = mp::K_LTSLOTQ8; r.lq8 = sp; r.B = NB;
@@ -1356,7 +1379,12 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             g.src = io.lty2; g.src_ld = 256; g.out = io.logits; g.out_ld = 2024;
             g.Wq = m.lt_out8.pq + (size_t)cb * m.lt_out8.head_q; g.q4 = m.lt_out8.nib;
             g.Wd = (const unsigned short *)((const char *)m.lt_out8.pd + (size_t)cb * q8p_head_d());
-            if ((rc = run("lt_e", tq.lt_e, g, Fq(m.lt_out8) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
+            mp::GemvFn efn = tq.lt_e;
+            if (sp.part) {  // the FFN merge is the head's prologue
+                g.part = io.ltp; g.addsrc = io.ltY;
+                efn = mp::q8_lt_em_1;
+            }
+            if ((rc = run("lt_e", efn, g, Fq(m.lt_out8) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
                 return rc;
         }
     } else
@@ -1640,6 +1668,7 @@ int mp_hip_load_model_ex(mp_dev *dev, const char *path, int weight_mode) {
     if (dev->m.q8p_arena) { hipFree(dev->m.q8p_arena); dev->m.q8p_arena = nullptr; }
     dev->m.q8_all = false;
     dev->m.lt_in8 = dev->m.lt_qkv8 = dev->m.lt_o8 = dev->m.lt_out8 = mp::QW{};
+    dev->m.lt_o8t = nullptr;
     dev->m.pk_lt_in = nullptr;  // set again by an F16 load
     // derived LT weight layouts of a previous model (rebuilt by build_ptab)
     for (void **pp : {(void **)&dev->m.lt_ff2s, (void **)&dev->m.lt_ff1h, (void **)&dev->m.lt_ff2h, (void **)&dev->m.lt_ff2q})

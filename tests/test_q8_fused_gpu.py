@@ -111,3 +111,47 @@ def test_q4_nibbles_equal_int8_repack(ma, q4_model, B):
     for b in range(B):
         assert np.array_equal(rn.codes[b], r8.codes[b]) and np.array_equal(rn.hidden[b], r8.hidden[b]), b
     assert bn["lt_e"] < b8["lt_e"] and bn["qkv" if B == 16 else "qkv_sa"] < b8["qkv" if B == 16 else "qkv_sa"]
+
+
+def _lt_dump(ma, path, toks, mode, tmp_path, weights="q8"):
+    """Eager run with MAGPIE_LTQ8=mode, slot 0's LT state after every LT step
+    (MAGPIE_DUMP_LT: the previous head's logits, codes, X, y per record)."""
+    dump = str(tmp_path / f"lt_{weights}_{mode}_{len(toks)}.bin")
+    env = {"MAGPIE_LTQ8": str(mode), "MAGPIE_EAGER": "1", "MAGPIE_DUMP_LT": dump}
+    os.environ.update(env)
+    try:
+        dev = ma.Device(path, weights=weights)
+        r = dev.synthesize(toks, speakers=[b % 5 for b in range(len(toks))], trace=True,
+                           max_dec_steps=6, ignore_eos=True)
+        dev.close()
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    rec = np.fromfile(dump, dtype=np.float32).reshape(-1, 2024 + 8 + 4 * 256)
+    return r, rec[:, :2024 + 8 + 2 * 256].view(np.uint32)  # (lty2 / ltq are not outputs of every form)
+
+
+@pytest.mark.parametrize("weights", ["q8", "q4"])
+def test_q8_lt_step_forms_equal(ma, q8_model, q4_model, weights, tmp_path):
+    """The Q8_0 LT step (lt_slot_q8_kernel) in its three forms -- o_net rows split over the
+    workgroups with a y hand-off and the FFN merge in the launch (MAGPIE_LTQ8=0), every
+    workgroup all 256 o_net rows from the transposed copy (1), and at batch 1 the FFN
+    merge deferred to the Q8_0 head's prologue (2, the default) -- give the same bits:
+    every head's logits, the codes, X and y of every LT step, and the decoder hidden."""
+    model = q8_model if weights == "q8" else q4_model
+    toks = [ma.synthetic_tokens(30, seed=8500)]
+    runs = {m: _lt_dump(ma, model, toks, m, tmp_path, weights) for m in (0, 1, 2)}
+    r0, d0 = runs[0]
+    assert d0.shape[0] >= 8 * 5, d0.shape
+    for m in (1, 2):
+        r, d = runs[m]
+        assert d.shape == d0.shape and np.array_equal(d, d0), f"MAGPIE_LTQ8={m}: LT state differs"
+        assert np.array_equal(r.codes[0], r0.codes[0]) and np.array_equal(r.hidden, r0.hidden), m
+    # batched: the split and the all-rows o_net forms (the deferred merge is batch 1 only)
+    toks4 = [ma.synthetic_tokens(30 + 5 * b, seed=8500 + b) for b in range(4)]
+    (ra, da), (rb, db) = (_lt_dump(ma, model, toks4, m, tmp_path, weights) for m in (0, 1))
+    assert np.array_equal(da, db)
+    for b in range(4):
+        assert np.array_equal(ra.codes[b], rb.codes[b]) and np.array_equal(ra.hidden[b], rb.hidden[b]), b
+    # and slot 0 of the batch is the single utterance (batch = single across the forms)
+    assert np.array_equal(ra.codes[0], r0.codes[0]) and np.array_equal(da[:d0.shape[0]], d0)

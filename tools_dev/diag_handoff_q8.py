@@ -55,6 +55,12 @@ def main():
             nxq = 0 if B <= XQ8_QIN_NB else XQG * B  # small batches: q in the attention workgroups
             nrow = len(ids) - nxq - XQ8A * B
             rows, xq, at = ids[:nrow], ids[nrow:nrow + nxq], ids[nrow + nxq:]
+            if nxq == 0:  # small batches: the q-in-attention workgroups' phase stamps (ts_phase 0..3)
+                print(f"iter {it} op {i}: oproj {len(rows)} wg end {rng(rel[rows, :4, 1])} | attn {len(at)} start "
+                      f"{rng(rel[at, :4, 0])} x1 seen {rng(rel[at, 4, 1])} q {rng(rel[at, 5, 1])} "
+                      f"attn {rng(rel[at, 6, 1])} aq {rng(rel[at, 7, 1])} end {rng(rel[at, :4, 1])}")
+                seen = True
+                continue
             print(f"iter {it} op {i}: oproj {len(rows)} wg end {rng(rel[rows, :4, 1])} | xq {len(xq)} "
                   f"start {rng(rel[xq, :4, 0])} x1 seen {rng(rel[xq, 4, 1])} end {rng(rel[xq, 0, 1])} | "
                   f"attn {len(at)} start {rng(rel[at, :4, 0])} attn done {rng(rel[at, 4:, 1])} "

@@ -507,13 +507,19 @@ hipError_t pack_q4(const signed char *q, int N, int K, unsigned char *oq, hipStr
 constexpr int XQ8_ROWS = 64;  // o_net rows per workgroup
 
 // a = softmax_t(q . K_t / sqrt(128)) V  of slot b into a_s[128] (every thread
-// returns after a barrier); pr: per-key scores [TMAX_LIMIT]. The first XA_PF_K
-// rounds of key rows and XA_PF_V rounds of value rows (the first 64 keys) are issued
-// at entry, before q is read: one memory round trip for a text of up to 64 tokens
-// instead of one per round; longer texts load the later rounds in the loops. Each
-// key's score is one half-wave dot and wave w accumulates its keys w, w + 4, ... in
-// ascending order, however the rows arrive.
-constexpr int XA_PF_K = 2, XA_PF_V = 4;  // rounds of 32 / 16 keys
+// returns after a barrier); pr: per-key scores, then weights [TMAX_LIMIT]. getq() makes
+// q readable (whatever hand-off that takes) and returns it (16 B aligned, global or LDS).
+// The first 64 keys' K rows and V rows are issued at entry, before getq: one memory
+// round trip for a text of up to 64 tokens; longer texts load 64 keys per round.
+//  1. scores: key t = 64 c + 16 w + lane / 4 of wave w, 4 lanes per key (32 dims each,
+//     one fmaf chain), the quad summed by two DPP steps (no cross-row exchange);
+//  2. weights: thread t exponentiates key t (one expf per key), sums its keys, the
+//     denominator is the wave sums in wave order;
+//  3. a[d] = sum_t e_t V_t[d] / den: wave w takes keys w, w + 4, ... in ascending order
+//     (lane owns dims lane, 64 + lane), the 4 waves' partials summed in order.
+// Branch-free per key (clamped loads, selects), so the DPP and LDS traffic of a round
+// issues back to back.
+constexpr int XA_PF_V = 4;  // rounds of 16 value rows issued at entry
 template <typename QF>
 __device__ __forceinline__ void xa_text_attention_q(QF getq, const float *Kb, const float *Vb, int Tb, float *pr,
                                                     float *a_s) {
@@ -521,17 +527,11 @@ __device__ __forceinline__ void xa_text_attention_q(QF getq, const float *Kb, co
     __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
     __shared__ float wred[2 * MP_NWAVES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int h = lane >> 5, d4 = 4 * (lane & 31);
-    // pass-1 rounds: keys t0 + 8 u + h, t0 = 2 w + 32 r; pass-2 rounds: keys t0 + 4 u, t0 = w + 16 r
-    float4 kpf[XA_PF_K][4];
+    const int kq = 16 * w + (lane >> 2), dq = 32 * (lane & 3);  // pass 1: key in the round, dims
+    f32x4 kpf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kpf[i] = *(const f32x4 *)(Kb + (size_t)min(kq, Tb - 1) * DXA + dq + 4 * i);
     float v0pf[XA_PF_V][4], v1pf[XA_PF_V][4];
-#pragma unroll
-    for (int r = 0; r < XA_PF_K; ++r)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = min(2 * w + 32 * r + 2 * MP_NWAVES * u + h, Tb - 1);
-            kpf[r][u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
-        }
 #pragma unroll
     for (int r = 0; r < XA_PF_V; ++r)
 #pragma unroll
@@ -540,51 +540,60 @@ __device__ __forceinline__ void xa_text_attention_q(QF getq, const float *Kb, co
             v0pf[r][u] = Vb[(size_t)t * DXA + lane];
             v1pf[r][u] = Vb[(size_t)t * DXA + 64 + lane];
         }
-    const float4 q4 = getq(d4);  // this lane's q[d4 .. d4 + 3]
+    const float *qp = getq();
+    f32x4 q4[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q4[i] = *(const f32x4 *)(qp + dq + 4 * i);
     const float scale = 1.0f / sqrtf((float)DXA);
     float mx = -INFINITY;
-    auto scores = [&](int t0, const float4 (&k4)[4]) {
+    auto score = [&](int t, const f32x4 (&k4)[8]) {
+        float s = 0.f;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = t0 + 2 * MP_NWAVES * u + h;
-            const float sv = group_sum<32>(dotv(q4, k4[u])) * scale;
-            if (t < Tb) {
-                if ((lane & 31) == 0) pr[t] = sv;
-                mx = fmaxf(mx, sv);
-            }
+        for (int i = 0; i < 8; ++i) {
+            s = fmaf(q4[i].x, k4[i].x, s);
+            s = fmaf(q4[i].y, k4[i].y, s);
+            s = fmaf(q4[i].z, k4[i].z, s);
+            s = fmaf(q4[i].w, k4[i].w, s);
         }
+        s += dpp_mov<0xB1>(s);  // (s0 + s1) + (s2 + s3) in every lane of the quad
+        s += dpp_mov<0x4E>(s);
+        const float sv = s * scale;
+        if ((lane & 3) == 0 && t < Tb) pr[t] = sv;
+        mx = fmaxf(mx, t < Tb ? sv : -INFINITY);
     };
+    score(kq, kpf);
+    for (int t0 = 64; t0 < Tb; t0 += 64) {
+        f32x4 k4[8];
 #pragma unroll
-    for (int r = 0; r < XA_PF_K; ++r)
-        if (2 * w + 32 * r < Tb) scores(2 * w + 32 * r, kpf[r]);
-    for (int t0 = 2 * w + 32 * XA_PF_K; t0 < Tb; t0 += 2 * MP_NWAVES * 4) {  // 4 key pairs in flight per wave
-        float4 k4[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = min(t0 + 2 * MP_NWAVES * u + h, Tb - 1);
-            k4[u] = *(const float4 *)(Kb + (size_t)t * DXA + d4);
-        }
-        scores(t0, k4);
+        for (int i = 0; i < 8; ++i) k4[i] = *(const f32x4 *)(Kb + (size_t)min(t0 + kq, Tb - 1) * DXA + dq + 4 * i);
+        score(t0 + kq, k4);
     }
     mx = wave_max(mx);
     if (lane == 0) wred[w] = mx;
     lds_sync();
     const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
+    float l = 0.f;
+    for (int t = tid; t < Tb; t += MP_BLOCK) {
+        const float e = expf(pr[t] - M);
+        pr[t] = e;
+        l += e;
+    }
+    l = wave_sum(l);
+    if (lane == 0) wred[MP_NWAVES + w] = l;
+    lds_sync();
     // o[d] = sum_t e_t V_t[d]: wave w takes keys t = w + 4 u, lane owns dims lane, 64 + lane
-    float l = 0.f, o0 = 0.f, o1 = 0.f;
+    float o0 = 0.f, o1 = 0.f;
     auto accum = [&](int t0, const float (&v0)[4], const float (&v1)[4]) {
-        float e[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int t = min(t0 + MP_NWAVES * u, Tb - 1);
-            e[u] = t0 + MP_NWAVES * u < Tb ? expf(pr[t] - M) : 0.f;
+            const int t = t0 + MP_NWAVES * u;
+            const float e = t < Tb ? pr[min(t, Tb - 1)] : 0.f;
+            o0 = fmaf(e, v0[u], o0);
+            o1 = fmaf(e, v1[u], o1);
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { l += e[u]; o0 = fmaf(e[u], v0[u], o0); o1 = fmaf(e[u], v1[u], o1); }
     };
 #pragma unroll
-    for (int r = 0; r < XA_PF_V; ++r)
-        if (w + 16 * r < Tb) accum(w + 16 * r, v0pf[r], v1pf[r]);
+    for (int r = 0; r < XA_PF_V; ++r) accum(w + 16 * r, v0pf[r], v1pf[r]);
     for (int t0 = w + 16 * XA_PF_V; t0 < Tb; t0 += MP_NWAVES * 4) {
         float v0[4], v1[4];
 #pragma unroll
@@ -597,7 +606,6 @@ __device__ __forceinline__ void xa_text_attention_q(QF getq, const float *Kb, co
     }
     pv[w][lane] = o0;
     pv[w][64 + lane] = o1;
-    if (lane == 0) wred[MP_NWAVES + w] = l;
     lds_sync();
     if (tid < DXA) {
         const float den = ((wred[4] + wred[5]) + wred[6]) + wred[7];
@@ -608,7 +616,7 @@ __device__ __forceinline__ void xa_text_attention_q(QF getq, const float *Kb, co
 
 __device__ __forceinline__ void xa_text_attention(const float *q, const float *Kb, const float *Vb, int Tb,
                                                   float *pr, float *a_s) {
-    xa_text_attention_q([&](int d4) { return *(const float4 *)(q + d4); }, Kb, Vb, Tb, pr, a_s);
+    xa_text_attention_q([&]() { return q; }, Kb, Vb, Tb, pr, a_s);
 }
 
 // a (LDS, [128]) -> Q8_0 blocks aq / ad (ggml quantises the o_net operand), wave 0
@@ -871,10 +879,10 @@ __device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_s
     };
     const size_t kv = ((size_t)(b * x.nlayers + x.layer) * x.Tmax) * DXA;
     xa_text_attention_q(
-        [&](int d4) {
+        [&]() {
             sweep((gu64 *)(x.qg + (size_t)b * DXA), qrow[w], DXA);
             wave_lds_sync();
-            return *(const float4 *)&qrow[w][d4];
+            return (const float *)qrow[w];
         },
         x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
     ts_mark(p.ts, t_start);  // profiling: attention done
@@ -920,7 +928,7 @@ __device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed ch
     load_lnw<PER>(x.lnw, g);
     const size_t kv = ((size_t)(b * x.nlayers + x.layer) * x.Tmax) * DXA;
     xa_text_attention_q(
-        [&](int d4) {
+        [&]() {
             float v[PER];
             xq8_sweep_x1(p, b, v);
             ts_phase<0>(p.ts, t_start);  // profiling: x1 seen
@@ -938,7 +946,7 @@ __device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed ch
             }
             lds_sync();
             ts_phase<1>(p.ts, t_start);  // profiling: q done
-            return *(const float4 *)&qs[d4];
+            return (const float *)qs;
         },
         x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
     ts_phase<2>(p.ts, t_start);  // profiling: attention done

@@ -727,6 +727,36 @@ __device__ __forceinline__ void xq8_sweep_x1(const GemvP &p, int b, float (&v)[D
         __builtin_amdgcn_s_sleep(1);
     }
 }
+// x1 of slot b into dst[768] (LDS), wave w sweeping its quarter (3 granules per lane) and
+// storing it; the caller's barrier publishes the row. One poller per granule: when every
+// wave polled the whole row, the barrier after it waited for the unluckiest wave's next
+// round trip (~1 us) after the row was complete.
+__device__ __forceinline__ void xq8_sweep_x1_quarter(const GemvP &p, int b, float *dst) {
+    constexpr int PQ = D / 64 / MP_NWAVES;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+    gu64 *gr = (gu64 *)(p.xh + (size_t)b * D) + w * PQ * 64;
+    float v[PQ];
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < PQ; ++j) {
+            const unsigned long long u = __hip_atomic_load(gr + lane + 64 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[j] = __uint_as_float((unsigned)u);
+            ok &= (unsigned)(u >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+            if (lane == 0) __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int j = 0; j < PQ; ++j) v[j] = __builtin_nanf("");
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int j = 0; j < PQ; ++j) dst[w * PQ * 64 + lane + 64 * j] = v[j];
+}
 // LN(x1) * lnw (PRO_LN at batch 1: every wave the whole row, wave w stores its quarter),
 // then the row's Q8_0 blocks (gemm_q8_kernel_dec's quantiser) into actq / actd
 __device__ __forceinline__ void xq8_ln_quant(const XaQ8P &x, const float (&v)[D / 64], const float (&g)[D / 64],
@@ -930,7 +960,10 @@ __device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed ch
     xa_text_attention_q(
         [&]() {
             float v[PER];
-            xq8_sweep_x1(p, b, v);
+            xq8_sweep_x1_quarter(p, b, pr);  // (pr is free until the scores)
+            lds_sync();
+#pragma unroll
+            for (int j = 0; j < PER; ++j) v[j] = pr[lane + 64 * j];
             ts_phase<0>(p.ts, t_start);  // profiling: x1 seen
             if (w == 0) {  // the residual rows of this workgroup's o_net
                 float xr = v[0];
@@ -939,19 +972,19 @@ __device__ __forceinline__ void xq8qa_tail(const GemvP &p, float *act, signed ch
                 x1s[lane] = xr;
             }
             xq8_ln_quant(x, v, g, act, actq, actd);
+            ts_phase<1>(p.ts, t_start);  // profiling: LN + quantised
 #pragma unroll
             for (int j = 0; j < QR; ++j) {
                 const float qv = xq8_dot(wq[j], wqs[j], qa, actq, actd);
                 if (qa == 0) qs[16 * w + 64 * j + (lane >> 2)] = qv;
             }
             lds_sync();
-            ts_phase<1>(p.ts, t_start);  // profiling: q done
+            ts_phase<2>(p.ts, t_start);  // profiling: q done
             return (const float *)qs;
         },
         x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
-    ts_phase<2>(p.ts, t_start);  // profiling: attention done
+    ts_phase<3>(p.ts, t_start);  // profiling: attention done
     xa_quantize_a(a_s, aq, ad);
-    ts_phase<3>(p.ts, t_start);  // profiling: a quantised
     xa_q8_onet<OG>(wo, wos, r0, aq, ad, x1s - rb * XQ8_ROWS, x.x2 + (size_t)b * D);
     ts_end(p.ts, t_start);
 }

@@ -57,8 +57,8 @@ def main():
             rows, xq, at = ids[:nrow], ids[nrow:nrow + nxq], ids[nrow + nxq:]
             if nxq == 0:  # small batches: the q-in-attention workgroups' phase stamps (ts_phase 0..3)
                 print(f"iter {it} op {i}: oproj {len(rows)} wg end {rng(rel[rows, :4, 1])} | attn {len(at)} start "
-                      f"{rng(rel[at, :4, 0])} x1 seen {rng(rel[at, 4, 1])} q {rng(rel[at, 5, 1])} "
-                      f"attn {rng(rel[at, 6, 1])} aq {rng(rel[at, 7, 1])} end {rng(rel[at, :4, 1])}")
+                      f"{rng(rel[at, :4, 0])} x1 seen {rng(rel[at, 4, 1])} ln+quant {rng(rel[at, 5, 1])} "
+                      f"q {rng(rel[at, 6, 1])} attn {rng(rel[at, 7, 1])} end {rng(rel[at, :4, 1])}")
                 seen = True
                 continue
             print(f"iter {it} op {i}: oproj {len(rows)} wg end {rng(rel[rows, :4, 1])} | xq {len(xq)} "

@@ -35,7 +35,7 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
 #pragma clang fp contract(off)
     __shared__ float wm[NW], wl[NW];
     __shared__ __attribute__((aligned(16))) float wo[NW][DH];
-    __shared__ __attribute__((aligned(16))) float wq[HANDOFF ? NW : 1][3 * DH];
+    __shared__ __attribute__((aligned(16))) float wq[1][3 * DH];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kk = lane >> 4, dc = lane & 15;
     const size_t base = ((size_t)(b * p.nlayers + p.layer) * p.max_seq) * D + h * DH + 4 * dc + dep;
@@ -54,40 +54,35 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
     }
     float4 q4, kn4 = make_float4(0.f, 0.f, 0.f, 0.f), vn4 = kn4;
     if constexpr (HANDOFF) {
-        const bool has_new = j0 <= jn && jn < j1;  // wave-uniform
-        gu64 *g = (gu64 *)const_cast<unsigned long long *>(qh) + (size_t)b * 3 * D + h * DH + lane;
-        float qv = 0.f, kv = 0.f, vv = 0.f;
-        for (unsigned spins = 0;; ++spins) {
-            const unsigned long long uq = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bool ok = (unsigned)(uq >> 32) == tag;
-            qv = __uint_as_float((unsigned)uq);
-            if (has_new) {
-                const unsigned long long uk = __hip_atomic_load(g + D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long uv = __hip_atomic_load(g + 2 * D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok &= (unsigned)(uk >> 32) == tag && (unsigned)(uv >> 32) == tag;
-                kv = __uint_as_float((unsigned)uk);
-                vv = __uint_as_float((unsigned)uv);
+        // one poller per array: wave 0 sweeps q, waves 1 and 2 the new key's k and v (when
+        // this split holds it), then the workgroup barrier publishes them (every wave
+        // polling all three made the merge barrier wait for the unluckiest wave's next
+        // round trip after the granules were complete)
+        const bool has_new = j0 <= jn && jn < j1;  // workgroup-uniform
+        if (w < (has_new ? 3 : 1)) {
+            gu64 *g = (gu64 *)const_cast<unsigned long long *>(qh) + (size_t)b * 3 * D + w * D + h * DH + lane;
+            float val;
+            for (unsigned spins = 0;; ++spins) {
+                const unsigned long long u = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                val = __uint_as_float((unsigned)u);
+                if (__all((unsigned)(u >> 32) == tag)) break;
+                if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
+                    if (lane == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_SA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    val = __builtin_nanf("");
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
-            if (__all(ok)) break;
-            if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
-                if (lane == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_SA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                qv = kv = vv = __builtin_nanf("");
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+            if constexpr (KV16)  // the new row as the cache holds it (kv_store's rounding)
+                if (w > 0) val = __uint_as_float((unsigned)f32_to_bf16_rne(val) << 16);
+            wq[0][w * DH + lane] = val;
         }
-        if constexpr (KV16) {  // the new row as the cache holds it (kv_store's rounding)
-            kv = __uint_as_float((unsigned)f32_to_bf16_rne(kv) << 16);
-            vv = __uint_as_float((unsigned)f32_to_bf16_rne(vv) << 16);
+        lds_sync();
+        q4 = *(const float4 *)&wq[0][4 * dc];
+        if (has_new) {
+            kn4 = *(const float4 *)&wq[0][DH + 4 * dc];
+            vn4 = *(const float4 *)&wq[0][2 * DH + 4 * dc];
         }
-        // to the float4 layout through this wave's own LDS row
-        wq[w][lane] = qv;
-        wq[w][DH + lane] = kv;
-        wq[w][2 * DH + lane] = vv;
-        wave_lds_sync();
-        q4 = *(const float4 *)&wq[w][4 * dc];
-        kn4 = *(const float4 *)&wq[w][DH + 4 * dc];
-        vn4 = *(const float4 *)&wq[w][2 * DH + 4 * dc];
     } else {
         q4 = *(const float4 *)(p.q + (size_t)b * D + h * DH + 4 * dc);
     }

@@ -91,6 +91,7 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
                                         int dep, unsigned long long *ts = nullptr, unsigned long long t_start = 0) {
     __shared__ float wm[XA_WAVES], wl[XA_WAVES];
     __shared__ __attribute__((aligned(16))) float wo[XA_WAVES][D];
+    __shared__ __attribute__((aligned(16))) float x1row[HANDOFF ? D : 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int Tb = p.T[b];
     const int chunk = (Tb + XA_SPLITS - 1) / XA_SPLITS;
@@ -114,12 +115,18 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
 #pragma unroll
         for (int i = 0; i < XA_V; ++i) g4[i] = *(const float4 *)(p.lnw + 4 * lane + 256 * i);
         if constexpr (HANDOFF) {
-            gu64 *g = (gu64 *)(xh + (size_t)b * D);
-            float xv[D / 64];
+            // wave w sweeps its quarter of x1 (3 granules per lane) into the shared row, the
+            // workgroup barrier publishes it (one poller per granule: with every wave
+            // polling the whole row, the merge barrier waited for the unluckiest wave's
+            // next round trip after x1 was complete)
+            constexpr int PQ = D / 64 / XA_WAVES;
+            static_assert(PQ * XA_WAVES * 64 == D, "x1 splits into one quarter per wave");
+            gu64 *g = (gu64 *)(xh + (size_t)b * D) + w * PQ * 64;
+            float xv[PQ];
             for (unsigned spins = 0;; ++spins) {
                 bool ok = true;
 #pragma unroll
-                for (int j = 0; j < D / 64; ++j) {
+                for (int j = 0; j < PQ; ++j) {
                     const unsigned long long u = __hip_atomic_load(g + lane + 64 * j, __ATOMIC_RELAXED,
                                                                    __HIP_MEMORY_SCOPE_AGENT);
                     xv[j] = __uint_as_float((unsigned)u);
@@ -129,18 +136,17 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
                 if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
                     if (lane == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-                    for (int j = 0; j < D / 64; ++j) xv[j] = __builtin_nanf("");
+                    for (int j = 0; j < PQ; ++j) xv[j] = __builtin_nanf("");
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            ts_mark(ts, t_start);  // profiling: when this wave saw all of x1
-            // to the float4 layout through this wave's own LDS row (reused for o below)
 #pragma unroll
-            for (int j = 0; j < D / 64; ++j) wo[w][lane + 64 * j] = xv[j];
-            wave_lds_sync();
+            for (int j = 0; j < PQ; ++j) x1row[w * PQ * 64 + lane + 64 * j] = xv[j];
+            lds_sync();
+            ts_mark(ts, t_start);  // profiling: when the workgroup saw all of x1
 #pragma unroll
-            for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)&wo[w][4 * lane + 256 * i];
+            for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)&x1row[4 * lane + 256 * i];
         } else {
 #pragma unroll
             for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)(p.x + (size_t)b * D + 4 * lane + 256 * i);

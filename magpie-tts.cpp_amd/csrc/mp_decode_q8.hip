@@ -703,30 +703,6 @@ __device__ __forceinline__ void xq8_load_rows(const XaQ8P &x, int qr, int qa, in
 #pragma unroll
     for (int j = 0; j < XQ_QB; ++j) wqs[j] = x.wqd[(size_t)qr * (D / 32) + qa * XQ_QB + j];
 }
-// x1 of slot b from the O-projection workgroups' granules (every wave sweeps the row)
-__device__ __forceinline__ void xq8_sweep_x1(const GemvP &p, int b, float (&v)[D / 64]) {
-    constexpr int PER = D / 64;
-    const int lane = threadIdx.x & 63;
-    const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
-    gu64 *gr = (gu64 *)(p.xh + (size_t)b * D);
-    for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const unsigned long long u = __hip_atomic_load(gr + lane + 64 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v[j] = __uint_as_float((unsigned)u);
-            ok &= (unsigned)(u >> 32) == tag;
-        }
-        if (__all(ok)) break;
-        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison the output and say so
-            if (lane == 0) __hip_atomic_fetch_or((gi32 *)p.hx_err, HX_ERR_XA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int j = 0; j < PER; ++j) v[j] = __builtin_nanf("");
-            break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
 // x1 of slot b into dst[768] (LDS), wave w sweeping its quarter (3 granules per lane) and
 // storing it; the caller's barrier publishes the row. One poller per granule: when every
 // wave polled the whole row, the barrier after it waited for the unluckiest wave's next
@@ -840,8 +816,12 @@ __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char
     constexpr int PER = D / 64;
     float g[PER];
     load_lnw<PER>(x.lnw, g);
+    __shared__ float x1row[D];
+    xq8_sweep_x1_quarter(p, b, x1row);
+    lds_sync();
     float v[PER];
-    xq8_sweep_x1(p, b, v);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) v[j] = x1row[lane + 64 * j];
     ts_mark(p.ts, t_start);  // profiling: x1 seen
     xq8_ln_quant(x, v, g, act, actq, actd);
     if (w != 0) return;
@@ -856,8 +836,8 @@ __device__ __forceinline__ void xq8_tail(const GemvP &p, float *act, signed char
 
 // The attention + o_net stage of the same launch (the launch's last XQ8A x NB
 // workgroups, XQ8_ROWS o_net rows each): o_net rows and the first 64 text keys and
-// values issued at entry, q swept from the q_net tail's granules (each wave the 128,
-// through its own LDS row into the float4 layout), then xa_q8_kernel's arithmetic:
+// values issued at entry, q swept from the q_net tail's granules (waves 0 and 1 a half
+// each, into one LDS row), then xa_q8_kernel's arithmetic:
 // the attention, a quantised to Q8_0, x2 = x1 + o_net a for its rows (x1 from the
 // O-projection's granules).
 constexpr int XQ8A = D / XQ8_ROWS;
@@ -868,7 +848,7 @@ __device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_s
     __shared__ __attribute__((aligned(16))) float a_s[DXA];
     __shared__ __attribute__((aligned(16))) signed char aq[DXA];
     __shared__ float ad[DXA / 32];
-    __shared__ __attribute__((aligned(16))) float qrow[MP_NWAVES][DXA];
+    __shared__ __attribute__((aligned(16))) float qrow[DXA];
     __shared__ float x1s[XQ8_ROWS];
     const int k = blockIdx.x - p.nrow_blocks - XQG * p.nslots, b = k / XQ8A, rb = k % XQ8A;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -909,10 +889,10 @@ __device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_s
     };
     const size_t kv = ((size_t)(b * x.nlayers + x.layer) * x.Tmax) * DXA;
     xa_text_attention_q(
-        [&]() {
-            sweep((gu64 *)(x.qg + (size_t)b * DXA), qrow[w], DXA);
-            wave_lds_sync();
-            return (const float *)qrow[w];
+        [&]() {  // waves 0 and 1 sweep a half of q each (one poller per granule)
+            if (w < 2) sweep((gu64 *)(x.qg + (size_t)b * DXA) + 64 * w, qrow + 64 * w, 64);
+            lds_sync();
+            return (const float *)qrow;
         },
         x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
     ts_mark(p.ts, t_start);  // profiling: attention done

@@ -878,12 +878,14 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
     }
     // ---- X_0 = s + lt_pos[0], LN(X_0) (PRO_LTX_LN's one-wave statistics): wave 0
     if (w == 0) {
-        float g[4], X[4];
+        float g[4], X[4], sv[4];
         load_lnw<4>(p.norm_self, g);
+        gh_wait_n<4, 64>(p.gh + lane, tag_s, sv, p.hx_err);  // in_proj outputs lane + 64 i
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = lane + 64 * i;
-            X[i] = gh_wait(p.gh + k, tag_s, p.hx_err) + p.lt_pos[k];
+            xs[k] = sv[i];  // kept for the FFN step below (xs is free until then)
+            X[i] = sv[i] + p.lt_pos[k];
         }
         if (pb == 0)
 #pragma unroll
@@ -912,11 +914,12 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
     // ---- codebook 0's FFN step (lt_ffn2_kernel<1>: y = X_0 + vo_0, wave 0)
     if (w == 0) {
         float xv[4], vv[4];
+        gh_wait_n<4, 1>(p.gh + LTD + 4 * lane, tag_v, vv, p.hx_err);  // vo_0 outputs 4 lane + c
+        wave_lds_sync();  // (xs: the in_proj outputs this wave stored above)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int k = 4 * lane + c;
-            xv[c] = gh_wait(p.gh + k, tag_s, p.hx_err) + p.lt_pos[k];
-            vv[c] = gh_wait(p.gh + LTD + k, tag_v, p.hx_err);
+            xv[c] = xs[k] + p.lt_pos[k];
         }
         const float4 y = make_float4(xv[0] + vv[0], xv[1] + vv[1], xv[2] + vv[2], xv[3] + vv[3]);
         if (pb == 0) *(float4 *)((float *)p.l.f.y + 4 * lane) = y;

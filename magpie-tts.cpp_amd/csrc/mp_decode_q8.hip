@@ -369,8 +369,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
             const float4 y4 = *(const float4 *)&ys[4 * lane];
             yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
         } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) yv[c] = gh_wait(p.gy + (size_t)b * LTD + 4 * lane + c, tag_y, p.hx_err);
+            gh_wait_n<4, 1>(p.gy + (size_t)b * LTD + 4 * lane, tag_y, yv, p.hx_err);
             *(float4 *)&ys[4 * lane] = make_float4(yv[0], yv[1], yv[2], yv[3]);
         }
         ts_mark(p.ts, t_start);  // profiling: y seen

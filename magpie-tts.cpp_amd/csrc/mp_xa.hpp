@@ -42,6 +42,30 @@ __device__ __forceinline__ float gh_wait(const unsigned long long *g, unsigned t
         __builtin_amdgcn_s_sleep(1);
     }
 }
+// N granules per lane (g[STRIDE j], j < N) polled together: one memory round trip per
+// poll for all of them (N gh_wait calls in a row cost N round trips even when every
+// granule is already there)
+template <int N, int STRIDE>
+__device__ __forceinline__ void gh_wait_n(const unsigned long long *g, unsigned tag, float (&v)[N], int *err) {
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const unsigned long long u = __hip_atomic_load((const gu64 *)g + STRIDE * j, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            v[j] = __uint_as_float((unsigned)u);
+            ok &= (unsigned)(u >> 32) == tag;
+        }
+        if (__all(ok)) return;
+        if (spins >= HX_SPIN_LIMIT) {  // never seen: poison and say so (HX_ERR_LT: the LT's edges use it)
+            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gi32 *)err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int j = 0; j < N; ++j) v[j] = __builtin_nanf("");
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
 // One round of the XA online softmax: keys tb + XA_WAVES u (u < XA_KPW; those >= t1
 // are masked), K' rows k[u], V' rows vv[u], query h (this lane's elements).
 // score_u = wave_sum(fmaf chain of k . h over the lane's elements) * scale; one

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
 }
 
 // ---------------------------------------------------------------- LT step, Q8_0 mode
-// LtSlotQ8P (mp_params.hpp). Workgroup (q, b), LTQ_P per slot at every batch size.
+// LtSlotQ8P (mp_params.hpp). Workgroup (q, b), WP per slot (below).
 // RED (p.wot set): every workgroup computes all 256 o_net rows itself (thread t row t,
 // from the transposed copy: 16 coalesced 16-byte loads, L2-resident after the first
 // workgroup), so y needs no hand-off. DEFER (p.part set, batch 1): the partial FFN-down
@@ -216,20 +216,26 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
 // same p-ascending sum, then + y), so the launch has no hand-off at all. Every variant
 // computes the same bits: the o_net row is the block-ordered sum of (int dot) x (d_w d_a)
 // from 0, the merge sums the LTQ_P partials in ascending p, then adds y.
-constexpr int LTQ_U = LTF / LTQ_P, LTQ_UPW = LTQ_U / MP_NWAVES, LTQ_R = LTD / LTQ_P, LTQ_RW = LTQ_R / MP_NWAVES;
+// WP workgroups per slot (64, or 32 from 8 slots: 512 instead of 1024 workgroups at 16),
+// each computing LTQ_P / WP of the LTQ_P partial sums (16 hidden units each), so the
+// partials, their order and the merge are the same for every WP.
+constexpr int LTQ_U = LTF / LTQ_P;  // hidden units per partial sum
 static_assert(LTQ_P == LT_FFN_P, "the deferred merge is the head's PRO_LTFFN_MERGE prologue");
-template <bool RED, bool DEFER>
+template <bool RED, bool DEFER, int WP>
 __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
 #pragma clang fp contract(off)
     const unsigned long long t_start = ts_begin(p.ts);
-    static_assert(LTD == MP_BLOCK && LTQ_RW >= 1 && LTQ_RW * MP_NWAVES * LTQ_P == LTD && LTQ_U % 4 == 0, "split");
+    constexpr int PPW = LTQ_P / WP, UW = LTF / WP, UWW = UW / MP_NWAVES, RWG = LTD / WP, RWW = RWG / MP_NWAVES;
+    constexpr int NPT = LTQ_P * RWG / MP_BLOCK;  // merge: partial granules per thread
+    static_assert(LTD == MP_BLOCK && RWW >= 1 && RWW * MP_NWAVES * WP == LTD && PPW * WP == LTQ_P && LTQ_U % 4 == 0 &&
+                      NPT * MP_BLOCK == LTQ_P * RWG, "split");
     static_assert(RED || !DEFER, "the deferred merge needs y in every workgroup");
     __shared__ __attribute__((aligned(16))) float xs[LTD];   // X (the attention residual), then LN(y)
     __shared__ __attribute__((aligned(16))) float ys[LTD];
     __shared__ __attribute__((aligned(16))) int aq[LTD / 4];  // the attention output as Q8_0 (4 int8 per lane)
     __shared__ float ad[LTD / 32];
-    __shared__ __attribute__((aligned(16))) float fs[LTQ_U];
-    __shared__ float mv[LTQ_P][LTQ_R];
+    __shared__ __attribute__((aligned(16))) float fs[UW];
+    __shared__ float mv[LTQ_P][RWG];
     __shared__ __attribute__((aligned(16))) float wsc[2 * VCB];
     const GemvP &g = p.g;
     const int q = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, cb = g.cb;
@@ -252,9 +258,9 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
             x4 = *(const float4 *)(g.ltX + (size_t)b * LTD + 4 * lane);
         }
     }
-    const int r0 = q * LTQ_R + LTQ_RW * w + dep;
-    int wq[LTQ_RW];
-    float wd[LTQ_RW];
+    const int r0 = q * RWG + RWW * w + dep;
+    int wq[RWW];
+    float wd[RWW];
     intx4 wr[RED ? LTD / 16 : 1];  // RED: row tid's 256 int8 (16 B per load, wot[i][tid])
     intx4 wrd;                     // RED: row tid's 8 fp16 block scales
     if constexpr (RED) {
@@ -263,17 +269,20 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
         wrd = *(const intx4 *)(p.wod + (size_t)tid * (LTD / 32));
     } else {
 #pragma unroll
-        for (int r = 0; r < LTQ_RW; ++r) {
+        for (int r = 0; r < RWW; ++r) {
             wq[r] = *(const int *)(p.woq + (size_t)(r0 + r) * LTD + 4 * lane);
             wd[r] = __half2float(__ushort_as_half(p.wod[(size_t)(r0 + r) * (LTD / 32) + (lane >> 3)]));
         }
     }
-    const int u0 = q * LTQ_U;
-    float4 a1[LTQ_UPW], a2[LTQ_U / 4];
+    const int u0 = q * UW;
+    float4 a1[UWW], a2[PPW][LTQ_U / 4];
 #pragma unroll
-    for (int r = 0; r < LTQ_UPW; ++r) a1[r] = *(const float4 *)(p.w1 + (size_t)(u0 + w * LTQ_UPW + r) * LTD + 4 * lane);
+    for (int r = 0; r < UWW; ++r) a1[r] = *(const float4 *)(p.w1 + (size_t)(u0 + w * UWW + r) * LTD + 4 * lane);
 #pragma unroll
-    for (int i = 0; i < LTQ_U / 4; ++i) a2[i] = *(const float4 *)(p.w2s + ((size_t)q * LTD + tid) * LTQ_U + 4 * i);
+    for (int k = 0; k < PPW; ++k)
+#pragma unroll
+        for (int i = 0; i < LTQ_U / 4; ++i)
+            a2[k][i] = *(const float4 *)(p.w2s + ((size_t)(q * PPW + k) * LTD + tid) * LTQ_U + 4 * i);
     // per codebook step its own tags (8 steps share the buffers within one frame)
     const unsigned tag_y = (unsigned)p.iter[0] * 64u + 32u + (unsigned)cb, tag_p = tag_y + 16u;
     if (w == 0) {
@@ -341,9 +350,9 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
         lds_sync();
     } else {
         const int av = aq[lane];
-        float o[LTQ_RW];
+        float o[RWW];
 #pragma unroll
-        for (int r = 0; r < LTQ_RW; ++r) {
+        for (int r = 0; r < RWW; ++r) {
             int is = __builtin_amdgcn_sdot4(wq[r], av, 0, false);
             is += __shfl_xor(is, 1, 64);
             is += __shfl_xor(is, 2, 64);
@@ -354,9 +363,12 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
             for (int kb = 0; kb < LTD / 32; ++kb) acc += __shfl(fb, 8 * kb, 64);
             o[r] = acc;
         }
-        if (lane < LTQ_RW) {
+        if (lane < RWW) {
             const int n = r0 + lane;
-            const float yv = (lane == 0 ? o[0] : o[LTQ_RW - 1]) + xs[n];
+            float ov = o[0];
+#pragma unroll
+            for (int r = 1; r < RWW; ++r) ov = lane == r ? o[r] : ov;
+            const float yv = ov + xs[n];
             __hip_atomic_store((gu64 *)p.gy + (size_t)b * LTD + n, ((unsigned long long)tag_y << 32) | __float_as_uint(yv),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             p.y[(size_t)b * LTD + n] = yv;
@@ -384,38 +396,50 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
     {
         const float4 xv = *(const float4 *)&xs[4 * lane];
 #pragma unroll
-        for (int r = 0; r < LTQ_UPW; ++r) {
+        for (int r = 0; r < UWW; ++r) {
             const float v = wave_sum(dotv(a1[r], xv));
-            if (lane == 0) fs[w * LTQ_UPW + r] = gelu_tanh(v);
+            if (lane == 0) fs[w * UWW + r] = gelu_tanh(v);
         }
     }
     lds_sync();
-    float acc = 0.f;
+    float acc[PPW];
 #pragma unroll
-    for (int i = 0; i < LTQ_U / 4; ++i) {
-        const float4 f4 = *(const float4 *)&fs[4 * i];
-        acc = fmaf(a2[i].x, f4.x, acc);
-        acc = fmaf(a2[i].y, f4.y, acc);
-        acc = fmaf(a2[i].z, f4.z, acc);
-        acc = fmaf(a2[i].w, f4.w, acc);
+    for (int k = 0; k < PPW; ++k) {
+        acc[k] = 0.f;
+#pragma unroll
+        for (int i = 0; i < LTQ_U / 4; ++i) {
+            const float4 f4 = *(const float4 *)&fs[k * LTQ_U + 4 * i];
+            acc[k] = fmaf(a2[k][i].x, f4.x, acc[k]);
+            acc[k] = fmaf(a2[k][i].y, f4.y, acc[k]);
+            acc[k] = fmaf(a2[k][i].z, f4.z, acc[k]);
+            acc[k] = fmaf(a2[k][i].w, f4.w, acc[k]);
+        }
     }
     if constexpr (DEFER) {  // the head's prologue merges (PRO_LTFFN_MERGE)
-        p.part[((size_t)b * LTQ_P + q) * LTD + tid] = acc;
+#pragma unroll
+        for (int k = 0; k < PPW; ++k) p.part[((size_t)b * LTQ_P + q * PPW + k) * LTD + tid] = acc[k];
         ts_end(p.ts, t_start);
         return;
     }
-    // partial sums through granules; this workgroup merges its LTQ_R outputs in q order
+    // partial sums through granules; this workgroup merges its RWG outputs in partial order
     gu64 *gp = (gu64 *)p.gp + (size_t)b * LTQ_P * LTD;
-    __hip_atomic_store(gp + (size_t)q * LTD + tid, ((unsigned long long)tag_p << 32) | __float_as_uint(acc),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mv[tid / LTQ_R][tid % LTQ_R] = gh_wait(p.gp + (size_t)b * LTQ_P * LTD + (size_t)(tid / LTQ_R) * LTD + LTQ_R * q + tid % LTQ_R,
-                                           tag_p, p.hx_err);
+#pragma unroll
+    for (int k = 0; k < PPW; ++k)
+        __hip_atomic_store(gp + (size_t)(q * PPW + k) * LTD + tid, ((unsigned long long)tag_p << 32) | __float_as_uint(acc[k]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    {   // thread t: partials t / RWG + (256 / RWG) i of output RWG q + t % RWG, one round trip per poll
+        float mvv[NPT];
+        gh_wait_n<NPT, (MP_BLOCK / RWG) * LTD>(p.gp + (size_t)b * LTQ_P * LTD + (size_t)(tid / RWG) * LTD + RWG * q + tid % RWG,
+                                               tag_p, mvv, p.hx_err);
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) mv[tid / RWG + (MP_BLOCK / RWG) * i][tid % RWG] = mvv[i];
+    }
     lds_sync();
-    if (tid < LTQ_R) {
+    if (tid < RWG) {
         float s = mv[0][tid];
 #pragma unroll 8
         for (int k = 1; k < LTQ_P; ++k) s += mv[k][tid];
-        p.y2[(size_t)b * LTD + LTQ_R * q + tid] = s + ys[LTQ_R * q + tid];
+        p.y2[(size_t)b * LTD + RWG * q + tid] = s + ys[RWG * q + tid];
     }
     ts_end(p.ts, t_start);
 }
@@ -427,9 +451,10 @@ hipError_t op_lt_slot_q8(const LtSlotQ8P &p, int NB, hipStream_t s) {
         (g.cb > 0 && (!g.logits || !g.codes_cur || !g.qkvtab || !g.ptab || !g.lt_pos || !g.step || !g.smp.cfg ||
                       !g.smp.argeos)))
         return hipErrorInvalidValue;
-    if (p.part) mp::launch(lt_slot_q8_kernel<true, true>, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
-    else if (p.wot) mp::launch(lt_slot_q8_kernel<true, false>, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
-    else mp::launch(lt_slot_q8_kernel<false, false>, dim3(LTQ_P, NB), dim3(MP_BLOCK), 0, s, p);
+    if (p.part) mp::launch(lt_slot_q8_kernel<true, true, 64>, dim3(64, NB), dim3(MP_BLOCK), 0, s, p);
+    else if (p.wot) mp::launch(lt_slot_q8_kernel<true, false, 64>, dim3(64, NB), dim3(MP_BLOCK), 0, s, p);
+    else if (NB >= 8) mp::launch(lt_slot_q8_kernel<false, false, 32>, dim3(32, NB), dim3(MP_BLOCK), 0, s, p);
+    else mp::launch(lt_slot_q8_kernel<false, false, 64>, dim3(64, NB), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 

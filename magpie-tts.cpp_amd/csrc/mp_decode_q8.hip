@@ -912,15 +912,23 @@ __device__ __forceinline__ void xq8a_tail(const GemvP &p, unsigned long long t_s
             if (lane + 64 * j < n) dst[lane + 64 * j] = v[j];
     };
     const size_t kv = ((size_t)(b * x.nlayers + x.layer) * x.Tmax) * DXA;
+    unsigned long long x1u = 0;
     xa_text_attention_q(
         [&]() {  // waves 0 and 1 sweep a half of q each (one poller per granule)
             if (w < 2) sweep((gu64 *)(x.qg + (size_t)b * DXA) + 64 * w, qrow + 64 * w, 64);
             lds_sync();
+            // q is complete, so x1 is (q_net read all of it): wave 0's residual rows issued
+            // now, used after the attention
+            if (w == 0) x1u = __hip_atomic_load((gu64 *)(p.xh + (size_t)b * D + rb * XQ8_ROWS) + lane, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
             return (const float *)qrow;
         },
         x.xak + kv, x.xav + kv, x.T[b], pr, a_s);
     ts_mark(p.ts, t_start);  // profiling: attention done
-    if (w == 0) sweep((gu64 *)(p.xh + (size_t)b * D + rb * XQ8_ROWS), x1s, XQ8_ROWS);
+    if (w == 0) {
+        if (__all((unsigned)(x1u >> 32) == tag)) x1s[lane] = __uint_as_float((unsigned)x1u);
+        else sweep((gu64 *)(p.xh + (size_t)b * D + rb * XQ8_ROWS), x1s, XQ8_ROWS);  // (never taken)
+    }
     xa_quantize_a(a_s, aq, ad);  // (its barrier also publishes x1s)
     xa_q8_onet<OG>(wo, wos, r0, aq, ad, x1s - rb * XQ8_ROWS, x.x2 + (size_t)b * D);
     ts_end(p.ts, t_start);

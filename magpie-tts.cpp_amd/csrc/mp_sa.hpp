@@ -31,7 +31,8 @@ __device__ __forceinline__ float sa_dot(float4 q, float4 k) {
 }
 template <bool KV16, int NW, bool HANDOFF>
 __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, const unsigned long long *qh,
-                                        unsigned tag, int *err, int dep) {
+                                        unsigned tag, int *err, int dep, unsigned long long *ts = nullptr,
+                                        unsigned long long t_start = 0) {
 #pragma clang fp contract(off)
     __shared__ float wm[NW], wl[NW];
     __shared__ __attribute__((aligned(16))) float wo[NW][DH];
@@ -78,6 +79,7 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
             wq[0][w * DH + lane] = val;
         }
         lds_sync();
+        ts_phase<0>(ts, t_start);  // profiling: q (and the new key) seen
         q4 = *(const float4 *)&wq[0][4 * dc];
         if (has_new) {
             kn4 = *(const float4 *)&wq[0][DH + 4 * dc];
@@ -121,6 +123,7 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
         }
         m = mn;
     }
+    ts_phase<1>(ts, t_start);  // profiling: this (first) wave's keys done
     // merge the 4 key groups of the wave (lanes l, l^16, l^32, l^48 share dims)
 #pragma unroll
     for (int msk = 16; msk <= 32; msk <<= 1) {
@@ -131,6 +134,7 @@ __device__ __forceinline__ void sa_part(const AttnP &p, int h, int sp, int b, co
     if (lane < 16) *(float4 *)(&wo[w][4 * lane]) = o;
     if (lane == 0) { wm[w] = m; wl[w] = l; }
     lds_sync();
+    ts_phase<2>(ts, t_start);  // profiling: every wave's keys done
     if (tid >= DH) return;
     float M = -INFINITY;
 #pragma unroll
@@ -215,8 +219,9 @@ __device__ __forceinline__ void sa_tail(const GemvP &p, unsigned long long t_sta
     const int k = blockIdx.x - p.nrow_blocks;
     const int h = k % NH, sp = (k / NH) % SA_SPLITS, b = k / (NH * SA_SPLITS);
     const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
-    if (p.sa.kv16) sa_part<true, MP_NWAVES, true>(p.sa, h, sp, b, p.qh, tag, p.hx_err, ts_dep(t_start));
-    else sa_part<false, MP_NWAVES, true>(p.sa, h, sp, b, p.qh, tag, p.hx_err, ts_dep(t_start));
+    if (p.sa.kv16) sa_part<true, MP_NWAVES, true>(p.sa, h, sp, b, p.qh, tag, p.hx_err, ts_dep(t_start), p.ts, t_start);
+    else sa_part<false, MP_NWAVES, true>(p.sa, h, sp, b, p.qh, tag, p.hx_err, ts_dep(t_start), p.ts, t_start);
+    ts_phase<3>(p.ts, t_start);  // profiling: split state stored
     if (p.sa.merged) sa_merge_split(p.sa, h, sp, b);
     ts_end(p.ts, t_start);
 }

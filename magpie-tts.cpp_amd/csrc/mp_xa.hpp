@@ -168,7 +168,7 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
 #pragma unroll
             for (int j = 0; j < PQ; ++j) x1row[w * PQ * 64 + lane + 64 * j] = xv[j];
             lds_sync();
-            ts_mark(ts, t_start);  // profiling: when the workgroup saw all of x1
+            ts_phase<0>(ts, t_start);  // profiling: when the workgroup saw all of x1
 #pragma unroll
             for (int i = 0; i < XA_V; ++i) x4[i] = *(const float4 *)&x1row[4 * lane + 256 * i];
         } else {
@@ -191,6 +191,7 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
                 h[i] = make_float4((float)(_Float16)h[i].x, (float)(_Float16)h[i].y, (float)(_Float16)h[i].z,
                                    (float)(_Float16)h[i].w);
     }
+    ts_phase<1>(ts, t_start);  // profiling: LN done
     const float scale = 1.0f / sqrtf((float)DXA);
     float m = -INFINITY, l = 0.f;
     float4 o[XA_V];
@@ -216,10 +217,12 @@ __device__ __forceinline__ void xa_part(const XaP &p, int sp, int b, unsigned lo
             }
         }
     }
+    ts_phase<2>(ts, t_start);  // profiling: this (first) wave's keys done
 #pragma unroll
     for (int i = 0; i < XA_V; ++i) *(float4 *)&wo[w][4 * lane + 256 * i] = o[i];
     if (lane == 0) { wm[w] = m; wl[w] = l; }
     lds_sync();
+    ts_phase<3>(ts, t_start);  // profiling: every wave's keys done
     float M = -INFINITY;
 #pragma unroll
     for (int q = 0; q < XA_WAVES; ++q) M = fmaxf(M, wm[q]);
@@ -272,6 +275,10 @@ __device__ __forceinline__ void xa_merge_split(const XaP &p, int sp, int b, cons
     const gu64 *g = (const gu64 *)p.gh + (size_t)b * XA_SPLITS * XA_PART;
     const int k = MO * sp + tid;
     float ms[XA_SPLITS], ls[XA_SPLITS], o[XA_SPLITS], e[XA_SPLITS], rd;
+    // x1 (complete: this workgroup saw all of it) issued ahead of the sweep, not a round
+    // trip after it
+    const float x1 = __uint_as_float((unsigned)__hip_atomic_load((const gu64 *)xh + (size_t)b * D + k, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT));
     for (unsigned spins = 0;; ++spins) {
         bool ok = true;
 #pragma unroll
@@ -293,8 +300,6 @@ __device__ __forceinline__ void xa_merge_split(const XaP &p, int sp, int b, cons
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    const float x1 = __uint_as_float((unsigned)__hip_atomic_load((const gu64 *)xh + (size_t)b * D + k, __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT));
     split_weights<XA_SPLITS>(ms, ls, e, rd);
     const float a = split_merge<XA_SPLITS>(e, o, rd);
     p.x2[(size_t)b * D + k] = xa_x2(make_float4(a, 0.f, 0.f, 0.f), make_float4(x1, 0.f, 0.f, 0.f)).x;

@@ -63,6 +63,12 @@ def main():
                 txt = f"   {role:5s} wgs {hi - lo:4d} end p50 {np.median(e2):5.2f} max {e2.max():5.2f}"
                 if m2.size:
                     txt += f" | mark p50 {np.median(m2):5.2f} min {m2.min():5.2f} max {m2.max():5.2f}"
+                if os.environ.get("PHASES"):  # ts_phase<k> stamps: slot 4 + k, p50 / max per phase
+                    for k in range(4):
+                        okk = ok[lo:hi, 4 + k]
+                        if okk.any():
+                            v = rel[lo:hi, 4 + k, 1][okk]
+                            txt += f" | ph{k} {np.median(v):5.2f}/{v.max():5.2f}"
                 print(txt)
     dev.close()
 

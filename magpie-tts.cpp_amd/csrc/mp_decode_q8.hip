@@ -311,9 +311,8 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
         *(float4 *)&xs[4 * lane] = x4;
         // a -> Q8_0 (quantize_row_q8_0_ref): block = 8 lanes x 4 elements
         float am = fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w)));
-        am = fmaxf(am, __shfl_xor(am, 1, 64));
-        am = fmaxf(am, __shfl_xor(am, 2, 64));
-        am = fmaxf(am, __shfl_xor(am, 4, 64));
+        am = quad_max(am);
+        am = fmaxf(am, dpp_mov<0x141>(am));  // the other quad of the 8-lane block (row half mirror)
         const float dd = am / 127.0f;
         const float id = dd != 0.f ? 1.0f / dd : 0.0f;
         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -354,9 +353,10 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
 #pragma unroll
         for (int r = 0; r < RWW; ++r) {
             int is = __builtin_amdgcn_sdot4(wq[r], av, 0, false);
-            is += __shfl_xor(is, 1, 64);
-            is += __shfl_xor(is, 2, 64);
-            is += __shfl_xor(is, 4, 64);
+            // the 8-lane block's integer sum (exact in any order) by DPP: quad, then half-row mirror
+            is += __builtin_amdgcn_update_dpp(0, is, 0xB1, 0xF, 0xF, false);
+            is += __builtin_amdgcn_update_dpp(0, is, 0x4E, 0xF, 0xF, false);
+            is += __builtin_amdgcn_update_dpp(0, is, 0x141, 0xF, 0xF, false);
             const float fb = (float)is * (wd[r] * ad[lane >> 3]);  // lanes 8kb .. 8kb+7: block kb's term
             float acc = 0.f;
 #pragma unroll
@@ -651,7 +651,12 @@ __device__ __forceinline__ void xa_quantize_a(const float *a_s, signed char *aq,
         for (int i = 0; i < 2; ++i) {  // element lane + 64 i; its Q8_0 block = this half-wave
             const float av = a_s[lane + 64 * i];
             float a = row_max16(fabsf(av));
-            a = fmaxf(a, __shfl_xor(a, 16, 64));
+            // the block = 2 rows of 16: their maxima from the rows' last lanes (readlane)
+            const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 15));
+            const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 31));
+            const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 47));
+            const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 63));
+            a = lane < 32 ? fmaxf(r0, r1) : fmaxf(r2, r3);
             const float dd = a / 127.0f;
             const float id = dd != 0.f ? 1.0f / dd : 0.0f;
             aq[lane + 64 * i] = (signed char)(int)roundf(av * id);
@@ -815,7 +820,8 @@ __device__ __forceinline__ float xq8_dot(const uint4 (&wq)[2 * XQ_QB], const uns
         const float dw = __half2float(__ushort_as_half(wqs[j]));
         acc = fmaf((float)sd, dw * actd[blk], acc);
     }
-    const float p1 = __shfl_down(acc, 1, 64), p2 = __shfl_down(acc, 2, 64), p3 = __shfl_down(acc, 3, 64);
+    // lanes 1..3 of the quad into lane 0 by DPP quad permutes (no LDS round trip)
+    const float p1 = dpp_mov<0xE5>(acc), p2 = dpp_mov<0xE6>(acc), p3 = dpp_mov<0xE7>(acc);
     return ((acc + p1) + p2) + p3;
 }
 

@@ -83,6 +83,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
         for (int i = 0; i < NV; ++i) wv[r][i] = ld_weight(wr + lane + 64 * i);
     }
     if constexpr (PRE) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (EPI != EPI_RESID_XA && EPI != EPI_QKV_SA) ts_phase<1>(p.ts, 0);  // profiling: weights issued
     float acc[RW][NB];
 #pragma unroll
     for (int hh = 0; hh < NB / NBS; ++hh) {
@@ -96,6 +97,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
             ph.src = p.src + (size_t)hh * NBS * p.src_ld;
             prologue<NBS, K, PRO>(ph, act, red, sc);
         }
+        if constexpr (EPI != EPI_RESID_XA && EPI != EPI_QKV_SA) ts_phase<2>(p.ts, 0);  // profiling: prologue done
 #pragma unroll
         for (int b = 0; b < NBS; ++b) {
             VT av[NV];
@@ -113,6 +115,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     // acc[][] is wave-uniform: lane r*NB + b owns output (row0 + r, slot b), so the
     // epilogue (GELU, KV append, residual) runs on RW*NB lanes in parallel.
     static_assert(RW * NB <= 64, "one lane per output");
+    if constexpr (EPI != EPI_RESID_XA && EPI != EPI_QKV_SA) ts_phase<3>(p.ts, 0);  // profiling: dot products
     float v = 0.f;
 #pragma unroll
     for (int r = 0; r < RW; ++r)
@@ -578,6 +581,7 @@ __device__ __forceinline__ float4 lt_y_finish(const LtFfn2P &p, int b, bool wb0,
     int amax;
     const int code = wave_pick_v(r.lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, cb - 1, wsc,
                                  amax);
+    ts_phase<0>(p.f.ts, 0);  // profiling: code picked
     const size_t rr = (size_t)(cb - 1) * VCB + code;
     const float *qkv = p.qkvtab + rr * (3 * LTD) + 4 * lane;
     const float4 q4 = *(const float4 *)qkv, k4 = *(const float4 *)(qkv + LTD);
@@ -645,6 +649,7 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     __builtin_amdgcn_sched_barrier(0);
     for (int b = w; b < NB; b += MP_NWAVES) {
         const float4 y = b == w ? lt_y_finish(p, b, pb == 0, wsc_all[w], yp) : lt_y_slot(p, b, pb == 0, wsc_all[w]);
+        if (b == 0) ts_phase<1>(p.f.ts, 0);  // profiling: y (gathers + attention)
         if (pb == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
         if (ys && b == 0) *(float4 *)&ys[4 * lane] = y;
         const float x[4] = {y.x, y.y, y.z, y.w};
@@ -666,6 +671,7 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
         }
     }
     lds_sync();
+    ts_phase<2>(p.f.ts, 0);  // profiling: FFN up
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         float acc = 0.f;

@@ -52,6 +52,12 @@ def main():
                 f"end p50 {np.median(en):5.2f} max {en.max():5.2f}")
         if mk.size:
             line += f" | mark p50 {np.median(mk):5.2f} max {mk.max():5.2f} (first stamp p50 {np.median(mk0):5.2f})"
+        if os.environ.get("PHASES") and not ROLE_SPLIT.get(n):  # ts_phase<k> of every workgroup
+            for k in range(4):
+                okk = ok[:nb, 4 + k]
+                if okk.any():
+                    v = rel[:nb, 4 + k, 1][okk]
+                    line += f" | ph{k} {np.median(v):5.2f}/{v.max():5.2f}"
         print(line)
         # launches with two roles (row workgroups, then the attention tail): each apart
         nrow = ROLE_SPLIT.get(n)

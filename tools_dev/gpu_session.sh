@@ -1,0 +1,66 @@
+#!/bin/bash
+# One gpurun call made of named steps (replaces the per-call rNNx.sh launch lines).
+# Every GPU step runs under its own time limit; the chain stops at the first step
+# that fails (a failing test run stops it too, unless the step is marked "tests?").
+#
+# usage: tools_dev/gpu_session.sh TAG STEP [STEP ...]
+#   tests[=LIB]          pytest -m gpu (LIB: an ab_libs/NAME.so to load instead)
+#   tests?[=LIB]         the same, but a test failure (pytest rc 1) does not stop the chain
+#   bench                the default bench.py line -> TAG_bench.json
+#   ab=N:LIB[,LIB...]    alternating bench A/B: default library vs each ab_libs/LIB.so, N rounds
+#   ops=MODE:B[:LIB]     per-op dispatch intervals + wave spans (tools_dev/mode_ops.py)
+#   tl=MODE:B[:OPS]      in-kernel phase timeline (tools_dev/diag_timeline.py, PHASES=1); OPS comma-separated
+#   prof                 rocprofv3 kernel-trace summary of the bench (eager) + phase cut
+#   pmc                  PMC passes (tools_dev/pmc_collect.sh TAG)
+#   codec                codec-only bench leg (tools_dev/codec_latency.py)
+set -e -o pipefail
+TAG=$1; shift
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for STEP in "$@"; do
+  name=${STEP%%=*}; arg=${STEP#*=}; [ "$arg" = "$STEP" ] && arg=""
+  case "$name" in
+    tests|tests\?)
+      env=()
+      [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
+      log="$OUT/${TAG}_tests${arg:+_$arg}.log"
+      set +e
+      env "${env[@]}" timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread > "$log" 2>&1
+      rc=$?
+      set -e
+      tail -1 "$log"
+      if [ $rc -ne 0 ]; then
+        if [ "$name" = "tests?" ] && [ $rc -eq 1 ]; then echo "tests failed (continuing)"; else echo "tests rc=$rc"; exit $rc; fi
+      fi ;;
+    bench)
+      timeout -k 10 300 python -u bench.py > "$OUT/${TAG}_bench.log" 2>&1
+      tail -1 "$OUT/${TAG}_bench.log" > "$OUT/${TAG}_bench.json"
+      echo "bench ok" ;;
+    ab)
+      n=${arg%%:*}; libs=${arg#*:}
+      bash tools_dev/ab_lib.sh "${TAG}_ab" "$n" $(echo "$libs" | tr ',' '\n' | sed 's#^#ab_libs/#; s#$#.so#') > "$OUT/${TAG}_ab.txt" 2>&1
+      cat "$OUT/${TAG}_ab.txt" ;;
+    ops)
+      IFS=: read -r mode b lib <<< "$arg"
+      env=()
+      [ -n "$lib" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$lib.so")
+      env "${env[@]}" timeout -k 10 200 python -u tools_dev/mode_ops.py "$mode" "$b" > "$OUT/${TAG}_ops_${mode}_b${b}${lib:+_$lib}.txt" 2>&1
+      head -1 "$OUT/${TAG}_ops_${mode}_b${b}${lib:+_$lib}.txt" ;;
+    tl)
+      IFS=: read -r mode b ops <<< "$arg"
+      PHASES=1 timeout -k 10 200 python -u tools_dev/diag_timeline.py "$mode" "$b" $(echo "$ops" | tr ',' ' ') > "$OUT/${TAG}_tl_${mode}_b${b}.txt" 2>&1
+      echo "timeline ok" ;;
+    prof)
+      MAGPIE_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/${TAG}_prof" -o prof \
+        -- python3 -u bench.py --no-cpu-baseline --no-extra > "$OUT/${TAG}_prof_bench.log" 2>&1
+      python3 tools_dev/prof_phase.py "$OUT/${TAG}_prof/prof_kernel_trace.csv" "$OUT/${TAG}_prof/phase_kernel_stats.csv" \
+        > "$OUT/${TAG}_prof_phase.log"
+      echo "rocprof ok" ;;
+    pmc)
+      bash tools_dev/pmc_collect.sh "$TAG" > "$OUT/${TAG}_pmc.log" 2>&1
+      echo "pmc ok" ;;
+    *) echo "unknown step $STEP"; exit 2 ;;
+  esac
+done
+echo "session $TAG done"

@@ -170,13 +170,20 @@ void magpie_free(magpie_context *ctx);
 const char *magpie_get_backend_name(magpie_context *ctx);
 // magpie.h:332: load a GGUF's weights into `model` (its device state is created on
 // first use, on the device MAGPIE_DEVICE names; a model already loaded is replaced).
-// The weight mode is picked from the file as magpie_init does. false + stderr on failure.
+// The weight mode is picked from the file as magpie_init does. false + stderr on failure;
+// a device state this call created is released again on failure. backend: AUTO / CUDA
+// select the HIP device; MAGPIE_BACKEND_CPU and METAL are refused (false + stderr: this
+// build has one backend). Ownership: model.dev belongs to the caller until handed to a
+// context; release a standalone model with magpie_model_free (magpie_free releases a
+// context's model).
 bool magpie_model_load(const std::string &path, magpie_model &model, magpie_backend_type backend = MAGPIE_BACKEND_AUTO);
+// Added: release the device state of a model loaded with magpie_model_load (no-op if none).
+void magpie_model_free(magpie_model &model);
 
 // magpie.h:555-558: run the text encoder for one utterance; ctx->state.encoder_output
 // ([n_tokens][d_model]) and enc_seq_len receive its output, as in the reference
-// (magpie.cpp:2284-2374). On the device this is the per-utterance preamble (encoder,
-// cross-attention K/V, context prefill) of a batch of one.
+// (magpie.cpp:2284-2374). The encoder alone (mp_hip_encode_text, a private device
+// workspace): a batch in progress on ctx is not touched.
 bool magpie_encode_text(magpie_context *ctx, const int32_t *tokens, int n_tokens);
 
 // ---- synthesis (magpie.h:571-595): frame-major codes [n_frames * 8], BOS

@@ -158,6 +158,12 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames);
 /* decoder hidden state after every step (BOS first): [B][max_dec_steps+1][768];
  * requires params.trace_hidden. */
 int mp_hip_get_trace(mp_dev *dev, float *hidden);
+/* magpie_encode_text (src/magpie.cpp:2284-2374): the text encoder alone (embedding +
+ * positions, the encoder layers, final LN) for one utterance, into a private device
+ * workspace; enc_out: host [n_tokens][768]. A batch in progress (mp_hip_begin_batch /
+ * mp_hip_decode) is not touched. Returns MP_OK or a negative MP_ERR_*. */
+int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *enc_out);
+
 /* Diagnostics: copy a per-batch device buffer to host after mp_hip_begin_batch /
  * mp_hip_decode. name: "enc_out" [NB][Tmax][768] (magpie_encode_text's output),
  * "xak"/"xav" [NB][L][Tmax][128] (XA K/V, magpie.cpp:1663-1711), "kc"/"vc"

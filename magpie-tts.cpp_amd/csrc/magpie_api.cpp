@@ -18,12 +18,21 @@ magpie_context *magpie_init(const char *model_path) { return magpie_init_with_ba
 
 // magpie_model_load (magpie.cpp:572-718 behind magpie.h:332): false + stderr on failure.
 bool magpie_model_load(const std::string &path, magpie_model &model, magpie_backend_type backend) {
-    (void)backend;  // single HIP device path
-    if (!model.dev && mp_hip_init(env_device(), &model.dev) != MP_OK) {
+    if (backend == MAGPIE_BACKEND_CPU || backend == MAGPIE_BACKEND_METAL) {
+        fprintf(stderr, "magpie: backend %s is not available in this build (HIP only)\n",
+                backend == MAGPIE_BACKEND_CPU ? "CPU" : "Metal");
+        return false;
+    }
+    const bool created = model.dev == nullptr;
+    if (created && mp_hip_init(env_device(), &model.dev) != MP_OK) {
         fprintf(stderr, "magpie: no usable HIP device\n");
         model.dev = nullptr;
         return false;
     }
+    auto fail_free = [&]() {
+        if (created) { mp_hip_free(model.dev); model.dev = nullptr; }
+        return false;
+    };
     // Weight mode (magpie_hip.h): a GGUF with Q8_0 / Q4_0 tensors runs them as ggml does
     // (MP_WEIGHTS_Q8), an F16 file with ggml's F16 semantics (MP_WEIGHTS_F16), any other
     // file as stored; MAGPIE_WEIGHTS=f32|bf16|q8|f16 overrides.
@@ -44,7 +53,7 @@ bool magpie_model_load(const std::string &path, magpie_model &model, magpie_back
         rc = mp_hip_load_model_ex(model.dev, path.c_str(), MP_WEIGHTS_AS_STORED);
     if (rc != MP_OK) {
         fprintf(stderr, "magpie: failed to load '%s': %s\n", path.c_str(), mp_hip_error(model.dev));
-        return false;
+        return fail_free();
     }
     int dec = 12, enc = 6;
     mp_hip_model_info(model.dev, &dec, &enc, nullptr);
@@ -55,6 +64,11 @@ bool magpie_model_load(const std::string &path, magpie_model &model, magpie_back
     model.hparams.dec_layers = dec;
     model.hparams.enc_layers = enc;
     return true;
+}
+
+void magpie_model_free(magpie_model &model) {
+    if (model.dev) mp_hip_free(model.dev);
+    model.dev = nullptr;
 }
 
 // magpie_init_with_backend (magpie.cpp:781-880): nullptr + stderr on failure.
@@ -158,29 +172,18 @@ std::vector<int32_t> magpie_synthesize_codes_optimized(magpie_context *ctx, cons
 }
 
 // magpie_encode_text (magpie.cpp:2284-2374): the encoder output lands in ctx->state.
+// Encoder only (mp_hip_encode_text): a batch in progress on this context is untouched.
 bool magpie_encode_text(magpie_context *ctx, const int32_t *tokens, int n_tokens) {
     if (!ctx || !ctx->model.dev || !tokens || n_tokens <= 0) {
         fprintf(stderr, "magpie_encode_text: invalid args\n");
         return false;
     }
-    const mp_params p = params_of(ctx);
-    const int32_t spk = ctx->speaker_id;
-    if (mp_hip_begin_batch(ctx->model.dev, tokens, &n_tokens, &spk, 1, n_tokens, &p) != MP_OK) {
+    std::vector<float> enc((size_t)n_tokens * 768);
+    if (mp_hip_encode_text(ctx->model.dev, tokens, n_tokens, enc.data()) != MP_OK) {
         fprintf(stderr, "magpie_encode_text: %s\n", mp_hip_error(ctx->model.dev));
         return false;
     }
-    const long long want = (long long)n_tokens * 768 * 4;
-    const long long eb = mp_hip_debug_buffer(ctx->model.dev, "enc_out", nullptr, 0);
-    if (eb < want) {
-        fprintf(stderr, "magpie_encode_text: encoder output unavailable\n");
-        return false;
-    }
-    std::vector<float> enc((size_t)eb / 4);
-    if (mp_hip_debug_buffer(ctx->model.dev, "enc_out", enc.data(), eb) != eb) {
-        fprintf(stderr, "magpie_encode_text: %s\n", mp_hip_error(ctx->model.dev));
-        return false;
-    }
-    ctx->state.encoder_output.assign(enc.begin(), enc.begin() + (size_t)n_tokens * 768);
+    ctx->state.encoder_output = std::move(enc);
     ctx->state.enc_seq_len = n_tokens;
     return true;
 }

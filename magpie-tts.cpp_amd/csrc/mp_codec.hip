@@ -760,11 +760,11 @@ __global__ __launch_bounds__(256) void conv_transpose2_kernel(ConvTP p) {
 #pragma unroll
             for (int ci = 0; ci < 2; ++ci) {
                 if (tau >= 1) {
-                    a0 += prev[ci] * w[ci][u + S];
-                    a1 += prev[2 + ci] * w[2 + ci][u + S];
+                    a0 = fmaf(prev[ci], w[ci][u + S], a0);
+                    a1 = fmaf(prev[2 + ci], w[2 + ci][u + S], a1);
                 }
-                a0 += cur[ci] * w[ci][u];
-                a1 += cur[2 + ci] * w[2 + ci][u];
+                a0 = fmaf(cur[ci], w[ci][u], a0);
+                a1 = fmaf(cur[2 + ci], w[2 + ci][u], a1);
             }
             if (live0) a0 += bias0;
             if (live1) a1 += bias1;
@@ -821,7 +821,7 @@ __global__ __launch_bounds__(256) void post_conv_kernel(PostP p) {
     float acc = 0.f;
     for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int i = 0; i < 27; ++i) acc += hs[threadIdx.x + k][i] * wh[i * 3 + k];
+        for (int i = 0; i < 27; ++i) acc = fmaf(hs[threadIdx.x + k][i], wh[i * 3 + k], acc);
     p.audio[cbase + t] = tanhf(acc + p.bias[0]);
 }
 

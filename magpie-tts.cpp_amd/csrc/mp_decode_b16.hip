@@ -153,11 +153,9 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     if constexpr (LNB) {
         // LN rows rounded straight into the 16-bit tile (no f32 staging pass): the same
         // y values the f32 rows held, rounded by the same RNE conversion
+        // (contraction off: the LN's last multiply is rounded to f32 before the conversion,
+        // as on the batch-1 path, not fused into it as v_fma_mixlo_f16)
         ln_finish<NB, K>(p, pre.r, [&](int b, int k, float y) {
-            // y materialised as an f32 register first: the compiler would otherwise fuse the
-            // LN's last multiply into the f16 conversion (v_fma_mixlo_f16, one rounding
-            // instead of the batch-1 path's two: f32 row, then f16)
-            asm volatile("" : "+v"(y));
             if constexpr (F16) actb[b * KP + k] = __builtin_bit_cast(unsigned short, (_Float16)y);
             else actb[b * KP + k] = __builtin_bit_cast(unsigned short, (__bf16)y);
         });
@@ -345,7 +343,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
                 pv[s2] = __uint_as_float((unsigned)u);
             }
             if (__all(ok)) break;
-            if (spins >= (1u << 20)) {
+            if (spins >= HX_SPIN_LIMIT) {
                 if ((tid & 63) == 0) __hip_atomic_fetch_or((__attribute__((address_space(1))) int *)p.hx_err, HX_ERR_KS,
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -420,6 +418,7 @@ constexpr int FF2_KS = MP_FF2_KS;
 #define MP_OPROJ_KS 1
 #endif
 constexpr int OPROJ_KS = MP_OPROJ_KS;
+int b16_oproj_ks() { return OPROJ_KS; }
 
 #define MP_B16_OPS(NB)                                                                                                  \
     hipError_t b16_qkv_##NB(const GemvP &p, hipStream_t s) { return launch_b16<NB, D, PRO_LN, EPI_QKV>(p, s); }             \

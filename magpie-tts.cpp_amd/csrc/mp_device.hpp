@@ -387,6 +387,8 @@ __device__ __forceinline__ T ld_weight(const T *p) {
 #endif
 }
 
-__device__ __forceinline__ float dotv(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
-__device__ __forceinline__ float dotv(float2 a, float2 b) { return a.x * b.x + a.y * b.y; }
+// The library is built with -ffp-contract=off (Makefile): every fused multiply-add is
+// written out, so an instantiation change cannot move a rounding (batch == single).
+__device__ __forceinline__ float dotv(float4 a, float4 b) { return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x))); }
+__device__ __forceinline__ float dotv(float2 a, float2 b) { return fmaf(a.y, b.y, a.x * b.x); }
 __device__ __forceinline__ float dotv(float a, float b) { return a * b; }

@@ -162,10 +162,7 @@ constexpr int ltc_off() { return NB * LTD; }
 // arithmetic is the same either way, at every batch size.
 // Inlined (a __noinline__ copy took its arrays through scratch memory); the rounding is
 // pinned instead (contraction off, explicit fmaf), so every caller computes the same bits.
-__device__ __forceinline__ float dot4_pinned(float4 a, float4 b) {
-#pragma clang fp contract(off)
-    return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
-}
+__device__ __forceinline__ float dot4_pinned(float4 a, float4 b) { return dotv(a, b); }
 template <bool CUR, bool PRE>
 __device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, float4 kc4, float4 vc4,
                                             const float4 (&kr)[NCB], const float4 (&vr)[NCB]) {

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * wv[j];
+                    for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], wv[j], acc[i][j]);
             }
             __syncthreads();
         }

@@ -106,6 +106,7 @@ hipError_t b16_lt_bo_8(const GemvP &, hipStream_t);
 hipError_t b16_lt_bo_16(const GemvP &, hipStream_t);
 hipError_t q8_lt_bo_8(const GemvP &, hipStream_t);
 hipError_t op_lt_em_1(const GemvP &, hipStream_t);
+int b16_oproj_ks();
 hipError_t op_lt_ffn(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_ffn2(const LtFfn2P &, int, hipStream_t);
@@ -871,6 +872,7 @@ bool want_xa_direct(const mp_dev *dev, int Tmax) {
     return dev->xa_mode == MP_XA_DIRECT || (dev->xa_mode == MP_XA_AUTO && Tmax > MP_XA_DIRECT_T);
 }
 
+static size_t enc_gpart_elems(size_t Me);
 int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     free_batch(dev);
     const int NB = B <= 1 ? 1 : B <= 2 ? 2 : B <= 4 ? 4 : B <= 8 ? 8 : 16;
@@ -913,9 +915,8 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(pXQ, rows * 128); A(pXAO, rows * 128); A(enc_out, (size_t)NB * Tmax * D);
     {   // largest S x M x N of the preamble GEMMs (encoder FFN up/down, prefill FFN)
         const size_t Me = (size_t)NB * Tmax, Mc = (size_t)NB * mp::CTX;
-        size_t cap = 0;
+        size_t cap = enc_gpart_elems(Me);
         auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits(K) * M * N); };
-        need(Me, 2304, 768); need(Me, 3072, 768 * 3); need(Me, 768, 3072 * 3); need(Me, 256, 768);
         need(Mc, 2304, 768); need(Mc, 3072, 768); need(Mc, 768, 3072); need(Mc, 768, 768);
         A(gpart, cap);
     }
@@ -1017,7 +1018,9 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
         g = gemv_base(dev); g.layer = l;
         g.W = W.o; g.Wb = b16 ? m.pk_o[l] : nullptr; g.N = 768; g.resid = dev->x; g.part = dev->sa_part;
         g.Wq = W.o8.pq; g.Wd = W.o8.pd; g.q4 = W.o8.nib;
-        if (b16) { g.kgh = dev->kgh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2; }  // split-K partial tiles
+        // split-K partial tiles (MP_OPROJ_KS > 1 builds only): the plain O-projection then
+        // carries a hand-off; with one slice it has none and stays timeable standalone
+        if (b16 && mp::b16_oproj_ks() > 1) { g.kgh = dev->kgh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2; }
         mp::XaP xp{dev->x, dev->xa_part, W.norm_xq, m.eps, dev->kp, dev->vp, dev->T, dev->Tmax, l, L};
         xp.q_f16 = m.weight_mode == MP_WEIGHTS_F16;
         const double xa_bytes = A * act * (768.0 + 2.0 * 768 * dev->Tmax + mp::XA_SPLITS * mp::XA_PART);
@@ -1506,50 +1509,75 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
 }
 
 // ------------------------------------------------------------------ preamble
+// The text encoder's buffers: the batch's preamble scratch (run_preamble) or a private
+// workspace (mp_hip_encode_text, which must not touch a batch in progress).
+struct EncWs {
+    const int32_t *tok, *T;  // device [NB][Tmax] token ids, [NB] lengths
+    int NB, Tmax;
+    float *pX, *pH, *pQKV, *pATT, *pF, *gpart, *enc_out;
+};
+static size_t enc_gpart_elems(size_t Me) {
+    size_t cap = 0;
+    auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits(K) * M * N); };
+    need(Me, 2304, 768); need(Me, 3072, 768 * 3); need(Me, 768, 3072 * 3); need(Me, 256, 768);
+    return cap;
+}
+// every preamble GEMM runs split-K over K (deterministic, batch-invariant)
+// F16 file: every projection's operand rounded to f16 as ggml's F16 mul_mat does
+// (the K'/V' precompute is weight algebra, not a mul_mat of the file)
+static hipError_t preamble_gemm(const mp::Model &m, float *gpart, mp::GemmP gp, int epi, hipStream_t st) {
+    gp.part = gpart;
+    gp.xround = gp.xround < 0 ? 0 : (m.weight_mode == MP_WEIGHTS_F16 ? 2 : 0);  // -1: opted out
+    return mp::pre_gemm(gp, epi, st);
+}
+// --- text encoder (magpie_build_full_encoder, 1960-1995) into w.enc_out [NB][Tmax][768]
+static int run_encoder(mp_dev *dev, const EncWs &w, hipStream_t s) {
+    using namespace mp;
+    const Model &m = dev->m;
+    const int Tmax = w.Tmax, Me = w.NB * Tmax;
+    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, w.gpart, gp, epi, st); };
+    HIPCHK(pre_embed_text(w.tok, w.T, w.NB, Tmax, m.text_emb, m.enc_pos, w.pX, s));
+    for (int l = 0; l < m.enc_layers; ++l) {
+        const EncLayerW &W = m.enc[l];
+        HIPCHK(pre_ln_rows(w.pX, 768, W.norm_self, w.pH, 768, Me, m.eps, s));
+        GemmP gp{};
+        gp.A = w.pH; gp.lda = 768; gp.W = W.qkv; gp.Wq = W.qkv8.q; gp.Wd = W.qkv8.d; gp.C = w.pQKV; gp.ldc = 2304; gp.M = Me; gp.N = 2304; gp.K = 768;
+        gp.rows_per_utt = Tmax; gp.T = w.T;
+        HIPCHK(pre_gemm(gp, GE_STORE, s));
+        RowAttnP ra{};
+        ra.Q = w.pQKV; ra.ldq = 2304; ra.Kb = w.pQKV + 768; ra.Vb = w.pQKV + 1536;
+        ra.utt_stride = (size_t)Tmax * 2304; ra.row_stride = 2304; ra.O = w.pATT; ra.M = Me; ra.rows_per_utt = Tmax;
+        ra.heads = 12; ra.T = w.T;
+        HIPCHK(pre_row_attn(ra, s));
+        gp = GemmP{};
+        gp.A = w.pATT; gp.lda = 768; gp.W = W.o; gp.Wq = W.o8.q; gp.Wd = W.o8.d; gp.C = w.pX; gp.ldc = 768; gp.M = Me; gp.N = 768; gp.K = 768;
+        gp.rows_per_utt = Tmax; gp.T = w.T;
+        HIPCHK(pre_gemm(gp, GE_RESID, s));
+        HIPCHK(pre_ln_rows(w.pX, 768, W.norm_ff, w.pH, 768, Me, m.eps, s));
+        gp = GemmP{};  // causal conv k=3 d_model -> d_ffn + GELU (1816-1869)
+        gp.A = w.pH; gp.lda = 768; gp.W = W.ff1; gp.C = w.pF; gp.ldc = 3072; gp.M = Me; gp.N = 3072;
+        gp.K = 768 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = w.T;
+        HIPCHK(pre_gemm(gp, GE_GELU, s));
+        gp = GemmP{};  // causal conv k=3 d_ffn -> d_model + residual (1875-1916)
+        gp.A = w.pF; gp.lda = 3072; gp.W = W.ff2; gp.C = w.pX; gp.ldc = 768; gp.M = Me; gp.N = 768;
+        gp.K = 3072 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = w.T;
+        HIPCHK(pre_gemm(gp, GE_RESID, s));
+    }
+    HIPCHK(pre_ln_rows(w.pX, 768, m.enc_norm_out, w.enc_out, 768, Me, m.eps, s));
+    return MP_OK;
+}
+
 int run_preamble(mp_dev *dev) {
     using namespace mp;
     const Model &m = dev->m;
     const int NB = dev->NB, Tmax = dev->Tmax, L = m.dec_layers;
     hipStream_t s = dev->stream;
     const int Me = NB * Tmax;
-    // every preamble GEMM runs split-K over K (deterministic, batch-invariant)
-    // F16 file: every projection's operand rounded to f16 as ggml's F16 mul_mat does
-    // (the K'/V' precompute below is weight algebra, not a mul_mat of the file)
-    const int xr = m.weight_mode == MP_WEIGHTS_F16 ? 2 : 0;
-    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) {
-        gp.part = dev->gpart;
-        gp.xround = gp.xround < 0 ? 0 : xr;  // -1: opted out
-        return mp::pre_gemm(gp, epi, st);
-    };
-    // --- text encoder (magpie_build_full_encoder, 1960-1995)
-    HIPCHK(pre_embed_text(dev->tok, dev->T, NB, Tmax, m.text_emb, m.enc_pos, dev->pX, s));
-    for (int l = 0; l < m.enc_layers; ++l) {
-        const EncLayerW &W = m.enc[l];
-        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_self, dev->pH, 768, Me, m.eps, s));
-        GemmP gp{};
-        gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.Wq = W.qkv8.q; gp.Wd = W.qkv8.d; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Me; gp.N = 2304; gp.K = 768;
-        gp.rows_per_utt = Tmax; gp.T = dev->T;
-        HIPCHK(pre_gemm(gp, GE_STORE, s));
-        RowAttnP ra{};
-        ra.Q = dev->pQKV; ra.ldq = 2304; ra.Kb = dev->pQKV + 768; ra.Vb = dev->pQKV + 1536;
-        ra.utt_stride = (size_t)Tmax * 2304; ra.row_stride = 2304; ra.O = dev->pATT; ra.M = Me; ra.rows_per_utt = Tmax;
-        ra.heads = 12; ra.T = dev->T;
-        HIPCHK(pre_row_attn(ra, s));
-        gp = GemmP{};
-        gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.Wq = W.o8.q; gp.Wd = W.o8.d; gp.C = dev->pX; gp.ldc = 768; gp.M = Me; gp.N = 768; gp.K = 768;
-        gp.rows_per_utt = Tmax; gp.T = dev->T;
-        HIPCHK(pre_gemm(gp, GE_RESID, s));
-        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_ff, dev->pH, 768, Me, m.eps, s));
-        gp = GemmP{};  // causal conv k=3 d_model -> d_ffn + GELU (1816-1869)
-        gp.A = dev->pH; gp.lda = 768; gp.W = W.ff1; gp.C = dev->pF; gp.ldc = 3072; gp.M = Me; gp.N = 3072;
-        gp.K = 768 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = dev->T;
-        HIPCHK(pre_gemm(gp, GE_GELU, s));
-        gp = GemmP{};  // causal conv k=3 d_ffn -> d_model + residual (1875-1916)
-        gp.A = dev->pF; gp.lda = 3072; gp.W = W.ff2; gp.C = dev->pX; gp.ldc = 768; gp.M = Me; gp.N = 768;
-        gp.K = 3072 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = dev->T;
-        HIPCHK(pre_gemm(gp, GE_RESID, s));
+    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, dev->gpart, gp, epi, st); };
+    {
+        const EncWs w{dev->tok, dev->T, NB, Tmax, dev->pX, dev->pH, dev->pQKV, dev->pATT, dev->pF, dev->gpart, dev->enc_out};
+        if (int rc = run_encoder(dev, w, s)) return rc;
     }
-    HIPCHK(pre_ln_rows(dev->pX, 768, m.enc_norm_out, dev->enc_out, 768, Me, m.eps, s));
     // --- cross-attention K/V per layer (1663-1711)
     for (int l = 0; l < L; ++l) {
         HIPCHK(pre_ln_rows(dev->enc_out, 768, m.dec[l].norm_xmem, dev->pH, 768, Me, m.eps, s));
@@ -1821,6 +1849,44 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
     dev->timing.preamble_ms = ms_since(t0);
     dev->batch_ready = true;
     return MP_OK;
+}
+
+// magpie_encode_text (magpie.cpp:2284-2374) on its own: the text encoder of one
+// utterance into a private device workspace (allocated and freed per call), the
+// output copied to enc_out [n_tokens][768]. A batch in progress is not touched.
+int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *enc_out) {
+    if (!dev) return MP_ERR_ARG;
+    if (!dev->loaded) return fail(dev, MP_ERR_STATE, "no model loaded");
+    if (!tokens || !enc_out || n_tokens < 1) return fail(dev, MP_ERR_ARG, "invalid arguments");
+    if (n_tokens > mp::TMAX_LIMIT || n_tokens > 4096) return fail(dev, MP_ERR_ARG, "too many text tokens");
+    for (int t = 0; t < n_tokens; ++t)
+        if (tokens[t] < 0 || tokens[t] >= dev->m.text_vocab) return fail(dev, MP_ERR_ARG, "token id out of range");
+    HIPCHK(hipSetDevice(dev->device));
+    const size_t M = (size_t)n_tokens, D = 768;
+    const size_t nf = M * D * 4 + M * 3 * D + M * 3072 + enc_gpart_elems(M) + M * D;  // pX pH pATT enc_out | pQKV | pF | gpart
+    char *ws = nullptr;
+    HIPCHK(hipMalloc(&ws, nf * 4 + 64 + M * 4));  // floats | T (64 B slot) | token ids
+    float *f = (float *)ws;
+    EncWs w{};
+    w.NB = 1; w.Tmax = n_tokens;
+    w.pX = f; f += M * D; w.pH = f; f += M * D; w.pATT = f; f += M * D; w.enc_out = f; f += M * D;
+    w.pQKV = f; f += M * 3 * D; w.pF = f; f += M * 3072; w.gpart = f; f += enc_gpart_elems(M);
+    int32_t *ti = (int32_t *)(ws + nf * 4 + 64);
+    int32_t *Ti = (int32_t *)(ws + nf * 4);
+    w.tok = ti; w.T = Ti;
+    int rc = MP_OK;
+    hipError_t e = hipMemcpyAsync(ti, tokens, M * 4, hipMemcpyHostToDevice, dev->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(Ti, &n_tokens, 4, hipMemcpyHostToDevice, dev->stream);
+    if (e != hipSuccess) rc = fail(dev, MP_ERR_HIP, hipGetErrorString(e));
+    if (rc == MP_OK) rc = run_encoder(dev, w, dev->stream);
+    if (rc == MP_OK) {
+        e = hipMemcpyAsync(enc_out, w.enc_out, M * D * 4, hipMemcpyDeviceToHost, dev->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(dev->stream);
+        if (e != hipSuccess) rc = fail(dev, MP_ERR_HIP, hipGetErrorString(e));
+    }
+    hipStreamSynchronize(dev->stream);
+    hipFree(ws);
+    return rc;
 }
 
 // Per-decode device state: BOS frame at position 110 (magpie.cpp:4243-4318).

@@ -75,6 +75,7 @@ SYMBOLS = [
     ("mp_hip_decode", _I, [_P, _P, _P]),
     ("mp_hip_get_trace", _I, [_P, _P]),
     ("mp_hip_debug_buffer", ctypes.c_int64, [_P, ctypes.c_char_p, _P, ctypes.c_int64]),
+    ("mp_hip_encode_text", _I, [_P, _P, _I, _P]),
     ("mp_hip_get_timing", _I, [_P, ctypes.POINTER(mp_timing)]),
     ("mp_hip_decode_stream", _I, [_P, _P, _I, AUDIO_CB, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)]),
     ("mp_hip_lt_sample", _I, [_P, _P, ctypes.c_float, _I, _I, ctypes.c_uint64, _P, _P]),
@@ -305,6 +306,14 @@ class Device:
             self._check(self.lib.mp_hip_get_trace(self.h, hidden.ctypes.data))
         return SynthResult([codes[b, :nf[b]].copy() for b in range(B)], nf, tm.preamble_ms, tm.decode_ms,
                            tm.iterations, hidden)
+
+    def encode_text(self, tokens) -> np.ndarray:
+        """mp_hip_encode_text (magpie_encode_text, magpie.cpp:2284-2374): the text encoder
+        alone for one utterance, [T][768]; a batch in progress is not touched."""
+        tok = np.ascontiguousarray(tokens, np.int32)
+        out = np.zeros((len(tok), 768), np.float32)
+        self._check(self.lib.mp_hip_encode_text(self.h, tok.ctypes.data, len(tok), out.ctypes.data))
+        return out
 
     def debug_buffer(self, name: str) -> np.ndarray:
         """mp_hip_debug_buffer: a per-batch device buffer (flat f32) for diagnostics."""

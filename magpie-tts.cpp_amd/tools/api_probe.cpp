@@ -18,7 +18,9 @@ int main(int argc, char **argv) {
     magpie_model m;
     const bool loaded = magpie_model_load(std::string(argv[1]), m);
     const int dec_layers = m.hparams.dec_layers;
-    if (m.dev) mp_hip_free(m.dev);
+    magpie_model_free(m);
+    magpie_model cpu;  // the CPU backend is refused (one HIP backend), without leaking a device
+    const bool cpu_refused = !magpie_model_load(std::string(argv[1]), cpu, MAGPIE_BACKEND_CPU) && cpu.dev == nullptr;
     magpie_context *ctx = magpie_init(argv[1]);
     if (!ctx) return 1;
     const std::vector<int32_t> ids = magpie_tokenize(&ctx->model.tokenizer, argv[4]);
@@ -36,7 +38,8 @@ int main(int argc, char **argv) {
            "\"tokens\": [",
            loaded ? "true" : "false", dec_layers, enc ? "true" : "false", ctx->state.enc_seq_len, (int)ids.size());
     for (size_t i = 0; i < ids.size(); ++i) printf("%s%d", i ? ", " : "", ids[i]);
-    printf("], \"codec_load\": %s, \"codec_samples\": %d}\n", cl ? "true" : "false", (int)audio.size());
+    printf("], \"codec_load\": %s, \"codec_samples\": %d, \"cpu_backend_refused\": %s}\n", cl ? "true" : "false",
+           (int)audio.size(), cpu_refused ? "true" : "false");
     magpie_free(ctx);
     return loaded && enc && cl ? 0 : 1;
 }

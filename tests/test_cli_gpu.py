@@ -97,6 +97,7 @@ def test_model_load_encode_text_codec_load(ma, oracle, small_model, codec_model,
     assert info["model_load"] and info["encode_text"] and info["codec_load"], info
     assert info["dec_layers"] == 2 and info["enc_seq_len"] == info["n_tokens"] > 2, info
     assert info["codec_samples"] == 4 * 1024
+    assert info["cpu_backend_refused"], info
     enc = np.fromfile(out, np.float32).reshape(info["n_tokens"], 768)
     om = oracle.Model(small_model)
     ref = om.encode(np.asarray(info["tokens"], np.int32))

@@ -501,3 +501,25 @@ def test_q4_batch_equals_single(ma, q4_model, B):
 def test_q8_mode_needs_q8_file(ma, small_model):
     with pytest.raises(ma.MagpieError):
         ma.Device(small_model, weights="q8")
+
+
+def test_encode_text_alone_leaves_batch_untouched(ma, oracle, small_model):
+    """mp_hip_encode_text (magpie_encode_text, magpie.cpp:2284-2374): the encoder output
+    equals the oracle's encoder, and calling it between a batch's preamble and its decode
+    changes nothing in that decode (own workspace)."""
+    tok_a, tok_b = ma.synthetic_tokens(24, seed=1000), ma.synthetic_tokens(40, seed=11)
+    dev = ma.Device(small_model)
+    try:
+        r1 = dev.synthesize([tok_a], speakers=[1], max_dec_steps=16, ignore_eos=True, trace=True)
+        enc = dev.encode_text(tok_b)
+        r2 = dev.decode(1, 16, trace=True)  # the same batch again (preamble state reused)
+    finally:
+        dev.close()
+    np.testing.assert_array_equal(r1.codes[0], r2.codes[0])
+    np.testing.assert_array_equal(r1.hidden, r2.hidden)
+    om = oracle.Model(small_model)
+    ref = om.encode(tok_b)
+    om.close()
+    err = float(np.abs(enc - ref).max())
+    print(f"encoder alone (T = {len(tok_b)}): max abs err {err:.3g} vs the oracle")
+    assert err < 2e-5

@@ -277,6 +277,11 @@ def test_library_has_no_packed_fp32_instructions(tmp_path):
                              capture_output=True, text=True, check=True).stdout
         bad = re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", dis)
         assert not bad, f"{co.name}: {len(bad)} packed-FP32 instructions ({bad[0]})"
+        # no mixed-precision FMA: an f32 multiply folded into its f16 / bf16 conversion
+        # rounds once where the same value computed elsewhere rounds twice (batch ==
+        # single, round 4); the library is built with -fma-mix-insts (Makefile)
+        mix = re.findall(r"\bv_(?:fma|mad)_mix\w*", dis)
+        assert not mix, f"{co.name}: {len(mix)} mixed-precision FMA instructions ({mix[0]})"
         # no kernel keeps registers in scratch memory (round 4: arrays of HIP's float4 /
         # uint4 structs assigned under a condition, and arrays passed to a __noinline__
         # function, went to scratch: a dependent memory round trip per element)

@@ -7,7 +7,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/magpie-tts.cpp_amd
 OUT=$ROOT/ab_libs/$NAME
 mkdir -p "$OUT"
-FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result -Wno-unused-value -Xclang -target-feature -Xclang -packed-fp32-ops $EXTRA"
+FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result -Wno-unused-value -Xclang -target-feature -Xclang -packed-fp32-ops -ffp-contract=off -Xclang -target-feature -Xclang -fma-mix-insts -Xclang -target-feature -Xclang -fma-mix-bf16-insts $EXTRA"
 pids=()
 for s in mp_decode mp_decode_b16 mp_decode_q8 mp_prefill mp_runtime mp_codec; do
   /opt/rocm/bin/hipcc $FLAGS -c "$PKG/csrc/$s.hip" -o "$OUT/$s.o" & pids+=($!)

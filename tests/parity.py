@@ -50,6 +50,7 @@ def compare_forced(gpu_codes, forced_orc, tie_eps=TIE_EPS, max_ties=None):
                                     f"with oracle margin {m[f, cb]:.3g} >= {tie_eps}")
     if max_ties is not None:
         assert len(diff) <= max_ties, f"{len(diff)} near-tie decisions, at most {max_ties} expected"
+    dm = [float(m[f, c]) for f, c in diff]
     print(f"teacher-forced: {g.size} decisions checked over {len(g)} frames, {len(diff)} near-tie differences"
-          f" (margins {[round(float(m[f, c]), 5) for f, c in diff[:4]]})")
+          f" (margins {[round(v, 5) for v in dm[:4]]}, largest {max(dm) if dm else 0.0:.4g})")
     return {"decisions": int(g.size), "differences": int(len(diff))}

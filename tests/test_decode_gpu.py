@@ -243,6 +243,7 @@ def _rel_l2(h_gpu, h_orc):
 def _check_hidden_b16(h_gpu, h_orc):
     err = np.abs(h_gpu - h_orc).max()
     rel = _rel_l2(h_gpu, h_orc)
+    print(f"hidden vs oracle: max abs err {err:.3g}, max relative L2 {rel.max():.3g} over {len(h_gpu)} steps")
     assert err < BF16_HIDDEN_TOL, f"hidden max abs err {err}"
     assert rel.max() < BF16_HIDDEN_REL, f"hidden rel L2 err {rel.max()}"
 
@@ -403,6 +404,7 @@ Q8_HIDDEN_REL = BF16_HIDDEN_REL
 def _check_hidden_q8(h_gpu, h_orc):
     err = np.abs(h_gpu - h_orc).max()
     rel = _rel_l2(h_gpu, h_orc)
+    print(f"Q8 hidden vs oracle mode 2: max abs err {err:.3g}, max relative L2 {rel.max():.3g} over {len(h_gpu)} steps")
     assert err < Q8_HIDDEN_TOL, f"hidden max abs err {err}"
     assert rel.max() < Q8_HIDDEN_REL, f"hidden rel L2 err {rel.max()}"
     return err

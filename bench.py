@@ -362,10 +362,23 @@ def main() -> None:
         pmc_codec = os.path.join(REPO, "profiles", PMC_CODEC)
         if os.path.exists(pmc_codec):  # counters of the same codec shape (tools_dev/pmc_report.py)
             sm = json.load(open(pmc_codec))["summary"]
-            codec["pmc"] = {"mfma_util": sm.get("mfma_util_traced"), "hbm_tbs": sm.get("hbm_tbs_traced"),
-                            "bytes_per_decode": sm.get("per_decode_bytes"),
-                            "source": f"profiles/{PMC_CODEC}: SQ_VALU_MFMA_BUSY_CYCLES / (traced duration x "
-                                      "2.4 GHz x 1024 SIMDs); FETCH_SIZE/WRITE_SIZE passes"}
+            # MFMA utilisation: the MFMA FLOPs the codec issues per decode of this shape
+            # (SQ_INSTS_VALU_MFMA_MOPS_F16 x 512, padding included) over the live decode
+            # time above, against the dense f16 peak; traffic: FETCH_SIZE + WRITE_SIZE per
+            # decode over the same live time (the PMC runs themselves are slowed by the
+            # counters, so their own durations are not used)
+            issued = sm.get("per_decode_mfma_flops")
+            nbytes = sm.get("per_decode_bytes")
+            pmc_chunks = sm.get("chunks", 8)
+            scale = (cframes / CODEC_CHUNK) / pmc_chunks
+            codec["pmc"] = {
+                "mfma_util": round(issued * scale / (codec_ms * 1e-3) / (MFMA_F16_PEAK_TFS * 1e12), 4) if issued else None,
+                "mfma_flops_issued_per_useful": round(issued / (CODEC_FLOP_PER_FRAME * pmc_chunks * CODEC_CHUNK), 3)
+                if issued else None,
+                "hbm_tbs": round(nbytes * scale / (codec_ms * 1e-3) / 1e12, 3) if nbytes else None,
+                "bytes_per_decode": nbytes,
+                "source": f"profiles/{PMC_CODEC}: MFMA op counts and FETCH_SIZE/WRITE_SIZE passes of the same "
+                          f"{pmc_chunks} x {CODEC_CHUNK}-frame decode, over this run's live decode time"}
 
     # ---- roofline of the dominant kernel, timed in situ: whole decode iterations
     # launched eagerly on the decode stream, each kernel through hipExtLaunchKernel

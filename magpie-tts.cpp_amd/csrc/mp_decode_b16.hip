@@ -146,7 +146,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     const uint4 *wf = (const uint4 *)p.Wb + ((size_t)rt * KC + ks * KCS + w * KW) * 64 + lane + ts_dep(t_start);
     uint4 a[KW];
 #pragma unroll
-    for (int i = 0; i < KW; ++i) a[i] = ld_weight(wf + (size_t)i * 64);
+    for (int i = 0; i < KW; ++i) a[i] = K == LTD ? ld_lt(wf + (size_t)i * 64) : ld_weight(wf + (size_t)i * 64);
     if constexpr (PRE || PLB || PLF) __builtin_amdgcn_sched_barrier(0);
 
     // activation rows -> bf16 in LDS; row NB is zero and feeds MFMA columns NB..15

@@ -389,6 +389,22 @@ __device__ __forceinline__ T ld_weight(const T *p) {
 
 // The library is built with -ffp-contract=off (Makefile): every fused multiply-add is
 // written out, so an instantiation change cannot move a rounding (batch == single).
+// The local transformer's weights (LT FFN, heads, in_proj, [W_k ; W_o W_v]) are re-read
+// every frame (the FFN 8 times per frame) and are 5 % of the frame's bytes: MP_LT_NT=0
+// loads them with the default cache policy (left in the Infinity Cache between uses)
+// instead of non-temporal.
+#ifndef MP_LT_NT
+#define MP_LT_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_lt(const T *p) {
+#if MP_LT_NT
+    return ld_weight(p);
+#else
+    return *p;
+#endif
+}
+
 __device__ __forceinline__ float dotv(float4 a, float4 b) { return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x))); }
 __device__ __forceinline__ float dotv(float2 a, float2 b) { return fmaf(a.y, b.y, a.x * b.x); }
 __device__ __forceinline__ float dotv(float a, float b) { return a * b; }

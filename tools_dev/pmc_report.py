@@ -141,7 +141,7 @@ def codec(tag, trace=None):
         out.append(rec)
     out.sort(key=lambda r: -r["dispatches"] * r["gui_active_cycles"])
     decodes = 4
-    summary = {"per_decode_bytes": round(tot["bytes"] / decodes), "per_decode_mfma_flops": round(tot["flops"] / decodes),
+    summary = {"chunks": 8, "per_decode_bytes": round(tot["bytes"] / decodes), "per_decode_mfma_flops": round(tot["flops"] / decodes),
                "mfma_util_gui_active": round(tot["busy"] / (tot["gui"] * SIMDS), 4) if tot["gui"] else None}
     if tot["t"]:
         summary["per_decode_traced_us"] = round(tot["t"] / decodes, 1)

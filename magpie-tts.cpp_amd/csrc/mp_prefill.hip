@@ -12,6 +12,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "mp_device.hpp"
 #include "mp_params.hpp"
@@ -135,6 +136,98 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
         }
     }
     gemm_store<EPI>(p, acc, m0 + ty * 4, n0 + tx * 4);
+}
+
+// The same GEMM on the exact-f32 matrix cores (v_mfma_f32_16x16x4_f32: one k-ordered
+// fmaf chain per output, bitwise the VALU kernel's acc = fmaf(a_k, w_k, acc) for k
+// ascending; MI355X_MICROARCH.md, FP32-input MFMA), at twice the unpacked VALU rate and
+// without the 4x4-per-thread LDS operand traffic. Same tiles, loader (register ring,
+// causal conv taps), split-K slices and epilogue. Wave w owns the 32 x 32 quadrant
+// (rows 32 (w & 1), columns 32 (w >> 1)) of the 64 x 64 tile: 2 x 2 MFMA tiles; lane l
+// feeds A[row l & 15][k l >> 4] and B[k l >> 4][col l & 15] and holds C rows
+// 4 (l >> 4) + i, column l & 15.
+template <int EPI, int TAPS>
+__global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
+    constexpr int BM = 64, BN = 64, BK = 16, PF = 4;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __shared__ float As[BK][BM + 4];
+    __shared__ float Ws[BK][BN + 4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int rq = 32 * (w & 1), cq = 32 * (w >> 1);  // the wave's quadrant
+    f4v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int lr = tid >> 2, lk = (tid & 3) * 4;  // loader: row lr, k lk..lk+3
+    const int ks = p.K / gridDim.z, kbeg = blockIdx.z * ks;
+    const int nsteps = ks / BK;
+    const int m = m0 + lr, n = n0 + lr;
+    auto load_a = [&](int k0) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < p.M) {
+            if constexpr (TAPS == 0) {
+                v = *(const float4 *)(p.A + (size_t)m * p.lda + k0 + lk);
+            } else {
+                const int t = m % p.rows_per_utt;
+                const int tap = k0 / p.lda, i = k0 % p.lda + lk;
+                if (t - (TAPS - 1) + tap >= 0) v = *(const float4 *)(p.A + (size_t)(m - (TAPS - 1) + tap) * p.lda + i);
+            }
+        }
+        return v;
+    };
+    auto load_w = [&](int k0) {
+        return n < p.N ? *(const float4 *)(p.W + (size_t)n * p.K + k0 + lk) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    float4 ra[PF], rw[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (u < nsteps) { ra[u] = load_a(kbeg + u * BK); rw[u] = load_w(kbeg + u * BK); }
+    const int fr = lane & 15, fk = lane >> 4;
+    for (int base = 0; base < nsteps; base += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int step = base + u;
+            if (step >= nsteps) break;
+            float a[4] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w};
+            if (p.xround)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[e] = (float)(_Float16)a[e];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) As[lk + e][lr] = a[e];
+            Ws[lk + 0][lr] = rw[u].x; Ws[lk + 1][lr] = rw[u].y; Ws[lk + 2][lr] = rw[u].z; Ws[lk + 3][lr] = rw[u].w;
+            if (step + PF < nsteps) { ra[u] = load_a(kbeg + (step + PF) * BK); rw[u] = load_w(kbeg + (step + PF) * BK); }
+            __syncthreads();
+#pragma unroll
+            for (int k4 = 0; k4 < BK; k4 += 4) {
+                float af[2], bf[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) af[i] = As[k4 + fk][rq + 16 * i + fr];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) bf[j] = Ws[k4 + fk][cq + 16 * j + fr];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+            }
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int nn = n0 + cq + 16 * j + fr;
+            if (nn >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mm = m0 + rq + 16 * i + 4 * fk + r;
+                if (mm >= p.M) continue;
+                if (p.part) p.part[((size_t)blockIdx.z * p.M + mm) * p.N + nn] = acc[i][j][r];
+                else gemm_store1<EPI>(p, mm, nn, acc[i][j][r]);
+            }
+        }
 }
 
 // Q8_0 weights (weight mode MP_WEIGHTS_Q8): ggml's quantised mul_mat. Every K
@@ -367,6 +460,12 @@ __global__ void round_bf16_kernel(const float *src, float *dst, size_t n) {
 }
 
 // ---------------------------------------------------------------- launchers
+// MAGPIE_PRE_VALU=1 runs the preamble GEMMs on the f32 VALU kernel (A/B, and the test
+// that both give the same bits; read at every launch, a few per preamble layer)
+static bool gemm_mfma() {
+    const char *e = getenv("MAGPIE_PRE_VALU");
+    return !(e && *e == '1');
+}
 template <int EPI>
 static hipError_t launch_reduce(const GemmP &p, int splits, hipStream_t s) {
     const size_t total = (size_t)p.M * p.N;
@@ -381,7 +480,8 @@ static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
     dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits);
     GemmP q = p;
     if (splits == 1) q.part = nullptr;
-    hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
+    if (gemm_mfma()) hipLaunchKernelGGL((gemm_f32_mfma_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
+    else hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
     if (hipError_t e = hipGetLastError(); e != hipSuccess || splits == 1) return e;
     return launch_reduce<EPI>(p, splits, s);
 }

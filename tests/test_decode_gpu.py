@@ -525,3 +525,25 @@ def test_encode_text_alone_leaves_batch_untouched(ma, oracle, small_model):
     err = float(np.abs(enc - ref).max())
     print(f"encoder alone (T = {len(tok_b)}): max abs err {err:.3g} vs the oracle")
     assert err < 2e-5
+
+
+@pytest.mark.parametrize("weights", ["f32", "f16"])
+def test_preamble_mfma_equals_valu(ma, small_model, f16_model, weights, monkeypatch):
+    """The preamble GEMMs on the exact-f32 matrix cores (v_mfma_f32_16x16x4_f32: a
+    k-ordered fmaf chain) compute the same bits as the f32 VALU kernel they replace
+    (MAGPIE_PRE_VALU=1): encoder output, codes and every hidden state."""
+    path = f16_model if weights == "f16" else small_model
+    tok = ma.synthetic_tokens(40, seed=11)
+    dev = ma.Device(path, weights=weights)
+    try:
+        a = dev.synthesize([tok], speakers=[3], max_dec_steps=12, ignore_eos=True, trace=True)
+        ea = dev.encode_text(tok)
+        monkeypatch.setenv("MAGPIE_PRE_VALU", "1")
+        b = dev.synthesize([tok], speakers=[3], max_dec_steps=12, ignore_eos=True, trace=True)
+        eb = dev.encode_text(tok)
+    finally:
+        dev.close()
+    assert np.array_equal(ea, eb)
+    assert np.array_equal(a.codes[0], b.codes[0]) and np.array_equal(a.hidden, b.hidden)
+    print(f"preamble MFMA == VALU ({weights}): encoder, {len(a.codes[0])} frames, hidden bitwise; "
+          f"preamble {a.preamble_ms:.2f} ms (MFMA) vs {b.preamble_ms:.2f} ms (VALU)")

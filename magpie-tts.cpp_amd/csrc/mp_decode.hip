@@ -844,6 +844,7 @@ hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
 // and the lane's vo_0 elements *v4 when non-null) -> LN(y) -> this workgroup's 16 FFN
 // units -> returns this thread's FFN-down partial sum (output tid) of codebook 0.
 constexpr int LTF_U = LTF / LT_FFN_P, LTF_UPW = LTF_U / MP_NWAVES;
+constexpr int LTFR_G = LTD / MP_NWAVES;  // lt_front workgroups: one in_proj / k / vo row per wave
 __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_in, const float4 (&wi)[3], float4 wk,
                                                float4 wv, const float4 (&a1)[LTF_UPW], const float4 (&a2)[LTF_U / 4],
                                                const float (&v)[D / 64], const float (&g)[D / 64], float *act, float *act2,
@@ -917,7 +918,9 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    // ---- codebook 0's FFN step (lt_ffn2_kernel<1>: y = X_0 + vo_0, wave 0)
+    // ---- codebook 0's FFN step (lt_ffn2_kernel<1>: y = X_0 + vo_0, wave 0), in the
+    // LT_FFN_P workgroups that own FFN units
+    if (pb >= LT_FFN_P) return 0.f;
     if (w == 0) {
         float xv[4], vv[4];
         gh_wait_n<4, 1>(p.gh + LTD + 4 * lane, tag_v, vv, p.hx_err);  // vo_0 outputs 4 lane + c
@@ -969,6 +972,13 @@ __device__ __forceinline__ void lt_front_weights(const LtFrontP &p, int pb, int 
     wk = ld_lt((const float4 *)(p.w_kvo + (size_t)n_in * LTD + 4 * lane));
     wv = ld_lt((const float4 *)(p.w_kvo + (size_t)(LTD + n_in) * LTD + 4 * lane));
     const int j0 = pb * LTF_U;
+    if (pb >= LT_FFN_P) {  // no FFN units in this workgroup (every element assigned: no scratch)
+#pragma unroll
+        for (int r = 0; r < LTF_UPW; ++r) a1[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < LTF_U / 4; ++i) a2[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < LTF_UPW; ++r)
         a1[r] = ld_lt((const float4 *)(p.l.f.w1 + (size_t)(j0 + w * LTF_UPW + r) * LTD + 4 * lane));
@@ -977,7 +987,7 @@ __device__ __forceinline__ void lt_front_weights(const LtFrontP &p, int pb, int 
 }
 __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     const unsigned long long t_start = ts_begin(p.l.f.ts);
-    static_assert(LTF_U % MP_NWAVES == 0 && LTD == MP_BLOCK && LT_FFN_P * MP_NWAVES == LTD, "unit split");
+    static_assert(LTF_U % MP_NWAVES == 0 && LTD == MP_BLOCK && LT_FFN_P <= LTFR_G, "unit split");
     __shared__ __attribute__((aligned(16))) float act[D];
     __shared__ __attribute__((aligned(16))) float act2[LTD];
     __shared__ __attribute__((aligned(16))) float xs[LTD];
@@ -997,7 +1007,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     lt_front_weights(p, pb, n_in, wi, wk, wv, a1, a2);
     __builtin_amdgcn_sched_barrier(0);
     const float acc = lt_front_core(p, pb, n_in, wi, wk, wv, a1, a2, v, g, act, act2, xs, fs, nullptr, nullptr);
-    p.l.f.part[(size_t)pb * LTD + tid] = acc;
+    if (pb < LT_FFN_P) p.l.f.part[(size_t)pb * LTD + tid] = acc;
     ts_end(p.l.f.ts, t_start);
 }
 hipError_t op_lt_front(const LtFrontP &p, hipStream_t s) {
@@ -1006,12 +1016,15 @@ hipError_t op_lt_front(const LtFrontP &p, hipStream_t s) {
         !p.iter || !p.hx_err || !p.l.f.y || !p.l.f.lnw || !p.l.f.w1 || !p.l.f.w2 || !p.l.f.part || !p.l.ltX ||
         !p.l.ltk || !p.l.ltv || !p.l.step || p.l.cb != 0)
         return hipErrorInvalidValue;
-    mp::launch(lt_front_kernel, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p);
+    mp::launch(lt_front_kernel, dim3(LTFR_G), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 
 // the LT head at batch 1 with the FFN merge as its prologue
-hipError_t op_lt_em_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 2, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
+#ifndef MP_RW_LTE
+#define MP_RW_LTE 2  // head rows per wave at batch 1 (253 workgroups at 2)
+#endif
+hipError_t op_lt_em_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, MP_RW_LTE, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 // f32 LT position 0: LN(X_0) -> [k_0 | vo_0] (W = [W_k ; W_o W_v], 512 x 256)
 hipError_t op_lt_kvo(const GemvP &p, int NB, hipStream_t s) {
     switch (NB) {

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
 // each computing LTQ_P / WP of the LTQ_P partial sums (16 hidden units each), so the
 // partials, their order and the merge are the same for every WP.
 constexpr int LTQ_U = LTF / LTQ_P;  // hidden units per partial sum
-static_assert(LTQ_P == LT_FFN_P, "the deferred merge is the head's PRO_LTFFN_MERGE prologue");
+// (the deferred merge at batch 1 is the Q8_0 head's PRO_LTQ_MERGE prologue: LTQ_P partials)
 template <bool RED, bool DEFER, int WP>
 __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
 #pragma clang fp contract(off)
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
             acc[k] = fmaf(a2[k][i].w, f4.w, acc[k]);
         }
     }
-    if constexpr (DEFER) {  // the head's prologue merges (PRO_LTFFN_MERGE)
+    if constexpr (DEFER) {  // the head's prologue merges (PRO_LTQ_MERGE)
 #pragma unroll
         for (int k = 0; k < PPW; ++k) p.part[((size_t)b * LTQ_P + q * PPW + k) * LTD + tid] = acc[k];
         ts_end(p.ts, t_start);
@@ -1047,7 +1047,7 @@ static bool q8_args_ok(const GemvP &p) {
     bool ok = true;
     if constexpr (PRO == PRO_PLAIN) ok &= p.src != nullptr;
     if constexpr (PRO == PRO_SA_MERGE) ok &= p.part != nullptr;
-    if constexpr (PRO == PRO_LTFFN_MERGE) ok &= p.part && p.addsrc;
+    if constexpr (PRO == PRO_LTFFN_MERGE || PRO == PRO_LTQ_MERGE) ok &= p.part && p.addsrc;
     if constexpr (PRO == PRO_XA_LN) ok &= p.part && p.src && p.lnw && p.xres;
     if constexpr (PRO == PRO_LN) ok &= p.src && p.lnw;
     if constexpr (PRO == PRO_LTX_LN) ok &= p.lt_s && p.lt_pos && p.ltX && p.lnw;
@@ -1109,6 +1109,6 @@ hipError_t q8_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_q8<1, D, P
 hipError_t q8_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_q8<8, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 hipError_t q8_lt_bo_16(const GemvP &p, hipStream_t s) { return launch_q8<16, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 // the LT head at batch 1 with the LT FFN merge as its prologue (lt_ffn_kernel)
-hipError_t q8_lt_em_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
+hipError_t q8_lt_em_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, PRO_LTQ_MERGE, EPI_BIAS>(p, s); }
 
 }  // namespace mp

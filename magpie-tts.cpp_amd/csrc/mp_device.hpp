@@ -126,7 +126,7 @@ __device__ __forceinline__ void ts_phase(unsigned long long *ts, unsigned long l
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         const int blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         if (threadIdx.x == 0 && blk < TS_BLOCKS)
-            *(ulonglong2 *)(ts + 2 * ((size_t)blk * TS_WAVES + TS_WAVES / 2 + K)) = make_ulonglong2(t0, t1);
+            *(ulonglong2 *)(ts + 2 * ((size_t)blk * TS_WAVES + TS_WAVES / 2 + K)) = make_ulonglong2(t0 ? t0 : t1, t1);
     }
 }
 __device__ __forceinline__ void ts_end(unsigned long long *ts, unsigned long long t0) {

@@ -200,11 +200,12 @@ __device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, fl
 // LT FFN output element k of slot b: the LT_FFN_P partial FFN-down sums added in
 // ascending order, then the residual (the same arithmetic in the head's prologue
 // at batch 1 and in lt_merge_kernel otherwise)
+template <int NP = LT_FFN_P>
 __device__ __forceinline__ float lt_ffn_merge(const float *part, const float *y, int b, int k) {
-    const float *pp = part + (size_t)b * LT_FFN_P * LTD + k;
+    const float *pp = part + (size_t)b * NP * LTD + k;
     float s = pp[0];
 #pragma unroll
-    for (int q = 1; q < LT_FFN_P; ++q) s += pp[(size_t)q * LTD];
+    for (int q = 1; q < NP; ++q) s += pp[(size_t)q * LTD];
     return s + y[(size_t)b * LTD + k];
 }
 
@@ -529,6 +530,11 @@ struct PreRows<NB, K, PRO_LTFFN_MERGE> {
     static constexpr bool ON = NB == 1 && K == MP_BLOCK;
     float pp[LT_FFN_P], y;
 };
+template <int NB, int K>
+struct PreRows<NB, K, PRO_LTQ_MERGE> {
+    static constexpr bool ON = NB == 1 && K == MP_BLOCK;
+    float pp[LTQ_P], y;
+};
 template <int NB, int K, int PRO>
 __device__ __forceinline__ void pre_load(const GemvP &p, PreRows<NB, K, PRO> &pr) {
     const int tid = threadIdx.x;
@@ -565,10 +571,10 @@ __device__ __forceinline__ void pre_load(const GemvP &p, PreRows<NB, K, PRO> &pr
             }
         }
         if constexpr (!SA) load_lnw<K / 64>(p.lnw, pr.g);
-    } else if constexpr (PRO == PRO_LTFFN_MERGE) {
+    } else if constexpr (PRO == PRO_LTFFN_MERGE || PRO == PRO_LTQ_MERGE) {
         const float *pp = p.part + tid;
 #pragma unroll
-        for (int q = 0; q < LT_FFN_P; ++q) pr.pp[q] = pp[(size_t)q * LTD];
+        for (int q = 0; q < ltm_count<PRO>(); ++q) pr.pp[q] = pp[(size_t)q * LTD];
         pr.y = p.addsrc[tid];
     }
 }
@@ -618,11 +624,11 @@ __device__ __forceinline__ void pre_finish(const GemvP &p, PreRows<NB, K, PRO> &
         }
         lds_sync();
         if constexpr (!SA) xa_ln_rows<NB, K>(p, act, pr.g);
-    } else if constexpr (PRO == PRO_LTFFN_MERGE) {
+    } else if constexpr (PRO == PRO_LTFFN_MERGE || PRO == PRO_LTQ_MERGE) {
         // lt_ffn_merge's arithmetic: partial sums in ascending order, then the residual
         float s2 = pr.pp[0];
 #pragma unroll
-        for (int q = 1; q < LT_FFN_P; ++q) s2 += pr.pp[q];
+        for (int q = 1; q < ltm_count<PRO>(); ++q) s2 += pr.pp[q];
         act[tid] = s2 + pr.y;
         lds_sync();
     }
@@ -704,9 +710,10 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         float g[PER];
         load_lnw<PER>(p.lnw, g);
         xa_ln_rows<NB, K>(p, act, g);
-    } else if constexpr (PRO == PRO_LTFFN_MERGE) {
+    } else if constexpr (PRO == PRO_LTFFN_MERGE || PRO == PRO_LTQ_MERGE) {
         static_assert(K == LTD, "LT is 256 wide");
-        for (int e = tid; e < NB * K; e += MP_BLOCK) act[e] = lt_ffn_merge(p.part, p.addsrc, e / K, e % K);
+        for (int e = tid; e < NB * K; e += MP_BLOCK)
+            act[e] = lt_ffn_merge<ltm_count<PRO>()>(p.part, p.addsrc, e / K, e % K);
         lds_sync();
     } else if constexpr (PRO == PRO_LTS_MERGE) {
         static_assert(K == LTD, "LT is 256 wide");

@@ -28,7 +28,10 @@ constexpr int SA_PART = 4 + DH;     // per (slot, head, split): m, l, -, -, O[64
 #endif
 constexpr int XA_SPLITS = MP_XA_SPLITS;  // text-key splits of the fused cross-attention (xa_part_kernel)
 constexpr int XA_PART = 4 + D;      // per (slot, split): m, l, -, -, O[768] (unnormalised)
-constexpr int LT_FFN_P = 64;        // LT FFN: workgroups of lt_ffn_kernel = partial FFN-down sums per slot
+#ifndef MP_LT_FFN_P
+#define MP_LT_FFN_P 64
+#endif
+constexpr int LT_FFN_P = MP_LT_FFN_P;  // LT FFN (f32 / F16 modes): workgroups of lt_ffn(2)_kernel = partial FFN-down sums per slot
 #ifndef MP_LTS_P
 #define MP_LTS_P 32
 #endif
@@ -54,7 +57,11 @@ enum Pro {
     PRO_LTFFN_MERGE = 12, // act = (sum over p of the LT_FFN_P partial FFN-down sums, p ascending)
                           //       + addsrc: the LT FFN output (lt_ffn_kernel, 983-992)
     PRO_LTS_MERGE = 13,   // the same over the LTS_P partial sums of lt_slot_kernel (bf16 mode, small batches)
+    PRO_LTQ_MERGE = 14,   // the same over the LTQ_P partial sums of lt_slot_q8_kernel (Q8_0 mode, batch 1)
 };
+// partial sums merged by the LT heads' merge prologues
+template <int PRO>
+constexpr int ltm_count() { return PRO == PRO_LTQ_MERGE ? LTQ_P : LT_FFN_P; }
 enum Epi {
     EPI_STORE = 0,      // out = v
     EPI_BIAS = 1,       // out = v + bias

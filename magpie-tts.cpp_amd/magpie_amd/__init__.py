@@ -99,6 +99,9 @@ SYMBOLS = [
     ("mp_hip_codec_error", ctypes.c_char_p, [_P]),
 ]
 
+# entry points added after round 4: absent from the A/B baseline libraries
+OPTIONAL = {"mp_hip_encode_text"}
+
 _lib = None
 
 
@@ -111,6 +114,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         raise MagpieError(f"{path} is missing: build it with `make -C {PKG_DIR}` (or __graft_entry__.build())")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, res, args in SYMBOLS:
+        if name in OPTIONAL and not hasattr(lib, name):
+            continue  # an older library (A/B runs against a previous round's build)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -79,14 +79,15 @@ struct ConvP {
 __device__ __forceinline__ float half_snake(float v, int c, int n_snake, int cin_real, const float *alpha) {
     // nano-codec.cpp:401-417 in ggml op order: mul, sin, sqr, div, add | leaky 0.01
     if (c < n_snake) {
-        // hardware sin (v_sin_f32) and a reciprocal instead of the libm sinf and an
-        // IEEE division: ~1e-7 relative, far below the f16 rounding every HalfSnake
-        // output gets next (the next conv's operand)
+        // hardware sin (v_sin_f32) and the hardware reciprocal (v_rcp_f32, 1 ulp) instead
+        // of the libm sinf and an IEEE division (__fdividef compiles to the full
+        // div_scale / div_fmas / div_fixup sequence here): ~1e-7 relative, far below the
+        // f16 rounding every HalfSnake output gets next (the next conv's operand)
         const float a = alpha[c];
         const float s = __sinf(v * a);
-        return v + __fdividef(s * s, a);
+        return v + (s * s) * __builtin_amdgcn_rcpf(a);
     }
-    if (c < cin_real) return v > 0.f ? v : 0.01f * v;
+    if (c < cin_real) return fmaxf(v, 0.01f * v);  // leaky 0.01: v > 0 ? v : 0.01 v
     return 0.f;
 }
 
@@ -94,8 +95,8 @@ __device__ __forceinline__ float half_snake(float v, int c, int n_snake, int cin
 // and selected (no divergent branch; same arithmetic as half_snake)
 __device__ __forceinline__ float half_snake_sel(float v, int c, int n_snake, int cin_real, float a) {
     const float s = __sinf(v * a);
-    const float snake = v + __fdividef(s * s, a);
-    const float leaky = v > 0.f ? v : 0.01f * v;
+    const float snake = v + (s * s) * __builtin_amdgcn_rcpf(a);  // 1 / a: loop-invariant per channel, hoisted
+    const float leaky = fmaxf(v, 0.01f * v);
     return c < n_snake ? snake : (c < cin_real ? leaky : 0.f);
 }
 

@@ -643,10 +643,14 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     __builtin_amdgcn_sched_barrier(0);
     float4 a1[UPW], a2[U / 4];
 #pragma unroll
-    for (int r = 0; r < UPW; ++r) a1[r] = ld_lt((const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane));
+    for (int r = 0; r < UPW; ++r) a1[r] = ld_ltffn((const float4 *)(p.f.w1 + (size_t)(j0 + w * UPW + r) * LTD + 4 * lane));
 #pragma unroll
-    for (int i = 0; i < U / 4; ++i) a2[i] = ld_lt((const float4 *)(p.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i));
+    for (int i = 0; i < U / 4; ++i) a2[i] = ld_ltffn((const float4 *)(p.f.w2 + (size_t)j0 * LTD + tid * U + 4 * i));
     __builtin_amdgcn_sched_barrier(0);
+    if (NB == 1 && p.f.ts && w == 0) {  // diagnostics: when wave 0's own loads (not the 8 weight loads) have landed
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        ts_phase<3>(p.f.ts, 0);
+    }
     for (int b = w; b < NB; b += MP_NWAVES) {
         const float4 y = b == w ? lt_y_finish(p, b, pb == 0, wsc_all[w], yp) : lt_y_slot(p, b, pb == 0, wsc_all[w]);
         if (b == 0) ts_phase<1>(p.f.ts, 0);  // profiling: y (gathers + attention)
@@ -743,10 +747,10 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
     __builtin_amdgcn_sched_barrier(0);
     uint2 a1[LTS_UPW];  // W1 rows u0 + LTS_UPW w + r, elements 4 lane .. 4 lane + 3
 #pragma unroll
-    for (int r = 0; r < LTS_UPW; ++r) a1[r] = ld_lt((const uint2 *)(p.w1h + (size_t)(u0 + w * LTS_UPW + r) * LTD + 4 * lane));
+    for (int r = 0; r < LTS_UPW; ++r) a1[r] = ld_ltffn((const uint2 *)(p.w1h + (size_t)(u0 + w * LTS_UPW + r) * LTD + 4 * lane));
     uint4 a2[LTS_U / 8];  // W2 row tid, units u0 .. u0 + LTS_U - 1
 #pragma unroll
-    for (int i = 0; i < LTS_U / 8; ++i) a2[i] = ld_lt((const uint4 *)(p.w2h + ((size_t)q * LTD + tid) * LTS_U + 8 * i));
+    for (int i = 0; i < LTS_U / 8; ++i) a2[i] = ld_ltffn((const uint4 *)(p.w2h + ((size_t)q * LTD + tid) * LTS_U + 8 * i));
     __builtin_amdgcn_sched_barrier(0);
     if (w == 0) {
         const float4 y = lt_y_finish(p, b, q == 0, wsc, yp);
@@ -981,9 +985,9 @@ __device__ __forceinline__ void lt_front_weights(const LtFrontP &p, int pb, int 
     }
 #pragma unroll
     for (int r = 0; r < LTF_UPW; ++r)
-        a1[r] = ld_lt((const float4 *)(p.l.f.w1 + (size_t)(j0 + w * LTF_UPW + r) * LTD + 4 * lane));
+        a1[r] = ld_ltffn((const float4 *)(p.l.f.w1 + (size_t)(j0 + w * LTF_UPW + r) * LTD + 4 * lane));
 #pragma unroll
-    for (int i = 0; i < LTF_U / 4; ++i) a2[i] = ld_lt((const float4 *)(p.l.f.w2 + (size_t)j0 * LTD + tid * LTF_U + 4 * i));
+    for (int i = 0; i < LTF_U / 4; ++i) a2[i] = ld_ltffn((const float4 *)(p.l.f.w2 + (size_t)j0 * LTD + tid * LTF_U + 4 * i));
 }
 __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     const unsigned long long t_start = ts_begin(p.l.f.ts);

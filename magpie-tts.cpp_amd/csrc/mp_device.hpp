@@ -404,6 +404,21 @@ __device__ __forceinline__ T ld_lt(const T *p) {
     return *p;
 #endif
 }
+// The LT FFN's W1 / W2 slices: read by the same workgroup index 8 times per frame (every
+// codebook's step), so the default cache policy keeps them on die between steps
+// (measured: lt_ffn2 6.24 -> 5.69 us at f32 batch 1, gpurun_out/r05b_ops_f32_b1_ltdef.txt);
+// MP_LTFFN_NT=1 restores the non-temporal loads.
+#ifndef MP_LTFFN_NT
+#define MP_LTFFN_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_ltffn(const T *p) {
+#if MP_LTFFN_NT
+    return ld_weight(p);
+#else
+    return *p;
+#endif
+}
 
 __device__ __forceinline__ float dotv(float4 a, float4 b) { return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x))); }
 __device__ __forceinline__ float dotv(float2 a, float2 b) { return fmaf(a.y, b.y, a.x * b.x); }

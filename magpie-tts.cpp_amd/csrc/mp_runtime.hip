@@ -905,7 +905,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
-    A(ltp, (size_t)NB * std::max(mp::LT_FFN_P, mp::LTS_P) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, 2 * 256); A(ltyg, (size_t)NB * 256);
+    A(ltp, (size_t)NB * std::max({mp::LT_FFN_P, mp::LTS_P, mp::LTQ_P}) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, 2 * 256); A(ltyg, (size_t)NB * 256);
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -2178,7 +2178,7 @@ int mp_hip_lt_sample(mp_dev *dev, const float *hidden, float temperature, int to
         int rc = MP_OK;
         if ((rc = al(&io.hidden, 768)) || (rc = al(&io.lt_s, 9 * 256)) || (rc = al(&io.ltX, 256)) ||
             (rc = al(&io.ltY, 256)) || (rc = al(&io.lty2, 256)) || (rc = al(&io.ltq, 256)) ||
-            (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) || (rc = al(&io.ltp, std::max(mp::LT_FFN_P, mp::LTS_P) * 256)) ||
+            (rc = al(&io.ltk, 8 * 256)) || (rc = al(&io.ltv, 8 * 256)) || (rc = al(&io.ltf, 1024)) || (rc = al(&io.ltp, std::max({mp::LT_FFN_P, mp::LTS_P, mp::LTQ_P}) * 256)) ||
 
             (rc = al(&io.logits, 2024)) || (rc = al(&io.codes_cur, 8)) || (rc = al(&io.step, 1)) ||
             (rc = al(&io.done, 1)) || (rc = al(&io.argeos, 1)) || (rc = al(&io.amax, 8)) || (rc = al(&io.cfg, 8)))

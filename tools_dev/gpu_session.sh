@@ -8,11 +8,12 @@
 #   tests?[=LIB]         the same, but a test failure (pytest rc 1) does not stop the chain
 #   bench                the default bench.py line -> TAG_bench.json
 #   ab=N:LIB[,LIB...]    alternating bench A/B: default library vs each ab_libs/LIB.so, N rounds
-#   ops=MODE:B[:LIB]     per-op dispatch intervals + wave spans (tools_dev/mode_ops.py)
+#   ops=MODE:B[:LIB[:K=V]]  per-op dispatch intervals + wave spans (tools_dev/mode_ops.py);
+#                        LIB "-" = the default library; K=V e.g. MODE_XA=direct, MODE_KV=bf16
 #   tl=MODE:B[:OPS]      in-kernel phase timeline (tools_dev/diag_timeline.py, PHASES=1); OPS comma-separated
 #   prof                 rocprofv3 kernel-trace summary of the bench (eager) + phase cut
 #   pmc                  PMC passes (tools_dev/pmc_collect.sh TAG)
-#   codec                codec-only bench leg (tools_dev/codec_latency.py)
+#   codec[=LIB]          codec wall / device time per call (tools_dev/codec_latency.py)
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out
@@ -42,11 +43,13 @@ for STEP in "$@"; do
       bash tools_dev/ab_lib.sh "${TAG}_ab" "$n" $(echo "$libs" | tr ',' '\n' | sed 's#^#ab_libs/#; s#$#.so#') > "$OUT/${TAG}_ab.txt" 2>&1
       cat "$OUT/${TAG}_ab.txt" ;;
     ops)
-      IFS=: read -r mode b lib <<< "$arg"
+      IFS=: read -r mode b lib kv <<< "$arg"
       env=()
-      [ -n "$lib" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$lib.so")
-      env "${env[@]}" timeout -k 10 200 python -u tools_dev/mode_ops.py "$mode" "$b" > "$OUT/${TAG}_ops_${mode}_b${b}${lib:+_$lib}.txt" 2>&1
-      head -1 "$OUT/${TAG}_ops_${mode}_b${b}${lib:+_$lib}.txt" ;;
+      [ -n "$lib" ] && [ "$lib" != "-" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$lib.so")
+      [ "$lib" = "-" ] && lib=""
+      suf="${lib:+_$lib}${kv:+_${kv//=/-}}"
+      env "${env[@]}" timeout -k 10 200 python -u tools_dev/mode_ops.py "$mode" "$b" $kv > "$OUT/${TAG}_ops_${mode}_b${b}${suf}.txt" 2>&1
+      head -1 "$OUT/${TAG}_ops_${mode}_b${b}${suf}.txt" ;;
     tl)
       IFS=: read -r mode b ops <<< "$arg"
       PHASES=1 timeout -k 10 200 python -u tools_dev/diag_timeline.py "$mode" "$b" $(echo "$ops" | tr ',' ' ') > "$OUT/${TAG}_tl_${mode}_b${b}.txt" 2>&1
@@ -60,6 +63,11 @@ for STEP in "$@"; do
     pmc)
       bash tools_dev/pmc_collect.sh "$TAG" > "$OUT/${TAG}_pmc.log" 2>&1
       echo "pmc ok" ;;
+    codec)
+      env=()
+      [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
+      env "${env[@]}" timeout -k 10 200 python -u tools_dev/codec_latency.py > "$OUT/${TAG}_codec${arg:+_$arg}.txt" 2>&1
+      cat "$OUT/${TAG}_codec${arg:+_$arg}.txt" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

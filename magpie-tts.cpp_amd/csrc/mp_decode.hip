@@ -487,11 +487,10 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_ffn_kernel(LtFfnP p) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const float4 xv = *(const float4 *)&xs[b][4 * lane];
+        float v[UPW];
 #pragma unroll
-        for (int r = 0; r < UPW; ++r) {
-            const float v = wave_sum(dotv(a1[r], xv));
-            if (lane == 0) fs[b][w * UPW + r] = gelu_tanh(v);
-        }
+        for (int r = 0; r < UPW; ++r) v[r] = dotv(a1[r], xv);
+        ffn_units_store<UPW>(v, &fs[b][w * UPW], [](float g) { return g; });
     }
     lds_sync();
 #pragma unroll
@@ -668,11 +667,10 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const float4 xv = *(const float4 *)&xs[b][4 * lane];
+        float v[UPW];
 #pragma unroll
-        for (int r = 0; r < UPW; ++r) {
-            const float v = wave_sum(dotv(a1[r], xv));
-            if (lane == 0) fs[b][w * UPW + r] = gelu_tanh(v);
-        }
+        for (int r = 0; r < UPW; ++r) v[r] = dotv(a1[r], xv);
+        ffn_units_store<UPW>(v, &fs[b][w * UPW], [](float g) { return g; });
     }
     lds_sync();
     ts_phase<2>(p.f.ts, 0);  // profiling: FFN up
@@ -767,11 +765,12 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
     }
     lds_sync();
     const float4 xv = *(const float4 *)&xs[4 * lane];
+    {
+        float v[LTS_UPW];
 #pragma unroll
-    for (int r = 0; r < LTS_UPW; ++r) {
-        const float4 wv = make_float4(bf16_lo(a1[r].x), bf16_hi(a1[r].x), bf16_lo(a1[r].y), bf16_hi(a1[r].y));
-        const float v = wave_sum(dotv(wv, xv));
-        if (lane == 0) hs[w * LTS_UPW + r] = bf16_round(gelu_tanh(v));
+        for (int r = 0; r < LTS_UPW; ++r)
+            v[r] = dotv(make_float4(bf16_lo(a1[r].x), bf16_hi(a1[r].x), bf16_lo(a1[r].y), bf16_hi(a1[r].y)), xv);
+        ffn_units_store<LTS_UPW>(v, &hs[w * LTS_UPW], [](float g) { return bf16_round(g); });
     }
     lds_sync();
     float acc = 0.f;
@@ -949,11 +948,10 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
     lds_sync();
     {
         const float4 xv = *(const float4 *)&xs[4 * lane];
+        float v[UPW];
 #pragma unroll
-        for (int r = 0; r < UPW; ++r) {
-            const float v = wave_sum(dotv(a1[r], xv));
-            if (lane == 0) fs[w * UPW + r] = gelu_tanh(v);
-        }
+        for (int r = 0; r < UPW; ++r) v[r] = dotv(a1[r], xv);
+        ffn_units_store<UPW>(v, &fs[w * UPW], [](float g) { return g; });
     }
     lds_sync();
     float acc = 0.f;

@@ -395,11 +395,10 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
     lds_sync();
     {
         const float4 xv = *(const float4 *)&xs[4 * lane];
+        float v[UWW];
 #pragma unroll
-        for (int r = 0; r < UWW; ++r) {
-            const float v = wave_sum(dotv(a1[r], xv));
-            if (lane == 0) fs[w * UWW + r] = gelu_tanh(v);
-        }
+        for (int r = 0; r < UWW; ++r) v[r] = dotv(a1[r], xv);
+        ffn_units_store<UWW>(v, &fs[w * UWW], [](float g) { return g; });
     }
     lds_sync();
     float acc[PPW];

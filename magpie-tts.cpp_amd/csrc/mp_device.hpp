@@ -64,6 +64,33 @@ __device__ __forceinline__ float wave_max(float v) {
                                                                     __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false)));
     return bcast_lane63(v);
 }
+// wave_sum of N values at once (value j: v[j]), the N DPP chains advanced in lockstep so
+// their dependent steps overlap; each total is wave_sum's exactly (same tree, same order).
+// Returns the totals uniformly in v.
+template <int N>
+__device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
+#define MP_WSN_STEP(...) _Pragma("unroll") for (int j = 0; j < N; ++j) v[j] += __VA_ARGS__(v[j]);
+    MP_WSN_STEP(dpp_mov<0xB1>)
+    MP_WSN_STEP(dpp_mov<0x4E>)
+    MP_WSN_STEP(dpp_mov<0x141>)
+    MP_WSN_STEP(dpp_mov<0x140>)
+    MP_WSN_STEP((dpp_mov<0x142, 0xA>))
+    MP_WSN_STEP((dpp_mov<0x143, 0xC>))
+#undef MP_WSN_STEP
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = bcast_lane63(v[j]);
+}
+// full-wave minimum of a non-negative int, returned uniformly (DPP, no LDS)
+__device__ __forceinline__ int wave_min_u(int v) {
+    auto step = [&](int x) { return x < v ? x : v; };
+    v = step(__builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));
+    v = step(__builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));
+    v = step(__builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
+    v = step(__builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
+    v = step(__builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false));
+    v = step(__builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
 // sum over lanes that differ only in the low log2(W) bits (W = 16 or 32)
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
@@ -336,6 +363,21 @@ __device__ __forceinline__ void wave_argmax(float &v, int &i) {
 __device__ __forceinline__ float gelu_tanh(float x) {
     // ggml_gelu: 0.5 x (1 + tanh(sqrt(2/pi) x (1 + 0.044715 x^2)))
     return 0.5f * x * (1.0f + tanhf(0.79788456080286535588f * x * (1.0f + 0.044715f * x * x)));
+}
+// One wave's FFN-up units: v[r] holds this lane's part of unit r's dot product; the N
+// totals (wave_sum_n: wave_sum's tree for each) go through GELU on lanes 0..N-1 in
+// parallel, lane r storing post(gelu(unit r)) to dst[r] (before: N wave sums and N GELUs
+// in sequence on lane 0 behind exec masks). Same value per unit.
+template <int N, typename F>
+__device__ __forceinline__ void ffn_units_store(float (&v)[N], float *dst, F post) {
+    static_assert(N <= 64, "one lane per unit");
+    wave_sum_n<N>(v);
+    const int lane = threadIdx.x & 63;
+    float mine = v[0];
+#pragma unroll
+    for (int r = 1; r < N; ++r)
+        if (lane == r) mine = v[r];
+    if (lane < N) dst[lane] = post(gelu_tanh(mine));
 }
 
 template <int VW> struct vecf;

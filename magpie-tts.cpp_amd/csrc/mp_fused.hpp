@@ -40,22 +40,28 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
                                   const Sampling &smp, int stream, int step, int cb, float *scratch, int &amax) {
     const int lane = threadIdx.x & 63;
     constexpr int R = PICK_R;
-    // masked first-max argmax: the wave's max by DPP, then the first index holding it
-    // (ballots in index order: r-major, lane-minor = ascending i)
+    // masked first-max argmax. The forbidden ids (audio_bos .. audio_bos + 7 but EOS, and
+    // the padding past VCB) lie in the rows r whose 64 ids reach audio_bos or VCB: a
+    // uniform (scalar) test per row skips the per-lane mask everywhere else. Then the
+    // wave's max by DPP, and the first index holding it as the wave's minimum of each
+    // lane's first matching index (VALU compares and one DPP min: no ballot / scalar
+    // round trip per row). Same value and index as a scan of i = 0, 1, ... with '>'.
+    const int lo = audio_bos < VCB ? audio_bos : VCB;
     float bv = -INFINITY;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int i = lane + 64 * r;
-        if (i >= VCB || (i >= audio_bos && i <= audio_bos + 7 && (i != audio_eos || forbid_eos))) lv[r] = -INFINITY;
+        if (64 * r + 63 >= lo) {  // uniform
+            const int i = lane + 64 * r;
+            if (i >= VCB || ((unsigned)(i - audio_bos) <= 7u && (i != audio_eos || forbid_eos))) lv[r] = -INFINITY;
+        }
         bv = fmaxf(bv, lv[r]);
     }
     bv = wave_max(bv);
-    int bi = VCB;
+    int first = 1 << 30;
 #pragma unroll
-    for (int r = R - 1; r >= 0; --r) {
-        const unsigned long long bal = __ballot(lv[r] == bv);
-        if (bal) bi = 64 * r + __builtin_ctzll(bal);
-    }
+    for (int r = R - 1; r >= 0; --r)
+        if (lv[r] == bv) first = lane + 64 * r;
+    int bi = wave_min_u(first);
     if (bi < 0 || bi >= VCB) bi = 0;
     amax = bi;
     if (!smp.on) return bi;

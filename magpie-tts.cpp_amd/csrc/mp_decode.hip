@@ -504,7 +504,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_ffn_kernel(LtFfnP p) {
             acc = fmaf(a2[i].z, f4.z, acc);
             acc = fmaf(a2[i].w, f4.w, acc);
         }
-        p.part[((size_t)b * LT_FFN_P + blockIdx.x) * LTD + tid] = acc;
+        p.part[ltp_idx(b, blockIdx.x, tid)] = acc;
     }
 }
 template <int NB>
@@ -596,11 +596,13 @@ __device__ __forceinline__ float4 lt_y_finish(const LtFfn2P &p, int b, bool wb0,
         *(float4 *)(p.ltk + row + cb * LTD) = k4;
         *(float4 *)(p.ltv + row + cb * LTD) = vo4;
     }
+    // the cb + 1 scores' wave sums advanced together (wave_sum_n: each wave_sum's tree)
     float sj[NCB];
 #pragma unroll
-    for (int j = 0; j < NCB; ++j)
-        sj[j] = j < cb ? wave_sum(dotv(q4, to_f4(r.kr[j < NCB - 1 ? j : 0]))) * (1.0f / 16.0f)
-                       : j == cb ? wave_sum(dotv(q4, k4)) * (1.0f / 16.0f) : -INFINITY;
+    for (int j = 0; j < NCB; ++j) sj[j] = dotv(q4, j < cb ? to_f4(r.kr[j < NCB - 1 ? j : 0]) : k4);
+    wave_sum_n<NCB>(sj);
+#pragma unroll
+    for (int j = 0; j < NCB; ++j) sj[j] = j <= cb ? sj[j] * (1.0f / 16.0f) : -INFINITY;
     float m = -INFINITY;
 #pragma unroll
     for (int j = 0; j < NCB; ++j) m = fmaxf(m, sj[j]);
@@ -694,7 +696,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_ffn2_kernel(LtFfn2P p) {
     float accs[NB];
     lt_step_body<NB>(p, blockIdx.x, ts_dep(t_start), accs, nullptr);
 #pragma unroll
-    for (int b = 0; b < NB; ++b) p.f.part[((size_t)b * LT_FFN_P + blockIdx.x) * LTD + threadIdx.x] = accs[b];
+    for (int b = 0; b < NB; ++b) p.f.part[ltp_idx(b, blockIdx.x, threadIdx.x)] = accs[b];
     ts_end(p.f.ts, t_start);
 }
 
@@ -1009,7 +1011,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
     lt_front_weights(p, pb, n_in, wi, wk, wv, a1, a2);
     __builtin_amdgcn_sched_barrier(0);
     const float acc = lt_front_core(p, pb, n_in, wi, wk, wv, a1, a2, v, g, act, act2, xs, fs, nullptr, nullptr);
-    if (pb < LT_FFN_P) p.l.f.part[(size_t)pb * LTD + tid] = acc;
+    if (pb < LT_FFN_P) p.l.f.part[ltp_idx(0, pb, tid)] = acc;
     ts_end(p.l.f.ts, t_start);
 }
 hipError_t op_lt_front(const LtFrontP &p, hipStream_t s) {

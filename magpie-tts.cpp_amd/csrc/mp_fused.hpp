@@ -46,16 +46,25 @@ __device__ inline int wave_pick_v(float (&lv)[PICK_R], bool forbid_eos, int audi
     // wave's max by DPP, and the first index holding it as the wave's minimum of each
     // lane's first matching index (VALU compares and one DPP min: no ballot / scalar
     // round trip per row). Same value and index as a scan of i = 0, 1, ... with '>'.
-    const int lo = audio_bos < VCB ? audio_bos : VCB;
-    float bv = -INFINITY;
+    // The reference's ids (magpie.h: audio_bos = 2016 = VCB - 8) put every forbidden id
+    // in the last row, lanes (VCB - 8) % 64 .. 63: that row alone is masked, with lane
+    // arithmetic only (a per-row mask mixing VALU compares and scalar logic cost ~0.8 us).
+    // Any other audio_bos takes the general per-row mask (uniform branch).
+    constexpr int RL = (VCB - 8) / 64, LL = (VCB - 8) % 64;
+    static_assert(RL == R - 1 && (VCB - 1) / 64 == RL, "the 8 special ids and the padding share the last row");
+    if (audio_bos == VCB - 8) {
+        const int i = lane + 64 * RL;
+        if (lane >= LL && (i >= VCB || i != audio_eos || forbid_eos)) lv[RL] = -INFINITY;
+    } else {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (64 * r + 63 >= lo) {  // uniform
+        for (int r = 0; r < R; ++r) {
             const int i = lane + 64 * r;
             if (i >= VCB || ((unsigned)(i - audio_bos) <= 7u && (i != audio_eos || forbid_eos))) lv[r] = -INFINITY;
         }
-        bv = fmaxf(bv, lv[r]);
     }
+    float bv = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < R; ++r) bv = fmaxf(bv, lv[r]);
     bv = wave_max(bv);
     int first = 1 << 30;
 #pragma unroll
@@ -206,12 +215,28 @@ __device__ __forceinline__ float4 lt_attend(const GemvP &p, int b, float4 q4, fl
 // LT FFN output element k of slot b: the LT_FFN_P partial FFN-down sums added in
 // ascending order, then the residual (the same arithmetic in the head's prologue
 // at batch 1 and in lt_merge_kernel otherwise)
-template <int NP = LT_FFN_P>
+// The LT_FFN_P partial FFN-down sums of the f32 / F16 LT are stored 4 partials interleaved
+// per output, [b][p / 4][k][p % 4]: a merge loads 4 consecutive partials of output k as one
+// float4 (16 loads per thread at batch 1 instead of 64; the sum order is unchanged).
+__device__ __forceinline__ size_t ltp_idx(int b, int p, int k) {
+    static_assert(LT_FFN_P % 4 == 0, "4 interleaved partials");
+    return (((size_t)b * (LT_FFN_P / 4) + p / 4) * LTD + k) * 4 + (p & 3);
+}
+// ILV: the interleaved layout above (LT_FFN_P partials); else [b][p][k] (the Q8_0 step's LTQ_P)
+template <int NP = LT_FFN_P, bool ILV = true>
 __device__ __forceinline__ float lt_ffn_merge(const float *part, const float *y, int b, int k) {
-    const float *pp = part + (size_t)b * NP * LTD + k;
-    float s = pp[0];
+    float s;
+    if constexpr (ILV) {
+        static_assert(NP == LT_FFN_P, "interleaved layout");
+        s = part[ltp_idx(b, 0, k)];
 #pragma unroll
-    for (int q = 1; q < NP; ++q) s += pp[(size_t)q * LTD];
+        for (int q = 1; q < NP; ++q) s += part[ltp_idx(b, q, k)];
+    } else {
+        const float *pp = part + (size_t)b * NP * LTD + k;
+        s = pp[0];
+#pragma unroll
+        for (int q = 1; q < NP; ++q) s += pp[(size_t)q * LTD];
+    }
     return s + y[(size_t)b * LTD + k];
 }
 
@@ -577,10 +602,17 @@ __device__ __forceinline__ void pre_load(const GemvP &p, PreRows<NB, K, PRO> &pr
             }
         }
         if constexpr (!SA) load_lnw<K / 64>(p.lnw, pr.g);
-    } else if constexpr (PRO == PRO_LTFFN_MERGE || PRO == PRO_LTQ_MERGE) {
+    } else if constexpr (PRO == PRO_LTFFN_MERGE) {
+#pragma unroll
+        for (int q = 0; q < LT_FFN_P; q += 4) {
+            const f32x4 v = *(const f32x4 *)(p.part + ltp_idx(0, q, tid));
+            pr.pp[q] = v.x; pr.pp[q + 1] = v.y; pr.pp[q + 2] = v.z; pr.pp[q + 3] = v.w;
+        }
+        pr.y = p.addsrc[tid];
+    } else if constexpr (PRO == PRO_LTQ_MERGE) {
         const float *pp = p.part + tid;
 #pragma unroll
-        for (int q = 0; q < ltm_count<PRO>(); ++q) pr.pp[q] = pp[(size_t)q * LTD];
+        for (int q = 0; q < LTQ_P; ++q) pr.pp[q] = pp[(size_t)q * LTD];
         pr.y = p.addsrc[tid];
     }
 }
@@ -719,7 +751,7 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
     } else if constexpr (PRO == PRO_LTFFN_MERGE || PRO == PRO_LTQ_MERGE) {
         static_assert(K == LTD, "LT is 256 wide");
         for (int e = tid; e < NB * K; e += MP_BLOCK)
-            act[e] = lt_ffn_merge<ltm_count<PRO>()>(p.part, p.addsrc, e / K, e % K);
+            act[e] = lt_ffn_merge<ltm_count<PRO>(), PRO == PRO_LTFFN_MERGE>(p.part, p.addsrc, e / K, e % K);
         lds_sync();
     } else if constexpr (PRO == PRO_LTS_MERGE) {
         static_assert(K == LTD, "LT is 256 wide");

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
 // RED (p.wot set): every workgroup computes all 256 o_net rows itself (thread t row t,
 // from the transposed copy: 16 coalesced 16-byte loads, L2-resident after the first
 // workgroup), so y needs no hand-off. DEFER (p.part set, batch 1): the partial FFN-down
-// sums are plain stores and the Q8_0 head's prologue merges them (PRO_LTFFN_MERGE: the
+// sums are plain stores and the Q8_0 head's prologue merges them (PRO_LTQ_MERGE: the
 // same p-ascending sum, then + y), so the launch has no hand-off at all. Every variant
 // computes the same bits: the o_net row is the block-ordered sum of (int dot) x (d_w d_a)
 // from 0, the merge sums the LTQ_P partials in ascending p, then adds y.
@@ -1109,5 +1109,8 @@ hipError_t q8_lt_bo_8(const GemvP &p, hipStream_t s) { return launch_q8<8, LTD, 
 hipError_t q8_lt_bo_16(const GemvP &p, hipStream_t s) { return launch_q8<16, LTD, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 // the LT head at batch 1 with the LT FFN merge as its prologue (lt_ffn_kernel)
 hipError_t q8_lt_em_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, PRO_LTQ_MERGE, EPI_BIAS>(p, s); }
+// the same head after lt_ffn_kernel (the standalone LT sample of a Q8_0 file): its LT_FFN_P
+// partials are interleaved (ltp_idx)
+hipError_t q8_lt_emf_1(const GemvP &p, hipStream_t s) { return launch_q8<1, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 
 }  // namespace mp

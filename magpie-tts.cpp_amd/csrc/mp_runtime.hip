@@ -99,6 +99,7 @@ hipError_t pack_q8(const signed char *, const unsigned short *, int, int, unsign
 hipError_t pack_q4(const signed char *, int, int, unsigned char *, hipStream_t);
 hipError_t q8_lt_inh_1(const GemvP &, hipStream_t);
 hipError_t q8_lt_em_1(const GemvP &, hipStream_t);
+hipError_t q8_lt_emf_1(const GemvP &, hipStream_t);
 hipError_t op_lt_pick(const GemvP &, int, hipStream_t);
 hipError_t op_embed(const EmbP &, int, hipStream_t);
 hipError_t op_lt_bo_8(const GemvP &, hipStream_t);
@@ -1486,9 +1487,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             g.Wd = (const unsigned short *)((const char *)m.lt_out8.pd + (size_t)cb * q8p_head_d());
         }
         mp::GemvFn efn = m.lt_out8 ? tq.lt_e : tb.lt_e;
-        if (ffn1 && NB == 1) {  // the FFN merge is the head's prologue
+        if (ffn1 && NB == 1) {  // the FFN merge (lt_ffn_kernel's interleaved partials) is the head's prologue
             g.part = io.ltp; g.addsrc = io.ltY;
-            efn = m.lt_out8 ? mp::q8_lt_em_1 : mp::op_lt_em_1;
+            efn = m.lt_out8 ? mp::q8_lt_emf_1 : mp::op_lt_em_1;
         }
         if ((rc = run("lt_e", efn, g,
                       (m.lt_out8 ? Fq(m.lt_out8) : F) * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)

@@ -456,7 +456,14 @@ def main() -> None:
         nall = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
         if nall != args.cpu_threads:
             ra = orc.time_decode_fps(model_path, toks[0], args.frames, threads=nall, acc64=False)
-            cpu["all_cores"] = {"value": round(ra["frames"] / ra["decode_s"], 2), "cores": nall}
+            try:
+                visible = len(os.sched_getaffinity(0))
+            except (AttributeError, OSError):
+                visible = os.cpu_count() or 1
+            cpu["all_cores"] = {"value": round(ra["frames"] / ra["decode_s"], 2), "cores": nall,
+                                "note": f"the lease's CPU share: OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', '-')}, "
+                                        f"{visible} CPUs in this process's affinity mask, "
+                                        f"{os.cpu_count()} on the machine"}
 
     # ---- the other BASELINE configs' shapes on this GPU (rank 0 at N=1 only)
     extra = None

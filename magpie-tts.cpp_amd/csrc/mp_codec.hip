@@ -53,6 +53,14 @@ constexpr int RATE[5] = {8, 8, 4, 2, 2};
 constexpr int KS[3] = {3, 7, 11};
 constexpr int DIL[3] = {1, 3, 5};
 constexpr int HOP = 1024;
+// LDS bytes per time row of a 32-channel f16 operand block: 64 B of data + 16 B of pad.
+// Measured and kept (round 5): a B fragment is one ds_read_b128 per lane at row base + l16,
+// byte 16 kg; by the 16-lane groups gfx950 serves a ds_read_b128 in (MI355X_MICROARCH.md
+// §LDS) an 80-byte row stride puts 3 lanes of each group on a taken bank quad and 96 bytes
+// none, yet 96 made the codec slower (8 x 32 frames 1.620 -> 1.637 / 1.654 ms, rb_kernel at
+// 64 channels 322 -> 345 us; gpurun_out/r05h_codec*.txt): the A-fragment stream and the
+// workgroups per CU, not LDS reads, bound these kernels.
+constexpr int LDS_ROWB = 80;
 
 enum InMode { IN_F16 = 0, IN_FSQ = 1 };
 
@@ -118,7 +126,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     constexpr int CWN = 4 / RW;          // column groups
     constexpr int WCOLS = BN / CWN;      // columns per wave
     constexpr int NT = WCOLS / 16;       // MFMA column tiles per wave
-    constexpr int ROWB = 80;             // LDS bytes per time row: 32 halves + 16 B pad
+    constexpr int ROWB = LDS_ROWB;       // LDS bytes per time row: 32 halves + pad
     constexpr int MAXHALO = 50;          // (11 - 1) * 5
     __shared__ __attribute__((aligned(16))) char xs[PIPE ? 2 : 1][(BN + MAXHALO) * ROWB];
 
@@ -278,7 +286,7 @@ template <int KS, int RWV, int CWV, int NCB, int R>
 __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
     constexpr int NTH = 64 * RWV * CWV;
     constexpr int BN = CWV * 16 * C2_NT;
-    constexpr int ROWB = 80;             // LDS bytes per time row: 32 halves + 16 B pad
+    constexpr int ROWB = LDS_ROWB;       // LDS bytes per time row: 32 halves + pad
     constexpr int MAXHALO = 50;          // (11 - 1) * 5
     constexpr int BUFB = (BN + MAXHALO) * ROWB;
     constexpr int RPT = ((BN + MAXHALO) * 4 + NTH - 1) / NTH;  // 16-byte row pieces per thread
@@ -419,7 +427,7 @@ __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
 template <int RWV, int CWV, int NCB, bool DEEP>
 __global__ __launch_bounds__(64 * RWV * CWV, DEEP ? 1 : 2) void conv2_kernel(ConvP p) {
     constexpr int BN = CWV * 16 * C2_NT;
-    constexpr int XSB = 2 * (BN + 50) * 80, CTB = BN * (RWV * 32 + 4) * 4;  // input buffers / epilogue tile
+    constexpr int XSB = 2 * (BN + 50) * LDS_ROWB, CTB = BN * (RWV * 32 + 4) * 4;  // input buffers / epilogue tile
     __shared__ __attribute__((aligned(16))) char xs[XSB > CTB ? XSB : CTB];
     switch (p.ks[blockIdx.z]) {
         case 3: conv2_body<3, RWV, CWV, NCB, DEEP ? 6 : 3>(p, xs); break;
@@ -455,7 +463,7 @@ struct RbP {
     int ks[3];
     int nsnake, creal, T, dil, tiles_per_chunk;
 };
-constexpr int RB_ROWB = 80;   // LDS bytes per time row of a 32-channel block
+constexpr int RB_ROWB = LDS_ROWB;  // LDS bytes per time row of a 32-channel block
 constexpr int RB_MAXHALO = 50;  // (11 - 1) * 5
 
 template <int RWV, int CWV, int NT>

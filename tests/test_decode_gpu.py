@@ -397,16 +397,23 @@ def test_f32_mode_rejects_batch_16(ma, small_model):
 # an oracle margin < 0.1, and at most 5 % of decisions may differ (the hidden-state
 # bar below is the precise check of the arithmetic).
 Q8_TIE_EPS = 1e-1
-Q8_HIDDEN_TOL = BF16_HIDDEN_TOL
-Q8_HIDDEN_REL = BF16_HIDDEN_REL
+# Hidden-state bars per case, ~2-4x the error each case measures (printed by every test;
+# gpurun_out/r05f_tests.log): small Q8 2.3e-3 / 6.7e-4, Q4 8.1e-3 / 2.2e-3, sampled
+# 5.5e-3 / 1.6e-3, full Q8 1.7e-2 / 4.5e-3 (max abs / max relative L2 over the steps).
+# The error is a few activation-quantisation flips, not drift: the median step's error
+# is printed beside the maximum.
+Q8_BARS = {"small": (1e-2, 3e-3), "q4": (2e-2, 5e-3), "sampled": (1.5e-2, 4e-3), "full": (3e-2, 5e-3)}
 
 
-def _check_hidden_q8(h_gpu, h_orc):
-    err = np.abs(h_gpu - h_orc).max()
+def _check_hidden_q8(h_gpu, h_orc, case):
+    tol, rtol = Q8_BARS[case]
+    per_step = np.abs(h_gpu - h_orc).max(axis=-1)
+    err = per_step.max()
     rel = _rel_l2(h_gpu, h_orc)
-    print(f"Q8 hidden vs oracle mode 2: max abs err {err:.3g}, max relative L2 {rel.max():.3g} over {len(h_gpu)} steps")
-    assert err < Q8_HIDDEN_TOL, f"hidden max abs err {err}"
-    assert rel.max() < Q8_HIDDEN_REL, f"hidden rel L2 err {rel.max()}"
+    print(f"Q8 hidden vs oracle mode 2 ({case}): max abs err {err:.3g} (median step {np.median(per_step):.3g}), "
+          f"max relative L2 {rel.max():.3g} over {len(h_gpu)} steps; bars {tol:g} / {rtol:g}")
+    assert err < tol, f"hidden max abs err {err}"
+    assert rel.max() < rtol, f"hidden rel L2 err {rel.max()}"
     return err
 
 
@@ -428,13 +435,13 @@ def test_q8_small_model_matches_oracle(ma, oracle, q8_model):
     free-running comparison ends at the first quantisation-sensitive decision."""
     tok = ma.synthetic_tokens(24, seed=1000)
     r, o = _q8_forced(ma, oracle, q8_model, tok, steps=40, speaker=1)
-    _check_hidden_q8(r.hidden[0, :41], o["hidden"])
+    _check_hidden_q8(r.hidden[0, :41], o["hidden"], "small")
 
 
 def test_q8_full_model_matches_oracle(ma, oracle, q8_full_model):
     tok = ma.synthetic_tokens(64, seed=1000)
     r, o = _q8_forced(ma, oracle, q8_full_model, tok, steps=24)
-    _check_hidden_q8(r.hidden[0, :25], o["hidden"])
+    _check_hidden_q8(r.hidden[0, :25], o["hidden"], "full")
     assert r.n_frames[0] == 24
 
 
@@ -468,16 +475,69 @@ def test_q8_batch_equals_single(ma, q8_model, B):
 
 
 def test_q8_sampling_matches_oracle(ma, oracle, q8_model):
-    """Sampled Q8 decisions are the most fragile of all: the oracle's own
-    f32-accumulating mode, teacher forced along its f64 run of this case, differs at
-    69 of 192 sampled decisions (the draw lands within ~4e-3 of an interval boundary
-    at the median). Bar: each differing decision has an oracle margin < Q8_TIE_EPS and
-    no more differ than that spread (50 %); the exact checks of Q8 sampling are the
-    batch-invariance tests (test_sampled_batch_equals_single[q8-*]). The arithmetic
-    under the draws is held to the Q8 hidden-state bars at every forced step."""
+    """Sampled Q8 decisions against the oracle's Q8_0 mode, teacher forced. They are
+    the most fragile of all: the oracle's own f32-accumulating mode, teacher forced
+    along its f64 run of this case, differs at 69 of 192 sampled decisions (a draw
+    lands within ~4e-3 of an interval boundary at the median, and the activation
+    quantiser's flips move the logits by ~1e-2). So here every differing decision
+    needs an oracle margin < Q8_TIE_EPS and the count is only a sanity bound (50 %);
+    the arithmetic under the draws is held to the Q8 hidden-state bars at every forced
+    step, and the draws themselves exactly by test_q8_sampling_draws_exact."""
     tok = ma.synthetic_tokens(12, seed=41)
     r, o = _q8_forced(ma, oracle, q8_model, tok, steps=24, tie_frac=0.5, temperature=0.7, top_k=80, seed=77)
-    _check_hidden_q8(r.hidden[0, :25], o["hidden"])
+    _check_hidden_q8(r.hidden[0, :25], o["hidden"], "sampled")
+
+
+def test_q8_sampling_draws_exact(ma, oracle, q8_model, tmp_path):
+    """Every sampled Q8 decision recomputed from the logits the GPU's Q8_0 heads
+    produced (MAGPIE_DUMP_LT, eager): the oracle's sample_top_k (magpie.cpp:1072-1109,
+    after the 1133-1145 mask) on those logits with the same counter-stream draw
+    u(seed, slot, step, cb) picks the GPU's code, decision for decision. This checks the
+    device's top-k (radix select, compaction, rank, sequential sum / cumsum) exactly,
+    apart from the logits' own numeric spread (test_q8_sampling_matches_oracle)."""
+    import os
+    steps, T, K, seed = 12, 0.7, 80, 77
+    dump = str(tmp_path / "lt_q8_sampled.bin")
+    env = {"MAGPIE_EAGER": "1", "MAGPIE_DUMP_LT": dump}
+    os.environ.update(env)
+    try:
+        dev = ma.Device(q8_model, weights="q8")
+        r = dev.synthesize([ma.synthetic_tokens(12, seed=41)], max_dec_steps=steps, ignore_eos=True,
+                           temperature=T, top_k=K, seed=seed)
+        dev.close()
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    rec = np.fromfile(dump, dtype=np.float32).reshape(-1, 2024 + 8 + 4 * 256)
+    # per iteration: the in_proj, position 0's q|k|v, then (LT step, head) for codebooks
+    # 0..7 (the loop may run an iteration past the last frame)
+    per = 18
+    assert rec.shape[0] % per == 0 and rec.shape[0] >= per * steps, rec.shape
+    codes = np.asarray(r.codes[0]).reshape(-1, 8)
+    assert codes.shape[0] == steps
+    cur = rec[:, 2024:2032].view(np.int32)
+    # the iteration of frame st: LT step cb + 1 holds codebook cb's pick (codes_cur)
+    nit = rec.shape[0] // per
+    picks = np.stack([[cur[per * i + 2 + 2 * (cb + 1), cb] for cb in range(7)] for i in range(nit)])
+    its = []
+    for st in range(steps):
+        cand = [i for i in range(its[-1] + 1 if its else 0, nit) if np.array_equal(picks[i], codes[st, :7])]
+        assert cand, f"no LT record block holds frame {st}'s codes {codes[st]} (picks {picks[:3]})"
+        its.append(cand[0])
+    bos, eos = 2016, 2017
+    close = []
+    for st in range(steps):
+        for cb in range(8):
+            lg = rec[per * its[st] + 3 + 2 * cb, :2024].astype(np.float32).copy()
+            lg[bos:bos + 8] = -np.inf  # ignore_eos: EOS masked too
+            u = oracle.draw_u(seed, 0, st, cb)
+            pick, mg = oracle.sample_top_k(lg, T, K, u)
+            if pick != codes[st, cb]:
+                assert mg < 1e-5, f"frame {st} cb {cb}: gpu {codes[st, cb]} oracle {pick} (margin {mg:.3g})"
+                close.append(mg)
+    print(f"Q8 sampled draws: {steps * 8} decisions recomputed from the GPU's logits, "
+          f"{len(close)} differ (all within 1e-5 of an interval boundary)")
+    assert len(close) <= 1
 
 
 def test_q4_small_model_matches_oracle(ma, oracle, q4_model):
@@ -486,7 +546,7 @@ def test_q4_small_model_matches_oracle(ma, oracle, q4_model):
     oracle's weight mode 2 on the same file, with the Q8 bars."""
     tok = ma.synthetic_tokens(24, seed=1000)
     r, o = _q8_forced(ma, oracle, q4_model, tok, steps=40, speaker=1)
-    _check_hidden_q8(r.hidden[0, :41], o["hidden"])
+    _check_hidden_q8(r.hidden[0, :41], o["hidden"], "q4")
 
 
 @pytest.mark.parametrize("B", [3, 16])

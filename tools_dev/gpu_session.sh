@@ -14,6 +14,7 @@
 #   prof                 rocprofv3 kernel-trace summary of the bench (eager) + phase cut
 #   pmc                  PMC passes (tools_dev/pmc_collect.sh TAG)
 #   codec[=LIB]          codec wall / device time per call (tools_dev/codec_latency.py)
+#   cprof[=LIB]          rocprofv3 kernel trace of 3 codec decodes, per-dispatch table of the last
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out
@@ -68,6 +69,14 @@ for STEP in "$@"; do
       [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
       env "${env[@]}" timeout -k 10 200 python -u tools_dev/codec_latency.py > "$OUT/${TAG}_codec${arg:+_$arg}.txt" 2>&1
       cat "$OUT/${TAG}_codec${arg:+_$arg}.txt" ;;
+    cprof)
+      env=()
+      [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
+      d="$OUT/${TAG}_cprof${arg:+_$arg}"
+      MAGPIE_LIB="${env[0]#MAGPIE_LIB=}" timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$d" -o prof \
+        -- python3 -u tools_dev/codec_prof.py > "$d.log" 2>&1
+      python3 tools_dev/codec_trace_report.py "$d/prof_kernel_trace.csv" > "$d.txt"
+      tail -12 "$d.txt" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

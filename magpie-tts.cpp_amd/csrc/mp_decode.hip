@@ -207,18 +207,48 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
         if (done) gather(p.codes_prev + b * NCB, p.pos[b], NCB, s, pe);
         else gather(p.codes_cur + b * NCB, p.pos[b] + 1, NCB - 1, s, pe);
     }
+    // greedy: codebook 7's pick split over the 4 waves (lt_step_body's split pick: each
+    // wave scans PICK_R / 4 logit rows, the pairs meet in LDS; the same code)
+    static_assert(FIN_THREADS / 64 == MP_NWAVES, "the split pick's rows per wave");
+    const bool quad = !p.smp.on;
+    float lq[QPR];
+    int stp_q = 0;
+    if (quad) {
+        const float *lg = p.logits + (size_t)b * VCB + ts_dep(t_start);
+#pragma unroll
+        for (int q = 0; q < QPR; ++q) {
+            const int i = (tid & 63) + 64 * (w * QPR + q);
+            lq[q] = i < VCB ? lg[i] : -INFINITY;
+        }
+        stp_q = p.step[b];
+    }
     __shared__ int sh_adv, sh_code, sh_stop;
-    __syncthreads();  // every read of pos / codes above precedes wave 0's updates
+    __syncthreads();  // every read of pos / codes / step above precedes wave 0's updates
     if (done) {
         if (embed && w >= 1) store_x(s, pe);
         return;
     }
+    int i0 = 0, amax = 0;
+    if (quad) {
+        __shared__ float qv[FIN_THREADS / 64];
+        __shared__ int qi[FIN_THREADS / 64];
+        float bv;
+        int bi = wave_pick_rows(lq, w, p.ignore_eos || stp_q < 4, p.audio_bos, p.audio_eos, bv);
+        if (bi < 0 || bi >= VCB) bi = 0;
+        if ((tid & 63) == 0) { qv[w] = bv; qi[w] = bi; }
+        __syncthreads();
+        float gm = qv[0];
+        i0 = qi[0];
+#pragma unroll
+        for (int u = 1; u < FIN_THREADS / 64; ++u)
+            if (qv[u] > gm) { gm = qv[u]; i0 = qi[u]; }
+        amax = i0;
+    }
     if (w == 0) {
         // codebook 7's pick with the same wave_pick as every other codebook (masked
         // first-max argmax; top-k draw when sampling); lane 0 keeps the books
-        __shared__ float scratch[2 * VCB];
-        int i0, amax;
-        {
+        if (!quad) {
+            __shared__ float scratch[2 * VCB];
             const int stp = p.step[b];
             i0 = wave_pick(p.logits + (size_t)b * VCB + ts_dep(t_start), p.ignore_eos || stp < 4, p.audio_bos,
                            p.audio_eos, p.smp, b, stp, NCB - 1, scratch, amax);
@@ -569,24 +599,29 @@ __device__ __forceinline__ void lt_y_load(const LtFfn2P &p, int b, LtYPre &r) {
     load_logits(p.logits + (size_t)b * VCB, r.lv);
     r.stp = p.step[b];
 }
-__device__ __forceinline__ float4 lt_y_finish(const LtFfn2P &p, int b, bool wb0, float *wsc, LtYPre &r) {
+// position cb's table rows for `code` (codebook cb-1's pick): q | k, o_net(v), P[code]
+// and the position embedding
+struct LtRows {
+    float4 q4, k4, vo4, x4, pos4;
+};
+__device__ __forceinline__ LtRows lt_gather(const LtFfn2P &p, int code) {
     const int lane = threadIdx.x & 63, cb = p.cb;
-    const size_t row = (size_t)b * NCB * LTD + 4 * lane;
-    if (cb == 0) {
-        const float4 x = to_f4(r.kr[0]), v = to_f4(r.vr[0]);
-        return make_float4(x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w);
-    }
-    const int stp = r.stp;
-    int amax;
-    const int code = wave_pick_v(r.lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, cb - 1, wsc,
-                                 amax);
-    ts_phase<0>(p.f.ts, 0);  // profiling: code picked
     const size_t rr = (size_t)(cb - 1) * VCB + code;
     const float *qkv = p.qkvtab + rr * (3 * LTD) + 4 * lane;
-    const float4 q4 = *(const float4 *)qkv, k4 = *(const float4 *)(qkv + LTD);
-    const float4 vo4 = *(const float4 *)(p.votab + rr * LTD + 4 * lane);
-    const float4 x4 = *(const float4 *)(p.ptab + rr * LTD + 4 * lane);
-    const float4 pos4 = *(const float4 *)(p.lt_pos + (size_t)cb * LTD + 4 * lane);
+    LtRows g;
+    g.q4 = *(const float4 *)qkv;
+    g.k4 = *(const float4 *)(qkv + LTD);
+    g.vo4 = *(const float4 *)(p.votab + rr * LTD + 4 * lane);
+    g.x4 = *(const float4 *)(p.ptab + rr * LTD + 4 * lane);
+    g.pos4 = *(const float4 *)(p.lt_pos + (size_t)cb * LTD + 4 * lane);
+    return g;
+}
+// the code's bookkeeping (workgroup 0) and y = X_cb + sum_j softmax_j(q k_j / 16) vo_j
+__device__ __forceinline__ float4 lt_y_attend(const LtFfn2P &p, int b, bool wb0, int code, int amax, const LtYPre &r,
+                                              const LtRows &g) {
+    const int lane = threadIdx.x & 63, cb = p.cb;
+    const size_t row = (size_t)b * NCB * LTD + 4 * lane;
+    const float4 q4 = g.q4, k4 = g.k4, vo4 = g.vo4, x4 = g.x4, pos4 = g.pos4;
     if (wb0) {
         if (lane == 0) {
             p.codes_cur[b * NCB + cb - 1] = code;
@@ -619,6 +654,65 @@ __device__ __forceinline__ float4 lt_y_finish(const LtFfn2P &p, int b, bool wb0,
     return make_float4(x4.x + pos4.x + a.x / l, x4.y + pos4.y + a.y / l, x4.z + pos4.z + a.z / l,
                        x4.w + pos4.w + a.w / l);
 }
+__device__ __forceinline__ float4 lt_y_finish(const LtFfn2P &p, int b, bool wb0, float *wsc, LtYPre &r) {
+    const int cb = p.cb;
+    if (cb == 0) {
+        const float4 x = to_f4(r.kr[0]), v = to_f4(r.vr[0]);
+        return make_float4(x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w);
+    }
+    const int stp = r.stp;
+    int amax;
+    const int code = wave_pick_v(r.lv, p.ignore_eos || stp < 4, p.audio_bos, p.audio_eos, p.smp, b, stp, cb - 1, wsc,
+                                 amax);
+    ts_phase<0>(p.f.ts, 0);  // profiling: code picked
+    return lt_y_attend(p, b, wb0, code, amax, r, lt_gather(p, code));
+}
+
+// Batch 1, greedy (codebooks >= 1): the pick split over the workgroup's MP_NWAVES waves.
+// One wave's pick is ~300 dependent VALU / DPP instructions (~0.9 us of the step, while
+// the other waves wait); here wave w scans logit rows [w QPR, (w + 1) QPR) with
+// wave_pick_v's mask and first-max rule, gathers its own candidate's table rows at once,
+// and the waves' (max, first index) pairs meet in LDS: the first wave holding the global
+// maximum has the global first index (its ids are the lowest), so the code is
+// wave_pick_v's, and that wave, whose rows are already in flight, computes y.
+__device__ __forceinline__ void lt_y_load_q(const LtFfn2P &p, int b, int w, LtYPre &r, float (&lq)[QPR]) {
+    const int lane = threadIdx.x & 63, cb = p.cb;
+    const size_t row = (size_t)b * NCB * LTD + 4 * lane;
+#pragma unroll
+    for (int j = 0; j < NCB - 1; ++j) {
+        const int jj = j < cb ? j : 0;
+        r.kr[j] = *(const f32x4 *)(p.ltk + row + jj * LTD);
+        r.vr[j] = *(const f32x4 *)(p.ltv + row + jj * LTD);
+    }
+    const float *lg = p.logits + (size_t)b * VCB;
+#pragma unroll
+    for (int q = 0; q < QPR; ++q) {
+        const int i = lane + 64 * (w * QPR + q);
+        lq[q] = i < VCB ? lg[i] : -INFINITY;
+    }
+    r.stp = p.step[b];
+}
+// every wave: its rows' pick, its candidate's table rows (g, in flight during the exchange),
+// the exchange; returns the wave holding the code (code: the code, in every wave)
+__device__ __forceinline__ int lt_pick_split(const LtFfn2P &p, int w, const LtYPre &yp, float (&lq)[QPR], LtRows &g,
+                                             int &code) {
+    __shared__ float qv[MP_NWAVES];
+    __shared__ int qi[MP_NWAVES];
+    float bv;
+    int bi = wave_pick_rows(lq, w, p.ignore_eos || yp.stp < 4, p.audio_bos, p.audio_eos, bv);
+    if (bi < 0 || bi >= VCB) bi = 0;
+    g = lt_gather(p, bi);
+    if ((threadIdx.x & 63) == 0) { qv[w] = bv; qi[w] = bi; }
+    lds_sync();
+    float gm = qv[0];
+    int win = 0;
+#pragma unroll
+    for (int u = 1; u < MP_NWAVES; ++u)
+        if (qv[u] > gm) { gm = qv[u]; win = u; }
+    code = qi[win];
+    return win;
+}
+
 __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, float *wsc) {
     LtYPre r;
     lt_y_load(p, b, r);
@@ -640,7 +734,10 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j0 = pb * U + dep;
     // the wave's first slot's loads (logits, earlier positions) ahead of the weights
     LtYPre yp;
-    if (w < NB) lt_y_load(p, w, yp);
+    float lq[QPR];
+    const bool quad = NB == 1 && p.cb > 0 && !p.smp.on;  // uniform: the split greedy pick
+    if (quad) lt_y_load_q(p, 0, w, yp, lq);
+    else if (w < NB) lt_y_load(p, w, yp);
     __builtin_amdgcn_sched_barrier(0);
     float4 a1[UPW], a2[U / 4];
 #pragma unroll
@@ -652,9 +749,7 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         ts_phase<3>(p.f.ts, 0);
     }
-    for (int b = w; b < NB; b += MP_NWAVES) {
-        const float4 y = b == w ? lt_y_finish(p, b, pb == 0, wsc_all[w], yp) : lt_y_slot(p, b, pb == 0, wsc_all[w]);
-        if (b == 0) ts_phase<1>(p.f.ts, 0);  // profiling: y (gathers + attention)
+    auto y_ln = [&](int b, float4 y) {  // y -> the head's residual row (workgroup 0), LN(y) -> xs[b]
         if (pb == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
         if (ys && b == 0) *(float4 *)&ys[4 * lane] = y;
         const float x[4] = {y.x, y.y, y.z, y.w};
@@ -664,6 +759,22 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
         const float4 g = *(const float4 *)(p.f.lnw + 4 * lane);
         *(float4 *)&xs[b][4 * lane] = make_float4(((x[0] - mean) * rstd) * g.x, ((x[1] - mean) * rstd) * g.y,
                                                   ((x[2] - mean) * rstd) * g.z, ((x[3] - mean) * rstd) * g.w);
+    };
+    if (quad) {
+        LtRows g;
+        int code;
+        if (lt_pick_split(p, w, yp, lq, g, code) == w) {
+            ts_phase_w<0>(p.f.ts);  // profiling: code picked
+            const float4 y = lt_y_attend(p, 0, pb == 0, code, code, yp, g);
+            ts_phase_w<1>(p.f.ts);  // profiling: y (gathers + attention)
+            y_ln(0, y);
+        }
+    } else {
+        for (int b = w; b < NB; b += MP_NWAVES) {
+            const float4 y = b == w ? lt_y_finish(p, b, pb == 0, wsc_all[w], yp) : lt_y_slot(p, b, pb == 0, wsc_all[w]);
+            if (b == 0) ts_phase<1>(p.f.ts, 0);  // profiling: y (gathers + attention)
+            y_ln(b, y);
+        }
     }
     lds_sync();
 #pragma unroll
@@ -743,7 +854,10 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
     const int u0 = q * LTS_U + ts_dep(t_start);
     // wave 0's logits / earlier positions first, then the weights (in-order completion)
     LtYPre yp;
-    if (w == 0) lt_y_load(p, b, yp);
+    float lq[QPR];
+    const bool quad = p.cb > 0 && !p.smp.on;  // uniform: the greedy pick split over the waves
+    if (quad) lt_y_load_q(p, b, w, yp, lq);
+    else if (w == 0) lt_y_load(p, b, yp);
     __builtin_amdgcn_sched_barrier(0);
     uint2 a1[LTS_UPW];  // W1 rows u0 + LTS_UPW w + r, elements 4 lane .. 4 lane + 3
 #pragma unroll
@@ -752,8 +866,17 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
 #pragma unroll
     for (int i = 0; i < LTS_U / 8; ++i) a2[i] = ld_ltffn((const uint4 *)(p.w2h + ((size_t)q * LTD + tid) * LTS_U + 8 * i));
     __builtin_amdgcn_sched_barrier(0);
-    if (w == 0) {
-        const float4 y = lt_y_finish(p, b, q == 0, wsc, yp);
+    int yw = 0;  // the wave computing y
+    float4 y;
+    if (quad) {
+        LtRows g;
+        int code;
+        yw = lt_pick_split(p, w, yp, lq, g, code);
+        if (w == yw) y = lt_y_attend(p, b, q == 0, code, code, yp, g);
+    } else if (w == 0) {
+        y = lt_y_finish(p, b, q == 0, wsc, yp);
+    }
+    if (w == yw) {
         if (q == 0) *(float4 *)((float *)p.f.y + (size_t)b * LTD + 4 * lane) = y;
         *(float4 *)&ys[4 * lane] = y;
         const float x[4] = {y.x, y.y, y.z, y.w};

@@ -246,7 +246,24 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
     const size_t rowb = (size_t)b * NCB * LTD + 4 * lane;
     float4 kr[NCB], vr[NCB], pos4, a4, x4;
     float lv[PICK_R];
-    if (w == 0) {
+    // greedy: the pick split over the 4 waves (lt_pick_split's scheme, mp_decode.hip): every
+    // wave loads its logit rows and what y needs; the wave holding the code continues
+    float lq[QPR];
+    int stq = 0;
+    const bool quad = cb > 0 && !g.smp.on;
+    if (quad) {
+        const float *lg = g.logits + (size_t)b * VCB;
+#pragma unroll
+        for (int r = 0; r < QPR; ++r) {
+            const int i = lane + 64 * (w * QPR + r);
+            lq[r] = i < VCB ? lg[i] : -INFINITY;
+        }
+#pragma unroll
+        for (int j = 0; j < NCB - 1; ++j)
+            if (j < cb) { kr[j] = *(const float4 *)(g.ltk + rowb + j * LTD); vr[j] = *(const float4 *)(g.ltv + rowb + j * LTD); }
+        pos4 = *(const float4 *)(g.lt_pos + (size_t)cb * LTD + 4 * lane);
+        stq = g.step[b];
+    } else if (w == 0) {
         if (cb > 0) {
             load_logits(g.logits + (size_t)b * VCB, lv);
 #pragma unroll
@@ -285,17 +302,38 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
             a2[k][i] = *(const float4 *)(p.w2s + ((size_t)(q * PPW + k) * LTD + tid) * LTQ_U + 4 * i);
     // per codebook step its own tags (8 steps share the buffers within one frame)
     const unsigned tag_y = (unsigned)p.iter[0] * 64u + 32u + (unsigned)cb, tag_p = tag_y + 16u;
-    if (w == 0) {
+    int yw = 0;  // the wave computing the attention output
+    int code = 0, amax = 0;
+    float4 q4, k4, v4, xp;
+    auto gather = [&](int c) {
+        const size_t rr = (size_t)(cb - 1) * VCB + c;
+        const float *row = g.qkvtab + rr * (3 * LTD) + 4 * lane;
+        q4 = *(const float4 *)row; k4 = *(const float4 *)(row + LTD); v4 = *(const float4 *)(row + 2 * LTD);
+        xp = *(const float4 *)(g.ptab + rr * LTD + 4 * lane);
+    };
+    if (quad) {
+        __shared__ float qv[MP_NWAVES];
+        __shared__ int qi[MP_NWAVES];
+        float bv;
+        int bi = wave_pick_rows(lq, w, g.ignore_eos || stq < 4, g.audio_bos, g.audio_eos, bv);
+        if (bi < 0 || bi >= VCB) bi = 0;
+        gather(bi);  // this wave's candidate, in flight during the exchange
+        if (lane == 0) { qv[w] = bv; qi[w] = bi; }
+        lds_sync();
+        float gm = qv[0];
+#pragma unroll
+        for (int u = 1; u < MP_NWAVES; ++u)
+            if (qv[u] > gm) { gm = qv[u]; yw = u; }
+        code = amax = qi[yw];
+    }
+    if (w == yw) {
         // the attention output a of position cb and its residual X (lt_pick_kernel's steps)
         if (cb > 0) {
-            const int stp = g.step[b];
-            int amax;
-            const int code = wave_pick_v(lv, g.ignore_eos || stp < 4, g.audio_bos, g.audio_eos, g.smp, b, stp, cb - 1, wsc,
-                                         amax);
-            const size_t rr = (size_t)(cb - 1) * VCB + code;
-            const float *row = g.qkvtab + rr * (3 * LTD) + 4 * lane;
-            const float4 q4 = *(const float4 *)row, k4 = *(const float4 *)(row + LTD), v4 = *(const float4 *)(row + 2 * LTD);
-            const float4 xp = *(const float4 *)(g.ptab + rr * LTD + 4 * lane);
+            if (!quad) {
+                const int stp = g.step[b];
+                code = wave_pick_v(lv, g.ignore_eos || stp < 4, g.audio_bos, g.audio_eos, g.smp, b, stp, cb - 1, wsc, amax);
+                gather(code);
+            }
             if (q == 0) {
                 if (lane == 0) {
                     g.codes_cur[b * NCB + cb - 1] = code;

@@ -156,6 +156,18 @@ __device__ __forceinline__ void ts_phase(unsigned long long *ts, unsigned long l
             *(ulonglong2 *)(ts + 2 * ((size_t)blk * TS_WAVES + TS_WAVES / 2 + K)) = make_ulonglong2(t0 ? t0 : t1, t1);
     }
 }
+// the same, stamped by the calling wave's lane 0 (a phase that one wave of the workgroup
+// reaches, whichever it is)
+template <int K>
+__device__ __forceinline__ void ts_phase_w(unsigned long long *ts) {
+    static_assert(K >= 0 && K < TS_WAVES / 2, "phase slot");
+    if (ts) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const int blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if ((threadIdx.x & 63) == 0 && blk < TS_BLOCKS)
+            *(ulonglong2 *)(ts + 2 * ((size_t)blk * TS_WAVES + TS_WAVES / 2 + K)) = make_ulonglong2(t1, t1);
+    }
+}
 __device__ __forceinline__ void ts_end(unsigned long long *ts, unsigned long long t0) {
     if (ts) {
         __builtin_amdgcn_s_waitcnt(0);

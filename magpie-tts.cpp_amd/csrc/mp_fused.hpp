@@ -164,6 +164,38 @@ __device__ inline int wave_pick(const float *lg, bool forbid_eos, int audio_bos,
     return wave_pick_v(lv, forbid_eos, audio_bos, audio_eos, smp, stream, step, cb, scratch, amax);
 }
 
+// The greedy pick split over a workgroup's MP_NWAVES waves (batch-1 LT step, finalize):
+// wave w scans logit rows [w QPR, (w + 1) QPR).
+constexpr int QPR = PICK_R / MP_NWAVES;
+static_assert(PICK_R % MP_NWAVES == 0 && (PICK_R - 1) / QPR == MP_NWAVES - 1, "logit rows split over the waves");
+// this wave's masked (max, first index) over its rows; the same mask as wave_pick_v
+__device__ __forceinline__ int wave_pick_rows(float (&lv)[QPR], int w, bool forbid_eos, int audio_bos, int audio_eos,
+                                              float &bv) {
+    const int lane = threadIdx.x & 63;
+    constexpr int RL = (VCB - 8) / 64, LL = (VCB - 8) % 64;
+    if (audio_bos == VCB - 8) {
+        if (w == RL / QPR) {
+            const int i = lane + 64 * RL;
+            if (lane >= LL && (i >= VCB || i != audio_eos || forbid_eos)) lv[RL % QPR] = -INFINITY;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < QPR; ++q) {
+            const int i = lane + 64 * (w * QPR + q);
+            if (i >= VCB || ((unsigned)(i - audio_bos) <= 7u && (i != audio_eos || forbid_eos))) lv[q] = -INFINITY;
+        }
+    }
+    bv = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < QPR; ++q) bv = fmaxf(bv, lv[q]);
+    bv = wave_max(bv);
+    int first = 1 << 30;
+#pragma unroll
+    for (int q = QPR - 1; q >= 0; --q)
+        if (lv[q] == bv) first = lane + 64 * (w * QPR + q);
+    return wave_min_u(first);
+}
+
 // PRO_LTARG_ATTN keeps each slot's residual row X = P[cb-1][code] + lt_pos[cb] in
 // sc[b*LTD ..] (the EPI_LTX_ADD epilogue adds it); the wave pick scratch follows.
 template <int NB>

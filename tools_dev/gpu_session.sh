@@ -15,6 +15,7 @@
 #   pmc                  PMC passes (tools_dev/pmc_collect.sh TAG)
 #   codec[=LIB]          codec wall / device time per call (tools_dev/codec_latency.py)
 #   cprof[=LIB]          rocprofv3 kernel trace of 3 codec decodes, per-dispatch table of the last
+#   cpmc                 the codec's SQ / TCC / TCP counter passes (tools_dev/codec_pmc.sh)
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out
@@ -77,6 +78,10 @@ for STEP in "$@"; do
         -- python3 -u tools_dev/codec_prof.py > "$d.log" 2>&1
       python3 tools_dev/codec_trace_report.py "$d/prof_kernel_trace.csv" > "$d.txt"
       tail -12 "$d.txt" ;;
+    cpmc)
+      bash tools_dev/codec_pmc.sh > "$OUT/${TAG}_cpmc.log" 2>&1
+      cp gpurun_out/cpmc/report.txt "$OUT/${TAG}_cpmc.txt"
+      echo "codec pmc ok" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

@@ -60,7 +60,10 @@ constexpr int HOP = 1024;
 // none, yet 96 made the codec slower (8 x 32 frames 1.620 -> 1.637 / 1.654 ms, rb_kernel at
 // 64 channels 322 -> 345 us; gpurun_out/r05h_codec*.txt): the A-fragment stream and the
 // workgroups per CU, not LDS reads, bound these kernels.
-constexpr int LDS_ROWB = 80;
+#ifndef MP_CODEC_ROWB
+#define MP_CODEC_ROWB 80
+#endif
+constexpr int LDS_ROWB = MP_CODEC_ROWB;
 
 enum InMode { IN_F16 = 0, IN_FSQ = 1 };
 
@@ -464,6 +467,11 @@ struct RbP {
     int nsnake, creal, T, dil, tiles_per_chunk;
 };
 constexpr int RB_ROWB = LDS_ROWB;  // LDS bytes per time row of a 32-channel block
+// A-fragment ring slots of the residual-block convs (steps of lead for the weight loads)
+#ifndef MP_RB_RING
+#define MP_RB_RING 3
+#endif
+constexpr int RB_RING = MP_RB_RING;
 constexpr int RB_MAXHALO = 50;  // (11 - 1) * 5
 
 template <int RWV, int CWV, int NT>
@@ -624,9 +632,9 @@ template <int RWV, int CWV, int NT>
 __global__ __launch_bounds__(64 * RWV * CWV, RWV * CWV > 8 || NT > 4 ? 1 : 2) void rb_kernel(RbP p) {
     __shared__ __attribute__((aligned(16))) char xs[rb_lds_bytes<RWV, CWV, NT>()];
     switch (p.ks[blockIdx.y]) {
-        case 3: rb_body<3, RWV, CWV, NT, 3>(p, xs); break;
-        case 7: rb_body<7, RWV, CWV, NT, 3>(p, xs); break;
-        default: rb_body<11, RWV, CWV, NT, 3>(p, xs); break;
+        case 3: rb_body<3, RWV, CWV, NT, RB_RING>(p, xs); break;
+        case 7: rb_body<7, RWV, CWV, NT, RB_RING>(p, xs); break;
+        default: rb_body<11, RWV, CWV, NT, RB_RING>(p, xs); break;
     }
 }
 

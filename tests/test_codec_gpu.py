@@ -80,3 +80,4 @@ def test_fused_blocks_equal_two_launch_blocks(gpu_codec, monkeypatch, F):
     monkeypatch.setenv("MAGPIE_CODEC_UNFUSED", "1")
     unfused = gpu_codec.decode_chunks(codes)
     np.testing.assert_array_equal(fused, unfused)
+

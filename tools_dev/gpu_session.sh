@@ -13,9 +13,9 @@
 #   tl=MODE:B[:OPS]      in-kernel phase timeline (tools_dev/diag_timeline.py, PHASES=1); OPS comma-separated
 #   prof                 rocprofv3 kernel-trace summary of the bench (eager) + phase cut
 #   pmc                  PMC passes (tools_dev/pmc_collect.sh TAG)
-#   codec[=LIB]          codec wall / device time per call (tools_dev/codec_latency.py)
+#   codec[=LIB[:K=V]]    codec wall / device time per call (tools_dev/codec_latency.py); LIB "-" = default
 #   cprof[=LIB]          rocprofv3 kernel trace of 3 codec decodes, per-dispatch table of the last
-#   cpmc                 the codec's SQ / TCC / TCP counter passes (tools_dev/codec_pmc.sh)
+#   cpmc[=LIB]           the codec's SQ / TCC / TCP counter passes (tools_dev/codec_pmc.sh)
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out
@@ -66,10 +66,14 @@ for STEP in "$@"; do
       bash tools_dev/pmc_collect.sh "$TAG" > "$OUT/${TAG}_pmc.log" 2>&1
       echo "pmc ok" ;;
     codec)
+      IFS=: read -r lib kv <<< "$arg"
       env=()
-      [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
-      env "${env[@]}" timeout -k 10 200 python -u tools_dev/codec_latency.py > "$OUT/${TAG}_codec${arg:+_$arg}.txt" 2>&1
-      cat "$OUT/${TAG}_codec${arg:+_$arg}.txt" ;;
+      [ -n "$lib" ] && [ "$lib" != "-" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$lib.so")
+      [ "$lib" = "-" ] && lib=""
+      [ -n "$kv" ] && env+=("$kv")
+      suf="${lib:+_$lib}${kv:+_${kv//=/-}}"
+      env "${env[@]}" timeout -k 10 200 python -u tools_dev/codec_latency.py > "$OUT/${TAG}_codec${suf}.txt" 2>&1
+      echo "codec ${lib:-default} ${kv}: $(tail -1 "$OUT/${TAG}_codec${suf}.txt")" ;;
     cprof)
       env=()
       [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
@@ -79,8 +83,8 @@ for STEP in "$@"; do
       python3 tools_dev/codec_trace_report.py "$d/prof_kernel_trace.csv" > "$d.txt"
       tail -12 "$d.txt" ;;
     cpmc)
-      bash tools_dev/codec_pmc.sh > "$OUT/${TAG}_cpmc.log" 2>&1
-      cp gpurun_out/cpmc/report.txt "$OUT/${TAG}_cpmc.txt"
+      MAGPIE_LIB="${arg:+$PWD/ab_libs/$arg.so}" bash tools_dev/codec_pmc.sh > "$OUT/${TAG}_cpmc${arg:+_$arg}.log" 2>&1
+      cp gpurun_out/cpmc/report.txt "$OUT/${TAG}_cpmc${arg:+_$arg}.txt"
       echo "codec pmc ok" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac

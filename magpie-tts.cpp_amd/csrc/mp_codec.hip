@@ -64,6 +64,19 @@ constexpr int HOP = 1024;
 #define MP_CODEC_ROWB 80
 #endif
 constexpr int LDS_ROWB = MP_CODEC_ROWB;
+// conv2_kernel pins each A-fragment ring load at its place in the tap loop (a scheduling
+// barrier after it): left free, the scheduler sank the loads to just before their MFMAs
+// (issue, then s_waitcnt vmcnt(1) four instructions later), exposing the L2 latency at
+// every step. Measured (gpurun_out/r05q_*): the 448-channel stage's conv2_kernel 241 ->
+// 180 us per decode; the same barrier in rb_kernel (3-slot ring, 2 workgroups per CU)
+// cost 5-7 % on every stage (it also fences the B-fragment reads), so only conv2 pins.
+#ifndef MP_CONV2_PIN
+#define MP_CONV2_PIN 1
+#endif
+#ifndef MP_RB_PIN
+#define MP_RB_PIN 0
+#endif
+constexpr bool CONV2_PIN = MP_CONV2_PIN != 0, RB_PIN = MP_RB_PIN != 0;
 
 enum InMode { IN_F16 = 0, IN_FSQ = 1 };
 
@@ -370,6 +383,7 @@ __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
                 ring[st % R][0] = *(const half8 *)(wrow0 + (size_t)(st + R) * 512);
                 ring[st % R][1] = *(const half8 *)(wrow1 + (size_t)(st + R) * 512);
             }
+            if constexpr (CONV2_PIN) __builtin_amdgcn_sched_barrier(0);  // the ring loads stay R steps ahead
             if (k + 1 < KS) {
 #pragma unroll
                 for (int j = 0; j < C2_NT; ++j) bc[j] = bn[j];
@@ -575,6 +589,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
                     ring[st % R][0] = *(const half8 *)(wrow0 + (size_t)(st + R) * 512);
                     ring[st % R][1] = *(const half8 *)(wrow1 + (size_t)(st + R) * 512);
                 }
+                if constexpr (RB_PIN) __builtin_amdgcn_sched_barrier(0);  // the ring loads stay R steps ahead
                 if (k + 1 < KS) {
 #pragma unroll
                     for (int j = 0; j < NT; ++j) bc[j] = bn[j];

@@ -230,18 +230,10 @@ __global__ __launch_bounds__(FIN_THREADS) void lt_finalize_kernel(FinP p) {
     }
     int i0 = 0, amax = 0;
     if (quad) {
-        __shared__ float qv[FIN_THREADS / 64];
-        __shared__ int qi[FIN_THREADS / 64];
         float bv;
         int bi = wave_pick_rows(lq, w, p.ignore_eos || stp_q < 4, p.audio_bos, p.audio_eos, bv);
         if (bi < 0 || bi >= VCB) bi = 0;
-        if ((tid & 63) == 0) { qv[w] = bv; qi[w] = bi; }
-        __syncthreads();
-        float gm = qv[0];
-        i0 = qi[0];
-#pragma unroll
-        for (int u = 1; u < FIN_THREADS / 64; ++u)
-            if (qv[u] > gm) { gm = qv[u]; i0 = qi[u]; }
+        pick_exchange(bv, bi, i0);
         amax = i0;
     }
     if (w == 0) {
@@ -696,21 +688,11 @@ __device__ __forceinline__ void lt_y_load_q(const LtFfn2P &p, int b, int w, LtYP
 // the exchange; returns the wave holding the code (code: the code, in every wave)
 __device__ __forceinline__ int lt_pick_split(const LtFfn2P &p, int w, const LtYPre &yp, float (&lq)[QPR], LtRows &g,
                                              int &code) {
-    __shared__ float qv[MP_NWAVES];
-    __shared__ int qi[MP_NWAVES];
     float bv;
     int bi = wave_pick_rows(lq, w, p.ignore_eos || yp.stp < 4, p.audio_bos, p.audio_eos, bv);
     if (bi < 0 || bi >= VCB) bi = 0;
     g = lt_gather(p, bi);
-    if ((threadIdx.x & 63) == 0) { qv[w] = bv; qi[w] = bi; }
-    lds_sync();
-    float gm = qv[0];
-    int win = 0;
-#pragma unroll
-    for (int u = 1; u < MP_NWAVES; ++u)
-        if (qv[u] > gm) { gm = qv[u]; win = u; }
-    code = qi[win];
-    return win;
+    return pick_exchange(bv, bi, code);
 }
 
 __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, float *wsc) {

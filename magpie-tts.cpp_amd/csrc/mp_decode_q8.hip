@@ -312,19 +312,12 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_q8_kernel(LtSlotQ8P p) {
         xp = *(const float4 *)(g.ptab + rr * LTD + 4 * lane);
     };
     if (quad) {
-        __shared__ float qv[MP_NWAVES];
-        __shared__ int qi[MP_NWAVES];
         float bv;
         int bi = wave_pick_rows(lq, w, g.ignore_eos || stq < 4, g.audio_bos, g.audio_eos, bv);
         if (bi < 0 || bi >= VCB) bi = 0;
         gather(bi);  // this wave's candidate, in flight during the exchange
-        if (lane == 0) { qv[w] = bv; qi[w] = bi; }
-        lds_sync();
-        float gm = qv[0];
-#pragma unroll
-        for (int u = 1; u < MP_NWAVES; ++u)
-            if (qv[u] > gm) { gm = qv[u]; yw = u; }
-        code = amax = qi[yw];
+        yw = pick_exchange(bv, bi, code);
+        amax = code;
     }
     if (w == yw) {
         // the attention output a of position cb and its residual X (lt_pick_kernel's steps)

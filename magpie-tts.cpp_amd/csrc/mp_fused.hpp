@@ -196,6 +196,25 @@ __device__ __forceinline__ int wave_pick_rows(float (&lv)[QPR], int w, bool forb
     return wave_min_u(first);
 }
 
+// The split pick's exchange: every wave's (max, first index) pair through LDS; returns the
+// first wave holding the workgroup-wide maximum (its first index is the global first
+// index: its ids are the lowest among the waves at that value) and its index in `code`.
+// Every wave of the workgroup calls it (one barrier).
+__device__ __forceinline__ int pick_exchange(float bv, int bi, int &code) {
+    __shared__ float qv[MP_NWAVES];
+    __shared__ int qi[MP_NWAVES];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { qv[w] = bv; qi[w] = bi; }
+    lds_sync();
+    float gm = qv[0];
+    int win = 0;
+#pragma unroll
+    for (int u = 1; u < MP_NWAVES; ++u)
+        if (qv[u] > gm) { gm = qv[u]; win = u; }
+    code = qi[win];
+    return win;
+}
+
 // PRO_LTARG_ATTN keeps each slot's residual row X = P[cb-1][code] + lt_pos[cb] in
 // sc[b*LTD ..] (the EPI_LTX_ADD epilogue adds it); the wave pick scratch follows.
 template <int NB>

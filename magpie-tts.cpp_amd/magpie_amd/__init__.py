@@ -139,9 +139,12 @@ DECISIVE = 32.0
 
 
 def synth_gguf(path: str, kind: str = "magpie", seed: int = 0x4D414750, dtype: str = "f32",
-               dec_layers: int = 12, enc_layers: int = 6, lt_head_scale: float = 1.0) -> str:
+               dec_layers: int = 12, enc_layers: int = 6, lt_head_scale: float = 1.0,
+               audio_bos: Optional[int] = None, eos_bias: Optional[float] = None) -> str:
     """Write (or reuse) a deterministic synthetic GGUF with the reference's layout.
-    lt_head_scale multiplies the std of the LT output heads (weights and bias)."""
+    lt_head_scale multiplies the std of the LT output heads (weights and bias);
+    audio_bos moves the 8 special audio ids (EOS = audio_bos + 1), eos_bias raises
+    codebook 3's EOS logit (test models)."""
     if os.path.exists(path):
         return path
     tmp = f"{path}.tmp{os.getpid()}"  # written aside, then renamed: never a partial file at `path`
@@ -149,6 +152,10 @@ def synth_gguf(path: str, kind: str = "magpie", seed: int = 0x4D414750, dtype: s
     if kind == "magpie":
         cmd += ["--dtype", dtype, "--dec-layers", str(dec_layers), "--enc-layers", str(enc_layers),
                 "--lt-head-scale", repr(float(lt_head_scale))]
+        if audio_bos is not None:
+            cmd += ["--audio-bos", str(int(audio_bos))]
+        if eos_bias is not None:
+            cmd += ["--eos-bias", repr(float(eos_bias))]
     try:
         subprocess.run(cmd, check=True)
         os.replace(tmp, path)

@@ -12,6 +12,7 @@
 // usage: mp_synth_gguf magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|q4_0|f16]
 //                      [--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V]
 //                      [--lt-head-scale K]  (LT output head weights N(0, (0.02 K)^2): decisive logits)
+//                      [--audio-bos N]      (the 8 special audio ids from N, EOS = N + 1; default 2016)
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -22,7 +23,8 @@ enum { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q8_0 = 8 };
 enum { KV_U32 = 4, KV_F32 = 6, KV_STR = 8 };
 
 static uint64_t g_seed = 0x4D414750ull;  // "MAGP"
-static float g_eos_bias = 0.f;            // test-only: added to out_proj[3].bias[2017]
+static float g_eos_bias = 0.f;            // test-only: added to out_proj[3].bias[audio_eos]
+static int g_audio_bos = 2016;            // test-only (--audio-bos): the 8 special ids' first; EOS = +1
 static float g_lt_head_scale = 1.f;       // LT output heads std = 0.02 * this
 
 static uint64_t splitmix64(uint64_t x) {
@@ -139,7 +141,7 @@ static void fill_f32(const tdesc *t, float *dst) {
     }
     // EOS-forcing variant for the stop-logic tests: codebook 3 prefers audio EOS
     // once it is no longer forbidden (step >= 4, magpie.cpp:4325)
-    if (g_eos_bias != 0.f && !strcmp(t->name, "local_transformer_out_projections.3.bias")) dst[2017] += g_eos_bias;
+    if (g_eos_bias != 0.f && !strcmp(t->name, "local_transformer_out_projections.3.bias")) dst[g_audio_bos + 1] += g_eos_bias;
 }
 
 // Q8_0 exactly as scripts/convert_magpie_to_gguf.py:79-104 (numpy): fp16 scale =
@@ -315,8 +317,8 @@ static void plan_magpie(int dtype, int dec_layers, int enc_layers, int dec_pos) 
         kv_u32("magpie.tokenizer.pad", 94);
         kv_u32("magpie.tokenizer.oov", 95);
     }
-    kv_u32("magpie.audio_bos_id", 2016);
-    kv_u32("magpie.audio_eos_id", 2017);
+    kv_u32("magpie.audio_bos_id", (uint32_t)g_audio_bos);
+    kv_u32("magpie.audio_eos_id", (uint32_t)g_audio_bos + 1);
     // keys the reader actually honours (magpie.cpp:85-120); only written when a
     // reduced test model deviates from the struct defaults
     if (dec_layers != 12) kv_u32("magpie.dec_layers", (uint32_t)dec_layers);
@@ -386,7 +388,7 @@ static void plan_codec(void) {
 int main(int argc, char **argv) {
     if (argc < 3) {
         fprintf(stderr, "usage: %s magpie|codec OUT.gguf [--seed S] [--dtype f32|q8_0|q4_0|f16] "
-                        "[--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V] [--lt-head-scale K]\n", argv[0]);
+                        "[--dec-layers N] [--enc-layers N] [--dec-pos P] [--eos-bias V] [--lt-head-scale K] [--audio-bos N]\n", argv[0]);
         return 2;
     }
     const char *kind = argv[1], *out = argv[2];
@@ -401,6 +403,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--enc-layers")) enc_layers = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--dec-pos")) dec_pos = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--eos-bias")) g_eos_bias = (float)atof(argv[i + 1]);
+        else if (!strcmp(argv[i], "--audio-bos")) g_audio_bos = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--lt-head-scale")) g_lt_head_scale = (float)atof(argv[i + 1]);
         else { fprintf(stderr, "unknown option %s\n", argv[i]); return 2; }
     }

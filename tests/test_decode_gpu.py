@@ -607,3 +607,81 @@ def test_preamble_mfma_equals_valu(ma, small_model, f16_model, weights, monkeypa
     assert np.array_equal(a.codes[0], b.codes[0]) and np.array_equal(a.hidden, b.hidden)
     print(f"preamble MFMA == VALU ({weights}): encoder, {len(a.codes[0])} frames, hidden bitwise; "
           f"preamble {a.preamble_ms:.2f} ms (MFMA) vs {b.preamble_ms:.2f} ms (VALU)")
+
+
+# ---------------------------------------------------------------- moved special ids
+# A GGUF may put the 8 special audio ids anywhere (magpie.audio_bos_id, EOS = bos + 1):
+# the pick then takes its general per-row mask (wave_pick_v / wave_pick_rows) instead
+# of the last-row fast path of the reference's ids (2016..2023).
+MOVED_BOS = 1000
+
+
+@pytest.fixture(scope="module")
+def moved_ids_model():
+    import os
+    import magpie_amd as ma
+    cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
+    os.makedirs(cache, exist_ok=True)
+    return ma.synth_gguf(os.path.join(cache, f"magpie_small_bos{MOVED_BOS}_k32.gguf"), dec_layers=2, enc_layers=1,
+                         lt_head_scale=ma.DECISIVE, audio_bos=MOVED_BOS)
+
+
+@pytest.fixture(scope="module")
+def moved_ids_eos_model():
+    import os
+    import magpie_amd as ma
+    cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
+    os.makedirs(cache, exist_ok=True)
+    return ma.synth_gguf(os.path.join(cache, f"magpie_small_bos{MOVED_BOS}_eos.gguf"), dec_layers=2, enc_layers=1,
+                         audio_bos=MOVED_BOS, eos_bias=8.0)
+
+
+def _no_special(codes, eos_ok=False):
+    c = np.asarray(codes).reshape(-1)
+    bad = [(MOVED_BOS <= v < MOVED_BOS + 8) and not (eos_ok and v == MOVED_BOS + 1) for v in c]
+    assert not any(bad), f"special id emitted: {c[np.array(bad)]}"
+
+
+def test_moved_special_ids_greedy(ma, oracle, moved_ids_model):
+    """Greedy f32 at batch 1 (the pick split over 4 waves) and at batch 3 (one wave per
+    slot) with the special ids at 1000..1007: codes equal the oracle's, no special id
+    emitted, the batch equals its single runs."""
+    tok = ma.synthetic_tokens(20, seed=1300)
+    r, o = _run_both(ma, oracle, moved_ids_model, tok, steps=32, ignore_eos=True)
+    compare_codes(r.codes[0], o["codes"], o["margins"])
+    _no_special(r.codes[0])
+    toks = [ma.synthetic_tokens(12 + 4 * b, seed=1310 + b) for b in range(3)]
+    dev = ma.Device(moved_ids_model)
+    rb = dev.synthesize(toks, speakers=[0, 1, 2], max_dec_steps=16, ignore_eos=True)
+    for b in range(3):
+        rs = dev.synthesize([toks[b]], speakers=[b], max_dec_steps=16, ignore_eos=True)
+        assert np.array_equal(rb.codes[b], rs.codes[0]), b
+        _no_special(rb.codes[b])
+    dev.close()
+    # bf16 mode: the split pick of lt_slot_kernel at 1 and 2 slots
+    d16 = ma.Device(moved_ids_model, weights="bf16")
+    r2 = d16.synthesize(toks[:2], speakers=[0, 1], max_dec_steps=16, ignore_eos=True)
+    r1 = d16.synthesize(toks[:1], speakers=[0], max_dec_steps=16, ignore_eos=True)
+    d16.close()
+    assert np.array_equal(r2.codes[0], r1.codes[0])
+    _no_special(r2.codes[0]); _no_special(r2.codes[1])
+
+
+def test_moved_special_ids_sampled_and_eos(ma, oracle, moved_ids_model, moved_ids_eos_model):
+    """Top-k draws with the moved ids equal the oracle's; with codebook 3's EOS logit
+    raised, both stop at frame 4 (EOS forbidden before, magpie.cpp:4340-4348)."""
+    toks = [ma.synthetic_tokens(14, seed=1320)]
+    r, outs = _sample_both(ma, oracle, moved_ids_model, toks, steps=20, temperature=0.7, top_k=80, seed=31,
+                           ignore_eos=True)
+    compare_codes(r.codes[0], outs[0]["codes"], outs[0]["margins"])
+    _no_special(r.codes[0])
+    for temp in (0.0, 0.7):
+        dev = ma.Device(moved_ids_eos_model)
+        re_ = dev.synthesize(toks, max_dec_steps=64, temperature=temp, top_k=80, seed=5)
+        dev.close()
+        om = oracle.Model(moved_ids_eos_model)
+        oe = om.synthesize(toks[0], max_steps=64, trace=False, temperature=temp, top_k=80, seed=5, stream=0)
+        om.close()
+        assert oe["n_frames"] == 4 and re_.n_frames[0] == 4, (temp, oe["n_frames"], re_.n_frames[0])
+        # default (near-flat) heads here: a genuine near-tie may end the comparison early
+        compare_codes(re_.codes[0], oe["codes"], oe["margins"], min_frames=0)

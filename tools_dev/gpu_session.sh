@@ -10,7 +10,7 @@
 #   ab=N:LIB[,LIB...]    alternating bench A/B: default library vs each ab_libs/LIB.so, N rounds
 #   ops=MODE:B[:LIB[:K=V]]  per-op dispatch intervals + wave spans (tools_dev/mode_ops.py);
 #                        LIB "-" = the default library; K=V e.g. MODE_XA=direct, MODE_KV=bf16
-#   tl=MODE:B[:OPS]      in-kernel phase timeline (tools_dev/diag_timeline.py, PHASES=1); OPS comma-separated
+#   tl=MODE:B[:OPS[:LIB]]  in-kernel phase timeline (tools_dev/diag_timeline.py, PHASES=1); OPS comma-separated
 #   prof                 rocprofv3 kernel-trace summary of the bench (eager) + phase cut
 #   pmc                  PMC passes (tools_dev/pmc_collect.sh TAG)
 #   codec[=LIB[:K=V]]    codec wall / device time per call (tools_dev/codec_latency.py); LIB "-" = default
@@ -53,8 +53,11 @@ for STEP in "$@"; do
       env "${env[@]}" timeout -k 10 200 python -u tools_dev/mode_ops.py "$mode" "$b" $kv > "$OUT/${TAG}_ops_${mode}_b${b}${suf}.txt" 2>&1
       head -1 "$OUT/${TAG}_ops_${mode}_b${b}${suf}.txt" ;;
     tl)
-      IFS=: read -r mode b ops <<< "$arg"
-      PHASES=1 timeout -k 10 200 python -u tools_dev/diag_timeline.py "$mode" "$b" $(echo "$ops" | tr ',' ' ') > "$OUT/${TAG}_tl_${mode}_b${b}.txt" 2>&1
+      IFS=: read -r mode b ops lib <<< "$arg"
+      env=()
+      [ -n "$lib" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$lib.so")
+      env "${env[@]}" PHASES=1 timeout -k 10 200 python -u tools_dev/diag_timeline.py "$mode" "$b" $(echo "$ops" | tr ',' ' ') \
+        > "$OUT/${TAG}_tl_${mode}_b${b}${lib:+_$lib}.txt" 2>&1
       echo "timeline ok" ;;
     prof)
       MAGPIE_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/${TAG}_prof" -o prof \

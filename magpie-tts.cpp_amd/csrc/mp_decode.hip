@@ -82,7 +82,13 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) wv[r][i] = K == LTD ? ld_lt(wr + lane + 64 * i) : ld_weight(wr + lane + 64 * i);
     }
-    if constexpr (PRE) __builtin_amdgcn_sched_barrier(0);
+    // the epilogue's operand of this lane's output (lane r*NB + b), behind the weights
+    float eop = 0.f;
+    if constexpr (epi_has_operand<EPI>()) {
+        const int nq = row0 + lane / NB;
+        if (lane < RW * NB && nq < p.N) eop = epi_operand<EPI>(p, nq, lane % NB);
+    }
+    if constexpr (PRE || epi_has_operand<EPI>()) __builtin_amdgcn_sched_barrier(0);
     if constexpr (EPI != EPI_RESID_XA && EPI != EPI_QKV_SA) ts_phase<1>(p.ts, 0);  // profiling: weights issued
     float acc[RW][NB];
 #pragma unroll
@@ -126,9 +132,11 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     const int b = lane % NB, n = row0 + lane / NB;
     if (n >= p.N) return;
     if constexpr (EPI == EPI_RESID_XA) {
-        publish_x1(p, v, n, b);
+        publish_x1_op(p, v, n, b, eop);
     } else if constexpr (EPI == EPI_QKV_SA) {
         publish_qkv(p, v, n, b);
+    } else if constexpr (EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_ADD_STORE) {
+        epi_store_op<EPI>(p, v, n, b, eop);
     } else {
         epi_store<EPI>(p, v, n, b, EPI == EPI_LTX_ADD ? sc[b * LTD + n] : 0.f);
     }
@@ -720,6 +728,9 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     const bool quad = NB == 1 && p.cb > 0 && !p.smp.on;  // uniform: the split greedy pick
     if (quad) lt_y_load_q(p, 0, w, yp, lq);
     else if (w < NB) lt_y_load(p, w, yp);
+    // the LN weights with the first loads: loaded after y (behind its stores) they cost an
+    // L2 round trip on the step's critical path
+    const float4 gln = *(const float4 *)(p.f.lnw + 4 * lane);
     __builtin_amdgcn_sched_barrier(0);
     float4 a1[UPW], a2[U / 4];
 #pragma unroll
@@ -738,7 +749,7 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
         float mean, var;
         wave_meanvar<4>(x, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.f.eps);
-        const float4 g = *(const float4 *)(p.f.lnw + 4 * lane);
+        const float4 g = gln;
         *(float4 *)&xs[b][4 * lane] = make_float4(((x[0] - mean) * rstd) * g.x, ((x[1] - mean) * rstd) * g.y,
                                                   ((x[2] - mean) * rstd) * g.z, ((x[3] - mean) * rstd) * g.w);
     };
@@ -840,6 +851,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
     const bool quad = p.cb > 0 && !p.smp.on;  // uniform: the greedy pick split over the waves
     if (quad) lt_y_load_q(p, b, w, yp, lq);
     else if (w == 0) lt_y_load(p, b, yp);
+    const float4 gln = *(const float4 *)(p.f.lnw + 4 * lane);  // LN weights with the first loads
     __builtin_amdgcn_sched_barrier(0);
     uint2 a1[LTS_UPW];  // W1 rows u0 + LTS_UPW w + r, elements 4 lane .. 4 lane + 3
 #pragma unroll
@@ -865,7 +877,7 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_slot_kernel(LtFfn2P p) {
         float mean, var;
         wave_meanvar<4>(x, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.f.eps);
-        const float4 g = *(const float4 *)(p.f.lnw + 4 * lane);
+        const float4 g = gln;
         *(float4 *)&xs[4 * lane] =
             make_float4(bf16_round(((x[0] - mean) * rstd) * g.x), bf16_round(((x[1] - mean) * rstd) * g.y),
                         bf16_round(((x[2] - mean) * rstd) * g.z), bf16_round(((x[3] - mean) * rstd) * g.w));
@@ -955,10 +967,29 @@ hipError_t op_lt_slot(const LtFfn2P &p, int NB, hipStream_t s) {
 // units -> returns this thread's FFN-down partial sum (output tid) of codebook 0.
 constexpr int LTF_U = LTF / LT_FFN_P, LTF_UPW = LTF_U / MP_NWAVES;
 constexpr int LTFR_G = LTD / MP_NWAVES;  // lt_front workgroups: one in_proj / k / vo row per wave
+// the front's small operands, loaded with the decoder row ahead of the weights: each read
+// where it is used was a dependent L2 round trip on the front's chain (after the in_proj
+// dot, after the in_proj / vo_0 granules, after y)
+struct LtFrontPre {
+    float bin;       // in_proj bias of this wave's row
+    float posa[4];   // lt_pos[0][lane + 64 i]
+    float gself[4];  // norm_self[lane + 64 i]
+    float4 posb;     // lt_pos[0][4 lane .. 4 lane + 3]
+    float4 gff;      // the LT FFN LayerNorm weights [4 lane .. 4 lane + 3]
+};
+__device__ __forceinline__ void lt_front_pre(const LtFrontP &p, int n_in, LtFrontPre &q) {
+    const int lane = threadIdx.x & 63;
+    q.bin = p.b_in[n_in];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q.posa[i] = p.lt_pos[lane + 64 * i];
+    load_lnw<4>(p.norm_self, q.gself);
+    q.posb = *(const float4 *)(p.lt_pos + 4 * lane);
+    q.gff = *(const float4 *)(p.l.f.lnw + 4 * lane);
+}
 __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_in, const float4 (&wi)[3], float4 wk,
                                                float4 wv, const float4 (&a1)[LTF_UPW], const float4 (&a2)[LTF_U / 4],
-                                               const float (&v)[D / 64], const float (&g)[D / 64], float *act, float *act2,
-                                               float *xs, float *fs, float4 *y4, float4 *v4) {
+                                               const float (&v)[D / 64], const float (&g)[D / 64], const LtFrontPre &q,
+                                               float *act, float *act2, float *xs, float *fs, float4 *y4, float4 *v4) {
     constexpr int U = LTF_U, UPW = LTF_UPW, PER = D / 64, Q = PER / MP_NWAVES;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const unsigned tag_s = (unsigned)p.iter[0] * 64u + 40u, tag_v = tag_s + 1u;
@@ -986,7 +1017,7 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < 3; ++i) s += dotv(wi[i], ((const float4 *)act)[lane + 64 * i]);
-        const float v = wave_sum(s) + p.b_in[n_in];
+        const float v = wave_sum(s) + q.bin;
         if (lane == 0) {
             p.lt_s[n_in] = v;
             __hip_atomic_store((gu64 *)p.gh + n_in, ((unsigned long long)tag_s << 32) | __float_as_uint(v),
@@ -995,14 +1026,14 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
     }
     // ---- X_0 = s + lt_pos[0], LN(X_0) (PRO_LTX_LN's one-wave statistics): wave 0
     if (w == 0) {
-        float g[4], X[4], sv[4];
-        load_lnw<4>(p.norm_self, g);
+        float X[4], sv[4];
+        const float(&g)[4] = q.gself;
         gh_wait_n<4, 64>(p.gh + lane, tag_s, sv, p.hx_err);  // in_proj outputs lane + 64 i
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = lane + 64 * i;
             xs[k] = sv[i];  // kept for the FFN step below (xs is free until then)
-            X[i] = sv[i] + p.lt_pos[k];
+            X[i] = sv[i] + q.posa[i];
         }
         if (pb == 0)
 #pragma unroll
@@ -1035,11 +1066,9 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
         float xv[4], vv[4];
         gh_wait_n<4, 1>(p.gh + LTD + 4 * lane, tag_v, vv, p.hx_err);  // vo_0 outputs 4 lane + c
         wave_lds_sync();  // (xs: the in_proj outputs this wave stored above)
+        const float pb4[4] = {q.posb.x, q.posb.y, q.posb.z, q.posb.w};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int k = 4 * lane + c;
-            xv[c] = xs[k] + p.lt_pos[k];
-        }
+        for (int c = 0; c < 4; ++c) xv[c] = xs[4 * lane + c] + pb4[c];
         const float4 y = make_float4(xv[0] + vv[0], xv[1] + vv[1], xv[2] + vv[2], xv[3] + vv[3]);
         if (pb == 0) *(float4 *)((float *)p.l.f.y + 4 * lane) = y;
         if (y4) *y4 = y;
@@ -1048,7 +1077,7 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
         float mean, var;
         wave_meanvar<4>(x, mean, var);
         const float rstd = 1.0f / sqrtf(var + p.l.f.eps);
-        const float4 g = *(const float4 *)(p.l.f.lnw + 4 * lane);
+        const float4 g = q.gff;
         *(float4 *)&xs[4 * lane] = make_float4(((x[0] - mean) * rstd) * g.x, ((x[1] - mean) * rstd) * g.y,
                                                ((x[2] - mean) * rstd) * g.z, ((x[3] - mean) * rstd) * g.w);
     }
@@ -1111,11 +1140,13 @@ __global__ __launch_bounds__(MP_BLOCK) void lt_front_kernel(LtFrontP p) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) v[i] = p.x[lane + 64 * i];
     load_lnw<PER>(p.norm_out, g);
+    LtFrontPre q;
+    lt_front_pre(p, n_in, q);
     __builtin_amdgcn_sched_barrier(0);
     float4 wi[3], wk, wv, a1[LTF_UPW], a2[LTF_U / 4];
     lt_front_weights(p, pb, n_in, wi, wk, wv, a1, a2);
     __builtin_amdgcn_sched_barrier(0);
-    const float acc = lt_front_core(p, pb, n_in, wi, wk, wv, a1, a2, v, g, act, act2, xs, fs, nullptr, nullptr);
+    const float acc = lt_front_core(p, pb, n_in, wi, wk, wv, a1, a2, v, g, q, act, act2, xs, fs, nullptr, nullptr);
     if (pb < LT_FFN_P) p.l.f.part[ltp_idx(0, pb, tid)] = acc;
     ts_end(p.l.f.ts, t_start);
 }

@@ -147,7 +147,13 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     uint4 a[KW];
 #pragma unroll
     for (int i = 0; i < KW; ++i) a[i] = K == LTD ? ld_lt(wf + (size_t)i * 64) : ld_weight(wf + (size_t)i * 64);
-    if constexpr (PRE || PLB || PLF) __builtin_amdgcn_sched_barrier(0);
+    // the epilogue's operand of this thread's output (row, column below), behind the weights
+    float eop = 0.f;
+    if constexpr (epi_has_operand<EPI>()) {
+        const int rq = KS == 1 ? tid >> 4 : ks * (16 / KS) + (tid >> 4), cq = tid & 15, nq = rt * 16 + rq;
+        if (cq < NB && nq < p.N && (KS == 1 || tid < (16 / KS) * 16)) eop = epi_operand<EPI>(p, nq, cq);
+    }
+    if constexpr (PRE || PLB || PLF || epi_has_operand<EPI>()) __builtin_amdgcn_sched_barrier(0);
 
     // activation rows -> bf16 in LDS; row NB is zero and feeds MFMA columns NB..15
     if constexpr (LNB) {
@@ -359,8 +365,9 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_b16_kernel(GemvP p) {
     if (col >= NB) return;
     const int n = rt * 16 + row;
     if (n >= p.N) return;
-    if constexpr (EPI == EPI_RESID_XA) publish_x1(p, v, n, col);
+    if constexpr (EPI == EPI_RESID_XA) publish_x1_op(p, v, n, col, eop);
     else if constexpr (EPI == EPI_QKV_SA) publish_qkv(p, v, n, col);
+    else if constexpr (EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_ADD_STORE) epi_store_op<EPI>(p, v, n, col, eop);
     else epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
     ts_end(p.ts, t_start);
 }

@@ -112,10 +112,18 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     uint4 sd[KW];
 #pragma unroll
     for (int i = 0; i < KW; ++i) { a[i] = ld_weight(wf + (size_t)i * 64); sd[i] = ld_weight(sf + (size_t)i * 4); }
+    // the epilogue's operand of this thread's output (row tid/16, column tid%16), behind the weights
+    constexpr int EOP = EPI == EPI_RESID_XQ8 ? EPI_RESID_XA : EPI;
+    float eop = 0.f;
+    if constexpr (epi_has_operand<EOP>()) {
+        const int cq = tid & 15, nq = rt * 16 + (tid >> 4);
+        if (cq < NB && nq < p.N) eop = epi_operand<EOP>(p, nq, cq);
+    }
     if constexpr (PRE) {
         __builtin_amdgcn_sched_barrier(0);
         pre_finish<NB, K, PRO>(p, pre, act, sc);
     } else {
+        if constexpr (epi_has_operand<EOP>()) __builtin_amdgcn_sched_barrier(0);
         prologue<NB, K, PRO>(p, act, red, sc);
     }
 
@@ -202,7 +210,8 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
     const int n = rt * 16 + row;
     if (n >= p.N) return;
     if constexpr (EPI == EPI_QKV_SA) publish_qkv(p, v, n, col);
-    else if constexpr (EPI == EPI_RESID_XQ8) publish_x1(p, v, n, col);
+    else if constexpr (EPI == EPI_RESID_XQ8) publish_x1_op(p, v, n, col, eop);
+    else if constexpr (EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_ADD_STORE) epi_store_op<EPI>(p, v, n, col, eop);
     else epi_store<EPI>(p, v, n, col, EPI == EPI_LTX_ADD ? sc[col * LTD + n] : 0.f);
     ts_end(p.ts, t_start);
 }

@@ -927,6 +927,30 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
     }
 }
 
+// The epilogue's own operand of output (row n, slot b) -- the bias, the residual row, the
+// added row -- loaded when the launch starts: read in the epilogue it was a dependent L2 /
+// Infinity-Cache round trip after the dot products, on every such launch's critical path.
+// Each element is read and rewritten by the one lane that owns it, so the early value is
+// the value the epilogue read; epi_store_op / publish_x1_op compute the same expressions.
+template <int EPI>
+constexpr bool epi_has_operand() {
+    return EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_ADD_STORE || EPI == EPI_RESID_XA;
+}
+template <int EPI>
+__device__ __forceinline__ float epi_operand(const GemvP &p, int n, int b) {
+    if constexpr (EPI == EPI_BIAS) return p.bias[n];
+    else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID_XA) return p.resid[(size_t)b * D + n];
+    else if constexpr (EPI == EPI_ADD_STORE) return p.addsrc[(size_t)b * p.out_ld + n];
+    else return 0.f;
+}
+template <int EPI>
+__device__ __forceinline__ void epi_store_op(const GemvP &p, float v, int n, int b, float op) {
+    static_assert(EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_ADD_STORE, "epilogues with an operand");
+    if constexpr (EPI == EPI_BIAS) p.out[(size_t)b * p.out_ld + n] = v + op;
+    else if constexpr (EPI == EPI_RESID) p.resid[(size_t)b * D + n] = v + op;
+    else p.out[(size_t)b * p.out_ld + n] = v + op;
+}
+
 // Epilogue of output (row n, slot b) of a fused projection.
 template <int EPI>
 __device__ __forceinline__ void epi_store(const GemvP &p, float v, int n, int b, float extra = 0.f) {

@@ -315,6 +315,14 @@ __device__ __forceinline__ void publish_x1(const GemvP &p, float v, int n, int b
     __hip_atomic_store((gu64 *)(p.xh + (size_t)b * D + n), ((unsigned long long)tag << 32) | __float_as_uint(x1),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the same with the residual element loaded at launch start (epi_operand)
+__device__ __forceinline__ void publish_x1_op(const GemvP &p, float v, int n, int b, float r0) {
+    const float x1 = v + r0;
+    p.resid[(size_t)b * D + n] = x1;
+    const unsigned tag = (unsigned)p.iter[0] * 64u + p.layer + 1u;
+    __hip_atomic_store((gu64 *)(p.xh + (size_t)b * D + n), ((unsigned long long)tag << 32) | __float_as_uint(x1),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // the launch's XA workgroups (blockIdx.x >= nrow_blocks): split k % XA_SPLITS of slot k / XA_SPLITS
 __device__ __forceinline__ void xa_tail(const GemvP &p, unsigned long long t_start) {

@@ -33,8 +33,10 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -416,14 +418,30 @@ __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
         const float4 a4 = *(const float4 *)(p.act_alpha[br] + o);
         al[0] = a4.x; al[1] = a4.y; al[2] = a4.z; al[3] = a4.w;
     }
-    for (int tl = tid / (BM / 4); tl < BN; tl += NTH / (BM / 4)) {
+    // the residual rows of every step this thread stores, loaded before the first store
+    // (a load behind a store to another buffer waited one round trip per step)
+    constexpr int RSTEP = NTH / (BM / 4), IT = BN / RSTEP;
+    static_assert(BN % RSTEP == 0, "whole steps per thread");
+    const int tl0 = tid / (BM / 4);
+    float4 rres[IT];
+    if (p.resid[br]) {
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            const int t = t0 + tl0 + i * RSTEP;
+            rres[i] = t < p.T ? *(const float4 *)(p.resid[br] + chunk_out + (size_t)t * p.Coutp + o)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const int tl = tl0 + i * RSTEP;
         const int t = t0 + tl;
         if (t >= p.T) break;
         const float4 a4 = *(const float4 *)(ct + tl * CST + cl);
         float4 v = make_float4(a4.x + bb.x, a4.y + bb.y, a4.z + bb.z, a4.w + bb.w);
         const size_t off = chunk_out + (size_t)t * p.Coutp + o;
         if (p.resid[br]) {
-            const float4 r = *(const float4 *)(p.resid[br] + off);
+            const float4 r = rres[i];
             v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;  // input + h (568-599)
         }
         if (p.out[br]) *(float4 *)(p.out[br] + off) = v;
@@ -478,32 +496,88 @@ struct RbP {
     const float *bd[3], *b1[3];     // biases, zero padded to CP
     const float *al_in[3], *al_sk[3];  // HalfSnake alphas, zero padded to CP
     int ks[3];
-    int nsnake, creal, T, dil, tiles_per_chunk;
+    int nsnake, creal, T, dil, tiles_per_chunk, nchunk;
+    int ntiles;     // tiles per branch (nchunk x tiles_per_chunk)
+    int order[3];   // item order: branch of items [k ntiles, (k + 1) ntiles), most taps first
+    int *ctr;       // this launch's item counter (zeroed once per decode)
+    unsigned long long *ts;  // diagnostics (MAGPIE_CODEC_TS): per workgroup 8 phase stamps, else null
 };
 constexpr int RB_ROWB = LDS_ROWB;  // LDS bytes per time row of a 32-channel block
+constexpr int RB_TS_GX = 65536;    // diagnostics: stamp rows per branch (grid.x bound)
 // A-fragment ring slots of the residual-block convs (steps of lead for the weight loads)
 #ifndef MP_RB_RING
 #define MP_RB_RING 3
 #endif
 constexpr int RB_RING = MP_RB_RING;
+// rb_kernel's work items: (branch, tile), heaviest branch (most taps) first, one workgroup
+// per item in a 1-D grid. MP_RB_PERSIST=1: persistent workgroups taking items from a
+// counter, the next item's x rows prefetched into registers during the current item's
+// convolutions. Measured (gpurun_out/r05z_*, 8 x 32 frames): per-item with heaviest-first
+// order 1.584-1.599 ms against 1.647-1.649 for the earlier branch-major 2-D grid
+// (the 11-tap branch's workgroups no longer start last); persistent 1.91-1.92 ms -- the
+// prefetched rows (48 VGPRs at 128 channels) halve the workgroups per CU. Off.
+#ifndef MP_RB_PERSIST
+#define MP_RB_PERSIST 0
+#endif
+constexpr bool RB_PERSIST = MP_RB_PERSIST != 0;
 constexpr int RB_MAXHALO = 50;  // (11 - 1) * 5
 
 template <int RWV, int CWV, int NT>
 constexpr int rb_lds_bytes() { return RWV * (16 * NT * CWV + RB_MAXHALO) * RB_ROWB; }
 
-// NT: 16-step column tiles per wave (each A fragment feeds 2 NT MFMAs)
-template <int KS, int RWV, int CWV, int NT, int R>
-__device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
-    constexpr int NCB = RWV, CPD = NCB * 32;  // one wave row per 32-channel block
-    constexpr int NTH = 64 * RWV * CWV;
-    constexpr int NCD = 16 * NT * CWV;        // conv_d columns
-    constexpr int BN = NCD - 16;              // outputs per workgroup
-    constexpr int XR = NCD + RB_MAXHALO;      // LDS rows per channel block
-    constexpr int NS = NCB * KS;              // A-stream steps (channel block, tap)
-    const int br = blockIdx.y;
+// Work items (branch, tile), heaviest branch first (RB_PERSIST above). With PERSIST the
+// grid holds as many workgroups as the chip runs at once; workgroup g starts with item g,
+// takes the next from a per-launch counter and loads its x rows into registers right after
+// the current item's rows are staged (their HBM latency under the current item's convs:
+// tools_dev/codec_rb_timeline.py shows ~6 us of rows per workgroup on every stage). Tiles
+// and their arithmetic are the same in every form: the same bits.
+template <int RWV, int CWV, int NT>
+struct RbGeo {
+    static constexpr int NCB = RWV, CPD = NCB * 32, NTH = 64 * RWV * CWV;
+    static constexpr int NCD = 16 * NT * CWV;       // conv_d columns
+    static constexpr int BN = NCD - 16;             // outputs per tile
+    static constexpr int XR = NCD + RB_MAXHALO;     // LDS rows per channel block
+    static constexpr int PPR = NCB * 4, RSTEP = NTH / PPR, NU = (XR + RSTEP - 1) / RSTEP;
+    static_assert(NTH % PPR == 0, "fixed piece per thread");
+};
+// the x rows item `it` stages (thread: piece pc of rows r0 + u RSTEP), zero outside the chunk
+template <int RWV, int CWV, int NT>
+__device__ __forceinline__ void rb_load_rows(const RbP &p, int it, float4 (&v)[RbGeo<RWV, CWV, NT>::NU][2]) {
+    using G = RbGeo<RWV, CWV, NT>;
+    const int tid = threadIdx.x, pc = tid % G::PPR, r0 = tid / G::PPR;
+    const int br = p.order[it / p.ntiles], tile = it % p.ntiles;
+    const int halo = (p.ks[br] - 1) * p.dil, rows = G::NCD + halo;
+    const int chunk = tile / p.tiles_per_chunk, t0 = (tile % p.tiles_per_chunk) * G::BN, tx0 = t0 - 16 - halo;
+    const float *src = p.x[br] + (size_t)chunk * p.T * G::CPD + pc * 8;
+#pragma unroll
+    for (int u = 0; u < G::NU; ++u) {
+        const int r = r0 + u * G::RSTEP, t = tx0 + r;
+        v[u][0] = v[u][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < rows && t >= 0 && t < p.T) {
+            v[u][0] = *(const float4 *)(src + (size_t)t * G::CPD);
+            v[u][1] = *(const float4 *)(src + (size_t)t * G::CPD + 4);
+        }
+    }
+}
+// One item: branch br's tile `tile`, its rows in v. `next`: the item whose rows are loaded
+// into v once this item's rows are staged (none if >= 3 ntiles).
+template <int KS, int RWV, int CWV, int NT, int R, bool PERSIST>
+__device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile, int next,
+                                        float4 (&v)[RbGeo<RWV, CWV, NT>::NU][2], bool first) {
+    using G = RbGeo<RWV, CWV, NT>;
+    constexpr int NCB = G::NCB, CPD = G::CPD, NCD = G::NCD, BN = G::BN, XR = G::XR, RSTEP = G::RSTEP, NU = G::NU;
+    constexpr int PPR = G::PPR;
+    constexpr int NS = NCB * KS;  // A-stream steps (channel block, tap)
+    // diagnostics: thread 0 stamps the phases of its first item (A x rows staged, B conv_d,
+    // C the intermediate staged, D conv_1, E stored)
+    unsigned long long *tsw = p.ts && first ? p.ts + 8 * ((size_t)br * RB_TS_GX + blockIdx.x) : nullptr;
+    auto stamp = [&](int k) {
+        if (tsw && threadIdx.x == 0) tsw[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     const int d = p.dil, halo = (KS - 1) * d;
-    const int chunk = blockIdx.x / p.tiles_per_chunk;
-    const int t0 = (blockIdx.x % p.tiles_per_chunk) * BN;
+    const int chunk = tile / p.tiles_per_chunk;
+    const int t0 = (tile % p.tiles_per_chunk) * BN;
     const int tx0 = t0 - 16 - halo;           // time of x row 0 (conv_d column 0 is t0 - 16)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int rw = w % RWV, cw = w / RWV;
@@ -512,8 +586,6 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
 
     // ---- A: x rows -> HS_in -> f16 -> LDS (each thread keeps one 8-channel piece)
     {
-        constexpr int PPR = NCB * 4, RSTEP = NTH / PPR, NU = (XR + RSTEP - 1) / RSTEP;
-        static_assert(NTH % PPR == 0, "fixed piece per thread");
         const int pc = tid % PPR, c0 = pc * 8, r0 = tid / PPR;
         float al[8];
         {
@@ -522,17 +594,6 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
             al[4] = a1.x; al[5] = a1.y; al[6] = a1.z; al[7] = a1.w;
         }
         const int rows = NCD + halo;
-        const float *src = p.x[br] + cbase + c0;
-        float4 v[NU][2];
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int r = r0 + u * RSTEP, t = tx0 + r;
-            v[u][0] = v[u][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < rows && t >= 0 && t < p.T) {
-                v[u][0] = *(const float4 *)(src + (size_t)t * CPD);
-                v[u][1] = *(const float4 *)(src + (size_t)t * CPD + 4);
-            }
-        }
         char *dst = xs + (pc >> 2) * XR * RB_ROWB + 16 * (pc & 3);
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
@@ -546,7 +607,11 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
             *(half8 *)(dst + r * RB_ROWB) = h;
         }
     }
+    // the next item's rows, in flight during this item's convolutions
+    if constexpr (PERSIST)
+        if (next < 3 * p.ntiles) rb_load_rows<RWV, CWV, NT>(p, next, v);
     __syncthreads();
+    stamp(1);
 
     // ---- B / D: one causal conv from the LDS operand (rows: column c, tap k -> row
     // c * 1 + rowoff + k * dk), A stream from `wf` (conv2's ring), NT column tiles
@@ -602,13 +667,21 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
     // each lane's 8 channels: rw * 32 + a * 16 + 4 kg + r
     const int chl = rw * 32 + 4 * kg;
     __syncthreads();  // every wave is done reading x rows
+    stamp(2);
     // ---- C: h = f16(HS_sk(conv_d + b)) into LDS rows 0 .. NCD-1 (row c = time t0 - 16 + c)
     {
         typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        // the bias / alpha rows of both fragments first: one round trip, not one per fragment
+        float4 bbs[C2_WR], als[C2_WR];
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a) {
+            bbs[a] = *(const float4 *)(p.bd[br] + chl + a * 16);
+            als[a] = *(const float4 *)(p.al_sk[br] + chl + a * 16);
+        }
 #pragma unroll
         for (int a = 0; a < C2_WR; ++a) {
             const int ch = chl + a * 16;
-            const float4 bb = *(const float4 *)(p.bd[br] + ch), al = *(const float4 *)(p.al_sk[br] + ch);
+            const float4 bb = bbs[a], al = als[a];
             const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, av[4] = {al.x, al.y, al.z, al.w};
 #pragma unroll
             for (int j = 0; j < NT; ++j) {
@@ -622,34 +695,82 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs) {
         }
     }
     __syncthreads();
+    stamp(3);
     // ---- D: conv_1, output column o = time t0 + o, h row o + 16 - (KS - 1) + k
     const int nt = cw == CWV - 1 ? NT - 1 : NT;  // BN = 16 NT CWV - 16 outputs
     conv(p.W1[br], 16 - (KS - 1), 1, nt);
-    // ---- E: + bias + x -> x'
+    stamp(4);
+    // ---- E: + bias + x -> x'. Every residual element and bias first, then the stores: a
+    // load after a store to the other buffer may alias it, so per fragment the loop had
+    // waited one L2 round trip each
+    float4 bb1[C2_WR], rx[C2_WR][NT];
 #pragma unroll
     for (int a = 0; a < C2_WR; ++a) {
         const int ch = chl + a * 16;
-        const float4 bb = *(const float4 *)(p.b1[br] + ch);
+        bb1[a] = *(const float4 *)(p.b1[br] + ch);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int t = t0 + cw * 16 * NT + j * 16 + l16;
+            rx[a][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j < nt && t < p.T) rx[a][j] = *(const float4 *)(p.x[br] + cbase + (size_t)t * CPD + ch);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < C2_WR; ++a) {
+        const int ch = chl + a * 16;
+        const float4 bb = bb1[a];
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const int t = t0 + cw * 16 * NT + j * 16 + l16;
             if (j >= nt || t >= p.T) continue;
             const size_t off = cbase + (size_t)t * CPD + ch;
-            const float4 r = *(const float4 *)(p.x[br] + off);
+            const float4 r = rx[a][j];
             const floatx4 y = acc[a][j];
-            const float4 v = make_float4(y[0] + bb.x, y[1] + bb.y, y[2] + bb.z, y[3] + bb.w);
-            *(float4 *)(p.out[br] + off) = make_float4(r.x + v.x, r.y + v.y, r.z + v.z, r.w + v.w);  // input + h
+            const float4 vo = make_float4(y[0] + bb.x, y[1] + bb.y, y[2] + bb.z, y[3] + bb.w);
+            *(float4 *)(p.out[br] + off) = make_float4(r.x + vo.x, r.y + vo.y, r.z + vo.z, r.w + vo.w);  // input + h
         }
+    }
+    if (tsw) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        stamp(5);
     }
 }
 
-template <int RWV, int CWV, int NT>
+// PERSIST false: one item per workgroup (the grid covers every item), no prefetch -- for
+// the 224-channel stage, whose 14-wave workgroups cannot hold a second tile's rows
+template <int RWV, int CWV, int NT, bool PERSIST>
 __global__ __launch_bounds__(64 * RWV * CWV, RWV * CWV > 8 || NT > 4 ? 1 : 2) void rb_kernel(RbP p) {
     __shared__ __attribute__((aligned(16))) char xs[rb_lds_bytes<RWV, CWV, NT>()];
-    switch (p.ks[blockIdx.y]) {
-        case 3: rb_body<3, RWV, CWV, NT, RB_RING>(p, xs); break;
-        case 7: rb_body<7, RWV, CWV, NT, RB_RING>(p, xs); break;
-        default: rb_body<11, RWV, CWV, NT, RB_RING>(p, xs); break;
+    __shared__ int sh_next;
+    using G = RbGeo<RWV, CWV, NT>;
+    const int total = 3 * p.ntiles;
+    int it = blockIdx.x;
+    if (it >= total) return;
+    float4 v[G::NU][2];
+    if constexpr (!PERSIST) {  // one item: its rows loaded and staged in one place
+        const int br = p.order[it / p.ntiles], tile = it % p.ntiles;
+        switch (p.ks[br]) {
+            case 3: rb_load_rows<RWV, CWV, NT>(p, it, v); rb_body<3, RWV, CWV, NT, RB_RING, false>(p, xs, br, tile, total, v, true); break;
+            case 7: rb_load_rows<RWV, CWV, NT>(p, it, v); rb_body<7, RWV, CWV, NT, RB_RING, false>(p, xs, br, tile, total, v, true); break;
+            default: rb_load_rows<RWV, CWV, NT>(p, it, v); rb_body<11, RWV, CWV, NT, RB_RING, false>(p, xs, br, tile, total, v, true); break;
+        }
+        return;
+    }
+    rb_load_rows<RWV, CWV, NT>(p, it, v);
+    for (bool first = true; it < total; first = false) {
+        // the next item: from the per-launch counter (items below gridDim.x are the static
+        // first ones); the previous item's barriers have retired every read of sh_next
+        if (threadIdx.x == 0) sh_next = PERSIST ? (int)gridDim.x + atomicAdd(p.ctr, 1) : total;
+        __syncthreads();  // sh_next published; the previous item's conv_1 is done with the LDS rows
+        const int next = sh_next;
+        const int br = p.order[it / p.ntiles], tile = it % p.ntiles;
+        switch (p.ks[br]) {
+            case 3: rb_body<3, RWV, CWV, NT, RB_RING, PERSIST>(p, xs, br, tile, next, v, first); break;
+            case 7: rb_body<7, RWV, CWV, NT, RB_RING, PERSIST>(p, xs, br, tile, next, v, first); break;
+            default: rb_body<11, RWV, CWV, NT, RB_RING, PERSIST>(p, xs, br, tile, next, v, first); break;
+        }
+        it = next;
     }
 }
 
@@ -880,6 +1001,11 @@ struct mp_codec {
     size_t codes_cap = 0, audio_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;  // device time of the last decode (launch sequence only)
+    int *rb_ctr = nullptr;  // rb_kernel's item counters, one per launch of a decode (zeroed per decode)
+    // diagnostics (MAGPIE_CODEC_TS=stage,block,file): the phase stamps of one rb_kernel launch
+    unsigned long long *ts_dev = nullptr;
+    int ts_stage = -1, ts_block = -1;
+    std::string ts_file;
 };
 
 namespace {
@@ -1033,11 +1159,32 @@ hipError_t launch_conv2(mpc::ConvP p, int nchunk, int nbranch, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int RWV, int CWV, int NT = 4>
+template <int RWV, int CWV, int NT = 4, bool PERSIST = mpc::RB_PERSIST>
 hipError_t launch_rb(mpc::RbP p, int nchunk, hipStream_t s) {
     constexpr int BN = 16 * NT * CWV - 16;
     p.tiles_per_chunk = (p.T + BN - 1) / BN;
-    hipLaunchKernelGGL((mpc::rb_kernel<RWV, CWV, NT>), dim3(nchunk * p.tiles_per_chunk, 3), dim3(64 * RWV * CWV), 0, s, p);
+    p.nchunk = nchunk;
+    p.ntiles = nchunk * p.tiles_per_chunk;
+    // items heaviest first: the branches by tap count, descending
+    for (int j = 0; j < 3; ++j) p.order[j] = j;
+    std::sort(p.order, p.order + 3, [&](int a, int b) { return p.ks[a] > p.ks[b]; });
+    const int total = 3 * p.ntiles;
+    // persistent: as many workgroups as the chip runs at once (the kernel's occupancy
+    // times the CU count), each taking items from the counter; else one per item
+    int gx = total;
+    if (PERSIST) {
+        static int per_cu = -1, ncu = 0;
+        if (per_cu < 0) {
+            int dev = 0;
+            hipGetDevice(&dev);
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mpc::rb_kernel<RWV, CWV, NT, PERSIST>, 64 * RWV * CWV, 0) !=
+                    hipSuccess || per_cu < 1)
+                per_cu = 1;
+        }
+        gx = std::min(total, std::max(1, per_cu * ncu));
+    }
+    hipLaunchKernelGGL((mpc::rb_kernel<RWV, CWV, NT, PERSIST>), dim3(gx), dim3(64 * RWV * CWV), 0, s, p);
     return hipGetLastError();
 }
 // the fused residual block for a stage's padded channel count (0: not fused)
@@ -1051,7 +1198,7 @@ hipError_t run_rb(const mpc::RbP &p, int Cp, int nchunk, hipStream_t s) {
     // per wave everywhere but the 32-channel stage (32: 240 vs 273 us); 128 per wave took
     // 1.2-1.5x longer (one workgroup per CU), 32 per wave 1.3x on 128 / 64 channels
     switch (Cp) {
-        case 224: return launch_rb<7, 2>(p, nchunk, s);
+        case 224: return launch_rb<7, 2, 4, false>(p, nchunk, s);
         case 128: return launch_rb<4, 2>(p, nchunk, s);
         case 64: return launch_rb<2, 4>(p, nchunk, s);
         case 32: return launch_rb<1, 8, 2>(p, nchunk, s);
@@ -1084,6 +1231,9 @@ hipError_t run_conv(const mpc::ConvP &p, int BM, int mode, int nchunk, int nbran
 int codec_run(mp_codec *c, int nchunk, int F) {
     using namespace mpc;
     hipStream_t s = c->stream;
+    constexpr size_t NCTR = (size_t)NSTAGE * 3 * 16;
+    if (!c->rb_ctr) CHK(hipMalloc((void **)&c->rb_ctr, NCTR * sizeof(int)));
+    CHK(hipMemsetAsync(c->rb_ctr, 0, NCTR * sizeof(int), s));
     // pre-conv with the FSQ dequant in its loader
     {
         ConvP p{};
@@ -1143,6 +1293,8 @@ int codec_run(mp_codec *c, int nchunk, int F) {
                     rp.ks[j] = KS[j];
                 }
                 rp.nsnake = C / 2; rp.creal = C; rp.T = T; rp.dil = DIL[k];
+                rp.ts = (c->ts_dev && i == c->ts_stage && k == c->ts_block) ? c->ts_dev : nullptr;
+                rp.ctr = c->rb_ctr + (i * 3 + k) * 16;  // 64 B apart
                 CHK(run_rb(rp, Cp, nchunk, s));
             }
             continue;
@@ -1208,12 +1360,31 @@ int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, 
     if (int rc = ensure_buffers(c, n_chunks, chunk_frames)) return rc;
     CHK(hipMemcpyAsync(c->codes, codes, (size_t)n_chunks * 8 * chunk_frames * 4, hipMemcpyHostToDevice, c->stream));
     if (!c->ev0) { CHK(hipEventCreate(&c->ev0)); CHK(hipEventCreate(&c->ev1)); }
+    // diagnostics: MAGPIE_CODEC_TS=stage,block,file -> the phase stamps of that stage's
+    // rb_kernel launch for residual block `block` (tools_dev/codec_rb_timeline.py)
+    constexpr size_t TS_N = (size_t)3 * mpc::RB_TS_GX * 8;
+    if (const char *e = getenv("MAGPIE_CODEC_TS")) {
+        char file[512] = {0};
+        if (sscanf(e, "%d,%d,%511s", &c->ts_stage, &c->ts_block, file) == 3) {
+            c->ts_file = file;
+            if (!c->ts_dev) CHK(hipMalloc((void **)&c->ts_dev, TS_N * 8));
+            CHK(hipMemsetAsync(c->ts_dev, 0, TS_N * 8, c->stream));
+        }
+    }
     CHK(hipEventRecord(c->ev0, c->stream));
     if (int rc = codec_run(c, n_chunks, chunk_frames)) return rc;
     CHK(hipEventRecord(c->ev1, c->stream));
     CHK(hipMemcpyAsync(audio_out, c->audio, (size_t)n_chunks * chunk_frames * mpc::HOP * 4, hipMemcpyDeviceToHost, c->stream));
     CHK(hipStreamSynchronize(c->stream));
     CHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    if (c->ts_dev && !c->ts_file.empty()) {
+        std::vector<unsigned long long> h(TS_N);
+        CHK(hipMemcpy(h.data(), c->ts_dev, TS_N * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = fopen(c->ts_file.c_str(), "wb")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
     return MP_OK;
 }
 
@@ -1232,6 +1403,8 @@ void mp_hip_codec_free(mp_codec *c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void *p : c->weight_allocs) hipFree(p);
+    if (c->ts_dev) hipFree(c->ts_dev);
+    if (c->rb_ctr) hipFree(c->rb_ctr);
     float *bufs[5] = {c->x_pre, c->x0, c->brb[0], c->brb[1], c->brb[2]};
     for (float *b : bufs) if (b) hipFree(b);
     for (int j = 0; j < 3; ++j) {

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Phase timeline of the codec's per-block residual kernel (rb_kernel), from its in-kernel
+stamps (MAGPIE_CODEC_TS): per stage (first residual block), per branch, the workgroups'
+durations of A (x rows -> HalfSnake -> LDS), B (conv_d), C (intermediate -> LDS),
+D (conv_1), E (residual + store), and how the launch's workgroups spread in time.
+usage: codec_rb_timeline.py [stages...]   (default 1 2 3 4; 8 x 32-frame chunks)"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "magpie-tts.cpp_amd"))
+import magpie_amd as ma  # noqa: E402
+
+GX = 65536
+cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
+os.makedirs(cache, exist_ok=True)
+stages = [int(a) for a in sys.argv[1:]] or [1, 2, 3, 4]
+cdc = ma.Codec(ma.synth_gguf(os.path.join(cache, "nano_codec.gguf"), kind="codec"))
+codes = np.random.default_rng(0).integers(0, 2016, (8, 8, 32)).astype(np.int32)
+cdc.decode_chunks(codes)
+dump = os.path.join(REPO, "gpurun_out", "codec_ts.bin")
+os.makedirs(os.path.dirname(dump), exist_ok=True)
+for st in stages:
+    os.environ["MAGPIE_CODEC_TS"] = f"{st},0,{dump}"
+    cdc.decode_chunks(codes)
+    del os.environ["MAGPIE_CODEC_TS"]
+    ts = np.fromfile(dump, dtype=np.uint64).reshape(3, GX, 8).astype(np.int64)
+    live = ts[:, :, 0] > 0
+    t_min = ts[:, :, 0][live].min()
+    t_max = ts[:, :, 5][live].max()
+    print(f"stage {st}: {live.sum()} workgroups, launch span {(t_max - t_min) * 0.01:.1f} us")
+    for br in range(3):
+        r = ts[br][live[br]]
+        if not len(r):
+            continue
+        d = np.diff(r[:, :6], axis=1) * 0.01
+        tot = (r[:, 5] - r[:, 0]) * 0.01
+        st0 = (r[:, 0] - t_min) * 0.01
+        names = ["A rows", "B conv_d", "C stage", "D conv_1", "E store"]
+        parts = " | ".join(f"{n} {np.median(d[:, i]):5.2f}" for i, n in enumerate(names))
+        print(f"  branch {br} ({len(r)} wgs): per workgroup p50 {parts} | total {np.median(tot):5.2f} "
+              f"(max {tot.max():5.2f}); starts spread {st0.max():5.1f} us")
+cdc.close()

@@ -70,15 +70,20 @@ constexpr int LDS_ROWB = MP_CODEC_ROWB;
 // barrier after it): left free, the scheduler sank the loads to just before their MFMAs
 // (issue, then s_waitcnt vmcnt(1) four instructions later), exposing the L2 latency at
 // every step. Measured (gpurun_out/r05q_*): the 448-channel stage's conv2_kernel 241 ->
-// 180 us per decode; the same barrier in rb_kernel (3-slot ring, 2 workgroups per CU)
-// cost 5-7 % on every stage (it also fences the B-fragment reads), so only conv2 pins.
+// 180 us per decode. rb_kernel: its steps run as one flat (channel block, tap) sequence,
+// each step's B fragments read one step ahead (across channel blocks too) and pinned
+// before the step's MFMAs, the ring loads pinned after them (MP_RB_PIN 2): 8 x 32 frames
+// 1.58 -> 1.48 ms (gpurun_out/r05ze_*; the ring loads alone, 1: 1.49; a 2-slot ring 1.53;
+// a 4-slot one takes more than 128 VGPRs). Pinned per tap loop with the B reads fenced at
+// every channel block's start, it had cost 5-7 %.
 #ifndef MP_CONV2_PIN
 #define MP_CONV2_PIN 1
 #endif
 #ifndef MP_RB_PIN
-#define MP_RB_PIN 0
+#define MP_RB_PIN 2
 #endif
-constexpr bool CONV2_PIN = MP_CONV2_PIN != 0, RB_PIN = MP_RB_PIN != 0;
+constexpr bool CONV2_PIN = MP_CONV2_PIN != 0;
+constexpr int RB_PIN = MP_RB_PIN;  // 1: sched barrier after the ring loads, 2: and after the B loads
 
 enum InMode { IN_F16 = 0, IN_FSQ = 1 };
 
@@ -124,6 +129,26 @@ __device__ __forceinline__ float half_snake_sel(float v, int c, int n_snake, int
     const float snake = v + (s * s) * __builtin_amdgcn_rcpf(a);  // 1 / a: loop-invariant per channel, hoisted
     const float leaky = fmaxf(v, 0.01f * v);
     return c < n_snake ? snake : (c < cin_real ? leaky : 0.f);
+}
+
+// The two HalfSnake forms apart (the same arithmetic as half_snake_sel's), for waves whose
+// channels are all of one kind: HalfSnake's split (C / 2) is a multiple of 16 on every
+// stage, so a wave's fragment or row piece is snake-only or leaky-only and computes one
+// form instead of both (hs_wave_kind's vote; mixed or padded channels take the select)
+__device__ __forceinline__ float hs_snake(float v, float a) {
+    const float s = __sinf(v * a);
+    return v + (s * s) * __builtin_amdgcn_rcpf(a);
+}
+__device__ __forceinline__ float hs_leaky(float v) { return fmaxf(v, 0.01f * v); }
+// 0: every lane's channels [c0, c1] snake, 1: every lane's leaky, 2: otherwise
+#ifndef MP_HS_SPLIT
+#define MP_HS_SPLIT 1
+#endif
+__device__ __forceinline__ int hs_wave_kind(int c0, int c1, int n_snake, int cin_real) {
+    if (!MP_HS_SPLIT) return 2;
+    if (__all(c1 < n_snake)) return 0;
+    if (__all(c0 >= n_snake && c1 < cin_real)) return 1;
+    return 2;
 }
 
 // fsq_dequantize_cpu (nano-codec.cpp:721-752): channel c = 4*cb + d
@@ -500,10 +525,11 @@ struct RbP {
     int ntiles;     // tiles per branch (nchunk x tiles_per_chunk)
     int order[3];   // item order: branch of items [k ntiles, (k + 1) ntiles), most taps first
     int *ctr;       // this launch's item counter (zeroed once per decode)
-    unsigned long long *ts;  // diagnostics (MAGPIE_CODEC_TS): per workgroup 8 phase stamps, else null
+    unsigned long long *ts;  // diagnostics (MAGPIE_CODEC_TS): per workgroup RB_TS_N phase stamps, else null
 };
 constexpr int RB_ROWB = LDS_ROWB;  // LDS bytes per time row of a 32-channel block
 constexpr int RB_TS_GX = 65536;    // diagnostics: stamp rows per branch (grid.x bound)
+constexpr int RB_TS_N = 16;        // diagnostics: stamps per workgroup
 // A-fragment ring slots of the residual-block convs (steps of lead for the weight loads)
 #ifndef MP_RB_RING
 #define MP_RB_RING 3
@@ -520,10 +546,24 @@ constexpr int RB_RING = MP_RB_RING;
 #define MP_RB_PERSIST 0
 #endif
 constexpr bool RB_PERSIST = MP_RB_PERSIST != 0;
+// rb_kernel's conv_d bias, HS_sk alpha and conv_1 bias staged in LDS with the x rows (1), or
+// loaded from global memory where phases C / E use them (0)
+#ifndef MP_RB_PRM
+#define MP_RB_PRM 1
+#endif
+constexpr bool RB_PRM = MP_RB_PRM != 0;
+// rb_kernel's residual rows (phase E) loaded before conv_1 (1) or after it (0)
+#ifndef MP_RB_RXPRE
+#define MP_RB_RXPRE 0
+#endif
+constexpr bool RB_RXPRE = MP_RB_RXPRE != 0;
 constexpr int RB_MAXHALO = 50;  // (11 - 1) * 5
 
 template <int RWV, int CWV, int NT>
 constexpr int rb_lds_bytes() { return RWV * (16 * NT * CWV + RB_MAXHALO) * RB_ROWB; }
+// + the staged parameters (RB_PRM): bd, al_sk, b1, CP floats each
+template <int RWV, int CWV, int NT>
+constexpr int rb_lds_total() { return rb_lds_bytes<RWV, CWV, NT>() + (RB_PRM ? 3 * RWV * 32 * 4 : 0); }
 
 // Work items (branch, tile), heaviest branch first (RB_PERSIST above). With PERSIST the
 // grid holds as many workgroups as the chip runs at once; workgroup g starts with item g,
@@ -539,12 +579,19 @@ struct RbGeo {
     static constexpr int XR = NCD + RB_MAXHALO;     // LDS rows per channel block
     static constexpr int PPR = NCB * 4, RSTEP = NTH / PPR, NU = (XR + RSTEP - 1) / RSTEP;
     static_assert(NTH % PPR == 0, "fixed piece per thread");
+    // the x-row pieces (8 channels) of a thread: with HALF, wave pair (2k, 2k + 1) holds
+    // rows k 64 / PH ... of the low / high channel half, so a wave's pieces are all snake
+    // or all leaky (hs_wave_kind); else thread t holds piece t % PPR of row t / PPR
+    static constexpr int PH = PPR / 2;
+    static constexpr bool HALF = PPR % 2 == 0 && 64 % PH == 0 && (NTH / 64) % 2 == 0;
+    __device__ static int piece(int tid) { return HALF ? ((tid >> 6) & 1) * PH + (tid & 63) % PH : tid % PPR; }
+    __device__ static int row0(int tid) { return HALF ? (tid >> 7) * (64 / PH) + (tid & 63) / PH : tid / PPR; }
 };
 // the x rows item `it` stages (thread: piece pc of rows r0 + u RSTEP), zero outside the chunk
 template <int RWV, int CWV, int NT>
 __device__ __forceinline__ void rb_load_rows(const RbP &p, int it, float4 (&v)[RbGeo<RWV, CWV, NT>::NU][2]) {
     using G = RbGeo<RWV, CWV, NT>;
-    const int tid = threadIdx.x, pc = tid % G::PPR, r0 = tid / G::PPR;
+    const int tid = threadIdx.x, pc = G::piece(tid), r0 = G::row0(tid);
     const int br = p.order[it / p.ntiles], tile = it % p.ntiles;
     const int halo = (p.ks[br] - 1) * p.dil, rows = G::NCD + halo;
     const int chunk = tile / p.tiles_per_chunk, t0 = (tile % p.tiles_per_chunk) * G::BN, tx0 = t0 - 16 - halo;
@@ -569,8 +616,9 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     constexpr int PPR = G::PPR;
     constexpr int NS = NCB * KS;  // A-stream steps (channel block, tap)
     // diagnostics: thread 0 stamps the phases of its first item (A x rows staged, B conv_d,
-    // C the intermediate staged, D conv_1, E stored)
-    unsigned long long *tsw = p.ts && first ? p.ts + 8 * ((size_t)br * RB_TS_GX + blockIdx.x) : nullptr;
+    // C the intermediate staged, D conv_1, E stored; wave 0's own: 9 conv_d done, 6 its part
+    // of C computed, 7 its residual rows landed, 8 its stores done)
+    unsigned long long *tsw = p.ts && first ? p.ts + RB_TS_N * ((size_t)br * RB_TS_GX + blockIdx.x) : nullptr;
     auto stamp = [&](int k) {
         if (tsw && threadIdx.x == 0) tsw[k] = __builtin_amdgcn_s_memrealtime();
     };
@@ -584,9 +632,21 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     const int kg = lane >> 4, l16 = lane & 15;
     const size_t cbase = (size_t)chunk * p.T * CPD;
 
+    // the staged parameters: [bd | al_sk | b1], CPD floats each, behind the row blocks
+    float *prm = (float *)(xs + rb_lds_bytes<RWV, CWV, NT>());
+    constexpr int NPRM = 3 * CPD / 4;  // float4 pieces
+    static_assert(NPRM <= G::NTH, "one piece per thread");
+    float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (RB_PRM) {
+        if (tid < NPRM) {
+            const int which = tid / (CPD / 4), o = (tid % (CPD / 4)) * 4;
+            const float *src = which == 0 ? p.bd[br] : which == 1 ? p.al_sk[br] : p.b1[br];
+            pv = *(const float4 *)(src + o);
+        }
+    }
     // ---- A: x rows -> HS_in -> f16 -> LDS (each thread keeps one 8-channel piece)
     {
-        const int pc = tid % PPR, c0 = pc * 8, r0 = tid / PPR;
+        const int pc = G::piece(tid), c0 = pc * 8, r0 = G::row0(tid);
         float al[8];
         {
             const float4 a0 = *(const float4 *)(p.al_in[br] + c0), a1 = *(const float4 *)(p.al_in[br] + c0 + 4);
@@ -595,18 +655,26 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
         }
         const int rows = NCD + halo;
         char *dst = xs + (pc >> 2) * XR * RB_ROWB + 16 * (pc & 3);
+        auto stage_rows = [&](auto hs) {
 #pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int r = r0 + u * RSTEP, t = tx0 + r;
-            if (r >= rows) break;
-            const float vv[8] = {v[u][0].x, v[u][0].y, v[u][0].z, v[u][0].w, v[u][1].x, v[u][1].y, v[u][1].z, v[u][1].w};
-            half8 h;
+            for (int u = 0; u < NU; ++u) {
+                const int r = r0 + u * RSTEP, t = tx0 + r;
+                if (r >= rows) break;
+                const float vv[8] = {v[u][0].x, v[u][0].y, v[u][0].z, v[u][0].w, v[u][1].x, v[u][1].y, v[u][1].z, v[u][1].w};
+                half8 h;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) h[i] = (_Float16)half_snake_sel(vv[i], c0 + i, p.nsnake, p.creal, al[i]);
-            if (t < 0 || t >= p.T) h = half8{0, 0, 0, 0, 0, 0, 0, 0};  // causal zero padding / past the chunk
-            *(half8 *)(dst + r * RB_ROWB) = h;
-        }
+                for (int i = 0; i < 8; ++i) h[i] = (_Float16)hs(vv[i], i);
+                if (t < 0 || t >= p.T) h = half8{0, 0, 0, 0, 0, 0, 0, 0};  // causal zero padding / past the chunk
+                *(half8 *)(dst + r * RB_ROWB) = h;
+            }
+        };
+        const int kind = hs_wave_kind(c0, c0 + 7, p.nsnake, p.creal);
+        if (kind == 0) stage_rows([&](float x, int i) { return hs_snake(x, al[i]); });
+        else if (kind == 1) stage_rows([&](float x, int) { return hs_leaky(x); });
+        else stage_rows([&](float x, int i) { return half_snake_sel(x, c0 + i, p.nsnake, p.creal, al[i]); });
     }
+    if constexpr (RB_PRM)
+        if (tid < NPRM) *(float4 *)(prm + 4 * tid) = pv;
     // the next item's rows, in flight during this item's convolutions
     if constexpr (PERSIST)
         if (next < 3 * p.ntiles) rb_load_rows<RWV, CWV, NT>(p, next, v);
@@ -630,35 +698,36 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
                 ring[q][0] = *(const half8 *)(wrow0 + (size_t)q * 512);
                 ring[q][1] = *(const half8 *)(wrow1 + (size_t)q * 512);
             }
+        // B fragment j of step (cb, k): x / h rows colb + rowoff + 16 j + k dk of channel block cb
+        const char *bbase = xs + (colb + rowoff) * RB_ROWB + 16 * kg;
+        auto bfrag = [&](int st, int j) {
+            return *(const half8 *)(bbase + (st / KS) * XR * RB_ROWB + (j * 16 + (st % KS) * dk) * RB_ROWB);
+        };
+        half8 bc[NT], bn[NT];
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-            const char *bbase = xs + cb * XR * RB_ROWB + (colb + rowoff) * RB_ROWB + 16 * kg;
-            half8 bc[NT], bn[NT];
+        for (int j = 0; j < NT; ++j) bc[j] = bfrag(0, j);
 #pragma unroll
-            for (int j = 0; j < NT; ++j) bc[j] = *(const half8 *)(bbase + j * 16 * RB_ROWB);
+        for (int st = 0; st < NS; ++st) {
+            if (st + 1 < NS) {  // the next step's B fragments (across channel blocks too)
 #pragma unroll
-            for (int k = 0; k < KS; ++k) {
-                const int st = cb * KS + k;
-                if (k + 1 < KS) {
+                for (int j = 0; j < NT; ++j) bn[j] = bfrag(st + 1, j);
+            }
+            if constexpr (RB_PIN >= 2) __builtin_amdgcn_sched_barrier(0);  // ... issued before this step's MFMAs
 #pragma unroll
-                    for (int j = 0; j < NT; ++j) bn[j] = *(const half8 *)(bbase + (j * 16 + (k + 1) * dk) * RB_ROWB);
+            for (int j = 0; j < NT; ++j) {
+                if (j < nt) {
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][0], bc[j], acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][1], bc[j], acc[1][j], 0, 0, 0);
                 }
+            }
+            if (st + R < NS) {
+                ring[st % R][0] = *(const half8 *)(wrow0 + (size_t)(st + R) * 512);
+                ring[st % R][1] = *(const half8 *)(wrow1 + (size_t)(st + R) * 512);
+            }
+            if constexpr (RB_PIN >= 1) __builtin_amdgcn_sched_barrier(0);  // the ring loads stay R steps ahead
+            if (st + 1 < NS) {
 #pragma unroll
-                for (int j = 0; j < NT; ++j) {
-                    if (j < nt) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][0], bc[j], acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][1], bc[j], acc[1][j], 0, 0, 0);
-                    }
-                }
-                if (st + R < NS) {
-                    ring[st % R][0] = *(const half8 *)(wrow0 + (size_t)(st + R) * 512);
-                    ring[st % R][1] = *(const half8 *)(wrow1 + (size_t)(st + R) * 512);
-                }
-                if constexpr (RB_PIN) __builtin_amdgcn_sched_barrier(0);  // the ring loads stay R steps ahead
-                if (k + 1 < KS) {
-#pragma unroll
-                    for (int j = 0; j < NT; ++j) bc[j] = bn[j];
-                }
+                for (int j = 0; j < NT; ++j) bc[j] = bn[j];
             }
         }
     };
@@ -666,6 +735,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     conv(p.Wd[br], 0, d, NT);
     // each lane's 8 channels: rw * 32 + a * 16 + 4 kg + r
     const int chl = rw * 32 + 4 * kg;
+    stamp(9);
     __syncthreads();  // every wave is done reading x rows
     stamp(2);
     // ---- C: h = f16(HS_sk(conv_d + b)) into LDS rows 0 .. NCD-1 (row c = time t0 - 16 + c)
@@ -675,45 +745,69 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
         float4 bbs[C2_WR], als[C2_WR];
 #pragma unroll
         for (int a = 0; a < C2_WR; ++a) {
-            bbs[a] = *(const float4 *)(p.bd[br] + chl + a * 16);
-            als[a] = *(const float4 *)(p.al_sk[br] + chl + a * 16);
+            if constexpr (RB_PRM) {
+                bbs[a] = *(const float4 *)(prm + chl + a * 16);
+                als[a] = *(const float4 *)(prm + CPD + chl + a * 16);
+            } else {
+                bbs[a] = *(const float4 *)(p.bd[br] + chl + a * 16);
+                als[a] = *(const float4 *)(p.al_sk[br] + chl + a * 16);
+            }
         }
 #pragma unroll
         for (int a = 0; a < C2_WR; ++a) {
             const int ch = chl + a * 16;
             const float4 bb = bbs[a], al = als[a];
             const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, av[4] = {al.x, al.y, al.z, al.w};
+            auto stage_frag = [&](auto hs) {
 #pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const int c = cw * 16 * NT + j * 16 + l16, t = t0 - 16 + c;
-                half4 h;
+                for (int j = 0; j < NT; ++j) {
+                    const int c = cw * 16 * NT + j * 16 + l16, t = t0 - 16 + c;
+                    half4 h;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) h[r] = (_Float16)half_snake_sel(acc[a][j][r] + bv[r], ch + r, p.nsnake, p.creal, av[r]);
-                if (t < 0) h = half4{0, 0, 0, 0};
-                *(half4 *)(xs + rw * XR * RB_ROWB + c * RB_ROWB + (a * 16 + 4 * kg) * 2) = h;
-            }
+                    for (int r = 0; r < 4; ++r) h[r] = (_Float16)hs(acc[a][j][r] + bv[r], r);
+                    if (t < 0) h = half4{0, 0, 0, 0};
+                    *(half4 *)(xs + rw * XR * RB_ROWB + c * RB_ROWB + (a * 16 + 4 * kg) * 2) = h;
+                }
+            };
+            const int kind = hs_wave_kind(ch, ch + 3, p.nsnake, p.creal);
+            if (kind == 0) stage_frag([&](float x, int r) { return hs_snake(x, av[r]); });
+            else if (kind == 1) stage_frag([&](float x, int) { return hs_leaky(x); });
+            else stage_frag([&](float x, int r) { return half_snake_sel(x, ch + r, p.nsnake, p.creal, av[r]); });
         }
     }
+    stamp(6);
     __syncthreads();
     stamp(3);
     // ---- D: conv_1, output column o = time t0 + o, h row o + 16 - (KS - 1) + k
     const int nt = cw == CWV - 1 ? NT - 1 : NT;  // BN = 16 NT CWV - 16 outputs
+    // ---- E's operands: every residual element and bias before the stores (a load after a
+    // store to the other buffer may alias it, so per fragment the loop had waited one L2
+    // round trip each); with RB_RXPRE before conv_1, their latency under its MFMAs
+    float4 bb1[C2_WR], rx[C2_WR][NT];
+    auto load_e = [&]() {
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a) {
+            const int ch = chl + a * 16;
+            bb1[a] = RB_PRM ? *(const float4 *)(prm + 2 * CPD + ch) : *(const float4 *)(p.b1[br] + ch);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int t = t0 + cw * 16 * NT + j * 16 + l16;
+                rx[a][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (j < nt && t < p.T) rx[a][j] = *(const float4 *)(p.x[br] + cbase + (size_t)t * CPD + ch);
+            }
+        }
+    };
+    if constexpr (RB_RXPRE) {
+        load_e();
+        __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to their use
+    }
     conv(p.W1[br], 16 - (KS - 1), 1, nt);
     stamp(4);
-    // ---- E: + bias + x -> x'. Every residual element and bias first, then the stores: a
-    // load after a store to the other buffer may alias it, so per fragment the loop had
-    // waited one L2 round trip each
-    float4 bb1[C2_WR], rx[C2_WR][NT];
-#pragma unroll
-    for (int a = 0; a < C2_WR; ++a) {
-        const int ch = chl + a * 16;
-        bb1[a] = *(const float4 *)(p.b1[br] + ch);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int t = t0 + cw * 16 * NT + j * 16 + l16;
-            rx[a][j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (j < nt && t < p.T) rx[a][j] = *(const float4 *)(p.x[br] + cbase + (size_t)t * CPD + ch);
-        }
+    // ---- E: + bias + x -> x'
+    if constexpr (!RB_RXPRE) load_e();
+    if (tsw) {  // diagnostics: wave 0's residual rows landed
+        __builtin_amdgcn_s_waitcnt(0);
+        stamp(7);
     }
 #pragma unroll
     for (int a = 0; a < C2_WR; ++a) {
@@ -732,6 +826,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     }
     if (tsw) {
         __builtin_amdgcn_s_waitcnt(0);
+        stamp(8);
         __syncthreads();
         stamp(5);
     }
@@ -739,9 +834,23 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
 
 // PERSIST false: one item per workgroup (the grid covers every item), no prefetch -- for
 // the 224-channel stage, whose 14-wave workgroups cannot hold a second tile's rows
+// minimum waves per SIMD the register allocation must allow (launch bounds): MP_RB3_W /
+// MP_RB4_W for the 64- / 32-channel stages' kernels (<2,4,4> / <1,8,2>), 0: the default
+#ifndef MP_RB3_W
+#define MP_RB3_W 0
+#endif
+#ifndef MP_RB4_W
+#define MP_RB4_W 0
+#endif
+template <int RWV, int CWV, int NT>
+constexpr int rb_minw() {
+    if (RWV == 2 && CWV == 4 && NT == 4 && MP_RB3_W) return MP_RB3_W;
+    if (RWV == 1 && CWV == 8 && NT == 2 && MP_RB4_W) return MP_RB4_W;
+    return RWV * CWV > 8 || NT > 4 ? 1 : 2;
+}
 template <int RWV, int CWV, int NT, bool PERSIST>
-__global__ __launch_bounds__(64 * RWV * CWV, RWV * CWV > 8 || NT > 4 ? 1 : 2) void rb_kernel(RbP p) {
-    __shared__ __attribute__((aligned(16))) char xs[rb_lds_bytes<RWV, CWV, NT>()];
+__global__ __launch_bounds__(64 * RWV * CWV, (rb_minw<RWV, CWV, NT>())) void rb_kernel(RbP p) {
+    __shared__ __attribute__((aligned(16))) char xs[rb_lds_total<RWV, CWV, NT>()];
     __shared__ int sh_next;
     using G = RbGeo<RWV, CWV, NT>;
     const int total = 3 * p.ntiles;
@@ -1362,7 +1471,7 @@ int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, 
     if (!c->ev0) { CHK(hipEventCreate(&c->ev0)); CHK(hipEventCreate(&c->ev1)); }
     // diagnostics: MAGPIE_CODEC_TS=stage,block,file -> the phase stamps of that stage's
     // rb_kernel launch for residual block `block` (tools_dev/codec_rb_timeline.py)
-    constexpr size_t TS_N = (size_t)3 * mpc::RB_TS_GX * 8;
+    constexpr size_t TS_N = (size_t)3 * mpc::RB_TS_GX * mpc::RB_TS_N;
     if (const char *e = getenv("MAGPIE_CODEC_TS")) {
         char file[512] = {0};
         if (sscanf(e, "%d,%d,%511s", &c->ts_stage, &c->ts_block, file) == 3) {

@@ -2,7 +2,7 @@
 """Phase timeline of the codec's per-block residual kernel (rb_kernel), from its in-kernel
 stamps (MAGPIE_CODEC_TS): per stage (first residual block), per branch, the workgroups'
 durations of A (x rows -> HalfSnake -> LDS), B (conv_d), C (intermediate -> LDS),
-D (conv_1), E (residual + store), and how the launch's workgroups spread in time.
+D (conv_1), E (residual + store), wave 0's own part of C and of E's loads, and how the launch's workgroups spread in time.
 usage: codec_rb_timeline.py [stages...]   (default 1 2 3 4; 8 x 32-frame chunks)"""
 import os
 import sys
@@ -26,7 +26,7 @@ for st in stages:
     os.environ["MAGPIE_CODEC_TS"] = f"{st},0,{dump}"
     cdc.decode_chunks(codes)
     del os.environ["MAGPIE_CODEC_TS"]
-    ts = np.fromfile(dump, dtype=np.uint64).reshape(3, GX, 8).astype(np.int64)
+    ts = np.fromfile(dump, dtype=np.uint64).reshape(3, GX, 16).astype(np.int64)
     live = ts[:, :, 0] > 0
     t_min = ts[:, :, 0][live].min()
     t_max = ts[:, :, 5][live].max()
@@ -40,6 +40,12 @@ for st in stages:
         st0 = (r[:, 0] - t_min) * 0.01
         names = ["A rows", "B conv_d", "C stage", "D conv_1", "E store"]
         parts = " | ".join(f"{n} {np.median(d[:, i]):5.2f}" for i, n in enumerate(names))
+        if (r[:, 6] > 0).all() and (r[:, 7] > 0).all():  # wave 0's own part of C / E
+            c0 = np.median(r[:, 6] - r[:, 2]) * 0.01
+            e0 = np.median(r[:, 7] - r[:, 4]) * 0.01
+            b0 = np.median(r[:, 9] - r[:, 1]) * 0.01
+            s0 = np.median(r[:, 8] - r[:, 7]) * 0.01
+            parts += f" || wave 0: conv_d {b0:5.2f} C {c0:4.2f} E rows {e0:4.2f} stores {s0:4.2f}"
         print(f"  branch {br} ({len(r)} wgs): per workgroup p50 {parts} | total {np.median(tot):5.2f} "
               f"(max {tot.max():5.2f}); starts spread {st0.max():5.1f} us")
 cdc.close()

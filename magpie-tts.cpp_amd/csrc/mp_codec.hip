@@ -105,6 +105,7 @@ struct ConvP {
     int act_nsnake, cout_real;
     int Cinp, Coutp, T, dil;
     int tiles_per_chunk;
+    int zorder[3];           // conv2_kernel: branch of grid.z slice z (most taps first)
 };
 
 __device__ __forceinline__ float half_snake(float v, int c, int n_snake, int cin_real, const float *alpha) {
@@ -333,7 +334,7 @@ __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
     constexpr int MAXHALO = 50;          // (11 - 1) * 5
     constexpr int BUFB = (BN + MAXHALO) * ROWB;
     constexpr int RPT = ((BN + MAXHALO) * 4 + NTH - 1) / NTH;  // 16-byte row pieces per thread
-    const int br = blockIdx.z;
+    const int br = p.zorder[blockIdx.z];
     const int dil = p.dil;
     const int pad = (KS - 1) * dil;
     const int m0 = blockIdx.x * (RWV * 32);
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(64 * RWV * CWV, DEEP ? 1 : 2) void conv2_kernel(Con
     constexpr int BN = CWV * 16 * C2_NT;
     constexpr int XSB = 2 * (BN + 50) * LDS_ROWB, CTB = BN * (RWV * 32 + 4) * 4;  // input buffers / epilogue tile
     __shared__ __attribute__((aligned(16))) char xs[XSB > CTB ? XSB : CTB];
-    switch (p.ks[blockIdx.z]) {
+    switch (p.ks[p.zorder[blockIdx.z]]) {
         case 3: conv2_body<3, RWV, CWV, NCB, DEEP ? 6 : 3>(p, xs); break;
         case 7: conv2_body<7, RWV, CWV, NCB, DEEP ? 7 : 3>(p, xs); break;
         default: conv2_body<11, RWV, CWV, NCB, DEEP ? 11 : 3>(p, xs); break;
@@ -528,8 +529,8 @@ struct RbP {
     unsigned long long *ts;  // diagnostics (MAGPIE_CODEC_TS): per workgroup RB_TS_N phase stamps, else null
 };
 constexpr int RB_ROWB = LDS_ROWB;  // LDS bytes per time row of a 32-channel block
-constexpr int RB_TS_GX = 65536;    // diagnostics: stamp rows per branch (grid.x bound)
-constexpr int RB_TS_N = 16;        // diagnostics: stamps per workgroup
+constexpr int RB_TS_GX = 16384;    // diagnostics: stamp rows per branch (workgroups beyond: none)
+constexpr int RB_TS_N = 48;        // diagnostics: stamps per workgroup (16 + 2 per wave)
 // A-fragment ring slots of the residual-block convs (steps of lead for the weight loads)
 #ifndef MP_RB_RING
 #define MP_RB_RING 3
@@ -618,7 +619,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     // diagnostics: thread 0 stamps the phases of its first item (A x rows staged, B conv_d,
     // C the intermediate staged, D conv_1, E stored; wave 0's own: 9 conv_d done, 6 its part
     // of C computed, 7 its residual rows landed, 8 its stores done)
-    unsigned long long *tsw = p.ts && first ? p.ts + RB_TS_N * ((size_t)br * RB_TS_GX + blockIdx.x) : nullptr;
+    unsigned long long *tsw = p.ts && first && blockIdx.x < RB_TS_GX ? p.ts + RB_TS_N * ((size_t)br * RB_TS_GX + blockIdx.x) : nullptr;
     auto stamp = [&](int k) {
         if (tsw && threadIdx.x == 0) tsw[k] = __builtin_amdgcn_s_memrealtime();
     };
@@ -736,6 +737,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     // each lane's 8 channels: rw * 32 + a * 16 + 4 kg + r
     const int chl = rw * 32 + 4 * kg;
     stamp(9);
+    if (tsw && lane == 0) tsw[16 + 2 * w] = __builtin_amdgcn_s_memrealtime();  // every wave's conv_d end
     __syncthreads();  // every wave is done reading x rows
     stamp(2);
     // ---- C: h = f16(HS_sk(conv_d + b)) into LDS rows 0 .. NCD-1 (row c = time t0 - 16 + c)
@@ -803,6 +805,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     }
     conv(p.W1[br], 16 - (KS - 1), 1, nt);
     stamp(4);
+    if (tsw && lane == 0) tsw[17 + 2 * w] = __builtin_amdgcn_s_memrealtime();  // every wave's conv_1 end
     // ---- E: + bias + x -> x'
     if constexpr (!RB_RXPRE) load_e();
     if (tsw) {  // diagnostics: wave 0's residual rows landed
@@ -842,10 +845,41 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
 #ifndef MP_RB4_W
 #define MP_RB4_W 0
 #endif
+// per stage (224 / 128 / 64 / 32 channels): column waves (CWV) and 16-column fragments
+// per wave (NT); a tile is 16 NT CWV - 16 outputs
+#ifndef MP_RB1_CWV
+#define MP_RB1_CWV 2
+#endif
+#ifndef MP_RB1_NT
+#define MP_RB1_NT 4
+#endif
+#ifndef MP_RB2_CWV
+#define MP_RB2_CWV 2
+#endif
+#ifndef MP_RB2_NT
+#define MP_RB2_NT 4
+#endif
+#ifndef MP_RB3_CWV
+#define MP_RB3_CWV 4
+#endif
+#ifndef MP_RB3_NT
+#define MP_RB3_NT 4
+#endif
+#ifndef MP_RB4_CWV
+#define MP_RB4_CWV 8
+#endif
+#ifndef MP_RB4_NT
+#define MP_RB4_NT 2
+#endif
+#ifndef MP_RB1_W
+#define MP_RB1_W 0
+#endif
 template <int RWV, int CWV, int NT>
 constexpr int rb_minw() {
     if (RWV == 2 && CWV == 4 && NT == 4 && MP_RB3_W) return MP_RB3_W;
     if (RWV == 1 && CWV == 8 && NT == 2 && MP_RB4_W) return MP_RB4_W;
+    if (RWV == 7 && MP_RB1_W) return MP_RB1_W;
+    if (NT >= 8) return 2;  // <= 256 registers
     return RWV * CWV > 8 || NT > 4 ? 1 : 2;
 }
 template <int RWV, int CWV, int NT, bool PERSIST>
@@ -1263,6 +1297,9 @@ hipError_t launch_conv2(mpc::ConvP p, int nchunk, int nbranch, hipStream_t s) {
     constexpr int BN = CWV * 16 * mpc::C2_NT;
     if (p.Cinp != NCB * 32) return hipErrorInvalidValue;
     p.tiles_per_chunk = (p.T + BN - 1) / BN;
+    // grid.z slices heaviest branch first (dispatched first)
+    for (int j = 0; j < 3; ++j) p.zorder[j] = j;
+    std::sort(p.zorder, p.zorder + nbranch, [&](int a, int b) { return p.ks[a] > p.ks[b]; });
     dim3 grid(p.Coutp / (RWV * 32), nchunk * p.tiles_per_chunk, nbranch);
     hipLaunchKernelGGL((mpc::conv2_kernel<RWV, CWV, NCB, DEEP>), grid, dim3(64 * RWV * CWV), 0, s, p);
     return hipGetLastError();
@@ -1307,10 +1344,10 @@ hipError_t run_rb(const mpc::RbP &p, int Cp, int nchunk, hipStream_t s) {
     // per wave everywhere but the 32-channel stage (32: 240 vs 273 us); 128 per wave took
     // 1.2-1.5x longer (one workgroup per CU), 32 per wave 1.3x on 128 / 64 channels
     switch (Cp) {
-        case 224: return launch_rb<7, 2, 4, false>(p, nchunk, s);
-        case 128: return launch_rb<4, 2>(p, nchunk, s);
-        case 64: return launch_rb<2, 4>(p, nchunk, s);
-        case 32: return launch_rb<1, 8, 2>(p, nchunk, s);
+        case 224: return launch_rb<7, MP_RB1_CWV, MP_RB1_NT, false>(p, nchunk, s);
+        case 128: return launch_rb<4, MP_RB2_CWV, MP_RB2_NT>(p, nchunk, s);
+        case 64: return launch_rb<2, MP_RB3_CWV, MP_RB3_NT>(p, nchunk, s);
+        case 32: return launch_rb<1, MP_RB4_CWV, MP_RB4_NT>(p, nchunk, s);
     }
     return hipErrorInvalidValue;
 }

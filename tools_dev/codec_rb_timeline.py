@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "magpie-tts.cpp_amd"))
 import magpie_amd as ma  # noqa: E402
 
-GX = 65536
+GX = 16384
 cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
 os.makedirs(cache, exist_ok=True)
 stages = [int(a) for a in sys.argv[1:]] or [1, 2, 3, 4]
@@ -26,10 +26,11 @@ for st in stages:
     os.environ["MAGPIE_CODEC_TS"] = f"{st},0,{dump}"
     cdc.decode_chunks(codes)
     del os.environ["MAGPIE_CODEC_TS"]
-    ts = np.fromfile(dump, dtype=np.uint64).reshape(3, GX, 16).astype(np.int64)
+    ts = np.fromfile(dump, dtype=np.uint64).reshape(3, GX, 48).astype(np.int64)
     live = ts[:, :, 0] > 0
     t_min = ts[:, :, 0][live].min()
     t_max = ts[:, :, 5][live].max()
+    waves = []
     print(f"stage {st}: {live.sum()} workgroups, launch span {(t_max - t_min) * 0.01:.1f} us")
     for br in range(3):
         r = ts[br][live[br]]
@@ -46,6 +47,15 @@ for st in stages:
             b0 = np.median(r[:, 9] - r[:, 1]) * 0.01
             s0 = np.median(r[:, 8] - r[:, 7]) * 0.01
             parts += f" || wave 0: conv_d {b0:5.2f} C {c0:4.2f} E rows {e0:4.2f} stores {s0:4.2f}"
+            # every wave's conv_d / conv_1 end (from the phase start), median per wave
+            nw = int(((r[:, 16:48:2] > 0).sum(axis=1)).max())
+            wd = [np.median(r[:, 16 + 2 * k] - r[:, 1]) * 0.01 for k in range(nw)]
+            w1 = [np.median(r[:, 17 + 2 * k] - r[:, 3]) * 0.01 for k in range(nw)]
+            waves.append((br, wd, w1))
         print(f"  branch {br} ({len(r)} wgs): per workgroup p50 {parts} | total {np.median(tot):5.2f} "
               f"(max {tot.max():5.2f}); starts spread {st0.max():5.1f} us")
+    for br, wd, w1 in waves:
+        print(f"  branch {br} per wave conv_d end: " + " ".join(f"{x:5.2f}" for x in wd))
+        print(f"  branch {br} per wave conv_1 end: " + " ".join(f"{x:5.2f}" for x in w1))
+os.remove(dump)  # 3 x GX x 48 stamps: not for the trip back
 cdc.close()

@@ -16,7 +16,7 @@
 #   codec[=LIB[:K=V]]    codec wall / device time per call (tools_dev/codec_latency.py); LIB "-" = default
 #   cprof[=LIB]          rocprofv3 kernel trace of 3 codec decodes, per-dispatch table of the last
 #   cpmc[=LIB]           the codec's SQ / TCC / TCP counter passes (tools_dev/codec_pmc.sh)
-#   ctl                  the residual-block kernel's phase stamps per stage (tools_dev/codec_rb_timeline.py)
+#   ctl[=LIB]            the residual-block kernel's phase stamps per stage (tools_dev/codec_rb_timeline.py)
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out
@@ -91,8 +91,10 @@ for STEP in "$@"; do
       cp gpurun_out/cpmc/report.txt "$OUT/${TAG}_cpmc${arg:+_$arg}.txt"
       echo "codec pmc ok" ;;
     ctl)
-      timeout -k 10 200 python -u tools_dev/codec_rb_timeline.py > "$OUT/${TAG}_ctl.txt" 2>&1
-      cat "$OUT/${TAG}_ctl.txt" ;;
+      env=()
+      [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
+      env "${env[@]}" timeout -k 10 200 python -u tools_dev/codec_rb_timeline.py > "$OUT/${TAG}_ctl${arg:+_$arg}.txt" 2>&1
+      cat "$OUT/${TAG}_ctl${arg:+_$arg}.txt" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

@@ -920,6 +920,11 @@ __global__ __launch_bounds__(64 * RWV * CWV, (rb_minw<RWV, CWV, NT>())) void rb_
 // Grouped ConvTranspose1d (nano-codec.cpp:481-565), HalfSnake on its input,
 // optional 3-branch mean before it: out[t][g] = b[g] + sum_{c in {2g,2g+1}}
 // sum_{tau: 0 <= t - tau*s < 2s} x[tau][c] * w[c][t - tau*s]; kept length T*s.
+// input steps per thread of the later stages' ConvTranspose (each thread re-reads one step
+// of halo: R = 8 reads 1.125x the input; 4: 1.25x, 1.45-1.47 vs 1.44-1.45 ms per decode)
+#ifndef MP_CT_R
+#define MP_CT_R 8
+#endif
 struct ConvTP {
     const float *x, *xa, *xb;  // input [chunk][Tin][Cinp] (xa/xb: AVG3)
     const float *alpha;
@@ -1095,21 +1100,30 @@ struct PostP {
 // causal halo), rounded to f16 like ggml's im2col, then each thread dots its 3
 // taps x 27 channels against the f16-rounded weights.
 __global__ __launch_bounds__(256) void post_conv_kernel(PostP p) {
-    __shared__ float hs[258][28];
+    __shared__ __attribute__((aligned(16))) float hs[258][28];
     __shared__ float wh[27 * 3];
     const int tiles = (p.T + 255) / 256;
     const int chunk = blockIdx.x / tiles, t0 = (blockIdx.x % tiles) * 256;
     const size_t cbase = (size_t)chunk * p.T;
     if (threadIdx.x < 81) wh[threadIdx.x] = (float)(_Float16)p.w[threadIdx.x];
-    for (int e = threadIdx.x; e < 258 * 27; e += 256) {
-        const int r = e / 27, i = e % 27, t = t0 - 2 + r;
-        float v = 0.f;
+    // channel quads: item e = (row e / 7, channels 4 (e % 7) ..): a float4 per branch, the
+    // rows' 28 stored channels (27 real + 1 zero pad), 4 items per thread in flight
+    constexpr int NQ = 7, NI = 258 * NQ;
+#pragma unroll 4
+    for (int e = threadIdx.x; e < NI; e += 256) {
+        const int r = e / NQ, i0 = 4 * (e % NQ), t = t0 - 2 + r;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (t >= 0 && t < p.T) {
-            const size_t o = (cbase + t) * 32 + i;
-            v = ((p.x[o] + p.xa[o]) + p.xb[o]) * (1.0f / 3.0f);
-            v = (float)(_Float16)half_snake(v, i, 13, 27, p.alpha);
+            const size_t o = (cbase + t) * 32 + i0;
+            const float4 a = *(const float4 *)(p.x + o), b = *(const float4 *)(p.xa + o), d = *(const float4 *)(p.xb + o);
+            const float m[4] = {((a.x + b.x) + d.x) * (1.0f / 3.0f), ((a.y + b.y) + d.y) * (1.0f / 3.0f),
+                                ((a.z + b.z) + d.z) * (1.0f / 3.0f), ((a.w + b.w) + d.w) * (1.0f / 3.0f)};
+            float hv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) hv[u] = i0 + u < 27 ? (float)(_Float16)half_snake(m[u], i0 + u, 13, 27, p.alpha) : 0.f;
+            v = make_float4(hv[0], hv[1], hv[2], hv[3]);
         }
-        hs[r][i] = v;
+        *(float4 *)&hs[r][i0] = v;
     }
     __syncthreads();
     const int t = t0 + threadIdx.x;
@@ -1401,7 +1415,7 @@ int codec_run(mp_codec *c, int nchunk, int F) {
         for (int j = 0; j < 3; ++j) { tp.act[j] = c->a16[j]; tp.act_alpha[j] = c->rb_alpha[i][j][0][0]; }
         tp.Tin = T; tp.s = RATE[i]; tp.nchunk = nchunk;
         // R input steps per thread: 1 on the short early stages (threads), 4 later (re-reads)
-        const int R = i == 0 ? 1 : i == 1 ? 2 : 4;
+        const int R = i == 0 ? 1 : i == 1 ? 2 : MP_CT_R;
         const dim3 g2((nchunk * ((T + R - 1) / R) * (Cp / 2) + 255) / 256);
         const bool fused = rb_fused(Cp);
         switch (i) {
@@ -1411,16 +1425,16 @@ int codec_run(mp_codec *c, int nchunk, int F) {
                 else hipLaunchKernelGGL((conv_transpose2_kernel<448, 224, 8, true, 2>), g2, dim3(256), 0, s, tp);
                 break;
             case 2:
-                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4, false>), g2, dim3(256), 0, s, tp);
-                else hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, 4>), g2, dim3(256), 0, s, tp);
+                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, MP_CT_R, false>), g2, dim3(256), 0, s, tp);
+                else hipLaunchKernelGGL((conv_transpose2_kernel<224, 128, 4, true, MP_CT_R>), g2, dim3(256), 0, s, tp);
                 break;
             case 3:
-                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, 4, false>), g2, dim3(256), 0, s, tp);
-                else hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, 4>), g2, dim3(256), 0, s, tp);
+                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, MP_CT_R, false>), g2, dim3(256), 0, s, tp);
+                else hipLaunchKernelGGL((conv_transpose2_kernel<128, 64, 2, true, MP_CT_R>), g2, dim3(256), 0, s, tp);
                 break;
             default:
-                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, 4, false>), g2, dim3(256), 0, s, tp);
-                else hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, 4>), g2, dim3(256), 0, s, tp);
+                if (fused) hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, MP_CT_R, false>), g2, dim3(256), 0, s, tp);
+                else hipLaunchKernelGGL((conv_transpose2_kernel<64, 32, 2, true, MP_CT_R>), g2, dim3(256), 0, s, tp);
                 break;
         }
         CHK(hipGetLastError());

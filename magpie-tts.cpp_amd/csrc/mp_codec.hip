@@ -152,6 +152,16 @@ __device__ __forceinline__ int hs_wave_kind(int c0, int c1, int n_snake, int cin
     return 2;
 }
 
+// Residual convs (x' = x + conv(h) + b): the accumulators start at the residual x, the
+// bias is added after the MFMAs -- (x + sum) + b in every kernel (conv_mfma_kernel,
+// conv2_kernel, rb_kernel, which loads x as phase C frees the registers, under conv_1's
+// MFMAs), the same bits across them; 0: (sum + b) + x, x loaded in the epilogue.
+// Measured (gpurun_out/r05zs_*): 1.49-1.51 -> 1.42-1.43 ms per 8 x 32-frame decode.
+#ifndef MP_RESINIT
+#define MP_RESINIT 1
+#endif
+constexpr bool RESINIT = MP_RESINIT != 0;
+
 // fsq_dequantize_cpu (nano-codec.cpp:721-752): channel c = 4*cb + d
 __device__ __forceinline__ float fsq(int code, int d) {
     const int base = d == 0 ? 1 : d == 1 ? 8 : d == 2 ? 56 : 336;
@@ -192,6 +202,17 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
     floatx4 acc[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (RESINIT && p.resid[br]) {  // the accumulators start at the residual (MP_RESINIT)
+        const int o = m0 + rw * 16 + 4 * kg;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int t = t0 + cw * WCOLS + j * 16 + l16;
+            if (t < p.T) {
+                const float4 r = *(const float4 *)(p.resid[br] + (size_t)chunk * p.T * p.Coutp + (size_t)t * p.Coutp + o);
+                acc[j] = floatx4{r.x, r.y, r.z, r.w};
+            }
+        }
+    }
 
     const int rows = BN + pad;
     if constexpr (!PIPE) {
@@ -297,7 +318,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvP p) {
         if (t >= p.T) continue;
         float4 v = make_float4(acc[j][0] + bb.x, acc[j][1] + bb.y, acc[j][2] + bb.z, acc[j][3] + bb.w);
         const size_t off = chunk_out + (size_t)t * p.Coutp + o;
-        if (p.resid[br]) {
+        if (!RESINIT && p.resid[br]) {
             const float4 r = *(const float4 *)(p.resid[br] + off);
             v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;  // input + h (568-599)
         }
@@ -354,6 +375,19 @@ __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
     for (int a = 0; a < C2_WR; ++a)
 #pragma unroll
         for (int j = 0; j < C2_NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (RESINIT && p.resid[br]) {  // the accumulators start at the residual (MP_RESINIT)
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+            for (int j = 0; j < C2_NT; ++j) {
+                const int t = t0 + cw * (16 * C2_NT) + j * 16 + l16;
+                if (t < p.T) {
+                    const float4 r = *(const float4 *)(p.resid[br] + (size_t)chunk * p.T * p.Coutp + (size_t)t * p.Coutp +
+                                                       m0 + rw * 32 + a * 16 + 4 * kg);
+                    acc[a][j] = floatx4{r.x, r.y, r.z, r.w};
+                }
+            }
+    }
 
     // A stream: step s = cb * KS + k (channel block, tap) is the 1 KiB fragment at
     // wrow + s * 512. The channel-block loop is unrolled (NCB is a template
@@ -450,7 +484,7 @@ __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
     static_assert(BN % RSTEP == 0, "whole steps per thread");
     const int tl0 = tid / (BM / 4);
     float4 rres[IT];
-    if (p.resid[br]) {
+    if (!RESINIT && p.resid[br]) {
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
             const int t = t0 + tl0 + i * RSTEP;
@@ -466,7 +500,7 @@ __device__ __forceinline__ void conv2_body(const ConvP &p, char *xs) {
         const float4 a4 = *(const float4 *)(ct + tl * CST + cl);
         float4 v = make_float4(a4.x + bb.x, a4.y + bb.y, a4.z + bb.z, a4.w + bb.w);
         const size_t off = chunk_out + (size_t)t * p.Coutp + o;
-        if (p.resid[br]) {
+        if (!RESINIT && p.resid[br]) {
             const float4 r = rres[i];
             v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;  // input + h (568-599)
         }
@@ -558,6 +592,7 @@ constexpr bool RB_PRM = MP_RB_PRM != 0;
 #define MP_RB_RXPRE 0
 #endif
 constexpr bool RB_RXPRE = MP_RB_RXPRE != 0;
+constexpr bool RB_RESINIT = RESINIT;
 constexpr int RB_MAXHALO = 50;  // (11 - 1) * 5
 
 template <int RWV, int CWV, int NT>
@@ -614,7 +649,6 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
                                         float4 (&v)[RbGeo<RWV, CWV, NT>::NU][2], bool first) {
     using G = RbGeo<RWV, CWV, NT>;
     constexpr int NCB = G::NCB, CPD = G::CPD, NCD = G::NCD, BN = G::BN, XR = G::XR, RSTEP = G::RSTEP, NU = G::NU;
-    constexpr int PPR = G::PPR;
     constexpr int NS = NCB * KS;  // A-stream steps (channel block, tap)
     // diagnostics: thread 0 stamps the phases of its first item (A x rows staged, B conv_d,
     // C the intermediate staged, D conv_1, E stored; wave 0's own: 9 conv_d done, 6 its part
@@ -687,11 +721,13 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     floatx4 acc[C2_WR][NT];
     half8 ring[R][C2_WR];
     const int colb = cw * 16 * NT + l16;
-    auto conv = [&](const _Float16 *wf, int rowoff, int dk, int nt) {
+    auto conv = [&](const _Float16 *wf, int rowoff, int dk, int nt, bool init) {
+        if (init) {
 #pragma unroll
-        for (int a = 0; a < C2_WR; ++a)
+            for (int a = 0; a < C2_WR; ++a)
 #pragma unroll
-            for (int j = 0; j < NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
         const _Float16 *wrow0 = wf + (size_t)(rw * 2) * NS * 512 + lane * 8, *wrow1 = wrow0 + (size_t)NS * 512;
 #pragma unroll
         for (int q = 0; q < R; ++q)
@@ -733,13 +769,14 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
         }
     };
     // B: conv_d, column c = time t0 - 16 + c, x row c + k d
-    conv(p.Wd[br], 0, d, NT);
+    conv(p.Wd[br], 0, d, NT, true);
     // each lane's 8 channels: rw * 32 + a * 16 + 4 kg + r
     const int chl = rw * 32 + 4 * kg;
     stamp(9);
     if (tsw && lane == 0) tsw[16 + 2 * w] = __builtin_amdgcn_s_memrealtime();  // every wave's conv_d end
     __syncthreads();  // every wave is done reading x rows
     stamp(2);
+    const int nt = cw == CWV - 1 ? NT - 1 : NT;  // conv_1: BN = 16 NT CWV - 16 outputs
     // ---- C: h = f16(HS_sk(conv_d + b)) into LDS rows 0 .. NCD-1 (row c = time t0 - 16 + c)
     {
         typedef _Float16 half4 __attribute__((ext_vector_type(4)));
@@ -769,6 +806,12 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
                     for (int r = 0; r < 4; ++r) h[r] = (_Float16)hs(acc[a][j][r] + bv[r], r);
                     if (t < 0) h = half4{0, 0, 0, 0};
                     *(half4 *)(xs + rw * XR * RB_ROWB + c * RB_ROWB + (a * 16 + 4 * kg) * 2) = h;
+                    if constexpr (RB_RESINIT) {  // conv_1's accumulator starts at its residual rows
+                        const int to = t0 + cw * 16 * NT + j * 16 + l16;
+                        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (j < nt && to < p.T) r = *(const float4 *)(p.x[br] + cbase + (size_t)to * CPD + chl + a * 16);
+                        acc[a][j] = floatx4{r.x, r.y, r.z, r.w};
+                    }
                 }
             };
             const int kind = hs_wave_kind(ch, ch + 3, p.nsnake, p.creal);
@@ -781,7 +824,6 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
     __syncthreads();
     stamp(3);
     // ---- D: conv_1, output column o = time t0 + o, h row o + 16 - (KS - 1) + k
-    const int nt = cw == CWV - 1 ? NT - 1 : NT;  // BN = 16 NT CWV - 16 outputs
     // ---- E's operands: every residual element and bias before the stores (a load after a
     // store to the other buffer may alias it, so per fragment the loop had waited one L2
     // round trip each); with RB_RXPRE before conv_1, their latency under its MFMAs
@@ -795,7 +837,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
             for (int j = 0; j < NT; ++j) {
                 const int t = t0 + cw * 16 * NT + j * 16 + l16;
                 rx[a][j] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (j < nt && t < p.T) rx[a][j] = *(const float4 *)(p.x[br] + cbase + (size_t)t * CPD + ch);
+                if (!RB_RESINIT && j < nt && t < p.T) rx[a][j] = *(const float4 *)(p.x[br] + cbase + (size_t)t * CPD + ch);
             }
         }
     };
@@ -803,7 +845,7 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
         load_e();
         __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to their use
     }
-    conv(p.W1[br], 16 - (KS - 1), 1, nt);
+    conv(p.W1[br], 16 - (KS - 1), 1, nt, !RB_RESINIT);
     stamp(4);
     if (tsw && lane == 0) tsw[17 + 2 * w] = __builtin_amdgcn_s_memrealtime();  // every wave's conv_1 end
     // ---- E: + bias + x -> x'
@@ -821,9 +863,13 @@ __device__ __forceinline__ void rb_body(const RbP &p, char *xs, int br, int tile
             const int t = t0 + cw * 16 * NT + j * 16 + l16;
             if (j >= nt || t >= p.T) continue;
             const size_t off = cbase + (size_t)t * CPD + ch;
-            const float4 r = rx[a][j];
             const floatx4 y = acc[a][j];
             const float4 vo = make_float4(y[0] + bb.x, y[1] + bb.y, y[2] + bb.z, y[3] + bb.w);
+            if constexpr (RB_RESINIT) {
+                *(float4 *)(p.out[br] + off) = vo;  // (input + conv_1) + bias
+                continue;
+            }
+            const float4 r = rx[a][j];
             *(float4 *)(p.out[br] + off) = make_float4(r.x + vo.x, r.y + vo.y, r.z + vo.z, r.w + vo.w);  // input + h
         }
     }

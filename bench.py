@@ -41,6 +41,7 @@ import magpie_amd as ma  # noqa: E402
 # so every N runs the kernels on /opt/rocm's runtime (tests/test_dist_cpu.py checks
 # /proc/self/maps after this import sequence).
 ma.load_library()
+LIB_SHA16 = ma.lib_sha16()  # the committed PMC profiles name the build they counted
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
@@ -159,7 +160,60 @@ def measure_extra(model_path: str, codec_path, args) -> dict:
                                     "rtf": round(total / 22050.0 / wall, 1), "chunk_frames": 4}
         cdc.close()
         dev.close()
+    if codec_path:
+        out["configs2_e2e"] = measure_configs2_e2e(model_path, codec_path, args)
     return out
+
+
+def measure_configs2_e2e(model_path: str, codec_path: str, args) -> dict:
+    """configs[2] end to end: bf16, 16 utterances, codes -> waveform on the device. The
+    decode runs on the model's stream; as every slot completes a 32-frame chunk (the CLI's
+    stateless chunks, magpie-tts.cpp:181-206) the codec decodes it on its own stream while
+    the decode continues (mp_hip_decode_stream, frames_per_chunk = 32). Reported against
+    the decode alone and against the serial form (decode, then the codec over all chunks)
+    measured in the same run on the same prompts."""
+    B, F = 16, args.frames
+    dev = ma.Device(model_path, weights="bf16")
+    cdc = ma.Codec(codec_path)
+    toks = [ma.synthetic_tokens(args.tokens, seed=1000 + b) for b in range(B)]
+    spk = [b % 5 for b in range(B)]
+    r = dev.synthesize(toks, speakers=spk, max_dec_steps=F, ignore_eos=True)
+    dec_ms = []
+    for _ in range(3):
+        dec_ms.append(dev.decode(B, F).decode_ms)
+    chunks = np.stack([c[s0:s0 + CODEC_CHUNK].T for c in r.codes for s0 in range(0, len(c), CODEC_CHUNK)
+                       if len(c[s0:s0 + CODEC_CHUNK]) == CODEC_CHUNK]).astype(np.int32)
+    cdc.decode_chunks(chunks)  # warm-up
+    cod_ms = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        cdc.decode_chunks(chunks)
+        cod_ms.append((time.perf_counter() - t0) * 1e3)
+    n = [0]
+
+    def on_audio(u, a):
+        n[0] += len(a)
+        return True
+    dev.synthesize_stream(cdc, toks, on_audio, speakers=spk, max_dec_steps=F, frames_per_chunk=CODEC_CHUNK,
+                          ignore_eos=True)  # warm-up (and the preamble, outside the timing below)
+    walls = []
+    for _ in range(3):
+        n[0] = 0
+        t0 = time.perf_counter()
+        codes, total, tm = dev.decode_stream_only(cdc, on_audio, B, F, CODEC_CHUNK)
+        walls.append(time.perf_counter() - t0)
+    wall = float(np.median(walls))
+    frames = B * F
+    dec = float(np.median(dec_ms)) * 1e-3
+    serial = dec + float(np.median(cod_ms)) * 1e-3
+    cdc.close()
+    dev.close()
+    return {"workload": f"Magpie-357M bf16, batch={B}, {F} frames/utterance, T={args.tokens}, codes -> waveform "
+                        f"({CODEC_CHUNK}-frame codec chunks overlapped with the decode on a second stream)",
+            "frames": frames, "samples": int(n[0]), "wall_s": round(wall, 4),
+            "fps": round(frames / wall, 1), "rtf": round(n[0] / 22050.0 / wall, 1),
+            "decode_only_fps": round(frames / dec, 1), "serial_fps": round(frames / serial, 1),
+            "e2e_over_decode_only": round(dec / wall, 4)}
 
 
 def spawn_ranks(n: int) -> int:
@@ -361,14 +415,16 @@ def main() -> None:
                  "frac": round(tfs / MFMA_F16_PEAK_TFS, 4), "audio_peak": round(float(np.abs(audio).max()), 4)}
         pmc_codec = os.path.join(REPO, "profiles", PMC_CODEC)
         if os.path.exists(pmc_codec):  # counters of the same codec shape (tools_dev/pmc_report.py)
-            sm = json.load(open(pmc_codec))["summary"]
+            pj = json.load(open(pmc_codec))
+            sm = pj["summary"]
+            stale = pj.get("lib_sha16") != LIB_SHA16  # counted on another build: not this run's kernels
             # MFMA utilisation: the MFMA FLOPs the codec issues per decode of this shape
             # (SQ_INSTS_VALU_MFMA_MOPS_F16 x 512, padding included) over the live decode
             # time above, against the dense f16 peak; traffic: FETCH_SIZE + WRITE_SIZE per
             # decode over the same live time (the PMC runs themselves are slowed by the
             # counters, so their own durations are not used)
-            issued = sm.get("per_decode_mfma_flops")
-            nbytes = sm.get("per_decode_bytes")
+            issued = None if stale else sm.get("per_decode_mfma_flops")
+            nbytes = None if stale else sm.get("per_decode_bytes")
             pmc_chunks = sm.get("chunks", 8)
             scale = (cframes / CODEC_CHUNK) / pmc_chunks
             codec["pmc"] = {
@@ -378,7 +434,8 @@ def main() -> None:
                 "hbm_tbs": round(nbytes * scale / (codec_ms * 1e-3) / 1e12, 3) if nbytes else None,
                 "bytes_per_decode": nbytes,
                 "source": f"profiles/{PMC_CODEC}: MFMA op counts and FETCH_SIZE/WRITE_SIZE passes of the same "
-                          f"{pmc_chunks} x {CODEC_CHUNK}-frame decode, over this run's live decode time"}
+                          f"{pmc_chunks} x {CODEC_CHUNK}-frame decode, over this run's live decode time",
+                "pmc_lib_sha16": pj.get("lib_sha16"), "stale": stale}
 
     # ---- roofline of the dominant kernel, timed in situ: whole decode iterations
     # launched eagerly on the decode stream, each kernel through hipExtLaunchKernel
@@ -432,7 +489,10 @@ def main() -> None:
         # correction for the 16 B/lane kernels)
         pmc_path = os.path.join(REPO, "profiles", PMC_TRAFFIC)
         if args.weights == "f32" and B == 1 and os.path.exists(pmc_path):
-            pmc_ops = json.load(open(pmc_path))["ops"]
+            pj = json.load(open(pmc_path))
+            pmc_ops = pj["ops"] if pj.get("lib_sha16") == LIB_SHA16 else {}  # another build's counters: unused
+            roofline["traffic_lib_sha16"] = pj.get("lib_sha16")
+            roofline["lib_sha16"] = LIB_SHA16
             pmc = pmc_ops.get(name)
             if pmc:
                 roofline["traffic"] = pmc["traffic_bytes"]
@@ -452,8 +512,12 @@ def main() -> None:
                "sample": f"1 utterance x {res['frames']} frames (T={args.tokens}), decode loop only "
                          f"(preamble {res['preamble_s']:.2f}s excluded), oracle f32-accumulate mode",
                "cpu_model": cpu_model_name()}
-        # also at every core this process may use (the box's CPU share)
-        nall = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+        # also at every core this process may use. The GPU box leases 16 CPUs per
+        # GPU (its OMP_NUM_THREADS) out of a machine whose affinity mask shows all of them; the
+        # operators' rule caps a one-GPU job's worker pool at that share, so it is a named
+        # cap here, not the machine's core count.
+        LEASE_CAP = 16
+        nall = max(1, min(LEASE_CAP, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
         if nall != args.cpu_threads:
             ra = orc.time_decode_fps(model_path, toks[0], args.frames, threads=nall, acc64=False)
             try:
@@ -461,6 +525,7 @@ def main() -> None:
             except (AttributeError, OSError):
                 visible = os.cpu_count() or 1
             cpu["all_cores"] = {"value": round(ra["frames"] / ra["decode_s"], 2), "cores": nall,
+                                "cores_cap": LEASE_CAP,
                                 "note": f"the lease's CPU share: OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', '-')}, "
                                         f"{visible} CPUs in this process's affinity mask, "
                                         f"{os.cpu_count()} on the machine"}

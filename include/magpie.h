@@ -21,9 +21,10 @@
 
 #include "magpie_hip.h"
 
-// magpie.h:24-29 — kept for source compatibility; every value selects the single
-// HIP device path (CPU/Metal requests are honoured as "the GPU" — there is no
-// CPU fallback by design).
+// magpie.h:24-29 — kept for source compatibility. CUDA and AUTO select the single
+// HIP device path; CPU and Metal requests are refused (magpie_model_load returns
+// false with a message on stderr, magpie_init_with_backend nullptr): there is no
+// CPU fallback by design.
 enum magpie_backend_type {
     MAGPIE_BACKEND_CPU = 0,
     MAGPIE_BACKEND_CUDA = 1,
@@ -168,10 +169,11 @@ magpie_context *magpie_init(const char *model_path);
 magpie_context *magpie_init_with_backend(const char *model_path, magpie_backend_type backend);
 void magpie_free(magpie_context *ctx);
 const char *magpie_get_backend_name(magpie_context *ctx);
-// magpie.h:332: load a GGUF's weights into `model` (its device state is created on
-// first use, on the device MAGPIE_DEVICE names; a model already loaded is replaced).
-// The weight mode is picked from the file as magpie_init does. false + stderr on failure;
-// a device state this call created is released again on failure. backend: AUTO / CUDA
+// magpie.h:332: load a GGUF's weights into `model` (on the device MAGPIE_DEVICE names).
+// The file is loaded into a fresh device state that replaces model.dev only on success:
+// a model already loaded is replaced by a successful load and left intact, weights and
+// hparams, by a failed one. The weight mode is picked from the file as magpie_init does.
+// false + stderr on failure. backend: AUTO / CUDA
 // select the HIP device; MAGPIE_BACKEND_CPU and METAL are refused (false + stderr: this
 // build has one backend). Ownership: model.dev belongs to the caller until handed to a
 // context; release a standalone model with magpie_model_free (magpie_free releases a

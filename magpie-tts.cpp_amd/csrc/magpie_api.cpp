@@ -23,16 +23,13 @@ bool magpie_model_load(const std::string &path, magpie_model &model, magpie_back
                 backend == MAGPIE_BACKEND_CPU ? "CPU" : "Metal");
         return false;
     }
-    const bool created = model.dev == nullptr;
-    if (created && mp_hip_init(env_device(), &model.dev) != MP_OK) {
+    // Always load into a fresh device state and swap it in only on success: a failed
+    // reload leaves a model that was already loaded intact (weights and hparams).
+    mp_dev *dev = nullptr;
+    if (mp_hip_init(env_device(), &dev) != MP_OK) {
         fprintf(stderr, "magpie: no usable HIP device\n");
-        model.dev = nullptr;
         return false;
     }
-    auto fail_free = [&]() {
-        if (created) { mp_hip_free(model.dev); model.dev = nullptr; }
-        return false;
-    };
     // Weight mode (magpie_hip.h): a GGUF with Q8_0 / Q4_0 tensors runs them as ggml does
     // (MP_WEIGHTS_Q8), an F16 file with ggml's F16 semantics (MP_WEIGHTS_F16), any other
     // file as stored; MAGPIE_WEIGHTS=f32|bf16|q8|f16 overrides.
@@ -46,15 +43,18 @@ bool magpie_model_load(const std::string &path, magpie_model &model, magpie_back
                : !strcmp(wm, "f16") ? MP_WEIGHTS_F16
                                     : MP_WEIGHTS_AS_STORED;
     }
-    int rc = mp_hip_load_model_ex(model.dev, path.c_str(), mode);
+    int rc = mp_hip_load_model_ex(dev, path.c_str(), mode);
     if (rc == MP_ERR_UNSUPPORTED && !forced)  // no block-quantised tensors: an F16 file?
-        rc = mp_hip_load_model_ex(model.dev, path.c_str(), MP_WEIGHTS_F16);
+        rc = mp_hip_load_model_ex(dev, path.c_str(), MP_WEIGHTS_F16);
     if (rc == MP_ERR_UNSUPPORTED && !forced)  // neither: as stored
-        rc = mp_hip_load_model_ex(model.dev, path.c_str(), MP_WEIGHTS_AS_STORED);
+        rc = mp_hip_load_model_ex(dev, path.c_str(), MP_WEIGHTS_AS_STORED);
     if (rc != MP_OK) {
-        fprintf(stderr, "magpie: failed to load '%s': %s\n", path.c_str(), mp_hip_error(model.dev));
-        return fail_free();
+        fprintf(stderr, "magpie: failed to load '%s': %s\n", path.c_str(), mp_hip_error(dev));
+        mp_hip_free(dev);
+        return false;
     }
+    if (model.dev) mp_hip_free(model.dev);  // the replaced model
+    model.dev = dev;
     int dec = 12, enc = 6;
     mp_hip_model_info(model.dev, &dec, &enc, nullptr);
     // the text front end rides in the same GGUF (magpie.cpp:853-858); optional

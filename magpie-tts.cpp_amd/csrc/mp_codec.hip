@@ -1379,14 +1379,21 @@ hipError_t launch_rb(mpc::RbP p, int nchunk, hipStream_t s) {
     // times the CU count), each taking items from the counter; else one per item
     int gx = total;
     if (PERSIST) {
-        static int per_cu = -1, ncu = 0;
-        if (per_cu < 0) {
-            int dev = 0;
-            hipGetDevice(&dev);
+        // cached per device (a process may drive devices of different CU counts)
+        constexpr int MAXDEV = 64;
+        static int per_cu_d[MAXDEV], ncu_d[MAXDEV];
+        int dev = 0;
+        hipGetDevice(&dev);
+        int per_cu = 1, ncu = 1;
+        if (dev >= 0 && dev < MAXDEV && per_cu_d[dev] > 0) {
+            per_cu = per_cu_d[dev];
+            ncu = ncu_d[dev];
+        } else {
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mpc::rb_kernel<RWV, CWV, NT, PERSIST>, 64 * RWV * CWV, 0) !=
                     hipSuccess || per_cu < 1)
                 per_cu = 1;
+            if (dev >= 0 && dev < MAXDEV) { ncu_d[dev] = ncu; per_cu_d[dev] = per_cu; }
         }
         gx = std::min(total, std::max(1, per_cu * ncu));
     }
@@ -1569,12 +1576,21 @@ int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, 
     // diagnostics: MAGPIE_CODEC_TS=stage,block,file -> the phase stamps of that stage's
     // rb_kernel launch for residual block `block` (tools_dev/codec_rb_timeline.py)
     constexpr size_t TS_N = (size_t)3 * mpc::RB_TS_GX * mpc::RB_TS_N;
-    if (const char *e = getenv("MAGPIE_CODEC_TS")) {
+    // (read per call: parsed into locals and committed only when all 3 fields parse;
+    // absent or malformed, the stamps are off again)
+    {
+        const char *e = getenv("MAGPIE_CODEC_TS");
         char file[512] = {0};
-        if (sscanf(e, "%d,%d,%511s", &c->ts_stage, &c->ts_block, file) == 3) {
+        int st = -1, bl = -1;
+        if (e && sscanf(e, "%d,%d,%511s", &st, &bl, file) == 3) {
+            c->ts_stage = st;
+            c->ts_block = bl;
             c->ts_file = file;
             if (!c->ts_dev) CHK(hipMalloc((void **)&c->ts_dev, TS_N * 8));
             CHK(hipMemsetAsync(c->ts_dev, 0, TS_N * 8, c->stream));
+        } else {
+            c->ts_stage = c->ts_block = -1;
+            c->ts_file.clear();
         }
     }
     CHK(hipEventRecord(c->ev0, c->stream));

@@ -200,6 +200,52 @@ __global__ __launch_bounds__(MP_BLOCK) void gemm_q8_kernel_dec(GemvP p) {
             }
         }
     }
+    if (p.q8dump) {
+        // diagnostics (MAGPIE_Q8DUMP): the operands this launch quantised and the integer
+        // block dots its MFMAs form from them (the same fragments and instructions as the
+        // loop above, without the scales), for an exact comparison with ggml's
+        // quantize_row_q8_0 / vec_dot_q8_0_q8_0 fed the same f32 rows (tests/test_q8_exact_gpu.py)
+        char *db = (char *)p.q8dump;
+        if (rt == 0) {
+            float *da = (float *)db;
+            signed char *dq = (signed char *)(db + (size_t)NB * K * 4);
+            float *dd = (float *)(db + (size_t)NB * K * 5);
+            for (int e = tid; e < NB * K; e += MP_BLOCK) {
+                da[e] = act[e];
+                dq[e] = actq[(e / K) * QS + e % K];
+            }
+            for (int e = tid; e < NB * NBLK; e += MP_BLOCK) dd[e] = actd[e];
+        }
+        int *ds = (int *)(db + (size_t)NB * K * 5 + (size_t)NB * NBLK * 4);
+#pragma unroll
+        for (int i = 0; i < KW; ++i) {
+            const int kp = w * KW + i;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int kc = 2 * kp + h;
+                long av;
+                if constexpr (Q4) {
+                    const unsigned wn = h ? a[i].y : a[i].x;
+                    av = (long)(((unsigned long)((wn >> 4) & 0x0F0F0F0Fu) << 32) | (wn & 0x0F0F0F0Fu));
+                } else {
+                    av = h ? (long)(((unsigned long)a[i].w << 32) | a[i].z) : (long)(((unsigned long)a[i].y << 32) | a[i].x);
+                }
+                const long bv = *(const long *)(bq + kc * 32);
+                const intx4 zero = {0, 0, 0, 0};
+                intx4 sv = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv, zero, 0, 0, 0);
+                if constexpr (Q4) {
+                    const int corr = 8 * bs[kc];
+                    sv[0] -= corr; sv[1] -= corr; sv[2] -= corr; sv[3] -= corr;
+                }
+                const int col = lane & 15;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = rt * 16 + 4 * (lane >> 4) + r;
+                    if (col < NB && n < p.N) ds[((size_t)n * NBLK + kc) * NB + col] = sv[r];
+                }
+            }
+        }
+    }
     part[w][lane] = acc;
     lds_sync();
     // thread t -> (row t/16, column t%16); D[row][col] sits in lane (row/4)*16 + col, register row%4

@@ -328,6 +328,10 @@ struct GemvP {
     const int *iter;
     int *hx_err;
     int nrow_blocks;     // set by the launcher: workgroups of the O-projection
+    // diagnostics (MAGPIE_Q8DUMP, gemm_q8_kernel_dec only; nullable): this launch's f32
+    // activation rows [NB][K], their Q8_0 blocks (int8 [NB][K], fp16 d as f32 [NB][K/32])
+    // and every integer block dot [N][K/32][NB] (int32), as the kernel's operands give them
+    void *q8dump;
 };
 
 // Q8_0 weight mode: the LT step of codebook cb as LTQ_P workgroups per slot

@@ -325,6 +325,17 @@ struct mp_dev {
     bool batch_ready = false;
     mp_timing timing{};
     int *h_ndone = nullptr;  // pinned
+    // mp_hip_encode_text's private workspace: grows on demand, freed by mp_hip_free (a
+    // per-call hipFree would synchronise the whole device, stalling other streams' work)
+    char *enc_ws = nullptr;
+    size_t enc_ws_bytes = 0;
+    // diagnostics (MAGPIE_Q8DUMP=1 at mp_hip_begin_batch, Q8_0 weights): one dump slot per
+    // int8-MFMA decode GEMM launch of the iteration (GemvP::q8dump), records in q8dump_index
+    char *q8dump = nullptr;
+    size_t q8dump_slot = 0;
+    int q8dump_cap = 0, q8dump_n = 0;
+    bool q8dump_live = false;  // set while enqueue_iteration runs (not for mp_hip_lt_sample)
+    std::vector<int> q8dump_index;
 };
 
 namespace {
@@ -364,6 +375,23 @@ void free_batch(mp_dev *dev) {
     dev->B = dev->NB = dev->Tmax = dev->max_steps = 0;
     dev->xa_direct = false;
     dev->kp = dev->vp = nullptr;
+    dev->q8dump = nullptr;  // (one of allocs)
+    dev->q8dump_cap = dev->q8dump_n = 0;
+    dev->q8dump_index.clear();
+}
+
+// MAGPIE_Q8DUMP: give a Q8_0 decode GEMM launch its dump slot and index record
+// [N, K, NB, layer, cb, byte offset, name (40 bytes)] (16 ints)
+constexpr int Q8DUMP_REC = 16;
+void q8dump_assign(mp_dev *dev, const char *name, mp::GemvP &g) {
+    g.q8dump = nullptr;
+    if (!dev->q8dump || !dev->q8dump_live || !g.Wq || dev->q8dump_n >= dev->q8dump_cap) return;
+    const int n = dev->q8dump_n++;
+    g.q8dump = dev->q8dump + (size_t)n * dev->q8dump_slot;
+    const int K = strncmp(name, "lt_in", 5) == 0 ? 768 : (strncmp(name, "lt_", 3) == 0 ? 256 : 768);
+    int rec[Q8DUMP_REC] = {g.N, K, dev->NB, g.layer, g.cb, (int)((size_t)n * dev->q8dump_slot)};
+    strncpy((char *)&rec[6], name, 39);
+    dev->q8dump_index.insert(dev->q8dump_index.end(), rec, rec + Q8DUMP_REC);
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -921,6 +949,13 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
         need(Mc, 2304, 768); need(Mc, 3072, 768); need(Mc, 768, 3072); need(Mc, 768, 768);
         A(gpart, cap);
     }
+    if (const char *qd = getenv("MAGPIE_Q8DUMP"); qd && atoi(qd) != 0 && dev->m.weight_mode == MP_WEIGHTS_Q8) {
+        // the largest launch: K = 768, N = 2304 (QKV): rows, blocks, d, dots
+        const size_t slot = ((size_t)NB * 768 * 5 + (size_t)NB * 24 * 4 + (size_t)2304 * 24 * NB * 4 + 255) / 256 * 256;
+        dev->q8dump_cap = 4 * L + 16;
+        dev->q8dump_slot = slot;
+        if ((rc = dalloc(dev, &dev->q8dump, slot * dev->q8dump_cap)) != MP_OK) return rc;
+    }
 #undef A
     return MP_OK;
 }
@@ -948,7 +983,16 @@ bool q8_unfused();
 // Enqueue one decode iteration: decoder step at pos (embedding codes_prev), LT
 // over 8 codebooks, finalize. When `record` is set, the op list is rebuilt for
 // measurement (mp_hip_time_op).
+int enqueue_iteration_body(mp_dev *dev, hipStream_t s, bool record);
 int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
+    dev->q8dump_n = 0;
+    dev->q8dump_index.clear();
+    dev->q8dump_live = true;
+    const int rc = enqueue_iteration_body(dev, s, record);
+    dev->q8dump_live = false;
+    return rc;
+}
+int enqueue_iteration_body(mp_dev *dev, hipStream_t s, bool record) {
     const mp::Model &m = dev->m;
     const int NB = dev->NB, L = m.dec_layers;
     const bool b16 = mp::h16_mode(m.weight_mode);  // 16-bit MFMA family (bf16 or F16 weights)
@@ -959,7 +1003,9 @@ int enqueue_iteration(mp_dev *dev, hipStream_t s, bool record) {
     // a quantised tensor's decode bytes per weight: Q8_0 34/32, Q4_0 nibble fragments 18/32
     auto Fq = [](const mp::QW &w) { return w.nib ? 18.0 / 32.0 : 34.0 / 32.0; };
     if (record) dev->ops.clear();
-    auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
+    auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g0, double bytes) -> int {
+        mp::GemvP g = g0;
+        q8dump_assign(dev, name, g);
         if (record) {
             mp::OpRec r{};
             r.name = name; r.kind = mp::K_GEMV; r.fn = fn; r.g = g; r.B = NB; r.bytes = bytes;
@@ -1179,7 +1225,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
     const double F = b16 ? 2.0 : 4.0, A = 4.0, act = (double)NB;
     // a quantised tensor's decode bytes per weight: Q8_0 34/32, Q4_0 nibble fragments 18/32
     auto Fq = [](const mp::QW &w) { return w.nib ? 18.0 / 32.0 : 34.0 / 32.0; };
-    auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g, double bytes) -> int {
+    auto run = [&](const char *name, mp::GemvFn fn, const mp::GemvP &g0, double bytes) -> int {
+        mp::GemvP g = g0;
+        q8dump_assign(dev, name, g);
         if (ops) {
             mp::OpRec r{};
             r.name = name; r.kind = mp::K_GEMV; r.fn = fn; r.g = g; r.B = NB; r.bytes = bytes;
@@ -1786,6 +1834,7 @@ void mp_hip_free(mp_dev *dev) {
     for (hipEvent_t e : dev->sev)
         if (e) hipEventDestroy(e);
     if (dev->h_codes) hipHostFree(dev->h_codes);
+    if (dev->enc_ws) hipFree(dev->enc_ws);
     if (dev->stream) hipStreamDestroy(dev->stream);
     delete dev;
 }
@@ -1853,7 +1902,7 @@ int mp_hip_begin_batch(mp_dev *dev, const int32_t *tokens, const int32_t *n_toke
 }
 
 // magpie_encode_text (magpie.cpp:2284-2374) on its own: the text encoder of one
-// utterance into a private device workspace (allocated and freed per call), the
+// utterance into a private device workspace (kept on the mp_dev, grown on demand), the
 // output copied to enc_out [n_tokens][768]. A batch in progress is not touched.
 int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *enc_out) {
     if (!dev) return MP_ERR_ARG;
@@ -1865,8 +1914,18 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
     HIPCHK(hipSetDevice(dev->device));
     const size_t M = (size_t)n_tokens, D = 768;
     const size_t nf = M * D * 4 + M * 3 * D + M * 3072 + enc_gpart_elems(M) + M * D;  // pX pH pATT enc_out | pQKV | pF | gpart
-    char *ws = nullptr;
-    HIPCHK(hipMalloc(&ws, nf * 4 + 64 + M * 4));  // floats | T (64 B slot) | token ids
+    const size_t need = nf * 4 + 64 + M * 4;  // floats | T (64 B slot) | token ids
+    if (dev->enc_ws_bytes < need) {
+        // the old workspace may still be read by this stream's earlier encode: wait for it
+        // (the stream only, not the device) before it goes
+        HIPCHK(hipStreamSynchronize(dev->stream));
+        if (dev->enc_ws) hipFree(dev->enc_ws);
+        dev->enc_ws = nullptr;
+        dev->enc_ws_bytes = 0;
+        HIPCHK(hipMalloc(&dev->enc_ws, need));
+        dev->enc_ws_bytes = need;
+    }
+    char *ws = dev->enc_ws;
     float *f = (float *)ws;
     EncWs w{};
     w.NB = 1; w.Tmax = n_tokens;
@@ -1875,19 +1934,15 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
     int32_t *ti = (int32_t *)(ws + nf * 4 + 64);
     int32_t *Ti = (int32_t *)(ws + nf * 4);
     w.tok = ti; w.T = Ti;
-    int rc = MP_OK;
-    hipError_t e = hipMemcpyAsync(ti, tokens, M * 4, hipMemcpyHostToDevice, dev->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(Ti, &n_tokens, 4, hipMemcpyHostToDevice, dev->stream);
-    if (e != hipSuccess) rc = fail(dev, MP_ERR_HIP, hipGetErrorString(e));
-    if (rc == MP_OK) rc = run_encoder(dev, w, dev->stream);
-    if (rc == MP_OK) {
-        e = hipMemcpyAsync(enc_out, w.enc_out, M * D * 4, hipMemcpyDeviceToHost, dev->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(dev->stream);
-        if (e != hipSuccess) rc = fail(dev, MP_ERR_HIP, hipGetErrorString(e));
+    HIPCHK(hipMemcpyAsync(ti, tokens, M * 4, hipMemcpyHostToDevice, dev->stream));
+    HIPCHK(hipMemcpyAsync(Ti, &n_tokens, 4, hipMemcpyHostToDevice, dev->stream));
+    if (int rc = run_encoder(dev, w, dev->stream)) {
+        hipStreamSynchronize(dev->stream);  // the host token copies above must land first
+        return rc;
     }
-    hipStreamSynchronize(dev->stream);
-    hipFree(ws);
-    return rc;
+    HIPCHK(hipMemcpyAsync(enc_out, w.enc_out, M * D * 4, hipMemcpyDeviceToHost, dev->stream));
+    HIPCHK(hipStreamSynchronize(dev->stream));
+    return MP_OK;
 }
 
 // Per-decode device state: BOS frame at position 110 (magpie.cpp:4243-4318).
@@ -2223,6 +2278,12 @@ int64_t mp_hip_debug_buffer(mp_dev *dev, const char *name, void *host, int64_t b
     else if (n == "kc") { src = dev->kc; sz = NB * L * S * 768 * (dev->kv16 ? 2 : 4); }
     else if (n == "vc") { src = dev->vc; sz = NB * L * S * 768 * (dev->kv16 ? 2 : 4); }
     else if (n == "x") { src = dev->x; sz = NB * 768 * 4; }
+    else if (n == "q8dump" && dev->q8dump) { src = dev->q8dump; sz = dev->q8dump_slot * dev->q8dump_n; }
+    else if (n == "q8dump_index" && dev->q8dump) {
+        sz = dev->q8dump_index.size() * 4;
+        if (host) memcpy(host, dev->q8dump_index.data(), std::min<size_t>(sz, (size_t)bytes));
+        return (int64_t)sz;
+    }
     else return fail(dev, MP_ERR_ARG, "unknown buffer " + n);
     if (host) {
         HIPCHK(hipSetDevice(dev->device));

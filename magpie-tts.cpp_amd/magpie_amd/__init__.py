@@ -123,6 +123,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
+def lib_sha16(path: str = LIB_PATH) -> str:
+    """sha256[:16] of the library file: ties a committed profile to the build it measured."""
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     load_library().mp_hip_device_count(ctypes.byref(n))
@@ -281,7 +288,12 @@ class Device:
         (False stops that utterance). The EOS frame is emitted, as the reference's streaming
         loop does. Returns (codes per utterance, total samples, timing)."""
         B = self.begin(tokens, speakers, max_dec_steps, temperature, top_k, ignore_eos, seed, False, stream_base, True)
+        return self.decode_stream_only(codec, on_audio, B, max_dec_steps, frames_per_chunk)
 
+    def decode_stream_only(self, codec: "Codec", on_audio, B: int, max_dec_steps: int, frames_per_chunk: int = 4):
+        """mp_hip_decode_stream on the batch the last begin() prepared (the preamble is not
+        re-run): the decode on this device's stream, each chunk through the codec on the
+        codec's stream as it completes. Returns (codes per utterance, total samples, timing)."""
         def _cb(utt, ptr, n, _user):
             if n == 0:  # end-of-utterance notice
                 return 1
@@ -335,6 +347,15 @@ class Device:
         out = np.zeros(n // 4, np.float32)
         self._check(0 if self.lib.mp_hip_debug_buffer(self.h, name.encode(), out.ctypes.data, n) == n else -5)
         return out
+
+    def debug_bytes(self, name: str) -> bytes:
+        """mp_hip_debug_buffer as raw bytes (e.g. "q8dump", "q8dump_index" with MAGPIE_Q8DUMP=1)."""
+        n = self.lib.mp_hip_debug_buffer(self.h, name.encode(), None, 0)
+        if n < 0:
+            self._check(int(n))
+        out = ctypes.create_string_buffer(max(int(n), 1))
+        self._check(0 if self.lib.mp_hip_debug_buffer(self.h, name.encode(), out, n) == n else -5)
+        return out.raw[:n]
 
     # ---- measurement
     def ops(self) -> List[str]:

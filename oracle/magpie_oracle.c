@@ -85,6 +85,34 @@ static void quant_row_q8(const float *x, int K, int8_t *q, float *d) {
     }
 }
 
+// the exact integer dot of one weight block with one activation block (the sumi of
+// ggml_vec_dot_q8_0_q8_0 / vec_dot_q4_0_q8_0, Q4_0 weights as q - 8)
+static int block_dot_q8(const int8_t *wq, const int8_t *aq) {
+    int s = 0;
+    for (int j = 0; j < 32; ++j) s += (int)wq[j] * (int)aq[j];
+    return s;
+}
+
+// a GGUF tensor's Q8_0 (type 8: fp16 d + 32 int8) or Q4_0 (type 2: fp16 d + 16 bytes,
+// byte j = q_j | q_{j+16} << 4, value (q - 8) d) blocks as int8 values + f32 scales
+static void unpack_qblocks(const uint8_t *src, int type, int64_t n, int8_t *q, float *d) {
+    for (int64_t b = 0; b < n / 32; ++b) {
+        uint16_t h;
+        if (type == 8) {
+            memcpy(&h, src + b * 34, 2);
+            memcpy(q + b * 32, src + b * 34 + 2, 32);
+        } else {  // Q4_0 as ggml's vec_dot_q4_0_q8_0 reads it: (nibble - 8), same integer dot
+            const uint8_t *blk = src + b * 18;
+            memcpy(&h, blk, 2);
+            for (int j = 0; j < 16; ++j) {
+                q[b * 32 + j] = (int8_t)((blk[2 + j] & 0x0F) - 8);
+                q[b * 32 + j + 16] = (int8_t)((blk[2 + j] >> 4) - 8);
+            }
+        }
+        d[b] = orc_f16_to_f32(h);
+    }
+}
+
 static void matmul_q8(const q8w_t *W, const float *bias, const float *X, float *Y, int M, int N, int K) {
     const int nb = K / 32;
     int8_t *xq = malloc((size_t)M * K);
@@ -100,8 +128,7 @@ static void matmul_q8(const q8w_t *W, const float *bias, const float *X, float *
             double v64 = 0.0;
             float v32 = 0.f;
             for (int b = 0; b < nb; ++b) {
-                int s = 0;
-                for (int j = 0; j < 32; ++j) s += (int)wq[b * 32 + j] * (int)aq[b * 32 + j];
+                const int s = block_dot_q8(wq + b * 32, aq + b * 32);
                 if (g_acc64) v64 += (double)s * ((double)wd[b] * (double)ad[b]);
                 else v32 += (float)s * (wd[b] * ad[b]);
             }
@@ -300,21 +327,7 @@ static float *take(orc_model *m, const orc_gguf *g, const char *name, int *ok) {
         e->w = p;
         e->q = malloc((size_t)n);
         e->d = malloc(sizeof(float) * (size_t)(n / 32));
-        for (int64_t b = 0; b < n / 32; ++b) {
-            uint16_t h;
-            if (t->type == 8) {
-                memcpy(&h, src + b * 34, 2);
-                memcpy(e->q + b * 32, src + b * 34 + 2, 32);
-            } else {  // Q4_0 as ggml's vec_dot_q4_0_q8_0 reads it: (nibble - 8), same integer dot
-                const uint8_t *blk = src + b * 18;
-                memcpy(&h, blk, 2);
-                for (int j = 0; j < 16; ++j) {
-                    e->q[b * 32 + j] = (int8_t)((blk[2 + j] & 0x0F) - 8);
-                    e->q[b * 32 + j + 16] = (int8_t)((blk[2 + j] >> 4) - 8);
-                }
-            }
-            e->d[b] = orc_f16_to_f32(h);
-        }
+        unpack_qblocks(src, (int)t->type, n, e->q, e->d);
     }
     return p;
 }
@@ -1098,6 +1111,25 @@ int orc_codec_decode(orc_codec *c, const int32_t *codes, int F, float *audio, in
 
 // Unit-test entry: y[N] = ggml Q8_0 mul_mat of the raw GGUF Q8_0 blocks
 // (34 bytes per 32 weights, row-major [N][K]) with the activation x[K].
+int orc_q8_quantize_row(const float *x, int K, int8_t *q, float *d) {
+    if (!x || !q || !d || K <= 0 || K % 32) return -1;
+    quant_row_q8(x, K, q, d);
+    return 0;
+}
+
+int orc_qblock_dots(const uint8_t *blocks, int type, int N, int K, const int8_t *aq, int32_t *dots) {
+    if (!blocks || !aq || !dots || N <= 0 || K <= 0 || K % 32 || (type != 8 && type != 2)) return -1;
+    const int nb = K / 32;
+    int8_t *wq = malloc((size_t)N * K);
+    float *wd = malloc(sizeof(float) * (size_t)N * nb);
+    unpack_qblocks(blocks, type, (int64_t)N * K, wq, wd);
+    for (int n = 0; n < N; ++n)
+        for (int b = 0; b < nb; ++b) dots[(size_t)n * nb + b] = block_dot_q8(wq + (size_t)n * K + b * 32, aq + b * 32);
+    free(wq);
+    free(wd);
+    return 0;
+}
+
 int orc_q8_matvec(const uint8_t *blocks, int N, int K, const float *x, float *y) {
     if (!blocks || !x || !y || N <= 0 || K <= 0 || K % 32) return -1;
     q8w_t w = {NULL, malloc((size_t)N * K), malloc(sizeof(float) * (size_t)N * (K / 32))};

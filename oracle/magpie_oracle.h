@@ -89,6 +89,12 @@ int orc_sample_top_k(const float *logits, int n, float temperature, int top_k, f
 int orc_encode(orc_model *m, const int32_t *tokens, int n_tokens, float *enc_out /*[T][768]*/);
 // ggml Q8_0 mul_mat of raw GGUF Q8_0 blocks ([N][K], 34 B per 32 weights) with x[K].
 int orc_q8_matvec(const uint8_t *blocks, int N, int K, const float *x, float *y);
+// ggml's quantize_row_q8_0 (the oracle's restatement, the same function its Q8_0
+// mul_mat uses): x[K] -> q[K] int8, d[K/32] (fp16 values as f32).
+int orc_q8_quantize_row(const float *x, int K, int8_t *q, float *d);
+// The exact integer block dots of raw GGUF blocks (type 8 = Q8_0, 2 = Q4_0 as q - 8)
+// [N][K] with one quantised activation row aq[K]: dots[N][K/32].
+int orc_qblock_dots(const uint8_t *blocks, int type, int N, int K, const int8_t *aq, int32_t *dots);
 
 orc_codec *orc_codec_load(const char *gguf_path);
 void orc_codec_free(orc_codec *c);

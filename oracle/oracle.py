@@ -50,6 +50,8 @@ def lib() -> ctypes.CDLL:
         L.orc_codec_decode.argtypes = [P, P, I, P, I]
         L.orc_fsq.argtypes = [P, I, P]
         L.orc_q8_matvec.argtypes = [P, I, I, P, P]
+        L.orc_q8_quantize_row.argtypes = [P, I, P, P]
+        L.orc_qblock_dots.argtypes = [P, I, I, I, P, P]
         _lib = L
     return _lib
 
@@ -177,6 +179,27 @@ def q8_matvec(blocks: bytes, N: int, K: int, x) -> np.ndarray:
     if lib().orc_q8_matvec(buf.ctypes.data, N, K, xv.ctypes.data, y.ctypes.data) != 0:
         raise RuntimeError("oracle q8_matvec failed")
     return y
+
+
+def q8_quantize_row(x):
+    """ggml quantize_row_q8_0 of x[K] (the oracle's restatement): (int8 q[K], f32 d[K/32])."""
+    xv = np.ascontiguousarray(x, np.float32)
+    K = xv.size
+    q = np.zeros(K, np.int8)
+    d = np.zeros(K // 32, np.float32)
+    if lib().orc_q8_quantize_row(xv.ctypes.data, K, q.ctypes.data, d.ctypes.data) != 0:
+        raise RuntimeError("oracle q8_quantize_row failed")
+    return q, d
+
+
+def qblock_dots(blocks: bytes, gguf_type: int, N: int, K: int, aq) -> np.ndarray:
+    """Exact integer block dots [N][K/32] of raw GGUF Q8_0 (8) / Q4_0 (2) blocks with aq[K]."""
+    buf = np.frombuffer(blocks, np.uint8)
+    a = np.ascontiguousarray(aq, np.int8)
+    out = np.zeros((N, K // 32), np.int32)
+    if lib().orc_qblock_dots(buf.ctypes.data, gguf_type, N, K, a.ctypes.data, out.ctypes.data) != 0:
+        raise RuntimeError("oracle qblock_dots failed")
+    return out
 
 
 def fsq(codes_cb_major):

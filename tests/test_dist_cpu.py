@@ -29,6 +29,93 @@ def _worker(rank, world, port, q):
     q.put((rank, mine, t, n))
 
 
+# ---- the natural-EOS work-queue: ranks claim utterances from a shared counter
+QLENS = [int(x) for x in "5 61 12 40 33 7 58 21 9 44 18 3 50 27 36 14 62 8 29 47 11 55 24 38 6 19 42 31 16 60 2 35 52".split()]
+
+
+def _fake_synth(toks, spks):
+    """A device batch runs until its longest utterance ends (EOS lengths differ); the
+    result identifies the utterance so the test can check it came back whole."""
+    import time
+    time.sleep(0.004 * max(len(t) for t in toks))
+    return [(int(sum(t)), len(t), s) for t, s in zip(toks, spks)]
+
+
+def _queue_worker(rank, world, port, q):
+    import sys
+    import time
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "magpie-tts.cpp_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from magpie_amd.dist import gather_results, synthesize_queue
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    toks = [list(range(i, i + n)) for i, n in enumerate(QLENS)]
+    spks = [i % 5 for i in range(len(QLENS))]
+    dist.barrier()
+    t0 = time.perf_counter()
+    mine = synthesize_queue(_fake_synth, toks, spks, batch=4)
+    busy = time.perf_counter() - t0
+    allres = gather_results(mine, len(toks))
+    # a second queue in the same process group starts from 0 again (its own store key)
+    mine2 = synthesize_queue(_fake_synth, toks[:5], spks[:5], batch=2)
+    all2 = gather_results(mine2, 5)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, sorted(mine), busy, allres, all2))
+
+
+def test_work_queue_local_drains_in_order():
+    from magpie_amd.dist import WorkQueue, gather_results, longest_first, synthesize_queue
+    q = WorkQueue(7)
+    assert q.claim(3) == [0, 1, 2] and q.claim(3) == [3, 4, 5] and q.claim(3) == [6] and q.claim(3) == []
+    toks = [[1] * n for n in (3, 9, 9, 1, 5)]
+    assert longest_first(toks) == [1, 2, 4, 0, 3]
+    seen = []
+
+    def synth(tb, sb):
+        seen.append([len(t) for t in tb])
+        return [len(t) for t in tb]
+    mine = synthesize_queue(synth, toks, batch=2)
+    assert seen == [[9, 9], [5, 3], [1]]  # longest text first, `batch` per claim
+    assert gather_results(mine, 5) == [3, 9, 9, 1, 5]
+
+
+def test_work_queue_gloo_world_size_2_unequal_lengths():
+    """Two ranks, 33 utterances of unequal (EOS-like) lengths: every utterance is decoded
+    exactly once, by whichever rank was free, both ranks work, and their busy times end
+    within about one batch of each other (a static split of these lengths does not)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_queue_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, m0, b0, all0, s0), (_, m1, b1, all1, s1) = res
+    n = len(QLENS)
+    assert sorted(m0 + m1) == list(range(n)) and not set(m0) & set(m1)
+    assert m0 and m1
+    want = [(int(sum(range(i, i + L))), L, i % 5) for i, L in enumerate(QLENS)]
+    assert all0 == want and all1 == want
+    assert s0 == s1 == want[:5]
+    one_batch = 0.004 * max(QLENS)
+    assert abs(b0 - b1) < one_batch + 0.25, (b0, b1)
+    # the static contiguous split of the same 33 utterances in batches of 4
+    from magpie_amd.dist import shard_utterances
+
+    def static_cost(rank):
+        ids = shard_utterances(n, rank, 2)
+        return sum(0.004 * max(QLENS[i] for i in ids[j:j + 4]) for j in range(0, len(ids), 4))
+    # the queue (longest first, claimed as batches free) ends well before the static split
+    # of these lengths (1.10 s of sleep on rank 0 against ~0.54 s per rank measured)
+    assert max(b0, b1) < max(static_cost(0), static_cost(1)), (b0, b1)
+    print(f"queue busy {b0:.3f} / {b1:.3f} s; static split {static_cost(0):.3f} / {static_cost(1):.3f} s")
+
+
 def test_shard_utterances_partition():
     from magpie_amd.dist import shard_utterances
     for n, w in [(64, 8), (64, 3), (7, 4), (1, 1)]:

@@ -155,3 +155,26 @@ def test_lt_sample_q8_matches_oracle(ma, oracle, q8_model):
         compare_codes(smp[None], o_smp[None], o_mg[None], tie_eps=1e-2)
     dev.close()
     om.close()
+
+
+def test_configs2_overlapped_codec_equals_serial(ma, small_model, codec):
+    """configs[2]'s end-to-end form (bench.py measure_configs2_e2e): bf16, 16 slots, each
+    slot's 32-frame chunks decoded by the codec on its stream while the decode continues
+    (mp_hip_decode_stream, frames_per_chunk = 32). The waveform equals the serial form
+    bit for bit: the decode alone, then the codec over the same chunks."""
+    B, F, C = 16, 64, 32
+    toks = [ma.synthetic_tokens(12 + (b % 5), seed=1900 + b) for b in range(B)]
+    spk = [b % 5 for b in range(B)]
+    dev = ma.Device(small_model, weights="bf16")
+    ser = dev.synthesize(toks, speakers=spk, max_dec_steps=F, ignore_eos=True)
+    chunks, cb = _collect(B)
+    codes, total, tm = dev.synthesize_stream(codec, toks, cb, speakers=spk, max_dec_steps=F, frames_per_chunk=C,
+                                             ignore_eos=True)
+    dev.close()
+    assert total == B * F * 1024
+    serial = codec.decode_chunks(np.stack([ser.codes[b][s0:s0 + C].T for b in range(B) for s0 in range(0, F, C)]))
+    for b in range(B):
+        assert np.array_equal(codes[b], ser.codes[b]), b
+        assert [len(c) for c in chunks[b]] == [C * 1024] * (F // C)
+        for k, got in enumerate(chunks[b]):
+            assert np.array_equal(got, serial[b * (F // C) + k]), (b, k)

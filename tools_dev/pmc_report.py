@@ -10,8 +10,9 @@ of a wide coalesced streaming read (16 B/lane) -> doubled here, but only for the
 kernels whose bulk loads are 16 B per lane (WIDE below); other kernels' fetch is
 reported raw and marked uncalibrated. WRITE_SIZE is exact for 16 B/lane stores.
 Infinity-Cache hits are counted: these are L2-miss (fabric) bytes, an upper bound
-on HBM bytes. MFMA utilisation = sum SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x
-1024 SIMDs) (rocprofv3's MfmaUtil expression); MFMA FLOPs = MOPS x 512. Under
+on HBM bytes. MFMA utilisation = sum SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x
+1024 SIMDs): GRBM_GUI_ACTIVE is the sum over the 8 XCDs, so / 8 gives the dispatch's
+cycles (round 5 divided by the sum, 8x too low); MFMA FLOPs = MOPS x 512. Under
 per-dispatch PMC collection GRBM_GUI_ACTIVE includes the profiler's own per-dispatch
 overhead, so with a kernel trace of the same workload (TRACE_CSV, e.g. the bench's
 rocprofv3 --kernel-trace run) the codec utilisation is also given against the traced
@@ -28,6 +29,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 SIMDS = 256 * 4
+XCDS = 8  # GRBM_GUI_ACTIVE is reported summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS row)
 CLK = 2.4e9  # shader clock (MI355X_MICROARCH.md)
 # kernels whose bulk global loads are 16 B per lane (float4 / uint4 / half8)
 WIDE = ("gemv_kernel", "gemm_b16_kernel", "xa_part_kernel", "sa_attn_kernel", "lt_ffn2_kernel", "lt_ffn_kernel",
@@ -85,7 +87,7 @@ def decode_ops(tag, pre, ops_file, mfma):
             busy, gui = float(np.mean(rec["SQ_VALU_MFMA_BUSY_CYCLES"])), float(np.mean(rec["GRBM_GUI_ACTIVE"]))
             o["mfma_busy_cycles"] = round(busy)
             o["gui_active_cycles"] = round(gui)
-            o["mfma_util"] = round(busy / (gui * SIMDS), 4) if gui else None
+            o["mfma_util"] = round(busy / (gui / XCDS * SIMDS), 4) if gui else None
             mops = [v for k, v in rec.items() if k.startswith("SQ_INSTS_VALU_MFMA_MOPS_")]
             if mops:
                 o["mfma_ops"] = round(float(np.mean(mops[0])) * 512)  # MOPS x 512 = multiply-adds x 2
@@ -124,7 +126,7 @@ def codec(tag, trace=None):
         fb = 2 * f if wide(kern) else f
         rec = {"kernel": kern, "grid": grid, "dispatches": n, "fetch_bytes": round(fb), "fetch_corrected": wide(kern),
                "write_bytes": round(w), "mfma_flops": round(flops), "mfma_busy_cycles": round(busy),
-               "gui_active_cycles": round(gui), "mfma_util": round(busy / (gui * SIMDS), 4) if gui else None}
+               "gui_active_cycles": round(gui), "mfma_util": round(busy / (gui / XCDS * SIMDS), 4) if gui else None}
         if flops:
             rec["busy_cycles_per_mfma_16x16x32"] = round(busy / (flops / 16384), 2)
         t = dur.get((kern, grid))
@@ -142,7 +144,7 @@ def codec(tag, trace=None):
     out.sort(key=lambda r: -r["dispatches"] * r["gui_active_cycles"])
     decodes = 4
     summary = {"chunks": 8, "per_decode_bytes": round(tot["bytes"] / decodes), "per_decode_mfma_flops": round(tot["flops"] / decodes),
-               "mfma_util_gui_active": round(tot["busy"] / (tot["gui"] * SIMDS), 4) if tot["gui"] else None}
+               "mfma_util_gui_active": round(tot["busy"] / (tot["gui"] / XCDS * SIMDS), 4) if tot["gui"] else None}
     if tot["t"]:
         summary["per_decode_traced_us"] = round(tot["t"] / decodes, 1)
         summary["mfma_util_traced"] = round(tot["busy"] / (tot["t"] * 1e-6 * CLK * SIMDS), 4)
@@ -159,7 +161,8 @@ def main():
     for pre, ops_file, mfma, name in (("f32b1", "pmc_ops_f32_1.json", False, "decode_f32_b1"),
                                       ("b16b16", "pmc_ops_bf16_16.json", True, "decode_bf16_b16"),
                                       ("q8b16", "pmc_ops_q8_16.json", True, "decode_q8_b16")):
-        res = {"source": src, "workload": name, "ops": decode_ops(tag, pre, ops_file, mfma)}
+        res = {"source": src, "workload": name, "ops": decode_ops(tag, pre, ops_file, mfma),
+               "lib_sha16": json.load(open(os.path.join(OUT, ops_file))).get("lib_sha16")}
         json.dump(res, open(os.path.join(REPO, "profiles", f"{tag}_pmc_{name}.json"), "w"), indent=1)
         print(f"== {name}")
         for op, v in res["ops"].items():
@@ -167,6 +170,8 @@ def main():
             print(f"  {op:10s} fetch {v['fetch_bytes'] / 1e6:8.3f} MB write {v['write_bytes'] / 1e6:7.3f} MB{extra}")
     c = codec(tag, sys.argv[2] if len(sys.argv) > 2 else None)
     c["source"] = src
+    bj = os.path.join(OUT, "pmc_codec_build.json")
+    c["lib_sha16"] = json.load(open(bj)).get("lib_sha16") if os.path.exists(bj) else None
     json.dump(c, open(os.path.join(REPO, "profiles", f"{tag}_pmc_codec.json"), "w"), indent=1)
     print("== codec", c["summary"])
     for r in c["kernels"][:14]:

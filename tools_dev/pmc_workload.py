@@ -26,6 +26,7 @@ if mode == "codec":
     for _ in range(4):
         c.decode_chunks(codes)
     c.close()
+    json.dump({"lib_sha16": ma.lib_sha16()}, open(os.path.join(REPO, "gpurun_out", "pmc_codec_build.json"), "w"))
     print("pmc codec workload done")
 else:
     weights = sys.argv[2] if len(sys.argv) > 2 else "f32"
@@ -38,7 +39,7 @@ else:
     toks = [ma.synthetic_tokens(64, seed=1000 + b) for b in range(B)]
     r = dev.synthesize(toks, speakers=[b % 5 for b in range(B)], max_dec_steps=int(os.environ.get("PMC_FRAMES", "64")),
                        ignore_eos=True)
-    json.dump({"ops": dev.ops(), "frames": int(r.n_frames[0])},
+    json.dump({"ops": dev.ops(), "frames": int(r.n_frames[0]), "lib_sha16": ma.lib_sha16()},
               open(os.path.join(REPO, "gpurun_out", f"pmc_ops_{weights}_{B}.json"), "w"))
     dev.close()
     print("pmc decode workload done", weights, B, r.n_frames[0], "frames")

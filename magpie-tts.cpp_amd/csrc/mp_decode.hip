@@ -128,6 +128,30 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
 #pragma unroll
         for (int b = 0; b < NB; ++b)
             if (lane == r * NB + b) v = acc[r][b];
+    if constexpr (NB == 1 && EPI == EPI_BIAS && PRO == PRO_LTFFN_MERGE) {
+        if (p.cand) {  // uniform: the f32 LT head's workgroup candidate (greedy, batch 1)
+            // the masked first-max of this workgroup's logits as one ordered key (every special
+            // id but EOS masked); EOS's own key goes to slot LT_HEAD_WGS, and the consumer
+            // (lt_step_body) drops it while EOS is forbidden (step < 4, or ignore_eos)
+            __shared__ unsigned long long ck[MP_NWAVES];
+            unsigned long long key = 0;
+            const int n = row0 + lane;
+            if (lane < RW && n < p.N) {
+                const float lv = v + eop;  // the logit epi_store_op<EPI_BIAS> stores
+                if (n == p.audio_eos) p.cand[LT_HEAD_WGS] = lt_cand_key(lv, n);
+                else if (!lt_forbidden(n, true, p.audio_bos, p.audio_eos)) key = lt_cand_key(lv, n);
+            }
+            key = wave_max_u64(key);
+            if (lane == 0) ck[w] = key;
+            lds_sync();
+            if (threadIdx.x == 0) {
+                unsigned long long k = ck[0];
+#pragma unroll
+                for (int u = 1; u < MP_NWAVES; ++u) k = ck[u] > k ? ck[u] : k;
+                p.cand[blockIdx.x] = k;
+            }
+        }
+    }
     if (lane >= RW * NB) return;
     const int b = lane % NB, n = row0 + lane / NB;
     if (n >= p.N) return;
@@ -703,6 +727,37 @@ __device__ __forceinline__ int lt_pick_split(const LtFfn2P &p, int w, const LtYP
     return pick_exchange(bv, bi, code);
 }
 
+// The same pick from the head's workgroup candidates (GemvP::cand, batch 1 greedy): wave w
+// holds candidates 64 w .. 64 w + 63 (one ordered key per lane; slot LT_HEAD_WGS is EOS's key,
+// dropped while EOS is forbidden), one 64-bit wave max gives the wave's (value, first index),
+// then the same gather and exchange as lt_pick_split. The candidates cover ascending row
+// ranges wave by wave, so the exchange's first wave at the maximum holds the first index:
+// the code is wave_pick_rows'.
+__device__ __forceinline__ void lt_y_load_c(const LtFfn2P &p, int w, LtYPre &r, unsigned long long &ck) {
+    const int lane = threadIdx.x & 63, cb = p.cb;
+    const size_t row = 4 * (size_t)lane;  // slot 0
+#pragma unroll
+    for (int j = 0; j < NCB - 1; ++j) {
+        const int jj = j < cb ? j : 0;
+        r.kr[j] = *(const f32x4 *)(p.ltk + row + jj * LTD);
+        r.vr[j] = *(const f32x4 *)(p.ltv + row + jj * LTD);
+    }
+    const int slot = 64 * w + lane;
+    ck = slot <= p.ncand ? p.cand[slot] : 0ull;
+    r.stp = p.step[0];
+}
+__device__ __forceinline__ int lt_pick_cand(const LtFfn2P &p, int w, const LtYPre &yp, unsigned long long ck, LtRows &g,
+                                            int &code) {
+    const int lane = threadIdx.x & 63;
+    if (64 * w + lane == p.ncand && (p.ignore_eos || yp.stp < 4)) ck = 0;  // EOS forbidden
+    ck = wave_max_u64(ck);
+    const float bv = ck ? lt_cand_value(ck) : -INFINITY;
+    int bi = ck ? lt_cand_index(ck) : 0;
+    if (bi < 0 || bi >= VCB) bi = 0;
+    g = lt_gather(p, bi);
+    return pick_exchange(bv, bi, code);
+}
+
 __device__ __forceinline__ float4 lt_y_slot(const LtFfn2P &p, int b, bool wb0, float *wsc) {
     LtYPre r;
     lt_y_load(p, b, r);
@@ -725,8 +780,11 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     // the wave's first slot's loads (logits, earlier positions) ahead of the weights
     LtYPre yp;
     float lq[QPR];
+    unsigned long long ck = 0;
     const bool quad = NB == 1 && p.cb > 0 && !p.smp.on;  // uniform: the split greedy pick
-    if (quad) lt_y_load_q(p, 0, w, yp, lq);
+    const bool cand = quad && p.cand;                      // uniform: ... from the head's candidates
+    if (cand) lt_y_load_c(p, w, yp, ck);
+    else if (quad) lt_y_load_q(p, 0, w, yp, lq);
     else if (w < NB) lt_y_load(p, w, yp);
     // the LN weights with the first loads: loaded after y (behind its stores) they cost an
     // L2 round trip on the step's critical path
@@ -756,7 +814,7 @@ __device__ __forceinline__ void lt_step_body(const LtFfn2P &p, int pb, int dep, 
     if (quad) {
         LtRows g;
         int code;
-        if (lt_pick_split(p, w, yp, lq, g, code) == w) {
+        if ((cand ? lt_pick_cand(p, w, yp, ck, g, code) : lt_pick_split(p, w, yp, lq, g, code)) == w) {
             ts_phase_w<0>(p.f.ts);  // profiling: code picked
             const float4 y = lt_y_attend(p, 0, pb == 0, code, code, yp, g);
             ts_phase_w<1>(p.f.ts);  // profiling: y (gathers + attention)
@@ -1161,9 +1219,6 @@ hipError_t op_lt_front(const LtFrontP &p, hipStream_t s) {
 }
 
 // the LT head at batch 1 with the FFN merge as its prologue
-#ifndef MP_RW_LTE
-#define MP_RW_LTE 2  // head rows per wave at batch 1 (253 workgroups at 2)
-#endif
 hipError_t op_lt_em_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, MP_RW_LTE, LTD, PRO_LTFFN_MERGE, EPI_BIAS>(p, s); }
 // f32 LT position 0: LN(X_0) -> [k_0 | vo_0] (W = [W_k ; W_o W_v], 512 x 256)
 hipError_t op_lt_kvo(const GemvP &p, int NB, hipStream_t s) {

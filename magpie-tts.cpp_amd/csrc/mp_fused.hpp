@@ -196,6 +196,35 @@ __device__ __forceinline__ int wave_pick_rows(float (&lv)[QPR], int w, bool forb
     return wave_min_u(first);
 }
 
+// A logit as an ordered 64-bit key: the float's bits mapped to an unsigned order (high word)
+// and 0xFFFFFFFF - index (low word), so the largest key is the largest value at the lowest
+// index: the masked first-max argmax of wave_pick_rows / sample_top_k's greedy branch. 0 is
+// below every real key (a forbidden id).
+__device__ __forceinline__ unsigned long long lt_cand_key(float v, int i) {
+    const unsigned u = __float_as_uint(v);
+    const unsigned o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)o << 32) | (0xFFFFFFFFu - (unsigned)i);
+}
+__device__ __forceinline__ float lt_cand_value(unsigned long long k) {
+    const unsigned o = (unsigned)(k >> 32);
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+__device__ __forceinline__ int lt_cand_index(unsigned long long k) { return (int)(0xFFFFFFFFu - (unsigned)k); }
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long k) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)k, off), hi = __shfl_xor((unsigned)(k >> 32), off);
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+        k = o > k ? o : k;
+    }
+    return k;
+}
+// Whether logit i is forbidden (sample_top_k's mask, magpie.cpp:1237-1248): the 8 special
+// audio ids except EOS, and EOS too while forbid_eos.
+__device__ __forceinline__ bool lt_forbidden(int i, bool forbid_eos, int audio_bos, int audio_eos) {
+    return i >= VCB || ((unsigned)(i - audio_bos) <= 7u && (i != audio_eos || forbid_eos));
+}
+
 // The split pick's exchange: every wave's (max, first index) pair through LDS; returns the
 // first wave holding the workgroup-wide maximum (its first index is the global first
 // index: its ids are the lowest among the waves at that value) and its index in `code`.

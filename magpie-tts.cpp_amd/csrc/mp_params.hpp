@@ -16,6 +16,10 @@ constexpr int LTD = 256;      // local transformer dim        (magpie.h:54)
 constexpr int LTF = 1024;     // LT ffn dim                   (magpie.h:55)
 constexpr int NCB = 8;        // codebooks                    (magpie.h:61)
 constexpr int VCB = 2024;     // vocab per codebook           (magpie.h:63)
+#ifndef MP_RW_LTE
+#define MP_RW_LTE 2  // f32 LT head rows per wave at batch 1 (253 workgroups at 2)
+#endif
+constexpr int LT_HEAD_WGS = (VCB + 4 * MP_RW_LTE - 1) / (4 * MP_RW_LTE);  // its workgroups = candidates
 constexpr int CTX = 110;      // baked context frames         (magpie.h:67)
 constexpr int SA_CHUNK = 64;  // cache rows are allocated in whole 64-key chunks
 constexpr int NCH_MAX = 16;   // -> max_seq <= 1024 (reference: 626, magpie.cpp:4077)
@@ -143,6 +147,9 @@ struct LtFfn2P {
     unsigned long long *gh;
     const int *iter;
     int *hx_err;
+    // f32 batch 1, greedy: the previous head's workgroup candidates (GemvP::cand), ncand of them
+    const unsigned long long *cand;
+    int ncand;
 };
 
 // f32 mode at batch 1: the LT's front in ONE launch (lt_front_kernel) instead of three
@@ -332,6 +339,10 @@ struct GemvP {
     // activation rows [NB][K], their Q8_0 blocks (int8 [NB][K], fp16 d as f32 [NB][K/32])
     // and every integer block dot [N][K/32][NB] (int32), as the kernel's operands give them
     void *q8dump;
+    // f32 LT head at batch 1, greedy (nullable): every workgroup also publishes its masked
+    // first-max logit as one ordered 64-bit key cand[blockIdx.x] (lt_cand_key), so the next
+    // LT step picks the code from the head's ~253 workgroup candidates instead of its 2024 logits
+    unsigned long long *cand;
 };
 
 // Q8_0 weight mode: the LT step of codebook cb as LTQ_P workgroups per slot

@@ -57,6 +57,40 @@ __device__ __forceinline__ void gemm_store(const GemmP &p, const float (&acc)[4]
     }
 }
 
+// Split-K reduction inside the GEMM launch (GemmP::ctr): every split of a 64 x 64 output
+// tile publishes its partial tile, then counts itself in; the last to arrive sums the
+// gridDim.z partials of the tile in split order and applies the epilogue - exactly
+// gemm_reduce_kernel's arithmetic, without its launch (one per split GEMM, ~100 per
+// preamble). The release fence makes the partial stores visible device-wide (every XCD's
+// L2) before the count; the last arriver's acquire fence orders its partial loads after it.
+template <int EPI>
+__device__ __forceinline__ void gemm_tile_reduce(const GemmP &p, int m0, int n0) {
+    __shared__ int last;
+    const int tid = threadIdx.x;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the whole device (every XCD)
+    __syncthreads();
+    if (tid == 0) {
+        int *c = p.ctr + blockIdx.y * gridDim.x + blockIdx.x;
+        const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (int)gridDim.z - 1;
+        if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next GEMM
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const size_t total = (size_t)p.M * p.N;
+    const int S = gridDim.z;
+#pragma unroll 4
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int m = m0 + e / 64, n = n0 + e % 64;
+        if (m >= p.M || n >= p.N) continue;
+        const size_t o = (size_t)m * p.N + n;
+        float v = p.part[o];
+        for (int s = 1; s < S; ++s) v += p.part[(size_t)s * total + o];
+        gemm_store1<EPI>(p, m, n, v);
+    }
+}
+
 // Split-K reduction: v = sum of the splits in order, then the epilogue.
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmP p, int splits) {
@@ -68,14 +102,14 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmP p, int splits) {
     }
 }
 
-// K steps of 16 with PF steps' operand loads in flight per thread (register ring):
+// K steps of 16 with PF = 8 steps' operand loads in flight per thread (register ring):
 // a step's loads are issued PF steps before its tile is staged, so the global latency
-// is paid once per PF steps, not per step (the preamble GEMMs have small grids: one
+// is paid once per PF steps (once per PRE_KS-wide split slice), not per step (the preamble GEMMs have small grids: one
 // workgroup per CU or fewer). The arithmetic (k order, FMA order) is the plain
 // LDS-tiled GEMM's.
 template <int EPI, int TAPS>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
-    constexpr int BM = 64, BN = 64, BK = 16, PF = 4;
+    constexpr int BM = 64, BN = 64, BK = 16, PF = 8;
     __shared__ float As[BK][BM + 4];
     __shared__ float Ws[BK][BN + 4];
     const int tid = threadIdx.x;
@@ -148,7 +182,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
 // 4 (l >> 4) + i, column l & 15.
 template <int EPI, int TAPS>
 __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
-    constexpr int BM = 64, BN = 64, BK = 16, PF = 4;
+    constexpr int BM = 64, BN = 64, BK = 16, PF = 8;
     typedef float f4v __attribute__((ext_vector_type(4)));
     __shared__ float As[BK][BM + 4];
     __shared__ float Ws[BK][BN + 4];
@@ -228,6 +262,7 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
                 else gemm_store1<EPI>(p, mm, nn, acc[i][j][r]);
             }
         }
+    if (p.part && p.ctr) gemm_tile_reduce<EPI>(p, m0, n0);
 }
 
 // Q8_0 weights (weight mode MP_WEIGHTS_Q8): ggml's quantised mul_mat. Every K
@@ -375,6 +410,109 @@ __global__ __launch_bounds__(256) void row_attn_kernel(RowAttnP p) {
     p.O[(size_t)m * D + h * DH + lane] = o / l;
 }
 
+// The same causal attention, tiled: workgroup (query block of 64 rows, head, utterance).
+// Keys are staged 64 at a time into LDS (coalesced row loads; bf16 cache rows widened)
+// and every wave runs an online softmax for 16 query rows: lane (row r = lane / 4,
+// quarter qq = lane % 4) scores keys 16 qq .. 16 qq + 15 of the tile against its row's
+// whole q (64 registers), the row's 4 lanes meet through DPP for the max and the sum, the
+// probabilities go through LDS, and the lane accumulates output dims 16 qq .. 16 qq + 15.
+// One workgroup per 64 rows and head replaces row_attn_kernel's wave per (row, head),
+// whose key loop made one dependent global round trip per 64 keys and its value loop
+// one per key.
+constexpr int RA_QB = 64, RA_KT = 64;
+template <bool KV16>
+__global__ __launch_bounds__(256) void row_attn_tile_kernel(RowAttnP p) {
+    __shared__ __attribute__((aligned(16))) float Ks[RA_KT][DH + 4];
+    __shared__ __attribute__((aligned(16))) float Vs[RA_KT][DH + 4];
+    __shared__ __attribute__((aligned(16))) float Ps[4][16][RA_KT + 4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int t0 = blockIdx.x * RA_QB, h = blockIdx.y, b = blockIdx.z;
+    const int R = p.rows_per_utt;
+    const int r = lane >> 2, qq = lane & 3;
+    const int t = t0 + 16 * w + r;  // this lane's query row (position in the utterance)
+    const bool live = t < R;
+    const int m = b * R + (live ? t : R - 1);
+    float q[DH];
+    {
+        const float *qp = p.Q + (size_t)m * p.ldq + h * DH;
+#pragma unroll
+        for (int d = 0; d < DH; d += 4) {
+            const float4 v = *(const float4 *)(qp + d);
+            q[d] = v.x; q[d + 1] = v.y; q[d + 2] = v.z; q[d + 3] = v.w;
+        }
+    }
+    float o[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[e] = 0.f;
+    float mx = -INFINITY, l = 0.f;
+    const int t_last = min(t0 + RA_QB, R) - 1;  // the block's last row: keys 0 .. t_last
+    const size_t kb0 = b * p.utt_stride + h * DH;
+    for (int j0 = 0; j0 <= t_last; j0 += RA_KT) {
+        // stage keys j0 .. j0 + 63: thread (key kr = tid / 4, 16 dims 16 (tid % 4))
+        {
+            const int kr = tid >> 2, dq = (tid & 3) * 16;
+            const int j = min(j0 + kr, t_last);
+            const size_t k = kb0 + (size_t)j * p.row_stride + dq;
+#pragma unroll
+            for (int d = 0; d < 16; d += 4) {
+                *(float4 *)&Ks[kr][dq + d] = kv_load4<KV16>(p.Kb, k + d);
+                *(float4 *)&Vs[kr][dq + d] = kv_load4<KV16>(p.Vb, k + d);
+            }
+        }
+        __syncthreads();
+        float sc[16];
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int kr = 16 * qq + jj;
+            float sv = 0.f;
+#pragma unroll
+            for (int d = 0; d < DH; d += 4) {
+                const float4 k4 = *(const float4 *)&Ks[kr][d];
+                sv += q[d] * k4.x + q[d + 1] * k4.y + q[d + 2] * k4.z + q[d + 3] * k4.w;
+            }
+            sv = j0 + kr <= t ? sv * 0.125f : -INFINITY;
+            sc[jj] = sv;
+            tmax = fmaxf(tmax, sv);
+        }
+        tmax = fmaxf(tmax, dpp_mov<0xB1>(tmax));  // the row's 4 lanes (a DPP quad)
+        tmax = fmaxf(tmax, dpp_mov<0x4E>(tmax));
+        const float mnew = fmaxf(mx, tmax);  // finite: key 0 .. t of every tile j0 <= t
+        const float corr = mx == -INFINITY ? 0.f : expf(mx - mnew);
+        float ls = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const float e = sc[jj] == -INFINITY ? 0.f : expf(sc[jj] - mnew);
+            ls += e;
+            Ps[w][r][16 * qq + jj] = e;
+        }
+        ls += dpp_mov<0xB1>(ls);
+        ls += dpp_mov<0x4E>(ls);
+        l = l * corr + ls;
+        mx = mnew;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row's probabilities are in LDS
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[e] *= corr;
+        const int jn = min(RA_KT, t_last - j0 + 1);
+        for (int kr = 0; kr < jn; ++kr) {
+            const float pj = Ps[w][r][kr];
+#pragma unroll
+            for (int e = 0; e < 16; e += 4) {
+                const float4 v4 = *(const float4 *)&Vs[kr][16 * qq + e];
+                o[e] += pj * v4.x; o[e + 1] += pj * v4.y; o[e + 2] += pj * v4.z; o[e + 3] += pj * v4.w;
+            }
+        }
+        __syncthreads();  // the tile's K / V rows are read by every wave before the next stage
+    }
+    if (!live) return;
+    const float il = 1.0f / l;
+    float *op = p.O + (size_t)m * D + h * DH + 16 * qq;
+#pragma unroll
+    for (int e = 0; e < 16; e += 4) *(float4 *)(op + e) = make_float4(o[e] * il, o[e + 1] * il, o[e + 2] * il, o[e + 3] * il);
+}
+
 // Cross-attention for a block of rows: 1 head x 128 over the utterance's T[b]
 // text positions (no mask).
 
@@ -480,9 +618,11 @@ static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
     dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits);
     GemmP q = p;
     if (splits == 1) q.part = nullptr;
-    if (gemm_mfma()) hipLaunchKernelGGL((gemm_f32_mfma_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
+    const bool mfma = gemm_mfma();
+    if (!mfma || grid.x * grid.y > PRE_CTR_TILES) q.ctr = nullptr;  // (the VALU kernel keeps the reduce launch)
+    if (mfma) hipLaunchKernelGGL((gemm_f32_mfma_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
     else hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
-    if (hipError_t e = hipGetLastError(); e != hipSuccess || splits == 1) return e;
+    if (hipError_t e = hipGetLastError(); e != hipSuccess || splits == 1 || q.ctr) return e;
     return launch_reduce<EPI>(p, splits, s);
 }
 template <int EPI>
@@ -535,6 +675,13 @@ hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s)
     return hipGetLastError();
 }
 hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s) {
+    static const bool old = getenv("MAGPIE_PRE_ROWATTN_OLD") != nullptr;  // A/B: the wave-per-(row, head) kernel
+    if (!old && p.M % p.rows_per_utt == 0) {
+        const dim3 grid((p.rows_per_utt + RA_QB - 1) / RA_QB, p.heads, p.M / p.rows_per_utt);
+        if (p.kv16) hipLaunchKernelGGL(row_attn_tile_kernel<true>, grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(row_attn_tile_kernel<false>, grid, dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     if (p.kv16) hipLaunchKernelGGL(row_attn_kernel<true>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(row_attn_kernel<false>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
     return hipGetLastError();

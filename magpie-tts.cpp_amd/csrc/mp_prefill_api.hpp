@@ -38,13 +38,26 @@ struct GemmP {
     // depend on M, i.e. on the batch), each written raw to part[s][M][N], then
     // summed in split order by a second launch that applies the epilogue.
     float *part;
+    // with part: the arrival counters of the output tiles ([grid.y][grid.x] ints, zero
+    // between GEMMs). When set, the MFMA kernel's last-arriving split of each tile sums
+    // the splits (the same order and epilogue as gemm_reduce_kernel) and zeroes the
+    // counter again: no second launch. Null: the separate reduce launch.
+    int *ctr;
     int xround;        // 2: round every A element to f16 as it is loaded (an F16 weight: ggml's
                        //    F16 mul_mat rounds src1 to f16; products then exact in f32)
 };
 
 // Split count of a preamble GEMM over K (fixed per K: batch-invariant results).
+// Pieces of PRE_KS = 128 (8 K steps of 16): every model K (128, 768, 2304, 3072, 9216) is a
+// multiple, and 8 steps are exactly the operand loads a thread keeps in flight
+// (gemm_f32_mfma_kernel's ring), so a workgroup pays one memory latency for its slice
+// instead of one per 4 steps (round 5: K / 96 pieces, at most 16: 576-wide slices of
+// the encoder's 9216-wide conv waited on memory 9 times).
+constexpr int PRE_KS = 128;
+constexpr int PRE_CTR_TILES = 4096;  // arrival counters per GEMM (GemmP::ctr): output tiles of 64 x 64
 inline int gemm_splits(int K) {
-    int s = K / 96;
+    if (K % PRE_KS == 0) return K / PRE_KS;
+    int s = K / 96;  // (no model K takes this path)
     if (s < 1) s = 1;
     if (s > 16) s = 16;
     while (s > 1 && (K % (s * 32)) != 0) --s;  // whole 32-wide (Q8_0) blocks per split

@@ -264,6 +264,7 @@ struct LtIo {
     float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel; lt_slot_kernel: [NB][LTS_P][256])
     unsigned long long *ltgh;  // [NB][LTS_P or LTQ_P][256] lt_slot(_q8)_kernel's partial-sum granules
     unsigned long long *ltfg;  // [2][256] lt_front_kernel's hand-off granules (f32, batch 1)
+    unsigned long long *ltcand;  // [256] the f32 batch-1 head's workgroup candidates (GemvP::cand; null: off)
     unsigned long long *ltyg;  // [NB][256] lt_slot_q8_kernel's y granules (Q8_0 mode)
     int *iter, *hx_err;        // decode iteration counter (hand-off tags), hand-off error bits
     int *codes_cur, *codes_prev, *codes_out, *step, *pos, *done, *nframes, *ndone, *argeos, *amax;
@@ -294,6 +295,7 @@ struct mp_dev {
     float *xqb = nullptr;  // Q8 mode: q_net output [NB][128]
     unsigned short *h_b16 = nullptr;  // bf16 mode: GELU(FFN up) as the bf16 FFN-down operand [NB][3072]
     float *gpart = nullptr;            // preamble split-K partial sums (mp::gemm_splits)
+    int *gctr = nullptr;               // their per-tile arrival counters (GemmP::ctr), zero between GEMMs
     hipEvent_t sev[2] = {nullptr, nullptr};  // streaming: the two chunk snapshots landed
     int32_t *h_codes = nullptr;              // streaming: pinned host mirror of codes_out [NB][S][8] + snapshots
     size_t h_codes_n = 0;
@@ -306,7 +308,7 @@ struct mp_dev {
     float *kc = nullptr, *vc = nullptr, *xak = nullptr, *xav = nullptr;
     float *lt_s = nullptr, *ltX = nullptr, *ltY = nullptr, *lty2 = nullptr, *ltq = nullptr, *ltk = nullptr,
           *ltv = nullptr, *ltf = nullptr, *logits = nullptr, *trace = nullptr, *ltp = nullptr;
-    unsigned long long *ltgh = nullptr, *ltfg = nullptr, *ltyg = nullptr;
+    unsigned long long *ltgh = nullptr, *ltfg = nullptr, *ltyg = nullptr, *ltcand = nullptr;
     int *T = nullptr, *spk = nullptr, *pos = nullptr, *step = nullptr, *done = nullptr, *nframes = nullptr,
         *ndone = nullptr, *codes_cur = nullptr, *codes_prev = nullptr, *codes_out = nullptr, *tok = nullptr,
         *argeos = nullptr, *amax = nullptr;
@@ -935,6 +937,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
     A(ltp, (size_t)NB * std::max({mp::LT_FFN_P, mp::LTS_P, mp::LTQ_P}) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, 2 * 256); A(ltyg, (size_t)NB * 256);
+    A(ltcand, 256);  // zeroed: slots past the head's workgroups + EOS slot stay 0
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
     A(argeos, NB); A(amax, NB * 8); A(smpcfg, 1);
@@ -948,6 +951,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
         auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits(K) * M * N); };
         need(Mc, 2304, 768); need(Mc, 3072, 768); need(Mc, 768, 3072); need(Mc, 768, 768);
         A(gpart, cap);
+        A(gctr, mp::PRE_CTR_TILES);
     }
     if (const char *qd = getenv("MAGPIE_Q8DUMP"); qd && atoi(qd) != 0 && dev->m.weight_mode == MP_WEIGHTS_Q8) {
         // the largest launch: K = 768, N = 2304 (QKV): rows, blocks, d, dots
@@ -979,6 +983,7 @@ mp::GemvP gemv_base(mp_dev *dev) {
 
 int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vector<mp::OpRec> *ops);
 bool q8_unfused();
+bool lt_cand_mode();
 
 // Enqueue one decode iteration: decoder step at pos (embedding codes_prev), LT
 // over 8 codebooks, finalize. When `record` is set, the op list is rebuilt for
@@ -1168,6 +1173,7 @@ int enqueue_iteration_body(mp_dev *dev, hipStream_t s, bool record) {
     io.lt_s = dev->lt_s; io.ltX = dev->ltX; io.ltY = dev->ltY; io.lty2 = dev->lty2; io.ltq = dev->ltq;
     io.ltk = dev->ltk; io.ltv = dev->ltv; io.ltf = dev->ltf; io.logits = dev->logits; io.ltp = dev->ltp;
     io.ltgh = dev->ltgh; io.ltfg = dev->ltfg; io.ltyg = dev->ltyg; io.iter = dev->ndone + 1; io.hx_err = dev->ndone + 2;
+    io.ltcand = lt_cand_mode() ? dev->ltcand : nullptr;
     io.codes_cur = dev->codes_cur; io.codes_prev = dev->codes_prev; io.codes_out = dev->codes_out; io.step = dev->step;
     io.pos = dev->pos; io.done = dev->done; io.nframes = dev->nframes; io.ndone = dev->ndone; io.argeos = dev->argeos;
     io.amax = dev->amax; io.cfg = dev->smpcfg;
@@ -1188,6 +1194,13 @@ bool eager_mode() {
 }
 // MAGPIE_Q8_UNFUSED=1: the Q8_0 mode's SA and XA as separate launches (the fused forms
 // compute the same bits; tests/test_q8_fused_gpu.py compares them)
+// MAGPIE_LT_CAND (f32 batch 1, greedy): 1 (default) = the LT head publishes a masked
+// first-max candidate per workgroup and the next LT step picks from those (GemvP::cand);
+// 0 = the step scans the head's 2024 logits. Both pick the same code.
+bool lt_cand_mode() {
+    const char *e = getenv("MAGPIE_LT_CAND");
+    return !(e && atoi(e) == 0);
+}
 bool q8_unfused() {
     const char *e = getenv("MAGPIE_Q8_UNFUSED");
     return e && atoi(e) != 0;
@@ -1349,6 +1362,9 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             l2.codes_cur = io.codes_cur; l2.step = io.step; l2.ignore_eos = io.ignore_eos;
             l2.audio_bos = m.audio_bos; l2.audio_eos = m.audio_eos;
             l2.smp = mp::Sampling{io.sampling, io.cfg, io.argeos, io.amax};
+            // greedy batch 1: the pick from the previous head's workgroup candidates
+            const bool cand = NB == 1 && !io.sampling && io.ltcand && !io.lt_only;
+            if (cand && cb > 0) { l2.cand = io.ltcand; l2.ncand = (2024 + 4 * MP_RW_LTE - 1) / (4 * MP_RW_LTE); }
             if (front && cb == 0) {
                 mp::LtFrontP fp{};
                 fp.l = l2; fp.x = io.x; fp.norm_out = m.dec_norm_out; fp.w_in = m.lt_in_w; fp.b_in = m.lt_in_b;
@@ -1391,6 +1407,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
             if (NB == 1) {  // the FFN merge is the head's prologue
                 g.part = io.ltp; g.addsrc = io.ltY;
                 efn = mp::op_lt_em_1;
+                if (cand && cb < 7) g.cand = io.ltcand;  // (codebook 7's code is the finalize's pick)
             }
             if ((rc = run("lt_e", efn, g, A * (2024.0 * 256) + A * 2024 + A * act * ((256 + 2024)))) != MP_OK)
                 return rc;
@@ -1564,6 +1581,7 @@ struct EncWs {
     const int32_t *tok, *T;  // device [NB][Tmax] token ids, [NB] lengths
     int NB, Tmax;
     float *pX, *pH, *pQKV, *pATT, *pF, *gpart, *enc_out;
+    int *gctr;  // split-K arrival counters (zeroed)
 };
 static size_t enc_gpart_elems(size_t Me) {
     size_t cap = 0;
@@ -1574,8 +1592,9 @@ static size_t enc_gpart_elems(size_t Me) {
 // every preamble GEMM runs split-K over K (deterministic, batch-invariant)
 // F16 file: every projection's operand rounded to f16 as ggml's F16 mul_mat does
 // (the K'/V' precompute is weight algebra, not a mul_mat of the file)
-static hipError_t preamble_gemm(const mp::Model &m, float *gpart, mp::GemmP gp, int epi, hipStream_t st) {
+static hipError_t preamble_gemm(const mp::Model &m, float *gpart, int *gctr, mp::GemmP gp, int epi, hipStream_t st) {
     gp.part = gpart;
+    gp.ctr = gctr;
     gp.xround = gp.xround < 0 ? 0 : (m.weight_mode == MP_WEIGHTS_F16 ? 2 : 0);  // -1: opted out
     return mp::pre_gemm(gp, epi, st);
 }
@@ -1584,7 +1603,7 @@ static int run_encoder(mp_dev *dev, const EncWs &w, hipStream_t s) {
     using namespace mp;
     const Model &m = dev->m;
     const int Tmax = w.Tmax, Me = w.NB * Tmax;
-    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, w.gpart, gp, epi, st); };
+    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, w.gpart, w.gctr, gp, epi, st); };
     HIPCHK(pre_embed_text(w.tok, w.T, w.NB, Tmax, m.text_emb, m.enc_pos, w.pX, s));
     for (int l = 0; l < m.enc_layers; ++l) {
         const EncLayerW &W = m.enc[l];
@@ -1622,9 +1641,10 @@ int run_preamble(mp_dev *dev) {
     const int NB = dev->NB, Tmax = dev->Tmax, L = m.dec_layers;
     hipStream_t s = dev->stream;
     const int Me = NB * Tmax;
-    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, dev->gpart, gp, epi, st); };
+    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, dev->gpart, dev->gctr, gp, epi, st); };
     {
-        const EncWs w{dev->tok, dev->T, NB, Tmax, dev->pX, dev->pH, dev->pQKV, dev->pATT, dev->pF, dev->gpart, dev->enc_out};
+        const EncWs w{dev->tok, dev->T, NB, Tmax, dev->pX, dev->pH, dev->pQKV, dev->pATT, dev->pF, dev->gpart, dev->enc_out,
+                      dev->gctr};
         if (int rc = run_encoder(dev, w, s)) return rc;
     }
     // --- cross-attention K/V per layer (1663-1711)
@@ -1914,7 +1934,7 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
     HIPCHK(hipSetDevice(dev->device));
     const size_t M = (size_t)n_tokens, D = 768;
     const size_t nf = M * D * 4 + M * 3 * D + M * 3072 + enc_gpart_elems(M) + M * D;  // pX pH pATT enc_out | pQKV | pF | gpart
-    const size_t need = nf * 4 + 64 + M * 4;  // floats | T (64 B slot) | token ids
+    const size_t need = nf * 4 + 64 + M * 4 + (size_t)mp::PRE_CTR_TILES * 4;  // floats | T (64 B) | ids | counters
     if (dev->enc_ws_bytes < need) {
         // the old workspace may still be read by this stream's earlier encode: wait for it
         // (the stream only, not the device) before it goes
@@ -1923,6 +1943,7 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
         dev->enc_ws = nullptr;
         dev->enc_ws_bytes = 0;
         HIPCHK(hipMalloc(&dev->enc_ws, need));
+        HIPCHK(hipMemsetAsync(dev->enc_ws, 0, need, dev->stream));  // the split-K counters start at 0
         dev->enc_ws_bytes = need;
     }
     char *ws = dev->enc_ws;
@@ -1934,6 +1955,7 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
     int32_t *ti = (int32_t *)(ws + nf * 4 + 64);
     int32_t *Ti = (int32_t *)(ws + nf * 4);
     w.tok = ti; w.T = Ti;
+    w.gctr = (int *)(ws + nf * 4 + 64 + M * 4);
     HIPCHK(hipMemcpyAsync(ti, tokens, M * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemcpyAsync(Ti, &n_tokens, 4, hipMemcpyHostToDevice, dev->stream));
     if (int rc = run_encoder(dev, w, dev->stream)) {

@@ -900,6 +900,7 @@ struct orc_codec {
     rblock rb[5][3][3];
     float **owned;
     int n_owned;
+    int resinit;  // orc_codec_set_resinit
 };
 static const int k_chans[6] = {864, 432, 216, 108, 54, 27};
 static const int k_rates[5] = {8, 8, 4, 2, 2};
@@ -1011,7 +1012,15 @@ static void half_snake(const snake_t *s, const float *x, float *y, int C, int T)
 
 // magpie_codec_build_causal_conv1d (nano-codec.cpp:429-466): left pad (k-1)*dil.
 // f16=1: operands rounded to fp16 as ggml_conv_1d's F16 im2col does (A.7).
+// resid (nullable): the accumulators start at resid[o][t] instead of 0, so y = (resid + sum)
+// + b: the rounding order of this build's residual convs (MP_RESINIT, mp_codec.hip), the
+// oracle's codec "resinit" mode; the reference's is (sum + b) + resid (nano-codec.cpp:454-462,
+// 568-599), the default.
+static void causal_conv_r(const conv_t *cv, const float *x, float *y, int T, int dil, int f16, const float *resid);
 static void causal_conv(const conv_t *cv, const float *x, float *y, int T, int dil, int f16) {
+    causal_conv_r(cv, x, y, T, dil, f16, NULL);
+}
+static void causal_conv_r(const conv_t *cv, const float *x, float *y, int T, int dil, int f16, const float *resid) {
     const int Ci = cv->cin, Co = cv->cout, K = cv->k, pad = (K - 1) * dil;
     const float *w = f16 ? cv->wh : cv->w;
     const float *xs = x;
@@ -1027,7 +1036,10 @@ static void causal_conv(const conv_t *cv, const float *x, float *y, int T, int d
         float *accf = malloc(sizeof(float) * (size_t)T);
 #pragma omp for schedule(static)
         for (int o = 0; o < Co; ++o) {
-            if (g_acc64) memset(acc, 0, sizeof(double) * (size_t)T);
+            if (resid) {
+                const float *ro = resid + (size_t)o * T;
+                for (int t = 0; t < T; ++t) { acc[t] = ro[t]; accf[t] = ro[t]; }
+            } else if (g_acc64) memset(acc, 0, sizeof(double) * (size_t)T);
             else memset(accf, 0, sizeof(float) * (size_t)T);
             for (int i = 0; i < Ci; ++i) {
                 const float *xi = xs + (size_t)i * T;
@@ -1070,6 +1082,10 @@ static void conv_transpose(const float *w, const float *bias, const float *x, fl
         }
 }
 
+void orc_codec_set_resinit(orc_codec *c, int on) {
+    if (c) c->resinit = on != 0;
+}
+
 // magpie_codec_build_decoder (nano-codec.cpp:676-715) + magpie_codec_decode (758-845)
 int orc_codec_decode(orc_codec *c, const int32_t *codes, int F, float *audio, int f16) {
     if (!c || F <= 0) return -1;
@@ -1094,8 +1110,13 @@ int orc_codec_decode(orc_codec *c, const int32_t *codes, int F, float *audio, in
                 half_snake(&r->in_act, rb, h, C, T);
                 causal_conv(&r->in_conv, h, h2, T, k_dil[k], f16);
                 half_snake(&r->sk_act, h2, h, C, T);
-                causal_conv(&r->sk_conv, h, h2, T, 1, f16);
-                for (size_t e = 0; e < (size_t)C * T; ++e) rb[e] = rb[e] + h2[e];
+                if (c->resinit) {  // (x + sum) + b, this build's order
+                    causal_conv_r(&r->sk_conv, h, h2, T, 1, f16, rb);
+                    memcpy(rb, h2, sizeof(float) * (size_t)C * T);
+                } else {  // (sum + b) + x, the reference's
+                    causal_conv(&r->sk_conv, h, h2, T, 1, f16);
+                    for (size_t e = 0; e < (size_t)C * T; ++e) rb[e] = rb[e] + h2[e];
+                }
             }
             if (j == 0) memcpy(acc, rb, sizeof(float) * (size_t)C * T);
             else for (size_t e = 0; e < (size_t)C * T; ++e) acc[e] = acc[e] + rb[e];
@@ -1109,8 +1130,6 @@ int orc_codec_decode(orc_codec *c, const int32_t *codes, int F, float *audio, in
     return T;
 }
 
-// Unit-test entry: y[N] = ggml Q8_0 mul_mat of the raw GGUF Q8_0 blocks
-// (34 bytes per 32 weights, row-major [N][K]) with the activation x[K].
 int orc_q8_quantize_row(const float *x, int K, int8_t *q, float *d) {
     if (!x || !q || !d || K <= 0 || K % 32) return -1;
     quant_row_q8(x, K, q, d);
@@ -1130,6 +1149,8 @@ int orc_qblock_dots(const uint8_t *blocks, int type, int N, int K, const int8_t 
     return 0;
 }
 
+// Unit-test entry: y[N] = ggml Q8_0 mul_mat of the raw GGUF Q8_0 blocks
+// (34 bytes per 32 weights, row-major [N][K]) with the activation x[K].
 int orc_q8_matvec(const uint8_t *blocks, int N, int K, const float *x, float *y) {
     if (!blocks || !x || !y || N <= 0 || K <= 0 || K % 32) return -1;
     q8w_t w = {NULL, malloc((size_t)N * K), malloc(sizeof(float) * (size_t)N * (K / 32))};

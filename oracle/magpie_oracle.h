@@ -101,6 +101,10 @@ void orc_codec_free(orc_codec *c);
 // magpie_codec_decode (nano-codec.cpp:758-845). codes: [8][n_frames] cb-major.
 // f16_operands=1 rounds conv_1d operands to fp16 as ggml's F16 im2col does (A.7).
 int orc_codec_decode(orc_codec *c, const int32_t *codes, int n_frames, float *audio_out, int f16_operands);
+// Residual-conv rounding order: 0 (default) = the reference's (sum + b) + x
+// (nano-codec.cpp:454-462, 568-599); 1 = (x + sum) + b, the order this build's kernels use
+// (accumulators initialised with the residual, bias after; mp_codec.hip MP_RESINIT).
+void orc_codec_set_resinit(orc_codec *c, int on);
 // fsq_dequantize_cpu (nano-codec.cpp:721-752): latent [32][n_frames] (time fastest).
 void orc_fsq(const int32_t *codes, int n_frames, float *latent);
 

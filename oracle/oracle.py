@@ -48,6 +48,7 @@ def lib() -> ctypes.CDLL:
         L.orc_codec_load.argtypes = [ctypes.c_char_p]
         L.orc_codec_free.argtypes = [P]
         L.orc_codec_decode.argtypes = [P, P, I, P, I]
+        L.orc_codec_set_resinit.argtypes = [P, I]
         L.orc_fsq.argtypes = [P, I, P]
         L.orc_q8_matvec.argtypes = [P, I, I, P, P]
         L.orc_q8_quantize_row.argtypes = [P, I, P, P]
@@ -156,7 +157,10 @@ class Codec:
         if not self.h:
             raise RuntimeError(f"oracle: cannot load codec {path}")
 
-    def decode(self, codes_cb_major, f16_operands=True):
+    def decode(self, codes_cb_major, f16_operands=True, resinit=False):
+        """resinit: residual convs rounded as (x + sum) + b (this build's kernels) instead of
+        the reference's (sum + b) + x."""
+        lib().orc_codec_set_resinit(self.h, int(resinit))
         c = np.ascontiguousarray(codes_cb_major, np.int32)
         F = c.shape[1]
         out = np.zeros(F * 1024, np.float32)

@@ -40,7 +40,9 @@ Each function cites the reference lines it restates (/root/reference/src/...):
                         trimmed right by K - s), residual block (568-599), HiFiGAN block
                         dilations 1, 3, 5 (602-616), ResLayer mean of 3 (619-641), post conv + tanh
 
-usage: python tests/golden/make_indep.py   (writes tests/golden/indep_small.npz, indep_codec.npz)
+usage: python tests/golden/make_indep.py [--small-only]
+  (writes tests/golden/indep_small.npz, indep_codec.npz; then indep_codec32.npz, a full 32-frame
+  codec chunk, and indep_full.npz, 32 frames of Magpie-357M's 12-layer / 6-encoder-layer shape)
 """
 import os
 import sys
@@ -366,6 +368,11 @@ CASES = [  # (seed, T, speaker, max_steps)
     (11, 40, 3, 12),
 ]
 CODEC_CODES_SEED, CODEC_FRAMES = 5, 6
+# the shipped shape: Magpie-357M's 12 decoder / 6 encoder layers, 32 frames of
+# the bench's T = 64 prompt; and one full 32-frame codec chunk (the CLI's chunk,
+# magpie-tts.cpp:181-206)
+FULL_CASE = (1004, 64, 0, 32)  # the prompt seed whose 256 decisions have no near-tie (min margin 2.5e-3)
+CODEC32_SEED, CODEC32_FRAMES = 7, 32
 
 
 def main():
@@ -395,6 +402,25 @@ def main():
     audio = c.decode(codes)
     np.savez_compressed(os.path.join(HERE, "indep_codec.npz"), codes=codes, audio=audio)
     print(f"codec: {audio.size} samples, peak {np.abs(audio).max():.4f}")
+    if "--small-only" in sys.argv:
+        return
+    # one full 32-frame chunk, stored as f32 (the values are within f32 rounding of the f64
+    # restatement's; the bars are 1e-6 and up)
+    codes = np.random.default_rng(CODEC32_SEED).integers(0, 2016, (8, CODEC32_FRAMES)).astype(np.int32)
+    audio = c.decode(codes)
+    np.savez_compressed(os.path.join(HERE, "indep_codec32.npz"), codes=codes, audio=audio.astype(np.float32))
+    print(f"codec 32-frame chunk: {audio.size} samples, peak {np.abs(audio).max():.4f}")
+    del c
+    # Magpie-357M (12 / 6 layers), the bench's prompt: codes, margins and the hidden state after
+    # every step (f32), 32 frames
+    fpath = ma.synth_gguf(os.path.join(cache, "magpie_357m_f32_k32.gguf"), lt_head_scale=ma.DECISIVE)
+    m = Magpie(fpath)
+    seed, T, spk, steps = FULL_CASE
+    tok = ma.synthetic_tokens(T, seed=seed)
+    r = m.synthesize(tok, spk, steps)
+    np.savez_compressed(os.path.join(HERE, "indep_full.npz"), tokens=tok, meta=np.array([spk, steps], np.int32),
+                        codes=r["codes"], hidden=r["hidden"].astype(np.float32), margins=r["margins"])
+    print(f"Magpie-357M: {len(r['codes'])} frames, min margin {r['margins'].min():.4f}")
 
 
 if __name__ == "__main__":

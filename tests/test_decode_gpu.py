@@ -685,3 +685,39 @@ def test_moved_special_ids_sampled_and_eos(ma, oracle, moved_ids_model, moved_id
         assert oe["n_frames"] == 4 and re_.n_frames[0] == 4, (temp, oe["n_frames"], re_.n_frames[0])
         # default (near-flat) heads here: a genuine near-tie may end the comparison early
         compare_codes(re_.codes[0], oe["codes"], oe["margins"], min_frames=0)
+
+
+@pytest.mark.parametrize("which", ["decisive", "default_heads", "moved_ids", "moved_ids_eos", "eos"])
+def test_lt_head_candidates_equal_logit_scan(ma, oracle, request, which):
+    """f32 batch 1, greedy: the LT step picks codebook c-1's code from the head's ~253
+    workgroup candidates (each head workgroup's masked first-max as an ordered key, EOS in
+    its own slot, dropped while step < 4 or ignore_eos; MAGPIE_LT_CAND=1, the default)
+    instead of scanning the 2024 logits (MAGPIE_LT_CAND=0). Same codes and hidden states
+    bit for bit, and equal to the oracle, with the reference's special ids, with the ids
+    moved (the general mask), near-flat heads (many near-ties) and EOS live."""
+    import os
+    path = {"decisive": "small_model", "default_heads": "full_model_default_heads", "moved_ids": "moved_ids_model",
+            "moved_ids_eos": "moved_ids_eos_model", "eos": "eos_model"}[which]
+    path = request.getfixturevalue(path)
+    ignore = which in ("decisive", "default_heads", "moved_ids")
+    steps = 24 if which == "default_heads" else 40
+    tok = ma.synthetic_tokens(20, seed=2300)
+    runs = {}
+    for mode in ("0", "1"):
+        os.environ["MAGPIE_LT_CAND"] = mode
+        try:
+            dev = ma.Device(path)
+            runs[mode] = dev.synthesize([tok], speakers=[1], max_dec_steps=steps, ignore_eos=ignore, trace=True)
+            dev.close()
+        finally:
+            os.environ.pop("MAGPIE_LT_CAND", None)
+    a, b = runs["0"], runs["1"]
+    assert int(a.n_frames[0]) == int(b.n_frames[0])
+    np.testing.assert_array_equal(a.codes[0], b.codes[0])
+    n = int(b.n_frames[0])
+    assert np.array_equal(a.hidden[0, :n + 1], b.hidden[0, :n + 1])
+    om = oracle.Model(path)
+    o = om.synthesize(tok, speaker=1, max_steps=steps, ignore_eos=ignore, trace=True)
+    om.close()
+    compare_codes(b.codes[0], o["codes"], o["margins"], min_frames=min(len(o["codes"]), 4))
+    print(f"{which}: {n} frames, candidate pick == logit scan bit for bit")

@@ -62,3 +62,36 @@ def test_gpu_codec_matches_independent_restatement(ma, codec_model):
     print(f"codec: {ref.size} samples, max abs err {err:.2e}, relative L2 {rel:.2e} vs the f64 restatement")
     assert g.shape == ref.shape
     assert err < 1e-2 and rel < 1e-2
+
+
+def test_gpu_full_shape_matches_independent_restatement(ma, full_model):
+    """Magpie-357M's shape (12 / 6 layers), the bench's T = 64 prompt, 32 frames on the bench's
+    f32 batch-1 path: codes identical to the f64 restatement, hidden within the f32 bar."""
+    d = np.load(os.path.join(GOLD, "indep_full.npz"))
+    spk, steps = (int(v) for v in d["meta"])
+    dev = ma.Device(full_model)
+    try:
+        r = dev.synthesize([d["tokens"]], speakers=[spk], max_dec_steps=steps, ignore_eos=False, trace=True)
+    finally:
+        dev.close()
+    ref_codes, ref_hidden = d["codes"], d["hidden"].astype(np.float64)
+    assert int(r.n_frames[0]) == len(ref_codes) == 32
+    np.testing.assert_array_equal(r.codes[0], ref_codes)
+    err = np.abs(r.hidden[0, :len(ref_hidden)].astype(np.float64) - ref_hidden).max()
+    print(f"Magpie-357M: 32 frames identical to the f64 restatement, hidden max abs err {err:.2e}")
+    assert err < 2e-5
+
+
+def test_gpu_codec_32_frame_chunk_matches_independent_restatement(ma, codec_model):
+    d = np.load(os.path.join(GOLD, "indep_codec32.npz"))
+    c = ma.Codec(codec_model)
+    try:
+        g = c.decode_chunks(d["codes"][None]).astype(np.float64)[0]
+    finally:
+        c.close()
+    ref = d["audio"].astype(np.float64)
+    err = np.abs(g - ref).max()
+    rel = np.linalg.norm(g - ref) / np.linalg.norm(ref)
+    print(f"codec 32-frame chunk: {ref.size} samples, max abs err {err:.2e}, relative L2 {rel:.2e}")
+    assert g.shape == ref.shape
+    assert err < 1e-2 and rel < 1e-2

@@ -477,3 +477,20 @@ def test_bf16_mode_spread_full_model_256(oracle, full_model):
     from test_long_range_gpu import BF16_LONG_TIE_EPS
     assert 3e-2 < shift < BF16_LONG_TIE_EPS, shift
     assert all(x < BF16_LONG_TIE_EPS for x in flipped), flipped
+
+
+def test_codec_resinit_order_is_rounding_only(codec_model, oracle):
+    """The oracle's resinit mode ((x + sum) + b, this build's residual-conv order) against the
+    reference's (sum + b) + x on the same codes: a rounding-level difference only."""
+    codes = np.random.default_rng(13).integers(0, 2016, (8, 4)).astype(np.int32)
+    c = oracle.Codec(codec_model)
+    try:
+        a = c.decode(codes, f16_operands=False, resinit=False)
+        b = c.decode(codes, f16_operands=False, resinit=True)
+        a2 = c.decode(codes, f16_operands=False, resinit=False)
+    finally:
+        c.close()
+    assert np.array_equal(a, a2)  # the mode is per call, not sticky
+    d = np.abs(a - b).max()
+    print(f"resinit vs reference order: max abs {d:.2e}")
+    assert 0 < d < 1e-5 or d == 0

@@ -95,6 +95,25 @@ for STEP in "$@"; do
       [ -n "$arg" ] && env=(MAGPIE_LIB="$PWD/ab_libs/$arg.so")
       env "${env[@]}" timeout -k 10 200 python -u tools_dev/codec_rb_timeline.py > "$OUT/${TAG}_ctl${arg:+_$arg}.txt" 2>&1
       cat "$OUT/${TAG}_ctl${arg:+_$arg}.txt" ;;
+    abkv)
+      # alternating env A/B, f32 B=1: abkv=N:K=V[,K=V...]|K=V...   ('|' separates the settings)
+      n=${arg%%:*}; rest=${arg#*:}
+      IFS='|' read -r -a sets <<< "$rest"
+      for k in "${!sets[@]}"; do sets[$k]=$(echo "${sets[$k]}" | tr ',' ' '); done
+      bash tools_dev/ab_kv.sh "${TAG}_abkv" "$n" "${sets[@]}" > "$OUT/${TAG}_abkv.txt" 2>&1
+      cat "$OUT/${TAG}_abkv.txt" ;;
+    pre)
+      # per-kernel time of one preamble (tools_dev/preamble_prof.py); arg: weights:B:T[:LIB]
+      IFS=: read -r w b t lib <<< "${arg:-f32:1:64}"
+      d="$OUT/${TAG}_pre_${w}_b${b}${lib:+_$lib}"
+      MAGPIE_EAGER=0 MAGPIE_LIB="${lib:+$PWD/ab_libs/$lib.so}" timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$d" -o prof \
+        -- python3 -u tools_dev/preamble_prof.py "$w" "$b" "$t" 3 > "$d.log" 2>&1
+      python3 tools_dev/preamble_report.py "$d/prof_kernel_trace.csv" 3 > "$d.txt"
+      head -1 "$d.txt"; grep "wall ms" "$d.log" ;;
+    prewall)
+      # preamble wall time without the profiler: arg weights:B:T[:LIB]
+      IFS=: read -r w b t lib <<< "${arg:-f32:1:64}"
+      MAGPIE_LIB="${lib:+$PWD/ab_libs/$lib.so}" timeout -k 10 200 python3 -u tools_dev/preamble_prof.py "$w" "$b" "$t" 10 ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

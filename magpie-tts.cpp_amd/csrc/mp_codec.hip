@@ -1553,7 +1553,9 @@ int mp_hip_codec_init(int device, const char *path, mp_codec **out) {
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return MP_ERR_HIP;
     mp_codec *c = new mp_codec();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    int least = 0, greatest = 0;  // the codec's stream at the least priority (see mp_hip_init)
+    if (hipSetDevice(device) != hipSuccess || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, least) != hipSuccess) {
         delete c;
         return MP_ERR_HIP;
     }

@@ -1742,7 +1742,12 @@ int mp_hip_init(int device, mp_dev **out) {
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return MP_ERR_HIP;
     mp_dev *dev = new mp_dev();
     dev->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
+    // the decode stream at the device's greatest priority: when the codec runs beside it (the
+    // streaming loop, configs[2]'s overlapped chunks) the dispatcher serves the latency-bound
+    // frame loop's workgroups first and the codec (least priority, mp_hip_codec_init) fills in
+    int least = 0, greatest = 0;
+    if (hipSetDevice(device) != hipSuccess || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&dev->stream, hipStreamNonBlocking, greatest) != hipSuccess ||
         hipHostMalloc((void **)&dev->h_ndone, 64, 0) != hipSuccess) {
         delete dev;
         return MP_ERR_HIP;

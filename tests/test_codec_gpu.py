@@ -86,9 +86,11 @@ def test_fused_blocks_equal_two_launch_blocks(gpu_codec, monkeypatch, F):
 def test_codec_matches_oracle_resinit_order(gpu_codec, cpu_codec):
     """This build's residual convs round as (x + sum) + b (accumulators initialised with the
     residual, MP_RESINIT); the reference's order is (sum + b) + x (nano-codec.cpp:454-462,
-    568-599). The oracle's resinit mode restates the build's order: both bars hold against
-    both orders, and the two orders differ only at f32 rounding (printed), so the 2e-3
-    waveform bar is not what absorbs the reordering."""
+    568-599). The oracle's resinit mode restates the build's order. With plain f32 operands the
+    two orders differ at f32 rounding (3e-7, tests/test_oracle_cpu.py); with ggml's f16 im2col
+    operands every ulp moved in a residual can move the next conv's f16 operand, and the two
+    orders differ by 3.8e-4 on this chunk (measured): the GPU must be as close to the order it
+    computes as to the reference's, both inside the 2e-3 bar (measured 3.7e-4 and 4.3e-4)."""
     codes = np.random.default_rng(7).integers(0, 2016, (8, 32)).astype(np.int32)
     g = gpu_codec.decode(codes)
     o_ref = cpu_codec.decode(codes, f16_operands=True, resinit=False)
@@ -97,4 +99,5 @@ def test_codec_matches_oracle_resinit_order(gpu_codec, cpu_codec):
     d = np.abs(o_ref - o_res).max()
     print(f"GPU vs oracle: reference order {e_ref:.2e}, resinit order {e_res:.2e}; the two orders differ by {d:.2e}")
     assert e_ref < WAVE_TOL and e_res < WAVE_TOL
-    assert d < 1e-4
+    assert e_res <= e_ref * 1.05
+    assert d < 1e-3

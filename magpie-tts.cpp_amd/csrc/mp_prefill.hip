@@ -18,6 +18,10 @@
 #include "mp_params.hpp"
 #include "mp_prefill_api.hpp"
 
+#ifndef MP_PRE_PF
+#define MP_PRE_PF 8  // K steps of operand loads in flight per thread (A/B: round 5 had 4)
+#endif
+
 namespace mp {
 
 // Epilogue of output (m, n) (bias, residual, GELU, KV-cache scatter, XA K/V split).
@@ -57,38 +61,31 @@ __device__ __forceinline__ void gemm_store(const GemmP &p, const float (&acc)[4]
     }
 }
 
-// Split-K reduction inside the GEMM launch (GemmP::ctr): every split of a 64 x 64 output
-// tile publishes its partial tile, then counts itself in; the last to arrive sums the
-// gridDim.z partials of the tile in split order and applies the epilogue - exactly
-// gemm_reduce_kernel's arithmetic, without its launch (one per split GEMM, ~100 per
-// preamble). The release fence makes the partial stores visible device-wide (every XCD's
-// L2) before the count; the last arriver's acquire fence orders its partial loads after it.
-template <int EPI>
-__device__ __forceinline__ void gemm_tile_reduce(const GemmP &p, int m0, int n0) {
-    __shared__ int last;
-    const int tid = threadIdx.x;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the whole device (every XCD)
-    __syncthreads();
-    if (tid == 0) {
-        int *c = p.ctr + blockIdx.y * gridDim.x + blockIdx.x;
-        const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        last = prev == (int)gridDim.z - 1;
-        if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next GEMM
-    }
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+// Split-K reduction of a residual GEMM whose rows are normalised next (GemmP::ln_w, N = 768):
+// one workgroup per row, x = C + sum of the splits in order (gemm_reduce_kernel<GE_RESID>'s
+// arithmetic) stored to C, then LN(x) * ln_w into ln_out (ln_rows_kernel's: the same thread
+// layout and block statistics) - one launch where the preamble had two.
+__global__ __launch_bounds__(256) void gemm_reduce_ln_kernel(GemmP p, int splits) {
+    __shared__ float red[8];
+    const int m = blockIdx.x, tid = threadIdx.x;
     const size_t total = (size_t)p.M * p.N;
-    const int S = gridDim.z;
-#pragma unroll 4
-    for (int e = tid; e < 64 * 64; e += 256) {
-        const int m = m0 + e / 64, n = n0 + e % 64;
-        if (m >= p.M || n >= p.N) continue;
-        const size_t o = (size_t)m * p.N + n;
-        float v = p.part[o];
-        for (int s = 1; s < S; ++s) v += p.part[(size_t)s * total + o];
-        gemm_store1<EPI>(p, m, n, v);
+    float v[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int n = tid + 256 * i;
+        const size_t e = (size_t)m * p.N + n;
+        float a = p.part[e];
+        for (int s = 1; s < splits; ++s) a += p.part[(size_t)s * total + e];
+        if (p.bias) a += p.bias[n];
+        const float x = a + p.C[(size_t)m * p.ldc + n];
+        p.C[(size_t)m * p.ldc + n] = x;
+        v[i] = x;
     }
+    float mean, var;
+    block_meanvar<3>(v, red, mean, var);
+    const float rstd = 1.0f / sqrtf(var + p.ln_eps);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p.ln_out[(size_t)m * p.ln_ld + tid + 256 * i] = ((v[i] - mean) * rstd) * p.ln_w[tid + 256 * i];
 }
 
 // Split-K reduction: v = sum of the splits in order, then the epilogue.
@@ -109,7 +106,7 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmP p, int splits) {
 // LDS-tiled GEMM's.
 template <int EPI, int TAPS>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
-    constexpr int BM = 64, BN = 64, BK = 16, PF = 8;
+    constexpr int BM = 64, BN = 64, BK = 16, PF = MP_PRE_PF;
     __shared__ float As[BK][BM + 4];
     __shared__ float Ws[BK][BN + 4];
     const int tid = threadIdx.x;
@@ -182,7 +179,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
 // 4 (l >> 4) + i, column l & 15.
 template <int EPI, int TAPS>
 __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
-    constexpr int BM = 64, BN = 64, BK = 16, PF = 8;
+    constexpr int BM = 64, BN = 64, BK = 16, PF = MP_PRE_PF;
     typedef float f4v __attribute__((ext_vector_type(4)));
     __shared__ float As[BK][BM + 4];
     __shared__ float Ws[BK][BN + 4];
@@ -194,9 +191,15 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    f4v tot[2][2];
     const int lr = tid >> 2, lk = (tid & 3) * 4;  // loader: row lr, k lk..lk+3
+    // split-K: one split per blockIdx.z (gridDim.z == nsplit: partials, summed after), or
+    // (large grids, gridDim.z == 1 < nsplit) every split of the tile here in turn, each its
+    // own chain from 0, folded into tot in split order: tot = p0, tot += p1, ... - the same
+    // float operations as the reduction of the partials, without writing them
     const int ks = p.K / gridDim.z, kbeg = blockIdx.z * ks;
     const int nsteps = ks / BK;
+    const int sl = (gridDim.z == 1 && p.nsplit > 1) ? (p.K / p.nsplit) / BK : nsteps;  // steps per split
     const int m = m0 + lr, n = n0 + lr;
     auto load_a = [&](int k0) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -246,6 +249,15 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
                     for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
             }
             __syncthreads();
+            if ((step + 1) % sl == 0) {  // a split's chain is complete: fold it in, split order
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        tot[i][j] = step + 1 == sl ? acc[i][j] : tot[i][j] + acc[i][j];
+                        acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+                    }
+            }
         }
     }
 #pragma unroll
@@ -258,11 +270,10 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
             for (int r = 0; r < 4; ++r) {
                 const int mm = m0 + rq + 16 * i + 4 * fk + r;
                 if (mm >= p.M) continue;
-                if (p.part) p.part[((size_t)blockIdx.z * p.M + mm) * p.N + nn] = acc[i][j][r];
-                else gemm_store1<EPI>(p, mm, nn, acc[i][j][r]);
+                if (p.part) p.part[((size_t)blockIdx.z * p.M + mm) * p.N + nn] = tot[i][j][r];
+                else gemm_store1<EPI>(p, mm, nn, tot[i][j][r]);
             }
         }
-    if (p.part && p.ctr) gemm_tile_reduce<EPI>(p, m0, n0);
 }
 
 // Q8_0 weights (weight mode MP_WEIGHTS_Q8): ggml's quantised mul_mat. Every K
@@ -410,109 +421,6 @@ __global__ __launch_bounds__(256) void row_attn_kernel(RowAttnP p) {
     p.O[(size_t)m * D + h * DH + lane] = o / l;
 }
 
-// The same causal attention, tiled: workgroup (query block of 64 rows, head, utterance).
-// Keys are staged 64 at a time into LDS (coalesced row loads; bf16 cache rows widened)
-// and every wave runs an online softmax for 16 query rows: lane (row r = lane / 4,
-// quarter qq = lane % 4) scores keys 16 qq .. 16 qq + 15 of the tile against its row's
-// whole q (64 registers), the row's 4 lanes meet through DPP for the max and the sum, the
-// probabilities go through LDS, and the lane accumulates output dims 16 qq .. 16 qq + 15.
-// One workgroup per 64 rows and head replaces row_attn_kernel's wave per (row, head),
-// whose key loop made one dependent global round trip per 64 keys and its value loop
-// one per key.
-constexpr int RA_QB = 64, RA_KT = 64;
-template <bool KV16>
-__global__ __launch_bounds__(256) void row_attn_tile_kernel(RowAttnP p) {
-    __shared__ __attribute__((aligned(16))) float Ks[RA_KT][DH + 4];
-    __shared__ __attribute__((aligned(16))) float Vs[RA_KT][DH + 4];
-    __shared__ __attribute__((aligned(16))) float Ps[4][16][RA_KT + 4];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int t0 = blockIdx.x * RA_QB, h = blockIdx.y, b = blockIdx.z;
-    const int R = p.rows_per_utt;
-    const int r = lane >> 2, qq = lane & 3;
-    const int t = t0 + 16 * w + r;  // this lane's query row (position in the utterance)
-    const bool live = t < R;
-    const int m = b * R + (live ? t : R - 1);
-    float q[DH];
-    {
-        const float *qp = p.Q + (size_t)m * p.ldq + h * DH;
-#pragma unroll
-        for (int d = 0; d < DH; d += 4) {
-            const float4 v = *(const float4 *)(qp + d);
-            q[d] = v.x; q[d + 1] = v.y; q[d + 2] = v.z; q[d + 3] = v.w;
-        }
-    }
-    float o[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) o[e] = 0.f;
-    float mx = -INFINITY, l = 0.f;
-    const int t_last = min(t0 + RA_QB, R) - 1;  // the block's last row: keys 0 .. t_last
-    const size_t kb0 = b * p.utt_stride + h * DH;
-    for (int j0 = 0; j0 <= t_last; j0 += RA_KT) {
-        // stage keys j0 .. j0 + 63: thread (key kr = tid / 4, 16 dims 16 (tid % 4))
-        {
-            const int kr = tid >> 2, dq = (tid & 3) * 16;
-            const int j = min(j0 + kr, t_last);
-            const size_t k = kb0 + (size_t)j * p.row_stride + dq;
-#pragma unroll
-            for (int d = 0; d < 16; d += 4) {
-                *(float4 *)&Ks[kr][dq + d] = kv_load4<KV16>(p.Kb, k + d);
-                *(float4 *)&Vs[kr][dq + d] = kv_load4<KV16>(p.Vb, k + d);
-            }
-        }
-        __syncthreads();
-        float sc[16];
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            const int kr = 16 * qq + jj;
-            float sv = 0.f;
-#pragma unroll
-            for (int d = 0; d < DH; d += 4) {
-                const float4 k4 = *(const float4 *)&Ks[kr][d];
-                sv += q[d] * k4.x + q[d + 1] * k4.y + q[d + 2] * k4.z + q[d + 3] * k4.w;
-            }
-            sv = j0 + kr <= t ? sv * 0.125f : -INFINITY;
-            sc[jj] = sv;
-            tmax = fmaxf(tmax, sv);
-        }
-        tmax = fmaxf(tmax, dpp_mov<0xB1>(tmax));  // the row's 4 lanes (a DPP quad)
-        tmax = fmaxf(tmax, dpp_mov<0x4E>(tmax));
-        const float mnew = fmaxf(mx, tmax);  // finite: key 0 .. t of every tile j0 <= t
-        const float corr = mx == -INFINITY ? 0.f : expf(mx - mnew);
-        float ls = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            const float e = sc[jj] == -INFINITY ? 0.f : expf(sc[jj] - mnew);
-            ls += e;
-            Ps[w][r][16 * qq + jj] = e;
-        }
-        ls += dpp_mov<0xB1>(ls);
-        ls += dpp_mov<0x4E>(ls);
-        l = l * corr + ls;
-        mx = mnew;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row's probabilities are in LDS
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[e] *= corr;
-        const int jn = min(RA_KT, t_last - j0 + 1);
-        for (int kr = 0; kr < jn; ++kr) {
-            const float pj = Ps[w][r][kr];
-#pragma unroll
-            for (int e = 0; e < 16; e += 4) {
-                const float4 v4 = *(const float4 *)&Vs[kr][16 * qq + e];
-                o[e] += pj * v4.x; o[e + 1] += pj * v4.y; o[e + 2] += pj * v4.z; o[e + 3] += pj * v4.w;
-            }
-        }
-        __syncthreads();  // the tile's K / V rows are read by every wave before the next stage
-    }
-    if (!live) return;
-    const float il = 1.0f / l;
-    float *op = p.O + (size_t)m * D + h * DH + 16 * qq;
-#pragma unroll
-    for (int e = 0; e < 16; e += 4) *(float4 *)(op + e) = make_float4(o[e] * il, o[e + 1] * il, o[e + 2] * il, o[e + 3] * il);
-}
-
 // Cross-attention for a block of rows: 1 head x 128 over the utterance's T[b]
 // text positions (no mask).
 
@@ -604,12 +512,26 @@ static bool gemm_mfma() {
     const char *e = getenv("MAGPIE_PRE_VALU");
     return !(e && *e == '1');
 }
+// GemmP::ln_w: the rows this GEMM completes are normalised next (LN(C) * ln_w -> ln_out):
+// in the split reduction when there is one (gemm_reduce_ln_kernel), else as ln_rows_kernel
+static hipError_t launch_ln_after(const GemmP &p, hipStream_t s) {
+    if (!p.ln_w) return hipSuccess;
+    hipLaunchKernelGGL(ln_rows_kernel, dim3(p.M), dim3(256), 0, s, p.C, p.ldc, p.ln_w, p.ln_out, p.ln_ld, p.ln_eps);
+    return hipGetLastError();
+}
 template <int EPI>
 static hipError_t launch_reduce(const GemmP &p, int splits, hipStream_t s) {
+    if constexpr (EPI == GE_RESID) {
+        if (p.ln_w && p.N == D) {
+            hipLaunchKernelGGL(gemm_reduce_ln_kernel, dim3(p.M), dim3(256), 0, s, p, splits);
+            return hipGetLastError();
+        }
+    }
     const size_t total = (size_t)p.M * p.N;
     const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3(grid), dim3(256), 0, s, p, splits);
-    return hipGetLastError();
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    return launch_ln_after(p, s);
 }
 template <int EPI, int TAPS>
 static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
@@ -619,10 +541,20 @@ static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
     GemmP q = p;
     if (splits == 1) q.part = nullptr;
     const bool mfma = gemm_mfma();
-    if (!mfma || grid.x * grid.y > PRE_CTR_TILES) q.ctr = nullptr;  // (the VALU kernel keeps the reduce launch)
+    q.nsplit = splits;
+    if (mfma && splits > 1 && grid.x * grid.y >= PRE_INWG_TILES) {
+        // enough output tiles to fill the chip: each workgroup runs its tile's splits in turn
+        // (no partial sums through memory: 0.1-0.2 GB per GEMM at 16 utterances)
+        grid.z = 1;
+        q.part = nullptr;
+        hipLaunchKernelGGL((gemm_f32_mfma_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        return launch_ln_after(p, s);
+    }
     if (mfma) hipLaunchKernelGGL((gemm_f32_mfma_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
     else hipLaunchKernelGGL((gemm_f32_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
-    if (hipError_t e = hipGetLastError(); e != hipSuccess || splits == 1 || q.ctr) return e;
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (splits == 1) return launch_ln_after(p, s);
     return launch_reduce<EPI>(p, splits, s);
 }
 template <int EPI>
@@ -633,7 +565,8 @@ static hipError_t launch_gemm_q8(const GemmP &p, hipStream_t s) {
     GemmP q = p;
     if (splits == 1) q.part = nullptr;
     hipLaunchKernelGGL((gemm_q8_kernel<EPI>), grid, dim3(256), 0, s, q);
-    if (hipError_t e = hipGetLastError(); e != hipSuccess || splits == 1) return e;
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (splits == 1) return launch_ln_after(p, s);
     return launch_reduce<EPI>(p, splits, s);
 }
 hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s) {
@@ -675,13 +608,6 @@ hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s)
     return hipGetLastError();
 }
 hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s) {
-    static const bool old = getenv("MAGPIE_PRE_ROWATTN_OLD") != nullptr;  // A/B: the wave-per-(row, head) kernel
-    if (!old && p.M % p.rows_per_utt == 0) {
-        const dim3 grid((p.rows_per_utt + RA_QB - 1) / RA_QB, p.heads, p.M / p.rows_per_utt);
-        if (p.kv16) hipLaunchKernelGGL(row_attn_tile_kernel<true>, grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL(row_attn_tile_kernel<false>, grid, dim3(256), 0, s, p);
-        return hipGetLastError();
-    }
     if (p.kv16) hipLaunchKernelGGL(row_attn_kernel<true>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(row_attn_kernel<false>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
     return hipGetLastError();

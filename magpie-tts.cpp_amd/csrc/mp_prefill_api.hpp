@@ -38,11 +38,13 @@ struct GemmP {
     // depend on M, i.e. on the batch), each written raw to part[s][M][N], then
     // summed in split order by a second launch that applies the epilogue.
     float *part;
-    // with part: the arrival counters of the output tiles ([grid.y][grid.x] ints, zero
-    // between GEMMs). When set, the MFMA kernel's last-arriving split of each tile sums
-    // the splits (the same order and epilogue as gemm_reduce_kernel) and zeroes the
-    // counter again: no second launch. Null: the separate reduce launch.
-    int *ctr;
+    int nsplit;        // gemm_splits(K), set by the launcher (the kernel's split length when gridDim.z == 1)
+    // optional: the rows of C this GEMM completes are normalised next, LN(C row) * ln_w ->
+    // ln_out[m * ln_ld] (N = 768; fused into the split reduction of a GE_RESID GEMM)
+    const float *ln_w;
+    float *ln_out;
+    int ln_ld;
+    float ln_eps;
     int xround;        // 2: round every A element to f16 as it is loaded (an F16 weight: ggml's
                        //    F16 mul_mat rounds src1 to f16; products then exact in f32)
 };
@@ -53,10 +55,14 @@ struct GemmP {
 // (gemm_f32_mfma_kernel's ring), so a workgroup pays one memory latency for its slice
 // instead of one per 4 steps (round 5: K / 96 pieces, at most 16: 576-wide slices of
 // the encoder's 9216-wide conv waited on memory 9 times).
-constexpr int PRE_KS = 128;
-constexpr int PRE_CTR_TILES = 4096;  // arrival counters per GEMM (GemmP::ctr): output tiles of 64 x 64
+#ifndef MP_PRE_KS
+#define MP_PRE_KS 128  // (A/B: 0 = round 5's K / 96 pieces, at most 16)
+#endif
+constexpr int PRE_KS = MP_PRE_KS;
+constexpr int PRE_CTR_TILES = 4096;
+constexpr int PRE_INWG_TILES = 256;  // output tiles from which a GEMM runs its splits inside each workgroup
 inline int gemm_splits(int K) {
-    if (K % PRE_KS == 0) return K / PRE_KS;
+    if (PRE_KS > 0 && K % PRE_KS == 0) return K / PRE_KS;
     int s = K / 96;  // (no model K takes this path)
     if (s < 1) s = 1;
     if (s > 16) s = 16;

@@ -295,7 +295,6 @@ struct mp_dev {
     float *xqb = nullptr;  // Q8 mode: q_net output [NB][128]
     unsigned short *h_b16 = nullptr;  // bf16 mode: GELU(FFN up) as the bf16 FFN-down operand [NB][3072]
     float *gpart = nullptr;            // preamble split-K partial sums (mp::gemm_splits)
-    int *gctr = nullptr;               // their per-tile arrival counters (GemmP::ctr), zero between GEMMs
     hipEvent_t sev[2] = {nullptr, nullptr};  // streaming: the two chunk snapshots landed
     int32_t *h_codes = nullptr;              // streaming: pinned host mirror of codes_out [NB][S][8] + snapshots
     size_t h_codes_n = 0;
@@ -951,7 +950,6 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
         auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits(K) * M * N); };
         need(Mc, 2304, 768); need(Mc, 3072, 768); need(Mc, 768, 3072); need(Mc, 768, 768);
         A(gpart, cap);
-        A(gctr, mp::PRE_CTR_TILES);
     }
     if (const char *qd = getenv("MAGPIE_Q8DUMP"); qd && atoi(qd) != 0 && dev->m.weight_mode == MP_WEIGHTS_Q8) {
         // the largest launch: K = 768, N = 2304 (QKV): rows, blocks, d, dots
@@ -1194,12 +1192,15 @@ bool eager_mode() {
 }
 // MAGPIE_Q8_UNFUSED=1: the Q8_0 mode's SA and XA as separate launches (the fused forms
 // compute the same bits; tests/test_q8_fused_gpu.py compares them)
-// MAGPIE_LT_CAND (f32 batch 1, greedy): 1 (default) = the LT head publishes a masked
-// first-max candidate per workgroup and the next LT step picks from those (GemvP::cand);
-// 0 = the step scans the head's 2024 logits. Both pick the same code.
+// MAGPIE_LT_CAND=1 (f32 batch 1, greedy): the LT head publishes a masked first-max
+// candidate per workgroup and the next LT step picks from those (GemvP::cand) instead of
+// scanning the head's 2024 logits. Both pick the same code (same bits). Off by default:
+// measured 1.6 % slower at f32 B=1 (2,985 vs 3,034 frames/s, three alternating pairs on one
+// box, profiles/r06b_ab_lt_cand.txt): the head's workgroup barrier and 64-bit reduction cost
+// more than the step saves, whose pick waits on the logits' memory round trip either way.
 bool lt_cand_mode() {
     const char *e = getenv("MAGPIE_LT_CAND");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) != 0;
 }
 bool q8_unfused() {
     const char *e = getenv("MAGPIE_Q8_UNFUSED");
@@ -1581,7 +1582,6 @@ struct EncWs {
     const int32_t *tok, *T;  // device [NB][Tmax] token ids, [NB] lengths
     int NB, Tmax;
     float *pX, *pH, *pQKV, *pATT, *pF, *gpart, *enc_out;
-    int *gctr;  // split-K arrival counters (zeroed)
 };
 static size_t enc_gpart_elems(size_t Me) {
     size_t cap = 0;
@@ -1592,9 +1592,9 @@ static size_t enc_gpart_elems(size_t Me) {
 // every preamble GEMM runs split-K over K (deterministic, batch-invariant)
 // F16 file: every projection's operand rounded to f16 as ggml's F16 mul_mat does
 // (the K'/V' precompute is weight algebra, not a mul_mat of the file)
-static hipError_t preamble_gemm(const mp::Model &m, float *gpart, int *gctr, mp::GemmP gp, int epi, hipStream_t st) {
+static hipError_t preamble_gemm(const mp::Model &m, float *gpart, mp::GemmP gp, int epi, hipStream_t st) {
     gp.part = gpart;
-    gp.ctr = gctr;
+    if (gp.ln_w) gp.ln_eps = m.eps;
     gp.xround = gp.xround < 0 ? 0 : (m.weight_mode == MP_WEIGHTS_F16 ? 2 : 0);  // -1: opted out
     return mp::pre_gemm(gp, epi, st);
 }
@@ -1603,11 +1603,13 @@ static int run_encoder(mp_dev *dev, const EncWs &w, hipStream_t s) {
     using namespace mp;
     const Model &m = dev->m;
     const int Tmax = w.Tmax, Me = w.NB * Tmax;
-    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, w.gpart, w.gctr, gp, epi, st); };
+    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, w.gpart, gp, epi, st); };
     HIPCHK(pre_embed_text(w.tok, w.T, w.NB, Tmax, m.text_emb, m.enc_pos, w.pX, s));
+    // the residual GEMMs (O-projection, FFN down) normalise the rows they complete for the
+    // next LayerNorm (GemmP::ln_w: fused into their split reduction)
+    HIPCHK(pre_ln_rows(w.pX, 768, m.enc[0].norm_self, w.pH, 768, Me, m.eps, s));
     for (int l = 0; l < m.enc_layers; ++l) {
         const EncLayerW &W = m.enc[l];
-        HIPCHK(pre_ln_rows(w.pX, 768, W.norm_self, w.pH, 768, Me, m.eps, s));
         GemmP gp{};
         gp.A = w.pH; gp.lda = 768; gp.W = W.qkv; gp.Wq = W.qkv8.q; gp.Wd = W.qkv8.d; gp.C = w.pQKV; gp.ldc = 2304; gp.M = Me; gp.N = 2304; gp.K = 768;
         gp.rows_per_utt = Tmax; gp.T = w.T;
@@ -1620,8 +1622,8 @@ static int run_encoder(mp_dev *dev, const EncWs &w, hipStream_t s) {
         gp = GemmP{};
         gp.A = w.pATT; gp.lda = 768; gp.W = W.o; gp.Wq = W.o8.q; gp.Wd = W.o8.d; gp.C = w.pX; gp.ldc = 768; gp.M = Me; gp.N = 768; gp.K = 768;
         gp.rows_per_utt = Tmax; gp.T = w.T;
+        gp.ln_w = W.norm_ff; gp.ln_out = w.pH; gp.ln_ld = 768;
         HIPCHK(pre_gemm(gp, GE_RESID, s));
-        HIPCHK(pre_ln_rows(w.pX, 768, W.norm_ff, w.pH, 768, Me, m.eps, s));
         gp = GemmP{};  // causal conv k=3 d_model -> d_ffn + GELU (1816-1869)
         gp.A = w.pH; gp.lda = 768; gp.W = W.ff1; gp.C = w.pF; gp.ldc = 3072; gp.M = Me; gp.N = 3072;
         gp.K = 768 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = w.T;
@@ -1629,9 +1631,11 @@ static int run_encoder(mp_dev *dev, const EncWs &w, hipStream_t s) {
         gp = GemmP{};  // causal conv k=3 d_ffn -> d_model + residual (1875-1916)
         gp.A = w.pF; gp.lda = 3072; gp.W = W.ff2; gp.C = w.pX; gp.ldc = 768; gp.M = Me; gp.N = 768;
         gp.K = 3072 * 3; gp.conv_taps = 3; gp.rows_per_utt = Tmax; gp.T = w.T;
+        if (l + 1 < m.enc_layers) { gp.ln_w = m.enc[l + 1].norm_self; gp.ln_out = w.pH; }
+        else { gp.ln_w = m.enc_norm_out; gp.ln_out = w.enc_out; }  // the encoder's final norm
+        gp.ln_ld = 768;
         HIPCHK(pre_gemm(gp, GE_RESID, s));
     }
-    HIPCHK(pre_ln_rows(w.pX, 768, m.enc_norm_out, w.enc_out, 768, Me, m.eps, s));
     return MP_OK;
 }
 
@@ -1641,10 +1645,9 @@ int run_preamble(mp_dev *dev) {
     const int NB = dev->NB, Tmax = dev->Tmax, L = m.dec_layers;
     hipStream_t s = dev->stream;
     const int Me = NB * Tmax;
-    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, dev->gpart, dev->gctr, gp, epi, st); };
+    auto pre_gemm = [&](GemmP gp, int epi, hipStream_t st) { return preamble_gemm(m, dev->gpart, gp, epi, st); };
     {
-        const EncWs w{dev->tok, dev->T, NB, Tmax, dev->pX, dev->pH, dev->pQKV, dev->pATT, dev->pF, dev->gpart, dev->enc_out,
-                      dev->gctr};
+        const EncWs w{dev->tok, dev->T, NB, Tmax, dev->pX, dev->pH, dev->pQKV, dev->pATT, dev->pF, dev->gpart, dev->enc_out};
         if (int rc = run_encoder(dev, w, s)) return rc;
     }
     // --- cross-attention K/V per layer (1663-1711)
@@ -1672,9 +1675,9 @@ int run_preamble(mp_dev *dev) {
     // --- baked context + 110-frame causal prefill (3991-4060, 4167-4238)
     const int Mc = NB * CTX;
     HIPCHK(pre_embed_context(dev->spk, NB, m.baked, m.dec_pos, dev->pX, s));
+    HIPCHK(pre_ln_rows(dev->pX, 768, m.dec[0].norm_self, dev->pH, 768, Mc, m.eps, s));
     for (int l = 0; l < L; ++l) {
         const DecLayerW &W = m.dec[l];
-        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_self, dev->pH, 768, Mc, m.eps, s));
         GemmP gp{};
         gp.A = dev->pH; gp.lda = 768; gp.W = W.qkv; gp.Wq = W.qkv8.q; gp.Wd = W.qkv8.d; gp.C = dev->pQKV; gp.ldc = 2304; gp.M = Mc; gp.N = 2304; gp.K = 768;
         gp.rows_per_utt = CTX; gp.kc = dev->kc; gp.vc = dev->vc; gp.kv16 = dev->kv16; gp.layer = l; gp.nlayers = L;
@@ -1693,8 +1696,8 @@ int run_preamble(mp_dev *dev) {
         gp = GemmP{};
         gp.A = dev->pATT; gp.lda = 768; gp.W = W.o; gp.Wq = W.o8.q; gp.Wd = W.o8.d; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 768;
         gp.rows_per_utt = CTX;
+        gp.ln_w = W.norm_xq; gp.ln_out = dev->pH; gp.ln_ld = 768;
         HIPCHK(pre_gemm(gp, GE_RESID, s));
-        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_xq, dev->pH, 768, Mc, m.eps, s));
         gp = GemmP{};
         gp.A = dev->pH; gp.lda = 768; gp.W = W.xq; gp.Wq = W.xq8.q; gp.Wd = W.xq8.d; gp.C = dev->pXQ; gp.ldc = 128; gp.M = Mc; gp.N = 128; gp.K = 768;
         gp.rows_per_utt = CTX;
@@ -1704,8 +1707,8 @@ int run_preamble(mp_dev *dev) {
         gp = GemmP{};
         gp.A = dev->pXAO; gp.lda = 128; gp.W = W.xo; gp.Wq = W.xo8.q; gp.Wd = W.xo8.d; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 128;
         gp.rows_per_utt = CTX;
+        gp.ln_w = W.norm_ff; gp.ln_out = dev->pH; gp.ln_ld = 768;
         HIPCHK(pre_gemm(gp, GE_RESID, s));
-        HIPCHK(pre_ln_rows(dev->pX, 768, W.norm_ff, dev->pH, 768, Mc, m.eps, s));
         gp = GemmP{};
         gp.A = dev->pH; gp.lda = 768; gp.W = W.ff1; gp.C = dev->pF; gp.ldc = 3072; gp.M = Mc; gp.N = 3072; gp.K = 768;
         gp.rows_per_utt = CTX;
@@ -1713,6 +1716,7 @@ int run_preamble(mp_dev *dev) {
         gp = GemmP{};
         gp.A = dev->pF; gp.lda = 3072; gp.W = W.ff2; gp.C = dev->pX; gp.ldc = 768; gp.M = Mc; gp.N = 768; gp.K = 3072;
         gp.rows_per_utt = CTX;
+        if (l + 1 < L) { gp.ln_w = m.dec[l + 1].norm_self; gp.ln_out = dev->pH; gp.ln_ld = 768; }
         HIPCHK(pre_gemm(gp, GE_RESID, s));
     }
     return MP_OK;
@@ -1939,7 +1943,7 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
     HIPCHK(hipSetDevice(dev->device));
     const size_t M = (size_t)n_tokens, D = 768;
     const size_t nf = M * D * 4 + M * 3 * D + M * 3072 + enc_gpart_elems(M) + M * D;  // pX pH pATT enc_out | pQKV | pF | gpart
-    const size_t need = nf * 4 + 64 + M * 4 + (size_t)mp::PRE_CTR_TILES * 4;  // floats | T (64 B) | ids | counters
+    const size_t need = nf * 4 + 64 + M * 4;  // floats | T (64 B slot) | token ids
     if (dev->enc_ws_bytes < need) {
         // the old workspace may still be read by this stream's earlier encode: wait for it
         // (the stream only, not the device) before it goes
@@ -1948,7 +1952,6 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
         dev->enc_ws = nullptr;
         dev->enc_ws_bytes = 0;
         HIPCHK(hipMalloc(&dev->enc_ws, need));
-        HIPCHK(hipMemsetAsync(dev->enc_ws, 0, need, dev->stream));  // the split-K counters start at 0
         dev->enc_ws_bytes = need;
     }
     char *ws = dev->enc_ws;
@@ -1960,7 +1963,6 @@ int mp_hip_encode_text(mp_dev *dev, const int32_t *tokens, int n_tokens, float *
     int32_t *ti = (int32_t *)(ws + nf * 4 + 64);
     int32_t *Ti = (int32_t *)(ws + nf * 4);
     w.tok = ti; w.T = Ti;
-    w.gctr = (int *)(ws + nf * 4 + 64 + M * 4);
     HIPCHK(hipMemcpyAsync(ti, tokens, M * 4, hipMemcpyHostToDevice, dev->stream));
     HIPCHK(hipMemcpyAsync(Ti, &n_tokens, 4, hipMemcpyHostToDevice, dev->stream));
     if (int rc = run_encoder(dev, w, dev->stream)) {

@@ -698,8 +698,8 @@ def test_moved_special_ids_sampled_and_eos(ma, oracle, moved_ids_model, moved_id
 def test_lt_head_candidates_equal_logit_scan(ma, oracle, request, which):
     """f32 batch 1, greedy: the LT step picks codebook c-1's code from the head's ~253
     workgroup candidates (each head workgroup's masked first-max as an ordered key, EOS in
-    its own slot, dropped while step < 4 or ignore_eos; MAGPIE_LT_CAND=1, the default)
-    instead of scanning the 2024 logits (MAGPIE_LT_CAND=0). Same codes and hidden states
+    its own slot, dropped while step < 4 or ignore_eos; MAGPIE_LT_CAND=1, opt-in: measured
+    slower) instead of scanning the 2024 logits (MAGPIE_LT_CAND=0, the default). Same codes and hidden states
     bit for bit, and equal to the oracle, with the reference's special ids, with the ids
     moved (the general mask), near-flat heads (many near-ties) and EOS live."""
     import os

@@ -1203,6 +1203,10 @@ struct mp_codec {
     int *codes = nullptr;
     size_t codes_cap = 0, audio_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // background decodes (mp_codec_set_background): a second stream confined to a share of the
+    // CUs (hipExtStreamCreateWithCUMask), for codec rounds that run beside a decode in flight
+    hipStream_t bg_stream = nullptr;
+    int bg = 0, bg_cus = 0;
     float last_ms = 0.f;  // device time of the last decode (launch sequence only)
     int *rb_ctr = nullptr;  // rb_kernel's item counters, one per launch of a decode (zeroed per decode)
     // diagnostics (MAGPIE_CODEC_TS=stage,block,file): the phase stamps of one rb_kernel launch
@@ -1568,10 +1572,22 @@ int mp_hip_codec_init(int device, const char *path, mp_codec **out) {
     return MP_OK;
 }
 
+// The stream a decode runs on: the background (CU-masked) one while set, else the codec's.
+// c->stream is swapped for the call's duration (every launch of codec_run reads it).
+struct CodecStreamScope {
+    mp_codec *c;
+    hipStream_t saved;
+    explicit CodecStreamScope(mp_codec *cc) : c(cc), saved(cc->stream) {
+        if (c->bg && c->bg_stream) c->stream = c->bg_stream;
+    }
+    ~CodecStreamScope() { c->stream = saved; }
+};
+
 int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, int chunk_frames, float *audio_out) {
     if (!c) return MP_ERR_ARG;
     if (!codes || !audio_out || n_chunks < 1 || chunk_frames < 1) { c->err = "invalid arguments"; return MP_ERR_ARG; }
     CHK(hipSetDevice(c->device));
+    CodecStreamScope scope(c);
     if (int rc = ensure_buffers(c, n_chunks, chunk_frames)) return rc;
     CHK(hipMemcpyAsync(c->codes, codes, (size_t)n_chunks * 8 * chunk_frames * 4, hipMemcpyHostToDevice, c->stream));
     if (!c->ev0) { CHK(hipEventCreate(&c->ev0)); CHK(hipEventCreate(&c->ev1)); }
@@ -1622,10 +1638,34 @@ int mp_hip_codec_decode(mp_codec *c, const int32_t *codes, int n_frames, float *
     return mp_hip_codec_decode_chunks(c, codes, 1, n_frames, audio_out);
 }
 
+// Internal (mp_hip_decode_stream): run this codec's next decodes in the background, i.e. on a
+// stream confined to `cus` of the device's CUs (0: back to the codec's own stream), so a decode
+// in flight on the model's stream keeps the rest of the chip; every decode computes the same bits
+// on either stream (the kernels do not depend on where their workgroups run).
+extern "C" int mp_codec_set_background(mp_codec *c, int cus) {
+    if (!c) return MP_ERR_ARG;
+    if (cus <= 0) { c->bg = 0; return MP_OK; }
+    CHK(hipSetDevice(c->device));
+    if (!c->bg_stream || c->bg_cus != cus) {
+        if (c->bg_stream) { CHK(hipStreamSynchronize(c->bg_stream)); hipStreamDestroy(c->bg_stream); c->bg_stream = nullptr; }
+        int ncu = 0;
+        CHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+        if (cus >= ncu) { c->bg = 0; return MP_OK; }
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        const int step = std::max(1, ncu / cus);  // every step-th CU: spread over the XCDs
+        for (int i = 0, n = 0; i < ncu && n < cus; i += step, ++n) mask[i / 32] |= 1u << (i % 32);
+        CHK(hipExtStreamCreateWithCUMask(&c->bg_stream, (uint32_t)mask.size(), mask.data()));
+        c->bg_cus = cus;
+    }
+    c->bg = 1;
+    return MP_OK;
+}
+
 void mp_hip_codec_free(mp_codec *c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->bg_stream) { hipStreamSynchronize(c->bg_stream); hipStreamDestroy(c->bg_stream); }
     for (void *p : c->weight_allocs) hipFree(p);
     if (c->ts_dev) hipFree(c->ts_dev);
     if (c->rb_ctr) hipFree(c->rb_ctr);

@@ -17,9 +17,10 @@
 #include "mp_device.hpp"
 #include "mp_params.hpp"
 #include "mp_prefill_api.hpp"
+#include "mp_xa.hpp"
 
 #ifndef MP_PRE_PF
-#define MP_PRE_PF 8  // K steps of operand loads in flight per thread (A/B: round 5 had 4)
+#define MP_PRE_PF 4  // K steps of operand loads in flight per thread (8 measured slower, round 6)
 #endif
 
 namespace mp {
@@ -62,30 +63,39 @@ __device__ __forceinline__ void gemm_store(const GemmP &p, const float (&acc)[4]
 }
 
 // Split-K reduction of a residual GEMM whose rows are normalised next (GemmP::ln_w, N = 768):
-// one workgroup per row, x = C + sum of the splits in order (gemm_reduce_kernel<GE_RESID>'s
-// arithmetic) stored to C, then LN(x) * ln_w into ln_out (ln_rows_kernel's: the same thread
-// layout and block statistics) - one launch where the preamble had two.
-__global__ __launch_bounds__(256) void gemm_reduce_ln_kernel(GemmP p, int splits) {
-    __shared__ float red[8];
-    const int m = blockIdx.x, tid = threadIdx.x;
+// one 768-thread workgroup per row, thread n: x = C + the splits summed in order
+// (gemm_reduce_kernel<GE_RESID>'s arithmetic) stored to C; then the row's mean and variance
+// (two passes: wave sums, the 12 wave partials added in wave order) and LN(x) * ln_w into
+// ln_out. One launch where the preamble had two, with the reduce kernel's parallelism (one
+// output per thread; round 6's first form, 3 outputs per thread of a 256-thread block, took
+// 19 us per row block against 5 + 5 as two launches).
+constexpr int RLN_T = D;  // threads per row
+__global__ __launch_bounds__(RLN_T) void gemm_reduce_ln_kernel(GemmP p, int splits) {
+    __shared__ float red[RLN_T / 64];
+    const int m = blockIdx.x, n = threadIdx.x, lane = n & 63, w = n >> 6;
     const size_t total = (size_t)p.M * p.N;
-    float v[3];
+    const size_t e = (size_t)m * p.N + n;
+    float a = p.part[e];
+#pragma unroll 8
+    for (int s = 1; s < splits; ++s) a += p.part[(size_t)s * total + e];
+    if (p.bias) a += p.bias[n];
+    const float x = a + p.C[(size_t)m * p.ldc + n];
+    p.C[(size_t)m * p.ldc + n] = x;
+    auto block_sum = [&](float v) {
+        v = wave_sum(v);
+        if (lane == 0) red[w] = v;
+        __syncthreads();
+        float t = red[0];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int n = tid + 256 * i;
-        const size_t e = (size_t)m * p.N + n;
-        float a = p.part[e];
-        for (int s = 1; s < splits; ++s) a += p.part[(size_t)s * total + e];
-        if (p.bias) a += p.bias[n];
-        const float x = a + p.C[(size_t)m * p.ldc + n];
-        p.C[(size_t)m * p.ldc + n] = x;
-        v[i] = x;
-    }
-    float mean, var;
-    block_meanvar<3>(v, red, mean, var);
+        for (int i = 1; i < RLN_T / 64; ++i) t += red[i];
+        __syncthreads();
+        return t;
+    };
+    const float mean = block_sum(x) * (1.0f / D);
+    const float d = x - mean;
+    const float var = block_sum(d * d) * (1.0f / D);
     const float rstd = 1.0f / sqrtf(var + p.ln_eps);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) p.ln_out[(size_t)m * p.ln_ld + tid + 256 * i] = ((v[i] - mean) * rstd) * p.ln_w[tid + 256 * i];
+    p.ln_out[(size_t)m * p.ln_ld + n] = (d * rstd) * p.ln_w[n];
 }
 
 // Split-K reduction: v = sum of the splits in order, then the epilogue.
@@ -467,6 +477,21 @@ __global__ __launch_bounds__(256) void row_xa_kernel(RowXaP p) {
     p.O[(size_t)m * DXA + 64 + lane] = o1 / l;
 }
 
+// The same cross-attention, one workgroup per row, on the decode's direct-form text
+// attention (xa_text_attention, mp_xa.hpp: 4 lanes per key, the first 64 keys' K and V
+// rows issued at entry, one exp per key, wave partials summed in wave order): a row's
+// attention is one memory round trip and a few DPP steps instead of a wave's serial
+// key loop (13.3 us per prefill layer at T = 64 with a wave per row, round 5).
+__global__ __launch_bounds__(MP_BLOCK) void row_xa_wg_kernel(RowXaP p) {
+    __shared__ float pr[TMAX_LIMIT];
+    __shared__ __attribute__((aligned(16))) float a_s[DXA];
+    const int m = blockIdx.x;
+    const int b = m / p.rows_per_utt;
+    const size_t kv = ((size_t)(b * p.nlayers + p.layer) * p.Tmax) * DXA;
+    xa_text_attention(p.Q + (size_t)m * DXA, p.xak + kv, p.xav + kv, p.T[b], pr, a_s);
+    if (threadIdx.x < DXA) p.O[(size_t)m * DXA + threadIdx.x] = a_s[threadIdx.x];
+}
+
 // x[b][t] = text_emb[tok] + enc_pos[t] (t < T[b]), zero rows for padding.
 __global__ void embed_text_kernel(const int *tok, const int *T, int Tmax, const float *text_emb,
                                   const float *enc_pos, float *X) {
@@ -523,7 +548,7 @@ template <int EPI>
 static hipError_t launch_reduce(const GemmP &p, int splits, hipStream_t s) {
     if constexpr (EPI == GE_RESID) {
         if (p.ln_w && p.N == D) {
-            hipLaunchKernelGGL(gemm_reduce_ln_kernel, dim3(p.M), dim3(256), 0, s, p, splits);
+            hipLaunchKernelGGL(gemm_reduce_ln_kernel, dim3(p.M), dim3(RLN_T), 0, s, p, splits);
             return hipGetLastError();
         }
     }
@@ -560,7 +585,7 @@ static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
 template <int EPI>
 static hipError_t launch_gemm_q8(const GemmP &p, hipStream_t s) {
     if (!p.Wd || p.K % 32 || p.conv_taps) return hipErrorInvalidValue;
-    const int splits = p.part ? gemm_splits(p.K) : 1;
+    const int splits = p.part ? gemm_splits_q8(p.K) : 1;
     dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits);
     GemmP q = p;
     if (splits == 1) q.part = nullptr;
@@ -613,6 +638,11 @@ hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t pre_row_xa(const RowXaP &p, hipStream_t s) {
+    static const bool old = getenv("MAGPIE_PRE_ROWXA_OLD") != nullptr;  // A/B: a wave per row (round 5)
+    if (!old) {
+        hipLaunchKernelGGL(row_xa_wg_kernel, dim3(p.M), dim3(MP_BLOCK), 0, s, p);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(row_xa_kernel, dim3((p.M + 3) / 4), dim3(256), 0, s, p);
     return hipGetLastError();
 }

@@ -49,26 +49,34 @@ struct GemmP {
                        //    F16 mul_mat rounds src1 to f16; products then exact in f32)
 };
 
-// Split count of a preamble GEMM over K (fixed per K: batch-invariant results).
-// Pieces of PRE_KS = 128 (8 K steps of 16): every model K (128, 768, 2304, 3072, 9216) is a
-// multiple, and 8 steps are exactly the operand loads a thread keeps in flight
-// (gemm_f32_mfma_kernel's ring), so a workgroup pays one memory latency for its slice
-// instead of one per 4 steps (round 5: K / 96 pieces, at most 16: 576-wide slices of
-// the encoder's 9216-wide conv waited on memory 9 times).
+// Split count of a preamble GEMM over K (fixed per K: batch-invariant results): K / 96
+// pieces, at most 16, whole 32-wide blocks (MP_PRE_KS = 128: K / 128 pieces with 8 steps of
+// loads in flight, measured slower in round 6: 3.17 vs 2.97 ms per preamble, more
+// workgroups each paying its own start-up and partial-tile stores).
 #ifndef MP_PRE_KS
-#define MP_PRE_KS 128  // (A/B: 0 = round 5's K / 96 pieces, at most 16)
+#define MP_PRE_KS 0  // 0: K / 96 pieces, at most 16 (round 5's); 128: K / 128 (measured slower, round 6)
 #endif
 constexpr int PRE_KS = MP_PRE_KS;
-constexpr int PRE_CTR_TILES = 4096;
-constexpr int PRE_INWG_TILES = 256;  // output tiles from which a GEMM runs its splits inside each workgroup
-inline int gemm_splits(int K) {
-    if (PRE_KS > 0 && K % PRE_KS == 0) return K / PRE_KS;
-    int s = K / 96;  // (no model K takes this path)
+#ifndef MP_PRE_INWG_TILES
+#define MP_PRE_INWG_TILES 256
+#endif
+constexpr int PRE_INWG_TILES = MP_PRE_INWG_TILES;  // output tiles from which a GEMM runs its splits inside each workgroup
+// The Q8_0 preamble GEMM (gemm_q8_kernel) always uses these pieces: its split order is part
+// of the Q8_0 mode's f32 rounding, which moves activation-quantisation flips (the configs[4]
+// long-form test's trajectory).
+inline int gemm_splits_q8(int K) {
+    int s = K / 96;
     if (s < 1) s = 1;
     if (s > 16) s = 16;
     while (s > 1 && (K % (s * 32)) != 0) --s;  // whole 32-wide (Q8_0) blocks per split
     return s;
 }
+inline int gemm_splits(int K) {
+    if (PRE_KS > 0 && K % PRE_KS == 0) return K / PRE_KS;
+    return gemm_splits_q8(K);  // (no model K takes this path)
+}
+// partial-sum capacity of either kernel's pieces
+inline int gemm_splits_max(int K) { return gemm_splits(K) > gemm_splits_q8(K) ? gemm_splits(K) : gemm_splits_q8(K); }
 
 // Causal multi-head attention for every (row, head) of a block of rows.
 struct RowAttnP {

@@ -947,7 +947,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     {   // largest S x M x N of the preamble GEMMs (encoder FFN up/down, prefill FFN)
         const size_t Me = (size_t)NB * Tmax, Mc = (size_t)NB * mp::CTX;
         size_t cap = enc_gpart_elems(Me);
-        auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits(K) * M * N); };
+        auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits_max(K) * M * N); };
         need(Mc, 2304, 768); need(Mc, 3072, 768); need(Mc, 768, 3072); need(Mc, 768, 768);
         A(gpart, cap);
     }
@@ -1585,7 +1585,7 @@ struct EncWs {
 };
 static size_t enc_gpart_elems(size_t Me) {
     size_t cap = 0;
-    auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits(K) * M * N); };
+    auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits_max(K) * M * N); };
     need(Me, 2304, 768); need(Me, 3072, 768 * 3); need(Me, 768, 3072 * 3); need(Me, 256, 768);
     return cap;
 }
@@ -2103,6 +2103,18 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
 // Every full chunk of a round goes through the codec in one launch sequence
 // (chunks are independent, magpie.cpp:4739-4742: the audio is the same); the
 // frames reach the host through a pinned mirror filled on the decode stream.
+extern "C" int mp_codec_set_background(mp_codec *c, int cus);  // mp_codec.hip (internal)
+// MAGPIE_CODEC_BG_CUS: CUs of the codec's background stream while a decode is in flight
+// (default 64 of 256; 0 = the codec's own stream, the whole chip, for every round)
+static int codec_bg_cus() {
+    const char *e = getenv("MAGPIE_CODEC_BG_CUS");
+    return e ? atoi(e) : 64;
+}
+// codec rounds of at least this many frames go to the background stream while the decode
+// continues (throughput: configs[2]'s 16 slots x 32-frame chunks); smaller rounds (a stream's
+// 4-frame chunks, whose first chunk is the time to first audio) keep the whole chip
+constexpr int CODEC_BG_MIN_FRAMES = 256;
+
 int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_audio_cb on_audio, void *user,
                          int32_t *codes_out, int32_t *n_frames, int64_t *total_samples) {
     if (!dev) return MP_ERR_ARG;
@@ -2195,9 +2207,17 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
             for (int t = 0; t < j.n; ++t)  // frame-major -> codebook-major (decode_frames_to_audio, 4468-4473)
                 for (int c = 0; c < 8; ++c) dst[(size_t)c * j.n + t] = fm[(size_t)t * 8 + c];
         }
-        if (nfull)
-            if (int rc = mp_hip_codec_decode_chunks(codec, cbm.data(), (int)nfull, fpc, audio.data()))
-                return fail(dev, rc, std::string("codec: ") + mp_hip_codec_error(codec));
+        if (nfull) {
+            // beside a decode still in flight, large rounds run on the codec's CU-masked
+            // background stream: the frame loop keeps most of the chip (with the whole chip the
+            // codec's long workgroups held the CUs the decode's next launches waited for, and
+            // overlapping bought nothing: 27.2k vs 27.5k frames/s serial, round 6 r06c)
+            const int bg = more && (int)nfull * fpc >= CODEC_BG_MIN_FRAMES ? codec_bg_cus() : 0;
+            if (int rc = mp_codec_set_background(codec, bg)) return fail(dev, rc, "codec background stream");
+            const int rc = mp_hip_codec_decode_chunks(codec, cbm.data(), (int)nfull, fpc, audio.data());
+            mp_codec_set_background(codec, 0);
+            if (rc) return fail(dev, rc, std::string("codec: ") + mp_hip_codec_error(codec));
+        }
         for (size_t q = 0; q < jobs.size(); ++q)
             if (jobs[q].n != fpc)
                 if (int rc = mp_hip_codec_decode(codec, cbm.data() + at[q] * 8 * fpc, jobs[q].n,

@@ -333,4 +333,118 @@ __device__ __forceinline__ void xa_tail(const GemvP &p, unsigned long long t_sta
     ts_end(p.ts, t_start);
 }
 
+// ---------------------------------------------------------------- text attention, direct form
+// a = softmax_t(q . K_t / sqrt(128)) V  of slot b into a_s[128] (every thread
+// returns after a barrier); pr: per-key scores, then weights [TMAX_LIMIT]. getq() makes
+// q readable (whatever hand-off that takes) and returns it (16 B aligned, global or LDS).
+// The first 64 keys' K rows and V rows are issued at entry, before getq: one memory
+// round trip for a text of up to 64 tokens; longer texts load 64 keys per round.
+//  1. scores: key t = 64 c + 16 w + lane / 4 of wave w, 4 lanes per key (32 dims each,
+//     one fmaf chain), the quad summed by two DPP steps (no cross-row exchange);
+//  2. weights: thread t exponentiates key t (one expf per key), sums its keys, the
+//     denominator is the wave sums in wave order;
+//  3. a[d] = sum_t e_t V_t[d] / den: wave w takes keys w, w + 4, ... in ascending order
+//     (lane owns dims lane, 64 + lane), the 4 waves' partials summed in order.
+// Branch-free per key (clamped loads, selects), so the DPP and LDS traffic of a round
+// issues back to back.
+constexpr int XA_PF_V = 4;  // rounds of 16 value rows issued at entry
+template <typename QF>
+__device__ __forceinline__ void xa_text_attention_q(QF getq, const float *Kb, const float *Vb, int Tb, float *pr,
+                                                    float *a_s) {
+#pragma clang fp contract(off)
+    __shared__ __attribute__((aligned(16))) float pv[MP_NWAVES][DXA];
+    __shared__ float wred[2 * MP_NWAVES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int kq = 16 * w + (lane >> 2), dq = 32 * (lane & 3);  // pass 1: key in the round, dims
+    f32x4 kpf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kpf[i] = *(const f32x4 *)(Kb + (size_t)min(kq, Tb - 1) * DXA + dq + 4 * i);
+    float v0pf[XA_PF_V][4], v1pf[XA_PF_V][4];
+#pragma unroll
+    for (int r = 0; r < XA_PF_V; ++r)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(w + 16 * r + MP_NWAVES * u, Tb - 1);
+            v0pf[r][u] = Vb[(size_t)t * DXA + lane];
+            v1pf[r][u] = Vb[(size_t)t * DXA + 64 + lane];
+        }
+    const float *qp = getq();
+    f32x4 q4[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q4[i] = *(const f32x4 *)(qp + dq + 4 * i);
+    const float scale = 1.0f / sqrtf((float)DXA);
+    float mx = -INFINITY;
+    auto score = [&](int t, const f32x4 (&k4)[8]) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            s = fmaf(q4[i].x, k4[i].x, s);
+            s = fmaf(q4[i].y, k4[i].y, s);
+            s = fmaf(q4[i].z, k4[i].z, s);
+            s = fmaf(q4[i].w, k4[i].w, s);
+        }
+        s += dpp_mov<0xB1>(s);  // (s0 + s1) + (s2 + s3) in every lane of the quad
+        s += dpp_mov<0x4E>(s);
+        const float sv = s * scale;
+        if ((lane & 3) == 0 && t < Tb) pr[t] = sv;
+        mx = fmaxf(mx, t < Tb ? sv : -INFINITY);
+    };
+    score(kq, kpf);
+    for (int t0 = 64; t0 < Tb; t0 += 64) {
+        f32x4 k4[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) k4[i] = *(const f32x4 *)(Kb + (size_t)min(t0 + kq, Tb - 1) * DXA + dq + 4 * i);
+        score(t0 + kq, k4);
+    }
+    mx = wave_max(mx);
+    if (lane == 0) wred[w] = mx;
+    lds_sync();
+    const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
+    float l = 0.f;
+    for (int t = tid; t < Tb; t += MP_BLOCK) {
+        const float e = expf(pr[t] - M);
+        pr[t] = e;
+        l += e;
+    }
+    l = wave_sum(l);
+    if (lane == 0) wred[MP_NWAVES + w] = l;
+    lds_sync();
+    // o[d] = sum_t e_t V_t[d]: wave w takes keys t = w + 4 u, lane owns dims lane, 64 + lane
+    float o0 = 0.f, o1 = 0.f;
+    auto accum = [&](int t0, const float (&v0)[4], const float (&v1)[4]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + MP_NWAVES * u;
+            const float e = t < Tb ? pr[min(t, Tb - 1)] : 0.f;
+            o0 = fmaf(e, v0[u], o0);
+            o1 = fmaf(e, v1[u], o1);
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < XA_PF_V; ++r) accum(w + 16 * r, v0pf[r], v1pf[r]);
+    for (int t0 = w + 16 * XA_PF_V; t0 < Tb; t0 += MP_NWAVES * 4) {
+        float v0[4], v1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(t0 + MP_NWAVES * u, Tb - 1);
+            v0[u] = Vb[(size_t)t * DXA + lane];
+            v1[u] = Vb[(size_t)t * DXA + 64 + lane];
+        }
+        accum(t0, v0, v1);
+    }
+    pv[w][lane] = o0;
+    pv[w][64 + lane] = o1;
+    lds_sync();
+    if (tid < DXA) {
+        const float den = ((wred[4] + wred[5]) + wred[6]) + wred[7];
+        a_s[tid] = (((pv[0][tid] + pv[1][tid]) + pv[2][tid]) + pv[3][tid]) / den;
+    }
+    lds_sync();
+}
+
+__device__ __forceinline__ void xa_text_attention(const float *q, const float *Kb, const float *Vb, int Tb,
+                                                  float *pr, float *a_s) {
+    xa_text_attention_q([&]() { return q; }, Kb, Vb, Tb, pr, a_s);
+}
+
 }  // namespace mp

@@ -102,6 +102,11 @@ for STEP in "$@"; do
       for k in "${!sets[@]}"; do sets[$k]=$(echo "${sets[$k]}" | tr ',' ' '); done
       bash tools_dev/ab_kv.sh "${TAG}_abkv" "$n" "${sets[@]}" > "$OUT/${TAG}_abkv.txt" 2>&1
       cat "$OUT/${TAG}_abkv.txt" ;;
+    e2e)
+      # configs[2] end to end under codec background CU shares: e2e=CUS,CUS:ROUNDS
+      IFS=: read -r cus rounds <<< "${arg:-0,64:2}"
+      timeout -k 10 400 python -u tools_dev/e2e_ab.py "$cus" "${rounds:-2}" > "$OUT/${TAG}_e2e.txt" 2>&1
+      cat "$OUT/${TAG}_e2e.txt" ;;
     pre)
       # per-kernel time of one preamble (tools_dev/preamble_prof.py); arg: weights:B:T[:LIB]
       IFS=: read -r w b t lib <<< "${arg:-f32:1:64}"

@@ -62,50 +62,19 @@ __device__ __forceinline__ void gemm_store(const GemmP &p, const float (&acc)[4]
     }
 }
 
-// Split-K reduction of a residual GEMM whose rows are normalised next (GemmP::ln_w, N = 768):
-// one 768-thread workgroup per row, thread n: x = C + the splits summed in order
-// (gemm_reduce_kernel<GE_RESID>'s arithmetic) stored to C; then the row's mean and variance
-// (two passes: wave sums, the 12 wave partials added in wave order) and LN(x) * ln_w into
-// ln_out. One launch where the preamble had two, with the reduce kernel's parallelism (one
-// output per thread; round 6's first form, 3 outputs per thread of a 256-thread block, took
-// 19 us per row block against 5 + 5 as two launches).
-constexpr int RLN_T = D;  // threads per row
-__global__ __launch_bounds__(RLN_T) void gemm_reduce_ln_kernel(GemmP p, int splits) {
-    __shared__ float red[RLN_T / 64];
-    const int m = blockIdx.x, n = threadIdx.x, lane = n & 63, w = n >> 6;
-    const size_t total = (size_t)p.M * p.N;
-    const size_t e = (size_t)m * p.N + n;
-    float a = p.part[e];
-#pragma unroll 8
-    for (int s = 1; s < splits; ++s) a += p.part[(size_t)s * total + e];
-    if (p.bias) a += p.bias[n];
-    const float x = a + p.C[(size_t)m * p.ldc + n];
-    p.C[(size_t)m * p.ldc + n] = x;
-    auto block_sum = [&](float v) {
-        v = wave_sum(v);
-        if (lane == 0) red[w] = v;
-        __syncthreads();
-        float t = red[0];
-#pragma unroll
-        for (int i = 1; i < RLN_T / 64; ++i) t += red[i];
-        __syncthreads();
-        return t;
-    };
-    const float mean = block_sum(x) * (1.0f / D);
-    const float d = x - mean;
-    const float var = block_sum(d * d) * (1.0f / D);
-    const float rstd = 1.0f / sqrtf(var + p.ln_eps);
-    p.ln_out[(size_t)m * p.ln_ld + n] = (d * rstd) * p.ln_w[n];
-}
-
 // Split-K reduction: v = sum of the splits in order, then the epilogue.
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmP p, int splits) {
     const size_t total = (size_t)p.M * p.N;
-    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (size_t)gridDim.x * 256) {
-        float v = p.part[e];
-        for (int s = 1; s < splits; ++s) v += p.part[(size_t)s * total + e];
-        gemm_store1<EPI>(p, (int)(e / p.N), (int)(e % p.N), v);
+    const int nb = p.nbatch > 1 ? p.nbatch : 1;  // batched GEMM: partials [batch][split][M][N]
+    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total * nb; e += (size_t)gridDim.x * 256) {
+        const int bz = (int)(e / total);
+        const size_t ee = e % total, base = (size_t)bz * splits * total + ee;
+        float v = p.part[base];
+        for (int s = 1; s < splits; ++s) v += p.part[base + (size_t)s * total];
+        GemmP q = p;
+        if (bz) { q.C += bz * p.sC; q.layer += bz; }
+        gemm_store1<EPI>(q, (int)(ee / p.N), (int)(ee % p.N), v);
     }
 }
 
@@ -124,7 +93,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
     const int tx = tid & 15, ty = tid >> 4;
     float acc[4][4] = {};
     const int lr = tid >> 2, lk = (tid & 3) * 4;  // loader: row lr, k lk..lk+3
-    const int ks = p.K / gridDim.z, kbeg = blockIdx.z * ks;  // split-K slice (gridDim.z == 1: all of K)
+    int zs;
+    const int S = gemm_batch_enter(p, zs);
+    const int ks = p.K / S, kbeg = zs * ks;  // split-K slice (S == 1: all of K)
     const int nsteps = ks / BK;
     const int m = m0 + lr, n = n0 + lr;
     auto load_a = [&](int k0) {
@@ -207,9 +178,11 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(GemmP p) {
     // (large grids, gridDim.z == 1 < nsplit) every split of the tile here in turn, each its
     // own chain from 0, folded into tot in split order: tot = p0, tot += p1, ... - the same
     // float operations as the reduction of the partials, without writing them
-    const int ks = p.K / gridDim.z, kbeg = blockIdx.z * ks;
+    int zs;
+    const int S = gemm_batch_enter(p, zs);
+    const int ks = p.K / S, kbeg = zs * ks;
     const int nsteps = ks / BK;
-    const int sl = (gridDim.z == 1 && p.nsplit > 1) ? (p.K / p.nsplit) / BK : nsteps;  // steps per split
+    const int sl = (S == 1 && p.nsplit > 1) ? (p.K / p.nsplit) / BK : nsteps;  // steps per split
     const int m = m0 + lr, n = n0 + lr;
     auto load_a = [&](int k0) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -308,7 +281,9 @@ __global__ __launch_bounds__(256) void gemm_q8_kernel(GemmP p) {
     const int tx = tid & 15, ty = tid >> 4;
     const int lr = tid >> 2, part = tid & 3;  // loader: row lr, elements 8 part .. 8 part + 7 of the block
     const int nblk = p.K / 32;
-    const int bs = nblk / gridDim.z, bbeg = blockIdx.z * bs;  // split-K slice in whole blocks
+    int zs;
+    const int S = gemm_batch_enter(p, zs);
+    const int bs = nblk / S, bbeg = zs * bs;  // split-K slice in whole blocks
     float acc[4][4] = {};
     // PF blocks' operand loads in flight per thread (register ring), as gemm_f32_kernel
     constexpr int PF = 4;
@@ -378,20 +353,60 @@ __global__ __launch_bounds__(256) void gemm_q8_kernel(GemmP p) {
     gemm_store<EPI>(p, acc, m0 + ty * 4, n0 + tx * 4);
 }
 
-// Y[m] = LN(X[m]) * w for rows of width 768 (ggml_norm + ggml_mul).
-__global__ __launch_bounds__(256) void ln_rows_kernel(const float *X, int ldx, const float *w, float *Y, int ldy,
-                                                      float eps) {
-    __shared__ float red[8];
-    const int m = blockIdx.x, tid = threadIdx.x;
-    const float *x = X + (size_t)m * ldx;
-    float v[3];
+// Y[m] = LN(X[m]) * w for rows of width 768 (ggml_norm + ggml_mul): one 768-thread block per
+// row, thread n element n; mean and variance in two passes (wave sums, the 12 wave partials
+// added in wave order). ln_row768 is shared with gemm_reduce_ln_kernel, so a row normalised
+// there or here (the large-grid GEMMs that reduce inside the workgroup) has the same bits.
+constexpr int RLN_T = D;  // threads per row
+__device__ __forceinline__ void ln_row768(float x, const float *w, float *y, float eps) {
+    __shared__ float red[RLN_T / 64];
+    const int n = threadIdx.x, lane = n & 63, wv = n >> 6;
+    auto block_sum = [&](float v) {
+        v = wave_sum(v);
+        if (lane == 0) red[wv] = v;
+        __syncthreads();
+        float t = red[0];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) v[i] = x[tid + 256 * i];
-    float mean, var;
-    block_meanvar<3>(v, red, mean, var);
+        for (int i = 1; i < RLN_T / 64; ++i) t += red[i];
+        __syncthreads();
+        return t;
+    };
+    const float mean = block_sum(x) * (1.0f / D);
+    const float d = x - mean;
+    const float var = block_sum(d * d) * (1.0f / D);
     const float rstd = 1.0f / sqrtf(var + eps);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) Y[(size_t)m * ldy + tid + 256 * i] = ((v[i] - mean) * rstd) * w[tid + 256 * i];
+    y[n] = (d * rstd) * w[n];
+}
+__global__ __launch_bounds__(RLN_T) void ln_rows_kernel(const float *X, int ldx, const float *w, float *Y, int ldy,
+                                                        float eps) {
+    const int m = blockIdx.x;
+    ln_row768(X[(size_t)m * ldx + threadIdx.x], w, Y + (size_t)m * ldy, eps);
+}
+// The same rows normalised with nw weight vectors at once (grid.y = g: w + g sw -> Y + g sy):
+// the XA K/V precompute's LN(encoder output) with every layer's norm_xmem in one launch
+__global__ __launch_bounds__(RLN_T) void ln_rows_multi_kernel(const float *X, int ldx, const float *w, long long sw,
+                                                              float *Y, int ldy, long long sy, float eps) {
+    const int m = blockIdx.x, g = blockIdx.y;
+    ln_row768(X[(size_t)m * ldx + threadIdx.x], w + g * sw, Y + g * sy + (size_t)m * ldy, eps);
+}
+
+// Split-K reduction of a residual GEMM whose rows are normalised next (GemmP::ln_w, N = 768):
+// one 768-thread workgroup per row, thread n: x = C + the splits summed in order
+// (gemm_reduce_kernel<GE_RESID>'s arithmetic) stored to C, then ln_row768 (ln_rows_kernel's
+// arithmetic) into ln_out. One launch where the preamble had two, with the reduce kernel's
+// parallelism (one output per thread; round 6's first form, 3 outputs per thread of a
+// 256-thread block, took 19 us per row block against 5 + 5 as two launches).
+__global__ __launch_bounds__(RLN_T) void gemm_reduce_ln_kernel(GemmP p, int splits) {
+    const int m = blockIdx.x, n = threadIdx.x;
+    const size_t total = (size_t)p.M * p.N;
+    const size_t e = (size_t)m * p.N + n;
+    float a = p.part[e];
+#pragma unroll 8
+    for (int s = 1; s < splits; ++s) a += p.part[(size_t)s * total + e];
+    if (p.bias) a += p.bias[n];
+    const float x = a + p.C[(size_t)m * p.ldc + n];
+    p.C[(size_t)m * p.ldc + n] = x;
+    ln_row768(x, p.ln_w, p.ln_out + (size_t)m * p.ln_ld, p.ln_eps);
 }
 
 // Causal multi-head attention for every (row, head): one wave per pair.
@@ -429,6 +444,78 @@ __global__ __launch_bounds__(256) void row_attn_kernel(RowAttnP p) {
         o += pr[w][j] * (KV16 ? __uint_as_float((unsigned)((const unsigned short *)p.Vb)[vi] << 16) : p.Vb[vi]);
     }
     p.O[(size_t)m * D + h * DH + lane] = o / l;
+}
+
+// The same causal attention, one workgroup per (row, head), in the direct-form pattern of
+// the decode's text attention (xa_text_attention, mp_xa.hpp): keys in rounds of 64, 4 lanes
+// per key (16 dims each, one chain, the quad summed by DPP), every key's K row of a round
+// issued at once, one exp per key by its own thread, the values summed by 4 waves (keys
+// w, w + 4, ...; lane = dim) and the wave partials added in wave order. round 5's wave per
+// (row, head) made a dependent memory round trip per key of its value loop.
+template <bool KV16>
+__global__ __launch_bounds__(MP_BLOCK) void row_attn_wg_kernel(RowAttnP p) {
+    __shared__ float pr[TMAX_LIMIT];
+    __shared__ float pv[MP_NWAVES][DH];
+    __shared__ float wred[2 * MP_NWAVES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m = blockIdx.x, h = blockIdx.y;
+    const int b = m / p.rows_per_utt, t = m % p.rows_per_utt;
+    const int nk = t + 1;
+    const size_t kb0 = b * p.utt_stride + h * DH;
+    const int kq = 16 * w + (lane >> 2), dq = 16 * (lane & 3);
+    float4 q4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q4[i] = *(const float4 *)(p.Q + (size_t)m * p.ldq + h * DH + dq + 4 * i);
+    float mx = -INFINITY;
+    for (int j0 = 0; j0 < nk; j0 += 64) {
+        const int j = j0 + kq;
+        const size_t k = kb0 + (size_t)min(j, nk - 1) * p.row_stride + dq;
+        float4 k4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) k4[i] = kv_load4<KV16>(p.Kb, k + 4 * i);
+        float sv = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sv += dotv(q4[i], k4[i]);
+        sv += dpp_mov<0xB1>(sv);
+        sv += dpp_mov<0x4E>(sv);
+        sv *= 0.125f;
+        if ((lane & 3) == 0 && j < nk) pr[j] = sv;
+        mx = fmaxf(mx, j < nk ? sv : -INFINITY);
+    }
+    mx = wave_max(mx);
+    if (lane == 0) wred[w] = mx;
+    lds_sync();
+    const float M = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
+    float l = 0.f;
+    for (int j = tid; j < nk; j += MP_BLOCK) {
+        const float e = expf(pr[j] - M);
+        pr[j] = e;
+        l += e;
+    }
+    l = wave_sum(l);
+    if (lane == 0) wred[MP_NWAVES + w] = l;
+    lds_sync();
+    float o = 0.f;
+    for (int j0 = w; j0 < nk; j0 += 4 * MP_NWAVES) {  // 4 keys' V rows in flight per wave
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = min(j0 + MP_NWAVES * u, nk - 1);
+            const size_t vi = kb0 + (size_t)j * p.row_stride + lane;
+            v[u] = KV16 ? __uint_as_float((unsigned)((const unsigned short *)p.Vb)[vi] << 16) : p.Vb[vi];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + MP_NWAVES * u;
+            o += (j < nk ? pr[min(j, nk - 1)] : 0.f) * v[u];
+        }
+    }
+    pv[w][lane] = o;
+    lds_sync();
+    if (tid < DH) {
+        const float den = ((wred[4] + wred[5]) + wred[6]) + wred[7];
+        p.O[(size_t)m * D + h * DH + tid] = (((pv[0][tid] + pv[1][tid]) + pv[2][tid]) + pv[3][tid]) / den;
+    }
 }
 
 // Cross-attention for a block of rows: 1 head x 128 over the utterance's T[b]
@@ -541,7 +628,7 @@ static bool gemm_mfma() {
 // in the split reduction when there is one (gemm_reduce_ln_kernel), else as ln_rows_kernel
 static hipError_t launch_ln_after(const GemmP &p, hipStream_t s) {
     if (!p.ln_w) return hipSuccess;
-    hipLaunchKernelGGL(ln_rows_kernel, dim3(p.M), dim3(256), 0, s, p.C, p.ldc, p.ln_w, p.ln_out, p.ln_ld, p.ln_eps);
+    hipLaunchKernelGGL(ln_rows_kernel, dim3(p.M), dim3(RLN_T), 0, s, p.C, p.ldc, p.ln_w, p.ln_out, p.ln_ld, p.ln_eps);
     return hipGetLastError();
 }
 template <int EPI>
@@ -552,7 +639,7 @@ static hipError_t launch_reduce(const GemmP &p, int splits, hipStream_t s) {
             return hipGetLastError();
         }
     }
-    const size_t total = (size_t)p.M * p.N;
+    const size_t total = (size_t)p.M * p.N * (p.nbatch > 1 ? p.nbatch : 1);
     const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3(grid), dim3(256), 0, s, p, splits);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
@@ -561,16 +648,17 @@ static hipError_t launch_reduce(const GemmP &p, int splits, hipStream_t s) {
 template <int EPI, int TAPS>
 static hipError_t launch_gemm(const GemmP &p, hipStream_t s) {
     const int splits = p.part ? gemm_splits(p.K) : 1;
-    if (p.K % (16 * splits)) return hipErrorInvalidValue;
-    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits);
+    const int nb = p.nbatch > 1 ? p.nbatch : 1;
+    if (p.K % (16 * splits) || (nb > 1 && p.ln_w)) return hipErrorInvalidValue;
+    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits * nb);
     GemmP q = p;
     if (splits == 1) q.part = nullptr;
     const bool mfma = gemm_mfma();
     q.nsplit = splits;
-    if (mfma && splits > 1 && grid.x * grid.y >= PRE_INWG_TILES) {
+    if (mfma && splits > 1 && grid.x * grid.y * nb >= PRE_INWG_TILES) {
         // enough output tiles to fill the chip: each workgroup runs its tile's splits in turn
         // (no partial sums through memory: 0.1-0.2 GB per GEMM at 16 utterances)
-        grid.z = 1;
+        grid.z = nb;
         q.part = nullptr;
         hipLaunchKernelGGL((gemm_f32_mfma_kernel<EPI, TAPS>), grid, dim3(256), 0, s, q);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
@@ -586,7 +674,9 @@ template <int EPI>
 static hipError_t launch_gemm_q8(const GemmP &p, hipStream_t s) {
     if (!p.Wd || p.K % 32 || p.conv_taps) return hipErrorInvalidValue;
     const int splits = p.part ? gemm_splits_q8(p.K) : 1;
-    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits);
+    const int nb = p.nbatch > 1 ? p.nbatch : 1;
+    if (nb > 1 && p.ln_w) return hipErrorInvalidValue;
+    dim3 grid((p.N + 63) / 64, (p.M + 63) / 64, splits * nb);
     GemmP q = p;
     if (splits == 1) q.part = nullptr;
     hipLaunchKernelGGL((gemm_q8_kernel<EPI>), grid, dim3(256), 0, s, q);
@@ -619,7 +709,12 @@ hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ldy, int M, float eps, hipStream_t s) {
-    hipLaunchKernelGGL(ln_rows_kernel, dim3(M), dim3(256), 0, s, X, ldx, w, Y, ldy, eps);
+    hipLaunchKernelGGL(ln_rows_kernel, dim3(M), dim3(RLN_T), 0, s, X, ldx, w, Y, ldy, eps);
+    return hipGetLastError();
+}
+hipError_t pre_ln_rows_multi(const float *X, int ldx, const float *w, long long sw, float *Y, int ldy, long long sy,
+                             int M, int nw, float eps, hipStream_t s) {
+    hipLaunchKernelGGL(ln_rows_multi_kernel, dim3(M, nw), dim3(RLN_T), 0, s, X, ldx, w, sw, Y, ldy, sy, eps);
     return hipGetLastError();
 }
 hipError_t pre_lt_tab_rows(const float *P, const float *lt_pos, const float *w, float eps, float *Y, int round,
@@ -633,6 +728,12 @@ hipError_t pre_round_bf16(const float *src, float *dst, size_t n, hipStream_t s)
     return hipGetLastError();
 }
 hipError_t pre_row_attn(const RowAttnP &p, hipStream_t s) {
+    static const bool old = getenv("MAGPIE_PRE_ROWATTN_OLD") != nullptr;  // A/B: a wave per (row, head)
+    if (!old) {
+        if (p.kv16) hipLaunchKernelGGL(row_attn_wg_kernel<true>, dim3(p.M, p.heads), dim3(MP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL(row_attn_wg_kernel<false>, dim3(p.M, p.heads), dim3(MP_BLOCK), 0, s, p);
+        return hipGetLastError();
+    }
     if (p.kv16) hipLaunchKernelGGL(row_attn_kernel<true>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(row_attn_kernel<false>, dim3((p.M * p.heads + 3) / 4), dim3(256), 0, s, p);
     return hipGetLastError();

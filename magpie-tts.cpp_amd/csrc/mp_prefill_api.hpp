@@ -47,7 +47,31 @@ struct GemmP {
     float ln_eps;
     int xround;        // 2: round every A element to f16 as it is loaded (an F16 weight: ggml's
                        //    F16 mul_mat rounds src1 to f16; products then exact in f32)
+    // batched (nbatch > 1): grid.z = nbatch x splits; batch z uses A + z sA, W (and Wq, Wd)
+    // + (z % wmod) sW (sWq, sWd), C + z sC and layer + z: every layer's XA K/V, or every
+    // (utterance, layer)'s K' / V', in one launch instead of one per layer (each is the same
+    // GEMM as alone: the same tiles, splits and order)
+    int nbatch, wmod;
+    long long sA, sW, sC, sWq, sWd;
 };
+
+// the batch of this workgroup (GemmP::nbatch): shifts p to it, returns the split count and
+// sets zs to the split index (blockIdx.z otherwise)
+__device__ __forceinline__ int gemm_batch_enter(GemmP &p, int &zs) {
+    const int nb = p.nbatch > 1 ? p.nbatch : 1;
+    const int S = (int)gridDim.z / nb, bz = (int)blockIdx.z / S;
+    zs = (int)blockIdx.z % S;
+    if (bz) {
+        const int wz = bz % (p.wmod > 0 ? p.wmod : nb);
+        p.A += bz * p.sA;
+        if (p.W) p.W += wz * p.sW;
+        if (p.Wq) p.Wq += wz * p.sWq;
+        if (p.Wd) p.Wd += wz * p.sWd;
+        if (p.C) p.C += bz * p.sC;
+        p.layer += bz;
+    }
+    return S;
+}
 
 // Split count of a preamble GEMM over K (fixed per K: batch-invariant results): K / 96
 // pieces, at most 16, whole 32-wide blocks (MP_PRE_KS = 128: K / 128 pieces with 8 steps of
@@ -101,6 +125,8 @@ struct RowXaP {
 };
 
 hipError_t pre_gemm(const GemmP &p, int epi, hipStream_t s);
+hipError_t pre_ln_rows_multi(const float *X, int ldx, const float *w, long long sw, float *Y, int ldy, long long sy,
+                             int M, int nw, float eps, hipStream_t s);
 hipError_t pre_ln_rows(const float *X, int ldx, const float *w, float *Y, int ldy, int M, float eps, hipStream_t s);
 // LT table rows: Y[r] = LN(P[r] + lt_pos[r / VCB + 1]) * w for r < 7 * VCB (the LN of
 // PRO_LTARG_ATTN's position, bit for bit), rounded to bf16 when `b16`

@@ -590,16 +590,19 @@ int load_model(mp_dev *dev, const char *path) {
         *gdst[k] = base;
         off += align_up((size_t)gsize[k] * 8 * 4);
     }
-    // W_q^T per decoder layer (for the per-utterance K' = K W_q of the fused XA)
-    for (float *p : m.xq_t) hipFree(p);
+    // W_q^T per decoder layer (for the per-utterance K' = K W_q of the fused XA), one
+    // allocation, layer l at l * 768 * 128 (the batched K' GEMM strides over it)
+    if (!m.xq_t.empty() && m.xq_t[0]) hipFree(m.xq_t[0]);
     m.xq_t.assign(m.dec_layers, nullptr);
     {
         std::vector<float> wq((size_t)128 * 768), wt((size_t)768 * 128);
+        float *all = nullptr;
+        HIPCHK(hipMalloc(&all, wt.size() * 4 * m.dec_layers));
         for (int l = 0; l < m.dec_layers; ++l) {
             HIPCHK(hipMemcpy(wq.data(), m.dec[l].xq, wq.size() * 4, hipMemcpyDeviceToHost));
             for (int j = 0; j < 128; ++j)
                 for (int n = 0; n < 768; ++n) wt[(size_t)n * 128 + j] = wq[(size_t)j * 768 + n];
-            HIPCHK(hipMalloc(&m.xq_t[l], wt.size() * 4));
+            m.xq_t[l] = all + (size_t)l * wt.size();
             HIPCHK(hipMemcpy(m.xq_t[l], wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
         }
     }
@@ -949,6 +952,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
         size_t cap = enc_gpart_elems(Me);
         auto need = [&](size_t M, int N, int K) { cap = std::max(cap, (size_t)mp::gemm_splits_max(K) * M * N); };
         need(Mc, 2304, 768); need(Mc, 3072, 768); need(Mc, 768, 3072); need(Mc, 768, 768);
+        need(Me, 256 * L, 768);  // the XA K/V GEMMs batched over layers
         A(gpart, cap);
     }
     if (const char *qd = getenv("MAGPIE_Q8DUMP"); qd && atoi(qd) != 0 && dev->m.weight_mode == MP_WEIGHTS_Q8) {
@@ -1650,28 +1654,67 @@ int run_preamble(mp_dev *dev) {
         const EncWs w{dev->tok, dev->T, NB, Tmax, dev->pX, dev->pH, dev->pQKV, dev->pATT, dev->pF, dev->gpart, dev->enc_out};
         if (int rc = run_encoder(dev, w, s)) return rc;
     }
-    // --- cross-attention K/V per layer (1663-1711)
-    for (int l = 0; l < L; ++l) {
-        HIPCHK(pre_ln_rows(dev->enc_out, 768, m.dec[l].norm_xmem, dev->pH, 768, Me, m.eps, s));
+    // --- cross-attention K/V per layer (1663-1711): LN(encoder output) with each layer's
+    //     norm_xmem, then kv_net. Layers whose tensors sit at one stride in the arena (the
+    //     loader places every layer's tensors alike) run G at a time: one LN launch for G
+    //     weight vectors, one batched GEMM (grid.z = G x splits) and its reduce, instead of
+    //     3 launches per layer; each layer's arithmetic is its own GEMM's
+    auto stride_of = [&](auto get) -> long long {  // elements between layers' tensors, or -1
+        if (L == 1) return 0;
+        const long long st = (long long)(get(1) - get(0));
+        for (int l = 2; l < L; ++l)
+            if ((long long)(get(l) - get(0)) != st * l) return -1;
+        return st;
+    };
+    const long long s_norm = stride_of([&](int l) { return m.dec[l].norm_xmem; });
+    const long long s_xkv = stride_of([&](int l) { return m.dec[l].xkv; });
+    const bool q8kv = (bool)m.dec[0].xkv8;
+    const long long s_xkvq = q8kv ? stride_of([&](int l) { return m.dec[l].xkv8.q; }) : 0;
+    const long long s_xkvd = q8kv ? stride_of([&](int l) { return m.dec[l].xkv8.d; }) : 0;
+    const size_t pf_rows = (size_t)NB * std::max(Tmax, (int)CTX);
+    const int G = (s_norm >= 0 && s_xkv >= 0 && s_xkvq >= 0 && s_xkvd >= 0)
+                      ? (int)std::max<size_t>(1, std::min<size_t>(L, pf_rows * 3072 / ((size_t)Me * 768)))
+                      : 1;
+    for (int l0 = 0; l0 < L; l0 += G) {
+        const int g = std::min(G, L - l0);
+        HIPCHK(pre_ln_rows_multi(dev->enc_out, 768, m.dec[l0].norm_xmem, s_norm, dev->pF, 768, (long long)Me * 768, Me, g,
+                                 m.eps, s));
         GemmP gp{};
-        gp.A = dev->pH; gp.lda = 768; gp.W = m.dec[l].xkv; gp.Wq = m.dec[l].xkv8.q; gp.Wd = m.dec[l].xkv8.d; gp.M = Me; gp.N = 256; gp.K = 768; gp.rows_per_utt = Tmax;
-        gp.T = dev->T; gp.xak = dev->xak; gp.xav = dev->xav; gp.layer = l; gp.nlayers = L; gp.Tmax = Tmax;
+        gp.A = dev->pF; gp.lda = 768; gp.W = m.dec[l0].xkv; gp.Wq = m.dec[l0].xkv8.q; gp.Wd = m.dec[l0].xkv8.d; gp.M = Me; gp.N = 256; gp.K = 768; gp.rows_per_utt = Tmax;
+        gp.T = dev->T; gp.xak = dev->xak; gp.xav = dev->xav; gp.layer = l0; gp.nlayers = L; gp.Tmax = Tmax;
+        gp.nbatch = g; gp.wmod = g; gp.sA = (long long)Me * 768; gp.sW = s_xkv; gp.sWq = s_xkvq; gp.sWd = s_xkvd;
         HIPCHK(pre_gemm(gp, GE_XAKV, s));
     }
     // --- K'_t = W_q^T K_t, V'_t = W_o V_t per utterance and layer (decode-time fused XA;
-    //     not with Q8_0 q_net / o_net, whose activations ggml quantises: unfused XA there)
-    for (int b = 0; b < NB; ++b)
-        for (int l = 0; l < L; ++l) {
-            if (m.dec[l].xq8 || dev->xa_direct) continue;
-            const size_t xo = ((size_t)(b * L + l) * Tmax) * 128, po = ((size_t)(b * L + l) * Tmax) * 768;
-            GemmP gp{};
-            gp.A = dev->xak + xo; gp.lda = 128; gp.W = m.xq_t[l]; gp.C = dev->kp + po; gp.ldc = 768;
-            gp.M = Tmax; gp.N = 768; gp.K = 128; gp.rows_per_utt = Tmax;
-            gp.xround = -1;
-            HIPCHK(pre_gemm(gp, GE_STORE, s));
-            gp.A = dev->xav + xo; gp.W = m.dec[l].xo; gp.C = dev->vp + po;
-            HIPCHK(pre_gemm(gp, GE_STORE, s));
-        }
+    //     not with Q8_0 q_net / o_net, whose activations ggml quantises: unfused XA there).
+    //     Every (utterance, layer) pair in one batched GEMM each (K = 128: no split): A rows
+    //     at stride Tmax x 128, weights of layer (pair % L), outputs at stride Tmax x 768
+    bool any_xq8 = false;
+    for (int l = 0; l < L; ++l) any_xq8 |= (bool)m.dec[l].xq8;
+    const long long s_xo = stride_of([&](int l) { return m.dec[l].xo; });
+    if (!dev->xa_direct && !any_xq8 && s_xo >= 0) {
+        GemmP gp{};
+        gp.A = dev->xak; gp.lda = 128; gp.W = m.xq_t[0]; gp.C = dev->kp; gp.ldc = 768;
+        gp.M = Tmax; gp.N = 768; gp.K = 128; gp.rows_per_utt = Tmax;
+        gp.xround = -1;
+        gp.nbatch = NB * L; gp.wmod = L; gp.sA = (long long)Tmax * 128; gp.sW = 768 * 128; gp.sC = (long long)Tmax * 768;
+        HIPCHK(pre_gemm(gp, GE_STORE, s));
+        gp.A = dev->xav; gp.W = m.dec[0].xo; gp.C = dev->vp; gp.sW = s_xo;
+        HIPCHK(pre_gemm(gp, GE_STORE, s));
+    } else {
+        for (int b = 0; b < NB; ++b)
+            for (int l = 0; l < L; ++l) {
+                if (m.dec[l].xq8 || dev->xa_direct) continue;
+                const size_t xo = ((size_t)(b * L + l) * Tmax) * 128, po = ((size_t)(b * L + l) * Tmax) * 768;
+                GemmP gp{};
+                gp.A = dev->xak + xo; gp.lda = 128; gp.W = m.xq_t[l]; gp.C = dev->kp + po; gp.ldc = 768;
+                gp.M = Tmax; gp.N = 768; gp.K = 128; gp.rows_per_utt = Tmax;
+                gp.xround = -1;
+                HIPCHK(pre_gemm(gp, GE_STORE, s));
+                gp.A = dev->xav + xo; gp.W = m.dec[l].xo; gp.C = dev->vp + po;
+                HIPCHK(pre_gemm(gp, GE_STORE, s));
+            }
+    }
     // --- baked context + 110-frame causal prefill (3991-4060, 4167-4238)
     const int Mc = NB * CTX;
     HIPCHK(pre_embed_context(dev->spk, NB, m.baked, m.dec_pos, dev->pX, s));
@@ -1858,7 +1901,7 @@ void mp_hip_free(mp_dev *dev) {
     if (dev->m.q8_arena) hipFree(dev->m.q8_arena);
     if (dev->m.q8p_arena) hipFree(dev->m.q8p_arena);
     for (void *p : dev->lt_allocs) hipFree(p);
-    for (float *p : dev->m.xq_t) hipFree(p);
+    if (!dev->m.xq_t.empty() && dev->m.xq_t[0]) hipFree(dev->m.xq_t[0]);  // one allocation (load_model)
     if (dev->h_ndone) hipHostFree(dev->h_ndone);
     for (hipEvent_t e : dev->sev)
         if (e) hipEventDestroy(e);

@@ -37,6 +37,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -1207,6 +1208,12 @@ struct mp_codec {
     // CUs (hipExtStreamCreateWithCUMask), for codec rounds that run beside a decode in flight
     hipStream_t bg_stream = nullptr;
     int bg = 0, bg_cus = 0;
+    // pinned host staging of the codes in / audio out: a copy from or to pageable memory is
+    // staged synchronously by the runtime and waited for the decode's queued work too
+    // (configs[2]: each overlapped round's codec finished only after the decode's next chunk)
+    int32_t *h_codes_pin = nullptr;
+    float *h_audio_pin = nullptr;
+    size_t h_codes_cap = 0, h_audio_cap = 0;
     float last_ms = 0.f;  // device time of the last decode (launch sequence only)
     int *rb_ctr = nullptr;  // rb_kernel's item counters, one per launch of a decode (zeroed per decode)
     // diagnostics (MAGPIE_CODEC_TS=stage,block,file): the phase stamps of one rb_kernel launch
@@ -1589,7 +1596,23 @@ int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, 
     CHK(hipSetDevice(c->device));
     CodecStreamScope scope(c);
     if (int rc = ensure_buffers(c, n_chunks, chunk_frames)) return rc;
-    CHK(hipMemcpyAsync(c->codes, codes, (size_t)n_chunks * 8 * chunk_frames * 4, hipMemcpyHostToDevice, c->stream));
+    const size_t ncodes = (size_t)n_chunks * 8 * chunk_frames, nsamp = (size_t)n_chunks * chunk_frames * mpc::HOP;
+    if (c->h_codes_cap < ncodes) {
+        if (c->h_codes_pin) hipHostFree(c->h_codes_pin);
+        c->h_codes_pin = nullptr;
+        c->h_codes_cap = 0;
+        CHK(hipHostMalloc((void **)&c->h_codes_pin, ncodes * 4, hipHostMallocDefault));
+        c->h_codes_cap = ncodes;
+    }
+    if (c->h_audio_cap < nsamp) {
+        if (c->h_audio_pin) hipHostFree(c->h_audio_pin);
+        c->h_audio_pin = nullptr;
+        c->h_audio_cap = 0;
+        CHK(hipHostMalloc((void **)&c->h_audio_pin, nsamp * 4, hipHostMallocDefault));
+        c->h_audio_cap = nsamp;
+    }
+    memcpy(c->h_codes_pin, codes, ncodes * 4);
+    CHK(hipMemcpyAsync(c->codes, c->h_codes_pin, ncodes * 4, hipMemcpyHostToDevice, c->stream));
     if (!c->ev0) { CHK(hipEventCreate(&c->ev0)); CHK(hipEventCreate(&c->ev1)); }
     // diagnostics: MAGPIE_CODEC_TS=stage,block,file -> the phase stamps of that stage's
     // rb_kernel launch for residual block `block` (tools_dev/codec_rb_timeline.py)
@@ -1614,8 +1637,9 @@ int mp_hip_codec_decode_chunks(mp_codec *c, const int32_t *codes, int n_chunks, 
     CHK(hipEventRecord(c->ev0, c->stream));
     if (int rc = codec_run(c, n_chunks, chunk_frames)) return rc;
     CHK(hipEventRecord(c->ev1, c->stream));
-    CHK(hipMemcpyAsync(audio_out, c->audio, (size_t)n_chunks * chunk_frames * mpc::HOP * 4, hipMemcpyDeviceToHost, c->stream));
+    CHK(hipMemcpyAsync(c->h_audio_pin, c->audio, nsamp * 4, hipMemcpyDeviceToHost, c->stream));
     CHK(hipStreamSynchronize(c->stream));
+    memcpy(audio_out, c->h_audio_pin, nsamp * 4);
     CHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
     if (c->ts_dev && !c->ts_file.empty()) {
         std::vector<unsigned long long> h(TS_N);
@@ -1651,9 +1675,7 @@ extern "C" int mp_codec_set_background(mp_codec *c, int cus) {
         int ncu = 0;
         CHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
         if (cus >= ncu) { c->bg = 0; return MP_OK; }
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        const int step = std::max(1, ncu / cus);  // every step-th CU: spread over the XCDs
-        for (int i = 0, n = 0; i < ncu && n < cus; i += step, ++n) mask[i / 32] |= 1u << (i % 32);
+        const std::vector<uint32_t> mask = mp::cu_share_mask(ncu, cus, false);
         CHK(hipExtStreamCreateWithCUMask(&c->bg_stream, (uint32_t)mask.size(), mask.data()));
         c->bg_cus = cus;
     }
@@ -1666,6 +1688,8 @@ void mp_hip_codec_free(mp_codec *c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->bg_stream) { hipStreamSynchronize(c->bg_stream); hipStreamDestroy(c->bg_stream); }
+    if (c->h_codes_pin) hipHostFree(c->h_codes_pin);
+    if (c->h_audio_pin) hipHostFree(c->h_audio_pin);
     for (void *p : c->weight_allocs) hipFree(p);
     if (c->ts_dev) hipFree(c->ts_dev);
     if (c->rb_ctr) hipFree(c->rb_ctr);

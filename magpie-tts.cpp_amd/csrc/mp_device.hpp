@@ -1,6 +1,8 @@
 // Device-side helpers shared by the gfx950 kernels (wave64 reductions, vector
 // loads, block reductions). CDNA4 only: wave = 64 lanes, 256-thread workgroups.
 #pragma once
+#include <stdint.h>
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -21,6 +23,21 @@ inline void launch(void (*k)(A...), dim3 grid, dim3 block, unsigned shm, hipStre
     if (g_kev[0]) hipExtLaunchKernelGGL(k, grid, block, shm, s, g_kev[0], g_kev[1], 0, args...);
     else hipLaunchKernelGGL(k, grid, block, shm, s, args...);
 }
+
+// Host: the CU mask of a stream confined to `cus` of `ncu` CUs (every (ncu / cus)-th CU, so the
+// share is spread over the XCDs), or its complement. The codec's background stream takes the
+// share, the frame loop's stream during an overlapped streaming round the complement
+// (hipExtStreamCreateWithCUMask): the two never wait for each other's workgroups.
+inline std::vector<uint32_t> cu_share_mask(int ncu, int cus, bool complement) {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    std::vector<char> in(ncu, 0);
+    const int step = cus > 0 ? (ncu / cus > 1 ? ncu / cus : 1) : ncu + 1;
+    for (int i = 0, n = 0; i < ncu && n < cus; i += step, ++n) in[i] = 1;
+    for (int i = 0; i < ncu; ++i)
+        if ((in[i] != 0) != complement) mask[i / 32] |= 1u << (i % 32);
+    return mask;
+}
+
 }  // namespace mp
 
 // ---- wave64 reductions on DPP (data-parallel primitives move lanes inside the

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <memory>
 #include <string>
 #include <type_traits>
@@ -330,6 +331,10 @@ struct mp_dev {
     // per-call hipFree would synchronise the whole device, stalling other streams' work)
     char *enc_ws = nullptr;
     size_t enc_ws_bytes = 0;
+    // streaming rounds overlapped with a background codec: the frame loop on the CUs the
+    // codec's background stream leaves (cu_share_mask complement), created on first use
+    hipStream_t stream_fg = nullptr;
+    int stream_fg_cus = 0;
     // diagnostics (MAGPIE_Q8DUMP=1 at mp_hip_begin_batch, Q8_0 weights): one dump slot per
     // int8-MFMA decode GEMM launch of the iteration (GemvP::q8dump), records in q8dump_index
     char *q8dump = nullptr;
@@ -1907,6 +1912,7 @@ void mp_hip_free(mp_dev *dev) {
         if (e) hipEventDestroy(e);
     if (dev->h_codes) hipHostFree(dev->h_codes);
     if (dev->enc_ws) hipFree(dev->enc_ws);
+    if (dev->stream_fg) { hipStreamSynchronize(dev->stream_fg); hipStreamDestroy(dev->stream_fg); }
     if (dev->stream) hipStreamDestroy(dev->stream);
     delete dev;
 }
@@ -2070,9 +2076,10 @@ int prepare_iteration(mp_dev *dev) {
     return reset_decode_state(dev);
 }
 
-int launch_iteration(mp_dev *dev) {
-    if (eager_mode()) return enqueue_iteration(dev, dev->stream, false);
-    HIPCHK(hipGraphLaunch(dev->exec, dev->stream));
+int launch_iteration(mp_dev *dev, hipStream_t s = nullptr) {
+    if (!s) s = dev->stream;
+    if (eager_mode()) return enqueue_iteration(dev, s, false);
+    HIPCHK(hipGraphLaunch(dev->exec, s));
     return MP_OK;
 }
 
@@ -2147,6 +2154,16 @@ int mp_hip_decode(mp_dev *dev, int32_t *codes_out, int32_t *n_frames) {
 // (chunks are independent, magpie.cpp:4739-4742: the audio is the same); the
 // frames reach the host through a pinned mirror filled on the decode stream.
 extern "C" int mp_codec_set_background(mp_codec *c, int cus);  // mp_codec.hip (internal)
+// MAGPIE_STREAM_ASYNC=0: queue each chunk from the calling thread (default 1: a helper thread)
+static bool stream_async() {
+    const char *e = getenv("MAGPIE_STREAM_ASYNC");
+    return !(e && atoi(e) == 0);
+}
+// MAGPIE_STREAM_TRACE=1: host-side timeline of the streaming loop on stderr (diagnostics)
+static bool stream_trace() {
+    const char *e = getenv("MAGPIE_STREAM_TRACE");
+    return e && atoi(e) != 0;
+}
 // MAGPIE_CODEC_BG_CUS: CUs of the codec's background stream while a decode is in flight
 // (default 64 of 256; 0 = the codec's own stream, the whole chip, for every round)
 static int codec_bg_cus() {
@@ -2189,26 +2206,42 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
     int it = 0;
     bool first = true;
     dev->timing = mp_timing{dev->timing.preamble_ms, 0.0, 0, 0, 0.0};
-    auto enqueue_chunk = [&](int slot) -> int {
+    // the stream the last chunk was queued on (the stop writes below follow it)
+    hipStream_t cur = dev->stream;
+    auto enqueue_chunk = [&](int slot, hipStream_t st) -> int {
         const int n_it = std::min(fpc, S - it);
         for (int i = 0; i < n_it; ++i)
-            if (int rc = launch_iteration(dev)) return rc;
+            if (int rc = launch_iteration(dev, st)) return rc;
         // the frames these iterations wrote (columns it..it+n_it of every slot) to the
         // pinned mirror, on the decode stream: no host copy waits on the GPU later
         HIPCHK(hipMemcpy2DAsync(dev->h_codes + (size_t)it * 8, (size_t)S * 32, dev->codes_out + (size_t)it * 8,
-                                (size_t)S * 32, (size_t)n_it * 32, NB, hipMemcpyDeviceToHost, dev->stream));
+                                (size_t)S * 32, (size_t)n_it * 32, NB, hipMemcpyDeviceToHost, st));
         it += n_it;
         int *h = snap + (size_t)slot * 3 * NB;
-        HIPCHK(hipMemcpyAsync(h, dev->step, NB * 4, hipMemcpyDeviceToHost, dev->stream));
-        HIPCHK(hipMemcpyAsync(h + NB, dev->done, NB * 4, hipMemcpyDeviceToHost, dev->stream));
-        HIPCHK(hipMemcpyAsync(h + 2 * NB, dev->nframes, NB * 4, hipMemcpyDeviceToHost, dev->stream));
-        HIPCHK(hipEventRecord(dev->sev[slot], dev->stream));
+        HIPCHK(hipMemcpyAsync(h, dev->step, NB * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(h + NB, dev->done, NB * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(h + 2 * NB, dev->nframes, NB * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(dev->sev[slot], st));
         return MP_OK;
     };
+    // rounds whose codec runs in the background: the decode on the complementary CUs. Every
+    // chunk is queued after the previous one landed (the host waited for its event), so
+    // moving between the two streams needs no other ordering.
+    const int bg_cus = codec_bg_cus();
+    const bool split_cus = B * fpc >= CODEC_BG_MIN_FRAMES && bg_cus > 0 && stream_async();
+    if (split_cus && (!dev->stream_fg || dev->stream_fg_cus != bg_cus)) {
+        if (dev->stream_fg) { HIPCHK(hipStreamSynchronize(dev->stream_fg)); hipStreamDestroy(dev->stream_fg); dev->stream_fg = nullptr; }
+        int ncu = 0, least = 0, greatest = 0;
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev->device));
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        const std::vector<uint32_t> mask = mp::cu_share_mask(ncu, bg_cus, true);
+        HIPCHK(hipExtStreamCreateWithCUMask(&dev->stream_fg, (uint32_t)mask.size(), mask.data()));
+        dev->stream_fg_cus = bg_cus;
+    }
     struct Job { int b, f0, n; };
     std::vector<Job> jobs;
     int slot = 0;
-    if (int rc = enqueue_chunk(0)) return rc;
+    if (int rc = enqueue_chunk(0, dev->stream)) return rc;
     for (;;) {
         HIPCHK(hipEventSynchronize(dev->sev[slot]));
         const int *h_step = snap + (size_t)slot * 3 * NB, *h_done = h_step + NB, *h_nf = h_step + 2 * NB;
@@ -2218,9 +2251,23 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
         // the next chunk's iterations are queued before this round's codec work, so
         // the decode runs on its stream while the codec runs on the codec's (bit-exact
         // beside it: tests/test_concurrency_gpu.py); a stop requested by a callback
-        // below takes effect after that chunk, whose frames are then not delivered
-        if (more)
-            if (int rc = enqueue_chunk(slot ^ 1)) return rc;
+        // below takes effect after that chunk, whose frames are then not delivered.
+        // Queuing a chunk's graph replays can block the host (the queue's packet slots fill
+        // up: 32 iterations of 65 launches), which left the codec waiting behind the next
+        // chunk's decode, serialising the two (configs[2]: 27.2k vs 27.5k frames/s serial,
+        // r06d): a round with codec work large enough to matter queues the chunk from a
+        // helper thread while this thread runs the codec (HIP calls are thread-safe; the
+        // helper touches only the decode stream and its pinned snapshot)
+        const double t_wait = ms_since(t0);
+        std::future<int> queued;
+        const bool async_q = more && stream_async() && B * fpc >= CODEC_BG_MIN_FRAMES;  // (a thread per round)
+        if (more) {
+            cur = async_q && split_cus ? dev->stream_fg : dev->stream;
+            if (async_q) queued = std::async(std::launch::async, [&, sl = slot ^ 1, st = cur]() { return enqueue_chunk(sl, st); });
+            else if (int rc = enqueue_chunk(slot ^ 1, cur)) return rc;
+        }
+        if (stream_trace()) fprintf(stderr, "[stream] round at %.3f ms: chunk landed, next queued %s at %.3f ms\n", t_wait,
+                                    async_q ? "(async)" : "", ms_since(t0));
         // this round's chunks, utterance by utterance, in delivery order
         jobs.clear();
         for (int b = 0; b < B; ++b) {
@@ -2266,6 +2313,9 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
                 if (int rc = mp_hip_codec_decode(codec, cbm.data() + at[q] * 8 * fpc, jobs[q].n,
                                                  audio.data() + at[q] * fpc * 1024))
                     return fail(dev, rc, std::string("codec: ") + mp_hip_codec_error(codec));
+        if (stream_trace()) fprintf(stderr, "[stream]   codec of %zu chunks done at %.3f ms\n", jobs.size(), ms_since(t0));
+        if (queued.valid())
+            if (int rc = queued.get()) return rc;
         for (size_t q = 0, b = 0; b < (size_t)B; ++b) {
             for (; q < jobs.size() && jobs[q].b == (int)b; ++q) {
                 const Job &j = jobs[q];
@@ -2280,8 +2330,8 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
                     // the callback asked to stop (4820-4824): the utterance ends here
                     stopped[b] = 1;
                     const int one = 1;
-                    HIPCHK(hipMemcpyAsync(dev->done + b, &one, 4, hipMemcpyHostToDevice, dev->stream));
-                    HIPCHK(hipStreamSynchronize(dev->stream));
+                    HIPCHK(hipMemcpyAsync(dev->done + b, &one, 4, hipMemcpyHostToDevice, cur));
+                    HIPCHK(hipStreamSynchronize(cur));
                 }
             }
             if ((h_done[b] != 0 || stopped[b]) && !ended[b]) {  // end-of-utterance notice: (utt, NULL, 0)
@@ -2293,6 +2343,7 @@ int mp_hip_decode_stream(mp_dev *dev, mp_codec *codec, int frames_per_chunk, mp_
         slot ^= 1;
     }
     HIPCHK(hipStreamSynchronize(dev->stream));
+    if (dev->stream_fg) HIPCHK(hipStreamSynchronize(dev->stream_fg));
     if (int rc = check_handoff(dev)) return rc;
     dev->timing.decode_ms = ms_since(t0);
     dev->timing.iterations = it;

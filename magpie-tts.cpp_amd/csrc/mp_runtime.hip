@@ -2168,7 +2168,7 @@ static bool stream_trace() {
 // (default 64 of 256; 0 = the codec's own stream, the whole chip, for every round)
 static int codec_bg_cus() {
     const char *e = getenv("MAGPIE_CODEC_BG_CUS");
-    return e ? atoi(e) : 64;
+    return e ? atoi(e) : 0;
 }
 // codec rounds of at least this many frames go to the background stream while the decode
 // continues (throughput: configs[2]'s 16 slots x 32-frame chunks); smaller rounds (a stream's

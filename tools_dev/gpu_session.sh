@@ -116,9 +116,10 @@ for STEP in "$@"; do
       python3 tools_dev/preamble_report.py "$d/prof_kernel_trace.csv" 3 > "$d.txt"
       head -1 "$d.txt"; grep "wall ms" "$d.log" ;;
     prewall)
-      # preamble wall time without the profiler: arg weights:B:T[:LIB]
-      IFS=: read -r w b t lib <<< "${arg:-f32:1:64}"
-      MAGPIE_LIB="${lib:+$PWD/ab_libs/$lib.so}" timeout -k 10 200 python3 -u tools_dev/preamble_prof.py "$w" "$b" "$t" 10 ;;
+      # preamble wall time without the profiler: arg weights:B:T[:LIB[:K=V]]
+      IFS=: read -r w b t lib kv <<< "${arg:-f32:1:64}"
+      echo -n "[$lib $kv] "
+      env MAGPIE_LIB="${lib:+$PWD/ab_libs/$lib.so}" $kv timeout -k 10 200 python3 -u tools_dev/preamble_prof.py "$w" "$b" "$t" 10 ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

@@ -964,6 +964,207 @@ __global__ __launch_bounds__(64 * RWV * CWV, (rb_minw<RWV, CWV, NT>())) void rb_
     }
 }
 
+// ---- A whole ResLayer branch per item (rl_kernel, the 64- and 32-channel stages): the
+// three residual blocks of one branch (dilations 1, 3, 5) over one time tile, x kept in
+// registers between them. rb_kernel reads and writes every block's f32 residual stream
+// (these stages' T is 131k-262k steps per 8 chunks: 100-200 MB per launch); here each tile
+// reads x once and writes the layer's output once. A tile of W columns (column c = time
+// ts + c) computes block b's outputs only where they are complete: a block's causal
+// receptive field is (ks - 1)(d + 1) columns, so after block b the columns from H_b =
+// (ks - 1) sum_{b' <= b} (d_b' + 1) on are exact and the tile outputs columns
+// [12 (ks - 1), W) (fragments wholly left of what a block needs are skipped). Rows left of
+// column 0 and times < 0 are zero, as every conv's causal padding is. Per time step the
+// operands, A / B fragments, (channel block, tap) accumulation order and the (x + conv_1) + b
+// epilogue are rb_kernel's: the same bits (tests/test_codec_gpu.py).
+struct RlP {
+    const float *x;                        // the ResLayer input (the convT output) [chunk][T][CP] f32
+    float *out[3];                         // each branch's output
+    const _Float16 *Wd[3][3], *W1[3][3];   // [branch][block] A-fragment order (Conv::wf)
+    const float *bd[3][3], *b1[3][3], *al_in[3][3], *al_sk[3][3];
+    int ks[3];
+    int nsnake, creal, T;
+    int bn[3], tpc[3];  // per branch: outputs per tile (W - 12 (ks - 1)), tiles per chunk
+    int order[3];       // branches heaviest first: items [first[k], first[k + 1]) are branch order[k]
+    int first[4];
+};
+constexpr int RL_HALO = RB_MAXHALO;  // zero rows left of column 0: conv_d's (ks - 1) d at most
+#ifndef MP_RL_NT32
+#define MP_RL_NT32 2  // 16-column fragments per wave, 32-channel stage (8 column waves)
+#endif
+#ifndef MP_RL_NT64
+#define MP_RL_NT64 4  // 64-channel stage (4 column waves)
+#endif
+
+template <int KS, int RWV, int CWV, int NT, int R>
+__device__ __forceinline__ void rl_body(const RlP &p, char *xs, int br, int tile) {
+    constexpr int NCB = RWV, CPD = NCB * 32, W = 16 * NT * CWV, XR = W + RL_HALO, NTH = 64 * RWV * CWV;
+    constexpr int NS = NCB * KS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rw = w % RWV, cw = w / RWV;
+    const int kg = lane >> 4, l16 = lane & 15;
+    const int chunk = tile / p.tpc[br];
+    const int ts = (tile % p.tpc[br]) * p.bn[br] - 12 * (KS - 1);  // time of column 0
+    const size_t cbase = (size_t)chunk * p.T * CPD;
+    const int chl = rw * 32 + 4 * kg;       // each lane's channels: chl + 16 a + r
+    const int cwb = cw * 16 * NT;           // this wave's first column
+    // x in the accumulator layout: fragment (a, j), lane: column cwb + 16 j + l16
+    floatx4 xr[C2_WR][NT];
+#pragma unroll
+    for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int t = ts + cwb + 16 * j + l16;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t >= 0 && t < p.T) v = *(const float4 *)(p.x + cbase + (size_t)t * CPD + chl + 16 * a);
+            xr[a][j] = floatx4{v.x, v.y, v.z, v.w};
+        }
+    // the zero rows left of column 0, every channel block (never written after)
+    constexpr int ZQ = RL_HALO * RB_ROWB / 16;
+    for (int i = tid; i < NCB * ZQ; i += NTH)
+        *(uint4 *)(xs + (size_t)(i / ZQ) * XR * RB_ROWB + (i % ZQ) * 16) = make_uint4(0, 0, 0, 0);
+    // v -> HalfSnake(v [+ bias]) -> f16 -> LDS row HALO + c of this lane's channel block; 0 at t < 0
+    auto put = [&](const floatx4 (&v)[C2_WR][NT], const float *alpha, const float *bias) {
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        float4 als[C2_WR], bbs[C2_WR];
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a) {
+            als[a] = *(const float4 *)(alpha + chl + a * 16);
+            bbs[a] = bias ? *(const float4 *)(bias + chl + a * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a) {
+            const int ch = chl + a * 16;
+            const float av[4] = {als[a].x, als[a].y, als[a].z, als[a].w};
+            const float bv[4] = {bbs[a].x, bbs[a].y, bbs[a].z, bbs[a].w};
+            auto frag = [&](auto hs) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const int c = cwb + j * 16 + l16;
+                    half4 h;
+                    if (bias) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) h[r] = (_Float16)hs(v[a][j][r] + bv[r], r);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) h[r] = (_Float16)hs(v[a][j][r], r);
+                    }
+                    if (ts + c < 0) h = half4{0, 0, 0, 0};
+                    *(half4 *)(xs + rw * XR * RB_ROWB + (RL_HALO + c) * RB_ROWB + (a * 16 + 4 * kg) * 2) = h;
+                }
+            };
+            const int kind = hs_wave_kind(ch, ch + 3, p.nsnake, p.creal);
+            if (kind == 0) frag([&](float x, int r) { return hs_snake(x, av[r]); });
+            else if (kind == 1) frag([&](float x, int) { return hs_leaky(x); });
+            else frag([&](float x, int r) { return half_snake_sel(x, ch + r, p.nsnake, p.creal, av[r]); });
+        }
+    };
+    // one causal conv from the LDS operand: column c, tap k reads row rowoff + c + k dk; the
+    // fragments below jlo are skipped (wave-uniform)
+    floatx4 acc[C2_WR][NT];
+    half8 ring[R][C2_WR];
+    auto conv = [&](const _Float16 *wf, int rowoff, int dk, int jlo) {
+        const _Float16 *wrow0 = wf + (size_t)(rw * 2) * NS * 512 + lane * 8, *wrow1 = wrow0 + (size_t)NS * 512;
+#pragma unroll
+        for (int q = 0; q < R; ++q)
+            if (q < NS) {
+                ring[q][0] = *(const half8 *)(wrow0 + (size_t)q * 512);
+                ring[q][1] = *(const half8 *)(wrow1 + (size_t)q * 512);
+            }
+        const char *bbase = xs + (cwb + l16 + rowoff) * RB_ROWB + 16 * kg;
+        auto bfrag = [&](int st, int j) {
+            return *(const half8 *)(bbase + (st / KS) * XR * RB_ROWB + (j * 16 + (st % KS) * dk) * RB_ROWB);
+        };
+        half8 bc[NT], bn[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bc[j] = bfrag(0, j);
+#pragma unroll
+        for (int st = 0; st < NS; ++st) {
+            if (st + 1 < NS) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) bn[j] = bfrag(st + 1, j);
+            }
+            if constexpr (RB_PIN >= 2) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                if (j >= jlo) {
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][0], bc[j], acc[0][j], 0, 0, 0);
+                    acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ring[st % R][1], bc[j], acc[1][j], 0, 0, 0);
+                }
+            }
+            if (st + R < NS) {
+                ring[st % R][0] = *(const half8 *)(wrow0 + (size_t)(st + R) * 512);
+                ring[st % R][1] = *(const half8 *)(wrow1 + (size_t)(st + R) * 512);
+            }
+            if constexpr (RB_PIN >= 1) __builtin_amdgcn_sched_barrier(0);
+            if (st + 1 < NS) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) bc[j] = bn[j];
+            }
+        }
+    };
+    // the first fragment of this wave holding a column >= need
+    auto first_frag = [&](int need) { return need > cwb ? (need - cwb) >> 4 : 0; };
+    int hdone = 0;  // columns from which the current x is exact
+#pragma unroll 1
+    for (int b = 0; b < 3; ++b) {
+        const int d = DIL[b];
+        put(xr, p.al_in[br][b], nullptr);  // HS_in(x)
+        __syncthreads();
+        // conv_d: column c = time ts + c, x row HALO + c - (KS - 1) d + k d
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[a][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        const int need_d = hdone + (KS - 1) * d, need_1 = need_d + (KS - 1);
+        conv(p.Wd[br][b], RL_HALO - (KS - 1) * d, d, first_frag(need_d));
+        __syncthreads();  // every wave is done reading the x rows
+        put(acc, p.al_sk[br][b], p.bd[br][b]);  // h = HS_sk(conv_d + bd)
+#pragma unroll
+        for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[a][j] = xr[a][j];  // conv_1's accumulator starts at x
+        __syncthreads();
+        conv(p.W1[br][b], RL_HALO - (KS - 1), 1, first_frag(need_1));
+        {
+            float4 bb[C2_WR];
+#pragma unroll
+            for (int a = 0; a < C2_WR; ++a) bb[a] = *(const float4 *)(p.b1[br][b] + chl + a * 16);
+#pragma unroll
+            for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    xr[a][j] = floatx4{acc[a][j][0] + bb[a].x, acc[a][j][1] + bb[a].y, acc[a][j][2] + bb[a].z,
+                                       acc[a][j][3] + bb[a].w};  // (x + conv_1) + b
+        }
+        hdone = need_1;
+        if (b < 2) __syncthreads();  // conv_1's h reads done before the next HS_in rows
+    }
+    // the exact columns [12 (KS - 1), W) inside the chunk
+#pragma unroll
+    for (int a = 0; a < C2_WR; ++a)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int c = cwb + 16 * j + l16, t = ts + c;
+            if (c < hdone || t >= p.T) continue;
+            *(float4 *)(p.out[br] + cbase + (size_t)t * CPD + chl + 16 * a) =
+                make_float4(xr[a][j][0], xr[a][j][1], xr[a][j][2], xr[a][j][3]);
+        }
+}
+
+template <int RWV, int CWV, int NT>
+__global__ __launch_bounds__(64 * RWV * CWV, 2) void rl_kernel(RlP p) {
+    __shared__ __attribute__((aligned(16))) char xs[RWV * (16 * NT * CWV + RL_HALO) * RB_ROWB];
+    const int it = blockIdx.x;
+    if (it >= p.first[3]) return;
+    const int k = it < p.first[1] ? 0 : it < p.first[2] ? 1 : 2;
+    const int br = p.order[k], tile = it - p.first[k];
+    switch (p.ks[br]) {
+        case 3: rl_body<3, RWV, CWV, NT, RB_RING>(p, xs, br, tile); break;
+        case 7: rl_body<7, RWV, CWV, NT, RB_RING>(p, xs, br, tile); break;
+        default: rl_body<11, RWV, CWV, NT, RB_RING>(p, xs, br, tile); break;
+    }
+}
+
 // Grouped ConvTranspose1d (nano-codec.cpp:481-565), HalfSnake on its input,
 // optional 3-branch mean before it: out[t][g] = b[g] + sum_{c in {2g,2g+1}}
 // sum_{tau: 0 <= t - tau*s < 2s} x[tau][c] * w[c][t - tau*s]; kept length T*s.
@@ -1430,6 +1631,36 @@ hipError_t run_rb(const mpc::RbP &p, int Cp, int nchunk, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+// one launch per ResLayer (rl_kernel) on the 64- and 32-channel stages (MAGPIE_CODEC_RL=0:
+// rb_kernel's three launches)
+bool rl_fused(int Cp) {
+    const char *e = getenv("MAGPIE_CODEC_RL");
+    const bool off = e && atoi(e) == 0;
+    return !off && (Cp == 64 || Cp == 32);
+}
+template <int RWV, int CWV, int NT>
+hipError_t launch_rl(mpc::RlP p, int nchunk, hipStream_t s) {
+    constexpr int W = 16 * NT * CWV;
+    static_assert(W > 12 * 10, "a tile must be wider than the 11-tap branch's receptive field");
+    for (int j = 0; j < 3; ++j) {
+        p.bn[j] = W - 12 * (p.ks[j] - 1);
+        p.tpc[j] = (p.T + p.bn[j] - 1) / p.bn[j];
+        p.order[j] = j;
+    }
+    std::sort(p.order, p.order + 3, [&](int a, int b) { return p.ks[a] > p.ks[b]; });
+    p.first[0] = 0;
+    for (int k = 0; k < 3; ++k) p.first[k + 1] = p.first[k] + nchunk * p.tpc[p.order[k]];
+    hipLaunchKernelGGL((mpc::rl_kernel<RWV, CWV, NT>), dim3(p.first[3]), dim3(64 * RWV * CWV), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t run_rl(const mpc::RlP &p, int Cp, int nchunk, hipStream_t s) {
+    switch (Cp) {
+        case 64: return launch_rl<2, 4, MP_RL_NT64>(p, nchunk, s);
+        case 32: return launch_rl<1, 8, MP_RL_NT32>(p, nchunk, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 hipError_t run_conv(const mpc::ConvP &p, int BM, int mode, int nchunk, int nbranch, hipStream_t s) {
     using namespace mpc;
     // ResLayer convs: the wide-tile kernel once a chunk fills at least half a tile
@@ -1503,6 +1734,22 @@ int codec_run(mp_codec *c, int nchunk, int F) {
         }
         CHK(hipGetLastError());
         T *= RATE[i];
+        if (fused && rl_fused(Cp)) {
+            RlP lp{};
+            lp.x = c->x0;
+            for (int j = 0; j < 3; ++j) {
+                lp.out[j] = c->brb[j];
+                lp.ks[j] = KS[j];
+                for (int k = 0; k < 3; ++k) {
+                    const mp_codec::Conv &cd = c->rb[i][j][k][0], &c1 = c->rb[i][j][k][1];
+                    lp.Wd[j][k] = cd.wf; lp.W1[j][k] = c1.wf; lp.bd[j][k] = cd.b; lp.b1[j][k] = c1.b;
+                    lp.al_in[j][k] = c->rb_alpha[i][j][k][0]; lp.al_sk[j][k] = c->rb_alpha[i][j][k][1];
+                }
+            }
+            lp.nsnake = C / 2; lp.creal = C; lp.T = T;
+            CHK(run_rl(lp, Cp, nchunk, s));
+            continue;
+        }
         if (fused) {
             // x0 -> brb (block 0) -> rbt (block 1) -> brb (block 2): out of place, since a
             // tile reads its left neighbour's rows as halo

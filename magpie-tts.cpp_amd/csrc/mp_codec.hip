@@ -989,7 +989,7 @@ struct RlP {
 };
 constexpr int RL_HALO = RB_MAXHALO;  // zero rows left of column 0: conv_d's (ks - 1) d at most
 #ifndef MP_RL_NT32
-#define MP_RL_NT32 2  // 16-column fragments per wave, 32-channel stage (8 column waves)
+#define MP_RL_NT32 4  // 16-column fragments per wave, 32-channel stage
 #endif
 #ifndef MP_RL_NT64
 #define MP_RL_NT64 4  // 64-channel stage (4 column waves)
@@ -1151,8 +1151,20 @@ __device__ __forceinline__ void rl_body(const RlP &p, char *xs, int br, int tile
         }
 }
 
+#ifndef MP_RL_W32
+#define MP_RL_W32 2  // minimum waves per SIMD the register allocation must allow, 32-channel stage
+#endif
+#ifndef MP_RL_W64
+#define MP_RL_W64 2
+#endif
+#ifndef MP_RL_CWV32
+#define MP_RL_CWV32 4  // column waves, 32-channel stage
+#endif
+#ifndef MP_RL_CWV64
+#define MP_RL_CWV64 4  // column waves, 64-channel stage
+#endif
 template <int RWV, int CWV, int NT>
-__global__ __launch_bounds__(64 * RWV * CWV, 2) void rl_kernel(RlP p) {
+__global__ __launch_bounds__(64 * RWV * CWV, RWV == 1 ? MP_RL_W32 : MP_RL_W64) void rl_kernel(RlP p) {
     __shared__ __attribute__((aligned(16))) char xs[RWV * (16 * NT * CWV + RL_HALO) * RB_ROWB];
     const int it = blockIdx.x;
     if (it >= p.first[3]) return;
@@ -1631,12 +1643,15 @@ hipError_t run_rb(const mpc::RbP &p, int Cp, int nchunk, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
-// one launch per ResLayer (rl_kernel) on the 64- and 32-channel stages (MAGPIE_CODEC_RL=0:
-// rb_kernel's three launches)
+// one launch per ResLayer (rl_kernel) on the 32-channel stage; MAGPIE_CODEC_RL=0: rb_kernel's
+// three launches there too, 2: rl_kernel on the 64-channel stage as well. Measured per stage
+// (8 x 32 frames, gpurun_out/r06j_cprof*): 32 channels 232 us (rb, 3 launches) -> 193 us
+// (rl, 4 waves x 64 columns) / 225-238 us (8 waves x 32 or 64 columns); 64 channels 274 us
+// (rb) against 340-394 us (rl: 167 VGPRs, one 8-wave workgroup per CU).
 bool rl_fused(int Cp) {
     const char *e = getenv("MAGPIE_CODEC_RL");
-    const bool off = e && atoi(e) == 0;
-    return !off && (Cp == 64 || Cp == 32);
+    const int mode = e ? atoi(e) : 1;
+    return (Cp == 32 && mode >= 1) || (Cp == 64 && mode >= 2);
 }
 template <int RWV, int CWV, int NT>
 hipError_t launch_rl(mpc::RlP p, int nchunk, hipStream_t s) {
@@ -1655,8 +1670,8 @@ hipError_t launch_rl(mpc::RlP p, int nchunk, hipStream_t s) {
 }
 hipError_t run_rl(const mpc::RlP &p, int Cp, int nchunk, hipStream_t s) {
     switch (Cp) {
-        case 64: return launch_rl<2, 4, MP_RL_NT64>(p, nchunk, s);
-        case 32: return launch_rl<1, 8, MP_RL_NT32>(p, nchunk, s);
+        case 64: return launch_rl<2, MP_RL_CWV64, MP_RL_NT64>(p, nchunk, s);
+        case 32: return launch_rl<1, MP_RL_CWV32, MP_RL_NT32>(p, nchunk, s);
     }
     return hipErrorInvalidValue;
 }

@@ -421,7 +421,10 @@ hipError_t op_lt_inh_1(const GemvP &p, hipStream_t s) { return launch_gemv<1, 1,
 hipError_t op_lt_in0_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, D, PRO_LN, EPI_BIAS>(p, s); }
 // Q8_0 weight mode at 16 slots: the FFN convs (F32 in the reference's Q8 file)
 hipError_t op_ff1_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 2, D, PRO_LN, EPI_GELU>(p, s); }
-hipError_t op_ff2_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
+#ifndef MP_RW_FF2_16
+#define MP_RW_FF2_16 1
+#endif
+hipError_t op_ff2_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, MP_RW_FF2_16, DFF, PRO_PLAIN, EPI_ADD_STORE>(p, s); }
 // the direct XA's f32 q_net at 16 slots (bf16 mode)
 hipError_t op_xq_16(const GemvP &p, hipStream_t s) { return launch_gemv<16, 1, D, PRO_LN, EPI_STORE>(p, s); }
 

@@ -839,9 +839,23 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
         lds_sync();
 
     } else if constexpr (PRO == PRO_PLAIN) {
-        for (int b = 0; b < NB; ++b)
-            for (int k = tid * 4; k < K; k += MP_BLOCK * 4)
-                *(float4 *)(act + b * K + k) = *(const float4 *)(p.src + (size_t)b * p.src_ld + k);
+        // PG float4 loads in flight per thread, then their LDS stores: the rolled
+        // load -> store loop waited one memory round trip per float4 (the Q8_0 file's F32
+        // FFN down at 16 slots: 24 per thread, 18.9 us per launch)
+        constexpr int ITEMS = NB * (K / 4), PT = (ITEMS + MP_BLOCK - 1) / MP_BLOCK, PG = PT < 12 ? PT : 12;
+        for (int u0 = 0; u0 < PT; u0 += PG) {
+            f32x4 v[PG];
+#pragma unroll
+            for (int u = 0; u < PG; ++u) {
+                const int e = min((u0 + u) * MP_BLOCK + tid, ITEMS - 1);  // every element assigned
+                v[u] = *(const f32x4 *)(p.src + (size_t)(e / (K / 4)) * p.src_ld + (e % (K / 4)) * 4);
+            }
+#pragma unroll
+            for (int u = 0; u < PG; ++u) {
+                const int e = (u0 + u) * MP_BLOCK + tid;
+                if (u0 + u < PT && e < ITEMS) *(f32x4 *)(act + (e / (K / 4)) * K + (e % (K / 4)) * 4) = v[u];
+            }
+        }
         lds_sync();
     } else if constexpr (PRO == PRO_LN && NB >= 2) {
         ln_slots<NB, K>(p, [&](int b, int k, float y) { act[b * K + k] = y; });

@@ -991,6 +991,7 @@ mp::GemvP gemv_base(mp_dev *dev) {
 int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vector<mp::OpRec> *ops);
 bool q8_unfused();
 bool lt_cand_mode();
+bool sa16_fused(int weight_mode);
 
 // Enqueue one decode iteration: decoder step at pos (embedding codes_prev), LT
 // over 8 codebooks, finalize. When `record` is set, the op list is rebuilt for
@@ -1048,12 +1049,11 @@ int enqueue_iteration_body(mp_dev *dev, hipStream_t s, bool record) {
         // batches still reproduce single runs (at 8 slots the SA merge runs in the QKV launch)
         const bool merge16 = NB >= 8 && m.weight_mode == MP_WEIGHTS_BF16 && !dev->xa_direct;
         if (merge16) { a.merged = dev->sa_out; a.gh = dev->sagh; a.iter = dev->ndone + 1; a.hx_err = dev->ndone + 2; }
-        // (not at 16 slots: bf16 B=16 20.1k vs 21.5k frames/s; both forms compute the
-        // same bits)
+        // (at 16 slots too unless MAGPIE_SA16=0, sa16_fused; both forms compute the same bits)
         // (Q8_0: the same hand-off in the int8 MFMA launch, mp_decode_q8.hip; MAGPIE_Q8_UNFUSED=1
         // keeps the separate launches, which compute the same bits)
         const bool q8_fuse = !q8_unfused();
-        const bool sa_in_qkv = (W.qkv8 ? q8_fuse && tq.qkv_sa : tb.qkv_sa != nullptr) && NB < 16;
+        const bool sa_in_qkv = (W.qkv8 ? q8_fuse && tq.qkv_sa : tb.qkv_sa != nullptr) && (NB < 16 || sa16_fused(m.weight_mode));
         {
             mp::GemvFn fn = W.qkv8 ? tq.qkv : tb.qkv;
             if (sa_in_qkv) {
@@ -1210,6 +1210,15 @@ bool eager_mode() {
 bool lt_cand_mode() {
     const char *e = getenv("MAGPIE_LT_CAND");
     return e && atoi(e) != 0;
+}
+// The SA in the QKV launch at 16 slots: MAGPIE_SA16 unset = the bf16 mode's, 1 = every
+// mode's, 0 = none (A/B; both forms compute the same bits). Round 3 kept it separate (bf16
+// B=16 20.1k vs 21.5k frames/s then); since round 4's single pollers the fused form is
+// faster: 31,891 -> 32,620 / 32,893 frames/s (qkv 4.54 + sa_attn 7.34 -> qkv_sa 11.05 us
+// per layer; gpurun_out/r06l_ops_bf16_b16*)
+bool sa16_fused(int weight_mode) {
+    const char *e = getenv("MAGPIE_SA16");
+    return e ? atoi(e) != 0 : weight_mode == MP_WEIGHTS_BF16;
 }
 bool q8_unfused() {
     const char *e = getenv("MAGPIE_Q8_UNFUSED");

@@ -22,7 +22,9 @@ def main():
     only = set(sys.argv[3:])
     cache = os.environ.get("MAGPIE_CACHE", "/tmp/magpie_amd_cache")
     os.makedirs(cache, exist_ok=True)
-    model = ma.synth_gguf(os.path.join(cache, "magpie_357m_f32_k32.gguf"), lt_head_scale=ma.DECISIVE)
+    fn, dt = {"q8": ("magpie_357m_q8_k32.gguf", "q8_0"), "q4": ("magpie_357m_q4_k32.gguf", "q4_0"),
+              "f16": ("magpie_357m_f16_k32.gguf", "f16")}.get(weights, ("magpie_357m_f32_k32.gguf", "f32"))
+    model = ma.synth_gguf(os.path.join(cache, fn), dtype=dt, lt_head_scale=ma.DECISIVE)
     dump = os.path.join(REPO, "gpurun_out", "ts_dump.bin")
     os.makedirs(os.path.dirname(dump), exist_ok=True)
     os.environ["MAGPIE_TS_DUMP"] = dump

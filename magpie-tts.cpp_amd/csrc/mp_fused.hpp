@@ -867,16 +867,27 @@ __device__ __forceinline__ void prologue(const GemvP &p, float *act, float *red,
     } else if constexpr (PRO == PRO_LTX_LN) {
         // one wave per slot at every batch size (wave_block_meanvar), so a batch
         // reproduces its utterances run alone bit for bit
+        // (every owned slot's row loaded before the first slot's arithmetic: one memory
+        // round trip per wave, not one per slot)
         const int lane = tid & 63, w = tid >> 6;
-        float g[4];
+        constexpr int SPW = (NB + MP_NWAVES - 1) / MP_NWAVES;
+        float g[4], ps[4], xs[SPW][4];
         load_lnw<4>(p.lnw, g);
-        for (int b = w; b < NB; b += MP_NWAVES) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ps[i] = p.lt_pos[(size_t)p.cb * LTD + lane + 64 * i];
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int b = min(w + MP_NWAVES * j, NB - 1);  // every element assigned
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xs[j][i] = p.lt_s[((size_t)b * 9 + p.cb) * LTD + lane + 64 * i];
+        }
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int b = w + MP_NWAVES * j;
+            if (b >= NB) break;  // wave-uniform
             float X[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int k = lane + 64 * i;
-                X[i] = p.lt_s[((size_t)b * 9 + p.cb) * LTD + k] + p.lt_pos[(size_t)p.cb * LTD + k];
-            }
+            for (int i = 0; i < 4; ++i) X[i] = xs[j][i] + ps[i];
             if (blockIdx.x == 0)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) p.ltX[(size_t)b * LTD + lane + 64 * i] = X[i];

@@ -992,6 +992,7 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
 bool q8_unfused();
 bool lt_cand_mode();
 bool sa16_fused(int weight_mode);
+int split_merge8();
 
 // Enqueue one decode iteration: decoder step at pos (embedding codes_prev), LT
 // over 8 codebooks, finalize. When `record` is set, the op list is rebuilt for
@@ -1047,8 +1048,10 @@ int enqueue_iteration_body(mp_dev *dev, hipStream_t s, bool record) {
         // 1 / SPLITS of its head's / slot's outputs), not by every O-projection / FFN-up
         // workgroup's prologue (196 / 245 KiB each at 16 slots); the same arithmetic, so
         // batches still reproduce single runs (at 8 slots the SA merge runs in the QKV launch)
-        const bool merge16 = NB >= 8 && m.weight_mode == MP_WEIGHTS_BF16 && !dev->xa_direct;
-        if (merge16) { a.merged = dev->sa_out; a.gh = dev->sagh; a.iter = dev->ndone + 1; a.hx_err = dev->ndone + 2; }
+        const bool mb16 = m.weight_mode == MP_WEIGHTS_BF16 && !dev->xa_direct;
+        const bool merge_sa = mb16 && (NB >= 16 || (NB == 8 && (split_merge8() & 1)));
+        const bool merge_xa = mb16 && (NB >= 16 || (NB == 8 && (split_merge8() & 2)));
+        if (merge_sa) { a.merged = dev->sa_out; a.gh = dev->sagh; a.iter = dev->ndone + 1; a.hx_err = dev->ndone + 2; }
         // (at 16 slots too unless MAGPIE_SA16=0, sa16_fused; both forms compute the same bits)
         // (Q8_0: the same hand-off in the int8 MFMA launch, mp_decode_q8.hip; MAGPIE_Q8_UNFUSED=1
         // keeps the separate launches, which compute the same bits)
@@ -1107,11 +1110,11 @@ int enqueue_iteration_body(mp_dev *dev, hipStream_t s, bool record) {
         } else if (xa_in_oproj) {
             // f32: the fused XA rides in the O-projection's launch on a hand-off of x1
             mp::GemvFn fn = tb.oproj_xa;
-            if (merge16) {
+            if (merge_sa) {  // the SA output merged by its split workgroups: plain rows
                 g.part = nullptr; g.src = dev->sa_out; g.src_ld = 768;
-                xp.x2 = dev->x2; xp.gh = dev->xagh;
                 fn = NB == 16 ? mp::b16_oproj_xa_pm_16 : mp::b16_oproj_xa_pm_8;
             }
+            if (merge_xa) { xp.x2 = dev->x2; xp.gh = dev->xagh; }  // x2 merged by the XA workgroups
             g.xa = xp; g.xh = dev->xh; g.iter = dev->ndone + 1; g.hx_err = dev->ndone + 2;
             if ((rc = run("oproj_xa", fn, g, F * (768.0 * 768) + A * act * (768 * 3) + xa_bytes)) != MP_OK)
                 return rc;
@@ -1154,7 +1157,7 @@ int enqueue_iteration_body(mp_dev *dev, hipStream_t s, bool record) {
         // LN + FFN up + GELU (1796-1799)
         g = gemv_base(dev); g.layer = l;
         g.W = W.ff1; g.Wb = b16 ? m.pk_ff1[l] : nullptr; g.N = 3072; g.lnw = W.norm_ff; g.out = dev->h; g.out_ld = 3072;
-        if (xa_dir || merge16) {  // x2 materialised by the direct XA / the XA tail's merge
+        if (xa_dir || merge_xa) {  // x2 materialised by the direct XA / the XA tail's merge
             g.src = dev->x2; g.src_ld = 768;
             if (b16) g.out_b16 = dev->h_b16;
             if ((rc = run("ff1", tb.ff1, g, F * (3072.0 * 768) + A * act * ((768 + 3072)))) != MP_OK) return rc;
@@ -1219,6 +1222,13 @@ bool lt_cand_mode() {
 bool sa16_fused(int weight_mode) {
     const char *e = getenv("MAGPIE_SA16");
     return e ? atoi(e) != 0 : weight_mode == MP_WEIGHTS_BF16;
+}
+// At 8 bf16 slots, which split states the split workgroups merge themselves (bit 0: SA, in
+// the QKV launch; bit 1: XA, in the O-projection's) rather than the consumers' prologues
+// (PRO_SA_MERGE, PRO_XA_LN): MAGPIE_MERGE8, default 3 (A/B; every setting the same bits)
+int split_merge8() {
+    const char *e = getenv("MAGPIE_MERGE8");
+    return e ? atoi(e) : 3;
 }
 bool q8_unfused() {
     const char *e = getenv("MAGPIE_Q8_UNFUSED");

@@ -50,8 +50,8 @@ CODEC_CHUNK = 32  # the CLI decodes stateless 32-frame chunks (magpie-tts.cpp:18
 FRAMES = 256
 SCALE_BATCH = 8  # configs[3]: batch 64 split 8 per GPU
 TEXT_TOKENS = 64
-PMC_TRAFFIC = "r05fin_pmc_decode_f32_b1.json"  # per-op HBM bytes of the N=1 workload (tools_dev/pmc_report.py)
-PMC_CODEC = "r05fin_pmc_codec.json"  # codec MFMA busy cycles + bytes per kernel (tools_dev/pmc_report.py)
+PMC_TRAFFIC = "r06fin_pmc_decode_f32_b1.json"  # per-op HBM bytes of the N=1 workload (tools_dev/pmc_report.py)
+PMC_CODEC = "r06fin_pmc_codec.json"  # codec MFMA busy cycles + bytes per kernel (tools_dev/pmc_report.py)
 
 
 def decoder_bytes_per_frame(B: int, L_mean: float, T: int, dec_layers: int = 12, weights: str = "f32") -> float:

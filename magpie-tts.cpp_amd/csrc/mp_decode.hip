@@ -1050,7 +1050,8 @@ __device__ __forceinline__ void lt_front_pre(const LtFrontP &p, int n_in, LtFron
 __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_in, const float4 (&wi)[3], float4 wk,
                                                float4 wv, const float4 (&a1)[LTF_UPW], const float4 (&a2)[LTF_U / 4],
                                                const float (&v)[D / 64], const float (&g)[D / 64], const LtFrontPre &q,
-                                               float *act, float *act2, float *xs, float *fs, float4 *y4, float4 *v4) {
+                                               float *act, float *act2, float *xs, float *fs, float4 *y4, float4 *v4,
+                                               float4 *k4 = nullptr) {
     constexpr int U = LTF_U, UPW = LTF_UPW, PER = D / 64, Q = PER / MP_NWAVES;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const unsigned tag_s = (unsigned)p.iter[0] * 64u + 40u, tag_v = tag_s + 1u;
@@ -1118,6 +1119,9 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
             p.l.ltv[n_in] = vo0;
             __hip_atomic_store((gu64 *)p.gh + LTD + n_in, ((unsigned long long)tag_v << 32) | __float_as_uint(vo0),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k4)  // (lt_all_kernel: k_0 too, every workgroup attends over it)
+                __hip_atomic_store((gu64 *)p.gh + 2 * LTD + n_in, ((unsigned long long)tag_v << 32) | __float_as_uint(k0),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // ---- codebook 0's FFN step (lt_ffn2_kernel<1>: y = X_0 + vo_0, wave 0), in the
@@ -1126,6 +1130,11 @@ __device__ __forceinline__ float lt_front_core(const LtFrontP &p, int pb, int n_
     if (w == 0) {
         float xv[4], vv[4];
         gh_wait_n<4, 1>(p.gh + LTD + 4 * lane, tag_v, vv, p.hx_err);  // vo_0 outputs 4 lane + c
+        if (k4) {
+            float kk[4];
+            gh_wait_n<4, 1>(p.gh + 2 * LTD + 4 * lane, tag_v, kk, p.hx_err);
+            *k4 = make_float4(kk[0], kk[1], kk[2], kk[3]);
+        }
         wave_lds_sync();  // (xs: the in_proj outputs this wave stored above)
         const float pb4[4] = {q.posb.x, q.posb.y, q.posb.z, q.posb.w};
 #pragma unroll
@@ -1218,6 +1227,198 @@ hipError_t op_lt_front(const LtFrontP &p, hipStream_t s) {
         !p.l.ltk || !p.l.ltv || !p.l.step || p.l.cb != 0)
         return hipErrorInvalidValue;
     mp::launch(lt_front_kernel, dim3(LTFR_G), dim3(MP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- the whole LT, f32 batch 1 greedy
+// LtAllP (mp_params.hpp). Workgroup pb: the front (lt_front_core), then per codebook cb its
+// FFN-down partial sums published, outputs 4 pb .. 4 pb + 3 merged (lt_ffn_merge's order: the
+// 64 partials ascending, then + y), y2 swept, head rows 32 pb .. 32 pb + 31 of codebook cb
+// (gemv_kernel<1, *, 256, PRO_LTFFN_MERGE, EPI_BIAS>'s per-row arithmetic) and the workgroup's
+// masked first-max key; wave 0 then picks codebook cb's code from the 64 keys (+ EOS's while
+// EOS is allowed: the first max of wave_pick_rows), gathers position cb + 1's table rows and
+// computes y as lt_y_attend with the earlier positions' k / vo rows kept in registers, and the
+// workgroup runs its 16 FFN units (lt_step_body's arithmetic). Codebook 7's code is the
+// finalize's pick from the logits. Three granule edges per codebook instead of two launches.
+constexpr int LTA_ROWS = 32, LTA_RPW = LTA_ROWS / MP_NWAVES;  // head rows per workgroup / wave
+static_assert(LTA_ROWS * LT_FFN_P >= VCB && LTFR_G == LT_FFN_P && LTA_RPW <= 64, "head split");
+// candidate key: the logit's order bits, then 2047 - id (lower ids win ties), then a 21-bit tag
+__device__ __forceinline__ unsigned long long lta_key(float v, int i, unsigned tc) {
+    const unsigned u = __float_as_uint(v);
+    const unsigned o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)o << 32) | ((unsigned long long)(2047u - (unsigned)i) << 21) | tc;
+}
+__device__ __forceinline__ int lta_index(unsigned long long k) { return 2047 - (int)((k >> 21) & 2047u); }
+__global__ __launch_bounds__(MP_BLOCK) void lt_all_kernel(LtAllP p) {
+    const unsigned long long t_start = ts_begin(p.f.l.f.ts);
+    __shared__ __attribute__((aligned(16))) float act[D];
+    __shared__ __attribute__((aligned(16))) float act2[LTD];
+    __shared__ __attribute__((aligned(16))) float xs[LTD];
+    __shared__ __attribute__((aligned(16))) float fs[LTF_U];
+    __shared__ __attribute__((aligned(16))) float ys[LTD];
+    __shared__ float mv[LT_FFN_P][4];
+    __shared__ unsigned long long ck[MP_NWAVES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, pb = blockIdx.x;
+    const int n_in = pb * MP_NWAVES + w + ts_dep(t_start);
+    constexpr int PER = D / 64;
+    float v[PER], g[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = p.f.x[lane + 64 * i];
+    load_lnw<PER>(p.f.norm_out, g);
+    LtFrontPre q;
+    lt_front_pre(p.f, n_in, q);
+    const int stp = p.f.l.step[0];
+    const unsigned it = (unsigned)p.f.iter[0];
+    const float4 gln = q.gff;  // the LT FFN LayerNorm weights [4 lane .. 4 lane + 3]
+    __builtin_amdgcn_sched_barrier(0);
+    float4 wi[3], wk, wv, a1[LTF_UPW], a2[LTF_U / 4];
+    lt_front_weights(p.f, pb, n_in, wi, wk, wv, a1, a2);
+    __builtin_amdgcn_sched_barrier(0);
+    float4 y4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = y4, k4 = y4;
+    float acc = lt_front_core(p.f, pb, n_in, wi, wk, wv, a1, a2, v, g, q, act, act2, xs, fs, &y4, &v4, &k4);
+    LtYPre r;  // wave 0: the positions' k / vo rows (lt_y_attend's operands)
+#pragma unroll
+    for (int j = 0; j < NCB - 1; ++j) r.kr[j] = r.vr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    r.kr[0] = to_v4(k4);
+    r.vr[0] = to_v4(v4);
+    if (w == 0) *(float4 *)&ys[4 * lane] = y4;
+    LtFfn2P lp = p.f.l;
+    const bool eos_ok = !(lp.ignore_eos || stp < 4);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+        const unsigned tag_p = it * 64u + 48u + (unsigned)cb, tag_y = it * 64u + 56u + (unsigned)cb;
+        const unsigned tc = ((it * 8u + (unsigned)cb) % 0x1FFFFFu) + 1u;
+        // codebook cb's head rows first: their latency under the two sweeps
+        const int n0 = pb * LTA_ROWS + w * LTA_RPW, nl = n0 + lane;
+        float4 hw[LTA_RPW];
+#pragma unroll
+        for (int rr = 0; rr < LTA_RPW; ++rr) {
+            const int n = min(n0 + rr, VCB - 1);
+            hw[rr] = ld_lt((const float4 *)(p.w_out + ((size_t)cb * VCB + n) * LTD + 4 * lane));
+        }
+        const float hb = lane < LTA_RPW && nl < VCB ? p.b_out[(size_t)cb * VCB + nl] : 0.f;
+        __builtin_amdgcn_sched_barrier(0);
+        // this thread's FFN-down partial sum (output tid), then outputs 4 pb + t % 4 from
+        // partial t / 4 (the 64 partials in ascending order, + y: lt_ffn_merge)
+        __hip_atomic_store((gu64 *)p.gp + pb * LTD + tid, ((unsigned long long)tag_p << 32) | __float_as_uint(acc),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        {
+            float vv[1];
+            gh_wait_n<1, 1>(p.gp + (tid >> 2) * LTD + 4 * pb + (tid & 3), tag_p, vv, p.f.hx_err);
+            mv[tid >> 2][tid & 3] = vv[0];
+        }
+        lds_sync();
+        if (tid < 4) {
+            float s2 = mv[0][tid];
+#pragma unroll 8
+            for (int q2 = 1; q2 < LT_FFN_P; ++q2) s2 += mv[q2][tid];
+            const float y2 = s2 + ys[4 * pb + tid];
+            __hip_atomic_store((gu64 *)p.gy + 4 * pb + tid, ((unsigned long long)tag_y << 32) | __float_as_uint(y2),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        {
+            float vv[1];
+            gh_wait_n<1, 1>(p.gy + tid, tag_y, vv, p.f.hx_err);
+            act2[tid] = vv[0];
+        }
+        lds_sync();
+        // the head rows and this workgroup's masked first-max key
+        {
+            const float4 av = *(const float4 *)&act2[4 * lane];
+            float lv = 0.f;
+#pragma unroll
+            for (int rr = 0; rr < LTA_RPW; ++rr) {
+                float sacc = 0.f;
+                sacc += dotv(hw[rr], av);
+                const float sr = wave_sum(sacc);
+                if (lane == rr) lv = sr;
+            }
+            unsigned long long key = tc;  // no candidate: below every real key, this codebook's tag
+            if (lane < LTA_RPW && nl < VCB) {
+                const float logit = lv + hb;
+                p.logits[nl] = logit;
+                if (nl == lp.audio_eos)
+                    __hip_atomic_store((gu64 *)p.gc + LT_FFN_P, lta_key(logit, nl, tc), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                else if (!lt_forbidden(nl, true, lp.audio_bos, lp.audio_eos)) key = lta_key(logit, nl, tc);
+            }
+            key = wave_max_u64(key);
+            if (lane == 0) ck[w] = key;
+        }
+        if (cb == NCB - 1) break;  // codebook 7's code: the finalize's pick
+        lds_sync();
+        if (tid == 0) {
+            unsigned long long k = ck[0];
+#pragma unroll
+            for (int u = 1; u < MP_NWAVES; ++u) k = ck[u] > k ? ck[u] : k;
+            __hip_atomic_store((gu64 *)p.gc + pb, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (w == 0) {
+            // codebook cb's code from the 64 workgroup keys (+ EOS's while allowed)
+            unsigned long long k1 = 0, k2 = 0;
+            for (unsigned spins = 0;; ++spins) {
+                k1 = __hip_atomic_load((const gu64 *)p.gc + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                k2 = __hip_atomic_load((const gu64 *)p.gc + LT_FFN_P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__all((unsigned)(k1 & 0x1FFFFFull) == tc && (unsigned)(k2 & 0x1FFFFFull) == tc)) break;
+                if (spins >= HX_SPIN_LIMIT) {  // never seen: say so (the code falls back to 0)
+                    if (lane == 0) __hip_atomic_fetch_or((gi32 *)p.f.hx_err, HX_ERR_LT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    k1 = k2 = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0 && eos_ok && k2 > k1) k1 = k2;
+            k1 = wave_max_u64(k1);
+            int code = k1 ? lta_index(k1) : 0;
+            if (code < 0 || code >= VCB) code = 0;
+            // position cb + 1: the code's table rows, y = X + sum_j softmax_j vo_j (lt_y_attend)
+            lp.cb = cb + 1;
+            const LtRows gr = lt_gather(lp, code);
+            const float4 y = lt_y_attend(lp, 0, pb == 0, code, code, r, gr);
+            if (cb + 1 < NCB - 1) {
+                r.kr[cb + 1] = to_v4(gr.k4);
+                r.vr[cb + 1] = to_v4(gr.vo4);
+            }
+            if (pb == 0) *(float4 *)((float *)lp.f.y + 4 * lane) = y;
+            *(float4 *)&ys[4 * lane] = y;
+            const float x[4] = {y.x, y.y, y.z, y.w};
+            float mean, var;
+            wave_meanvar<4>(x, mean, var);
+            const float rstd = 1.0f / sqrtf(var + lp.f.eps);
+            *(float4 *)&xs[4 * lane] = make_float4(((x[0] - mean) * rstd) * gln.x, ((x[1] - mean) * rstd) * gln.y,
+                                                   ((x[2] - mean) * rstd) * gln.z, ((x[3] - mean) * rstd) * gln.w);
+        }
+        lds_sync();
+        // this workgroup's 16 FFN units of position cb + 1 (lt_step_body)
+        {
+            const float4 xv = *(const float4 *)&xs[4 * lane];
+            float uv[LTF_UPW];
+#pragma unroll
+            for (int rr = 0; rr < LTF_UPW; ++rr) uv[rr] = dotv(a1[rr], xv);
+            ffn_units_store<LTF_UPW>(uv, &fs[w * LTF_UPW], [](float gg) { return gg; });
+        }
+        lds_sync();
+        acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < LTF_U / 4; ++i) {
+            const float4 f4 = *(const float4 *)&fs[4 * i];
+            acc = fmaf(a2[i].x, f4.x, acc);
+            acc = fmaf(a2[i].y, f4.y, acc);
+            acc = fmaf(a2[i].z, f4.z, acc);
+            acc = fmaf(a2[i].w, f4.w, acc);
+        }
+    }
+    ts_end(p.f.l.f.ts, t_start);
+}
+hipError_t op_lt_all(const LtAllP &p, hipStream_t s) {
+    static_assert(sizeof(LtAllP) < 4096, "kernel argument size");
+    if (!p.f.x || !p.f.norm_out || !p.f.w_in || !p.f.b_in || !p.f.lt_s || !p.f.lt_pos || !p.f.norm_self || !p.f.w_kvo ||
+        !p.f.gh || !p.f.iter || !p.f.hx_err || !p.f.l.f.y || !p.f.l.f.lnw || !p.f.l.f.w1 || !p.f.l.f.w2 ||
+        !p.f.l.ltX || !p.f.l.ltk || !p.f.l.ltv || !p.f.l.step || !p.f.l.qkvtab || !p.f.l.votab || !p.f.l.ptab ||
+        !p.f.l.lt_pos || !p.f.l.codes_cur || !p.f.l.smp.argeos || p.f.l.cb != 0 || p.f.l.smp.on || !p.w_out ||
+        !p.b_out || !p.logits || !p.gp || !p.gy || !p.gc)
+        return hipErrorInvalidValue;
+    mp::launch(lt_all_kernel, dim3(LT_FFN_P), dim3(MP_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 

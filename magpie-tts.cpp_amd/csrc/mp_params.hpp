@@ -174,6 +174,23 @@ struct LtFrontP {
     int *hx_err;
 };
 
+// f32 mode at batch 1, greedy: the whole LT of a frame in ONE launch (lt_all_kernel, 64
+// workgroups): the front as lt_front_kernel (k_0 handed over too), then per codebook the
+// FFN-down partial sums as {tag, value} granules gp[64][256] (tag iter * 64 + 48 + cb), each
+// workgroup merging 4 of the 256 outputs in partial order into y2 granules gy[256] (+ 56 + cb),
+// every workgroup 32 head rows on the swept y2 and its masked first-max logit as one ordered
+// key gc[wg] (EOS's own key in gc[64]; the low 21 bits a per-codebook tag), and every
+// workgroup the next code from the 65 keys, that position's y and its 16 FFN units. Per row,
+// output and step the arithmetic of lt_ffn2_kernel<1> and the batch-1 head (same bits).
+struct LtAllP {
+    LtFrontP f;                  // the front; f.l: tables, FFN weights, y, codes, step, logits (read)
+    const float *w_out, *b_out;  // heads [8][2024][256], biases [8][2024]
+    float *logits;               // [2024] each codebook's logits (codebook 7's: the finalize's pick)
+    unsigned long long *gp;      // [LT_FFN_P][256]
+    unsigned long long *gy;      // [256]
+    unsigned long long *gc;      // [LT_FFN_P + 1]
+};
+
 // Frame embedding of every slot (layer 0's residual input, magpie.cpp:2746-2787,
 // 4376-4379): x[b] = (sum_cb emb[cb][code_cb]) / 8 + pos_emb[pos[b]]
 struct EmbP {

@@ -114,6 +114,7 @@ hipError_t op_lt_merge(const LtFfnP &, int, hipStream_t);
 hipError_t op_lt_ffn2(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_slot(const LtFfn2P &, int, hipStream_t);
 hipError_t op_lt_front(const LtFrontP &, hipStream_t);
+hipError_t op_lt_all(const LtAllP &, hipStream_t);
 hipError_t op_lt_slot_q8(const LtSlotQ8P &, int, hipStream_t);
 hipError_t op_lt_kvo(const GemvP &, int, hipStream_t);
 hipError_t op_sa_attn(const AttnP &, int, hipStream_t);
@@ -237,7 +238,11 @@ struct Model {
 };
 
 enum OpKind { K_GEMV = 0, K_ATTN = 1, K_FIN = 2, K_XA = 3, K_XAQ8 = 5, K_LTFFN = 6, K_LTMERGE = 7, K_LTPICK = 8, K_EMBED = 9,
-              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12, K_LTFRONT = 13, K_LTSLOTQ8 = 14 };
+              K_LTFFN2 = 10, K_LTKVO = 11, K_LTSLOT = 12, K_LTFRONT = 13, K_LTSLOTQ8 = 14, K_LTALL = 15 };
+// the f32 batch-1 LT's granules (one zeroed buffer): the front's in_proj / vo_0 / k_0, then
+// lt_all_kernel's FFN-down partials, y2 and workgroup keys
+constexpr size_t LTFG_GP = 3 * 256, LTFG_GY = LTFG_GP + (size_t)LT_FFN_P * 256, LTFG_GC = LTFG_GY + 256,
+                 LTFG_TOTAL = LTFG_GC + 128;
 struct OpRec {
     std::string name;
     int kind;
@@ -250,6 +255,7 @@ struct OpRec {
     LtFfnP lf;
     LtFfn2P l2;
     LtFrontP lf3;
+    LtAllP la;
     LtSlotQ8P lq8;
     EmbP e;
     int B;
@@ -264,7 +270,7 @@ struct LtIo {
     float *lt_s, *ltX, *ltY, *lty2, *ltq, *ltk, *ltv, *ltf, *logits;
     float *ltp;  // [NB][LT_FFN_P][256] partial FFN-down sums (lt_ffn_kernel; lt_slot_kernel: [NB][LTS_P][256])
     unsigned long long *ltgh;  // [NB][LTS_P or LTQ_P][256] lt_slot(_q8)_kernel's partial-sum granules
-    unsigned long long *ltfg;  // [2][256] lt_front_kernel's hand-off granules (f32, batch 1)
+    unsigned long long *ltfg;  // lt_front / lt_all_kernel's hand-off granules (f32, batch 1; LTFG_* below)
     unsigned long long *ltcand;  // [256] the f32 batch-1 head's workgroup candidates (GemvP::cand; null: off)
     unsigned long long *ltyg;  // [NB][256] lt_slot_q8_kernel's y granules (Q8_0 mode)
     int *iter, *hx_err;        // decode iteration counter (hand-off tags), hand-off error bits
@@ -626,6 +632,15 @@ static unsigned short bf16_bits(float x) {
 // f32 mode's LT (lt_ffn2_kernel) needs o_net applied to v rows ahead of time:
 // VO[c][v] = W_o V[c][v] for every table row, and [W_k ; W_o W_v] for position 0.
 bool f32_lt_mode(const mp::Model &m) { return m.weight_mode == MP_WEIGHTS_AS_STORED; }
+// MAGPIE_LT_ALL=1: the whole f32 batch-1 greedy LT of a frame in one launch (lt_all_kernel)
+// instead of the front + 7 x {lt_ffn2, lt_e} + lt_e launches (the same bits). Off by default:
+// its three granule edges per codebook (FFN-down partials -> 4-output merges -> y2 -> head
+// keys -> pick) cost ~9 us per codebook against 2 launches' ~9.2: 73.5 vs 76.7 us per frame
+// in the per-op timing, 2,967 vs 3,070 frames/s graph-replayed (gpurun_out/r06t_ops_f32_b1*)
+bool lt_all_mode() {
+    const char *e = getenv("MAGPIE_LT_ALL");
+    return e && atoi(e) != 0;
+}
 // the LT attention through the load-time q|k|vo tables in f32: the f32 mode, and the bf16
 // mode (whose LT FFN and heads are bf16: lt_slot_kernel + the bf16 head)
 bool lt_table_attn(const mp::Model &m) { return m.weight_mode == MP_WEIGHTS_AS_STORED || m.weight_mode == MP_WEIGHTS_BF16; }
@@ -943,7 +958,7 @@ int alloc_batch(mp_dev *dev, int B, int Tmax, int max_steps, bool trace) {
     A(xak, (size_t)NB * L * Tmax * 128); A(xav, (size_t)NB * L * Tmax * 128);
     A(lt_s, NB * 9 * 256); A(ltX, NB * 256); A(ltY, NB * 256); A(lty2, NB * 256); A(ltq, NB * 256);
     A(ltk, NB * 8 * 256); A(ltv, NB * 8 * 256); A(ltf, NB * 1024); A(logits, NB * 2024);
-    A(ltp, (size_t)NB * std::max({mp::LT_FFN_P, mp::LTS_P, mp::LTQ_P}) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, 2 * 256); A(ltyg, (size_t)NB * 256);
+    A(ltp, (size_t)NB * std::max({mp::LT_FFN_P, mp::LTS_P, mp::LTQ_P}) * 256); A(ltgh, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256); A(ltfg, mp::LTFG_TOTAL); A(ltyg, (size_t)NB * 256);
     A(ltcand, 256);  // zeroed: slots past the head's workgroups + EOS slot stay 0
     if (trace) A(trace, (size_t)NB * (max_steps + 1) * D);
     A(T, NB); A(spk, NB); A(pos, NB); A(step, NB); A(done, NB); A(nframes, NB); A(ndone, 4);  // ndone: [done count, iteration, hand-off timeout, -]
@@ -1400,6 +1415,23 @@ int enqueue_lt(mp_dev *dev, const mp::LtIo &io, int NB, hipStream_t s, std::vect
                 fp.lt_s = io.lt_s; fp.hidden_out = io.hidden; fp.lt_pos = m.lt_pos; fp.norm_self = m.lt_norm_self;
                 fp.w_kvo = m.lt_kvo; fp.gh = io.ltfg; fp.iter = io.iter; fp.hx_err = io.hx_err;
                 if (io.trace) { fp.trace = io.trace; fp.trace_steps = io.trace_steps; }
+                if (!io.sampling && lt_all_mode()) {
+                    // the whole LT in one launch (lt_all_kernel): the front, then every codebook's
+                    // FFN merge, head and greedy pick through granules; codebook 7's pick is the finalize's
+                    mp::LtAllP la{};
+                    la.f = fp; la.w_out = m.lt_out_w; la.b_out = m.lt_out_b; la.logits = io.logits;
+                    la.gp = io.ltfg + mp::LTFG_GP; la.gy = io.ltfg + mp::LTFG_GY; la.gc = io.ltfg + mp::LTFG_GC;
+                    if (ops) {
+                        mp::OpRec r{};
+                        r.name = "lt_all"; r.kind = mp::K_LTALL; r.la = la; r.B = NB;
+                        r.bytes = A * (256.0 * 768 + 512.0 * 256 + 1024.0 * 256 * 2 + 8.0 * 2024 * 256 + 8.0 * 2024) +
+                                  A * (768 * 2 + 256 * 4) + A * 7.0 * (3 * 256 + 2 * 256);
+                        ops->push_back(r);
+                    }
+                    HIPCHK(mp::op_lt_all(la, s));
+                    dump_lt(io, s);
+                    break;
+                }
                 if (ops) {
                     mp::OpRec r{};
                     r.name = "lt_front"; r.kind = mp::K_LTFRONT; r.lf3 = fp; r.B = NB;
@@ -2061,7 +2093,7 @@ int reset_decode_state(mp_dev *dev) {
     HIPCHK(hipMemsetAsync(dev->qh, 0, (size_t)NB * 3 * 768 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xqh, 0, (size_t)NB * 128 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->ltgh, 0, (size_t)NB * std::max(mp::LTS_P, mp::LTQ_P) * 256 * 8, dev->stream));
-    HIPCHK(hipMemsetAsync(dev->ltfg, 0, 2 * 256 * 8, dev->stream));
+    HIPCHK(hipMemsetAsync(dev->ltfg, 0, mp::LTFG_TOTAL * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->ltyg, 0, (size_t)NB * 256 * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->sagh, 0, (size_t)NB * mp::NH * mp::SA_SPLITS * mp::SA_PART * 8, dev->stream));
     HIPCHK(hipMemsetAsync(dev->xagh, 0, (size_t)NB * mp::XA_SPLITS * mp::XA_PART * 8, dev->stream));
@@ -2496,6 +2528,7 @@ static hipError_t launch_rec(const mp::OpRec &r, hipStream_t s) {
     case mp::K_LTFFN2: return mp::op_lt_ffn2(r.l2, r.B, s);
     case mp::K_LTSLOT: return mp::op_lt_slot(r.l2, r.B, s);
     case mp::K_LTFRONT: return mp::op_lt_front(r.lf3, s);
+    case mp::K_LTALL: return mp::op_lt_all(r.la, s);
     case mp::K_LTSLOTQ8: return mp::op_lt_slot_q8(r.lq8, r.B, s);
     case mp::K_LTKVO: return mp::op_lt_kvo(r.g, r.B, s);
     case mp::K_EMBED: return mp::op_embed(r.e, r.B, s);
@@ -2640,7 +2673,8 @@ int mp_hip_time_op(mp_dev *dev, int op, int reps, float *avg_us) {
     // iteration counter: relaunched with the same tag, its consumers would find the previous
     // launch's granules and not wait for their producers (a different, shorter critical path)
     const bool handoff = (r.kind == mp::K_GEMV && r.g.iter) || (r.kind == mp::K_LTSLOT && r.l2.gh) ||
-                         r.kind == mp::K_LTFRONT || r.kind == mp::K_LTSLOTQ8 || (r.kind == mp::K_ATTN && r.a.gh);
+                         r.kind == mp::K_LTFRONT || r.kind == mp::K_LTALL || r.kind == mp::K_LTSLOTQ8 ||
+                         (r.kind == mp::K_ATTN && r.a.gh);
     if (handoff)
         return fail(dev, MP_ERR_ARG, "op carries an in-launch hand-off: back-to-back timing would not wait for it");
     HIPCHK(launch());  // warm

@@ -695,6 +695,42 @@ def test_moved_special_ids_sampled_and_eos(ma, oracle, moved_ids_model, moved_id
 
 
 @pytest.mark.parametrize("which", ["decisive", "default_heads", "moved_ids", "moved_ids_eos", "eos"])
+def test_lt_all_equals_launch_sequence(ma, oracle, request, which):
+    """f32 batch 1, greedy: the whole local transformer of a frame in one launch (lt_all_kernel,
+    MAGPIE_LT_ALL=1, opt-in: measured slower; FFN merges, heads and picks through in-launch
+    granules, the pick from the 64 workgroups' masked first-max keys with EOS in its own slot)
+    computes the same codes and hidden states bit for bit as the launch sequence (MAGPIE_LT_ALL=0,
+    the default: the front, then 7 x {lt_ffn2, lt_e} and lt_e), and they equal the oracle's: the reference's special ids,
+    moved ids (the general mask), near-flat heads (near-ties) and EOS live."""
+    import os
+    path = {"decisive": "small_model", "default_heads": "full_model_default_heads", "moved_ids": "moved_ids_model",
+            "moved_ids_eos": "moved_ids_eos_model", "eos": "eos_model"}[which]
+    path = request.getfixturevalue(path)
+    ignore = which in ("decisive", "default_heads", "moved_ids")
+    steps = 24 if which == "default_heads" else 40
+    tok = ma.synthetic_tokens(20, seed=2400)
+    runs = {}
+    for mode in ("0", "1"):
+        os.environ["MAGPIE_LT_ALL"] = mode
+        try:
+            dev = ma.Device(path)
+            runs[mode] = dev.synthesize([tok], speakers=[2], max_dec_steps=steps, ignore_eos=ignore, trace=True)
+            dev.close()
+        finally:
+            os.environ.pop("MAGPIE_LT_ALL", None)
+    a, b = runs["0"], runs["1"]
+    assert int(a.n_frames[0]) == int(b.n_frames[0])
+    np.testing.assert_array_equal(a.codes[0], b.codes[0])
+    n = int(b.n_frames[0])
+    assert np.array_equal(a.hidden[0, :n + 1], b.hidden[0, :n + 1])
+    om = oracle.Model(path)
+    o = om.synthesize(tok, speaker=2, max_steps=steps, ignore_eos=ignore, trace=True)
+    om.close()
+    compare_codes(b.codes[0], o["codes"], o["margins"], min_frames=min(len(o["codes"]), 4))
+    print(f"{which}: {n} frames, one-launch LT == launch sequence bit for bit")
+
+
+@pytest.mark.parametrize("which", ["decisive", "default_heads", "moved_ids", "moved_ids_eos", "eos"])
 def test_lt_head_candidates_equal_logit_scan(ma, oracle, request, which):
     """f32 batch 1, greedy: the LT step picks codebook c-1's code from the head's ~253
     workgroup candidates (each head workgroup's masked first-max as an ordered key, EOS in

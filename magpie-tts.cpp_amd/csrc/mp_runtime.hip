@@ -1848,9 +1848,12 @@ int mp_hip_init(int device, mp_dev **out) {
     // the decode stream at the device's greatest priority: when the codec runs beside it (the
     // streaming loop, configs[2]'s overlapped chunks) the dispatcher serves the latency-bound
     // frame loop's workgroups first and the codec (least priority, mp_hip_codec_init) fills in
+    // (MAGPIE_STREAM_PRIO=0: the default priority, A/B)
     int least = 0, greatest = 0;
+    const char *pe = getenv("MAGPIE_STREAM_PRIO");
+    const bool prio = !pe || atoi(pe) != 0;
     if (hipSetDevice(device) != hipSuccess || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
-        hipStreamCreateWithPriority(&dev->stream, hipStreamNonBlocking, greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&dev->stream, hipStreamNonBlocking, prio ? greatest : 0) != hipSuccess ||
         hipHostMalloc((void **)&dev->h_ndone, 64, 0) != hipSuccess) {
         delete dev;
         return MP_ERR_HIP;

@@ -11,7 +11,7 @@
 #   ops=MODE:B[:LIB[:K=V]]  per-op dispatch intervals + wave spans (tools_dev/mode_ops.py);
 #                        LIB "-" = the default library; K=V e.g. MODE_XA=direct, MODE_KV=bf16
 #   tl=MODE:B[:OPS[:LIB]]  in-kernel phase timeline (tools_dev/diag_timeline.py, PHASES=1); OPS comma-separated
-#   prof                 rocprofv3 kernel-trace summary of the bench (eager) + phase cut
+#   prof[=K=V]           rocprofv3 kernel-trace summary of the bench (eager) + phase cut (K=V: env of the run)
 #   pmc                  PMC passes (tools_dev/pmc_collect.sh TAG)
 #   codec[=LIB[:K=V]]    codec wall / device time per call (tools_dev/codec_latency.py); LIB "-" = default
 #   cprof[=LIB]          rocprofv3 kernel trace of 3 codec decodes, per-dispatch table of the last
@@ -61,11 +61,12 @@ for STEP in "$@"; do
         > "$OUT/${TAG}_tl_${mode}_b${b}${lib:+_$lib}.txt" 2>&1
       echo "timeline ok" ;;
     prof)
-      MAGPIE_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/${TAG}_prof" -o prof \
-        -- python3 -u bench.py --no-cpu-baseline --no-extra > "$OUT/${TAG}_prof_bench.log" 2>&1
-      python3 tools_dev/prof_phase.py "$OUT/${TAG}_prof/prof_kernel_trace.csv" "$OUT/${TAG}_prof/phase_kernel_stats.csv" \
-        > "$OUT/${TAG}_prof_phase.log"
-      echo "rocprof ok" ;;
+      # arg (optional): K=V set for the profiled run, e.g. prof=MAGPIE_STREAM_PRIO=0
+      d="$OUT/${TAG}_prof${arg:+_${arg//=/-}}"
+      env MAGPIE_EAGER=1 $arg timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$d" -o prof \
+        -- python3 -u bench.py --no-cpu-baseline --no-extra > "$d.bench.log" 2>&1
+      python3 tools_dev/prof_phase.py "$d/prof_kernel_trace.csv" "$d/phase_kernel_stats.csv" > "$d.phase.log"
+      echo "rocprof ${arg:-default}: $(head -1 "$d.phase.log")" ;;
     pmc)
       bash tools_dev/pmc_collect.sh "$TAG" > "$OUT/${TAG}_pmc.log" 2>&1
       echo "pmc ok" ;;

@@ -60,6 +60,32 @@ def test_bf16_full_model_batch_equals_single(ma, oracle, full_model, B):
     _hidden_ok(rb.hidden[0, :steps + 1], o["hidden"])
 
 
+@pytest.mark.parametrize("B,env", [(8, "MAGPIE_MERGE8=0"), (8, "MAGPIE_MERGE8=1"), (8, "MAGPIE_MERGE8=2"),
+                                   (16, "MAGPIE_SA16=0")])
+def test_bf16_batched_forms_equal(ma, full_model, B, env):
+    """The batched bf16 layer's alternative forms compute the default's bits: at 8 slots which
+    split states the split workgroups merge themselves (MAGPIE_MERGE8, default 3 = SA and XA),
+    at 16 slots the SA in the QKV launch (the default) or as its own launch (MAGPIE_SA16=0)."""
+    import os
+    steps = 16
+    toks = [ma.synthetic_tokens(40 + 3 * b, seed=7400 + b) for b in range(B)]
+    spk = [b % 5 for b in range(B)]
+    k, v = env.split("=")
+    runs = []
+    for setting in (None, v):
+        if setting is not None:
+            os.environ[k] = setting
+        try:
+            dev = ma.Device(full_model, weights="bf16")
+            runs.append(dev.synthesize(toks, speakers=spk, max_dec_steps=steps, ignore_eos=True, trace=True))
+            dev.close()
+        finally:
+            os.environ.pop(k, None)
+    a, b = runs
+    np.testing.assert_array_equal(a.codes, b.codes)
+    assert np.array_equal(a.hidden, b.hidden)
+
+
 def test_bf16_full_model_sampled_batch8_equals_single(ma, full_model):
     """configs[3]'s per-GPU batch with top-k sampling: slot b draws from stream b, so
     it reproduces its single run with stream_base=b bit for bit."""

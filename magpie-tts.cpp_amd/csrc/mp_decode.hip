@@ -28,6 +28,9 @@ namespace mp {
 // Rows [row0, row0+RW) of W (row-major [N][K]) dotted with act[NB][K].
 // Lane l owns elements 4*(l + 64*i): every weight load is a 1 KiB coalesced
 // wave-instruction; activations come from LDS with conflict-free ds_read_b128.
+#ifndef MP_GEMV_WSN
+#define MP_GEMV_WSN 1  // the GEMV family's wave sums advanced together (0: one after another)
+#endif
 template <int NB, int RW, int K, int PRO, int EPI>
 __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
     const unsigned long long t_start = ts_begin(p.ts);
@@ -104,6 +107,9 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
             prologue<NBS, K, PRO>(ph, act, red, sc);
         }
         if constexpr (EPI != EPI_RESID_XA && EPI != EPI_QKV_SA) ts_phase<2>(p.ts, 0);  // profiling: prologue done
+        // every (row, slot) partial first, then their wave sums advanced together
+        // (wave_sum_n: each total is wave_sum's, same tree and order)
+        float sv[RW * NBS];
 #pragma unroll
         for (int b = 0; b < NBS; ++b) {
             VT av[NV];
@@ -114,9 +120,19 @@ __global__ __launch_bounds__(MP_BLOCK) void gemv_kernel(GemvP p) {
                 float s = 0.f;
 #pragma unroll
                 for (int i = 0; i < NV; ++i) s += dotv(wv[r][i], av[i]);
-                acc[r][hh * NBS + b] = wave_sum(s);
+                sv[r * NBS + b] = s;
             }
         }
+        if constexpr (MP_GEMV_WSN) {
+            wave_sum_n<RW * NBS>(sv);
+        } else {
+#pragma unroll
+            for (int j = 0; j < RW * NBS; ++j) sv[j] = wave_sum(sv[j]);
+        }
+#pragma unroll
+        for (int b = 0; b < NBS; ++b)
+#pragma unroll
+            for (int r = 0; r < RW; ++r) acc[r][hh * NBS + b] = sv[r * NBS + b];
     }
     // acc[][] is wave-uniform: lane r*NB + b owns output (row0 + r, slot b), so the
     // epilogue (GELU, KV append, residual) runs on RW*NB lanes in parallel.

@@ -86,7 +86,14 @@ __device__ __forceinline__ void xa_round(const float4 (&k)[XA_KPW][XA_V], const 
             acc = fmaf(k[u][i].z, h[i].z, acc);
             acc = fmaf(k[u][i].w, h[i].w, acc);
         }
-        sv[u] = tb + XA_WAVES * u < t1 ? wave_sum(acc) * scale : -INFINITY;
+        sv[u] = acc;
+    }
+    // the keys' wave sums advanced together, unconditionally (wave_sum_n: wave_sum's tree per
+    // key), then the keys past t1 masked: the same values as one guarded wave_sum per key
+    wave_sum_n<XA_KPW>(sv);
+#pragma unroll
+    for (int u = 0; u < XA_KPW; ++u) {
+        sv[u] = tb + XA_WAVES * u < t1 ? sv[u] * scale : -INFINITY;
         mn = fmaxf(mn, sv[u]);
     }
     const float c = expf(m - mn);

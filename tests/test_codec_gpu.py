@@ -83,7 +83,7 @@ def test_fused_blocks_equal_two_launch_blocks(gpu_codec, monkeypatch, F):
 
 
 @pytest.mark.parametrize("mode", ["1", "2"])
-@pytest.mark.parametrize("F", [1, 4, 32])
+@pytest.mark.parametrize("F", [1, 4, 32, 96])
 def test_reslayer_launch_equals_block_launches(gpu_codec, monkeypatch, F, mode):
     """A ResLayer as one launch (rl_kernel: a branch's three residual blocks per time tile,
     x in registers between them; MAGPIE_CODEC_RL=1, the default: the 32-channel stage, 2: the
@@ -91,7 +91,8 @@ def test_reslayer_launch_equals_block_launches(gpu_codec, monkeypatch, F, mode):
     (MAGPIE_CODEC_RL=0): per time step the same f16 operands, fragments, accumulation order
     and (x + conv_1) + b epilogue. Three chunks, so tiles straddle chunk starts and ends;
     F = 1 leaves a single partial tile per chunk."""
-    codes = np.random.default_rng(70 + F).integers(0, 2016, (3, 8, F)).astype(np.int32)
+    nchunk = 1 if F > 32 else 3  # F = 96: one long chunk, 98k steps on the 32-channel stage
+    codes = np.random.default_rng(70 + F).integers(0, 2016, (nchunk, 8, F)).astype(np.int32)
     monkeypatch.setenv("MAGPIE_CODEC_RL", mode)
     one = gpu_codec.decode_chunks(codes)
     monkeypatch.setenv("MAGPIE_CODEC_RL", "0")
